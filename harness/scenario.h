@@ -1,0 +1,387 @@
+// harness/scenario.h -- loopback workload definitions shared by every driver.
+//
+// This is the MI355X build's analogue of the reference's loopback simulator
+// (reference tests/unit_test.cpp:79-125 payloads, :380-655 StreamingTest,
+// :173-377 BlockRecoveryTest).  One "stream" is an encoder -> lossy channel ->
+// decoder pipeline driven through the siamese.h call sequence.  The workload
+// is a deterministic function of (config, global stream index), so the same
+// stream run through the upstream reference (oracle/_ref), through the
+// drop-in per-call API of libsiamese_amd, or through its batched device API
+// must produce the same event digest -- that digest is the parity check.
+//
+// The per-stream logic is a resumable state machine (Stream::step) so the
+// batched driver can advance thousands of streams in lock-step rounds while
+// issuing exactly the same per-stream call sequence as the sequential driver.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace scen {
+
+// PCG-XSH-RR 64/32, seeded the way the reference seeds it
+// (reference SiameseTools.h:80-102).  Used for payloads and the loss channel.
+struct Pcg
+{
+    uint64_t state = 0, inc = 0;
+    void seed(uint64_t y, uint64_t x = 0)
+    {
+        state = 0;
+        inc = (y << 1u) | 1u;
+        next();
+        state += x;
+        next();
+    }
+    uint32_t next()
+    {
+        const uint64_t s = state;
+        state = s * 6364136223846793005ULL + inc;
+        const uint32_t xs = (uint32_t)(((s >> 18) ^ s) >> 27);
+        const uint32_t r = (uint32_t)(s >> 59);
+        return (xs >> r) | (xs << ((32u - r) & 31u));
+    }
+};
+
+// Variable packet size 2..1199 (reference unit_test.cpp:79-88)
+inline unsigned variable_bytes(unsigned id)
+{
+    Pcg p;
+    p.seed(id, 24124);
+    return 2 + (p.next() % (1200 - 2));
+}
+
+// Self-validating payload: LE32 length then PCG(id, bytes) words
+// (reference unit_test.cpp:90-116).
+inline void fill_payload(unsigned id, uint8_t* buf, unsigned bytes)
+{
+    Pcg p;
+    p.seed(id, bytes);
+    if (bytes >= 4) {
+        const uint32_t b = bytes;
+        std::memcpy(buf, &b, 4);
+        buf += 4;
+        bytes -= 4;
+    }
+    while (bytes >= 4) {
+        const uint32_t w = p.next();
+        std::memcpy(buf, &w, 4);
+        buf += 4;
+        bytes -= 4;
+    }
+    if (bytes > 0) {
+        uint32_t w = p.next();
+        for (unsigned i = 0; i < bytes; ++i, w >>= 8)
+            buf[i] = (uint8_t)w;
+    }
+}
+
+struct Fnv
+{
+    uint64_t h = 1469598103934665603ULL;
+    void bytes(const void* p, size_t n)
+    {
+        const uint8_t* b = (const uint8_t*)p;
+        for (size_t i = 0; i < n; ++i) {
+            h ^= b[i];
+            h *= 1099511628211ULL;
+        }
+    }
+    void u64(uint64_t v) { bytes(&v, 8); }
+};
+
+inline uint64_t hash_bytes(const void* p, size_t n)
+{
+    Fnv f;
+    f.bytes(p, n);
+    return f.h;
+}
+
+} // namespace scen
+
+extern "C" {
+
+/// Scenario knobs (ctypes-visible; keep POD, all uint32).
+struct ScenarioConfig
+{
+    uint32_t block_mode;        ///< 0 = streaming, 1 = block (add all, then encode)
+    uint32_t streams;           ///< streams simulated by this call
+    uint32_t first_stream;      ///< global index of the first stream (sharding)
+    uint32_t originals;         ///< originals per stream (N)
+    uint32_t payload_bytes;     ///< fixed payload size; 0 = variable 2..1199
+    uint32_t loss_pct;          ///< original loss percentage
+    uint32_t recovery_loss_pct; ///< recovery loss percentage
+    uint32_t recovery_interval; ///< streaming: encode when i % interval == phase
+    uint32_t recovery_phase;
+    uint32_t ack_policy;        ///< 0 none, 1 immediate remove_before, 2 lag-based
+    uint32_t ack_lag;           ///< lag for policy 2
+    uint32_t tail_limit;        ///< extra encodes after the last original / block limit
+    uint32_t seed;              ///< loss channel seed (1013 = reference kSeed)
+};
+
+/// Per-stream outcome (ctypes-visible).
+struct StreamResult
+{
+    uint64_t digest;            ///< FNV-1a-64 over the stream's event log
+    uint64_t recovery_bytes;    ///< bytes of recovery packets emitted
+    uint64_t payload_bytes;     ///< payload bytes of originals added
+    uint32_t encodes;           ///< successful siamese_encode calls
+    uint32_t recovery_lost;     ///< recovery packets dropped by the channel
+    uint32_t originals_lost;    ///< originals dropped by the channel
+    uint32_t recovered;         ///< packets returned by siamese_decode
+    uint32_t decode_calls;
+    uint32_t decode_fail;       ///< decode returned NeedMoreData
+    uint32_t delivered;         ///< in-order deliveries (== originals when done)
+    uint32_t status;            ///< 0 complete, 1 stalled, 2 api error, 3 data mismatch
+};
+
+} // extern "C"
+
+namespace scen {
+
+enum Event : uint64_t
+{
+    EV_ENC_ADD = 1, EV_DEC_ADD_ORIG, EV_ENCODE, EV_DEC_ADD_REC,
+    EV_IS_READY, EV_DECODE, EV_DECODED_PKT, EV_GET, EV_REMOVE
+};
+
+inline uint64_t ev(uint64_t type, uint64_t result, uint64_t a = 0, uint64_t b = 0)
+{
+    return (type << 56) ^ (result << 48) ^ (a << 24) ^ b;
+}
+
+/*
+    Codec concept (duck-typed) used by Stream<Codec>:
+
+      int  enc_add(const uint8_t* data, unsigned bytes, unsigned* packetNum);
+      int  encode(Rec* rec);                 // Rec: driver-defined handle w/ .bytes
+      int  dec_add_original(unsigned num, const uint8_t* data, unsigned bytes);
+      int  dec_add_recovery(const Rec& rec);
+      int  is_ready();
+      int  decode(std::vector<Pkt>* out);     // Pkt: driver-defined w/ .num .bytes
+      int  dec_get(unsigned num, Pkt* out);
+      int  enc_remove_before(unsigned num);
+      // data tokens (a hash now, or a deferred slot resolved after a flush)
+      uint64_t rec_token(const Rec& rec);
+      uint64_t pkt_token(const Pkt& p, unsigned expectedId, bool* ok); // verifies payload
+      bool wants_yield_after_decode();
+*/
+
+template <class Codec, class Rec, class Pkt>
+struct Stream
+{
+    enum Phase { ADD, ENCODE, DECODE_LOOP, ACK, TAIL, DONE };
+
+    const ScenarioConfig* cfg = nullptr;
+    Codec* codec = nullptr;
+    StreamResult* res = nullptr;
+    unsigned global = 0;          // global stream index
+    std::vector<uint64_t> log;    // event log (tokens may be filled in later)
+
+    Pcg loss;
+    Phase phase = ADD;
+    unsigned i = 0;               // next original index
+    unsigned tail = 0;            // encodes issued after the originals
+    unsigned nextExpected = 0;
+    unsigned lastNum = 0;         // PacketNum of the most recent add
+    bool tailMode = false;        // all originals added; only encodes remain
+    std::vector<uint8_t> buf;
+    bool dataOk = true;           // every returned packet matched its payload
+
+    void init(const ScenarioConfig* c, Codec* k, StreamResult* r, unsigned globalIndex)
+    {
+        cfg = c;
+        codec = k;
+        res = r;
+        global = globalIndex;
+        std::memset(res, 0, sizeof(*res));
+        loss.seed(cfg->seed, global);
+        buf.resize(cfg->payload_bytes ? cfg->payload_bytes + 8 : 1208);
+        phase = ADD;
+    }
+
+    unsigned packet_id(unsigned index) const { return global * cfg->originals + index; }
+
+    bool done() const { return phase == DONE; }
+
+    void fail(unsigned status)
+    {
+        res->status = status;
+        phase = DONE;
+    }
+
+    // Pull every in-order packet already present at the decoder.
+    bool deliver()
+    {
+        while (nextExpected < cfg->originals) {
+            Pkt p;
+            const int r = codec->dec_get(nextExpected, &p);
+            if (r != 0) {
+                log.push_back(ev(EV_GET, r, nextExpected));
+                return r == 2; // NeedMoreData is the normal stop
+            }
+            log.push_back(ev(EV_GET, 0, nextExpected, p.bytes));
+            log.push_back(codec->pkt_token(p, packet_id(nextExpected), &dataOk));
+            ++nextExpected;
+            ++res->delivered;
+        }
+        return true;
+    }
+
+    // One encode + channel + add_recovery.  Returns false when the stream
+    // should stop (error) -- the caller then inspects res->status.
+    bool encode_once()
+    {
+        Rec rec;
+        const int r = codec->encode(&rec);
+        log.push_back(ev(EV_ENCODE, r, r == 0 ? rec.bytes : 0));
+        if (r == 2)
+            return true; // nothing to encode yet
+        if (r != 0) {
+            fail(2);
+            return false;
+        }
+        log.push_back(codec->rec_token(rec));
+        ++res->encodes;
+        res->recovery_bytes += rec.bytes;
+        const bool lost = (loss.next() % 100) < cfg->recovery_loss_pct;
+        if (lost) {
+            ++res->recovery_lost;
+            return true;
+        }
+        const int a = codec->dec_add_recovery(rec);
+        log.push_back(ev(EV_DEC_ADD_REC, a));
+        if (a != 0) {
+            fail(2);
+            return false;
+        }
+        phase = DECODE_LOOP;
+        return true;
+    }
+
+    // Advance by one unit of work.  Returns true if the driver should stop
+    // stepping this stream until outstanding device work has been flushed.
+    bool step()
+    {
+        switch (phase) {
+        case ADD: {
+            if (i >= cfg->originals) {
+                tailMode = true;
+                phase = TAIL;
+                return false;
+            }
+            const unsigned id = packet_id(i);
+            const unsigned bytes = cfg->payload_bytes ? cfg->payload_bytes : variable_bytes(id);
+            fill_payload(id, buf.data(), bytes);
+            unsigned num = 0;
+            const int r = codec->enc_add(buf.data(), bytes, &num);
+            log.push_back(ev(EV_ENC_ADD, r, num));
+            if (r != 0) {
+                fail(2);
+                return false;
+            }
+            lastNum = num;
+            res->payload_bytes += bytes;
+            const bool lost = (loss.next() % 100) < cfg->loss_pct;
+            if (lost) {
+                ++res->originals_lost;
+            } else {
+                const int a = codec->dec_add_original(num, buf.data(), bytes);
+                log.push_back(ev(EV_DEC_ADD_ORIG, a, num));
+                if (a != 0 && a != 4) {
+                    fail(2);
+                    return false;
+                }
+                if (num == nextExpected && !deliver()) {
+                    fail(2);
+                    return false;
+                }
+            }
+            ++i;
+            if (cfg->block_mode) {
+                phase = ADD;
+                return false;
+            }
+            phase = ((i - 1) % cfg->recovery_interval == cfg->recovery_phase) ? ENCODE : ACK;
+            return false;
+        }
+        case ENCODE:
+            phase = ACK;
+            encode_once();
+            return false;
+        case DECODE_LOOP: {
+            const int ready = codec->is_ready();
+            log.push_back(ev(EV_IS_READY, ready));
+            if (ready != 0) {
+                phase = tailMode ? TAIL : ACK;
+                return false;
+            }
+            std::vector<Pkt> pkts;
+            ++res->decode_calls;
+            const int r = codec->decode(&pkts);
+            log.push_back(ev(EV_DECODE, r, (uint64_t)pkts.size()));
+            if (r == 2) {
+                ++res->decode_fail;
+                return false;
+            }
+            if (r != 0) {
+                fail(2);
+                return false;
+            }
+            for (const Pkt& p : pkts) {
+                log.push_back(ev(EV_DECODED_PKT, 0, p.num, p.bytes));
+                log.push_back(codec->pkt_token(p, packet_id(p.num), &dataOk));
+                ++res->recovered;
+            }
+            if (!deliver()) {
+                fail(2);
+                return false;
+            }
+            return codec->wants_yield_after_decode();
+        }
+        case ACK: {
+            phase = (i >= cfg->originals) ? TAIL : ADD;
+            tailMode = (phase == TAIL);
+            if (cfg->ack_policy == 1) {
+                const int r = codec->enc_remove_before(nextExpected);
+                log.push_back(ev(EV_REMOVE, r, nextExpected));
+            } else if (cfg->ack_policy == 2) {
+                const unsigned lag = (lastNum - nextExpected) & 0x3fffff;
+                if (lag >= cfg->ack_lag && lag < 0x200000) {
+                    const int r = codec->enc_remove_before(nextExpected);
+                    log.push_back(ev(EV_REMOVE, r, nextExpected));
+                }
+            }
+            return false;
+        }
+        case TAIL:
+            if (nextExpected >= cfg->originals) {
+                phase = DONE;
+                return false;
+            }
+            if (tail >= cfg->tail_limit) {
+                fail(1);
+                return false;
+            }
+            ++tail;
+            encode_once();
+            return false;
+        case DONE:
+            return false;
+        }
+        return false;
+    }
+
+    void finish()
+    {
+        if (!dataOk && res->status == 0)
+            res->status = 3;
+        Fnv f;
+        for (uint64_t e : log)
+            f.u64(e);
+        f.u64(res->status);
+        res->digest = f.h;
+    }
+};
+
+} // namespace scen

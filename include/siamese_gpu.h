@@ -1,0 +1,85 @@
+/*
+    siamese_gpu.h -- device-resident batch API of libsiamese_amd (additive;
+    not part of the upstream interface).
+
+    siamese.h moves every packet through host memory and waits for the GPU on
+    each siamese_encode / siamese_decode, which is the drop-in contract.  This
+    header exposes the same codec with packets that stay in HBM:
+
+      * originals are ingested from device pointers;
+      * siamese_encode's result is a device-resident recovery packet that can
+        be handed straight to a decoder on the same GPU;
+      * nothing waits for the GPU until sgpu_flush(), so thousands of
+        independent encoder/decoder pairs are driven per kernel launch.
+
+    Per-instance call semantics, result codes and outputs are those of the
+    corresponding siamese.h call (reference siamese.h:213-483); only the data
+    location and the completion point differ.  Recovered packets returned by
+    sgpu_decode carry device pointers whose DataBytes are exact after the
+    next sgpu_flush() (they read 0 until then).
+*/
+#ifndef SIAMESE_GPU_H
+#define SIAMESE_GPU_H
+
+#include "siamese.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct SgpuEncoderImpl { int impl; }* SgpuEncoder;
+typedef struct SgpuDecoderImpl { int impl; }* SgpuDecoder;
+
+/// Device-resident recovery packet (valid until the next sgpu_encode on the
+/// same encoder).  Footer/Head are host copies the decoder parses directly.
+typedef struct SgpuRecoveryPacket
+{
+    const unsigned char* DeviceData;   ///< payload + footer in HBM
+    unsigned DataBytes;
+    unsigned FooterBytes;
+    unsigned char Footer[8];
+    unsigned char Head[4];
+    void* Producer;                    ///< internal: encoder that owns DeviceData
+} SgpuRecoveryPacket;
+
+/// Initialise the library on HIP device `device` (<0: current device).
+SIAMESE_EXPORT int sgpu_init(int device);
+
+SIAMESE_EXPORT SgpuEncoder sgpu_encoder_create(void);
+SIAMESE_EXPORT void sgpu_encoder_free(SgpuEncoder encoder);
+SIAMESE_EXPORT SiameseResult sgpu_encoder_add(SgpuEncoder encoder, const void* deviceData,
+                                              unsigned bytes, unsigned* packetNumOut);
+SIAMESE_EXPORT SiameseResult sgpu_encoder_remove_before(SgpuEncoder encoder, unsigned firstKept);
+SIAMESE_EXPORT SiameseResult sgpu_encode(SgpuEncoder encoder, SgpuRecoveryPacket* out);
+
+SIAMESE_EXPORT SgpuDecoder sgpu_decoder_create(void);
+SIAMESE_EXPORT void sgpu_decoder_free(SgpuDecoder decoder);
+SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original(SgpuDecoder decoder, unsigned packetNum,
+                                                       const void* deviceData, unsigned bytes);
+SIAMESE_EXPORT SiameseResult sgpu_decoder_add_recovery(SgpuDecoder decoder,
+                                                       const SgpuRecoveryPacket* packet);
+SIAMESE_EXPORT SiameseResult sgpu_decoder_is_ready(SgpuDecoder decoder);
+SIAMESE_EXPORT SiameseResult sgpu_decode(SgpuDecoder decoder, SiameseOriginalPacket** packetsOut,
+                                         unsigned* countOut);
+/// Returns a device pointer; waits for outstanding work if the packet's
+/// exact length is still being computed.
+SIAMESE_EXPORT SiameseResult sgpu_decoder_get(SgpuDecoder decoder, SiameseOriginalPacket* packet);
+/// Non-blocking lookup: Success if the packet is present (length may still
+/// be pending), NeedMoreData if not.
+SIAMESE_EXPORT SiameseResult sgpu_decoder_has(SgpuDecoder decoder, unsigned packetNum);
+
+/// Submit all queued device work of every instance and wait for it.
+SIAMESE_EXPORT int sgpu_flush(void);
+/// Submit without waiting (the next sgpu_flush completes it).
+SIAMESE_EXPORT int sgpu_submit(void);
+
+/// Device timing of flushed work since the last reset (milliseconds).
+SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs);
+/// Counters of the engine (flushes, launches, ops, terms, solves, ingests, upload bytes).
+SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out7);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SIAMESE_GPU_H */

@@ -1,0 +1,264 @@
+// api.cpp -- the drop-in siamese.h entry points (reference siamese.cpp:35-302).
+//
+// Argument validation and result codes follow the reference entry points
+// one-for-one.  Each call takes the process-wide engine lock; calls that must
+// hand host memory back to the caller (siamese_encode, siamese_decode, and
+// siamese_decoder_get on a freshly recovered packet) flush the queued device
+// work and wait for it, copying the bytes into host buffers whose lifetime
+// matches the reference contract (siamese.h:335-336, :410-414).
+#define SIAMESE_BUILDING
+#include "../../include/siamese.h"
+
+#include "backend.h"
+#include "decoder.h"
+#include "encoder.h"
+#include "engine.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <new>
+
+using namespace sgpu;
+
+namespace {
+
+bool g_initialized = false;
+
+struct ApiEncoder
+{
+    EncoderCore core{Engine::global(), true};
+    std::vector<uint8_t> out; // last recovery packet (host copy)
+};
+
+struct ApiDecoder
+{
+    DecoderCore core{Engine::global(), true};
+};
+
+inline ApiEncoder* E(SiameseEncoder e) { return reinterpret_cast<ApiEncoder*>(e); }
+inline ApiDecoder* D(SiameseDecoder d) { return reinterpret_cast<ApiDecoder*>(d); }
+
+using Lock = std::lock_guard<std::mutex>;
+
+} // namespace
+
+extern "C" {
+
+SIAMESE_EXPORT int siamese_init_(int version)
+{
+    if (version != SIAMESE_VERSION)
+        return Siamese_Disabled;
+    if (!gf_init())
+        return Siamese_Disabled;
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    const char* err = "unknown";
+    int device = -1;
+    if (const char* s = std::getenv("SIAMESE_AMD_DEVICE"))
+        device = std::atoi(s);
+    if (!eng->init(device, &err)) {
+        std::fprintf(stderr, "siamese_amd: initialisation failed: %s\n", err);
+        return Siamese_Disabled;
+    }
+    g_initialized = true;
+    return Siamese_Success;
+}
+
+// ---- Encoder --------------------------------------------------------------
+
+SIAMESE_EXPORT SiameseEncoder siamese_encoder_create()
+{
+    if (!g_initialized)
+        return nullptr;
+    Lock lock(Engine::global()->mutex());
+    return reinterpret_cast<SiameseEncoder>(new (std::nothrow) ApiEncoder);
+}
+
+SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder)
+{
+    if (!encoder)
+        return;
+    Lock lock(Engine::global()->mutex());
+    delete E(encoder);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_is_ready(SiameseEncoder encoder)
+{
+    if (!encoder)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    // keep two slots of slack for the application (siamese.cpp:86-91)
+    if (E(encoder)->core.remaining_slots() <= 2)
+        return Siamese_MaxPacketsReached;
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder, SiameseOriginalPacket* packet)
+{
+    if (!encoder || !packet || !packet->Data || packet->DataBytes <= 0 ||
+        packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return E(encoder)->core.add(*packet);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder, SiameseOriginalPacket* packet)
+{
+    if (!encoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return E(encoder)->core.get(*packet);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_remove_before(SiameseEncoder encoder, unsigned packetNum)
+{
+    if (!encoder || packetNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    E(encoder)->core.remove_before(packetNum);
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder, const void* buffer,
+                                                 unsigned bytes, unsigned* nextExpectedPacketNum)
+{
+    if (!encoder || !buffer || bytes < 1 || !nextExpectedPacketNum)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return E(encoder)->core.acknowledge((const uint8_t*)buffer, bytes, *nextExpectedPacketNum);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder,
+                                                        SiameseOriginalPacket* original)
+{
+    if (!encoder || !original)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return E(encoder)->core.retransmit(*original);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder, SiameseRecoveryPacket* recovery)
+{
+    if (!encoder || !recovery)
+        return Siamese_InvalidInput;
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    ApiEncoder* enc = E(encoder);
+    EncodeOut o;
+    const SiameseResult r = enc->core.encode(o);
+    if (r != Siamese_Success) {
+        if (r == Siamese_NeedMoreData)
+            recovery->DataBytes = 0;
+        return r;
+    }
+    enc->out.resize(o.bytes);
+    eng->download(enc->out.data(), o.buf.addr(), o.bytes);
+    if (!eng->flush_and_sync())
+        return Siamese_Disabled;
+    recovery->Data = enc->out.data();
+    recovery->DataBytes = o.bytes;
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder, uint64_t* statsOut,
+                                                   unsigned statsCount)
+{
+    if (!encoder || !statsOut || statsCount <= 0)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return E(encoder)->core.stats(statsOut, statsCount);
+}
+
+// ---- Decoder --------------------------------------------------------------
+
+SIAMESE_EXPORT SiameseDecoder siamese_decoder_create()
+{
+    if (!g_initialized)
+        return nullptr;
+    Lock lock(Engine::global()->mutex());
+    return reinterpret_cast<SiameseDecoder>(new (std::nothrow) ApiDecoder);
+}
+
+SIAMESE_EXPORT void siamese_decoder_free(SiameseDecoder decoder)
+{
+    if (!decoder)
+        return;
+    Lock lock(Engine::global()->mutex());
+    delete D(decoder);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_add_original(SiameseDecoder decoder,
+                                                          const SiameseOriginalPacket* packet)
+{
+    if (!decoder || !packet || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES ||
+        packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return D(decoder)->core.add_original(*packet);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_add_recovery(SiameseDecoder decoder,
+                                                          const SiameseRecoveryPacket* packet)
+{
+    if (!decoder || !packet || !packet->Data || packet->DataBytes <= 0 ||
+        packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return D(decoder)->core.add_recovery(*packet);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder, SiameseOriginalPacket* packet)
+{
+    if (!decoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return D(decoder)->core.get(*packet);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_is_ready(SiameseDecoder decoder)
+{
+    if (!decoder)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return D(decoder)->core.is_ready();
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder, SiameseOriginalPacket** packetsPtrOut,
+                                            unsigned* countOut)
+{
+    if (!decoder || (!packetsPtrOut != !countOut))
+        return Siamese_InvalidInput;
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    DecoderCore& core = D(decoder)->core;
+    const SiameseResult r = core.decode(packetsPtrOut, countOut);
+    if (core.has_pending()) {
+        core.download_recovered();
+        if (!eng->flush_and_sync())
+            return Siamese_Disabled;
+        if (core.disabled())
+            return Siamese_Disabled;
+    }
+    return r;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder, void* buffer, unsigned byteLimit,
+                                                 unsigned* usedBytes)
+{
+    if (!decoder || !buffer || !usedBytes || byteLimit < SIAMESE_ACK_MIN_BYTES)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return D(decoder)->core.acknowledgement((uint8_t*)buffer, byteLimit, *usedBytes);
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_stats(SiameseDecoder decoder, uint64_t* statsOut,
+                                                   unsigned statsCount)
+{
+    if (!decoder || !statsOut || statsCount <= 0)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return D(decoder)->core.stats(statsOut, statsCount);
+}
+
+} // extern "C"

@@ -1,0 +1,45 @@
+// backend.h -- the only interface between the host control plane and the
+// device.  libsiamese_amd.so implements it with HIP on gfx950
+// (backend_hip.hip).  A host simulation of the same contract exists ONLY for
+// the CPU test suite (tests/hostsim/), never in the shipped library.
+#pragma once
+
+#include "ops.h"
+#include <cstddef>
+#include <cstdint>
+
+namespace sgpu {
+
+/// Initialise the device (HIP device index; <0 = current).  Returns false
+/// with a message in *err when no usable MI355X device exists.
+bool be_init(int device, const char** err);
+const char* be_name();
+
+void* be_dev_alloc(size_t bytes);
+void be_dev_free(void* p);
+void* be_host_alloc(size_t bytes);   // page-locked
+void be_host_free(void* p);
+
+// All transfers and launches are asynchronous on the engine's stream.
+void be_h2d(void* dst, const void* src, size_t bytes);
+void be_d2h(void* dst, const void* src, size_t bytes);
+void be_memset(void* dst, int value, size_t bytes);
+
+void be_launch_ingest(const IngestDesc* descs, const IngestItem* items, uint32_t count);
+void be_launch_exec(const GfOp* ops, const GfTerm* terms, const ExecItem* items, uint32_t count);
+void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
+                            uint32_t* results, uint32_t count);
+void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
+                          const uint32_t* results, const SolveItem* items, uint32_t count);
+
+/// Block until all queued work has finished.  Returns false on a device fault.
+bool be_sync();
+
+/// Device-time accounting: every executor/solve launch is bracketed with
+/// events; these return the accumulated milliseconds since the last reset.
+void be_timing_enable(bool on);
+void be_timing_reset();
+double be_timing_exec_ms();
+double be_timing_total_ms();
+
+} // namespace sgpu

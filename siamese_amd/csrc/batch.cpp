@@ -1,0 +1,235 @@
+// batch.cpp -- siamese_gpu.h: the device-resident batch API.  Same control
+// plane as the drop-in API; instances keep no host mirrors and never wait
+// for the device until sgpu_flush().
+#define SIAMESE_BUILDING
+#include "../../include/siamese_gpu.h"
+
+#include "backend.h"
+#include "decoder.h"
+#include "encoder.h"
+#include "engine.h"
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+using namespace sgpu;
+
+namespace {
+
+bool g_batchReady = false;
+
+struct BatchEncoder
+{
+    EncoderCore core{Engine::global(), false};
+};
+
+struct BatchDecoder
+{
+    DecoderCore core{Engine::global(), false};
+};
+
+inline BatchEncoder* BE(SgpuEncoder e) { return reinterpret_cast<BatchEncoder*>(e); }
+inline BatchDecoder* BD(SgpuDecoder d) { return reinterpret_cast<BatchDecoder*>(d); }
+using Lock = std::lock_guard<std::mutex>;
+
+} // namespace
+
+extern "C" {
+
+SIAMESE_EXPORT int sgpu_init(int device)
+{
+    if (!gf_init())
+        return Siamese_Disabled;
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    const char* err = "unknown";
+    if (!eng->init(device, &err)) {
+        std::fprintf(stderr, "siamese_amd: initialisation failed: %s\n", err);
+        return Siamese_Disabled;
+    }
+    g_batchReady = true;
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SgpuEncoder sgpu_encoder_create(void)
+{
+    if (!g_batchReady)
+        return nullptr;
+    Lock lock(Engine::global()->mutex());
+    return reinterpret_cast<SgpuEncoder>(new (std::nothrow) BatchEncoder);
+}
+
+SIAMESE_EXPORT void sgpu_encoder_free(SgpuEncoder encoder)
+{
+    if (!encoder)
+        return;
+    Lock lock(Engine::global()->mutex());
+    delete BE(encoder);
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_encoder_add(SgpuEncoder encoder, const void* deviceData, unsigned bytes,
+                                              unsigned* packetNumOut)
+{
+    if (!encoder || !deviceData || bytes == 0 || bytes > SIAMESE_MAX_PACKET_BYTES)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    SiameseOriginalPacket p;
+    p.PacketNum = 0;
+    p.Data = (const unsigned char*)deviceData;
+    p.DataBytes = bytes;
+    const SiameseResult r = BE(encoder)->core.add(p, (uint64_t)(uintptr_t)deviceData);
+    if (packetNumOut)
+        *packetNumOut = p.PacketNum;
+    return r;
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_encoder_remove_before(SgpuEncoder encoder, unsigned firstKept)
+{
+    if (!encoder || firstKept > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    BE(encoder)->core.remove_before(firstKept);
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_encode(SgpuEncoder encoder, SgpuRecoveryPacket* out)
+{
+    if (!encoder || !out)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    EncoderCore& core = BE(encoder)->core;
+    EncodeOut o;
+    const SiameseResult r = core.encode(o);
+    if (r != Siamese_Success) {
+        out->DataBytes = 0;
+        return r;
+    }
+    out->DeviceData = o.buf.ptr;
+    out->DataBytes = o.bytes;
+    out->FooterBytes = o.footerBytes;
+    std::memcpy(out->Footer, o.footer, sizeof(out->Footer));
+    std::memcpy(out->Head, o.head, sizeof(out->Head));
+    out->Producer = &core.program();
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SgpuDecoder sgpu_decoder_create(void)
+{
+    if (!g_batchReady)
+        return nullptr;
+    Lock lock(Engine::global()->mutex());
+    return reinterpret_cast<SgpuDecoder>(new (std::nothrow) BatchDecoder);
+}
+
+SIAMESE_EXPORT void sgpu_decoder_free(SgpuDecoder decoder)
+{
+    if (!decoder)
+        return;
+    Lock lock(Engine::global()->mutex());
+    delete BD(decoder);
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original(SgpuDecoder decoder, unsigned packetNum,
+                                                       const void* deviceData, unsigned bytes)
+{
+    if (!decoder || !deviceData || bytes == 0 || bytes > SIAMESE_MAX_PACKET_BYTES ||
+        packetNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    SiameseOriginalPacket p;
+    p.PacketNum = packetNum;
+    p.Data = (const unsigned char*)deviceData;
+    p.DataBytes = bytes;
+    return BD(decoder)->core.add_original(p, (uint64_t)(uintptr_t)deviceData);
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_decoder_add_recovery(SgpuDecoder decoder, const SgpuRecoveryPacket* packet)
+{
+    if (!decoder || !packet || !packet->DeviceData || packet->DataBytes == 0 ||
+        packet->FooterBytes == 0 || packet->FooterBytes > 8 || packet->FooterBytes >= packet->DataBytes)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    DeviceRecovery r;
+    r.data = (uint64_t)(uintptr_t)packet->DeviceData;
+    r.bytes = packet->DataBytes;
+    r.footer = packet->Footer;
+    r.footerBytes = packet->FooterBytes;
+    r.head = packet->Head;
+    r.producer = reinterpret_cast<Program*>(packet->Producer);
+    return BD(decoder)->core.add_recovery_device(r);
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_decoder_is_ready(SgpuDecoder decoder)
+{
+    if (!decoder)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return BD(decoder)->core.is_ready();
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_decode(SgpuDecoder decoder, SiameseOriginalPacket** packetsOut,
+                                         unsigned* countOut)
+{
+    if (!decoder || (!packetsOut != !countOut))
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return BD(decoder)->core.decode(packetsOut, countOut);
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_decoder_get(SgpuDecoder decoder, SiameseOriginalPacket* packet)
+{
+    if (!decoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return BD(decoder)->core.get(*packet);
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_decoder_has(SgpuDecoder decoder, unsigned packetNum)
+{
+    if (!decoder || packetNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    Lock lock(Engine::global()->mutex());
+    return BD(decoder)->core.has(packetNum) ? Siamese_Success : Siamese_NeedMoreData;
+}
+
+SIAMESE_EXPORT int sgpu_flush(void)
+{
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    return eng->flush_and_sync() ? 0 : -1;
+}
+
+SIAMESE_EXPORT int sgpu_submit(void)
+{
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    eng->flush();
+    return 0;
+}
+
+SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs)
+{
+    be_timing_enable(enable != 0);
+    if (execMs)
+        *execMs = be_timing_exec_ms();
+    if (totalMs)
+        *totalMs = be_timing_total_ms();
+    if (reset)
+        be_timing_reset();
+}
+
+SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out7)
+{
+    const Engine::Stats& s = Engine::global()->stats;
+    out7[0] = s.flushes;
+    out7[1] = s.launches;
+    out7[2] = s.ops;
+    out7[3] = s.terms;
+    out7[4] = s.solves;
+    out7[5] = s.ingests;
+    out7[6] = s.uploadBytes;
+}
+
+} // extern "C"

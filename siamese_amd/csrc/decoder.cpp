@@ -1,0 +1,1355 @@
+// decoder.cpp -- see decoder.h.  Line citations are to the reference
+// SiameseDecoder.cpp unless stated otherwise.
+#include "decoder.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace sgpu {
+
+namespace {
+
+inline unsigned popcount_range(uint64_t bits, unsigned begin, unsigned end)
+{
+    if (begin >= end)
+        return 0;
+    uint64_t mask = (end >= 64 ? ~0ULL : ((1ULL << end) - 1)) & ~((1ULL << begin) - 1);
+    return (unsigned)__builtin_popcountll(bits & mask);
+}
+
+inline unsigned first_clear(uint64_t bits, unsigned from)
+{
+    if (from >= 64)
+        return 64;
+    const uint64_t inv = ~bits & (~0ULL << from);
+    return inv ? (unsigned)__builtin_ctzll(inv) : 64;
+}
+
+} // namespace
+
+DecoderCore::DecoderCore(Engine* eng, bool hostMirror)
+    : eng_(eng), prog_(eng, 1), mirror_(hostMirror), alive_(std::make_shared<int>(0))
+{
+}
+
+DecoderCore::~DecoderCore()
+{
+    for (RecPacket* r = head_; r;) {
+        RecPacket* n = r->next;
+        free_packet(r);
+        r = n;
+    }
+    for (auto& sw : subwindows_)
+        for (DecSlot& s : sw->slot)
+            eng_->release(s.buf);
+    for (auto& lane : lanes_)
+        for (Sum& s : lane)
+            eng_->release(s.d.buf);
+}
+
+// ---------------------------------------------------------------------------
+// Receive window (:1260-1536)
+
+bool DecoderCore::mark_got(unsigned column)
+{
+    const unsigned element = column_to_element(column);
+    if (element >= count_) {
+        disabled_ = true;
+        return false;
+    }
+    DecSubwindow* sw = subwindows_[element / kSubwindow].get();
+    sw->gotCount++;
+    sw->got |= 1ULL << (element % kSubwindow);
+    return element == nextExpected_;
+}
+
+unsigned DecoderCore::range_lost(unsigned start, unsigned end)
+{
+    if (start >= end)
+        return 0;
+    unsigned lost = 0;
+    unsigned sub = start / kSubwindow;
+    const unsigned bitStart = start % kSubwindow;
+    if (bitStart > 0) {
+        unsigned bitEnd = bitStart + end - start;
+        if (bitEnd > kSubwindow)
+            bitEnd = kSubwindow;
+        lost += (bitEnd - bitStart) - popcount_range(subwindows_[sub]->got, bitStart, bitEnd);
+        ++sub;
+    }
+    const unsigned subEnd = end / kSubwindow;
+    for (unsigned i = sub; i < subEnd; ++i)
+        lost += kSubwindow - subwindows_[i]->gotCount;
+    if (subEnd >= sub) {
+        const unsigned lastBits = end - subEnd * kSubwindow;
+        if (lastBits > 0)
+            lost += lastBits - popcount_range(subwindows_[subEnd]->got, 0, lastBits);
+    }
+    return lost;
+}
+
+unsigned DecoderCore::find_next_lost(unsigned start)
+{
+    if (start >= count_)
+        return count_;
+    const unsigned subEnd = (count_ + kSubwindow - 1) / kSubwindow;
+    unsigned sub = start / kSubwindow;
+    unsigned bit = start % kSubwindow;
+    while (sub < subEnd) {
+        const DecSubwindow* sw = subwindows_[sub].get();
+        if (sw->gotCount < kSubwindow) {
+            bit = first_clear(sw->got, bit);
+            if (bit < kSubwindow) {
+                const unsigned e = sub * kSubwindow + bit;
+                return e > count_ ? count_ : e;
+            }
+        }
+        bit = 0;
+        ++sub;
+    }
+    return count_;
+}
+
+void DecoderCore::iterate_next_expected(unsigned start)
+{
+    if (nextExpected_ >= count_)
+        return;
+    nextExpected_ = find_next_lost(start);
+}
+
+bool DecoderCore::grow_window(unsigned end)
+{
+    const unsigned needed = (end + kLanes + kSubwindow - 1) / kSubwindow;
+    while (subwindows_.size() < needed)
+        subwindows_.emplace_back(new DecSubwindow);
+    if (end > count_)
+        count_ = end;
+    return true;
+}
+
+SiameseResult DecoderCore::add_original(const SiameseOriginalPacket& packet, uint64_t deviceSrc)
+{
+    // :1467-1536
+    if (disabled_)
+        return Siamese_Disabled;
+    const unsigned element = column_to_element(packet.PacketNum);
+    if (column_delta_negative(element)) {
+        stats_[SiameseDecoderStats_DupedOriginalCount]++;
+        return Siamese_DuplicateData;
+    }
+    grow_window(element + 1);
+    DecSubwindow* sw = subwindows_[element / kSubwindow].get();
+    const unsigned bit = element % kSubwindow;
+    DecSlot& s = sw->slot[bit];
+    if (s.bytes > 0) {
+        stats_[SiameseDecoderStats_DupedOriginalCount]++;
+        return Siamese_DuplicateData;
+    }
+
+    uint8_t hdr[kMaxLengthPrefix];
+    const unsigned h = write_length_prefix(packet.DataBytes, hdr);
+    eng_->release(s.buf);
+    s.buf = eng_->alloc(h + packet.DataBytes);
+    if (!s.buf) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    if (deviceSrc)
+        prog_.ingest_device(s.buf, deviceSrc, packet.DataBytes, hdr, h);
+    else
+        prog_.ingest_host(s.buf, packet.Data, packet.DataBytes, hdr, h);
+    if (mirror_) {
+        s.host.resize(h + packet.DataBytes);
+        std::memcpy(s.host.data(), hdr, h);
+        std::memcpy(s.host.data() + h, packet.Data, packet.DataBytes);
+    }
+    s.header = h;
+    s.bytes = h + packet.DataBytes;
+    s.column = packet.PacketNum;
+    s.pending = false;
+
+    sw->gotCount++;
+    sw->got |= 1ULL << bit;
+
+    if (element == nextExpected_) {
+        iterate_next_expected(element + 1);
+        list_delete_before(nextExpected_);
+    }
+    if (element >= region_.elementStart && element < region_.nextCheckStart)
+        region_reset();
+
+    stats_[SiameseDecoderStats_OriginalCount]++;
+    stats_[SiameseDecoderStats_OriginalBytes] += packet.DataBytes;
+    return Siamese_Success;
+}
+
+// ---------------------------------------------------------------------------
+// Running sums over received originals (:1538-1739)
+
+bool DecoderCore::grow_sum(DevSum& s, unsigned bytes)
+{
+    if (bytes <= s.bytes)
+        return true;
+    if (bytes > s.buf.cap) {
+        DevBuf nb = eng_->alloc(bytes);
+        if (!nb) {
+            disabled_ = true;
+            return false;
+        }
+        if (s.devValid) {
+            prog_.lc_begin(nb.addr(), s.devValid, 0);
+            prog_.lc_term(s.buf.addr(), s.devValid, 1);
+            prog_.lc_end();
+        }
+        eng_->release(s.buf);
+        s.buf = nb;
+    }
+    s.bytes = bytes; // [devValid, bytes) is zero, materialised lazily
+    return true;
+}
+
+void DecoderCore::materialize(DevSum& s)
+{
+    if (s.devValid >= s.bytes)
+        return;
+    prog_.lc_begin(s.buf.addr(), s.bytes, s.devValid);
+    prog_.lc_end();
+    s.devValid = s.bytes;
+}
+
+static uint8_t sum_coeff(unsigned sumIndex, unsigned column)
+{
+    if (sumIndex == 0)
+        return 1;
+    const uint8_t cx = column_value(column);
+    return sumIndex == 2 ? gf_sqr(cx) : cx;
+}
+
+DevSum& DecoderCore::get_sum(unsigned lane, unsigned s, unsigned elementEnd)
+{
+    Sum& S = sum(lane, s);
+    unsigned element = S.elementEnd;
+    if (element >= elementEnd)
+        return S.d;
+
+    unsigned newBytes = S.d.bytes;
+    struct T
+    {
+        uint64_t src;
+        unsigned len;
+        uint8_t c;
+    };
+    std::vector<T> terms;
+    do {
+        const DecSlot& o = slot(element);
+        if (o.bytes > 0) {
+            newBytes = std::max(newBytes, o.bytes);
+            terms.push_back(T{o.buf.addr(), o.bytes, sum_coeff(s, o.column)});
+        }
+        element += kLanes;
+    } while (element < elementEnd);
+
+    if (!terms.empty()) {
+        if (!grow_sum(S.d, newBytes))
+            return S.d;
+        prog_.lc_begin(S.d.buf.addr(), S.d.bytes, S.d.devValid);
+        for (const T& t : terms)
+            prog_.lc_term(t.src, t.len, t.c);
+        prog_.lc_end();
+        S.d.devValid = S.d.bytes;
+    }
+    S.elementEnd = element;
+    return S.d;
+}
+
+bool DecoderCore::plug_sum_holes(unsigned elementStart)
+{
+    for (unsigned column : recoveredColumns_) {
+        const unsigned element = column_to_element(column);
+        if (element >= count_)
+            continue;
+        const unsigned lane = column % kLanes;
+        const unsigned laneStart = next_lane_element(elementStart, lane);
+        for (unsigned s = 0; s < kSums; ++s) {
+            Sum& S = sum(lane, s);
+            if (element < laneStart || element >= S.elementEnd)
+                continue;
+            const DecSlot& o = slot(element);
+            if (o.bytes == 0)
+                return false;
+            if (!grow_sum(S.d, o.bytes))
+                return false;
+            prog_.lc_begin(S.d.buf.addr(), S.d.bytes, S.d.devValid);
+            prog_.lc_term(o.buf.addr(), o.bytes, sum_coeff(s, column));
+            prog_.lc_end();
+            S.d.devValid = S.d.bytes;
+        }
+    }
+    recoveredColumns_.clear();
+    return true;
+}
+
+void DecoderCore::reset_sums(unsigned elementStart)
+{
+    for (unsigned lane = 0; lane < kLanes; ++lane) {
+        const unsigned laneStart = next_lane_element(elementStart, lane);
+        for (unsigned s = 0; s < kSums; ++s) {
+            Sum& S = sum(lane, s);
+            S.elementStart = laneStart;
+            S.elementEnd = laneStart;
+            S.d.bytes = 0;
+            S.d.devValid = 0;
+        }
+    }
+    recoveredColumns_.clear();
+}
+
+bool DecoderCore::start_sums(unsigned elementStart, unsigned bufferBytes)
+{
+    for (unsigned lane = 0; lane < kLanes; ++lane) {
+        const unsigned laneStart = next_lane_element(elementStart, lane);
+        for (unsigned s = 0; s < kSums; ++s) {
+            Sum& S = sum(lane, s);
+            if (S.d.bytes == 0) {
+                S.elementEnd = laneStart;
+            } else if (S.elementStart != laneStart) {
+                S.elementEnd = laneStart;
+                S.d.bytes = 0;
+                S.d.devValid = 0;
+            }
+            S.elementStart = laneStart;
+            if (!grow_sum(S.d, bufferBytes))
+                return false;
+        }
+    }
+    if (!recoveredColumns_.empty() && !plug_sum_holes(elementStart))
+        return false;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Window removal (:1778-2033)
+
+void DecoderCore::remove_elements()
+{
+    if (nextExpected_ < kRemoveThreshold)
+        return;
+
+    unsigned firstKept = 0;
+    unsigned targetStart = 0, targetCount = 0, initialBytes = 0;
+    bool seenSum = false;
+
+    const RecPacket* r = head_;
+    if (!r) {
+        const RowMeta m = lastMeta_;
+        const unsigned end = column_to_element(m.columnStart + m.sumCount);
+        if (column_delta_negative(end) || end < m.ldpcCount) {
+            disabled_ = true;
+            return;
+        }
+        firstKept = end - m.ldpcCount;
+        targetStart = m.columnStart;
+        targetCount = m.sumCount;
+        initialBytes = lastBytes_;
+        if (m.sumCount > kCauchyThreshold)
+            seenSum = true;
+    } else {
+        firstKept = r->elementStart;
+        initialBytes = r->bytes;
+        for (;;) {
+            const unsigned sc = r->meta.sumCount;
+            const unsigned cs = r->meta.columnStart;
+            if (sc > kCauchyThreshold) {
+                if (!seenSum) {
+                    targetStart = cs;
+                    targetCount = sc;
+                    seenSum = true;
+                } else if (cs != targetStart || sc < targetCount) {
+                    const unsigned firstSum = column_to_element(cs);
+                    if (firstSum >= count_) {
+                        disabled_ = true;
+                        return;
+                    }
+                    if (firstKept > firstSum)
+                        firstKept = firstSum;
+                }
+            }
+            r = r->next;
+            if (!r)
+                break;
+            if (firstKept > r->elementStart)
+                firstKept = r->elementStart;
+            if (initialBytes < r->bytes)
+                initialBytes = r->bytes;
+        }
+    }
+
+    if (firstKept < kRemoveThreshold)
+        return;
+
+    const unsigned keptSub = firstKept / kSubwindow;
+    const unsigned removed = keptSub * kSubwindow;
+
+    if (seenSum) {
+        unsigned sumElementStart = column_to_element(targetStart);
+        if (sumColumnStart_ != targetStart || sumColumnCount_ > targetCount) {
+            if (sumElementStart >= count_) {
+                disabled_ = true;
+                return;
+            }
+            reset_sums(sumElementStart);
+            sumColumnStart_ = targetStart;
+            sumColumnCount_ = targetCount;
+        } else {
+            if (sumElementStart >= count_)
+                sumElementStart = 0;
+            if (!start_sums(sumElementStart, initialBytes)) {
+                disabled_ = true;
+                return;
+            }
+        }
+        for (unsigned lane = 0; lane < kLanes; ++lane) {
+            for (unsigned s = 0; s < kSums; ++s) {
+                get_sum(lane, s, removed);
+                Sum& S = sum(lane, s);
+                if (S.elementStart >= removed)
+                    S.elementStart -= removed;
+                else
+                    S.elementStart = lane;
+                S.elementEnd -= removed;
+            }
+        }
+    } else {
+        // Only Cauchy rows remain: stop maintaining running sums
+        sumColumnCount_ = 0;
+    }
+
+    for (unsigned i = 0; i < keptSub; ++i)
+        subwindows_[i]->reset();
+    std::rotate(subwindows_.begin(), subwindows_.begin() + keptSub, subwindows_.end());
+
+    count_ -= removed;
+    columnStart_ = element_to_column(removed);
+    nextExpected_ -= removed;
+
+    for (RecPacket* p = head_; p; p = p->next) {
+        p->elementEnd -= removed;
+        p->elementStart -= removed;
+    }
+    if (region_.elementStart < removed || region_.nextCheckStart < removed)
+        region_reset();
+    else {
+        region_.elementStart -= removed;
+        region_.nextCheckStart -= removed;
+    }
+    prevNextCheckStart_ = prevNextCheckStart_ > removed ? prevNextCheckStart_ - removed : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Recovery packet list (:2567-2666)
+
+void DecoderCore::free_packet(RecPacket* r)
+{
+    eng_->release(r->buf);
+    delete r;
+}
+
+void DecoderCore::list_insert(RecPacket* r, bool outOfOrder)
+{
+    RecPacket* prev = tail_;
+    RecPacket* next = nullptr;
+    const unsigned rs = r->meta.columnStart;
+    const unsigned re = r->elementEnd;
+    // Keep both edges of the recovery ranges monotone (SiameseDecoder.h:40-50)
+    for (; prev; next = prev, prev = prev->prev) {
+        const unsigned pe = prev->elementEnd;
+        if (re >= pe) {
+            if (re > pe)
+                break;
+            if (column_delta_negative(column_sub(rs, prev->meta.columnStart)))
+                break;
+        }
+    }
+    r->next = next;
+    r->prev = prev;
+    if (prev)
+        prev->next = r;
+    else
+        head_ = r;
+    if (next)
+        next->prev = r;
+    else
+        tail_ = r;
+    if (!prev || next)
+        region_reset(); // a smaller solution may now exist
+    ++listCount_;
+    if (!outOfOrder) {
+        lastMeta_ = r->meta;
+        lastBytes_ = r->bytes;
+    }
+}
+
+void DecoderCore::list_delete_before(unsigned element)
+{
+    RecPacket* r = head_;
+    unsigned deleted = 0;
+    while (r && r->elementEnd <= element) {
+        RecPacket* n = r->next;
+        free_packet(r);
+        ++deleted;
+        r = n;
+    }
+    head_ = r;
+    if (r) {
+        r->prev = nullptr;
+        listCount_ -= deleted;
+    } else {
+        tail_ = nullptr;
+        listCount_ = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Recovery packets in (:257-539)
+
+SiameseResult DecoderCore::add_recovery(const SiameseRecoveryPacket& packet)
+{
+    if (disabled_)
+        return Siamese_Disabled;
+    RowMeta m;
+    const int footer = read_footer(packet.Data, packet.DataBytes, &m);
+    if (footer < 0) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    return add_recovery_common(m, footer, packet.DataBytes, packet.Data, 0, packet.Data, nullptr);
+}
+
+SiameseResult DecoderCore::add_recovery_device(const DeviceRecovery& rec)
+{
+    if (disabled_)
+        return Siamese_Disabled;
+    RowMeta m;
+    // The footer sits at the end of the packet; the producer handed us a
+    // host copy of exactly those bytes.
+    int footer = read_footer(rec.footer, rec.footerBytes, &m);
+    if (footer < 0 || (unsigned)footer != rec.footerBytes) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    return add_recovery_common(m, footer, rec.bytes, nullptr, rec.data, rec.head, rec.producer);
+}
+
+SiameseResult DecoderCore::add_recovery_common(const RowMeta& m, int footer, unsigned totalBytes,
+                                               const void* hostData, uint64_t devData,
+                                               const uint8_t* headBytes, Program* producer)
+{
+    stats_[SiameseDecoderStats_RecoveryCount]++;
+    stats_[SiameseDecoderStats_RecoveryBytes] += totalBytes;
+
+    const bool outOfOrder = column_delta_negative(m.columnStart + m.sumCount - latestColumn_);
+    if (!outOfOrder)
+        latestColumn_ = (m.columnStart + m.sumCount) % kColumnPeriod;
+
+    unsigned elementStart, elementEnd;
+    if (count_ == 0) {
+        if (outOfOrder) {
+            stats_[SiameseDecoderStats_DupedRecoveryCount]++;
+            return Siamese_Success;
+        }
+        columnStart_ = m.columnStart;
+        grow_window(m.sumCount);
+        elementEnd = m.sumCount;
+        elementStart = elementEnd - m.ldpcCount;
+    } else {
+        elementEnd = column_to_element(m.columnStart + m.sumCount);
+        if (column_delta_negative(elementEnd) || elementEnd < m.ldpcCount) {
+            stats_[SiameseDecoderStats_DupedRecoveryCount]++;
+            return Siamese_Success;
+        }
+        elementStart = elementEnd - m.ldpcCount;
+        if (elementEnd <= nextExpected_) {
+            if (outOfOrder) {
+                stats_[SiameseDecoderStats_DupedRecoveryCount]++;
+                return Siamese_Success;
+            }
+            if (elementStart >= kRemoveThreshold) {
+                lastMeta_ = m;
+                lastBytes_ = totalBytes - footer;
+                remove_elements();
+            }
+            stats_[SiameseDecoderStats_DupedRecoveryCount]++;
+            return Siamese_Success;
+        }
+        if (m.sumCount > kCauchyThreshold) {
+            if (sumColumnCount_ == 0 || sumColumnStart_ != m.columnStart) {
+                if (column_to_element(m.columnStart) >= count_) {
+                    stats_[SiameseDecoderStats_DupedRecoveryCount]++;
+                    return Siamese_Success;
+                }
+            }
+        }
+        grow_window(elementEnd);
+    }
+
+    const unsigned payload = totalBytes - footer;
+    if (m.sumCount == 1) {
+        if (!add_single(m, headBytes, payload, hostData, devData, producer)) {
+            disabled_ = true;
+            return Siamese_Disabled;
+        }
+        return Siamese_Success;
+    }
+
+    RecPacket* r = new RecPacket;
+    r->buf = eng_->alloc(payload + payload / 16);
+    if (!r->buf) {
+        delete r;
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    static const uint8_t none[1] = {0};
+    if (hostData)
+        prog_.ingest_host(r->buf, hostData, payload, none, 0);
+    else if (producer) {
+        producer->lc_begin(r->buf.addr(), payload, 0);
+        producer->lc_term(devData, payload, 1);
+        producer->lc_end();
+    } else
+        prog_.ingest_device(r->buf, devData, payload, none, 0);
+    r->bytes = payload;
+    r->meta = m;
+    r->elementStart = elementStart;
+    r->elementEnd = elementEnd;
+    list_insert(r, outOfOrder);
+    if (elementStart >= kRemoveThreshold)
+        remove_elements();
+    return Siamese_Success;
+}
+
+bool DecoderCore::add_single(const RowMeta& m, const uint8_t* headBytes, unsigned payloadBytes,
+                             const void* hostData, uint64_t devData, Program* producer)
+{
+    const unsigned element = column_to_element(m.columnStart);
+    if (element >= count_)
+        return false;
+    DecSlot& s = slot(element);
+    if (s.bytes != 0)
+        return true; // duplicate of data we already hold
+
+    unsigned length = 0;
+    const int headerBytes = read_length_prefix(headBytes, std::min(payloadBytes, kMaxLengthPrefix), &length);
+    if (headerBytes < 1 || length == 0 || length + (unsigned)headerBytes != payloadBytes)
+        return false;
+
+    uint8_t hdr[kMaxLengthPrefix];
+    const unsigned h = write_length_prefix(length, hdr);
+    eng_->release(s.buf);
+    s.buf = eng_->alloc(h + length);
+    if (!s.buf)
+        return false;
+    if (hostData)
+        prog_.ingest_host(s.buf, (const uint8_t*)hostData + headerBytes, length, hdr, h);
+    else if (producer && (unsigned)headerBytes == h) {
+        // Same byte alignment: an in-order copy on the producing program
+        producer->lc_begin(s.buf.addr(), h + length, 0);
+        producer->lc_term(devData, h + length, 1);
+        producer->lc_end();
+    } else
+        prog_.ingest_device(s.buf, devData + headerBytes, length, hdr, h);
+    if (mirror_) {
+        s.host.resize(h + length);
+        std::memcpy(s.host.data(), hdr, h);
+        std::memcpy(s.host.data() + h, (const uint8_t*)hostData + headerBytes, length);
+    }
+    s.header = h;
+    s.bytes = h + length;
+    s.column = m.columnStart;
+    s.pending = false;
+
+    if (!hasRecovered_) {
+        hasRecovered_ = true;
+        recovered_.clear();
+    }
+    SiameseOriginalPacket out;
+    out.PacketNum = m.columnStart;
+    out.DataBytes = length;
+    out.Data = (mirror_ ? s.host.data() : s.buf.ptr) + h;
+    recovered_.push_back(out);
+    recoveredColumns_.push_back(m.columnStart);
+
+    if (element >= region_.elementStart && element < region_.nextCheckStart)
+        region_reset();
+
+    if (mark_got(m.columnStart)) {
+        iterate_next_expected(element + 1);
+        list_delete_before(nextExpected_);
+        if (region_.nextCheckStart >= kRemoveThreshold)
+            remove_elements();
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Solvability search and decode driver (:541-810)
+
+void DecoderCore::matrix_reset()
+{
+    cols_.clear();
+    rows_.clear();
+    pivots_.clear();
+    matRows_ = matCols_ = 0;
+    prevNextCheckStart_ = 0;
+    geResume_ = 0;
+}
+
+void DecoderCore::region_reset()
+{
+    region_.elementStart = 0;
+    region_.nextCheckStart = 0;
+    region_.first = nullptr;
+    region_.last = nullptr;
+    region_.recoveryCount = 0;
+    region_.lostCount = 0;
+    region_.solveFailed = false;
+    matrix_reset();
+}
+
+bool DecoderCore::check_recovery_possible()
+{
+    if (disabled_)
+        return false;
+    RecPacket* r;
+    unsigned nextCheck, recCount, lost;
+    if (!region_.last) {
+        r = head_;
+        if (!r)
+            return false;
+        region_.first = r;
+        region_.elementStart = r->elementStart;
+        recCount = 1;
+        nextCheck = r->elementEnd;
+        lost = range_lost(r->elementStart, nextCheck);
+        region_.solveFailed = false;
+        r->lostCount = lost;
+    } else {
+        recCount = region_.recoveryCount;
+        lost = region_.lostCount;
+        if (recCount >= lost && !region_.solveFailed)
+            return lost <= kMaxLossRecovery;
+        r = region_.last;
+        nextCheck = region_.nextCheckStart;
+    }
+    while ((recCount < lost || region_.solveFailed) && r->next) {
+        r = r->next;
+        ++recCount;
+        unsigned end = r->elementEnd;
+        if (end < nextCheck)
+            end = nextCheck;
+        lost += range_lost(nextCheck, end);
+        nextCheck = end;
+        r->lostCount = lost;
+        region_.solveFailed = false;
+    }
+    region_.last = r;
+    region_.recoveryCount = recCount;
+    region_.lostCount = lost;
+    region_.nextCheckStart = nextCheck;
+    if (lost > kMaxLossRecovery)
+        return false;
+    return recCount >= lost && !region_.solveFailed;
+}
+
+SiameseResult DecoderCore::is_ready()
+{
+    if (hasRecovered_ || check_recovery_possible())
+        return Siamese_Success;
+    return Siamese_NeedMoreData;
+}
+
+SiameseResult DecoderCore::decode(SiameseOriginalPacket** packetsOut, unsigned* countOut)
+{
+    if (disabled_)
+        return Siamese_Disabled;
+    if (hasRecovered_) {
+        hasRecovered_ = false;
+        if (packetsOut) {
+            *packetsOut = recovered_.data();
+            *countOut = (unsigned)recovered_.size();
+        }
+        return Siamese_Success;
+    }
+    if (packetsOut) {
+        *packetsOut = nullptr;
+        *countOut = 0;
+    }
+    if (!check_recovery_possible())
+        return Siamese_NeedMoreData;
+
+    RecPacket* r = region_.last;
+    unsigned nextCheck = region_.nextCheckStart;
+    unsigned recCount = region_.recoveryCount;
+    unsigned lost = region_.lostCount;
+
+    for (;;) {
+        if (recCount >= lost) {
+            const SiameseResult res = decode_region();
+            if (res == Siamese_Success) {
+                if (packetsOut) {
+                    *packetsOut = recovered_.data();
+                    *countOut = (unsigned)recovered_.size();
+                }
+                return Siamese_Success;
+            }
+            if (res != Siamese_NeedMoreData)
+                return res;
+        }
+        if (!r->next)
+            break;
+        r = r->next;
+        ++recCount;
+        unsigned end = r->elementEnd;
+        if (end < nextCheck)
+            end = nextCheck;
+        lost += range_lost(nextCheck, end);
+        r->lostCount = lost;
+        nextCheck = end;
+    }
+    region_.last = r;
+    region_.nextCheckStart = nextCheck;
+    region_.recoveryCount = recCount;
+    region_.lostCount = lost;
+    return Siamese_NeedMoreData;
+}
+
+SiameseResult DecoderCore::decode_region()
+{
+    if (!generate_matrix()) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    if (!gaussian_elimination()) {
+        region_.solveFailed = true;
+        stats_[SiameseDecoderStats_SolveFailCount]++;
+        return Siamese_NeedMoreData;
+    }
+    if (!eliminate_original_data()) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    const SiameseResult res = solve_and_substitute();
+    region_reset();
+    return res;
+}
+
+// ---------------------------------------------------------------------------
+// Recovery matrix on coefficients (:2039-2531)
+
+bool DecoderCore::matrix_resize(unsigned rows, unsigned columns, bool initialize)
+{
+    // GrowingAlignedByteMatrix semantics (reference SiameseCommon.cpp:51-117)
+    const unsigned stride = align_up(columns + 4);
+    if (initialize) {
+        matAllocRows_ = rows + 4;
+        matStride_ = stride;
+        mat_.resize((size_t)matAllocRows_ * matStride_);
+    } else if (!(rows <= matAllocRows_ && columns <= matStride_)) {
+        std::vector<uint8_t> nm((size_t)(rows + 4) * stride);
+        const unsigned copy = std::min(matCols_, columns);
+        if (matCols_ > 0)
+            for (unsigned i = 0; i < matRows_; ++i)
+                std::memcpy(nm.data() + (size_t)i * stride, mat_.data() + (size_t)i * matStride_, copy);
+        mat_.swap(nm);
+        matAllocRows_ = rows + 4;
+        matStride_ = stride;
+    }
+    matRows_ = rows;
+    matCols_ = columns;
+    return true;
+}
+
+void DecoderCore::populate_columns(unsigned oldColumns, unsigned newColumns)
+{
+    if (oldColumns >= newColumns)
+        return;
+    cols_.resize(newColumns);
+    unsigned elementStart = prevNextCheckStart_;
+    prevNextCheckStart_ = region_.nextCheckStart;
+    const unsigned elementEnd = region_.nextCheckStart;
+    if (elementStart < region_.elementStart)
+        elementStart = region_.elementStart;
+    const unsigned subEnd = (elementEnd + kSubwindow - 1) / kSubwindow;
+    unsigned sub = elementStart / kSubwindow;
+    unsigned bit = elementStart % kSubwindow;
+    unsigned column = oldColumns;
+    while (sub < subEnd) {
+        DecSubwindow* sw = subwindows_[sub].get();
+        if (sw->gotCount < kSubwindow) {
+            do {
+                bit = first_clear(sw->got, bit);
+                if (bit >= kSubwindow)
+                    break;
+                ColInfo& c = cols_[column];
+                c.column = element_to_column(sub * kSubwindow + bit);
+                c.original = &sw->slot[bit];
+                c.cx = column_value(c.column);
+                c.original->column = column; // lost slot -> matrix column
+                if (++column >= newColumns)
+                    return;
+            } while (++bit < kSubwindow);
+        }
+        bit = 0;
+        ++sub;
+    }
+    disabled_ = true; // ran out of lost columns: should never happen
+}
+
+void DecoderCore::populate_rows(unsigned oldRows, unsigned newRows)
+{
+    if (oldRows >= newRows)
+        return;
+    rows_.resize(newRows);
+    RecPacket* r = oldRows > 0 ? rows_[oldRows - 1].rec->next : region_.first;
+    for (unsigned i = oldRows; i < newRows; ++i, r = r->next) {
+        rows_[i].rec = r;
+        rows_[i].used = false;
+        rows_[i].columnCount = r->lostCount;
+    }
+}
+
+bool DecoderCore::generate_matrix()
+{
+    const unsigned columns = region_.lostCount;
+    const unsigned rows = region_.recoveryCount;
+    unsigned oldRows = (unsigned)rows_.size();
+    unsigned oldColumns = (unsigned)cols_.size();
+    if (rows < oldRows || columns < oldColumns) {
+        matrix_reset();
+        oldRows = 0;
+        oldColumns = 0;
+    }
+    matrix_resize(rows, columns, oldRows == 0);
+    populate_columns(oldColumns, columns);
+    populate_rows(oldRows, rows);
+
+    const unsigned startRow = (columns <= oldColumns) ? oldRows : 0;
+    const size_t matBytes = mat_.size();
+    for (unsigned i = startRow; i < rows; ++i) {
+        uint8_t* row = mrow(i);
+        const RecPacket* rec = rows_[i].rec;
+        const RowMeta m = rec->meta;
+        const unsigned startCol = (i < oldRows) ? oldColumns : 0;
+
+        if (m.sumCount <= kCauchyThreshold) {
+            for (unsigned j = startCol; j < columns; ++j) {
+                const unsigned column = cols_[j].column;
+                if (column_sub(column, m.columnStart) >= m.sumCount) {
+                    std::memset(row + j, 0, columns - j);
+                    break;
+                }
+                row[j] = m.row == 0 ? 1 : cauchy_element(m.row - 1, column % kCauchyMaxColumns);
+            }
+            continue;
+        }
+
+        const uint8_t rx = row_value(m.row);
+        for (unsigned j = startCol; j < columns; ++j) {
+            const unsigned column = cols_[j].column;
+            if (column_sub(column, m.columnStart) >= m.sumCount) {
+                std::memset(row + j, 0, columns - j);
+                break;
+            }
+            const uint8_t cx = cols_[j].cx;
+            const uint8_t cx2 = gf_sqr(cx);
+            const unsigned op = row_opcode(column % kLanes, m.row);
+            uint8_t v = 0;
+            if (op & 1)
+                v ^= 1;
+            if (op & 2)
+                v ^= cx;
+            if (op & 4)
+                v ^= cx2;
+            if (op & 8)
+                v ^= rx;
+            if (op & 16)
+                v ^= gf_mul(cx, rx);
+            if (op & 32)
+                v ^= gf_mul(cx2, rx);
+            row[j] = v;
+        }
+
+        // Sparse columns that landed on lost data
+        Pcg32 prng;
+        prng.seed(m.row, m.ldpcCount);
+        const unsigned pairs = (m.ldpcCount + kPairRate - 1) / kPairRate;
+        const size_t rowOff = (size_t)i * matStride_;
+        for (unsigned k = 0; k < pairs; ++k) {
+            const DecSlot& a = slot(rec->elementStart + prng.next() % m.ldpcCount);
+            if (a.bytes == 0 && a.column >= startCol && rowOff + a.column < matBytes)
+                mat_[rowOff + a.column] ^= 1;
+            const DecSlot& b = slot(rec->elementStart + prng.next() % m.ldpcCount);
+            if (b.bytes == 0 && b.column >= startCol && rowOff + b.column < matBytes)
+                mat_[rowOff + b.column] ^= rx;
+        }
+    }
+
+    pivots_.resize(rows);
+    for (unsigned i = oldRows; i < rows; ++i)
+        pivots_[i] = i;
+    if (geResume_ > 0)
+        resume_ge(oldRows, rows);
+    return true;
+}
+
+bool DecoderCore::eliminate_row(const uint8_t* geRow, uint8_t* remRow, unsigned pivot, unsigned end,
+                                uint8_t valI)
+{
+    // SiameseDecoder.h:522-541
+    const uint8_t valJ = remRow[pivot];
+    if (valJ == 0)
+        return false;
+    const uint8_t y = gf_div(valJ, valI);
+    remRow[pivot] = y;
+    if (end > pivot + 1)
+        gf_muladd_row(remRow + pivot + 1, geRow + pivot + 1, y, end - pivot - 1);
+    return true;
+}
+
+void DecoderCore::resume_ge(unsigned oldRows, unsigned rows)
+{
+    if (oldRows >= rows)
+        return;
+    for (unsigned p = 0; p < geResume_; ++p) {
+        const unsigned ri = pivots_[p];
+        const uint8_t* ge = mrow(ri);
+        const uint8_t val = ge[p];
+        const unsigned end = rows_[ri].columnCount;
+        for (unsigned k = oldRows; k < rows; ++k)
+            if (eliminate_row(ge, mrow(k), p, end, val) && rows_[k].columnCount < end)
+                rows_[k].columnCount = end;
+    }
+}
+
+bool DecoderCore::gaussian_elimination()
+{
+    if (geResume_ > 0)
+        return pivoted_ge(geResume_);
+    const unsigned columns = matCols_;
+    const unsigned rows = matRows_;
+    for (unsigned p = 0; p < columns; ++p) {
+        uint8_t* ge = mrow(p);
+        const uint8_t val = ge[p];
+        if (val == 0)
+            return pivoted_ge(p);
+        rows_[p].used = true;
+        const unsigned end = rows_[p].columnCount;
+        for (unsigned k = p + 1; k < rows; ++k)
+            eliminate_row(ge, mrow(k), p, end, val);
+    }
+    return true;
+}
+
+bool DecoderCore::pivoted_ge(unsigned pivot)
+{
+    const unsigned columns = matCols_;
+    const unsigned rows = matRows_;
+    unsigned j = pivot + 1; // the caller already found column `pivot` zero here
+    bool resume = true;
+    for (; pivot < columns; ++pivot) {
+        if (!resume)
+            j = pivot;
+        resume = false;
+        bool found = false;
+        for (; j < rows; ++j) {
+            const unsigned rj = pivots_[j];
+            const uint8_t* ge = mrow(rj);
+            const uint8_t val = ge[pivot];
+            if (val == 0)
+                continue;
+            if (pivot != j)
+                std::swap(pivots_[pivot], pivots_[j]);
+            rows_[rj].used = true;
+            const unsigned end = rows_[rj].columnCount;
+            if (pivot >= columns - 1)
+                return true;
+            for (unsigned k = pivot + 1; k < rows; ++k) {
+                const unsigned rk = pivots_[k];
+                if (eliminate_row(ge, mrow(rk), pivot, end, val) && rows_[rk].columnCount < end)
+                    rows_[rk].columnCount = end;
+            }
+            found = true;
+            break;
+        }
+        if (!found) {
+            geResume_ = pivot;
+            return false;
+        }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Eliminate received data from the used rows (:812-1063)
+
+bool DecoderCore::eliminate_original_data()
+{
+    const unsigned rows = region_.recoveryCount;
+    for (unsigned ri = 0; ri < rows; ++ri) {
+        if (!rows_[ri].used)
+            continue;
+        RecPacket* rec = rows_[ri].rec;
+        const RowMeta m = rec->meta;
+        const unsigned es = rec->elementStart;
+        const unsigned ee = rec->elementEnd;
+        const unsigned rb = rec->bytes;
+
+        if (m.sumCount <= kCauchyThreshold) {
+            prog_.lc_begin(rec->buf.addr(), rb, rb);
+            for (unsigned j = es; j < ee; ++j) {
+                const DecSlot& o = slot(j);
+                if (o.bytes == 0)
+                    continue;
+                const uint8_t y = m.row == 0 ? 1 : cauchy_element(m.row - 1, o.column % kCauchyMaxColumns);
+                prog_.lc_term(o.buf.addr(), std::min(o.bytes, rb), y);
+            }
+            prog_.lc_end();
+            continue;
+        }
+
+        unsigned sumElementStart = column_to_element(m.columnStart);
+        if (m.columnStart != sumColumnStart_ || m.sumCount < sumColumnCount_) {
+            if (sumElementStart >= count_)
+                return false;
+            reset_sums(sumElementStart);
+            sumColumnStart_ = m.columnStart;
+        } else {
+            if (sumElementStart >= count_)
+                sumElementStart = 0;
+            if (!start_sums(sumElementStart, rb))
+                return false;
+        }
+        sumColumnCount_ = m.sumCount;
+
+        struct T
+        {
+            uint64_t src;
+            unsigned len;
+            uint8_t acc;
+        };
+        std::vector<T> terms;
+        for (unsigned lane = 0; lane < kLanes; ++lane) {
+            const unsigned op = row_opcode(lane, m.row);
+            for (unsigned bit = 0; bit < 2 * kSums; ++bit) {
+                if (!(op & (1u << bit)))
+                    continue;
+                DevSum& s = get_sum(lane, bit % kSums, ee);
+                if (s.bytes > 0) {
+                    materialize(s);
+                    terms.push_back(T{s.buf.addr(), std::min(s.bytes, rb), (uint8_t)(bit / kSums)});
+                }
+            }
+        }
+        Pcg32 prng;
+        prng.seed(m.row, m.ldpcCount);
+        const unsigned pairs = (m.ldpcCount + kPairRate - 1) / kPairRate;
+        for (unsigned k = 0; k < pairs; ++k) {
+            const DecSlot& a = slot(es + prng.next() % m.ldpcCount);
+            if (a.bytes > 0)
+                terms.push_back(T{a.buf.addr(), std::min(a.bytes, rb), 0});
+            const DecSlot& b = slot(es + prng.next() % m.ldpcCount);
+            if (b.bytes > 0)
+                terms.push_back(T{b.buf.addr(), std::min(b.bytes, rb), 1});
+        }
+        prog_.lc_begin(rec->buf.addr(), rb, rb, row_value(m.row));
+        for (const T& t : terms)
+            prog_.lc_term(t.src, t.len, 1, t.acc);
+        prog_.lc_end();
+    }
+    return !disabled_;
+}
+
+// ---------------------------------------------------------------------------
+// Lower-triangle multiply + back-substitution (:1065-1238) as one device solve
+
+SiameseResult DecoderCore::solve_and_substitute()
+{
+    const unsigned m = region_.lostCount;
+    std::vector<RecPacket*> pr(m);
+    std::vector<unsigned> len(m);
+    for (unsigned i = 0; i < m; ++i) {
+        pr[i] = rows_[pivots_[i]].rec;
+        len[i] = pr[i]->bytes;
+    }
+    std::vector<SolveRow> desc(m);
+    for (unsigned i = 0; i < m; ++i) {
+        std::memset(&desc[i], 0, sizeof(SolveRow));
+        desc[i].initBytes = len[i];
+    }
+    // Row growth of MultiplyLowerTriangle (GrowZeroPadded), simulated here
+    for (unsigned i = 0; i + 1 < m; ++i) {
+        desc[i].lowerLen = len[i];
+        for (unsigned j = i + 1; j < m; ++j)
+            if (mrow(pivots_[j])[i] != 0 && len[j] < len[i])
+                len[j] = len[i];
+    }
+    if (m > 0)
+        desc[m - 1].lowerLen = len[m - 1];
+
+    uint32_t maxBytes = 0;
+    for (unsigned i = 0; i < m; ++i) {
+        RecPacket* r = pr[i];
+        if (len[i] > r->buf.cap) {
+            DevBuf nb = eng_->alloc(len[i]);
+            if (!nb) {
+                disabled_ = true;
+                return Siamese_Disabled;
+            }
+            prog_.lc_begin(nb.addr(), desc[i].initBytes, 0);
+            prog_.lc_term(r->buf.addr(), desc[i].initBytes, 1);
+            prog_.lc_end();
+            eng_->release(r->buf);
+            r->buf = nb;
+        }
+        desc[i].buf = r->buf.addr();
+        desc[i].finalBytes = len[i];
+        maxBytes = std::max(maxBytes, len[i]);
+    }
+    std::vector<uint8_t> coef((size_t)m * m);
+    for (unsigned j = 0; j < m; ++j)
+        std::memcpy(coef.data() + (size_t)j * m, mrow(pivots_[j]), m);
+
+    const uint32_t base = prog_.solve(desc, coef, maxBytes);
+
+    // Host side of BackSubstitution: swap buffers into the window, record
+    // the outputs (lengths patched in resolve()).
+    recovered_.resize(m);
+    ++decodeSerial_;
+    std::vector<Fix> fixes;
+    fixes.reserve(m);
+    bool advanced = false;
+    for (int ci = (int)m - 1; ci >= 0; --ci) {
+        RecPacket* r = pr[ci];
+        ColInfo& col = cols_[ci];
+        DecSlot* o = col.original;
+        DevBuf old = o->buf;
+        o->buf = r->buf;
+        o->bytes = len[ci];
+        o->column = col.column;
+        o->header = 0;
+        o->pending = true;
+        r->buf = old;
+        r->bytes = 0;
+        SiameseOriginalPacket& out = recovered_[ci];
+        out.PacketNum = col.column;
+        out.DataBytes = 0;
+        out.Data = nullptr;
+        recoveredColumns_.push_back(col.column);
+        advanced |= mark_got(col.column);
+        fixes.push_back(Fix{o, o->buf.ptr, (uint32_t)ci, (unsigned)ci, len[ci]});
+    }
+    lastDecoded_ = fixes;
+    std::weak_ptr<int> alive = alive_;
+    const uint64_t serial = decodeSerial_;
+    pendingSolves_++;
+    eng_->on_complete([this, alive, fixes, base, m, serial](const uint32_t* results) {
+        if (alive.expired())
+            return;
+        resolve_solve(results, base, m, fixes, serial);
+    });
+
+    if (!advanced) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    iterate_next_expected(region_.nextCheckStart);
+    list_delete_before(nextExpected_);
+    if (region_.nextCheckStart >= kRemoveThreshold)
+        remove_elements();
+    stats_[SiameseDecoderStats_SolveSuccessCount]++;
+    return Siamese_Success;
+}
+
+void DecoderCore::resolve_solve(const uint32_t* results, uint32_t base, unsigned m,
+                                const std::vector<Fix>& fixes, uint64_t serial)
+{
+    const unsigned okCount = results[base];
+    if (okCount < m)
+        disabled_ = true; // corrupt length prefix (reference :1142-1154)
+    for (const Fix& f : fixes) {
+        const unsigned ci = f.outIndex;
+        if (ci + okCount < m)
+            continue; // not reached before the failure
+        const uint32_t w = results[base + 1 + ci];
+        const unsigned hdr = w >> 29;
+        const unsigned len = w & kSolveLengthMask;
+        DecSlot* s = f.slot;
+        if (s->pending && s->buf.ptr == f.buf) {
+            s->bytes = hdr + len;
+            s->header = hdr;
+            s->pending = false;
+            if (mirror_ && s->host.size() < s->bytes)
+                s->host.resize(s->bytes);
+        }
+        if (serial == decodeSerial_ && ci < recovered_.size()) {
+            SiameseOriginalPacket& out = recovered_[ci];
+            out.DataBytes = len;
+            out.Data = (mirror_ ? s->host.data() : f.buf) + hdr;
+        }
+    }
+    pendingSolves_--;
+}
+
+void DecoderCore::download_recovered()
+{
+    if (!mirror_)
+        return;
+    for (const Fix& f : lastDecoded_) {
+        DecSlot* s = f.slot;
+        s->host.resize(f.bound);
+        eng_->download(s->host.data(), (uint64_t)(uintptr_t)f.buf, f.bound);
+    }
+    lastDecoded_.clear();
+}
+
+SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
+{
+    if (disabled_)
+        return Siamese_Disabled;
+    const unsigned element = column_to_element(packet.PacketNum);
+    if (element >= count_ || slot(element).bytes == 0) {
+        packet.Data = nullptr;
+        packet.DataBytes = 0;
+        return Siamese_NeedMoreData;
+    }
+    if (slot(element).pending) {
+        // Exact length still on the device: finish the outstanding work.
+        eng_->flush_and_sync();
+        if (disabled_)
+            return Siamese_Disabled;
+    }
+    DecSlot& s = slot(element);
+    packet.Data = (mirror_ ? s.host.data() : s.buf.ptr) + s.header;
+    packet.DataBytes = s.bytes - s.header;
+    return Siamese_Success;
+}
+
+SiameseResult DecoderCore::stats(uint64_t* out, unsigned count)
+{
+    if (count > SiameseDecoderStats_Count)
+        count = SiameseDecoderStats_Count;
+    uint64_t mem = 0;
+    for (auto& sw : subwindows_)
+        for (DecSlot& s : sw->slot)
+            mem += s.buf.cap;
+    for (auto& lane : lanes_)
+        for (Sum& s : lane)
+            mem += s.d.buf.cap;
+    for (RecPacket* r = head_; r; r = r->next)
+        mem += r->buf.cap;
+    stats_[SiameseDecoderStats_MemoryUsed] = mem;
+    for (unsigned i = 0; i < count; ++i)
+        out[i] = stats_[i];
+    return Siamese_Success;
+}
+
+} // namespace sgpu

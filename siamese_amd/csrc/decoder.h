@@ -1,0 +1,248 @@
+// decoder.h -- host control plane of the decoder.
+//
+// The bookkeeping (receive window, recovery list ordering, checked region,
+// matrix generation and Gaussian elimination on coefficients) mirrors the
+// reference decoder so decode timing and results are identical
+// (reference SiameseDecoder.h:108-632, SiameseDecoder.cpp:255-2700).
+// Symbol work -- eliminating received originals, lane sums, the triangular
+// solve -- is emitted as device ops; coefficients never leave the host.
+//
+// Recovered lengths are only known once the device has solved the length
+// prefix.  Until then a recovered slot carries an UPPER BOUND (its recovery
+// row's length) with the device guaranteeing zeros beyond the true length,
+// which makes every later op numerically identical; the exact value is
+// patched in when the flush completes (see resolve()).
+#pragma once
+
+#include "codedef.h"
+#include "encoder.h"
+#include "engine.h"
+#include "../../include/siamese.h"
+
+#include <memory>
+#include <vector>
+
+namespace sgpu {
+
+struct DecSlot
+{
+    DevBuf buf;
+    unsigned bytes = 0;         // prefix + payload (upper bound while pending)
+    unsigned column = 0;        // packet number, or matrix column while lost
+    unsigned header = 0;
+    bool pending = false;       // recovered, exact length not yet known
+    std::vector<uint8_t> host;  // host mirror (drop-in mode)
+};
+
+struct DecSubwindow
+{
+    DecSlot slot[kSubwindow];
+    uint64_t got = 0;           // CustomBitSet<64> (PacketAllocator.h:189-437)
+    unsigned gotCount = 0;
+    void reset()
+    {
+        got = 0;
+        gotCount = 0;
+        for (DecSlot& s : slot) {
+            s.column = 0;
+            s.bytes = 0;
+            s.pending = false;
+        }
+    }
+};
+
+struct RecPacket
+{
+    RecPacket* next = nullptr;
+    RecPacket* prev = nullptr;
+    RowMeta meta;
+    unsigned elementStart = 0;
+    unsigned elementEnd = 0;
+    unsigned lostCount = 0;
+    DevBuf buf;
+    unsigned bytes = 0;
+};
+
+/// Handle to a recovery packet that already lives in device memory (batch API).
+struct DeviceRecovery
+{
+    uint64_t data = 0;          // device address of the packet (payload+footer)
+    unsigned bytes = 0;
+    const uint8_t* footer = nullptr;  // host copy of the footer bytes
+    unsigned footerBytes = 0;
+    const uint8_t* head = nullptr;    // host copy of the first bytes (single rows)
+    Program* producer = nullptr;      // program that must perform the copy
+};
+
+class DecoderCore
+{
+public:
+    DecoderCore(Engine* eng, bool hostMirror);
+    ~DecoderCore();
+
+    Program& program() { return prog_; }
+
+    SiameseResult add_original(const SiameseOriginalPacket& packet, uint64_t deviceSrc = 0);
+    /// Host-memory recovery packet (drop-in API).
+    SiameseResult add_recovery(const SiameseRecoveryPacket& packet);
+    /// Device-resident recovery packet (batch API).
+    SiameseResult add_recovery_device(const DeviceRecovery& rec);
+    SiameseResult is_ready();
+    /// Queues the solve; packets' lengths become exact after resolve().
+    SiameseResult decode(SiameseOriginalPacket** packetsOut, unsigned* countOut);
+    SiameseResult get(SiameseOriginalPacket& packet);
+    SiameseResult stats(uint64_t* out, unsigned count);
+    /// ARQ: siamese_decoder_ack (arq.cpp)
+    SiameseResult acknowledgement(uint8_t* buffer, unsigned byteLimit, unsigned& usedBytes);
+
+    bool disabled() const { return disabled_; }
+    /// Packet present in the window (received or recovered, length may be pending)
+    bool has(unsigned packetNum)
+    {
+        const unsigned e = column_to_element(packetNum);
+        return !disabled_ && e < count_ && slot(e).bytes > 0;
+    }
+    /// True while a queued solve has not been resolved by a completed flush.
+    bool has_pending() const { return pendingSolves_ > 0; }
+    /// Drop-in mode: queue D2H copies of the packets just recovered.
+    void download_recovered();
+
+private:
+    // ---- window (reference DecoderPacketWindow) ----
+    DecSlot& slot(unsigned e) { return subwindows_[e / kSubwindow]->slot[e % kSubwindow]; }
+    unsigned column_to_element(unsigned c) const { return column_sub(c, columnStart_); }
+    unsigned element_to_column(unsigned e) const { return column_add(e, columnStart_); }
+    unsigned next_lane_element(unsigned element, unsigned lane) const
+    {
+        unsigned e = element - (element % kLanes) + lane;
+        return e < element ? e + kLanes : e;
+    }
+    bool mark_got(unsigned column);
+    unsigned range_lost(unsigned start, unsigned end);
+    unsigned find_next_lost(unsigned start);
+    unsigned find_next_got(unsigned start);
+    void iterate_next_expected(unsigned start);
+    bool grow_window(unsigned end);
+
+    struct Sum
+    {
+        unsigned elementStart = 0, elementEnd = 0;
+        DevSum d;
+    };
+    Sum& sum(unsigned lane, unsigned s) { return lanes_[lane][s]; }
+    bool grow_sum(DevSum& s, unsigned bytes);
+    void materialize(DevSum& s);
+    DevSum& get_sum(unsigned lane, unsigned s, unsigned elementEnd);
+    bool start_sums(unsigned elementStart, unsigned bufferBytes);
+    void reset_sums(unsigned elementStart);
+    bool plug_sum_holes(unsigned elementStart);
+    void remove_elements();
+
+    // ---- recovery list (RecoveryPacketList) ----
+    void list_insert(RecPacket* r, bool outOfOrder);
+    void list_delete_before(unsigned element);
+    void free_packet(RecPacket* r);
+
+    // ---- checked region / matrix ----
+    void region_reset();
+    void matrix_reset();
+    bool check_recovery_possible();
+    SiameseResult decode_region();
+    bool generate_matrix();
+    void populate_columns(unsigned oldColumns, unsigned newColumns);
+    void populate_rows(unsigned oldRows, unsigned newRows);
+    void resume_ge(unsigned oldRows, unsigned rows);
+    bool gaussian_elimination();
+    bool pivoted_ge(unsigned pivot);
+    bool eliminate_row(const uint8_t* geRow, uint8_t* remRow, unsigned pivot, unsigned end,
+                       uint8_t valI);
+    uint8_t* mrow(unsigned r) { return mat_.data() + (size_t)r * matStride_; }
+    bool matrix_resize(unsigned rows, unsigned columns, bool initialize);
+
+    bool eliminate_original_data();
+    SiameseResult solve_and_substitute();
+
+    bool add_single(const RowMeta& m, const uint8_t* headBytes, unsigned payloadBytes,
+                    const void* hostData, uint64_t devData, Program* producer);
+    SiameseResult add_recovery_common(const RowMeta& m, int footerBytes, unsigned totalBytes,
+                                      const void* hostData, uint64_t devData,
+                                      const uint8_t* headBytes, Program* producer);
+
+    Engine* eng_;
+    Program prog_;
+    bool mirror_;
+    bool disabled_ = false;
+
+    // window
+    unsigned count_ = 0;
+    unsigned columnStart_ = 0;
+    unsigned nextExpected_ = 0;
+    std::vector<std::unique_ptr<DecSubwindow>> subwindows_;
+    Sum lanes_[kLanes][kSums];
+    unsigned sumColumnStart_ = 0;
+    unsigned sumColumnCount_ = 0;
+    std::vector<SiameseOriginalPacket> recovered_;
+    bool hasRecovered_ = false;
+    std::vector<unsigned> recoveredColumns_;
+
+    // recovery list
+    RecPacket* head_ = nullptr;
+    RecPacket* tail_ = nullptr;
+    unsigned listCount_ = 0;
+    RowMeta lastMeta_;
+    unsigned lastBytes_ = 0;
+
+    // checked region
+    struct
+    {
+        unsigned elementStart = 0;
+        RecPacket* first = nullptr;
+        RecPacket* last = nullptr;
+        unsigned nextCheckStart = 0;
+        unsigned recoveryCount = 0, lostCount = 0;
+        bool solveFailed = false;
+    } region_;
+
+    // recovery matrix
+    struct RowInfo
+    {
+        RecPacket* rec = nullptr;
+        bool used = false;
+        unsigned columnCount = 0;
+    };
+    struct ColInfo
+    {
+        DecSlot* original = nullptr;
+        unsigned column = 0;
+        uint8_t cx = 0;
+    };
+    std::vector<RowInfo> rows_;
+    std::vector<ColInfo> cols_;
+    unsigned prevNextCheckStart_ = 0;
+    std::vector<uint8_t> mat_;
+    unsigned matRows_ = 0, matCols_ = 0, matAllocRows_ = 0, matStride_ = 0;
+    std::vector<unsigned> pivots_;
+    unsigned geResume_ = 0;
+
+    unsigned latestColumn_ = 0;
+
+    // Recovered slots awaiting their exact length from the device
+    struct Fix
+    {
+        DecSlot* slot;
+        uint8_t* buf;          // buffer swapped into the slot by the solve
+        uint32_t resultWord;   // column index within the solve's result block
+        unsigned outIndex;     // index into recovered_
+        unsigned bound;        // upper bound on the length (row length)
+    };
+    void resolve_solve(const uint32_t* results, uint32_t base, unsigned m,
+                       const std::vector<Fix>& fixes, uint64_t serial);
+    std::vector<Fix> lastDecoded_;
+    std::shared_ptr<int> alive_;     // lets completion callbacks outlive us safely
+    uint64_t decodeSerial_ = 0;
+    unsigned pendingSolves_ = 0;
+
+    uint64_t stats_[SiameseDecoderStats_Count] = {};
+};
+
+} // namespace sgpu

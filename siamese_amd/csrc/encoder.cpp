@@ -1,0 +1,470 @@
+// encoder.cpp -- see encoder.h.  Line citations are to the reference
+// SiameseEncoder.cpp unless stated otherwise.
+#include "encoder.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace sgpu {
+
+EncoderCore::EncoderCore(Engine* eng, bool hostMirror) : eng_(eng), prog_(eng, 0), mirror_(hostMirror)
+{
+    // Window starts cleared (:63-82)
+    for (unsigned l = 0; l < kLanes; ++l)
+        for (unsigned s = 0; s < kSums; ++s)
+            lanes_[l].next[s] = l;
+}
+
+EncoderCore::~EncoderCore()
+{
+    for (auto& sw : subwindows_)
+        for (EncSlot& s : sw->slot)
+            eng_->release(s.buf);
+    for (Lane& l : lanes_)
+        for (DevSum& s : l.sum)
+            eng_->release(s.buf);
+    eng_->release(recovery_);
+}
+
+// ---------------------------------------------------------------------------
+// Window bookkeeping
+
+SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc)
+{
+    // :85-161
+    if (disabled_)
+        return Siamese_Disabled;
+    if (remaining_slots() == 0)
+        return Siamese_MaxPacketsReached;
+
+    const unsigned column = nextColumn_;
+    unsigned element = count_;
+    packet.PacketNum = column;
+
+    // Keep one lane-width of spare slots ahead of the last subwindow (:108-118)
+    if (element + kLanes >= subwindows_.size() * kSubwindow)
+        subwindows_.emplace_back(new EncSubwindow);
+
+    if (count_ > 0)
+        ++count_;
+    else {
+        element = column % kLanes;
+        start_window(column);
+    }
+
+    EncSlot& s = slot(element);
+    uint8_t hdr[kMaxLengthPrefix];
+    const unsigned h = write_length_prefix(packet.DataBytes, hdr);
+    eng_->release(s.buf);
+    s.buf = eng_->alloc(h + packet.DataBytes);
+    if (!s.buf) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    if (deviceSrc)
+        prog_.ingest_device(s.buf, deviceSrc, packet.DataBytes, hdr, h);
+    else
+        prog_.ingest_host(s.buf, packet.Data, packet.DataBytes, hdr, h);
+    if (mirror_) {
+        s.host.resize(h + packet.DataBytes);
+        std::memcpy(s.host.data(), hdr, h);
+        std::memcpy(s.host.data() + h, packet.Data, packet.DataBytes);
+    }
+    s.header = h;
+    s.bytes = h + packet.DataBytes;
+    s.column = column;
+    s.lastSend = (uint32_t)now_msec();
+
+    nextColumn_ = column_add(nextColumn_, 1);
+
+    Lane& lane = lanes_[column % kLanes];
+    if (lane.longest < s.bytes)
+        lane.longest = s.bytes;
+    if (longest_ < s.bytes)
+        longest_ = s.bytes;
+
+    stats_[SiameseEncoderStats_OriginalCount]++;
+    stats_[SiameseEncoderStats_OriginalBytes] += packet.DataBytes;
+    return Siamese_Success;
+}
+
+void EncoderCore::start_window(unsigned column)
+{
+    // :163-181 -- element % 8 == column % 8 is an invariant of the window
+    const unsigned element = column % kLanes;
+    columnStart_ = column - element;
+    sumStart_ = element;
+    sumEnd_ = element;
+    firstUnremoved_ = element;
+    count_ = element + 1;
+    longest_ = 0;
+    for (Lane& l : lanes_)
+        l.longest = 0;
+}
+
+void EncoderCore::remove_before(unsigned firstKeptColumn)
+{
+    // :183-216
+    if (disabled_)
+        return;
+    const unsigned element = column_to_element(firstKeptColumn);
+    if (element >= count_) {
+        if (!column_delta_negative(element))
+            count_ = 0; // everything acknowledged
+        return;
+    }
+    if (firstUnremoved_ < element)
+        firstUnremoved_ = element;
+}
+
+void EncoderCore::reset_sums(unsigned elementStart)
+{
+    // :218-237
+    for (unsigned l = 0; l < kLanes; ++l) {
+        const unsigned first = next_lane_element(elementStart, l);
+        for (unsigned s = 0; s < kSums; ++s) {
+            lanes_[l].next[s] = first;
+            lanes_[l].sum[s].bytes = 0;
+            lanes_[l].sum[s].devValid = 0;
+        }
+    }
+    sumStart_ = elementStart;
+    sumEnd_ = elementStart;
+    sumColumnStart_ = element_to_column(elementStart);
+    sumErased_ = 0;
+}
+
+void EncoderCore::remove_elements()
+{
+    // :239-357 -- drop whole subwindows before FirstUnremovedElement
+    const unsigned keptSub = firstUnremoved_ / kSubwindow;
+    const unsigned removed = keptSub * kSubwindow;
+
+    if (sumEnd_ > sumStart_) {
+        // Roll the running sums past the removal point before the data goes
+        for (unsigned l = 0; l < kLanes; ++l) {
+            for (unsigned s = 0; s < kSums; ++s) {
+                get_sum(l, s, removed);
+                lanes_[l].next[s] -= removed;
+            }
+        }
+        if (removed > sumStart_)
+            sumErased_ += removed - sumStart_;
+        sumEnd_ = sumEnd_ > removed ? sumEnd_ - removed : 0;
+        sumStart_ = sumStart_ > removed ? sumStart_ - removed : 0;
+    }
+
+    // Removed subwindows rotate to the back for reuse
+    std::rotate(subwindows_.begin(), subwindows_.begin() + keptSub, subwindows_.end());
+
+    count_ -= removed;
+    columnStart_ = element_to_column(removed);
+    firstUnremoved_ -= removed;
+
+    unsigned longest = 0;
+    unsigned laneLongest[kLanes] = {0};
+    for (unsigned e = firstUnremoved_; e < count_; ++e) {
+        const unsigned b = slot(e).bytes;
+        longest = std::max(longest, b);
+        laneLongest[e % kLanes] = std::max(laneLongest[e % kLanes], b);
+    }
+    longest_ = longest;
+    for (unsigned l = 0; l < kLanes; ++l)
+        lanes_[l].longest = laneLongest[l];
+
+    if (sumEnd_ <= sumStart_)
+        reset_sums(firstUnremoved_);
+}
+
+bool EncoderCore::grow_sum(DevSum& s, unsigned bytes)
+{
+    if (bytes <= s.bytes)
+        return true;
+    if (bytes > s.buf.cap) {
+        DevBuf nb = eng_->alloc(bytes);
+        if (!nb) {
+            disabled_ = true;
+            return false;
+        }
+        if (s.devValid) {
+            prog_.lc_begin(nb.addr(), s.devValid, 0);
+            prog_.lc_term(s.buf.addr(), s.devValid, 1);
+            prog_.lc_end();
+        }
+        eng_->release(s.buf);
+        s.buf = nb;
+    }
+    s.bytes = bytes;
+    return true;
+}
+
+DevSum& EncoderCore::get_sum(unsigned lane, unsigned sumIndex, unsigned elementEnd)
+{
+    // :359-418 -- lazily fold this lane's new originals into the running sum.
+    // Sum0 += X, Sum1 += CX*X, Sum2 += CX^2*X.
+    Lane& L = lanes_[lane];
+    DevSum& sum = L.sum[sumIndex];
+    unsigned element = L.next[sumIndex];
+    if (element >= elementEnd)
+        return sum;
+
+    unsigned newBytes = sum.bytes;
+    if (L.longest > 0)
+        newBytes = std::max(newBytes, L.longest);
+    struct T
+    {
+        uint64_t src;
+        unsigned len;
+        uint8_t c;
+    };
+    std::vector<T> terms;
+    terms.reserve((elementEnd - element) / kLanes + 1);
+    do {
+        const EncSlot& o = slot(element);
+        newBytes = std::max(newBytes, o.bytes);
+        uint8_t c = 1;
+        if (sumIndex > 0) {
+            c = column_value(o.column);
+            if (sumIndex == 2)
+                c = gf_sqr(c);
+        }
+        terms.push_back(T{o.buf.addr(), o.bytes, c});
+        element += kLanes;
+    } while (element < elementEnd);
+
+    if (!grow_sum(sum, newBytes))
+        return sum;
+    prog_.lc_begin(sum.buf.addr(), sum.bytes, sum.devValid);
+    for (const T& t : terms)
+        prog_.lc_term(t.src, t.len, t.c);
+    prog_.lc_end();
+    sum.devValid = sum.bytes;
+    L.next[sumIndex] = element;
+    return sum;
+}
+
+SiameseResult EncoderCore::get(SiameseOriginalPacket& packet)
+{
+    if (disabled_)
+        return Siamese_Disabled;
+    const unsigned element = column_to_element(packet.PacketNum);
+    if (element >= count_ || slot(element).bytes == 0) {
+        packet.Data = nullptr;
+        packet.DataBytes = 0;
+        return Siamese_NeedMoreData;
+    }
+    EncSlot& s = slot(element);
+    packet.PacketNum = s.column;
+    packet.Data = mirror_ ? s.host.data() + s.header : s.buf.ptr + s.header;
+    packet.DataBytes = s.bytes - s.header;
+    return Siamese_Success;
+}
+
+// ---------------------------------------------------------------------------
+// Encode
+
+bool EncoderCore::ensure_recovery(unsigned bytes)
+{
+    if (recovery_.cap >= bytes)
+        return true;
+    eng_->release(recovery_);
+    recovery_ = eng_->alloc(bytes + bytes / 8);
+    if (!recovery_) {
+        disabled_ = true;
+        return false;
+    }
+    return true;
+}
+
+void EncoderCore::finish_row(EncodeOut& out, const RowMeta& meta, unsigned payloadBytes)
+{
+    out.meta = meta;
+    out.footerBytes = write_footer(meta, out.footer);
+    prog_.literal(recovery_.addr(), payloadBytes, out.footer, out.footerBytes);
+    out.buf = recovery_;
+    out.bytes = payloadBytes + out.footerBytes;
+    stats_[SiameseEncoderStats_RecoveryCount]++;
+    stats_[SiameseEncoderStats_RecoveryBytes] += out.bytes;
+}
+
+SiameseResult EncoderCore::encode(EncodeOut& out)
+{
+    // :1146-1254
+    if (disabled_)
+        return Siamese_Disabled;
+    if (count_ == 0) {
+        out.bytes = 0;
+        return Siamese_NeedMoreData;
+    }
+    if (firstUnremoved_ >= kRemoveThreshold)
+        remove_elements();
+
+    const unsigned inFlight = unacked();
+    if (inFlight == 1)
+        return single_row(out);
+
+    const unsigned sumWidthBound = count_ - sumStart_ + sumErased_;
+    if (sumEnd_ <= sumStart_ || sumWidthBound >= kMaxPacketsInFlight) {
+        if (inFlight <= kCauchyThreshold)
+            return cauchy_row(out);
+        reset_sums(firstUnremoved_);
+    } else if (inFlight <= kSumResetThreshold || sumWidthBound <= kCauchyThreshold) {
+        sumEnd_ = sumStart_; // stop the running sums
+        return cauchy_row(out);
+    }
+
+    const unsigned row = nextRow_;
+    if (++nextRow_ >= kRowValuePeriod)
+        nextRow_ = 0;
+    return siamese_row(out, row);
+}
+
+SiameseResult EncoderCore::single_row(EncodeOut& out)
+{
+    // :1296-1329 -- the lone original itself, with a SumCount=1 footer
+    const EncSlot& o = slot(firstUnremoved_);
+    if (!ensure_recovery(o.bytes + kMaxFooterBytes))
+        return Siamese_Disabled;
+    prog_.lc_begin(recovery_.addr(), o.bytes, 0);
+    prog_.lc_term(o.buf.addr(), o.bytes, 1);
+    prog_.lc_end();
+    write_length_prefix(o.bytes - o.header, out.head);
+    RowMeta m;
+    m.sumCount = 1;
+    m.ldpcCount = 1;
+    m.columnStart = o.column;
+    m.row = 0;
+    finish_row(out, m, o.bytes);
+    return Siamese_Success;
+}
+
+SiameseResult EncoderCore::cauchy_row(EncodeOut& out)
+{
+    // :1334-1441 -- parity row (Row 0) or Cauchy row over the unacked window
+    const unsigned first = firstUnremoved_;
+    if (!ensure_recovery(longest_ + kMaxFooterBytes))
+        return Siamese_Disabled;
+    const unsigned inFlight = unacked();
+    RowMeta m;
+    m.sumCount = inFlight;
+    m.ldpcCount = inFlight;
+    m.columnStart = element_to_column(first);
+
+    struct T
+    {
+        uint64_t src;
+        unsigned len;
+        uint8_t c;
+    };
+    std::vector<T> terms;
+    terms.reserve(count_ - first);
+    unsigned used = 0;
+
+    const unsigned parityElement = column_to_element(nextParityColumn_);
+    if (parityElement <= first || column_delta_negative(parityElement)) {
+        nextParityColumn_ = column_add(m.columnStart, inFlight);
+        m.row = 0;
+        for (unsigned e = first; e < count_; ++e) {
+            const EncSlot& o = slot(e);
+            terms.push_back(T{o.buf.addr(), o.bytes, 1});
+            used = std::max(used, o.bytes);
+        }
+    } else {
+        const unsigned crow = nextCauchyRow_;
+        m.row = crow + 1;
+        if (++nextCauchyRow_ >= kCauchyMaxRows)
+            nextCauchyRow_ = 0;
+        unsigned ccol = m.columnStart % kCauchyMaxColumns;
+        for (unsigned e = first; e < count_; ++e) {
+            const EncSlot& o = slot(e);
+            terms.push_back(T{o.buf.addr(), o.bytes, cauchy_element(crow, ccol)});
+            used = std::max(used, o.bytes);
+            ccol = (ccol + 1) % kCauchyMaxColumns;
+        }
+    }
+
+    prog_.lc_begin(recovery_.addr(), used, 0);
+    for (const T& t : terms)
+        prog_.lc_term(t.src, t.len, t.c);
+    prog_.lc_end();
+    finish_row(out, m, used);
+    return Siamese_Success;
+}
+
+SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
+{
+    const unsigned recoveryBytes = longest_;
+    if (!ensure_recovery(recoveryBytes + kMaxFooterBytes))
+        return Siamese_Disabled;
+
+    struct T
+    {
+        uint64_t src;
+        unsigned len;
+        uint8_t acc;
+    };
+    std::vector<T> terms;
+    terms.reserve(64);
+
+    // Dense part (:1046-1098): opcode bits 0-2 feed the row, 3-5 the product
+    for (unsigned lane = 0; lane < kLanes; ++lane) {
+        const unsigned opcode = row_opcode(lane, row);
+        for (unsigned bit = 0; bit < 2 * kSums; ++bit) {
+            if (!(opcode & (1u << bit)))
+                continue;
+            DevSum& sum = get_sum(lane, bit % kSums, count_);
+            if (disabled_)
+                return Siamese_Disabled;
+            if (sum.bytes > 0)
+                terms.push_back(T{sum.buf.addr(), std::min(sum.bytes, recoveryBytes),
+                                  (uint8_t)(bit / kSums)});
+        }
+    }
+    sumEnd_ = count_;
+
+    // Sparse part (:1100-1144): ceil(n/16) PCG-chosen pairs
+    const unsigned start = firstUnremoved_;
+    const unsigned n = sumEnd_ - start;
+    Pcg32 prng;
+    prng.seed(row, n);
+    const unsigned pairs = (n + kPairRate - 1) / kPairRate;
+    for (unsigned i = 0; i < pairs; ++i) {
+        const EncSlot& a = slot(start + prng.next() % n);
+        const EncSlot& b = slot(start + prng.next() % n);
+        terms.push_back(T{a.buf.addr(), a.bytes, 0});
+        terms.push_back(T{b.buf.addr(), b.bytes, 1});
+    }
+
+    // Recovery = row sums ^ RX * product  (:1232-1233), one fused device op
+    prog_.lc_begin(recovery_.addr(), recoveryBytes, 0, row_value(row));
+    for (const T& t : terms)
+        prog_.lc_term(t.src, t.len, 1, t.acc);
+    prog_.lc_end();
+
+    RowMeta m;
+    m.sumCount = sumEnd_ - sumStart_ + sumErased_;
+    m.ldpcCount = unacked();
+    m.columnStart = sumColumnStart_;
+    m.row = row;
+    finish_row(out, m, recoveryBytes);
+    return Siamese_Success;
+}
+
+SiameseResult EncoderCore::stats(uint64_t* out, unsigned count)
+{
+    if (count > SiameseEncoderStats_Count)
+        count = SiameseEncoderStats_Count;
+    uint64_t mem = recovery_.cap;
+    for (auto& sw : subwindows_)
+        for (EncSlot& s : sw->slot)
+            mem += s.buf.cap;
+    for (Lane& l : lanes_)
+        for (DevSum& s : l.sum)
+            mem += s.buf.cap;
+    stats_[SiameseEncoderStats_MemoryUsed] = mem;
+    for (unsigned i = 0; i < count; ++i)
+        out[i] = stats_[i];
+    return Siamese_Success;
+}
+
+} // namespace sgpu

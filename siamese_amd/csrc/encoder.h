@@ -1,0 +1,136 @@
+// encoder.h -- host control plane of the encoder.
+//
+// Decision logic (window bookkeeping, path selection, row numbering, footer)
+// follows the reference encoder exactly so the emitted bit stream is
+// identical (reference SiameseEncoder.h:104-421, SiameseEncoder.cpp:56-1441).
+// Every symbol-sized operation is emitted as a device op into this
+// instance's Program; the symbols themselves live in HBM.
+#pragma once
+
+#include "arq.h"
+#include "codedef.h"
+#include "engine.h"
+#include "../../include/siamese.h"
+
+#include <memory>
+#include <vector>
+
+namespace sgpu {
+
+struct EncSlot
+{
+    DevBuf buf;                 // [length prefix || payload] in HBM
+    unsigned bytes = 0;         // prefix + payload
+    unsigned column = 0;
+    unsigned header = 0;        // length-prefix bytes
+    uint32_t lastSend = 0;      // msec timestamp of the last (re)send (ARQ)
+    std::vector<uint8_t> host;  // host mirror (drop-in mode only)
+};
+
+struct EncSubwindow
+{
+    EncSlot slot[kSubwindow];
+};
+
+/// Running sum of one (lane, sum-index) in HBM.
+struct DevSum
+{
+    DevBuf buf;
+    unsigned bytes = 0;     // logical length (reference Buffer.Bytes)
+    unsigned devValid = 0;  // bytes actually materialised on the device
+};
+
+/// Result of an encode in device terms.
+struct EncodeOut
+{
+    DevBuf buf;             // recovery packet (valid until the next encode)
+    unsigned bytes = 0;     // payload + footer
+    uint8_t footer[kMaxFooterBytes] = {};
+    unsigned footerBytes = 0;
+    uint8_t head[kMaxLengthPrefix] = {}; // first bytes (single-packet rows only)
+    RowMeta meta;
+};
+
+class EncoderCore
+{
+public:
+    EncoderCore(Engine* eng, bool hostMirror);
+    ~EncoderCore();
+
+    Program& program() { return prog_; }
+
+    unsigned remaining_slots() const { return kMaxPacketsInFlight - count_; }
+
+    /// siamese_encoder_add.  Source is host memory or (device != 0) HBM.
+    SiameseResult add(SiameseOriginalPacket& packet, uint64_t deviceSrc = 0);
+    void remove_before(unsigned firstKeptColumn);
+    SiameseResult get(SiameseOriginalPacket& packet);
+    /// Generate the next recovery packet (device ops queued, not flushed).
+    SiameseResult encode(EncodeOut& out);
+    SiameseResult stats(uint64_t* out, unsigned count);
+    /// ARQ: siamese_encoder_ack / siamese_encoder_retransmit (arq.cpp)
+    SiameseResult acknowledge(const uint8_t* data, unsigned bytes, unsigned& nextExpectedOut);
+    SiameseResult retransmit(SiameseOriginalPacket& out);
+
+    bool disabled() const { return disabled_; }
+    uint64_t stat(unsigned i) const { return stats_[i]; }
+
+private:
+    // window (reference EncoderPacketWindow)
+    EncSlot& slot(unsigned element)
+    {
+        return subwindows_[element / kSubwindow]->slot[element % kSubwindow];
+    }
+    unsigned column_to_element(unsigned c) const { return column_sub(c, columnStart_); }
+    unsigned element_to_column(unsigned e) const { return column_add(e, columnStart_); }
+    unsigned next_lane_element(unsigned element, unsigned lane) const
+    {
+        unsigned e = element - (element % kLanes) + lane;
+        return e < element ? e + kLanes : e;
+    }
+    unsigned unacked() const { return count_ - firstUnremoved_; }
+    void start_window(unsigned column);
+    void reset_sums(unsigned elementStart);
+    void remove_elements();
+    /// Lazily accumulate lane sums up to elementEnd; returns the sum.
+    DevSum& get_sum(unsigned lane, unsigned sumIndex, unsigned elementEnd);
+    bool grow_sum(DevSum& s, unsigned bytes);
+
+    SiameseResult single_row(EncodeOut& out);
+    SiameseResult cauchy_row(EncodeOut& out);
+    SiameseResult siamese_row(EncodeOut& out, unsigned row);
+    bool ensure_recovery(unsigned bytes);
+    void finish_row(EncodeOut& out, const RowMeta& meta, unsigned payloadBytes);
+    void update_rto();
+    SiameseResult retransmit_slot(EncSlot& s, SiameseOriginalPacket& out);
+    AckState ack_;
+
+    Engine* eng_;
+    Program prog_;
+    bool mirror_;
+    bool disabled_ = false;
+
+    std::vector<std::unique_ptr<EncSubwindow>> subwindows_;
+    unsigned nextColumn_ = 0;
+    unsigned count_ = 0;
+    unsigned columnStart_ = 0;
+    unsigned longest_ = 0;
+    unsigned firstUnremoved_ = 0;
+    unsigned sumStart_ = 0, sumEnd_ = 0, sumColumnStart_ = 0, sumErased_ = 0;
+
+    struct Lane
+    {
+        unsigned next[kSums];
+        DevSum sum[kSums];
+        unsigned longest = 0;
+    } lanes_[kLanes];
+
+    DevBuf recovery_;          // reused recovery packet buffer
+    unsigned nextRow_ = 0;
+    unsigned nextParityColumn_ = 0;
+    unsigned nextCauchyRow_ = 0;
+
+    uint64_t stats_[SiameseEncoderStats_Count] = {};
+};
+
+} // namespace sgpu

@@ -1,0 +1,39 @@
+// gf.h -- host-side GF(2^8) arithmetic for the control plane.
+//
+// Field: GF(2^8) modulo x^8+x^6+x^3+x^2+1 (0x14D), the polynomial the
+// reference selects (reference gf256.cpp:357-372, index 3 of its table).
+// The host only touches COEFFICIENTS (recovery-matrix generation and the
+// Gaussian elimination on <=255x255 bytes); every symbol-sized operation is
+// executed on the MI355X by the kernels in kernels.hip.
+#pragma once
+
+#include <cstdint>
+
+namespace sgpu {
+
+struct GfTables
+{
+    uint8_t exp[512 + 2];   // exp[i] = g^(i mod 255), doubled to skip a modulo
+    uint16_t log[256];      // log[0] unused
+    uint8_t mul[256][256];  // mul[y][x] = x*y
+    uint8_t inv[256];       // inv[0] = 0
+    uint8_t sqr[256];
+    // Nibble tables for the AVX2 row kernel: lo[y][n] = y*n, hi[y][n] = y*(n<<4)
+    alignas(32) uint8_t nib_lo[256][16];
+    alignas(32) uint8_t nib_hi[256][16];
+};
+
+extern GfTables g_gf;
+
+/// Build the tables; idempotent.  Returns false if the self-check fails.
+bool gf_init();
+
+inline uint8_t gf_mul(uint8_t x, uint8_t y) { return g_gf.mul[y][x]; }
+inline uint8_t gf_inv(uint8_t x) { return g_gf.inv[x]; }
+inline uint8_t gf_sqr(uint8_t x) { return g_gf.sqr[x]; }
+inline uint8_t gf_div(uint8_t x, uint8_t y) { return y ? g_gf.mul[g_gf.inv[y]][x] : 0; }
+
+/// dst[i] ^= y * src[i] for i < n (host rows of the coefficient matrix).
+void gf_muladd_row(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n);
+
+} // namespace sgpu

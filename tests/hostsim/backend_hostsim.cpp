@@ -1,0 +1,297 @@
+// tests/hostsim/backend_hostsim.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// A CPU simulation of the backend.h contract, used solely by the CPU test
+// suite to exercise the host control plane (encoder/decoder/engine) on a
+// machine without a GPU.  It is linked into tests/hostsim/libsiamese_hostsim.so
+// and NEVER into the product library siamese_amd/libsiamese_amd.so, whose
+// only backend is backend_hip.hip.  The kernels' byte semantics are restated
+// here one lane-tile at a time (including the v_perm_b32 GF(256) multiply),
+// so a wrong op stream or table fails the same parity tests the GPU runs.
+#include "../../siamese_amd/csrc/backend.h"
+#include "../../siamese_amd/csrc/gf.h"
+
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace sgpu {
+
+namespace {
+
+uint32_t g_perm[256][8];
+uint8_t g_inv[256];
+
+// v_perm_b32 byte select for selector values 0..7 (and 12 -> 0)
+uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel)
+{
+    const uint64_t data = ((uint64_t)s0 << 32) | s1;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t s = (sel >> (8 * i)) & 0xff;
+        uint32_t b = 0;
+        if (s < 8)
+            b = (uint32_t)(data >> (8 * s)) & 0xff;
+        else if (s == 12)
+            b = 0;
+        else if (s >= 13)
+            b = 0xff;
+        r |= b << (8 * i);
+    }
+    return r;
+}
+
+uint32_t mul_dword(uint32_t x, uint32_t y)
+{
+    const uint32_t* t = g_perm[y];
+    return perm(t[1], t[0], x & 0x07070707u) ^ perm(t[3], t[2], (x >> 3) & 0x07070707u) ^
+           perm(0u, t[4], (x >> 6) & 0x03030303u);
+}
+
+void mul_bytes(uint8_t* v, unsigned n, uint8_t y)
+{
+    // operate dword-wise like the kernel
+    for (unsigned i = 0; i < n; i += 4) {
+        uint32_t w = 0;
+        const unsigned k = n - i < 4 ? n - i : 4;
+        std::memcpy(&w, v + i, k);
+        w = mul_dword(w, y);
+        std::memcpy(v + i, &w, k);
+    }
+}
+
+int parse_prefix(const uint8_t* b, unsigned avail, unsigned* len)
+{
+    if (avail < 1)
+        return -1;
+    const unsigned top = b[0] >> 6;
+    if (top <= 1) {
+        *len = b[0];
+        return 1;
+    }
+    if (top == 2) {
+        if (avail < 2)
+            return -1;
+        *len = (((unsigned)b[0] << 8) | b[1]) & 0x3fff;
+        return 2;
+    }
+    if ((b[0] & 0xE0) == 0xC0) {
+        if (avail < 3)
+            return -1;
+        *len = (((unsigned)b[0] << 16) | ((unsigned)b[1] << 8) | b[2]) & 0x1fffff;
+        return 3;
+    }
+    if (avail < 4)
+        return -1;
+    *len = (((unsigned)b[0] << 24) | ((unsigned)b[1] << 16) | ((unsigned)b[2] << 8) | b[3]) & 0x1fffffff;
+    return 4;
+}
+
+inline uint8_t* P(uint64_t a) { return reinterpret_cast<uint8_t*>(a); }
+
+void exec_tile(const GfOp* ops, const GfTerm* terms, const ExecItem& it)
+{
+    for (uint32_t oi = 0; oi < it.opCount; ++oi) {
+        const GfOp& op = ops[it.opBegin + oi];
+        const uint32_t t0 = it.tileBase, t1 = it.tileBase + kTileBytes;
+        if (op.kind == OP_LITERAL) {
+            for (uint32_t k = 0; k < op.valid; ++k) {
+                const uint32_t b = op.n + k;
+                if (b >= t0 && b < t1)
+                    P(op.dst)[b] = op.lit[k];
+            }
+            continue;
+        }
+        const uint32_t end = op.n < t1 ? op.n : t1;
+        if (t0 >= end)
+            continue;
+        const unsigned w = end - t0;
+        uint8_t acc0[kTileBytes], acc1[kTileBytes], tmp[kTileBytes];
+        std::memset(acc0, 0, w);
+        std::memset(acc1, 0, w);
+        for (uint32_t k = 0; k < op.termCount; ++k) {
+            const GfTerm& tm = terms[op.termBegin + k];
+            if (t0 >= tm.len)
+                continue;
+            const unsigned n = (tm.len < end ? tm.len : end) - t0;
+            std::memcpy(tmp, P(tm.src) + t0, n);
+            if (tm.coeff != 1)
+                mul_bytes(tmp, n, tm.coeff);
+            uint8_t* acc = tm.acc ? acc1 : acc0;
+            for (unsigned i = 0; i < n; ++i)
+                acc[i] ^= tmp[i];
+        }
+        if (op.mix > 1)
+            mul_bytes(acc1, w, (uint8_t)op.mix);
+        uint8_t* dst = P(op.dst) + t0;
+        for (unsigned i = 0; i < w; ++i) {
+            const uint8_t prior = (t0 + i < op.valid) ? dst[i] : 0;
+            dst[i] = prior ^ acc0[i] ^ acc1[i];
+        }
+    }
+}
+
+} // namespace
+
+bool be_init(int, const char** err)
+{
+    if (!gf_init()) {
+        *err = "gf_init failed";
+        return false;
+    }
+    for (unsigned y = 0; y < 256; ++y) {
+        uint8_t ta[8], tb[8], tc[4];
+        for (unsigned k = 0; k < 8; ++k) {
+            ta[k] = gf_mul((uint8_t)k, (uint8_t)y);
+            tb[k] = gf_mul((uint8_t)(k << 3), (uint8_t)y);
+        }
+        for (unsigned k = 0; k < 4; ++k)
+            tc[k] = gf_mul((uint8_t)(k << 6), (uint8_t)y);
+        std::memset(g_perm[y], 0, sizeof(g_perm[y]));
+        std::memcpy(&g_perm[y][0], ta, 8);
+        std::memcpy(&g_perm[y][2], tb, 8);
+        std::memcpy(&g_perm[y][4], tc, 4);
+    }
+    std::memcpy(g_inv, g_gf.inv, 256);
+    return true;
+}
+
+const char* be_name() { return "hostsim (test only)"; }
+
+void* be_dev_alloc(size_t bytes)
+{
+    void* p = nullptr;
+    if (posix_memalign(&p, 256, bytes) != 0)
+        return nullptr;
+    std::memset(p, 0xA5, bytes); // garbage, like fresh device memory
+    return p;
+}
+void be_dev_free(void* p) { std::free(p); }
+void* be_host_alloc(size_t bytes) { return be_dev_alloc(bytes); }
+void be_host_free(void* p) { std::free(p); }
+void be_h2d(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
+void be_d2h(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
+void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
+
+void be_launch_ingest(const IngestDesc* descs, const IngestItem* items, uint32_t count)
+{
+    for (uint32_t i = 0; i < count; ++i) {
+        const IngestDesc& d = descs[items[i].desc];
+        const uint32_t total = d.hdrLen + d.bytes;
+        const uint32_t t0 = items[i].tileBase;
+        const uint32_t t1 = t0 + kTileBytes < total ? t0 + kTileBytes : total;
+        for (uint32_t k = t0; k < t1; ++k)
+            P(d.dst)[k] = k < d.hdrLen ? d.hdr[k] : P(d.src)[k - d.hdrLen];
+    }
+}
+
+void be_launch_exec(const GfOp* ops, const GfTerm* terms, const ExecItem* items, uint32_t count)
+{
+    for (uint32_t i = 0; i < count; ++i)
+        exec_tile(ops, terms, items[i]);
+}
+
+void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
+                            uint32_t* results, uint32_t count)
+{
+    for (uint32_t s = 0; s < count; ++s) {
+        const SolveDesc& sd = solves[s];
+        const uint32_t m = sd.m;
+        const SolveRow* R = rows + sd.rowBegin;
+        const uint8_t* C = coef + sd.coefOffset;
+        uint32_t* out = results + sd.result;
+        std::vector<uint8_t> pre((size_t)m * 4, 0);
+        for (uint32_t j = 0; j < m; ++j)
+            for (uint32_t b = 0; b < 4 && b < R[j].initBytes; ++b)
+                pre[j * 4 + b] = P(R[j].buf)[b];
+        for (uint32_t i = 0; i + 1 < m; ++i)
+            for (uint32_t j = i + 1; j < m; ++j) {
+                const uint8_t y = C[(size_t)j * m + i];
+                if (!y)
+                    continue;
+                for (uint32_t b = 0; b < 4 && b < R[i].lowerLen; ++b)
+                    pre[j * 4 + b] ^= gf_mul(pre[i * 4 + b], y);
+            }
+        uint32_t ok = 0;
+        for (int i = (int)m - 1; i >= 0; --i) {
+            const uint32_t fb = R[i].finalBytes;
+            const uint32_t lc = fb < 32 ? fb : 32;
+            const uint8_t inv = g_inv[C[(size_t)i * m + i]];
+            uint8_t x[4] = {0, 0, 0, 0};
+            for (uint32_t b = 0; b < 4 && b < lc; ++b)
+                x[b] = gf_mul(pre[i * 4 + b], inv);
+            unsigned len = 0;
+            const int h = parse_prefix(x, lc, &len);
+            if (h < 1 || len == 0 || (uint32_t)h + len > fb)
+                break;
+            out[1 + i] = ((uint32_t)h << 29) | len;
+            const uint32_t bb = (uint32_t)h + len;
+            ++ok;
+            for (uint32_t j = 0; j < (uint32_t)i; ++j) {
+                const uint8_t c = C[(size_t)j * m + i];
+                if (!c)
+                    continue;
+                const uint32_t ab = bb < R[j].finalBytes ? bb : R[j].finalBytes;
+                for (uint32_t b = 0; b < 4 && b < ab; ++b)
+                    pre[j * 4 + b] ^= gf_mul(x[b], c);
+            }
+        }
+        out[0] = ok;
+    }
+}
+
+void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
+                          const uint32_t* results, const SolveItem* items, uint32_t count)
+{
+    for (uint32_t it = 0; it < count; ++it) {
+        const SolveDesc& sd = solves[items[it].solve];
+        const uint32_t m = sd.m;
+        const SolveRow* R = rows + sd.rowBegin;
+        const uint8_t* C = coef + sd.coefOffset;
+        const uint32_t* res = results + sd.result;
+        const uint32_t t0 = items[it].tileBase, t1 = t0 + kTileBytes;
+        auto clip = [&](uint32_t v) { return v < t1 ? v : t1; };
+        for (uint32_t j = 0; j < m; ++j)
+            for (uint32_t b = (R[j].initBytes > t0 ? R[j].initBytes : t0); b < clip(R[j].finalBytes); ++b)
+                P(R[j].buf)[b] = 0;
+        std::vector<uint8_t> tmp(kTileBytes);
+        for (uint32_t i = 0; i + 1 < m; ++i) {
+            const uint32_t L = clip(R[i].lowerLen);
+            if (t0 >= L)
+                continue;
+            for (uint32_t j = i + 1; j < m; ++j) {
+                const uint8_t y = C[(size_t)j * m + i];
+                if (!y)
+                    continue;
+                for (uint32_t b = t0; b < L; ++b)
+                    P(R[j].buf)[b] ^= gf_mul(P(R[i].buf)[b], y);
+            }
+        }
+        const uint32_t ok = res[0];
+        for (int i = (int)m - 1; i >= 0; --i) {
+            if ((uint32_t)(m - 1 - i) >= ok)
+                break;
+            const uint32_t w = res[1 + i];
+            const uint32_t bb = (w >> 29) + (w & kSolveLengthMask);
+            const uint32_t fb = clip(R[i].finalBytes);
+            const uint8_t inv = g_inv[C[(size_t)i * m + i]];
+            for (uint32_t b = t0; b < fb; ++b)
+                P(R[i].buf)[b] = b < bb ? gf_mul(P(R[i].buf)[b], inv) : 0;
+            for (uint32_t j = 0; j < (uint32_t)i; ++j) {
+                const uint8_t c = C[(size_t)j * m + i];
+                if (!c)
+                    continue;
+                const uint32_t ab = clip(bb < R[j].finalBytes ? bb : R[j].finalBytes);
+                for (uint32_t b = t0; b < ab; ++b)
+                    P(R[j].buf)[b] ^= gf_mul(P(R[i].buf)[b], c);
+            }
+        }
+    }
+}
+
+bool be_sync() { return true; }
+void be_timing_enable(bool) {}
+void be_timing_reset() {}
+double be_timing_exec_ms() { return 0; }
+double be_timing_total_ms() { return 0; }
+
+} // namespace sgpu

@@ -1,0 +1,117 @@
+"""ctypes front-end of harness/libscenario.so (the loopback workload driver).
+
+Test infrastructure: used by tests/, bench.py (cpu_baseline leg and the GPU
+leg) and __graft_entry__.smoke().  It drives any siamese.h implementation --
+the upstream reference compiled into oracle/_ref/, the drop-in API of
+siamese_amd/libsiamese_amd.so, or the test-only host simulation -- through
+the same deterministic call sequence and returns per-stream event digests.
+"""
+import ctypes
+import os
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCENARIO_LIB = os.path.join(ROOT, "harness", "libscenario.so")
+REF_LIB = os.path.join(ROOT, "oracle", "_ref", "libsiamese_ref.so")
+AMD_LIB = os.path.join(ROOT, "siamese_amd", "libsiamese_amd.so")
+SIM_LIB = os.path.join(ROOT, "tests", "hostsim", "libsiamese_hostsim.so")
+
+_FIELDS = ("block_mode streams first_stream originals payload_bytes loss_pct "
+           "recovery_loss_pct recovery_interval recovery_phase ack_policy ack_lag "
+           "tail_limit seed").split()
+
+
+class Config(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in _FIELDS]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n in _FIELDS}
+
+
+class StreamResult(ctypes.Structure):
+    _fields_ = ([("digest", ctypes.c_uint64), ("recovery_bytes", ctypes.c_uint64),
+                 ("payload_bytes", ctypes.c_uint64)] +
+                [(n, ctypes.c_uint32) for n in
+                 "encodes recovery_lost originals_lost recovered decode_calls "
+                 "decode_fail delivered status".split()])
+
+
+def make_config(**kw):
+    base = dict(block_mode=0, streams=1, first_stream=0, originals=200, payload_bytes=1400,
+                loss_pct=10, recovery_loss_pct=5, recovery_interval=8, recovery_phase=0,
+                ack_policy=0, ack_lag=40, tail_limit=600, seed=1013)
+    base.update(kw)
+    return Config(**base)
+
+
+# Workloads of BASELINE.json / SURVEY.md section 8(d).  `streams` is the
+# full size; tests scale it down with replace().
+CONFIGS = {
+    # C1: reference StreamingTest semantics, 200 x 1400 B, 10% loss
+    "C1": make_config(originals=200, loss_pct=10, recovery_loss_pct=5, recovery_interval=8,
+                      ack_policy=2, ack_lag=40),
+    # C1 with the reference's variable packet sizes 2..1199 B
+    "C1var": make_config(originals=300, payload_bytes=0, loss_pct=10, recovery_loss_pct=5,
+                         recovery_interval=8, ack_policy=2, ack_lag=40, streams=4),
+    # C2: 1024 streams x 256 x 1400 B, 10% loss, 1-in-8, immediate ack (Cauchy path)
+    "C2": make_config(streams=1024, originals=256, loss_pct=10, recovery_loss_pct=10,
+                      recovery_interval=8, ack_policy=1),
+    # C3: single stream 8192 x 1400 B, 20% loss, 1-in-3, no acks (Siamese path)
+    "C3": make_config(originals=8192, loss_pct=20, recovery_loss_pct=20, recovery_interval=3),
+    # C4: 8192 streams x 256 x 1400 B, 20% loss, block mode
+    "C4": make_config(block_mode=1, streams=8192, originals=256, loss_pct=20,
+                      recovery_loss_pct=20),
+    # C5: 16000 x 65536 B, 5% loss, 1-in-10, no acks
+    "C5": make_config(originals=16000, payload_bytes=65536, loss_pct=5, recovery_loss_pct=5,
+                      recovery_interval=10),
+}
+
+
+def replace(cfg, **kw):
+    d = cfg.as_dict()
+    d.update(kw)
+    return Config(**d)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(SCENARIO_LIB)
+        _lib.scenario_run_capi.restype = ctypes.c_int
+        _lib.scenario_run_capi.argtypes = [ctypes.c_char_p, ctypes.POINTER(Config),
+                                           ctypes.POINTER(StreamResult), ctypes.c_uint,
+                                           ctypes.POINTER(ctypes.c_double), ctypes.c_char_p]
+    return _lib
+
+
+def run_capi(library, cfg, threads=1, event_log=None):
+    """Run `cfg` through the siamese.h API of `library`.
+
+    Returns (results array, codec seconds, wall seconds)."""
+    res = (StreamResult * cfg.streams)()
+    sec = ctypes.c_double()
+    t0 = time.time()
+    rc = lib().scenario_run_capi(library.encode(), ctypes.byref(cfg), res, threads,
+                                 ctypes.byref(sec), event_log.encode() if event_log else None)
+    wall = time.time() - t0
+    if rc != 0:
+        raise RuntimeError("scenario_run_capi(%s) failed rc=%d" % (library, rc))
+    return res, sec.value, wall
+
+
+def digests(results):
+    return [int(r.digest) for r in results]
+
+
+def summary(results):
+    keys = ("encodes recovery_lost originals_lost recovered decode_calls decode_fail "
+            "delivered").split()
+    out = {k: int(sum(getattr(r, k) for r in results)) for k in keys}
+    out["payload_bytes"] = int(sum(r.payload_bytes for r in results))
+    out["recovery_bytes"] = int(sum(r.recovery_bytes for r in results))
+    st = [int(r.status) for r in results]
+    out["status"] = {str(s): st.count(s) for s in sorted(set(st))}
+    return out
