@@ -117,6 +117,7 @@ struct ScenarioConfig
     uint32_t ack_lag;           ///< lag for policy 2
     uint32_t tail_limit;        ///< extra encodes after the last original / block limit
     uint32_t seed;              ///< loss channel seed (1013 = reference kSeed)
+    uint32_t hash_data;         ///< 1: digests cover packet bytes; 0: lengths only
 };
 
 /// Per-stream outcome (ctypes-visible).
@@ -153,30 +154,42 @@ inline uint64_t ev(uint64_t type, uint64_t result, uint64_t a = 0, uint64_t b = 
 /*
     Codec concept (duck-typed) used by Stream<Codec>:
 
-      int  enc_add(const uint8_t* data, unsigned bytes, unsigned* packetNum);
-      int  encode(Rec* rec);                 // Rec: driver-defined handle w/ .bytes
-      int  dec_add_original(unsigned num, const uint8_t* data, unsigned bytes);
+      bool needs_host_payload();              // false: payload already on device
+      int  enc_add(unsigned id, const uint8_t* host, unsigned bytes, unsigned* packetNum);
+      int  encode(Rec* rec);                  // Rec: driver-defined handle w/ .bytes
+      int  dec_add_original(unsigned id, unsigned num, const uint8_t* host, unsigned bytes);
       int  dec_add_recovery(const Rec& rec);
       int  is_ready();
-      int  decode(std::vector<Pkt>* out);     // Pkt: driver-defined w/ .num .bytes
+      int  decode(std::vector<Pkt>* out);     // Pkt: driver-defined w/ .num
       int  dec_get(unsigned num, Pkt* out);
       int  enc_remove_before(unsigned num);
-      // data tokens (a hash now, or a deferred slot resolved after a flush)
+      // Digest tokens: hash of (length || bytes) when cfg->hash_data, else the
+      // length.  pkt_token also checks the bytes against the payload `id`.
       uint64_t rec_token(const Rec& rec);
-      uint64_t pkt_token(const Pkt& p, unsigned expectedId, bool* ok); // verifies payload
-      bool wants_yield_after_decode();
+      uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok);
+      bool wants_yield_after_decode();        // batch: lengths known after a flush
 */
+
+inline uint64_t data_token(bool hashData, const uint8_t* p, unsigned bytes)
+{
+    if (!hashData)
+        return bytes;
+    Fnv f;
+    f.u64(bytes);
+    f.bytes(p, bytes);
+    return f.h;
+}
 
 template <class Codec, class Rec, class Pkt>
 struct Stream
 {
-    enum Phase { ADD, ENCODE, DECODE_LOOP, ACK, TAIL, DONE };
+    enum Phase { ADD, ENCODE, DECODE_LOOP, DECODED, ACK, TAIL, DONE };
 
     const ScenarioConfig* cfg = nullptr;
     Codec* codec = nullptr;
     StreamResult* res = nullptr;
     unsigned global = 0;          // global stream index
-    std::vector<uint64_t> log;    // event log (tokens may be filled in later)
+    std::vector<uint64_t> log;    // event log
 
     Pcg loss;
     Phase phase = ADD;
@@ -186,6 +199,7 @@ struct Stream
     unsigned lastNum = 0;         // PacketNum of the most recent add
     bool tailMode = false;        // all originals added; only encodes remain
     std::vector<uint8_t> buf;
+    std::vector<Pkt> decoded;     // output of the last successful decode
     bool dataOk = true;           // every returned packet matched its payload
 
     void init(const ScenarioConfig* c, Codec* k, StreamResult* r, unsigned globalIndex)
@@ -201,6 +215,10 @@ struct Stream
     }
 
     unsigned packet_id(unsigned index) const { return global * cfg->originals + index; }
+    unsigned packet_bytes(unsigned id) const
+    {
+        return cfg->payload_bytes ? cfg->payload_bytes : variable_bytes(id);
+    }
 
     bool done() const { return phase == DONE; }
 
@@ -220,7 +238,7 @@ struct Stream
                 log.push_back(ev(EV_GET, r, nextExpected));
                 return r == 2; // NeedMoreData is the normal stop
             }
-            log.push_back(ev(EV_GET, 0, nextExpected, p.bytes));
+            log.push_back(ev(EV_GET, 0, nextExpected));
             log.push_back(codec->pkt_token(p, packet_id(nextExpected), &dataOk));
             ++nextExpected;
             ++res->delivered;
@@ -228,18 +246,17 @@ struct Stream
         return true;
     }
 
-    // One encode + channel + add_recovery.  Returns false when the stream
-    // should stop (error) -- the caller then inspects res->status.
-    bool encode_once()
+    // One encode + channel + add_recovery.
+    void encode_once()
     {
         Rec rec;
         const int r = codec->encode(&rec);
-        log.push_back(ev(EV_ENCODE, r, r == 0 ? rec.bytes : 0));
+        log.push_back(ev(EV_ENCODE, r));
         if (r == 2)
-            return true; // nothing to encode yet
+            return; // nothing to encode yet
         if (r != 0) {
             fail(2);
-            return false;
+            return;
         }
         log.push_back(codec->rec_token(rec));
         ++res->encodes;
@@ -247,16 +264,15 @@ struct Stream
         const bool lost = (loss.next() % 100) < cfg->recovery_loss_pct;
         if (lost) {
             ++res->recovery_lost;
-            return true;
+            return;
         }
         const int a = codec->dec_add_recovery(rec);
         log.push_back(ev(EV_DEC_ADD_REC, a));
         if (a != 0) {
             fail(2);
-            return false;
+            return;
         }
         phase = DECODE_LOOP;
-        return true;
     }
 
     // Advance by one unit of work.  Returns true if the driver should stop
@@ -271,10 +287,14 @@ struct Stream
                 return false;
             }
             const unsigned id = packet_id(i);
-            const unsigned bytes = cfg->payload_bytes ? cfg->payload_bytes : variable_bytes(id);
-            fill_payload(id, buf.data(), bytes);
+            const unsigned bytes = packet_bytes(id);
+            const uint8_t* host = nullptr;
+            if (codec->needs_host_payload()) {
+                fill_payload(id, buf.data(), bytes);
+                host = buf.data();
+            }
             unsigned num = 0;
-            const int r = codec->enc_add(buf.data(), bytes, &num);
+            const int r = codec->enc_add(id, host, bytes, &num);
             log.push_back(ev(EV_ENC_ADD, r, num));
             if (r != 0) {
                 fail(2);
@@ -286,7 +306,7 @@ struct Stream
             if (lost) {
                 ++res->originals_lost;
             } else {
-                const int a = codec->dec_add_original(num, buf.data(), bytes);
+                const int a = codec->dec_add_original(id, num, host, bytes);
                 log.push_back(ev(EV_DEC_ADD_ORIG, a, num));
                 if (a != 0 && a != 4) {
                     fail(2);
@@ -308,7 +328,7 @@ struct Stream
         case ENCODE:
             phase = ACK;
             encode_once();
-            return false;
+            return codec->wants_yield_after_encode();
         case DECODE_LOOP: {
             const int ready = codec->is_ready();
             log.push_back(ev(EV_IS_READY, ready));
@@ -316,10 +336,10 @@ struct Stream
                 phase = tailMode ? TAIL : ACK;
                 return false;
             }
-            std::vector<Pkt> pkts;
+            decoded.clear();
             ++res->decode_calls;
-            const int r = codec->decode(&pkts);
-            log.push_back(ev(EV_DECODE, r, (uint64_t)pkts.size()));
+            const int r = codec->decode(&decoded);
+            log.push_back(ev(EV_DECODE, r, (uint64_t)decoded.size()));
             if (r == 2) {
                 ++res->decode_fail;
                 return false;
@@ -328,16 +348,20 @@ struct Stream
                 fail(2);
                 return false;
             }
-            for (const Pkt& p : pkts) {
-                log.push_back(ev(EV_DECODED_PKT, 0, p.num, p.bytes));
+            phase = DECODED;
+            return codec->wants_yield_after_decode();
+        }
+        case DECODED: {
+            for (const Pkt& p : decoded) {
+                log.push_back(ev(EV_DECODED_PKT, 0, p.num));
                 log.push_back(codec->pkt_token(p, packet_id(p.num), &dataOk));
                 ++res->recovered;
             }
-            if (!deliver()) {
+            decoded.clear();
+            phase = DECODE_LOOP;
+            if (!deliver())
                 fail(2);
-                return false;
-            }
-            return codec->wants_yield_after_decode();
+            return false;
         }
         case ACK: {
             phase = (i >= cfg->originals) ? TAIL : ADD;
@@ -365,7 +389,7 @@ struct Stream
             }
             ++tail;
             encode_once();
-            return false;
+            return codec->wants_yield_after_encode();
         case DONE:
             return false;
         }

@@ -1,0 +1,438 @@
+// harness/scenario_batch.cpp -- lock-step batched driver over the
+// device-resident API (include/siamese_gpu.h) of libsiamese_amd.
+//
+// Every stream runs the same Stream<> state machine as the per-call driver,
+// so each stream issues the identical call sequence; only the interleaving
+// across streams differs.  A round advances every live stream until it
+// yields (after a successful decode, whose recovered lengths the device
+// resolves at the flush), then one sgpu_flush() executes the round's device
+// work for all streams in a few kernel launches.
+//
+// Originals are staged in HBM once before timing starts ("device-resident").
+//
+// Exported (ctypes):
+//   int scenario_run_batch(const char* lib, const ScenarioConfig* cfg,
+//                          StreamResult* results, const BatchOptions* opt,
+//                          BatchReport* report)
+#include "scenario.h"
+#include "../include/siamese_gpu.h"
+
+#include <dlfcn.h>
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <memory>
+
+extern "C" {
+
+struct BatchOptions
+{
+    uint32_t steps;    ///< timed repetitions of the whole workload
+    uint32_t warmup;   ///< untimed repetitions before timing
+    uint32_t verify;   ///< check every recovered packet's bytes (first run only)
+    int32_t device;    ///< HIP device (-1 = current)
+};
+
+struct BatchReport
+{
+    double seconds;        ///< wall time of the timed steps (total)
+    double device_ms;      ///< device time of all launches in the timed steps
+    double exec_ms;        ///< device time of the executor launches only
+    double setup_seconds;  ///< payload generation + staging (untimed)
+    uint64_t rounds;       ///< rounds (flushes) in the timed steps
+    uint64_t engine[10];   ///< engine counters over the timed steps (see sgpu_engine_stats)
+    uint64_t checked;      ///< packets whose bytes were verified
+    uint64_t mismatches;   ///< verification failures
+};
+
+} // extern "C"
+
+namespace {
+
+constexpr int kEngineStats = 10;
+using Clock = std::chrono::steady_clock;
+
+struct Api
+{
+    int (*init)(int);
+    SgpuEncoder (*encoder_create)(void);
+    void (*encoder_free)(SgpuEncoder);
+    SiameseResult (*encoder_add)(SgpuEncoder, const void*, unsigned, unsigned*);
+    SiameseResult (*encoder_remove_before)(SgpuEncoder, unsigned);
+    SiameseResult (*encode)(SgpuEncoder, SgpuRecoveryPacket*);
+    SgpuDecoder (*decoder_create)(void);
+    void (*decoder_free)(SgpuDecoder);
+    SiameseResult (*decoder_add_original)(SgpuDecoder, unsigned, const void*, unsigned);
+    SiameseResult (*decoder_add_recovery)(SgpuDecoder, const SgpuRecoveryPacket*);
+    SiameseResult (*decoder_is_ready)(SgpuDecoder);
+    SiameseResult (*decode)(SgpuDecoder, SiameseOriginalPacket**, unsigned*);
+    SiameseResult (*decoder_get)(SgpuDecoder, SiameseOriginalPacket*);
+    int (*flush)(void);
+    void* (*device_alloc)(size_t);
+    void (*device_free)(void*);
+    int (*h2d)(void*, const void*, size_t);
+    int (*gather)(unsigned, const void* const*, const unsigned*, void*);
+    void (*timing)(int, int, double*, double*);
+    void (*engine_stats)(uint64_t*);
+};
+
+template <class F>
+bool bind(void* h, F& fn, const char* name)
+{
+    fn = reinterpret_cast<F>(dlsym(h, name));
+    if (!fn)
+        std::fprintf(stderr, "scenario_batch: missing symbol %s\n", name);
+    return fn != nullptr;
+}
+
+bool load_api(const char* path, Api& a)
+{
+    void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        std::fprintf(stderr, "scenario_batch: dlopen(%s) failed: %s\n", path, dlerror());
+        return false;
+    }
+    return bind(h, a.init, "sgpu_init") && bind(h, a.encoder_create, "sgpu_encoder_create") &&
+           bind(h, a.encoder_free, "sgpu_encoder_free") && bind(h, a.encoder_add, "sgpu_encoder_add") &&
+           bind(h, a.encoder_remove_before, "sgpu_encoder_remove_before") &&
+           bind(h, a.encode, "sgpu_encode") && bind(h, a.decoder_create, "sgpu_decoder_create") &&
+           bind(h, a.decoder_free, "sgpu_decoder_free") &&
+           bind(h, a.decoder_add_original, "sgpu_decoder_add_original") &&
+           bind(h, a.decoder_add_recovery, "sgpu_decoder_add_recovery") &&
+           bind(h, a.decoder_is_ready, "sgpu_decoder_is_ready") && bind(h, a.decode, "sgpu_decode") &&
+           bind(h, a.decoder_get, "sgpu_decoder_get") && bind(h, a.flush, "sgpu_flush") &&
+           bind(h, a.device_alloc, "sgpu_device_alloc") && bind(h, a.device_free, "sgpu_device_free") &&
+           bind(h, a.h2d, "sgpu_h2d") && bind(h, a.gather, "sgpu_gather") &&
+           bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats");
+}
+
+struct Rec
+{
+    unsigned bytes = 0;
+    SgpuRecoveryPacket pkt{};
+};
+
+struct Pkt
+{
+    unsigned num = 0, bytes = 0;
+    const unsigned char* data = nullptr;          // device pointer (get)
+    const SiameseOriginalPacket* entry = nullptr; // decode output entry (resolved at flush)
+};
+
+// A token whose value needs device bytes, resolved once the flush that
+// produced them has completed.
+struct Request
+{
+    std::vector<uint64_t>* log;
+    size_t pos;
+    const void* dev;
+    unsigned bytes;
+    unsigned id;     // payload id to verify against (packets only)
+    bool isPacket;
+    bool* ok;
+};
+
+struct Shared
+{
+    const Api* api;
+    const ScenarioConfig* cfg;
+    uint8_t* payload;        // all originals, device-resident
+    size_t stride;
+    bool hashData;
+    bool verify;
+    std::vector<Request> cur, prev;
+    uint64_t checked = 0, mismatches = 0;
+};
+
+struct BatchCodec
+{
+    Shared* sh;
+    SgpuEncoder enc = nullptr;
+    SgpuDecoder dec = nullptr;
+    std::vector<uint64_t>* log = nullptr;
+
+    const void* dev_payload(unsigned id) const { return sh->payload + (size_t)id * sh->stride; }
+
+    bool needs_host_payload() const { return false; }
+    int enc_add(unsigned id, const uint8_t*, unsigned bytes, unsigned* num)
+    {
+        return sh->api->encoder_add(enc, dev_payload(id), bytes, num);
+    }
+    int encode(Rec* r)
+    {
+        const int res = sh->api->encode(enc, &r->pkt);
+        r->bytes = r->pkt.DataBytes;
+        return res;
+    }
+    int dec_add_original(unsigned id, unsigned num, const uint8_t*, unsigned bytes)
+    {
+        return sh->api->decoder_add_original(dec, num, dev_payload(id), bytes);
+    }
+    int dec_add_recovery(const Rec& r) { return sh->api->decoder_add_recovery(dec, &r.pkt); }
+    int is_ready() { return sh->api->decoder_is_ready(dec); }
+    int decode(std::vector<Pkt>* out)
+    {
+        SiameseOriginalPacket* p = nullptr;
+        unsigned n = 0;
+        const int r = sh->api->decode(dec, &p, &n);
+        if (r == 0)
+            for (unsigned i = 0; i < n; ++i) {
+                Pkt k;
+                k.num = p[i].PacketNum;
+                k.entry = &p[i];
+                out->push_back(k);
+            }
+        return r;
+    }
+    int dec_get(unsigned num, Pkt* out)
+    {
+        SiameseOriginalPacket p;
+        p.PacketNum = num;
+        p.Data = nullptr;
+        p.DataBytes = 0;
+        const int r = sh->api->decoder_get(dec, &p);
+        out->num = num;
+        out->bytes = p.DataBytes;
+        out->data = p.Data;
+        return r;
+    }
+    int enc_remove_before(unsigned num) { return sh->api->encoder_remove_before(enc, num); }
+
+    uint64_t rec_token(const Rec& r)
+    {
+        if (sh->hashData)
+            sh->cur.push_back(Request{log, log->size(), r.pkt.DeviceData, r.bytes, 0, false, nullptr});
+        return r.bytes;
+    }
+    uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok)
+    {
+        const unsigned bytes = p.entry ? p.entry->DataBytes : p.bytes;
+        const void* data = p.entry ? p.entry->Data : p.data;
+        const unsigned want = sh->cfg->payload_bytes ? sh->cfg->payload_bytes : scen::variable_bytes(id);
+        if (bytes != want || !data)
+            *ok = false;
+        else if (sh->hashData || sh->verify)
+            sh->cur.push_back(Request{log, log->size(), data, bytes, id, true, ok});
+        return bytes;
+    }
+    bool wants_yield_after_decode() const { return true; }
+    bool wants_yield_after_encode() const { return sh->hashData; }
+};
+
+using BatchStream = scen::Stream<BatchCodec, Rec, Pkt>;
+
+// Resolve tokens whose data was produced by an already completed flush.
+void resolve_requests(Shared& sh, std::vector<Request>& reqs)
+{
+    if (reqs.empty())
+        return;
+    std::vector<const void*> srcs;
+    std::vector<unsigned> lens;
+    size_t total = 0;
+    for (const Request& r : reqs) {
+        srcs.push_back(r.dev);
+        lens.push_back(r.bytes);
+        total += r.bytes;
+    }
+    std::vector<uint8_t> host(total + 16);
+    if (sh.api->gather((unsigned)reqs.size(), srcs.data(), lens.data(), host.data()) != 0) {
+        for (const Request& r : reqs)
+            if (r.ok)
+                *r.ok = false;
+        reqs.clear();
+        return;
+    }
+    std::vector<uint8_t> expect;
+    size_t off = 0;
+    for (const Request& r : reqs) {
+        const uint8_t* d = host.data() + off;
+        off += r.bytes;
+        if (r.isPacket) {
+            expect.resize(r.bytes + 8);
+            scen::fill_payload(r.id, expect.data(), r.bytes);
+            ++sh.checked;
+            if (std::memcmp(expect.data(), d, r.bytes) != 0) {
+                ++sh.mismatches;
+                *r.ok = false;
+            }
+        }
+        if (sh.hashData)
+            (*r.log)[r.pos] = scen::data_token(true, d, r.bytes);
+    }
+    reqs.clear();
+}
+
+int run_once(Shared& sh, StreamResult* results, uint64_t* rounds)
+{
+    const Api& api = *sh.api;
+    const ScenarioConfig* cfg = sh.cfg;
+    const unsigned n = cfg->streams;
+    std::vector<BatchCodec> codecs(n);
+    std::unique_ptr<BatchStream[]> streams(new BatchStream[n]);
+    for (unsigned s = 0; s < n; ++s) {
+        codecs[s].sh = &sh;
+        codecs[s].enc = api.encoder_create();
+        codecs[s].dec = api.decoder_create();
+        codecs[s].log = &streams[s].log;
+        streams[s].init(cfg, &codecs[s], &results[s], cfg->first_stream + s);
+        if (!codecs[s].enc || !codecs[s].dec)
+            streams[s].fail(2);
+    }
+    std::vector<unsigned> live(n);
+    for (unsigned s = 0; s < n; ++s)
+        live[s] = s;
+    int rc = 0;
+    while (!live.empty()) {
+        for (unsigned s : live) {
+            BatchStream& st = streams[s];
+            while (!st.done())
+                if (st.step())
+                    break;
+        }
+        // bytes produced by the previous flush are final now
+        resolve_requests(sh, sh.prev);
+        if (api.flush() != 0) {
+            rc = -3;
+            break;
+        }
+        ++*rounds;
+        std::swap(sh.prev, sh.cur);
+        live.erase(std::remove_if(live.begin(), live.end(),
+                                  [&](unsigned s) { return streams[s].done(); }),
+                   live.end());
+    }
+    resolve_requests(sh, sh.prev);
+    resolve_requests(sh, sh.cur);
+    for (unsigned s = 0; s < n; ++s) {
+        streams[s].finish();
+        api.encoder_free(codecs[s].enc);
+        api.decoder_free(codecs[s].dec);
+    }
+    api.flush();
+    return rc;
+}
+
+} // namespace
+
+namespace {
+
+struct Session
+{
+    Api* api;
+    ScenarioConfig cfg;
+    uint8_t* dev = nullptr;
+    Shared sh;
+    double setupSeconds = 0;
+};
+
+Api g_api;
+bool g_loaded = false;
+
+} // namespace
+
+extern "C" __attribute__((visibility("default")))
+void* scenario_batch_open(const char* lib, const ScenarioConfig* cfg, int device)
+{
+    if (!g_loaded) {
+        if (!load_api(lib, g_api))
+            return nullptr;
+        g_loaded = true;
+    }
+    if (g_api.init(device) != 0)
+        return nullptr;
+    Session* ss = new Session;
+    ss->api = &g_api;
+    ss->cfg = *cfg;
+    const ScenarioConfig* c = &ss->cfg;
+
+    // Stage every original of every stream in HBM (untimed).
+    const auto t0 = Clock::now();
+    const size_t total = (size_t)c->streams * c->originals;
+    const unsigned maxBytes = c->payload_bytes ? c->payload_bytes : 1200;
+    const size_t stride = (maxBytes + 63) & ~(size_t)63;
+    ss->dev = (uint8_t*)g_api.device_alloc(total * stride);
+    if (!ss->dev) {
+        delete ss;
+        return nullptr;
+    }
+    const size_t chunkPackets = std::max<size_t>(1, (size_t)(64u << 20) / stride);
+    std::vector<uint8_t> host(chunkPackets * stride);
+    for (size_t base = 0; base < total; base += chunkPackets) {
+        const size_t cnt = std::min(chunkPackets, total - base);
+        for (size_t k = 0; k < cnt; ++k) {
+            const unsigned id = (unsigned)((size_t)c->first_stream * c->originals + base + k);
+            const unsigned b = c->payload_bytes ? c->payload_bytes : scen::variable_bytes(id);
+            scen::fill_payload(id, host.data() + k * stride, b);
+        }
+        g_api.h2d(ss->dev + base * stride, host.data(), cnt * stride);
+    }
+    // payload ids are global; offset the base so an id indexes it directly
+    ss->sh.api = &g_api;
+    ss->sh.cfg = c;
+    ss->sh.payload = ss->dev - (size_t)c->first_stream * c->originals * stride;
+    ss->sh.stride = stride;
+    ss->sh.hashData = c->hash_data != 0;
+    ss->setupSeconds = std::chrono::duration<double>(Clock::now() - t0).count();
+    return ss;
+}
+
+extern "C" __attribute__((visibility("default")))
+int scenario_batch_run(void* session, StreamResult* results, const BatchOptions* opt,
+                       BatchReport* report)
+{
+    Session* ss = (Session*)session;
+    const Api& api = *ss->api;
+    Shared& sh = ss->sh;
+    std::memset(report, 0, sizeof(*report));
+    report->setup_seconds = ss->setupSeconds;
+    sh.checked = sh.mismatches = 0;
+    int rc = 0;
+    const unsigned runs = opt->warmup + opt->steps;
+    for (unsigned r = 0; r < runs && rc == 0; ++r) {
+        const bool timed = r >= opt->warmup;
+        sh.verify = opt->verify && r == 0;
+        uint64_t rounds = 0;
+        uint64_t e0[kEngineStats], e1[kEngineStats];
+        api.engine_stats(e0);
+        api.timing(timed ? 1 : 0, 1, nullptr, nullptr);
+        const auto t1 = Clock::now();
+        rc = run_once(sh, results, &rounds);
+        const double dt = std::chrono::duration<double>(Clock::now() - t1).count();
+        double execMs = 0, totalMs = 0;
+        api.timing(0, 1, &execMs, &totalMs);
+        api.engine_stats(e1);
+        if (timed) {
+            report->seconds += dt;
+            report->device_ms += totalMs;
+            report->exec_ms += execMs;
+            report->rounds += rounds;
+            for (int k = 0; k < kEngineStats; ++k)
+                report->engine[k] += e1[k] - e0[k];
+        }
+    }
+    report->checked = sh.checked;
+    report->mismatches = sh.mismatches;
+    return rc;
+}
+
+extern "C" __attribute__((visibility("default")))
+void scenario_batch_close(void* session)
+{
+    Session* ss = (Session*)session;
+    if (!ss)
+        return;
+    ss->api->device_free(ss->dev);
+    delete ss;
+}
+
+extern "C" __attribute__((visibility("default")))
+int scenario_run_batch(const char* lib, const ScenarioConfig* cfg, StreamResult* results,
+                       const BatchOptions* opt, BatchReport* report)
+{
+    void* s = scenario_batch_open(lib, cfg, opt->device);
+    if (!s)
+        return -2;
+    const int rc = scenario_batch_run(s, results, opt, report);
+    scenario_batch_close(s);
+    return rc;
+}

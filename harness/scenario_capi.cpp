@@ -16,7 +16,6 @@
 #include <chrono>
 #include <cstdio>
 #include <thread>
-#include <atomic>
 
 namespace {
 
@@ -80,23 +79,26 @@ struct Pkt
 
 using Clock = std::chrono::steady_clock;
 
+struct Timer
+{
+    double& acc;
+    Clock::time_point t0;
+    explicit Timer(double& a) : acc(a), t0(Clock::now()) {}
+    ~Timer() { acc += std::chrono::duration<double>(Clock::now() - t0).count(); }
+};
+
 struct CapiCodec
 {
     const CApi* api = nullptr;
+    const ScenarioConfig* cfg = nullptr;
     SiameseEncoder enc = nullptr;
     SiameseDecoder dec = nullptr;
     std::vector<uint8_t> expect;
     double seconds = 0;
 
-    struct Timer
-    {
-        double& acc;
-        Clock::time_point t0;
-        explicit Timer(double& a) : acc(a), t0(Clock::now()) {}
-        ~Timer() { acc += std::chrono::duration<double>(Clock::now() - t0).count(); }
-    };
+    bool needs_host_payload() const { return true; }
 
-    int enc_add(const uint8_t* data, unsigned bytes, unsigned* num)
+    int enc_add(unsigned, const uint8_t* data, unsigned bytes, unsigned* num)
     {
         SiameseOriginalPacket p;
         p.PacketNum = 0;
@@ -122,7 +124,7 @@ struct CapiCodec
         rec->data = r.Data;
         return res;
     }
-    int dec_add_original(unsigned num, const uint8_t* data, unsigned bytes)
+    int dec_add_original(unsigned, unsigned num, const uint8_t* data, unsigned bytes)
     {
         SiameseOriginalPacket p;
         p.PacketNum = num;
@@ -179,28 +181,31 @@ struct CapiCodec
         Timer t(seconds);
         return api->encoder_remove_before(enc, num);
     }
-    uint64_t rec_token(const Rec& rec) { return scen::hash_bytes(rec.data, rec.bytes); }
+    uint64_t rec_token(const Rec& rec) { return scen::data_token(cfg->hash_data, rec.data, rec.bytes); }
     uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok)
     {
         expect.resize(p.bytes + 8);
         scen::fill_payload(id, expect.data(), p.bytes);
-        if (!p.data || std::memcmp(expect.data(), p.data, p.bytes) != 0)
+        const unsigned want = cfg->payload_bytes ? cfg->payload_bytes : scen::variable_bytes(id);
+        if (!p.data || p.bytes != want || std::memcmp(expect.data(), p.data, p.bytes) != 0)
             *ok = false;
-        return p.data ? scen::hash_bytes(p.data, p.bytes) : 0;
+        return p.data ? scen::data_token(cfg->hash_data, p.data, p.bytes) : 0;
     }
-    bool wants_yield_after_decode() { return false; }
+    bool wants_yield_after_decode() const { return false; }
+    bool wants_yield_after_encode() const { return false; }
 };
 
 using CapiStream = scen::Stream<CapiCodec, Rec, Pkt>;
 
-void run_range(const CApi* api, const ScenarioConfig* cfg, StreamResult* results,
-               unsigned begin, unsigned end, double* seconds, FILE* log)
+void run_range(const CApi* api, const ScenarioConfig* cfg, StreamResult* results, unsigned begin,
+               unsigned end, double* seconds, FILE* log)
 {
     for (unsigned s = begin; s < end; ++s) {
         CapiCodec codec;
         codec.api = api;
+        codec.cfg = cfg;
         {
-            CapiCodec::Timer t(codec.seconds);
+            Timer t(codec.seconds);
             codec.enc = api->encoder_create();
             codec.dec = api->decoder_create();
         }
@@ -212,7 +217,7 @@ void run_range(const CApi* api, const ScenarioConfig* cfg, StreamResult* results
             st.step();
         st.finish();
         {
-            CapiCodec::Timer t(codec.seconds);
+            Timer t(codec.seconds);
             api->encoder_free(codec.enc);
             api->decoder_free(codec.dec);
         }
@@ -253,8 +258,7 @@ int scenario_run_capi(const char* lib, const ScenarioConfig* cfg, StreamResult* 
         for (unsigned t = 0; t < threads; ++t) {
             const unsigned b = (unsigned)((uint64_t)cfg->streams * t / threads);
             const unsigned e = (unsigned)((uint64_t)cfg->streams * (t + 1) / threads);
-            pool.emplace_back(run_range, &api, cfg, results, b, e, &secs[t],
-                              t == 0 ? log : nullptr);
+            pool.emplace_back(run_range, &api, cfg, results, b, e, &secs[t], t == 0 ? log : nullptr);
         }
         for (auto& th : pool)
             th.join();
@@ -262,8 +266,8 @@ int scenario_run_capi(const char* lib, const ScenarioConfig* cfg, StreamResult* 
     const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
     if (log)
         std::fclose(log);
-    // Single thread: sum of codec-call time.  Multi-thread: codec time is
-    // spread over cores, so report the wall time of the whole pool.
+    // One thread: the sum of codec-call time.  Several threads: wall time of
+    // the pool (codec work spread over cores).
     double total = 0;
     for (double s : secs)
         total += s;

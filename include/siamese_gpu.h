@@ -22,6 +22,7 @@
 #define SIAMESE_GPU_H
 
 #include "siamese.h"
+#include <stddef.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -73,10 +74,21 @@ SIAMESE_EXPORT int sgpu_flush(void);
 /// Submit without waiting (the next sgpu_flush completes it).
 SIAMESE_EXPORT int sgpu_submit(void);
 
+/// Device memory helpers for applications and the benchmark harness.
+SIAMESE_EXPORT void* sgpu_device_alloc(size_t bytes);
+SIAMESE_EXPORT void sgpu_device_free(void* p);
+SIAMESE_EXPORT int sgpu_h2d(void* deviceDst, const void* hostSrc, size_t bytes);
+/// Gather `count` device ranges into one host buffer (concatenated in order).
+/// Runs immediately; queued-but-unflushed codec work is left untouched.
+SIAMESE_EXPORT int sgpu_gather(unsigned count, const void* const* deviceSrcs, const unsigned* bytes,
+                               void* hostOut);
+
 /// Device timing of flushed work since the last reset (milliseconds).
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs);
-/// Counters of the engine (flushes, launches, ops, terms, solves, ingests, upload bytes).
-SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out7);
+/// Engine counters: flushes, launches, ops, terms, solves, ingests, upload
+/// bytes, algorithmic op bytes, algorithmic output bytes, and the part of
+/// the algorithmic bytes handled by the solve kernels (10 values).
+SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out10);
 
 #ifdef __cplusplus
 }

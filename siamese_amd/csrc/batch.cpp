@@ -209,6 +209,37 @@ SIAMESE_EXPORT int sgpu_submit(void)
     return 0;
 }
 
+SIAMESE_EXPORT void* sgpu_device_alloc(size_t bytes)
+{
+    if (!g_batchReady)
+        return nullptr;
+    Lock lock(Engine::global()->mutex());
+    return be_dev_alloc(bytes);
+}
+
+SIAMESE_EXPORT void sgpu_device_free(void* p)
+{
+    Lock lock(Engine::global()->mutex());
+    be_dev_free(p);
+}
+
+SIAMESE_EXPORT int sgpu_h2d(void* deviceDst, const void* hostSrc, size_t bytes)
+{
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    eng->sync();
+    be_h2d(deviceDst, hostSrc, bytes);
+    return be_sync() ? 0 : -1;
+}
+
+SIAMESE_EXPORT int sgpu_gather(unsigned count, const void* const* deviceSrcs, const unsigned* bytes,
+                               void* hostOut)
+{
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    return eng->gather(count, deviceSrcs, bytes, hostOut) ? 0 : -1;
+}
+
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs)
 {
     be_timing_enable(enable != 0);
@@ -220,16 +251,20 @@ SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* t
         be_timing_reset();
 }
 
-SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out7)
+SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out10)
 {
     const Engine::Stats& s = Engine::global()->stats;
-    out7[0] = s.flushes;
-    out7[1] = s.launches;
-    out7[2] = s.ops;
-    out7[3] = s.terms;
-    out7[4] = s.solves;
-    out7[5] = s.ingests;
-    out7[6] = s.uploadBytes;
+    uint64_t* out9 = out10;
+    out10[9] = s.solveBytes;
+    out9[0] = s.flushes;
+    out9[1] = s.launches;
+    out9[2] = s.ops;
+    out9[3] = s.terms;
+    out9[4] = s.solves;
+    out9[5] = s.ingests;
+    out9[6] = s.uploadBytes;
+    out9[7] = s.refOpBytes;
+    out9[8] = s.outBytes;
 }
 
 } // extern "C"

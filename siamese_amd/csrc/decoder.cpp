@@ -253,9 +253,13 @@ DevSum& DecoderCore::get_sum(unsigned lane, unsigned s, unsigned elementEnd)
         if (!grow_sum(S.d, newBytes))
             return S.d;
         prog_.lc_begin(S.d.buf.addr(), S.d.bytes, S.d.devValid);
-        for (const T& t : terms)
+        uint64_t opBytes = 0;
+        for (const T& t : terms) {
             prog_.lc_term(t.src, t.len, t.c);
+            opBytes += t.len;
+        }
         prog_.lc_end();
+        eng_->account(opBytes);
         S.d.devValid = S.d.bytes;
     }
     S.elementEnd = element;
@@ -282,6 +286,7 @@ bool DecoderCore::plug_sum_holes(unsigned elementStart)
             prog_.lc_begin(S.d.buf.addr(), S.d.bytes, S.d.devValid);
             prog_.lc_term(o.buf.addr(), o.bytes, sum_coeff(s, column));
             prog_.lc_end();
+            eng_->account(o.bytes);
             S.d.devValid = S.d.bytes;
         }
     }
@@ -1111,6 +1116,7 @@ bool DecoderCore::eliminate_original_data()
                     continue;
                 const uint8_t y = m.row == 0 ? 1 : cauchy_element(m.row - 1, o.column % kCauchyMaxColumns);
                 prog_.lc_term(o.buf.addr(), std::min(o.bytes, rb), y);
+                eng_->account(std::min(o.bytes, rb));
             }
             prog_.lc_end();
             continue;
@@ -1161,9 +1167,13 @@ bool DecoderCore::eliminate_original_data()
                 terms.push_back(T{b.buf.addr(), std::min(b.bytes, rb), 1});
         }
         prog_.lc_begin(rec->buf.addr(), rb, rb, row_value(m.row));
-        for (const T& t : terms)
+        uint64_t opBytes = rb; // RX * product muladd
+        for (const T& t : terms) {
             prog_.lc_term(t.src, t.len, 1, t.acc);
+            opBytes += t.len;
+        }
         prog_.lc_end();
+        eng_->account(opBytes);
     }
     return !disabled_;
 }
@@ -1186,12 +1196,18 @@ SiameseResult DecoderCore::solve_and_substitute()
         desc[i].initBytes = len[i];
     }
     // Row growth of MultiplyLowerTriangle (GrowZeroPadded), simulated here
+    uint64_t lowerOpBytes = 0;
     for (unsigned i = 0; i + 1 < m; ++i) {
         desc[i].lowerLen = len[i];
-        for (unsigned j = i + 1; j < m; ++j)
-            if (mrow(pivots_[j])[i] != 0 && len[j] < len[i])
+        for (unsigned j = i + 1; j < m; ++j) {
+            if (mrow(pivots_[j])[i] == 0)
+                continue;
+            lowerOpBytes += len[i];
+            if (len[j] < len[i])
                 len[j] = len[i];
+        }
     }
+    eng_->account(lowerOpBytes, 0, true);
     if (m > 0)
         desc[m - 1].lowerLen = len[m - 1];
 
@@ -1251,7 +1267,25 @@ SiameseResult DecoderCore::solve_and_substitute()
     std::weak_ptr<int> alive = alive_;
     const uint64_t serial = decodeSerial_;
     pendingSolves_++;
-    eng_->on_complete([this, alive, fixes, base, m, serial](const uint32_t* results) {
+    Engine* eng = eng_;
+    std::vector<unsigned> finals(len.begin(), len.end());
+    eng_->on_complete([this, alive, fixes, base, m, serial, coef, finals, eng](const uint32_t* results) {
+        // Back-substitution bytes of the reference (:1131-1212) need the
+        // recovered lengths, so they are counted once those are known.
+        const unsigned ok = results[base];
+        uint64_t opBytes = 0, outBytes = 0;
+        for (unsigned k = 0; k < ok && k < m; ++k) {
+            const unsigned i = m - 1 - k;
+            const uint32_t w = results[base + 1 + i];
+            const unsigned bb = (w >> 29) + (w & kSolveLengthMask);
+            const unsigned lc = std::min(32u, finals[i]);
+            opBytes += std::max(lc, bb);
+            outBytes += bb;
+            for (unsigned j = 0; j < i; ++j)
+                if (coef[(size_t)j * m + i])
+                    opBytes += std::min(bb, finals[j]);
+        }
+        eng->account(opBytes, outBytes, true);
         if (alive.expired())
             return;
         resolve_solve(results, base, m, fixes, serial);

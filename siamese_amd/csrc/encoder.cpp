@@ -235,9 +235,13 @@ DevSum& EncoderCore::get_sum(unsigned lane, unsigned sumIndex, unsigned elementE
     if (!grow_sum(sum, newBytes))
         return sum;
     prog_.lc_begin(sum.buf.addr(), sum.bytes, sum.devValid);
-    for (const T& t : terms)
+    uint64_t opBytes = 0;
+    for (const T& t : terms) {
         prog_.lc_term(t.src, t.len, t.c);
+        opBytes += t.len; // one add/muladd per original in the reference
+    }
     prog_.lc_end();
+    eng_->account(opBytes);
     sum.devValid = sum.bytes;
     L.next[sumIndex] = element;
     return sum;
@@ -283,6 +287,7 @@ void EncoderCore::finish_row(EncodeOut& out, const RowMeta& meta, unsigned paylo
     prog_.literal(recovery_.addr(), payloadBytes, out.footer, out.footerBytes);
     out.buf = recovery_;
     out.bytes = payloadBytes + out.footerBytes;
+    eng_->account(0, out.bytes);
     stats_[SiameseEncoderStats_RecoveryCount]++;
     stats_[SiameseEncoderStats_RecoveryBytes] += out.bytes;
 }
@@ -384,9 +389,15 @@ SiameseResult EncoderCore::cauchy_row(EncodeOut& out)
     }
 
     prog_.lc_begin(recovery_.addr(), used, 0);
-    for (const T& t : terms)
-        prog_.lc_term(t.src, t.len, t.c);
+    uint64_t opBytes = 0;
+    for (size_t k = 0; k < terms.size(); ++k) {
+        prog_.lc_term(terms[k].src, terms[k].len, terms[k].c);
+        // the reference memcpy's the first parity column (no GF op)
+        if (k > 0 || m.row != 0)
+            opBytes += terms[k].len;
+    }
     prog_.lc_end();
+    eng_->account(opBytes);
     finish_row(out, m, used);
     return Siamese_Success;
 }
@@ -437,9 +448,13 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
 
     // Recovery = row sums ^ RX * product  (:1232-1233), one fused device op
     prog_.lc_begin(recovery_.addr(), recoveryBytes, 0, row_value(row));
-    for (const T& t : terms)
+    uint64_t opBytes = recoveryBytes; // final RX * product muladd
+    for (const T& t : terms) {
         prog_.lc_term(t.src, t.len, 1, t.acc);
+        opBytes += t.len;
+    }
     prog_.lc_end();
+    eng_->account(opBytes);
 
     RowMeta m;
     m.sumCount = sumEnd_ - sumStart_ + sumErased_;

@@ -540,6 +540,62 @@ void Engine::flush()
     resultWords_ = 0;
 }
 
+bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut)
+{
+    if (flight_.active)
+        sync();
+    if (count == 0)
+        return true;
+    std::vector<IngestDesc> descs(count);
+    std::vector<IngestItem> items;
+    size_t total = 0;
+    for (unsigned i = 0; i < count; ++i) {
+        std::memset(&descs[i], 0, sizeof(IngestDesc));
+        descs[i].src = (uint64_t)(uintptr_t)srcs[i];
+        descs[i].bytes = bytes[i];
+        descs[i].dst = total; // offset for now
+        for (uint32_t t = 0; t < bytes[i]; t += kTileBytes)
+            items.push_back(IngestItem{i, t});
+        total = align16(total + bytes[i]);
+    }
+    const size_t dBytes = count * sizeof(IngestDesc);
+    const size_t upBytes = align16(dBytes) + items.size() * sizeof(IngestItem);
+    auto grow = [](uint8_t*& h, uint8_t*& d, size_t& cap, size_t need) {
+        if (need <= cap)
+            return;
+        size_t c = cap ? cap : (1u << 20);
+        while (c < need)
+            c *= 2;
+        if (h)
+            be_host_free(h);
+        if (d)
+            be_dev_free(d);
+        h = (uint8_t*)be_host_alloc(c);
+        d = (uint8_t*)be_dev_alloc(c);
+        cap = c;
+    };
+    grow(gUpHost_, gUpDev_, gUpCap_, upBytes);
+    grow(gHost_, gDev_, gCap_, total);
+    for (IngestDesc& d : descs)
+        d.dst += (uint64_t)(uintptr_t)gDev_;
+    std::memcpy(gUpHost_, descs.data(), dBytes);
+    std::memcpy(gUpHost_ + align16(dBytes), items.data(), items.size() * sizeof(IngestItem));
+    be_h2d(gUpDev_, gUpHost_, upBytes);
+    if (!items.empty())
+        be_launch_ingest((const IngestDesc*)gUpDev_, (const IngestItem*)(gUpDev_ + align16(dBytes)),
+                         (uint32_t)items.size());
+    be_d2h(gHost_, gDev_, total);
+    const bool ok = be_sync();
+    uint8_t* out = (uint8_t*)hostOut;
+    size_t off = 0;
+    for (unsigned i = 0; i < count; ++i) {
+        std::memcpy(out, gHost_ + off, bytes[i]);
+        out += bytes[i];
+        off = align16(off + bytes[i]);
+    }
+    return ok;
+}
+
 bool Engine::sync()
 {
     if (!flight_.active)

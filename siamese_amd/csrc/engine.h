@@ -121,6 +121,10 @@ public:
 
     bool pending() const { return !dirty_.empty() || !ingest_.empty() || !downloads_.empty(); }
 
+    /// Copy device ranges into one host buffer right now (after completing
+    /// any flush in flight).  Queued, unflushed work is not touched.
+    bool gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut);
+
     std::mutex& mutex() { return mu_; }
 
     // statistics of the last flushes (for the bench / profiles)
@@ -128,7 +132,20 @@ public:
     {
         uint64_t flushes = 0, launches = 0, ops = 0, terms = 0, solves = 0, ingests = 0;
         uint64_t uploadBytes = 0;
+        // Algorithmic bytes: source bytes of every bulk GF op
+        // the reference codec performs for the same call sequence, and bytes
+        // of recovery packets / recovered originals produced.
+        uint64_t refOpBytes = 0, outBytes = 0;
+        uint64_t solveBytes = 0;   // the part of both done by the solve kernels
     } stats;
+
+    void account(uint64_t opBytes, uint64_t outBytes = 0, bool inSolve = false)
+    {
+        stats.refOpBytes += opBytes;
+        stats.outBytes += outBytes;
+        if (inSolve)
+            stats.solveBytes += opBytes + outBytes;
+    }
 
 private:
     friend class Program;
@@ -198,6 +215,14 @@ private:
     size_t downCap_ = 0;
     void ensure_up(size_t bytes);
     void ensure_down(size_t bytes);
+
+    // gather buffers (separate from the flush buffers)
+    uint8_t* gUpHost_ = nullptr;
+    uint8_t* gUpDev_ = nullptr;
+    size_t gUpCap_ = 0;
+    uint8_t* gHost_ = nullptr;
+    uint8_t* gDev_ = nullptr;
+    size_t gCap_ = 0;
 };
 
 } // namespace sgpu

@@ -18,7 +18,7 @@ SIM_LIB = os.path.join(ROOT, "tests", "hostsim", "libsiamese_hostsim.so")
 
 _FIELDS = ("block_mode streams first_stream originals payload_bytes loss_pct "
            "recovery_loss_pct recovery_interval recovery_phase ack_policy ack_lag "
-           "tail_limit seed").split()
+           "tail_limit seed hash_data").split()
 
 
 class Config(ctypes.Structure):
@@ -39,7 +39,7 @@ class StreamResult(ctypes.Structure):
 def make_config(**kw):
     base = dict(block_mode=0, streams=1, first_stream=0, originals=200, payload_bytes=1400,
                 loss_pct=10, recovery_loss_pct=5, recovery_interval=8, recovery_phase=0,
-                ack_policy=0, ack_lag=40, tail_limit=600, seed=1013)
+                ack_policy=0, ack_lag=40, tail_limit=600, seed=1013, hash_data=1)
     base.update(kw)
     return Config(**base)
 
@@ -73,6 +73,18 @@ def replace(cfg, **kw):
     return Config(**d)
 
 
+class BatchOptions(ctypes.Structure):
+    _fields_ = [("steps", ctypes.c_uint32), ("warmup", ctypes.c_uint32),
+                ("verify", ctypes.c_uint32), ("device", ctypes.c_int32)]
+
+
+class BatchReport(ctypes.Structure):
+    _fields_ = [("seconds", ctypes.c_double), ("device_ms", ctypes.c_double),
+                ("exec_ms", ctypes.c_double), ("setup_seconds", ctypes.c_double),
+                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 10),
+                ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64)]
+
+
 _lib = None
 
 
@@ -84,6 +96,11 @@ def lib():
         _lib.scenario_run_capi.argtypes = [ctypes.c_char_p, ctypes.POINTER(Config),
                                            ctypes.POINTER(StreamResult), ctypes.c_uint,
                                            ctypes.POINTER(ctypes.c_double), ctypes.c_char_p]
+        _lib.scenario_run_batch.restype = ctypes.c_int
+        _lib.scenario_run_batch.argtypes = [ctypes.c_char_p, ctypes.POINTER(Config),
+                                            ctypes.POINTER(StreamResult),
+                                            ctypes.POINTER(BatchOptions),
+                                            ctypes.POINTER(BatchReport)]
     return _lib
 
 
@@ -100,6 +117,60 @@ def run_capi(library, cfg, threads=1, event_log=None):
     if rc != 0:
         raise RuntimeError("scenario_run_capi(%s) failed rc=%d" % (library, rc))
     return res, sec.value, wall
+
+
+def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1):
+    """Run `cfg` through the device-resident batch API (lock-step rounds).
+
+    Returns (results of the last run, BatchReport)."""
+    res = (StreamResult * cfg.streams)()
+    opt = BatchOptions(steps, warmup, 1 if verify else 0, device)
+    rep = BatchReport()
+    rc = lib().scenario_run_batch(library.encode(), ctypes.byref(cfg), res, ctypes.byref(opt),
+                                  ctypes.byref(rep))
+    if rc != 0:
+        raise RuntimeError("scenario_run_batch(%s) failed rc=%d" % (library, rc))
+    return res, rep
+
+
+ENGINE_KEYS = ("flushes launches ops terms solves ingests upload_bytes ref_op_bytes "
+               "out_bytes solve_bytes").split()
+
+
+def engine_dict(report):
+    return {k: int(report.engine[i]) for i, k in enumerate(ENGINE_KEYS)}
+
+
+class BatchSession:
+    """Payloads staged in HBM once; run() repeats the workload (bench.py)."""
+
+    def __init__(self, library, cfg, device=-1):
+        L = lib()
+        L.scenario_batch_open.restype = ctypes.c_void_p
+        L.scenario_batch_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(Config), ctypes.c_int]
+        L.scenario_batch_run.restype = ctypes.c_int
+        L.scenario_batch_run.argtypes = [ctypes.c_void_p, ctypes.POINTER(StreamResult),
+                                         ctypes.POINTER(BatchOptions),
+                                         ctypes.POINTER(BatchReport)]
+        L.scenario_batch_close.argtypes = [ctypes.c_void_p]
+        self.cfg = cfg
+        self.handle = L.scenario_batch_open(library.encode(), ctypes.byref(cfg), device)
+        if not self.handle:
+            raise RuntimeError("scenario_batch_open(%s) failed" % library)
+
+    def run(self, steps=1, warmup=0, verify=False):
+        res = (StreamResult * self.cfg.streams)()
+        opt = BatchOptions(steps, warmup, 1 if verify else 0, -1)
+        rep = BatchReport()
+        rc = lib().scenario_batch_run(self.handle, res, ctypes.byref(opt), ctypes.byref(rep))
+        if rc != 0:
+            raise RuntimeError("scenario_batch_run failed rc=%d" % rc)
+        return res, rep
+
+    def close(self):
+        if self.handle:
+            lib().scenario_batch_close(self.handle)
+            self.handle = None
 
 
 def digests(results):
