@@ -498,12 +498,20 @@ void DecoderCore::list_delete_before(unsigned element)
 {
     RecPacket* r = head_;
     unsigned deleted = 0;
+    bool regionStale = false;
     while (r && r->elementEnd <= element) {
         RecPacket* n = r->next;
+        // The reference keeps using a checked region whose packets it has
+        // just freed (use-after-free; it crashes under reordered input, see
+        // DESIGN.md "Deviations").  Drop such a region instead.
+        if (r == region_.first || r == region_.last)
+            regionStale = true;
         free_packet(r);
         ++deleted;
         r = n;
     }
+    if (regionStale)
+        region_reset();
     head_ = r;
     if (r) {
         r->prev = nullptr;

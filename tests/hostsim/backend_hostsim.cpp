@@ -172,8 +172,12 @@ void be_h2d(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, by
 void be_d2h(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
+static bool noexec();
+
 void be_launch_ingest(const IngestDesc* descs, const IngestItem* items, uint32_t count)
 {
+    if (noexec())
+        return;
     for (uint32_t i = 0; i < count; ++i) {
         const IngestDesc& d = descs[items[i].desc];
         const uint32_t total = d.hdrLen + d.bytes;
@@ -184,8 +188,21 @@ void be_launch_ingest(const IngestDesc* descs, const IngestItem* items, uint32_t
     }
 }
 
+// HOSTSIM_NOEXEC=1 skips all symbol arithmetic so the host control plane
+// can be timed on its own (profiling aid; results are fabricated lengths
+// that are only valid for fixed-size 1400-byte payloads).
+static bool noexec()
+{
+    static int v = -1;
+    if (v < 0)
+        v = std::getenv("HOSTSIM_NOEXEC") ? 1 : 0;
+    return v == 1;
+}
+
 void be_launch_exec(const GfOp* ops, const GfTerm* terms, const ExecItem* items, uint32_t count)
 {
+    if (noexec())
+        return;
     for (uint32_t i = 0; i < count; ++i)
         exec_tile(ops, terms, items[i]);
 }
@@ -199,6 +216,12 @@ void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const
         const SolveRow* R = rows + sd.rowBegin;
         const uint8_t* C = coef + sd.coefOffset;
         uint32_t* out = results + sd.result;
+        if (noexec()) {
+            out[0] = m;
+            for (uint32_t i = 0; i < m; ++i)
+                out[1 + i] = (2u << 29) | (R[i].finalBytes - 2);
+            continue;
+        }
         std::vector<uint8_t> pre((size_t)m * 4, 0);
         for (uint32_t j = 0; j < m; ++j)
             for (uint32_t b = 0; b < 4 && b < R[j].initBytes; ++b)
@@ -242,6 +265,8 @@ void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const
 void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
                           const uint32_t* results, const SolveItem* items, uint32_t count)
 {
+    if (noexec())
+        return;
     for (uint32_t it = 0; it < count; ++it) {
         const SolveDesc& sd = solves[items[it].solve];
         const uint32_t m = sd.m;

@@ -1,0 +1,92 @@
+"""API-level parity of the host control plane (CPU test double of the backend)
+against the upstream reference: randomised call sequences, argument
+validation, and the ARQ side channel."""
+import os
+
+import pytest
+
+import api_fuzz
+import scenario_lib as S
+from siamese_amd.binding import (SiameseLib, Success, InvalidInput, NeedMoreData,
+                                 DuplicateData)
+
+
+@pytest.fixture(scope="module")
+def ref():
+    if not os.path.exists(S.REF_LIB):
+        pytest.skip("oracle/_ref not built")
+    return SiameseLib(S.REF_LIB).init()
+
+
+@pytest.fixture(scope="module")
+def sim():
+    return SiameseLib(S.SIM_LIB).init()
+
+
+@pytest.mark.parametrize("seed", list(range(12)))
+def test_random_call_sequences(ref, sim, seed):
+    a = api_fuzz.run_isolated(S.REF_LIB, seed)
+    b = api_fuzz.normalise(api_fuzz.run(sim, seed))   # also checks recovered bytes
+    if a is None:
+        pytest.skip("the reference itself crashes on seed %d (use-after-free in its "
+                    "decoder under reordered input; DESIGN.md Deviations)" % seed)
+    assert api_fuzz.first_difference(a, b) is None
+
+
+def test_argument_validation(ref, sim):
+    for lib in (ref, sim):
+        L = lib.L
+        assert lib.encoder_add(None, None) == InvalidInput
+        assert lib.encode(None, None) == InvalidInput
+        assert lib.decoder_is_ready(None) == InvalidInput
+        assert lib.decoder_add_recovery(None, None) == InvalidInput
+        assert lib.encoder_remove_before(None, 0) == InvalidInput
+        enc = lib.Encoder()
+        assert enc.add_raw(b"")[0] == InvalidInput
+        assert enc.encode_raw()[0] == NeedMoreData
+        assert enc.remove_before(0x400000) == InvalidInput
+        dec = lib.Decoder()
+        assert dec.add_original(0x400000, b"x") == InvalidInput
+        assert dec.add_recovery(b"") == InvalidInput
+        assert dec.ack(limit=15)[0] == InvalidInput
+        assert dec.ack()[0] == NeedMoreData
+        assert dec.decode_raw()[0] == NeedMoreData
+        assert L is not None
+
+
+def test_duplicates_and_get(ref, sim):
+    outs = []
+    for lib in (ref, sim):
+        enc, dec = lib.Encoder(), lib.Decoder()
+        o = []
+        for i in range(10):
+            n = enc.add(bytes([i]) * (i + 1))
+            o.append(dec.add_original(n, bytes([i]) * (i + 1)))
+        o.append(dec.add_original(3, b"\x03" * 4))
+        o.append(enc.get(5))
+        o.append(dec.get(5))
+        o.append(dec.get(11))
+        o.append(dec.ack())
+        outs.append(o)
+    assert outs[0] == outs[1]
+    assert outs[0][10] == DuplicateData
+
+
+def test_ack_roundtrip_removes_window(ref, sim):
+    outs = []
+    for lib in (ref, sim):
+        enc, dec = lib.Encoder(), lib.Decoder()
+        o = []
+        for i in range(200):
+            n = enc.add(b"%05d" % i * 50)
+            if i % 7 != 3:
+                dec.add_original(n, b"%05d" % i * 50)
+        rc, msg = dec.ack()
+        o.append((rc, msg))
+        o.append(enc.ack(msg))
+        o.append(enc.retransmit())   # RTO (500 ms) not expired yet
+        o.append(enc.encode())
+        o.append(enc.stats()[:8])
+        outs.append(o)
+    assert outs[0] == outs[1]
+    assert outs[0][0][0] == Success

@@ -1,0 +1,61 @@
+"""CPU parity of the host control plane.
+
+* The reference build (oracle/_ref) reproduces the committed golden digests,
+  so the fixtures and the harness are pinned.
+* The control plane of libsiamese_amd, linked against the CPU test double of
+  its backend (tests/hostsim -- never shipped), reproduces the reference
+  digests through both the drop-in per-call API and the batched device API.
+The same comparisons run on the MI355X with the real HIP backend in
+test_gpu_parity.py.
+"""
+import os
+
+import pytest
+
+import golden
+import scenario_lib as S
+
+SMALL = ["smoke_C4x8", "C1", "C1var", "C2x64", "edge_tiny", "edge_var_block", "edge_heavy",
+         "edge_maxloss", "edge_lag"]
+
+
+def _check(name, results):
+    want = golden.load(name)
+    got = S.digests(results)
+    bad = [i for i, (a, b) in enumerate(zip(got, want["digests"])) if a != b]
+    assert not bad, "%s: %d/%d streams differ (first %s)" % (name, len(bad), len(got), bad[:5])
+    assert [int(r.status) for r in results] == want["status"]
+
+
+@pytest.mark.parametrize("name", SMALL + ["C3", "C4x256", "C2"])
+def test_reference_matches_golden(name, ref_available):
+    if not ref_available:
+        pytest.skip("oracle/_ref not built")
+    cfg = golden.config(name)
+    res, _, _ = S.run_capi(S.REF_LIB, cfg, threads=min(8, cfg.streams))
+    _check(name, res)
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_hostsim_dropin_matches_golden(name):
+    cfg = golden.config(name)
+    res, _, _ = S.run_capi(S.SIM_LIB, cfg)
+    _check(name, res)
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_hostsim_batch_matches_golden(name):
+    cfg = golden.config(name)
+    res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True)
+    _check(name, res)
+    assert rep.mismatches == 0
+
+
+def test_hostsim_batch_length_only_digest():
+    """hash_data=0 digests (used for the full-size GPU runs) also agree."""
+    cfg = S.replace(golden.config("C4x256"), streams=32, hash_data=0)
+    ref, _, _ = S.run_capi(S.REF_LIB, cfg, threads=8) if os.path.exists(S.REF_LIB) else (None,) * 3
+    res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True)
+    assert rep.mismatches == 0 and rep.checked > 0
+    if ref is not None:
+        assert S.digests(res) == S.digests(ref)
