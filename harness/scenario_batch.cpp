@@ -16,6 +16,7 @@
 //                          BatchReport* report)
 #include "scenario.h"
 #include "../include/siamese_gpu.h"
+#include "../siamese_amd/csrc/pool.h"
 
 #include <dlfcn.h>
 #include <algorithm>
@@ -31,6 +32,7 @@ struct BatchOptions
     uint32_t warmup;   ///< untimed repetitions before timing
     uint32_t verify;   ///< check every recovered packet's bytes (first run only)
     int32_t device;    ///< HIP device (-1 = current)
+    uint32_t threads;  ///< host threads driving streams (0 = default)
 };
 
 struct BatchReport
@@ -140,8 +142,8 @@ struct Shared
     size_t stride;
     bool hashData;
     bool verify;
-    std::vector<Request> cur, prev;
     uint64_t checked = 0, mismatches = 0;
+    std::unique_ptr<sgpu::WorkerPool> pool;
 };
 
 struct BatchCodec
@@ -150,6 +152,7 @@ struct BatchCodec
     SgpuEncoder enc = nullptr;
     SgpuDecoder dec = nullptr;
     std::vector<uint64_t>* log = nullptr;
+    std::vector<Request> cur, prev;   // tokens waiting for device bytes
 
     const void* dev_payload(unsigned id) const { return sh->payload + (size_t)id * sh->stride; }
 
@@ -201,7 +204,7 @@ struct BatchCodec
     uint64_t rec_token(const Rec& r)
     {
         if (sh->hashData)
-            sh->cur.push_back(Request{log, log->size(), r.pkt.DeviceData, r.bytes, 0, false, nullptr});
+            cur.push_back(Request{log, log->size(), r.pkt.DeviceData, r.bytes, 0, false, nullptr});
         return r.bytes;
     }
     uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok)
@@ -212,7 +215,7 @@ struct BatchCodec
         if (bytes != want || !data)
             *ok = false;
         else if (sh->hashData || sh->verify)
-            sh->cur.push_back(Request{log, log->size(), data, bytes, id, true, ok});
+            cur.push_back(Request{log, log->size(), data, bytes, id, true, ok});
         return bytes;
     }
     bool wants_yield_after_decode() const { return true; }
@@ -262,6 +265,18 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
     reqs.clear();
 }
 
+// fn(i) for i in [0, count), blocks of a few streams per pool task
+template <class F>
+void for_streams(Shared& sh, size_t count, const F& fn)
+{
+    constexpr size_t kBlock = 4;
+    sh.pool->run((count + kBlock - 1) / kBlock, [&](size_t b) {
+        const size_t end = std::min(count, (b + 1) * kBlock);
+        for (size_t i = b * kBlock; i < end; ++i)
+            fn(i);
+    });
+}
+
 int run_once(Shared& sh, StreamResult* results, uint64_t* rounds)
 {
     const Api& api = *sh.api;
@@ -269,45 +284,61 @@ int run_once(Shared& sh, StreamResult* results, uint64_t* rounds)
     const unsigned n = cfg->streams;
     std::vector<BatchCodec> codecs(n);
     std::unique_ptr<BatchStream[]> streams(new BatchStream[n]);
-    for (unsigned s = 0; s < n; ++s) {
+    for_streams(sh, n, [&](size_t s) {
         codecs[s].sh = &sh;
         codecs[s].enc = api.encoder_create();
         codecs[s].dec = api.decoder_create();
         codecs[s].log = &streams[s].log;
-        streams[s].init(cfg, &codecs[s], &results[s], cfg->first_stream + s);
+        streams[s].init(cfg, &codecs[s], &results[s], cfg->first_stream + (unsigned)s);
         if (!codecs[s].enc || !codecs[s].dec)
             streams[s].fail(2);
-    }
+    });
+    // requests of every stream that wait for device bytes
+    auto take = [&](bool prev) {
+        std::vector<Request> reqs;
+        for (BatchCodec& c : codecs) {
+            std::vector<Request>& q = prev ? c.prev : c.cur;
+            reqs.insert(reqs.end(), q.begin(), q.end());
+            q.clear();
+        }
+        return reqs;
+    };
     std::vector<unsigned> live(n);
     for (unsigned s = 0; s < n; ++s)
         live[s] = s;
     int rc = 0;
     while (!live.empty()) {
-        for (unsigned s : live) {
-            BatchStream& st = streams[s];
+        // Every live stream advances until it yields; streams are
+        // independent, so the host threads drive them concurrently.
+        for_streams(sh, live.size(), [&](size_t k) {
+            BatchStream& st = streams[live[k]];
             while (!st.done())
                 if (st.step())
                     break;
-        }
+        });
         // bytes produced by the previous flush are final now
-        resolve_requests(sh, sh.prev);
+        std::vector<Request> reqs = take(true);
+        resolve_requests(sh, reqs);
         if (api.flush() != 0) {
             rc = -3;
             break;
         }
         ++*rounds;
-        std::swap(sh.prev, sh.cur);
+        for (BatchCodec& c : codecs)
+            std::swap(c.prev, c.cur);
         live.erase(std::remove_if(live.begin(), live.end(),
                                   [&](unsigned s) { return streams[s].done(); }),
                    live.end());
     }
-    resolve_requests(sh, sh.prev);
-    resolve_requests(sh, sh.cur);
-    for (unsigned s = 0; s < n; ++s) {
+    std::vector<Request> reqs = take(true);
+    resolve_requests(sh, reqs);
+    reqs = take(false);
+    resolve_requests(sh, reqs);
+    for_streams(sh, n, [&](size_t s) {
         streams[s].finish();
         api.encoder_free(codecs[s].enc);
         api.decoder_free(codecs[s].dec);
-    }
+    });
     api.flush();
     return rc;
 }
@@ -391,6 +422,9 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
     for (unsigned r = 0; r < runs && rc == 0; ++r) {
         const bool timed = r >= opt->warmup;
         sh.verify = opt->verify && r == 0;
+        const unsigned threads = opt->threads ? opt->threads : sgpu::WorkerPool::default_threads();
+        if (!sh.pool || sh.pool->size() != threads)
+            sh.pool.reset(new sgpu::WorkerPool(threads));
         uint64_t rounds = 0;
         uint64_t e0[kEngineStats], e1[kEngineStats];
         api.engine_stats(e0);

@@ -17,6 +17,13 @@
     location and the completion point differ.  Recovered packets returned by
     sgpu_decode carry device pointers whose DataBytes are exact after the
     next sgpu_flush() (they read 0 until then).
+
+    Threading: instances may be driven from many host threads at once, each
+    instance by one thread at a time (handing a recovery packet to a decoder
+    also touches the encoder that produced it).  Per-instance calls take no
+    global lock.  sgpu_init, sgpu_flush, sgpu_submit, sgpu_gather, sgpu_h2d,
+    and sgpu_decoder_get on a packet whose length is still pending (it
+    flushes) must not run concurrently with any other call.
 */
 #ifndef SIAMESE_GPU_H
 #define SIAMESE_GPU_H

@@ -25,12 +25,15 @@ void be_h2d(void* dst, const void* src, size_t bytes);
 void be_d2h(void* dst, const void* src, size_t bytes);
 void be_memset(void* dst, int value, size_t bytes);
 
-void be_launch_ingest(const IngestDesc* descs, const IngestItem* items, uint32_t count);
+/// One wave per descriptor (count descriptors), looping over its tiles.
+void be_launch_ingest(const IngestDesc* descs, uint32_t count);
 void be_launch_exec(const GfOp* ops, const GfTerm* terms, const ExecItem* items, uint32_t count);
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
                             uint32_t* results, uint32_t count);
+/// maxRows: largest m among the solves this launch covers (sizes LDS staging).
 void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                          const uint32_t* results, const SolveItem* items, uint32_t count);
+                          const uint32_t* results, const SolveItem* items, uint32_t count,
+                          uint32_t maxRows);
 
 /// Block until all queued work has finished.  Returns false on a device fault.
 bool be_sync();

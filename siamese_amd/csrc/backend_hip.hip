@@ -82,114 +82,205 @@ __device__ __forceinline__ void st16(uint64_t addr, uint4 v)
 // ---------------------------------------------------------------------------
 // Ingest
 
-__global__ __launch_bounds__(64) void k_ingest(const IngestDesc* descs, const IngestItem* items)
+// One wave per symbol; lane L of each 1 KiB tile writes dst bytes
+// [16L, 16L+16).  The source is shifted by the 1-4 byte length prefix, so a
+// lane's 16 bytes straddle two aligned 16-byte source words: both are loaded
+// (coalesced) and recombined with v_alignbyte_b32.  The word offset and byte
+// shift are uniform per symbol, so the selection is a uniform branch, not a
+// register-indexed gather.  Only 16-byte-aligned words holding at least one
+// source byte are loaded (never past the source's last page).
+constexpr unsigned kIngestWaves = 4;
+
+__device__ __forceinline__ uint32_t pick(const uint32_t* w, unsigned q, unsigned r, unsigned k)
 {
-    const IngestItem it = items[blockIdx.x];
-    const IngestDesc d = descs[it.desc];
+    return __builtin_amdgcn_alignbyte(w[q + k + 1], w[q + k], r);
+}
+
+__global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* __restrict__ descs,
+                                                              uint32_t count)
+{
+    const uint32_t di = blockIdx.x * kIngestWaves + (threadIdx.x >> 6);
+    if (di >= count)
+        return;
+    const uint32_t lane = threadIdx.x & 63;
+    const IngestDesc d = descs[di];
     const uint32_t total = d.hdrLen + d.bytes;
-    const uint32_t p = it.tileBase + threadIdx.x * 16;
-    if (p >= total)
-        return;
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(d.src);
-    uint8_t* dst = reinterpret_cast<uint8_t*>(d.dst);
-    const uint64_t shifted = d.src - d.hdrLen; // address that lines up with dst
-    if (p >= d.hdrLen && p + 16 <= total && (shifted & 15u) == 0) {
-        st16((uint64_t)(dst + p), ld16(shifted + p));
-        return;
+    const uint64_t dst = d.dst;
+    // source address that lines up with dst byte 0
+    const uint64_t base = d.src - d.hdrLen;
+    const unsigned sh = (unsigned)(base & 15u);
+    const unsigned q = sh >> 2, r = sh & 3;
+    const uint64_t srcEnd = d.src + d.bytes;
+
+    for (uint32_t t = 0; t < total; t += kTileBytes) {
+        const uint32_t p = t + lane * 16;
+        if (p >= total)
+            break;
+        uint4 out;
+        if (p >= d.hdrLen && p + 16 <= total) {
+            const uint64_t a = (base + p) & ~(uint64_t)15;
+            const uint4 lo = ld16(a);
+            const uint4 hi = (sh != 0 && a + 16 < srcEnd) ? ld16(a + 16) : make_uint4(0, 0, 0, 0);
+            const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            switch (q) {   // wave-uniform
+            case 0:
+                out = make_uint4(pick(w, 0, r, 0), pick(w, 0, r, 1), pick(w, 0, r, 2), pick(w, 0, r, 3));
+                break;
+            case 1:
+                out = make_uint4(pick(w, 1, r, 0), pick(w, 1, r, 1), pick(w, 1, r, 2), pick(w, 1, r, 3));
+                break;
+            case 2:
+                out = make_uint4(pick(w, 2, r, 0), pick(w, 2, r, 1), pick(w, 2, r, 2), pick(w, 2, r, 3));
+                break;
+            default:
+                out = make_uint4(pick(w, 3, r, 0), pick(w, 3, r, 1), pick(w, 3, r, 2), pick(w, 3, r, 3));
+                break;
+            }
+        } else {
+            // the header lane and the last partial lane: byte by byte
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(d.src);
+            uint32_t v[4] = {0, 0, 0, 0};
+            for (uint32_t k = 0; k < 16; ++k) {
+                const uint32_t pk = p + k;
+                uint32_t b = 0;
+                if (pk < d.hdrLen)
+                    b = d.hdr[pk];
+                else if (pk < total)
+                    b = src[pk - d.hdrLen];
+                v[k >> 2] |= b << (8 * (k & 3));
+            }
+            out = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        st16(dst + p, out);
     }
-    const uint32_t end = p + 16 < total ? p + 16 : total;
-    for (uint32_t k = p; k < end; ++k)
-        dst[k] = k < d.hdrLen ? d.hdr[k] : src[k - d.hdrLen];
 }
 
 // ---------------------------------------------------------------------------
 // Executor
 
-__global__ __launch_bounds__(64) void k_exec(const GfOp* __restrict__ ops,
-                                             const GfTerm* __restrict__ terms,
-                                             const ExecItem* __restrict__ items)
+// One workgroup of kExecWaves waves per (instance segment, 1 KiB tile).  All
+// waves walk the segment's op list together; each op's terms are dealt
+// round-robin to the waves (wave w takes terms w, w+W, ...), every wave keeps
+// up to kExecDepth source loads in flight, and the partial sums meet in LDS.
+// Wave 0 then merges the destination's kept prefix/tail and stores; a
+// barrier orders the store before any later op of the segment reads it
+// (stores from one CU are visible to the CU's other waves after the
+// workgroup-scope fence of __syncthreads on gfx950).
+constexpr unsigned kExecWaves = 4;
+constexpr unsigned kExecDepth = 8;
+constexpr unsigned kExecSolo = 4;   // ops with <= this many terms run on wave 0 alone
+
+__device__ __forceinline__ uint4 term_value(uint4 x, uint32_t p, uint32_t len, uint32_t coeff)
 {
-    const ExecItem it = items[blockIdx.x];
-    const uint32_t p = it.tileBase + threadIdx.x * 16;
+    if (p + 16 > len)
+        x = mask16(x, (int)len - (int)p);
+    if (coeff != 1)
+        x = gf_mul16(x, coeff);
+    return x;
+}
 
-    for (uint32_t oi = 0; oi < it.opCount; ++oi) {
-        const GfOp op = ops[it.opBegin + oi];
-        if (op.kind == OP_LITERAL) {
-            const uint32_t a = op.n, b = op.n + op.valid;
-            if (b <= p || a >= p + 16)
-                continue;
-            uint8_t* dst = reinterpret_cast<uint8_t*>(op.dst);
-            for (uint32_t k = (a > p ? a : p); k < b && k < p + 16; ++k)
-                dst[k] = op.lit[k - a];
-            continue;
-        }
-        if (p >= op.n)
-            continue;
-
-        uint4 acc0 = make_uint4(0, 0, 0, 0);
-        uint4 acc1 = make_uint4(0, 0, 0, 0);
-        const GfTerm* t = terms + op.termBegin;
-        const uint32_t nt = op.termCount;
-        uint32_t k = 0;
-        // Issue loads for 4 terms at a time so several HBM requests are in
-        // flight per lane before the first XOR consumes one.
-        for (; k + 4 <= nt; k += 4) {
-            GfTerm tt[4];
-            uint4 v[4];
+// Accumulate terms k0, k0+stride, ... of one op into acc0/acc1.
+__device__ __forceinline__ void gather_terms(const GfTerm* __restrict__ t, uint32_t nt, uint32_t k0,
+                                             uint32_t stride, uint32_t p, uint4& acc0, uint4& acc1)
+{
+    for (uint32_t k = k0; k < nt; k += stride * kExecDepth) {
+        GfTerm tt[kExecDepth];
+        uint4 v[kExecDepth];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                tt[u] = t[k + u];
-                v[u] = p < tt[u].len ? ld16(tt[u].src + p) : make_uint4(0, 0, 0, 0);
+        for (unsigned u = 0; u < kExecDepth; ++u) {
+            const uint32_t idx = k + u * stride;
+            if (idx < nt) {   // wave-uniform
+                tt[u] = t[idx];
+                // lanes past the term's end load the term's first line (always
+                // mapped) and mask it away, so no load sits behind a branch
+                v[u] = ld16(tt[u].src + (p < tt[u].len ? p : 0));
             }
+        }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                uint4 x = v[u];
-                if (p + 16 > tt[u].len)
-                    x = mask16(x, (int)tt[u].len - (int)p);
-                if (tt[u].coeff != 1)
-                    x = gf_mul16(x, tt[u].coeff);
+        for (unsigned u = 0; u < kExecDepth; ++u) {
+            const uint32_t idx = k + u * stride;
+            if (idx < nt) {
+                const uint4 x = term_value(v[u], p, tt[u].len, tt[u].coeff);
                 if (tt[u].acc)
                     acc1 = xor16(acc1, x);
                 else
                     acc0 = xor16(acc0, x);
             }
         }
-        for (; k < nt; ++k) {
-            const GfTerm tm = t[k];
-            if (p >= tm.len)
-                continue;
-            uint4 x = ld16(tm.src + p);
-            if (p + 16 > tm.len)
-                x = mask16(x, (int)tm.len - (int)p);
-            if (tm.coeff != 1)
-                x = gf_mul16(x, tm.coeff);
-            if (tm.acc)
-                acc1 = xor16(acc1, x);
-            else
-                acc0 = xor16(acc0, x);
+    }
+}
+
+__global__ __launch_bounds__(64 * kExecWaves) void k_exec(const GfOp* __restrict__ ops,
+                                                          const GfTerm* __restrict__ terms,
+                                                          const ExecItem* __restrict__ items)
+{
+    __shared__ uint4 part[kExecWaves - 1][64];
+    const ExecItem it = items[blockIdx.x];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t p = it.tileBase + lane * 16;
+
+    for (uint32_t oi = 0; oi < it.opCount; ++oi) {
+        const GfOp op = ops[it.opBegin + oi];
+        if (op.kind == OP_LITERAL) {
+            if (wave == 0) {
+                const uint32_t a = op.n, b = op.n + op.valid;
+                if (b > p && a < p + 16) {
+                    uint8_t* dst = reinterpret_cast<uint8_t*>(op.dst);
+                    for (uint32_t k = (a > p ? a : p); k < b && k < p + 16; ++k)
+                        dst[k] = op.lit[k - a];
+                }
+            }
+            __syncthreads();
+            continue;
         }
+        if (it.tileBase >= op.n)
+            continue;   // op does not reach this tile (uniform over the workgroup)
+
+        const GfTerm* t = terms + op.termBegin;
+        const uint32_t nt = op.termCount;
+        const bool solo = nt <= kExecSolo;
+        uint4 acc0 = make_uint4(0, 0, 0, 0);
+        uint4 acc1 = make_uint4(0, 0, 0, 0);
+        if (!solo || wave == 0)
+            gather_terms(t, nt, solo ? 0 : wave, solo ? 1 : kExecWaves, p, acc0, acc1);
         if (op.mix > 1)
             acc1 = gf_mul16(acc1, op.mix);
         uint4 out = xor16(acc0, acc1);
-        if (p < op.valid) {
-            uint4 prior = ld16(op.dst + p);
-            if (p + 16 > op.valid)
-                prior = mask16(prior, (int)op.valid - (int)p);
-            out = xor16(out, prior);
+        if (!solo) {
+            if (wave != 0)
+                part[wave - 1][lane] = out;
+            __syncthreads();
         }
-        if (p + 16 > op.n) {
-            // keep dst bytes at and beyond n
-            const int nb = (int)op.n - (int)p;
-            const uint4 old = ld16(op.dst + p);
-            const uint4 keep = make_uint4(~byte_mask(nb), ~byte_mask(nb - 4), ~byte_mask(nb - 8),
-                                          ~byte_mask(nb - 12));
-            out = mask16(out, nb);
-            out.x |= old.x & keep.x;
-            out.y |= old.y & keep.y;
-            out.z |= old.z & keep.z;
-            out.w |= old.w & keep.w;
+        if (wave == 0) {
+            if (!solo) {
+#pragma unroll
+                for (unsigned w = 0; w + 1 < kExecWaves; ++w)
+                    out = xor16(out, part[w][lane]);
+            }
+            if (p < op.n) {
+                if (p < op.valid) {
+                    uint4 prior = ld16(op.dst + p);
+                    if (p + 16 > op.valid)
+                        prior = mask16(prior, (int)op.valid - (int)p);
+                    out = xor16(out, prior);
+                }
+                if (p + 16 > op.n) {
+                    // keep dst bytes at and beyond n
+                    const int nb = (int)op.n - (int)p;
+                    const uint4 old = ld16(op.dst + p);
+                    const uint4 keep = make_uint4(~byte_mask(nb), ~byte_mask(nb - 4),
+                                                  ~byte_mask(nb - 8), ~byte_mask(nb - 12));
+                    out = mask16(out, nb);
+                    out.x |= old.x & keep.x;
+                    out.y |= old.y & keep.y;
+                    out.z |= old.z & keep.z;
+                    out.w |= old.w & keep.w;
+                }
+                st16(op.dst + p, out);
+            }
         }
-        st16(op.dst + p, out);
+        __syncthreads();
     }
 }
 
@@ -301,18 +392,105 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
         out[0] = ok;
 }
 
-__global__ __launch_bounds__(64) void k_solve_main(const SolveDesc* __restrict__ solves,
-                                                   const SolveRow* __restrict__ rows,
-                                                   const uint8_t* __restrict__ coef,
-                                                   const uint32_t* __restrict__ results,
-                                                   const SolveItem* __restrict__ items)
+// k_solve_main: one workgroup of kSolveWaves waves per (solve, 1 KiB tile).
+//
+// LDS path (m * 1 KiB fits the launch's dynamic LDS): the tile of all m rows
+// is staged in LDS once (bytes past each row's initial length read as zero:
+// the reference's zero-padded growth), wave w owns rows j = w (mod W), and
+// both triangular sweeps run in LDS with one barrier per pivot step.  Each
+// recovered row is stored once, right after its back-substitution step;
+// rows left unsolved (a corrupt length prefix) are stored at the end.  HBM
+// traffic is one read and one write of each row instead of ~m of each.
+//
+// Global path (larger m): wave 0 alone, rows updated in place in HBM.
+constexpr unsigned kSolveWaves = 4;
+constexpr unsigned kSolveLdsMaxRows = 120;
+
+__device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow* __restrict__ R,
+                               const uint8_t* __restrict__ C, const uint32_t* __restrict__ res,
+                               uint32_t tileBase)
 {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t p = tileBase + lane * 16;
+
+    for (uint32_t j = wave; j < m; j += kSolveWaves) {
+        const uint32_t ib = R[j].initBytes;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (p < ib) {
+            v = ld16(R[j].buf + p);
+            if (p + 16 > ib)
+                v = mask16(v, (int)ib - (int)p);
+        }
+        X[j * 64 + lane] = v;
+    }
+    __syncthreads();
+
+    // MultiplyLowerTriangle in pivot order (reference SiameseDecoder.cpp:1065-1104)
+    for (uint32_t i = 0; i + 1 < m; ++i) {
+        const uint32_t L = R[i].lowerLen;
+        if (tileBase >= L)
+            continue;   // uniform: row i contributes nothing to this tile
+        uint4 src = X[i * 64 + lane];
+        if (p + 16 > L)
+            src = mask16(src, (int)L - (int)p);
+        const uint32_t first = i + 1 + ((wave + kSolveWaves - (i + 1) % kSolveWaves) % kSolveWaves);
+        for (uint32_t j = first; j < m; j += kSolveWaves) {
+            const uint32_t y = C[(size_t)j * m + i];
+            if (y)
+                X[j * 64 + lane] = xor16(X[j * 64 + lane], gf_mul16(src, y));
+        }
+        __syncthreads();
+    }
+
+    // BackSubstitution from the right-most column (reference :1106-1238)
+    const uint32_t ok = res[0];
+    uint32_t done = 0;
+    for (int i = (int)m - 1; i >= 0 && done < ok; --i, ++done) {
+        const uint32_t w = res[1 + i];
+        const uint32_t bb = (w >> 29) + (w & kSolveLengthMask);
+        const uint32_t y = C[(size_t)i * m + i];
+        uint4 x = gf_mul16(X[i * 64 + lane], c_inv[y]);
+        x = mask16(x, (int)bb - (int)p); // zero beyond the recovered length
+        if ((uint32_t)i % kSolveWaves == wave && p < R[i].finalBytes)
+            st16(R[i].buf + p, x);
+        if (tileBase < bb) {
+            const uint32_t first = wave;
+            for (uint32_t j = first; j < (uint32_t)i; j += kSolveWaves) {
+                const uint32_t c = C[(size_t)j * m + i];
+                if (!c)
+                    continue;
+                const uint32_t ab = bb < R[j].finalBytes ? bb : R[j].finalBytes;
+                const uint4 xs = mask16(x, (int)ab - (int)p);
+                X[j * 64 + lane] = xor16(X[j * 64 + lane], gf_mul16(xs, c));
+            }
+        }
+        __syncthreads();
+    }
+    // rows the back-substitution did not reach
+    for (uint32_t j = wave; j + done < m; j += kSolveWaves)
+        if (p < R[j].finalBytes)
+            st16(R[j].buf + p, X[j * 64 + lane]);
+}
+
+__global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
+    const SolveDesc* __restrict__ solves, const SolveRow* __restrict__ rows,
+    const uint8_t* __restrict__ coef, const uint32_t* __restrict__ results,
+    const SolveItem* __restrict__ items, uint32_t ldsRows)
+{
+    extern __shared__ uint4 X[];
     const SolveItem it = items[blockIdx.x];
     const SolveDesc sd = solves[it.solve];
     const uint32_t m = sd.m;
     const SolveRow* R = rows + sd.rowBegin;
     const uint8_t* C = coef + sd.coefOffset;
     const uint32_t* res = results + sd.result;
+    if (m <= ldsRows) {
+        solve_tile_lds(X, m, R, C, res, it.tileBase);
+        return;
+    }
+    if (threadIdx.x >= 64)
+        return;
     const uint32_t p = it.tileBase + threadIdx.x * 16;
     if (p >= sd.maxBytes)
         return;
@@ -384,6 +562,7 @@ namespace {
 hipStream_t g_stream = nullptr;
 bool g_ready = false;
 bool g_timing = false;
+uint32_t g_solveLdsRows = 64;   // raised at init if the device grants more dynamic LDS
 double g_execMs = 0, g_totalMs = 0;
 
 struct EvPair
@@ -400,8 +579,8 @@ EvPair take_events(bool exec)
         e = g_evFree.back();
         g_evFree.pop_back();
     } else {
-        hipEventCreate(&e.a);
-        hipEventCreate(&e.b);
+        (void)hipEventCreate(&e.a);
+        (void)hipEventCreate(&e.b);
     }
     e.exec = exec;
     return e;
@@ -415,13 +594,13 @@ struct Timed
     {
         if (on) {
             ev = take_events(exec);
-            hipEventRecord(ev.a, g_stream);
+            (void)hipEventRecord(ev.a, g_stream);
         }
     }
     ~Timed()
     {
         if (on) {
-            hipEventRecord(ev.b, g_stream);
+            (void)hipEventRecord(ev.b, g_stream);
             g_evUsed.push_back(ev);
         }
     }
@@ -450,7 +629,7 @@ bool be_init(int device, const char** err)
         return false;
     }
     int cur = 0;
-    hipGetDevice(&cur);
+    (void)hipGetDevice(&cur);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, cur) != hipSuccess) {
         *err = "hipGetDeviceProperties failed";
@@ -484,6 +663,10 @@ bool be_init(int device, const char** err)
     }
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_perm), perm, sizeof(perm)), "hipMemcpyToSymbol(perm)");
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_inv), g_gf.inv, 256), "hipMemcpyToSymbol(inv)");
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_main),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(kSolveLdsMaxRows * 64 * sizeof(uint4))) == hipSuccess)
+        g_solveLdsRows = kSolveLdsMaxRows;
     if (hipDeviceSynchronize() != hipSuccess) {
         *err = "device synchronisation failed during init";
         return false;
@@ -505,7 +688,7 @@ void* be_dev_alloc(size_t bytes)
 void be_dev_free(void* p)
 {
     if (p)
-        hipFree(p);
+        (void)hipFree(p);
 }
 
 void* be_host_alloc(size_t bytes)
@@ -519,7 +702,7 @@ void* be_host_alloc(size_t bytes)
 void be_host_free(void* p)
 {
     if (p)
-        hipHostFree(p);
+        (void)hipHostFree(p);
 }
 
 void be_h2d(void* dst, const void* src, size_t bytes)
@@ -537,16 +720,19 @@ void be_memset(void* dst, int value, size_t bytes)
     check(hipMemsetAsync(dst, value, bytes, g_stream), "memset");
 }
 
-void be_launch_ingest(const IngestDesc* descs, const IngestItem* items, uint32_t count)
+void be_launch_ingest(const IngestDesc* descs, uint32_t count)
 {
+    if (count == 0)
+        return;
     Timed t(false);
-    hipLaunchKernelGGL(k_ingest, dim3(count), dim3(64), 0, g_stream, descs, items);
+    hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves),
+                       dim3(64 * kIngestWaves), 0, g_stream, descs, count);
 }
 
 void be_launch_exec(const GfOp* ops, const GfTerm* terms, const ExecItem* items, uint32_t count)
 {
     Timed t(true);
-    hipLaunchKernelGGL(k_exec, dim3(count), dim3(64), 0, g_stream, ops, terms, items);
+    hipLaunchKernelGGL(k_exec, dim3(count), dim3(64 * kExecWaves), 0, g_stream, ops, terms, items);
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
@@ -558,11 +744,16 @@ void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const
 }
 
 void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                          const uint32_t* results, const SolveItem* items, uint32_t count)
+                          const uint32_t* results, const SolveItem* items, uint32_t count,
+                          uint32_t maxRows)
 {
+    if (count == 0)
+        return;
     Timed t(false);
-    hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64), 0, g_stream, solves, rows, coef,
-                       results, items);
+    const uint32_t ldsRows = maxRows < g_solveLdsRows ? maxRows : g_solveLdsRows;
+    hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
+                       (size_t)ldsRows * 64 * sizeof(uint4), g_stream, solves, rows, coef, results,
+                       items, ldsRows);
 }
 
 bool be_sync()
@@ -574,7 +765,7 @@ bool be_sync()
     }
     for (const EvPair& ev : g_evUsed) {
         float ms = 0;
-        hipEventElapsedTime(&ms, ev.a, ev.b);
+        (void)hipEventElapsedTime(&ms, ev.a, ev.b);
         g_totalMs += ms;
         if (ev.exec)
             g_execMs += ms;

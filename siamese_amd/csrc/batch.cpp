@@ -57,7 +57,6 @@ SIAMESE_EXPORT SgpuEncoder sgpu_encoder_create(void)
 {
     if (!g_batchReady)
         return nullptr;
-    Lock lock(Engine::global()->mutex());
     return reinterpret_cast<SgpuEncoder>(new (std::nothrow) BatchEncoder);
 }
 
@@ -65,7 +64,6 @@ SIAMESE_EXPORT void sgpu_encoder_free(SgpuEncoder encoder)
 {
     if (!encoder)
         return;
-    Lock lock(Engine::global()->mutex());
     delete BE(encoder);
 }
 
@@ -74,7 +72,6 @@ SIAMESE_EXPORT SiameseResult sgpu_encoder_add(SgpuEncoder encoder, const void* d
 {
     if (!encoder || !deviceData || bytes == 0 || bytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     SiameseOriginalPacket p;
     p.PacketNum = 0;
     p.Data = (const unsigned char*)deviceData;
@@ -89,7 +86,6 @@ SIAMESE_EXPORT SiameseResult sgpu_encoder_remove_before(SgpuEncoder encoder, uns
 {
     if (!encoder || firstKept > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     BE(encoder)->core.remove_before(firstKept);
     return Siamese_Success;
 }
@@ -98,7 +94,6 @@ SIAMESE_EXPORT SiameseResult sgpu_encode(SgpuEncoder encoder, SgpuRecoveryPacket
 {
     if (!encoder || !out)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     EncoderCore& core = BE(encoder)->core;
     EncodeOut o;
     const SiameseResult r = core.encode(o);
@@ -119,7 +114,6 @@ SIAMESE_EXPORT SgpuDecoder sgpu_decoder_create(void)
 {
     if (!g_batchReady)
         return nullptr;
-    Lock lock(Engine::global()->mutex());
     return reinterpret_cast<SgpuDecoder>(new (std::nothrow) BatchDecoder);
 }
 
@@ -127,7 +121,6 @@ SIAMESE_EXPORT void sgpu_decoder_free(SgpuDecoder decoder)
 {
     if (!decoder)
         return;
-    Lock lock(Engine::global()->mutex());
     delete BD(decoder);
 }
 
@@ -137,7 +130,6 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original(SgpuDecoder decoder, unsi
     if (!decoder || !deviceData || bytes == 0 || bytes > SIAMESE_MAX_PACKET_BYTES ||
         packetNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     SiameseOriginalPacket p;
     p.PacketNum = packetNum;
     p.Data = (const unsigned char*)deviceData;
@@ -150,7 +142,6 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_add_recovery(SgpuDecoder decoder, cons
     if (!decoder || !packet || !packet->DeviceData || packet->DataBytes == 0 ||
         packet->FooterBytes == 0 || packet->FooterBytes > 8 || packet->FooterBytes >= packet->DataBytes)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     DeviceRecovery r;
     r.data = (uint64_t)(uintptr_t)packet->DeviceData;
     r.bytes = packet->DataBytes;
@@ -165,7 +156,6 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_is_ready(SgpuDecoder decoder)
 {
     if (!decoder)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     return BD(decoder)->core.is_ready();
 }
 
@@ -174,7 +164,6 @@ SIAMESE_EXPORT SiameseResult sgpu_decode(SgpuDecoder decoder, SiameseOriginalPac
 {
     if (!decoder || (!packetsOut != !countOut))
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     return BD(decoder)->core.decode(packetsOut, countOut);
 }
 
@@ -182,7 +171,6 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_get(SgpuDecoder decoder, SiameseOrigin
 {
     if (!decoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     return BD(decoder)->core.get(*packet);
 }
 
@@ -190,7 +178,6 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_has(SgpuDecoder decoder, unsigned pack
 {
     if (!decoder || packetNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
     return BD(decoder)->core.has(packetNum) ? Siamese_Success : Siamese_NeedMoreData;
 }
 
@@ -253,7 +240,7 @@ SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* t
 
 SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out10)
 {
-    const Engine::Stats& s = Engine::global()->stats;
+    const EngineStats s = Engine::global()->stats();
     uint64_t* out9 = out10;
     out10[9] = s.solveBytes;
     out9[0] = s.flushes;

@@ -1242,7 +1242,7 @@ SiameseResult DecoderCore::solve_and_substitute()
     for (unsigned j = 0; j < m; ++j)
         std::memcpy(coef.data() + (size_t)j * m, mrow(pivots_[j]), m);
 
-    const uint32_t base = prog_.solve(desc, coef, maxBytes);
+    const uint32_t base = prog_.solve(desc, coef.data(), maxBytes);
 
     // Host side of BackSubstitution: swap buffers into the window, record
     // the outputs (lengths patched in resolve()).
@@ -1277,7 +1277,7 @@ SiameseResult DecoderCore::solve_and_substitute()
     pendingSolves_++;
     Engine* eng = eng_;
     std::vector<unsigned> finals(len.begin(), len.end());
-    eng_->on_complete([this, alive, fixes, base, m, serial, coef, finals, eng](const uint32_t* results) {
+    prog_.on_complete([this, alive, fixes, base, m, serial, coef, finals, eng](const uint32_t* results) {
         // Back-substitution bytes of the reference (:1131-1212) need the
         // recovered lengths, so they are counted once those are known.
         const unsigned ok = results[base];

@@ -1,6 +1,7 @@
 // engine.cpp -- arena, programs and flush (see engine.h).
 #include "engine.h"
 #include "backend.h"
+#include "pool.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -8,36 +9,86 @@
 
 namespace sgpu {
 
+void EngineStats::add(const EngineStats& o)
+{
+    flushes += o.flushes;
+    launches += o.launches;
+    ops += o.ops;
+    terms += o.terms;
+    solves += o.solves;
+    ingests += o.ingests;
+    uploadBytes += o.uploadBytes;
+    refOpBytes += o.refOpBytes;
+    outBytes += o.outBytes;
+    solveBytes += o.solveBytes;
+}
+
 // ---------------------------------------------------------------------------
 // Program
 
 Program::~Program()
 {
-    if (eng_)
-        eng_->forget(this);
+    if (!shard_)
+        return;
+    // The instance goes away with work still queued (e.g. an encoder freed
+    // right after its last recovery packet was handed to a decoder, whose
+    // copy op lives in this program).  The queued ops still run: hand them
+    // to an orphan program the engine deletes after the next flush.  The
+    // buffers they touch were released by the instance and are not reused
+    // before that flush completes.
+    Program* orphan = new Program(eng_, group_);
+    orphan->shard_ = shard_;
+    orphan->resultWords_ = resultWords_;
+    orphan->nsegs_ = nsegs_;
+    orphan->segs_.swap(segs_);
+    orphan->solves_.swap(solves_);
+    orphan->callbacks_.swap(callbacks_);
+    orphan->group_ = group_ | 2;   // bit 1: delete after flush
+    std::lock_guard<std::mutex> g(shard_->mu);
+    auto it = std::find(shard_->dirty.begin(), shard_->dirty.end(), this);
+    if (it != shard_->dirty.end())
+        *it = orphan;
 }
 
-void Program::touch()
+void Program::attach()
 {
-    if (!dirty_) {
-        dirty_ = true;
-        eng_->register_dirty(this);
-    }
+    Shard& s = eng_->shard();
+    shard_ = &s;
+    std::lock_guard<std::mutex> g(s.mu);
+    s.dirty.push_back(this);
 }
 
-Program::Segment& Program::seg()
+void Program::new_segment()
 {
-    if (segs_.empty())
+    if (nsegs_ == segs_.size())
         segs_.emplace_back();
-    return segs_.back();
+    Segment& s = segs_[nsegs_++];
+    s.ops.clear();
+    s.terms.clear();
+    s.maxExtent = 0;
+}
+
+void Program::reset_after_flush()
+{
+    for (size_t k = 0; k < nsegs_; ++k) {
+        segs_[k].ops.clear();
+        segs_[k].terms.clear();
+        segs_[k].maxExtent = 0;
+    }
+    nsegs_ = 0;
+    solves_.clear();
+    callbacks_.clear();
+    resultWords_ = 0;
+    shard_ = nullptr;
 }
 
 void Program::lc_begin(uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix)
 {
     touch();
-    Segment& s = seg();
+    if (nsegs_ == 0)
+        new_segment();
+    Segment& s = segs_[nsegs_ - 1];
     GfOp op;
-    std::memset(&op, 0, sizeof(op));
     op.dst = dst;
     op.n = n;
     op.valid = valid < n ? valid : n;
@@ -46,32 +97,12 @@ void Program::lc_begin(uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix)
     op.termBegin = (uint32_t)s.terms.size();
     op.termCount = 0;
     s.ops.push_back(op);
-    open_ = true;
-}
-
-void Program::lc_term(uint64_t src, uint32_t len, uint8_t coeff, uint8_t acc)
-{
-    Segment& s = seg();
-    GfOp& op = s.ops.back();
-    if (len > op.n)
-        len = op.n;
-    if (len == 0 || coeff == 0)
-        return;
-    GfTerm t;
-    t.src = src;
-    t.len = len;
-    t.coeff = coeff;
-    t.acc = acc;
-    t.pad = 0;
-    s.terms.push_back(t);
-    ++op.termCount;
 }
 
 void Program::lc_end()
 {
-    Segment& s = seg();
+    Segment& s = segs_[nsegs_ - 1];
     GfOp& op = s.ops.back();
-    open_ = false;
     // An op that keeps all of dst and adds nothing is a no-op.
     if (op.termCount == 0 && op.valid >= op.n) {
         s.ops.pop_back();
@@ -121,7 +152,9 @@ void Program::literal(uint64_t dst, uint32_t offset, const uint8_t* bytes, uint3
     if (len == 0)
         return;
     touch();
-    Segment& s = seg();
+    if (nsegs_ == 0)
+        new_segment();
+    Segment& s = segs_[nsegs_ - 1];
     GfOp op;
     std::memset(&op, 0, sizeof(op));
     op.dst = dst;
@@ -150,35 +183,44 @@ void Program::ingest_device(const DevBuf& dst, uint64_t src, uint32_t bytes, con
     d.bytes = bytes;
     d.hdrLen = hdrLen;
     std::memcpy(d.hdr, hdr, hdrLen);
-    eng_->add_ingest(d, (uint32_t)-1);
+    eng_->add_ingest(d, -1);
 }
 
-uint32_t Program::solve(const std::vector<SolveRow>& rows, const std::vector<uint8_t>& coef,
-                        uint32_t maxBytes)
+uint32_t Program::solve(const std::vector<SolveRow>& rows, const uint8_t* coef, uint32_t maxBytes)
 {
     touch();
-    seg(); // make sure the segment preceding this solve exists
+    if (nsegs_ == 0)
+        new_segment(); // the segment preceding this solve
     PendingSolve ps;
     std::memset(&ps.desc, 0, sizeof(ps.desc));
     ps.desc.m = (uint32_t)rows.size();
     ps.desc.maxBytes = maxBytes;
-    ps.desc.result = eng_->reserve_results(ps.desc.m + 1);
+    ps.desc.result = resultWords_;
+    resultWords_ += ps.desc.m + 1;
     ps.rows = rows;
-    ps.coef = coef;
+    ps.coef.assign(coef, coef + rows.size() * rows.size());
     const uint32_t r = ps.desc.result;
     solves_.push_back(std::move(ps));
-    segs_.emplace_back(); // ops after the solve go to the next segment
+    new_segment(); // ops after the solve go to the next segment
     return r;
 }
 
+void Program::on_complete(Completion fn)
+{
+    touch();
+    callbacks_.push_back(std::move(fn));
+}
+
 // ---------------------------------------------------------------------------
-// Engine: arena
+// Engine: shards, arena, statistics
 
 Engine* Engine::global()
 {
     static Engine e;
     return &e;
 }
+
+Engine::~Engine() = default;
 
 bool Engine::init(int device, const char** err)
 {
@@ -190,7 +232,56 @@ bool Engine::init(int device, const char** err)
     return true;
 }
 
-static uint32_t round_cap(uint32_t bytes)
+Shard& Engine::shard()
+{
+    thread_local Engine* owner = nullptr;
+    thread_local Shard* mine = nullptr;
+    if (owner != this) {
+        std::lock_guard<std::mutex> g(shardsMu_);
+        shards_.emplace_back(new Shard);
+        mine = shards_.back().get();
+        owner = this;
+    }
+    return *mine;
+}
+
+WorkerPool& Engine::pool()
+{
+    if (!pool_)
+        pool_.reset(new WorkerPool(WorkerPool::default_threads()));
+    return *pool_;
+}
+
+void Engine::account(uint64_t opBytes, uint64_t outBytes, bool inSolve)
+{
+    EngineStats& s = shard().stats;
+    s.refOpBytes += opBytes;
+    s.outBytes += outBytes;
+    if (inSolve)
+        s.solveBytes += opBytes + outBytes;
+}
+
+EngineStats Engine::stats() const
+{
+    EngineStats t = flushStats_;
+    std::lock_guard<std::mutex> g(shardsMu_);
+    for (const auto& s : shards_)
+        t.add(s->stats);
+    return t;
+}
+
+uint64_t Engine::bytes_in_use() const
+{
+    int64_t t = 0;
+    std::lock_guard<std::mutex> g(shardsMu_);
+    for (const auto& s : shards_)
+        t += s->inUse;
+    return (uint64_t)t;
+}
+
+namespace {
+
+uint32_t round_cap(uint32_t bytes)
 {
     if (bytes < 64)
         return 64;
@@ -201,102 +292,101 @@ static uint32_t round_cap(uint32_t bytes)
     return (bytes + 65535) & ~65535u;
 }
 
-std::vector<uint8_t*>* Engine::free_list(uint32_t cap)
+size_t cap_class(uint32_t cap)
 {
-    auto it = std::lower_bound(freeLists_.begin(), freeLists_.end(), cap,
-                               [](const std::pair<uint32_t, std::vector<uint8_t*>>& a, uint32_t c) {
-                                   return a.first < c;
-                               });
-    if (it == freeLists_.end() || it->first != cap)
-        it = freeLists_.insert(it, std::make_pair(cap, std::vector<uint8_t*>()));
-    return &it->second;
+    if (cap <= 4096)
+        return cap / 64 - 1;                 // 0..63
+    if (cap <= 131072)
+        return 64 + cap / 1024 - 5;          // 64..187
+    return 188 + cap / 65536 - 3;
+}
+
+} // namespace
+
+uint8_t* Engine::carve(uint32_t cap)
+{
+    const size_t kChunk = 64u << 20;
+    std::lock_guard<std::mutex> g(arenaMu_);
+    if (cap > kChunk / 4)
+        return (uint8_t*)be_dev_alloc(cap);
+    if (chunks_.empty() || chunks_.back().used + cap > chunks_.back().size) {
+        uint8_t* base = (uint8_t*)be_dev_alloc(kChunk);
+        if (!base)
+            return nullptr;
+        chunks_.push_back(Chunk{base, kChunk, 0});
+    }
+    Chunk& c = chunks_.back();
+    uint8_t* p = c.base + c.used;
+    c.used += cap;
+    return p;
 }
 
 DevBuf Engine::alloc(uint32_t bytes)
 {
     DevBuf b;
     const uint32_t cap = round_cap(bytes);
-    std::vector<uint8_t*>* fl = free_list(cap);
-    if (!fl->empty()) {
-        b.ptr = fl->back();
-        fl->pop_back();
-        b.cap = cap;
-        inUse_ += cap;
-        return b;
-    }
-    const size_t kChunk = 64u << 20;
-    if (cap > kChunk / 4) {
-        b.ptr = (uint8_t*)be_dev_alloc(cap);
+    Shard& s = shard();
+    const size_t cls = cap_class(cap);
+    if (cls < s.freeLists.size() && !s.freeLists[cls].empty()) {
+        b.ptr = s.freeLists[cls].back();
+        s.freeLists[cls].pop_back();
+    } else {
+        b.ptr = carve(cap);
         if (!b.ptr)
             return DevBuf();
-        b.cap = cap;
-        inUse_ += cap;
-        return b;
     }
-    if (chunks_.empty() || chunks_.back().used + cap > chunks_.back().size) {
-        uint8_t* base = (uint8_t*)be_dev_alloc(kChunk);
-        if (!base)
-            return DevBuf();
-        chunks_.push_back(Chunk{base, kChunk, 0});
-    }
-    Chunk& c = chunks_.back();
-    b.ptr = c.base + c.used;
     b.cap = cap;
-    c.used += cap;
-    inUse_ += cap;
+    s.inUse += cap;
     return b;
 }
 
 void Engine::release(DevBuf& b)
 {
     if (b.ptr) {
-        pendingFree_.push_back(b);
-        inUse_ -= b.cap;
+        Shard& s = shard();
+        s.pendingFree.push_back(b);
+        s.inUse -= b.cap;
     }
     b = DevBuf();
-}
-
-void Engine::forget(Program* p)
-{
-    auto it = std::find(dirty_.begin(), dirty_.end(), p);
-    if (it != dirty_.end())
-        dirty_.erase(it);
 }
 
 void Engine::download(void* hostDst, uint64_t devSrc, uint32_t bytes)
 {
     if (bytes)
-        downloads_.push_back(Download{hostDst, devSrc, bytes});
-}
-
-void Engine::on_complete(std::function<void(const uint32_t*)> fn)
-{
-    callbacks_.push_back(std::move(fn));
+        shard().downloads.push_back(Shard::Download{hostDst, devSrc, bytes});
 }
 
 void Engine::stage_host_ingest(const DevBuf& dst, const void* data, uint32_t bytes,
                                const uint8_t* hdr, uint32_t hdrLen)
 {
     // Stage hdr || data contiguously so the device copy is aligned.
-    const size_t off = (hostStage_.size() + 15) & ~(size_t)15;
-    hostStage_.resize(off + hdrLen + bytes);
-    std::memcpy(hostStage_.data() + off, hdr, hdrLen);
-    std::memcpy(hostStage_.data() + off + hdrLen, data, bytes);
+    Shard& s = shard();
+    const size_t off = (s.hostStage.size() + 15) & ~(size_t)15;
+    s.hostStage.resize(off + hdrLen + bytes);
+    std::memcpy(s.hostStage.data() + off, hdr, hdrLen);
+    std::memcpy(s.hostStage.data() + off + hdrLen, data, bytes);
     IngestDesc d;
     std::memset(&d, 0, sizeof(d));
     d.dst = dst.addr();
     d.src = 0;
     d.bytes = hdrLen + bytes;
     d.hdrLen = 0;
-    add_ingest(d, (uint32_t)off);
+    add_ingest(d, (int64_t)off);
 }
 
-void Engine::add_ingest(const IngestDesc& d, uint32_t hostStageOffset)
+void Engine::add_ingest(const IngestDesc& d, int64_t hostStageOffset)
 {
-    IngestRec r;
-    r.d = d;
-    r.hostOffset = hostStageOffset == (uint32_t)-1 ? -1 : (int64_t)hostStageOffset;
-    ingest_.push_back(r);
+    Shard& s = shard();
+    s.ingest.push_back(Shard::IngestRec{d, hostStageOffset});
+}
+
+bool Engine::pending() const
+{
+    std::lock_guard<std::mutex> g(shardsMu_);
+    for (const auto& s : shards_)
+        if (!s->dirty.empty() || !s->ingest.empty() || !s->downloads.empty())
+            return true;
+    return false;
 }
 
 void Engine::ensure_up(size_t bytes)
@@ -333,6 +423,13 @@ void Engine::ensure_down(size_t bytes)
 
 // ---------------------------------------------------------------------------
 // Engine: flush
+//
+// 1. A sequential pass over the queued programs fixes every segment's place
+//    in the upload (ops, terms, work items) and every solve's place in the
+//    result array.
+// 2. The pool copies segments, ingest descriptors and staged host payloads
+//    into the pinned upload buffer in parallel.
+// 3. One H2D copy, then ingest, executor and solve launches in phase order.
 
 namespace {
 
@@ -343,6 +440,20 @@ struct Phase
     enum Kind { EXEC, SOLVE } kind;
     size_t itemBegin, itemCount;    // exec items or solve items
     size_t solveBegin, solveCount;  // solve descs (SOLVE)
+    uint32_t maxRows;               // largest m among them (SOLVE)
+};
+
+struct SegRef
+{
+    Program* prog;
+    uint32_t seg;
+    uint32_t opBase, termBase, itemBase;
+};
+
+struct ShardRef
+{
+    Shard* shard;
+    size_t descBase, stageBase;
 };
 
 } // namespace
@@ -351,70 +462,78 @@ void Engine::flush()
 {
     if (flight_.active)
         sync();
-    if (!pending() && callbacks_.empty() && pendingFree_.empty())
+
+    std::vector<Shard*> shards;
+    {
+        std::lock_guard<std::mutex> g(shardsMu_);
+        for (auto& s : shards_)
+            shards.push_back(s.get());
+    }
+    bool any = false;
+    for (Shard* s : shards)
+        any = any || !s->dirty.empty() || !s->ingest.empty() || !s->downloads.empty() ||
+              !s->pendingFree.empty();
+    if (!any)
         return;
 
-    // ---- gather host-side arrays --------------------------------------
-    std::vector<IngestDesc> ingDescs;
-    std::vector<IngestItem> ingItems;
-    ingDescs.reserve(ingest_.size());
-    for (const IngestRec& r : ingest_) {
-        const uint32_t idx = (uint32_t)ingDescs.size();
-        ingDescs.push_back(r.d);
-        const uint32_t total = r.d.hdrLen + r.d.bytes;
-        for (uint32_t t = 0; t < total; t += kTileBytes)
-            ingItems.push_back(IngestItem{idx, t});
-    }
+    // ---- 1. layout -----------------------------------------------------------
+    std::vector<Program*> progs[2];
+    for (Shard* s : shards)
+        for (Program* p : s->dirty)
+            progs[p->group_ & 1].push_back(p);
 
-    std::vector<GfOp> ops;
-    std::vector<GfTerm> terms;
-    std::vector<ExecItem> items;
+    uint32_t resultWords = 0;
+    std::vector<uint32_t> resultBase[2];
+    for (int g = 0; g < 2; ++g)
+        for (Program* p : progs[g]) {
+            resultBase[g].push_back(resultWords);
+            resultWords += p->resultWords_;
+        }
+
+    std::vector<SegRef> segs;
+    std::vector<Phase> phases;
     std::vector<SolveDesc> sdescs;
     std::vector<SolveRow> srows;
     std::vector<uint8_t> coef;
     std::vector<SolveItem> sitems;
-    std::vector<Phase> phases;
-
-    for (int group = 0; group < 2; ++group) {
+    size_t nOps = 0, nTerms = 0, nItems = 0;
+    for (int g = 0; g < 2; ++g) {
         size_t maxSegs = 0;
-        for (Program* p : dirty_)
-            if (p->group_ == group)
-                maxSegs = std::max(maxSegs, p->segs_.size());
+        for (Program* p : progs[g])
+            maxSegs = std::max(maxSegs, p->nsegs_);
         for (size_t k = 0; k < maxSegs; ++k) {
-            Phase ex{Phase::EXEC, items.size(), 0, 0, 0};
-            for (Program* p : dirty_) {
-                if (p->group_ != group || k >= p->segs_.size())
+            Phase ex{Phase::EXEC, nItems, 0, 0, 0, 0};
+            for (Program* p : progs[g]) {
+                if (k >= p->nsegs_)
                     continue;
-                Program::Segment& s = p->segs_[k];
+                const Program::Segment& s = p->segs_[k];
                 if (s.ops.empty())
                     continue;
-                const uint32_t opBase = (uint32_t)ops.size();
-                const uint32_t termBase = (uint32_t)terms.size();
-                for (GfOp op : s.ops) {
-                    if (op.kind == OP_LINCOMB)
-                        op.termBegin += termBase;
-                    ops.push_back(op);
-                }
-                terms.insert(terms.end(), s.terms.begin(), s.terms.end());
-                for (uint32_t t = 0; t < s.maxExtent; t += kTileBytes)
-                    items.push_back(ExecItem{opBase, (uint32_t)s.ops.size(), t, 0});
+                segs.push_back(SegRef{p, (uint32_t)k, (uint32_t)nOps, (uint32_t)nTerms,
+                                      (uint32_t)nItems});
+                nOps += s.ops.size();
+                nTerms += s.terms.size();
+                nItems += (s.maxExtent + kTileBytes - 1) / kTileBytes;
             }
-            ex.itemCount = items.size() - ex.itemBegin;
+            ex.itemCount = nItems - ex.itemBegin;
             if (ex.itemCount)
                 phases.push_back(ex);
 
-            Phase sv{Phase::SOLVE, sitems.size(), 0, sdescs.size(), 0};
-            for (Program* p : dirty_) {
-                if (p->group_ != group || k >= p->solves_.size())
+            Phase sv{Phase::SOLVE, sitems.size(), 0, sdescs.size(), 0, 0};
+            for (size_t pi = 0; pi < progs[g].size(); ++pi) {
+                Program* p = progs[g][pi];
+                if (k >= p->solves_.size())
                     continue;
-                Program::PendingSolve& ps = p->solves_[k];
+                const Program::PendingSolve& ps = p->solves_[k];
                 SolveDesc d = ps.desc;
+                d.result += resultBase[g][pi];
                 d.rowBegin = (uint32_t)srows.size();
                 d.coefOffset = coef.size();
                 srows.insert(srows.end(), ps.rows.begin(), ps.rows.end());
                 coef.insert(coef.end(), ps.coef.begin(), ps.coef.end());
                 const uint32_t sidx = (uint32_t)sdescs.size();
                 sdescs.push_back(d);
+                sv.maxRows = std::max(sv.maxRows, d.m);
                 for (uint32_t t = 0; t < d.maxBytes; t += kTileBytes)
                     sitems.push_back(SolveItem{sidx, t});
             }
@@ -425,20 +544,25 @@ void Engine::flush()
         }
     }
 
-    // ---- lay out the single upload --------------------------------------
+    std::vector<ShardRef> srefs;
+    size_t nIngest = 0, stageBytes = 0;
+    for (Shard* s : shards) {
+        srefs.push_back(ShardRef{s, nIngest, stageBytes});
+        nIngest += s->ingest.size();
+        stageBytes = align16(stageBytes + s->hostStage.size());
+    }
+
     size_t off = 0;
     const size_t oStage = off;
-    off = align16(off + hostStage_.size());
+    off = align16(off + stageBytes);
     const size_t oIngD = off;
-    off = align16(off + ingDescs.size() * sizeof(IngestDesc));
-    const size_t oIngI = off;
-    off = align16(off + ingItems.size() * sizeof(IngestItem));
+    off = align16(off + nIngest * sizeof(IngestDesc));
     const size_t oOps = off;
-    off = align16(off + ops.size() * sizeof(GfOp));
+    off = align16(off + nOps * sizeof(GfOp));
     const size_t oTerms = off;
-    off = align16(off + terms.size() * sizeof(GfTerm));
+    off = align16(off + nTerms * sizeof(GfTerm));
     const size_t oItems = off;
-    off = align16(off + items.size() * sizeof(ExecItem));
+    off = align16(off + nItems * sizeof(ExecItem));
     const size_t oSD = off;
     off = align16(off + sdescs.size() * sizeof(SolveDesc));
     const size_t oSR = off;
@@ -448,45 +572,82 @@ void Engine::flush()
     const size_t oSI = off;
     off = align16(off + sitems.size() * sizeof(SolveItem));
     const size_t upBytes = off;
-
     if (upBytes)
         ensure_up(upBytes);
-    for (size_t i = 0; i < ingest_.size(); ++i)
-        if (ingest_[i].hostOffset >= 0)
-            ingDescs[i].src = (uint64_t)(uintptr_t)(upDev_ + oStage + ingest_[i].hostOffset);
 
-    auto put = [&](size_t o, const void* src, size_t n) {
-        if (n)
-            std::memcpy(upHost_ + o, src, n);
+    // ---- 2. parallel assembly into the pinned upload buffer ----------------
+    uint8_t* up = upHost_;
+    const uint64_t stageDev = (uint64_t)(uintptr_t)(upDev_ + oStage);
+    constexpr size_t kIngestChunk = 16384;
+    struct Task
+    {
+        int kind;   // 0 = segment, 1 = ingest chunk
+        size_t a, b;
     };
-    put(oStage, hostStage_.data(), hostStage_.size());
-    put(oIngD, ingDescs.data(), ingDescs.size() * sizeof(IngestDesc));
-    put(oIngI, ingItems.data(), ingItems.size() * sizeof(IngestItem));
-    put(oOps, ops.data(), ops.size() * sizeof(GfOp));
-    put(oTerms, terms.data(), terms.size() * sizeof(GfTerm));
-    put(oItems, items.data(), items.size() * sizeof(ExecItem));
-    put(oSD, sdescs.data(), sdescs.size() * sizeof(SolveDesc));
-    put(oSR, srows.data(), srows.size() * sizeof(SolveRow));
-    put(oCoef, coef.data(), coef.size());
-    put(oSI, sitems.data(), sitems.size() * sizeof(SolveItem));
+    std::vector<Task> tasks;
+    for (size_t i = 0; i < segs.size(); ++i)
+        tasks.push_back(Task{0, i, 0});
+    for (size_t si = 0; si < srefs.size(); ++si)
+        for (size_t c = 0; c < srefs[si].shard->ingest.size(); c += kIngestChunk)
+            tasks.push_back(Task{1, si, c});
+    pool().run(tasks.size(), [&](size_t ti) {
+        const Task& t = tasks[ti];
+        if (t.kind == 0) {
+            const SegRef& r = segs[t.a];
+            const Program::Segment& s = r.prog->segs_[r.seg];
+            GfOp* ops = (GfOp*)(up + oOps) + r.opBase;
+            for (size_t i = 0; i < s.ops.size(); ++i) {
+                GfOp op = s.ops[i];
+                if (op.kind == OP_LINCOMB)
+                    op.termBegin += r.termBase;
+                ops[i] = op;
+            }
+            std::memcpy((GfTerm*)(up + oTerms) + r.termBase, s.terms.data(),
+                        s.terms.size() * sizeof(GfTerm));
+            ExecItem* items = (ExecItem*)(up + oItems) + r.itemBase;
+            uint32_t n = 0;
+            for (uint32_t tb = 0; tb < s.maxExtent; tb += kTileBytes)
+                items[n++] = ExecItem{r.opBase, (uint32_t)s.ops.size(), tb, 0};
+        } else {
+            const ShardRef& sr = srefs[t.a];
+            const Shard& s = *sr.shard;
+            const size_t end = std::min(s.ingest.size(), t.b + kIngestChunk);
+            IngestDesc* descs = (IngestDesc*)(up + oIngD) + sr.descBase;
+            for (size_t i = t.b; i < end; ++i) {
+                IngestDesc d = s.ingest[i].d;
+                if (s.ingest[i].hostOffset >= 0)
+                    d.src = stageDev + sr.stageBase + (uint64_t)s.ingest[i].hostOffset;
+                descs[i] = d;
+            }
+            if (t.b == 0 && !s.hostStage.empty())
+                std::memcpy(up + oStage + sr.stageBase, s.hostStage.data(), s.hostStage.size());
+        }
+    });
+    if (!sdescs.empty()) {
+        std::memcpy(up + oSD, sdescs.data(), sdescs.size() * sizeof(SolveDesc));
+        std::memcpy(up + oSR, srows.data(), srows.size() * sizeof(SolveRow));
+        std::memcpy(up + oCoef, coef.data(), coef.size());
+        std::memcpy(up + oSI, sitems.data(), sitems.size() * sizeof(SolveItem));
+    }
 
     // download area: results first, then each requested range
-    size_t dOff = align16((size_t)resultWords_ * 4);
-    std::vector<Download> dls = downloads_;
-    std::vector<size_t> dlOff;
-    for (const Download& d : dls) {
-        dlOff.push_back(dOff);
-        dOff = align16(dOff + d.bytes);
-    }
+    size_t dOff = align16((size_t)resultWords * 4);
+    flight_.downloads.clear();
+    std::vector<Shard::Download> dls;
+    for (Shard* s : shards)
+        for (const Shard::Download& d : s->downloads) {
+            flight_.downloads.push_back(InFlight::Download{d.host, dOff, d.bytes});
+            dls.push_back(d);
+            dOff = align16(dOff + d.bytes);
+        }
     if (dOff)
         ensure_down(dOff);
 
-    // ---- launch ----------------------------------------------------------
+    // ---- 3. launch -----------------------------------------------------------
     if (upBytes)
         be_h2d(upDev_, upHost_, upBytes);
-    if (!ingItems.empty())
-        be_launch_ingest((const IngestDesc*)(upDev_ + oIngD), (const IngestItem*)(upDev_ + oIngI),
-                         (uint32_t)ingItems.size());
+    if (nIngest)
+        be_launch_ingest((const IngestDesc*)(upDev_ + oIngD), (uint32_t)nIngest);
     uint32_t* resultsDev = (uint32_t*)downDev_;
     for (const Phase& ph : phases) {
         if (ph.kind == Phase::EXEC) {
@@ -500,44 +661,45 @@ void Engine::flush()
             be_launch_solve_main((const SolveDesc*)(upDev_ + oSD), (const SolveRow*)(upDev_ + oSR),
                                  upDev_ + oCoef, resultsDev,
                                  (const SolveItem*)(upDev_ + oSI) + ph.itemBegin,
-                                 (uint32_t)ph.itemCount);
+                                 (uint32_t)ph.itemCount, ph.maxRows);
         }
     }
-    if (resultWords_)
-        be_d2h(downHost_, resultsDev, (size_t)resultWords_ * 4);
+    if (resultWords)
+        be_d2h(downHost_, resultsDev, (size_t)resultWords * 4);
     for (size_t i = 0; i < dls.size(); ++i)
-        be_d2h(downHost_ + dlOff[i], (const void*)(uintptr_t)dls[i].dev, dls[i].bytes);
+        be_d2h(downHost_ + flight_.downloads[i].off, (const void*)(uintptr_t)dls[i].dev,
+               dls[i].bytes);
 
-    // ---- bookkeeping -----------------------------------------------------
-    stats.flushes++;
-    stats.launches += phases.size() + (ingItems.empty() ? 0 : 1);
-    stats.ops += ops.size();
-    stats.terms += terms.size();
-    stats.solves += sdescs.size();
-    stats.ingests += ingDescs.size();
-    stats.uploadBytes += upBytes;
+    // ---- bookkeeping -----------------------------------------------------------
+    flushStats_.flushes++;
+    flushStats_.launches += phases.size() + (nIngest ? 1 : 0);
+    flushStats_.ops += nOps;
+    flushStats_.terms += nTerms;
+    flushStats_.solves += sdescs.size();
+    flushStats_.ingests += nIngest;
+    flushStats_.uploadBytes += upBytes;
 
-    flight_.downloads.clear();
-    for (size_t i = 0; i < dls.size(); ++i)
-        flight_.downloads.push_back(Download{dls[i].host, (uint64_t)dlOff[i], dls[i].bytes});
-    flight_.callbacks.swap(callbacks_);
-    callbacks_.clear();
-    flight_.resultWords = resultWords_;
+    flight_.callbacks.clear();
+    for (int g = 0; g < 2; ++g)
+        for (size_t pi = 0; pi < progs[g].size(); ++pi) {
+            Program* p = progs[g][pi];
+            for (Completion& fn : p->callbacks_)
+                flight_.callbacks.emplace_back(resultBase[g][pi], std::move(fn));
+            if (p->group_ & 2)
+                delete p;   // orphan of a freed instance (see ~Program)
+            else
+                p->reset_after_flush();
+        }
     flight_.active = true;
-    // Buffers released before this flush may be reused once it completes.
-    flightFree_.swap(pendingFree_);
-    pendingFree_.clear();
-
-    for (Program* p : dirty_) {
-        p->segs_.clear();
-        p->solves_.clear();
-        p->dirty_ = false;
+    for (Shard* s : shards) {
+        s->dirty.clear();
+        s->ingest.clear();
+        s->hostStage.clear();
+        s->downloads.clear();
+        // buffers released before this flush may be reused once it completes
+        s->flightFree.swap(s->pendingFree);
+        s->pendingFree.clear();
     }
-    dirty_.clear();
-    ingest_.clear();
-    hostStage_.clear();
-    downloads_.clear();
-    resultWords_ = 0;
 }
 
 bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut)
@@ -547,19 +709,15 @@ bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* byt
     if (count == 0)
         return true;
     std::vector<IngestDesc> descs(count);
-    std::vector<IngestItem> items;
     size_t total = 0;
     for (unsigned i = 0; i < count; ++i) {
         std::memset(&descs[i], 0, sizeof(IngestDesc));
         descs[i].src = (uint64_t)(uintptr_t)srcs[i];
         descs[i].bytes = bytes[i];
         descs[i].dst = total; // offset for now
-        for (uint32_t t = 0; t < bytes[i]; t += kTileBytes)
-            items.push_back(IngestItem{i, t});
         total = align16(total + bytes[i]);
     }
-    const size_t dBytes = count * sizeof(IngestDesc);
-    const size_t upBytes = align16(dBytes) + items.size() * sizeof(IngestItem);
+    const size_t upBytes = count * sizeof(IngestDesc);
     auto grow = [](uint8_t*& h, uint8_t*& d, size_t& cap, size_t need) {
         if (need <= cap)
             return;
@@ -578,12 +736,9 @@ bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* byt
     grow(gHost_, gDev_, gCap_, total);
     for (IngestDesc& d : descs)
         d.dst += (uint64_t)(uintptr_t)gDev_;
-    std::memcpy(gUpHost_, descs.data(), dBytes);
-    std::memcpy(gUpHost_ + align16(dBytes), items.data(), items.size() * sizeof(IngestItem));
+    std::memcpy(gUpHost_, descs.data(), upBytes);
     be_h2d(gUpDev_, gUpHost_, upBytes);
-    if (!items.empty())
-        be_launch_ingest((const IngestDesc*)gUpDev_, (const IngestItem*)(gUpDev_ + align16(dBytes)),
-                         (uint32_t)items.size());
+    be_launch_ingest((const IngestDesc*)gUpDev_, count);
     be_d2h(gHost_, gDev_, total);
     const bool ok = be_sync();
     uint8_t* out = (uint8_t*)hostOut;
@@ -601,18 +756,29 @@ bool Engine::sync()
     if (!flight_.active)
         return true;
     const bool ok = be_sync();
-    for (const Download& d : flight_.downloads)
-        std::memcpy(d.host, downHost_ + d.dev, d.bytes);
+    for (const InFlight::Download& d : flight_.downloads)
+        std::memcpy(d.host, downHost_ + d.off, d.bytes);
     const uint32_t* results = (const uint32_t*)downHost_;
-    for (auto& fn : flight_.callbacks)
-        fn(results);
+    for (auto& cb : flight_.callbacks)
+        cb.second(results + cb.first);
     flight_.callbacks.clear();
     flight_.downloads.clear();
     flight_.active = false;
-    for (DevBuf& b : flightFree_) {
-        free_list(b.cap)->push_back(b.ptr);
+    std::vector<Shard*> shards;
+    {
+        std::lock_guard<std::mutex> g(shardsMu_);
+        for (auto& s : shards_)
+            shards.push_back(s.get());
     }
-    flightFree_.clear();
+    for (Shard* s : shards) {
+        for (const DevBuf& b : s->flightFree) {
+            const size_t cls = cap_class(b.cap);
+            if (cls >= s->freeLists.size())
+                s->freeLists.resize(cls + 1);
+            s->freeLists[cls].push_back(b.ptr);
+        }
+        s->flightFree.clear();
+    }
     return ok;
 }
 

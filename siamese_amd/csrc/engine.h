@@ -1,16 +1,28 @@
 // engine.h -- device-side resources of the codec: an arena of symbol
 // buffers in HBM, per-instance op programs, and the flush that turns all
 // pending programs into a handful of kernel launches.
+//
+// Threading: codec instances may be driven concurrently from different host
+// threads (one thread per instance at a time).  Everything an instance call
+// touches in the engine lives in the calling thread's Shard (buffer free
+// lists, ingest queue, downloads, statistics) or in the instance's own
+// Program, so per-instance calls take no global lock.  flush()/sync()/
+// gather() are exclusive: the caller guarantees no instance call runs
+// concurrently with them (the siamese_gpu.h contract).
 #pragma once
 
 #include "ops.h"
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <vector>
 
 namespace sgpu {
+
+class WorkerPool;
 
 /// A symbol-sized buffer in device memory.  Capacity is a multiple of 64 B.
 struct DevBuf
@@ -22,6 +34,11 @@ struct DevBuf
 };
 
 class Engine;
+struct Shard;
+
+/// Completion callback of a flush; `results` is the solve-result word array
+/// as seen by the program that registered it (indices returned by solve()).
+using Completion = std::function<void(const uint32_t* results)>;
 
 /// Ops of one codec instance since the last flush.  Segments are separated
 /// by triangular solves; `group` orders instances inside a flush (group 0 =
@@ -38,7 +55,23 @@ public:
 
     /// LINCOMB: dst[i] = (i < valid ? dst[i] : 0) ^ acc0 ^ mix*acc1, i < n.
     void lc_begin(uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix = 0);
-    void lc_term(uint64_t src, uint32_t len, uint8_t coeff, uint8_t acc = 0);
+    void lc_term(uint64_t src, uint32_t len, uint8_t coeff, uint8_t acc = 0)
+    {
+        Segment& s = segs_[nsegs_ - 1];
+        GfOp& op = s.ops.back();
+        if (len > op.n)
+            len = op.n;
+        if (len == 0 || coeff == 0)
+            return;
+        GfTerm t;
+        t.src = src;
+        t.len = len;
+        t.coeff = coeff;
+        t.acc = acc;
+        t.pad = 0;
+        s.terms.push_back(t);
+        ++op.termCount;
+    }
     void lc_end();
 
     /// Convenience single-term forms of the reference bulk ops
@@ -58,11 +91,13 @@ public:
                        uint32_t hdrLen);
 
     /// Queue a triangular solve; returns the result-word index it will fill
-    /// (valid in the completion callback of the flush that runs it).
-    uint32_t solve(const std::vector<SolveRow>& rows, const std::vector<uint8_t>& coef,
-                   uint32_t maxBytes);
+    /// (valid in this program's completion callbacks of the flush that runs it).
+    uint32_t solve(const std::vector<SolveRow>& rows, const uint8_t* coef, uint32_t maxBytes);
 
-    bool empty() const { return segs_.empty() || (segs_.size() == 1 && segs_[0].ops.empty()); }
+    /// Run `fn(results)` once the next flush has completed.
+    void on_complete(Completion fn);
+
+    bool empty() const { return nsegs_ == 0 || (nsegs_ == 1 && segs_[0].ops.empty()); }
 
 private:
     friend class Engine;
@@ -79,37 +114,56 @@ private:
         std::vector<uint8_t> coef;
     };
 
-    Segment& seg();
-    void touch();
+    void touch()
+    {
+        if (!shard_)
+            attach();
+    }
+    void attach();
+    void new_segment();
+    void reset_after_flush();
 
     Engine* eng_;
     int group_;
-    bool dirty_ = false;
-    bool open_ = false;       // inside lc_begin/lc_end
+    Shard* shard_ = nullptr;     // shard this program is queued in (null: clean)
+    uint32_t resultWords_ = 0;   // result words reserved since the last flush
+    size_t nsegs_ = 0;           // segments in use (capacity is kept across flushes)
     std::vector<Segment> segs_;
     std::vector<PendingSolve> solves_;   // solve k follows segment k
+    std::vector<Completion> callbacks_;
+};
+
+/// Algorithmic byte accounting and flush counters.
+struct EngineStats
+{
+    uint64_t flushes = 0, launches = 0, ops = 0, terms = 0, solves = 0, ingests = 0;
+    uint64_t uploadBytes = 0;
+    // Source bytes of every bulk GF op the reference codec performs for the
+    // same call sequence, and bytes of recovery packets / recovered
+    // originals produced.
+    uint64_t refOpBytes = 0, outBytes = 0;
+    uint64_t solveBytes = 0;   // the part of both done by the solve kernels
+
+    void add(const EngineStats& o);
 };
 
 class Engine
 {
 public:
-    /// Process-wide engine used by the drop-in siamese.h entry points.
+    /// Process-wide engine used by both ABIs.
     static Engine* global();
+    ~Engine();
 
     bool init(int device, const char** err);
     bool ready() const { return ready_; }
 
     DevBuf alloc(uint32_t bytes);
-    void release(DevBuf& b);               // recycled after the next sync
-    uint64_t bytes_in_use() const { return inUse_; }
+    void release(DevBuf& b);               // recycled after the next flush completes
+    uint64_t bytes_in_use() const;
 
     /// Copy `bytes` of device memory to host memory once the next flush has
     /// executed; the data is in place after sync().
     void download(void* hostDst, uint64_t devSrc, uint32_t bytes);
-
-    /// Run `fn(results)` after the next flush completes; `results` is the
-    /// solve-result word array of that flush.
-    void on_complete(std::function<void(const uint32_t*)> fn);
 
     void flush();
     bool sync();
@@ -118,93 +172,63 @@ public:
         flush();
         return sync();
     }
-
-    bool pending() const { return !dirty_.empty() || !ingest_.empty() || !downloads_.empty(); }
+    bool pending() const;
 
     /// Copy device ranges into one host buffer right now (after completing
     /// any flush in flight).  Queued, unflushed work is not touched.
     bool gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut);
 
+    /// Serialises the drop-in siamese.h entry points and the exclusive
+    /// siamese_gpu.h calls.
     std::mutex& mutex() { return mu_; }
 
-    // statistics of the last flushes (for the bench / profiles)
-    struct Stats
-    {
-        uint64_t flushes = 0, launches = 0, ops = 0, terms = 0, solves = 0, ingests = 0;
-        uint64_t uploadBytes = 0;
-        // Algorithmic bytes: source bytes of every bulk GF op
-        // the reference codec performs for the same call sequence, and bytes
-        // of recovery packets / recovered originals produced.
-        uint64_t refOpBytes = 0, outBytes = 0;
-        uint64_t solveBytes = 0;   // the part of both done by the solve kernels
-    } stats;
+    /// Counts toward the calling thread's statistics.
+    void account(uint64_t opBytes, uint64_t outBytes = 0, bool inSolve = false);
+    /// Totals over all threads.
+    EngineStats stats() const;
 
-    void account(uint64_t opBytes, uint64_t outBytes = 0, bool inSolve = false)
-    {
-        stats.refOpBytes += opBytes;
-        stats.outBytes += outBytes;
-        if (inSolve)
-            stats.solveBytes += opBytes + outBytes;
-    }
+    /// The calling thread's shard.
+    Shard& shard();
 
 private:
     friend class Program;
-    void register_dirty(Program* p) { dirty_.push_back(p); }
-    void forget(Program* p);
-    uint32_t reserve_results(uint32_t words)
-    {
-        const uint32_t r = resultWords_;
-        resultWords_ += words;
-        return r;
-    }
     void stage_host_ingest(const DevBuf& dst, const void* data, uint32_t bytes, const uint8_t* hdr,
                            uint32_t hdrLen);
-    void add_ingest(const IngestDesc& d, uint32_t hostStageOffset);
+    void add_ingest(const IngestDesc& d, int64_t hostStageOffset);
+    uint8_t* carve(uint32_t cap);
+    WorkerPool& pool();
 
     bool ready_ = false;
     std::mutex mu_;
 
-    // ---- arena ----
+    // ---- arena (chunks are carved under arenaMu_; free lists are per shard)
     struct Chunk
     {
         uint8_t* base;
         size_t size, used;
     };
+    std::mutex arenaMu_;
     std::vector<Chunk> chunks_;
-    std::vector<std::pair<uint32_t, std::vector<uint8_t*>>> freeLists_; // sorted by cap
-    std::vector<DevBuf> pendingFree_;   // released since the last flush
-    std::vector<DevBuf> flightFree_;    // released before the flush in flight
-    uint64_t inUse_ = 0;
-    std::vector<uint8_t*>* free_list(uint32_t cap);
 
-    // ---- pending work ----
-    std::vector<Program*> dirty_;
-    struct IngestRec
-    {
-        IngestDesc d;
-        int64_t hostOffset;   // >= 0: src lives in the host staging area
-    };
-    std::vector<IngestRec> ingest_;
-    std::vector<uint8_t> hostStage_;   // host payloads awaiting H2D
-    struct Download
-    {
-        void* host;
-        uint64_t dev;
-        uint32_t bytes;
-    };
-    std::vector<Download> downloads_;
-    std::vector<std::function<void(const uint32_t*)>> callbacks_;
-    uint32_t resultWords_ = 0;
+    // ---- shards (one per host thread that touched the engine)
+    mutable std::mutex shardsMu_;
+    std::vector<std::unique_ptr<Shard>> shards_;
 
-    // ---- in flight ----
+    // ---- flush-level state (exclusive)
+    EngineStats flushStats_;
     struct InFlight
     {
+        struct Download
+        {
+            void* host;
+            size_t off;
+            uint32_t bytes;
+        };
         std::vector<Download> downloads;
-        std::vector<std::function<void(const uint32_t*)>> callbacks;
-        uint32_t resultWords = 0;
-        size_t downloadBytes = 0;
+        std::vector<std::pair<uint32_t, Completion>> callbacks;   // (results base, fn)
         bool active = false;
     } flight_;
+    std::unique_ptr<WorkerPool> pool_;
 
     // transfer buffers (grown on demand)
     uint8_t* upHost_ = nullptr;
@@ -223,6 +247,35 @@ private:
     uint8_t* gHost_ = nullptr;
     uint8_t* gDev_ = nullptr;
     size_t gCap_ = 0;
+};
+
+/// Per-host-thread engine state.  Only its owning thread touches it between
+/// flushes, except `dirty`, which a program's destructor may edit from
+/// another thread (guarded by `mu`).
+struct Shard
+{
+    struct IngestRec
+    {
+        IngestDesc d;
+        int64_t hostOffset;   // >= 0: src lives in this shard's host staging area
+    };
+    struct Download
+    {
+        void* host;
+        uint64_t dev;
+        uint32_t bytes;
+    };
+
+    std::mutex mu;
+    std::vector<Program*> dirty;
+    std::vector<IngestRec> ingest;
+    std::vector<uint8_t> hostStage;
+    std::vector<Download> downloads;
+    std::vector<DevBuf> pendingFree;   // released since the last flush
+    std::vector<DevBuf> flightFree;    // released before the flush in flight
+    std::vector<std::vector<uint8_t*>> freeLists;   // by capacity class
+    int64_t inUse = 0;
+    EngineStats stats;
 };
 
 } // namespace sgpu

@@ -101,7 +101,9 @@ struct SolveItem
 
 /// Ingest of one symbol into a FRESH device buffer (never referenced by any
 /// op of the same flush before this point), so ingest can run as the first
-/// launch of a flush:  dst[0,hdrLen) = hdr,  dst[hdrLen, hdrLen+bytes) = src.
+/// launch of a flush:  dst[0,hdrLen) = hdr,  dst[hdrLen, hdrLen+bytes) = src,
+/// and dst[total, align16(total)) = 0 (whole 16-byte lanes are stored; dst is
+/// 16-byte aligned with capacity >= align16(total)).
 struct IngestDesc
 {
     uint64_t dst;
@@ -109,13 +111,6 @@ struct IngestDesc
     uint32_t bytes;
     uint32_t hdrLen;
     uint8_t hdr[8];
-};
-
-/// Ingest work item: one (symbol, destination tile).
-struct IngestItem
-{
-    uint32_t desc;
-    uint32_t tileBase;
 };
 
 constexpr unsigned kTileBytes = 1024;   // 64 lanes x 16 bytes

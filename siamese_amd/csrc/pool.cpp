@@ -1,0 +1,92 @@
+// pool.cpp -- see pool.h.
+#include "pool.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace sgpu {
+
+unsigned WorkerPool::default_threads()
+{
+    for (const char* var : {"SIAMESE_AMD_THREADS", "OMP_NUM_THREADS"}) {
+        const char* v = std::getenv(var);
+        if (v && std::atoi(v) > 0)
+            return (unsigned)std::min(256, std::atoi(v));
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return std::max(1u, std::min(16u, hw));
+}
+
+WorkerPool::WorkerPool(unsigned threads)
+{
+    for (unsigned i = 1; i < threads; ++i)
+        workers_.emplace_back([this] { loop(); });
+}
+
+WorkerPool::~WorkerPool()
+{
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread& t : workers_)
+        t.join();
+}
+
+void WorkerPool::drain()
+{
+    for (;;) {
+        const size_t i = next_.fetch_add(1, std::memory_order_acq_rel);
+        if (i >= count_)
+            return;
+        (*fn_)(i);
+    }
+}
+
+void WorkerPool::loop()
+{
+    uint64_t seen = 0;
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_)
+                return;
+            seen = gen_;
+            ++busy_;
+        }
+        drain();
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            if (--busy_ == 0)
+                doneCv_.notify_all();
+        }
+    }
+}
+
+void WorkerPool::run(size_t count, const std::function<void(size_t)>& fn)
+{
+    if (count == 0)
+        return;
+    if (workers_.empty() || count == 1) {
+        for (size_t i = 0; i < count; ++i)
+            fn(i);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        fn_ = &fn;
+        count_ = count;
+        next_.store(0, std::memory_order_release);
+        ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(mu_);
+    // every index has been claimed; wait for the workers still finishing one
+    doneCv_.wait(lk, [&] { return busy_ == 0; });
+    fn_ = nullptr;
+}
+
+} // namespace sgpu

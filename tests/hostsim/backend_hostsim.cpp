@@ -174,17 +174,17 @@ void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, byt
 
 static bool noexec();
 
-void be_launch_ingest(const IngestDesc* descs, const IngestItem* items, uint32_t count)
+void be_launch_ingest(const IngestDesc* descs, uint32_t count)
 {
     if (noexec())
         return;
     for (uint32_t i = 0; i < count; ++i) {
-        const IngestDesc& d = descs[items[i].desc];
+        const IngestDesc& d = descs[i];
         const uint32_t total = d.hdrLen + d.bytes;
-        const uint32_t t0 = items[i].tileBase;
-        const uint32_t t1 = t0 + kTileBytes < total ? t0 + kTileBytes : total;
-        for (uint32_t k = t0; k < t1; ++k)
-            P(d.dst)[k] = k < d.hdrLen ? d.hdr[k] : P(d.src)[k - d.hdrLen];
+        // the kernel stores whole 16-byte lanes, zero past the symbol
+        const uint32_t end = (total + 15) & ~15u;
+        for (uint32_t k = 0; k < end; ++k)
+            P(d.dst)[k] = k < d.hdrLen ? d.hdr[k] : (k < total ? P(d.src)[k - d.hdrLen] : 0);
     }
 }
 
@@ -263,7 +263,8 @@ void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const
 }
 
 void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                          const uint32_t* results, const SolveItem* items, uint32_t count)
+                          const uint32_t* results, const SolveItem* items, uint32_t count,
+                          uint32_t)
 {
     if (noexec())
         return;

@@ -75,7 +75,8 @@ def replace(cfg, **kw):
 
 class BatchOptions(ctypes.Structure):
     _fields_ = [("steps", ctypes.c_uint32), ("warmup", ctypes.c_uint32),
-                ("verify", ctypes.c_uint32), ("device", ctypes.c_int32)]
+                ("verify", ctypes.c_uint32), ("device", ctypes.c_int32),
+                ("threads", ctypes.c_uint32)]
 
 
 class BatchReport(ctypes.Structure):
@@ -119,12 +120,13 @@ def run_capi(library, cfg, threads=1, event_log=None):
     return res, sec.value, wall
 
 
-def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1):
-    """Run `cfg` through the device-resident batch API (lock-step rounds).
+def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0):
+    """Run `cfg` through the device-resident batch API (lock-step rounds),
+    streams driven by `threads` host threads (0 = library default).
 
     Returns (results of the last run, BatchReport)."""
     res = (StreamResult * cfg.streams)()
-    opt = BatchOptions(steps, warmup, 1 if verify else 0, device)
+    opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads)
     rep = BatchReport()
     rc = lib().scenario_run_batch(library.encode(), ctypes.byref(cfg), res, ctypes.byref(opt),
                                   ctypes.byref(rep))
@@ -158,9 +160,9 @@ class BatchSession:
         if not self.handle:
             raise RuntimeError("scenario_batch_open(%s) failed" % library)
 
-    def run(self, steps=1, warmup=0, verify=False):
+    def run(self, steps=1, warmup=0, verify=False, threads=0):
         res = (StreamResult * self.cfg.streams)()
-        opt = BatchOptions(steps, warmup, 1 if verify else 0, -1)
+        opt = BatchOptions(steps, warmup, 1 if verify else 0, -1, threads)
         rep = BatchReport()
         rc = lib().scenario_batch_run(self.handle, res, ctypes.byref(opt), ctypes.byref(rep))
         if rc != 0:
