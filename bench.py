@@ -101,14 +101,14 @@ def run_rank(rank, world, local, args, library, use_cuda):
     cfg = workload(rank, args.streams)
     sess = S.BatchSession(library, cfg, device=local if use_cuda else -1)
     # untimed warm-up; its first run checks every recovered byte against the payload
-    res, rep = sess.run(steps=0, warmup=max(1, args.warmup), verify=True)
+    res, rep = sess.run(steps=0, warmup=max(1, args.warmup), verify=True, threads=args.threads)
     if rep.mismatches or any(r.status for r in res):
         raise RuntimeError("bench: verification failed: %d byte mismatches, status %s"
                            % (rep.mismatches, S.summary(res)["status"]))
 
     coll.barrier()
     t0 = time.perf_counter()
-    res, rep = sess.run(steps=args.steps, warmup=0, verify=False)
+    res, rep = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads)
     coll.barrier()
     elapsed = time.perf_counter() - t0
     sess.close()
@@ -162,7 +162,13 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "launches_per_step": eng["launches"] / steps,
             "terms_per_step": eng["terms"] / steps,
             "algorithmic_bytes_per_step": alg_bytes // steps,
+            "upload_bytes_per_step": eng["upload_bytes"] // steps,
             "rank0_digest": digest,
+        },
+        "host": {
+            "threads": args.threads or "default",
+            "phase_ms_per_step": {k: round(v * 1e3 / steps, 3)
+                                  for k, v in zip(S.PHASES, rep.phase_seconds)},
         },
         "roofline": {
             "bound": "hbm",
@@ -194,6 +200,7 @@ def main(argv=None):
     ap.add_argument("--streams", type=int, default=STREAMS_PER_GPU)
     ap.add_argument("--cpu-streams", type=int, default=4096)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--threads", type=int, default=0, help="host threads driving streams (0 = library default)")
     ap.add_argument("--library", default=S.AMD_LIB, help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 

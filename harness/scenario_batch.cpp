@@ -45,6 +45,10 @@ struct BatchReport
     uint64_t engine[10];   ///< engine counters over the timed steps (see sgpu_engine_stats)
     uint64_t checked;      ///< packets whose bytes were verified
     uint64_t mismatches;   ///< verification failures
+    /// wall time of the timed steps split by phase: codec create, stream
+    /// stepping (host control plane), sgpu_flush (assembly + upload + device
+    /// + completion), token resolution, finish + free
+    double phase_seconds[5];
 };
 
 } // extern "C"
@@ -277,11 +281,17 @@ void for_streams(Shared& sh, size_t count, const F& fn)
     });
 }
 
-int run_once(Shared& sh, StreamResult* results, uint64_t* rounds)
+int run_once(Shared& sh, StreamResult* results, uint64_t* rounds, double* phase)
 {
     const Api& api = *sh.api;
     const ScenarioConfig* cfg = sh.cfg;
     const unsigned n = cfg->streams;
+    auto t = Clock::now();
+    auto lap = [&](int k) {
+        const auto now = Clock::now();
+        phase[k] += std::chrono::duration<double>(now - t).count();
+        t = now;
+    };
     std::vector<BatchCodec> codecs(n);
     std::unique_ptr<BatchStream[]> streams(new BatchStream[n]);
     for_streams(sh, n, [&](size_t s) {
@@ -293,6 +303,7 @@ int run_once(Shared& sh, StreamResult* results, uint64_t* rounds)
         if (!codecs[s].enc || !codecs[s].dec)
             streams[s].fail(2);
     });
+    lap(0);
     // requests of every stream that wait for device bytes
     auto take = [&](bool prev) {
         std::vector<Request> reqs;
@@ -316,13 +327,16 @@ int run_once(Shared& sh, StreamResult* results, uint64_t* rounds)
                 if (st.step())
                     break;
         });
+        lap(1);
         // bytes produced by the previous flush are final now
         std::vector<Request> reqs = take(true);
         resolve_requests(sh, reqs);
+        lap(3);
         if (api.flush() != 0) {
             rc = -3;
             break;
         }
+        lap(2);
         ++*rounds;
         for (BatchCodec& c : codecs)
             std::swap(c.prev, c.cur);
@@ -334,12 +348,14 @@ int run_once(Shared& sh, StreamResult* results, uint64_t* rounds)
     resolve_requests(sh, reqs);
     reqs = take(false);
     resolve_requests(sh, reqs);
+    lap(3);
     for_streams(sh, n, [&](size_t s) {
         streams[s].finish();
         api.encoder_free(codecs[s].enc);
         api.decoder_free(codecs[s].dec);
     });
     api.flush();
+    lap(4);
     return rc;
 }
 
@@ -426,11 +442,12 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         if (!sh.pool || sh.pool->size() != threads)
             sh.pool.reset(new sgpu::WorkerPool(threads));
         uint64_t rounds = 0;
+        double phase[5] = {0, 0, 0, 0, 0};
         uint64_t e0[kEngineStats], e1[kEngineStats];
         api.engine_stats(e0);
         api.timing(timed ? 1 : 0, 1, nullptr, nullptr);
         const auto t1 = Clock::now();
-        rc = run_once(sh, results, &rounds);
+        rc = run_once(sh, results, &rounds, phase);
         const double dt = std::chrono::duration<double>(Clock::now() - t1).count();
         double execMs = 0, totalMs = 0;
         api.timing(0, 1, &execMs, &totalMs);
@@ -440,6 +457,8 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
             report->device_ms += totalMs;
             report->exec_ms += execMs;
             report->rounds += rounds;
+            for (int k = 0; k < 5; ++k)
+                report->phase_seconds[k] += phase[k];
             for (int k = 0; k < kEngineStats; ++k)
                 report->engine[k] += e1[k] - e0[k];
         }

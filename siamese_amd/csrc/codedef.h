@@ -96,6 +96,21 @@ struct Pcg32
     }
 };
 
+/// a % d for a fixed divisor without a division instruction (Lemire,
+/// Kaser & Kurz, "Faster remainder by direct computation", 2019): exact for
+/// every 32-bit a and d >= 1.  The LDPC picks take two remainders per pair.
+struct FastMod
+{
+    uint64_t m;
+    uint32_t d;
+    explicit FastMod(uint32_t divisor) : m(~0ULL / divisor + 1), d(divisor) {}
+    uint32_t operator()(uint32_t a) const
+    {
+        const uint64_t low = m * a;
+        return (uint32_t)(((unsigned __int128)low * d) >> 64);
+    }
+};
+
 // ---- Metadata carried in every recovery footer (SiameseCommon.h:364-389) --
 struct RowMeta
 {

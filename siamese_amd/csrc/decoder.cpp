@@ -233,35 +233,32 @@ DevSum& DecoderCore::get_sum(unsigned lane, unsigned s, unsigned elementEnd)
         return S.d;
 
     unsigned newBytes = S.d.bytes;
-    struct T
-    {
-        uint64_t src;
-        unsigned len;
-        uint8_t c;
-    };
-    std::vector<T> terms;
-    do {
-        const DecSlot& o = slot(element);
-        if (o.bytes > 0) {
-            newBytes = std::max(newBytes, o.bytes);
-            terms.push_back(T{o.buf.addr(), o.bytes, sum_coeff(s, o.column)});
+    unsigned got = 0;
+    for (unsigned e = element; e < elementEnd; e += kLanes) {
+        const unsigned b = slot(e).bytes;
+        if (b > 0) {
+            newBytes = std::max(newBytes, b);
+            ++got;
         }
-        element += kLanes;
-    } while (element < elementEnd);
-
-    if (!terms.empty()) {
+    }
+    if (got > 0) {
         if (!grow_sum(S.d, newBytes))
             return S.d;
         prog_.lc_begin(S.d.buf.addr(), S.d.bytes, S.d.devValid);
         uint64_t opBytes = 0;
-        for (const T& t : terms) {
-            prog_.lc_term(t.src, t.len, t.c);
-            opBytes += t.len;
+        for (unsigned e = element; e < elementEnd; e += kLanes) {
+            const DecSlot& o = slot(e);
+            if (o.bytes == 0)
+                continue;
+            prog_.lc_term(o.buf.addr(), o.bytes, sum_coeff(s, o.column));
+            opBytes += o.bytes;
         }
         prog_.lc_end();
         eng_->account(opBytes);
         S.d.devValid = S.d.bytes;
     }
+    while (element < elementEnd)
+        element += kLanes;
     S.elementEnd = element;
     return S.d;
 }
@@ -906,6 +903,9 @@ void DecoderCore::populate_columns(unsigned oldColumns, unsigned newColumns)
                 c.column = element_to_column(sub * kSubwindow + bit);
                 c.original = &sw->slot[bit];
                 c.cx = column_value(c.column);
+                const uint8_t cx2 = gf_sqr(c.cx);
+                for (unsigned k = 0; k < 8; ++k)
+                    c.comb[k] = (uint8_t)((k & 1) ^ ((k & 2) ? c.cx : 0) ^ ((k & 4) ? cx2 : 0));
                 c.original->column = column; // lost slot -> matrix column
                 if (++column >= newColumns)
                     return;
@@ -965,30 +965,22 @@ bool DecoderCore::generate_matrix()
             continue;
         }
 
+        // Dense coefficient of column x in row r: the opcode's low three bits
+        // select {1, CX, CX^2} for the row sum, the high three the same for
+        // the product, which is scaled by RX:  v = comb[op&7] ^ RX*comb[op>>3]
         const uint8_t rx = row_value(m.row);
+        const uint8_t* mulRx = g_gf.mul[rx];
+        unsigned opcodes[kLanes];
+        for (unsigned lane = 0; lane < kLanes; ++lane)
+            opcodes[lane] = row_opcode(lane, m.row);
         for (unsigned j = startCol; j < columns; ++j) {
-            const unsigned column = cols_[j].column;
-            if (column_sub(column, m.columnStart) >= m.sumCount) {
+            const ColInfo& c = cols_[j];
+            if (column_sub(c.column, m.columnStart) >= m.sumCount) {
                 std::memset(row + j, 0, columns - j);
                 break;
             }
-            const uint8_t cx = cols_[j].cx;
-            const uint8_t cx2 = gf_sqr(cx);
-            const unsigned op = row_opcode(column % kLanes, m.row);
-            uint8_t v = 0;
-            if (op & 1)
-                v ^= 1;
-            if (op & 2)
-                v ^= cx;
-            if (op & 4)
-                v ^= cx2;
-            if (op & 8)
-                v ^= rx;
-            if (op & 16)
-                v ^= gf_mul(cx, rx);
-            if (op & 32)
-                v ^= gf_mul(cx2, rx);
-            row[j] = v;
+            const unsigned op = opcodes[c.column % kLanes];
+            row[j] = (uint8_t)(c.comb[op & 7] ^ mulRx[c.comb[op >> 3]]);
         }
 
         // Sparse columns that landed on lost data
@@ -996,11 +988,12 @@ bool DecoderCore::generate_matrix()
         prng.seed(m.row, m.ldpcCount);
         const unsigned pairs = (m.ldpcCount + kPairRate - 1) / kPairRate;
         const size_t rowOff = (size_t)i * matStride_;
+        const FastMod mod(m.ldpcCount ? m.ldpcCount : 1);
         for (unsigned k = 0; k < pairs; ++k) {
-            const DecSlot& a = slot(rec->elementStart + prng.next() % m.ldpcCount);
+            const DecSlot& a = slot(rec->elementStart + mod(prng.next()));
             if (a.bytes == 0 && a.column >= startCol && rowOff + a.column < matBytes)
                 mat_[rowOff + a.column] ^= 1;
-            const DecSlot& b = slot(rec->elementStart + prng.next() % m.ldpcCount);
+            const DecSlot& b = slot(rec->elementStart + mod(prng.next()));
             if (b.bytes == 0 && b.column >= startCol && rowOff + b.column < matBytes)
                 mat_[rowOff + b.column] ^= rx;
         }
@@ -1144,13 +1137,15 @@ bool DecoderCore::eliminate_original_data()
         }
         sumColumnCount_ = m.sumCount;
 
-        struct T
+        // decoder sums first (their ops precede this row's op)
+        struct DenseTerm
         {
             uint64_t src;
             unsigned len;
             uint8_t acc;
         };
-        std::vector<T> terms;
+        DenseTerm dense[kLanes * 2 * kSums];
+        unsigned nDense = 0;
         for (unsigned lane = 0; lane < kLanes; ++lane) {
             const unsigned op = row_opcode(lane, m.row);
             for (unsigned bit = 0; bit < 2 * kSums; ++bit) {
@@ -1159,26 +1154,32 @@ bool DecoderCore::eliminate_original_data()
                 DevSum& s = get_sum(lane, bit % kSums, ee);
                 if (s.bytes > 0) {
                     materialize(s);
-                    terms.push_back(T{s.buf.addr(), std::min(s.bytes, rb), (uint8_t)(bit / kSums)});
+                    dense[nDense++] = DenseTerm{s.buf.addr(), std::min(s.bytes, rb),
+                                                (uint8_t)(bit / kSums)};
                 }
             }
+        }
+        prog_.lc_begin(rec->buf.addr(), rb, rb, row_value(m.row));
+        uint64_t opBytes = rb; // RX * product muladd
+        for (unsigned k = 0; k < nDense; ++k) {
+            prog_.lc_term(dense[k].src, dense[k].len, 1, dense[k].acc);
+            opBytes += dense[k].len;
         }
         Pcg32 prng;
         prng.seed(m.row, m.ldpcCount);
         const unsigned pairs = (m.ldpcCount + kPairRate - 1) / kPairRate;
+        const FastMod mod(m.ldpcCount ? m.ldpcCount : 1);
         for (unsigned k = 0; k < pairs; ++k) {
-            const DecSlot& a = slot(es + prng.next() % m.ldpcCount);
-            if (a.bytes > 0)
-                terms.push_back(T{a.buf.addr(), std::min(a.bytes, rb), 0});
-            const DecSlot& b = slot(es + prng.next() % m.ldpcCount);
-            if (b.bytes > 0)
-                terms.push_back(T{b.buf.addr(), std::min(b.bytes, rb), 1});
-        }
-        prog_.lc_begin(rec->buf.addr(), rb, rb, row_value(m.row));
-        uint64_t opBytes = rb; // RX * product muladd
-        for (const T& t : terms) {
-            prog_.lc_term(t.src, t.len, 1, t.acc);
-            opBytes += t.len;
+            const DecSlot& a = slot(es + mod(prng.next()));
+            if (a.bytes > 0) {
+                prog_.lc_term(a.buf.addr(), std::min(a.bytes, rb), 1, 0);
+                opBytes += std::min(a.bytes, rb);
+            }
+            const DecSlot& b = slot(es + mod(prng.next()));
+            if (b.bytes > 0) {
+                prog_.lc_term(b.buf.addr(), std::min(b.bytes, rb), 1, 1);
+                opBytes += std::min(b.bytes, rb);
+            }
         }
         prog_.lc_end();
         eng_->account(opBytes);

@@ -211,35 +211,24 @@ DevSum& EncoderCore::get_sum(unsigned lane, unsigned sumIndex, unsigned elementE
     unsigned newBytes = sum.bytes;
     if (L.longest > 0)
         newBytes = std::max(newBytes, L.longest);
-    struct T
-    {
-        uint64_t src;
-        unsigned len;
-        uint8_t c;
-    };
-    std::vector<T> terms;
-    terms.reserve((elementEnd - element) / kLanes + 1);
+    for (unsigned e = element; e < elementEnd; e += kLanes)
+        newBytes = std::max(newBytes, slot(e).bytes);
+    if (!grow_sum(sum, newBytes))
+        return sum;
+    prog_.lc_begin(sum.buf.addr(), sum.bytes, sum.devValid);
+    uint64_t opBytes = 0;
     do {
         const EncSlot& o = slot(element);
-        newBytes = std::max(newBytes, o.bytes);
         uint8_t c = 1;
         if (sumIndex > 0) {
             c = column_value(o.column);
             if (sumIndex == 2)
                 c = gf_sqr(c);
         }
-        terms.push_back(T{o.buf.addr(), o.bytes, c});
+        prog_.lc_term(o.buf.addr(), o.bytes, c);
+        opBytes += o.bytes; // one add/muladd per original in the reference
         element += kLanes;
     } while (element < elementEnd);
-
-    if (!grow_sum(sum, newBytes))
-        return sum;
-    prog_.lc_begin(sum.buf.addr(), sum.bytes, sum.devValid);
-    uint64_t opBytes = 0;
-    for (const T& t : terms) {
-        prog_.lc_term(t.src, t.len, t.c);
-        opBytes += t.len; // one add/muladd per original in the reference
-    }
     prog_.lc_end();
     eng_->account(opBytes);
     sum.devValid = sum.bytes;
@@ -355,15 +344,11 @@ SiameseResult EncoderCore::cauchy_row(EncodeOut& out)
     m.ldpcCount = inFlight;
     m.columnStart = element_to_column(first);
 
-    struct T
-    {
-        uint64_t src;
-        unsigned len;
-        uint8_t c;
-    };
-    std::vector<T> terms;
-    terms.reserve(count_ - first);
     unsigned used = 0;
+    for (unsigned e = first; e < count_; ++e)
+        used = std::max(used, slot(e).bytes);
+    prog_.lc_begin(recovery_.addr(), used, 0);
+    uint64_t opBytes = 0;
 
     const unsigned parityElement = column_to_element(nextParityColumn_);
     if (parityElement <= first || column_delta_negative(parityElement)) {
@@ -371,8 +356,10 @@ SiameseResult EncoderCore::cauchy_row(EncodeOut& out)
         m.row = 0;
         for (unsigned e = first; e < count_; ++e) {
             const EncSlot& o = slot(e);
-            terms.push_back(T{o.buf.addr(), o.bytes, 1});
-            used = std::max(used, o.bytes);
+            prog_.lc_term(o.buf.addr(), o.bytes, 1);
+            // the reference memcpy's the first parity column (no GF op)
+            if (e > first)
+                opBytes += o.bytes;
         }
     } else {
         const unsigned crow = nextCauchyRow_;
@@ -382,19 +369,10 @@ SiameseResult EncoderCore::cauchy_row(EncodeOut& out)
         unsigned ccol = m.columnStart % kCauchyMaxColumns;
         for (unsigned e = first; e < count_; ++e) {
             const EncSlot& o = slot(e);
-            terms.push_back(T{o.buf.addr(), o.bytes, cauchy_element(crow, ccol)});
-            used = std::max(used, o.bytes);
+            prog_.lc_term(o.buf.addr(), o.bytes, cauchy_element(crow, ccol));
+            opBytes += o.bytes;
             ccol = (ccol + 1) % kCauchyMaxColumns;
         }
-    }
-
-    prog_.lc_begin(recovery_.addr(), used, 0);
-    uint64_t opBytes = 0;
-    for (size_t k = 0; k < terms.size(); ++k) {
-        prog_.lc_term(terms[k].src, terms[k].len, terms[k].c);
-        // the reference memcpy's the first parity column (no GF op)
-        if (k > 0 || m.row != 0)
-            opBytes += terms[k].len;
     }
     prog_.lc_end();
     eng_->account(opBytes);
@@ -408,16 +386,17 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     if (!ensure_recovery(recoveryBytes + kMaxFooterBytes))
         return Siamese_Disabled;
 
-    struct T
+    // Dense part (:1046-1098): opcode bits 0-2 feed the row, 3-5 the product.
+    // The lane sums are brought up to date first (their own ops precede the
+    // row's op in the program).
+    struct DenseTerm
     {
         uint64_t src;
         unsigned len;
         uint8_t acc;
     };
-    std::vector<T> terms;
-    terms.reserve(64);
-
-    // Dense part (:1046-1098): opcode bits 0-2 feed the row, 3-5 the product
+    DenseTerm dense[kLanes * 2 * kSums];
+    unsigned nDense = 0;
     for (unsigned lane = 0; lane < kLanes; ++lane) {
         const unsigned opcode = row_opcode(lane, row);
         for (unsigned bit = 0; bit < 2 * kSums; ++bit) {
@@ -427,11 +406,19 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
             if (disabled_)
                 return Siamese_Disabled;
             if (sum.bytes > 0)
-                terms.push_back(T{sum.buf.addr(), std::min(sum.bytes, recoveryBytes),
-                                  (uint8_t)(bit / kSums)});
+                dense[nDense++] = DenseTerm{sum.buf.addr(), std::min(sum.bytes, recoveryBytes),
+                                            (uint8_t)(bit / kSums)};
         }
     }
     sumEnd_ = count_;
+
+    // Recovery = row sums ^ RX * product  (:1232-1233), one fused device op
+    prog_.lc_begin(recovery_.addr(), recoveryBytes, 0, row_value(row));
+    uint64_t opBytes = recoveryBytes; // final RX * product muladd
+    for (unsigned k = 0; k < nDense; ++k) {
+        prog_.lc_term(dense[k].src, dense[k].len, 1, dense[k].acc);
+        opBytes += dense[k].len;
+    }
 
     // Sparse part (:1100-1144): ceil(n/16) PCG-chosen pairs
     const unsigned start = firstUnremoved_;
@@ -439,19 +426,13 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     Pcg32 prng;
     prng.seed(row, n);
     const unsigned pairs = (n + kPairRate - 1) / kPairRate;
+    const FastMod mod(n ? n : 1);
     for (unsigned i = 0; i < pairs; ++i) {
-        const EncSlot& a = slot(start + prng.next() % n);
-        const EncSlot& b = slot(start + prng.next() % n);
-        terms.push_back(T{a.buf.addr(), a.bytes, 0});
-        terms.push_back(T{b.buf.addr(), b.bytes, 1});
-    }
-
-    // Recovery = row sums ^ RX * product  (:1232-1233), one fused device op
-    prog_.lc_begin(recovery_.addr(), recoveryBytes, 0, row_value(row));
-    uint64_t opBytes = recoveryBytes; // final RX * product muladd
-    for (const T& t : terms) {
-        prog_.lc_term(t.src, t.len, 1, t.acc);
-        opBytes += t.len;
+        const EncSlot& a = slot(start + mod(prng.next()));
+        const EncSlot& b = slot(start + mod(prng.next()));
+        prog_.lc_term(a.buf.addr(), a.bytes, 1, 0);
+        prog_.lc_term(b.buf.addr(), b.bytes, 1, 1);
+        opBytes += a.bytes + b.bytes;
     }
     prog_.lc_end();
     eng_->account(opBytes);

@@ -83,7 +83,10 @@ class BatchReport(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("device_ms", ctypes.c_double),
                 ("exec_ms", ctypes.c_double), ("setup_seconds", ctypes.c_double),
                 ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 10),
-                ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64)]
+                ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64),
+                ("phase_seconds", ctypes.c_double * 5)]
+
+PHASES = ("create", "step", "flush", "resolve", "finish")
 
 
 _lib = None
