@@ -101,14 +101,16 @@ def run_rank(rank, world, local, args, library, use_cuda):
     cfg = workload(rank, args.streams)
     sess = S.BatchSession(library, cfg, device=local if use_cuda else -1)
     # untimed warm-up; its first run checks every recovered byte against the payload
-    res, rep = sess.run(steps=0, warmup=max(1, args.warmup), verify=True, threads=args.threads)
+    res, rep = sess.run(steps=0, warmup=max(1, args.warmup), verify=True, threads=args.threads,
+                        groups=args.groups)
     if rep.mismatches or any(r.status for r in res):
         raise RuntimeError("bench: verification failed: %d byte mismatches, status %s"
                            % (rep.mismatches, S.summary(res)["status"]))
 
     coll.barrier()
     t0 = time.perf_counter()
-    res, rep = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads)
+    res, rep = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
+                        groups=args.groups)
     coll.barrier()
     elapsed = time.perf_counter() - t0
     sess.close()
@@ -167,8 +169,12 @@ def run_rank(rank, world, local, args, library, use_cuda):
         },
         "host": {
             "threads": args.threads or "default",
+            "groups": args.groups,
             "phase_ms_per_step": {k: round(v * 1e3 / steps, 3)
                                   for k, v in zip(S.PHASES, rep.phase_seconds)},
+            "engine_ms_per_step": {k[:-3]: round(eng[k] / 1e6 / steps, 3)
+                                   for k in ("assemble_ns", "wait_ns", "complete_ns",
+                                             "reclaim_ns")},
         },
         "roofline": {
             "bound": "hbm",
@@ -200,7 +206,10 @@ def main(argv=None):
     ap.add_argument("--streams", type=int, default=STREAMS_PER_GPU)
     ap.add_argument("--cpu-streams", type=int, default=4096)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--threads", type=int, default=0, help="host threads driving streams (0 = library default)")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="host threads driving streams (0 = library default)")
+    ap.add_argument("--groups", type=int, default=2,
+                    help="stream groups alternating host and device work (1 = no overlap)")
     ap.add_argument("--library", default=S.AMD_LIB, help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 

@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <memory>
 
 extern "C" {
@@ -33,6 +35,7 @@ struct BatchOptions
     uint32_t verify;   ///< check every recovered packet's bytes (first run only)
     int32_t device;    ///< HIP device (-1 = current)
     uint32_t threads;  ///< host threads driving streams (0 = default)
+    uint32_t groups;   ///< stream groups alternating host work and device work (0 = 1)
 };
 
 struct BatchReport
@@ -42,7 +45,7 @@ struct BatchReport
     double exec_ms;        ///< device time of the executor launches only
     double setup_seconds;  ///< payload generation + staging (untimed)
     uint64_t rounds;       ///< rounds (flushes) in the timed steps
-    uint64_t engine[10];   ///< engine counters over the timed steps (see sgpu_engine_stats)
+    uint64_t engine[14];   ///< engine counters over the timed steps (see sgpu_engine_stats)
     uint64_t checked;      ///< packets whose bytes were verified
     uint64_t mismatches;   ///< verification failures
     /// wall time of the timed steps split by phase: codec create, stream
@@ -55,7 +58,7 @@ struct BatchReport
 
 namespace {
 
-constexpr int kEngineStats = 10;
+constexpr int kEngineStats = 14;
 using Clock = std::chrono::steady_clock;
 
 struct Api
@@ -74,6 +77,7 @@ struct Api
     SiameseResult (*decode)(SgpuDecoder, SiameseOriginalPacket**, unsigned*);
     SiameseResult (*decoder_get)(SgpuDecoder, SiameseOriginalPacket*);
     int (*flush)(void);
+    int (*submit)(void);
     void* (*device_alloc)(size_t);
     void (*device_free)(void*);
     int (*h2d)(void*, const void*, size_t);
@@ -106,7 +110,7 @@ bool load_api(const char* path, Api& a)
            bind(h, a.decoder_add_original, "sgpu_decoder_add_original") &&
            bind(h, a.decoder_add_recovery, "sgpu_decoder_add_recovery") &&
            bind(h, a.decoder_is_ready, "sgpu_decoder_is_ready") && bind(h, a.decode, "sgpu_decode") &&
-           bind(h, a.decoder_get, "sgpu_decoder_get") && bind(h, a.flush, "sgpu_flush") &&
+           bind(h, a.decoder_get, "sgpu_decoder_get") && bind(h, a.flush, "sgpu_flush") && bind(h, a.submit, "sgpu_submit") &&
            bind(h, a.device_alloc, "sgpu_device_alloc") && bind(h, a.device_free, "sgpu_device_free") &&
            bind(h, a.h2d, "sgpu_h2d") && bind(h, a.gather, "sgpu_gather") &&
            bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats");
@@ -148,6 +152,7 @@ struct Shared
     bool verify;
     uint64_t checked = 0, mismatches = 0;
     std::unique_ptr<sgpu::WorkerPool> pool;
+    unsigned groups = 1;
 };
 
 struct BatchCodec
@@ -216,9 +221,12 @@ struct BatchCodec
         const unsigned bytes = p.entry ? p.entry->DataBytes : p.bytes;
         const void* data = p.entry ? p.entry->Data : p.data;
         const unsigned want = sh->cfg->payload_bytes ? sh->cfg->payload_bytes : scen::variable_bytes(id);
-        if (bytes != want || !data)
+        if (bytes != want || !data) {
+            if (std::getenv("SCENARIO_DEBUG"))
+                std::fprintf(stderr, "pkt_token: id %u entry %d bytes %u want %u data %p\n", id,
+                             p.entry != nullptr, bytes, want, data);
             *ok = false;
-        else if (sh->hashData || sh->verify)
+        } else if (sh->hashData || sh->verify)
             cur.push_back(Request{log, log->size(), data, bytes, id, true, ok});
         return bytes;
     }
@@ -304,56 +312,97 @@ int run_once(Shared& sh, StreamResult* results, uint64_t* rounds, double* phase)
             streams[s].fail(2);
     });
     lap(0);
-    // requests of every stream that wait for device bytes
-    auto take = [&](bool prev) {
+    // Streams are split into `groups` contiguous groups.  With one group a
+    // round is: step every live stream, then flush and wait.  With two, the
+    // groups alternate: a group's flush is submitted without waiting and
+    // the other group's host work runs while it executes on the device; the
+    // next submit completes it first (sgpu_submit semantics), before that
+    // group steps again.
+    const unsigned G = std::max(1u, std::min(sh.groups, n));
+    auto group_begin = [&](unsigned g) { return (unsigned)((uint64_t)n * g / G); };
+    // requests of group g's streams that wait for device bytes
+    auto take = [&](unsigned g, bool prev) {
         std::vector<Request> reqs;
-        for (BatchCodec& c : codecs) {
-            std::vector<Request>& q = prev ? c.prev : c.cur;
+        for (unsigned s = group_begin(g); s < group_begin(g + 1); ++s) {
+            std::vector<Request>& q = prev ? codecs[s].prev : codecs[s].cur;
             reqs.insert(reqs.end(), q.begin(), q.end());
             q.clear();
         }
         return reqs;
     };
-    std::vector<unsigned> live(n);
-    for (unsigned s = 0; s < n; ++s)
-        live[s] = s;
+    std::vector<std::vector<unsigned>> live(G);
+    for (unsigned g = 0; g < G; ++g)
+        for (unsigned s = group_begin(g); s < group_begin(g + 1); ++s)
+            live[g].push_back(s);
     int rc = 0;
-    while (!live.empty()) {
-        // Every live stream advances until it yields; streams are
-        // independent, so the host threads drive them concurrently.
-        for_streams(sh, live.size(), [&](size_t k) {
-            BatchStream& st = streams[live[k]];
-            while (!st.done())
-                if (st.step())
-                    break;
-        });
-        lap(1);
-        // bytes produced by the previous flush are final now
-        std::vector<Request> reqs = take(true);
-        resolve_requests(sh, reqs);
-        lap(3);
-        if (api.flush() != 0) {
-            rc = -3;
-            break;
+    int inflight = -1;   // group whose flush was submitted last and may still run
+    for (bool any = true; any && rc == 0;) {
+        any = false;
+        for (unsigned g = 0; g < G && rc == 0; ++g) {
+            std::vector<unsigned>& lv = live[g];
+            if (lv.empty())
+                continue;
+            any = true;
+            if (inflight == (int)g) {
+                // no other group submitted since: complete this group's flush
+                if (api.flush() != 0)
+                    rc = -3;
+                inflight = -1;
+                lap(2);
+            }
+            // Every live stream advances until it yields; streams are
+            // independent, so the host threads drive them concurrently.
+            for_streams(sh, lv.size(), [&](size_t k) {
+                BatchStream& st = streams[lv[k]];
+                while (!st.done())
+                    if (st.step())
+                        break;
+            });
+            lap(1);
+            // bytes produced by this group's previous flush are final now
+            std::vector<Request> reqs = take(g, true);
+            resolve_requests(sh, reqs);
+            lap(3);
+            if ((G == 1 ? api.flush() : api.submit()) != 0)
+                rc = -3;
+            inflight = G == 1 ? -1 : (int)g;
+            lap(2);
+            ++*rounds;
+            for (unsigned s = group_begin(g); s < group_begin(g + 1); ++s)
+                std::swap(codecs[s].prev, codecs[s].cur);
+            lv.erase(std::remove_if(lv.begin(), lv.end(),
+                                    [&](unsigned s) { return streams[s].done(); }),
+                     lv.end());
         }
-        lap(2);
-        ++*rounds;
-        for (BatchCodec& c : codecs)
-            std::swap(c.prev, c.cur);
-        live.erase(std::remove_if(live.begin(), live.end(),
-                                  [&](unsigned s) { return streams[s].done(); }),
-                   live.end());
     }
-    std::vector<Request> reqs = take(true);
-    resolve_requests(sh, reqs);
-    reqs = take(false);
-    resolve_requests(sh, reqs);
+    if (api.flush() != 0)
+        rc = -3;
+    lap(2);
+    for (unsigned g = 0; g < G; ++g) {
+        std::vector<Request> reqs = take(g, true);
+        resolve_requests(sh, reqs);
+        reqs = take(g, false);
+        resolve_requests(sh, reqs);
+    }
     lap(3);
     for_streams(sh, n, [&](size_t s) {
         streams[s].finish();
         api.encoder_free(codecs[s].enc);
         api.decoder_free(codecs[s].dec);
     });
+    // debugging aid: SCENARIO_DUMP="<stream index>:<path>" writes that
+    // stream's event log (same format as scenario_run_capi's)
+    if (const char* dump = std::getenv("SCENARIO_DUMP")) {
+        const unsigned idx = (unsigned)std::strtoul(dump, nullptr, 10);
+        const char* path = std::strchr(dump, ':');
+        if (path && idx < n) {
+            if (FILE* f = std::fopen(path + 1, "w")) {
+                for (uint64_t e : streams[idx].log)
+                    std::fprintf(f, "%016llx\n", (unsigned long long)e);
+                std::fclose(f);
+            }
+        }
+    }
     api.flush();
     lap(4);
     return rc;
@@ -441,6 +490,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         const unsigned threads = opt->threads ? opt->threads : sgpu::WorkerPool::default_threads();
         if (!sh.pool || sh.pool->size() != threads)
             sh.pool.reset(new sgpu::WorkerPool(threads));
+        sh.groups = opt->groups ? opt->groups : 1;
         uint64_t rounds = 0;
         double phase[5] = {0, 0, 0, 0, 0};
         uint64_t e0[kEngineStats], e1[kEngineStats];

@@ -238,20 +238,13 @@ SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* t
         be_timing_reset();
 }
 
-SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out10)
+SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out14)
 {
     const EngineStats s = Engine::global()->stats();
-    uint64_t* out9 = out10;
-    out10[9] = s.solveBytes;
-    out9[0] = s.flushes;
-    out9[1] = s.launches;
-    out9[2] = s.ops;
-    out9[3] = s.terms;
-    out9[4] = s.solves;
-    out9[5] = s.ingests;
-    out9[6] = s.uploadBytes;
-    out9[7] = s.refOpBytes;
-    out9[8] = s.outBytes;
+    const uint64_t v[14] = {s.flushes,    s.launches,    s.ops,        s.terms,    s.solves,
+                            s.ingests,    s.uploadBytes, s.refOpBytes, s.outBytes, s.solveBytes,
+                            s.assembleNs, s.waitNs,      s.completeNs, s.reclaimNs};
+    std::memcpy(out14, v, sizeof(v));
 }
 
 } // extern "C"

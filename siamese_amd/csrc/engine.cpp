@@ -4,6 +4,7 @@
 #include "pool.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 
@@ -21,7 +22,22 @@ void EngineStats::add(const EngineStats& o)
     refOpBytes += o.refOpBytes;
     outBytes += o.outBytes;
     solveBytes += o.solveBytes;
+    assembleNs += o.assembleNs;
+    waitNs += o.waitNs;
+    completeNs += o.completeNs;
+    reclaimNs += o.reclaimNs;
 }
+
+namespace {
+
+uint64_t now_ns()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+} // namespace
 
 // ---------------------------------------------------------------------------
 // Program
@@ -475,6 +491,7 @@ void Engine::flush()
               !s->pendingFree.empty();
     if (!any)
         return;
+    const uint64_t t0 = now_ns();
 
     // ---- 1. layout -----------------------------------------------------------
     std::vector<Program*> progs[2];
@@ -678,6 +695,7 @@ void Engine::flush()
     flushStats_.solves += sdescs.size();
     flushStats_.ingests += nIngest;
     flushStats_.uploadBytes += upBytes;
+    flushStats_.assembleNs += now_ns() - t0;
 
     flight_.callbacks.clear();
     for (int g = 0; g < 2; ++g)
@@ -755,22 +773,27 @@ bool Engine::sync()
 {
     if (!flight_.active)
         return true;
+    const uint64_t t0 = now_ns();
     const bool ok = be_sync();
     for (const InFlight::Download& d : flight_.downloads)
         std::memcpy(d.host, downHost_ + d.off, d.bytes);
+    const uint64_t t1 = now_ns();
     const uint32_t* results = (const uint32_t*)downHost_;
     for (auto& cb : flight_.callbacks)
         cb.second(results + cb.first);
     flight_.callbacks.clear();
     flight_.downloads.clear();
     flight_.active = false;
+    const uint64_t t2 = now_ns();
     std::vector<Shard*> shards;
     {
         std::lock_guard<std::mutex> g(shardsMu_);
         for (auto& s : shards_)
             shards.push_back(s.get());
     }
-    for (Shard* s : shards) {
+    // each shard's released buffers go back to its own free lists
+    pool().run(shards.size(), [&](size_t i) {
+        Shard* s = shards[i];
         for (const DevBuf& b : s->flightFree) {
             const size_t cls = cap_class(b.cap);
             if (cls >= s->freeLists.size())
@@ -778,7 +801,11 @@ bool Engine::sync()
             s->freeLists[cls].push_back(b.ptr);
         }
         s->flightFree.clear();
-    }
+    });
+    const uint64_t t3 = now_ns();
+    flushStats_.waitNs += t1 - t0;
+    flushStats_.completeNs += t2 - t1;
+    flushStats_.reclaimNs += t3 - t2;
     return ok;
 }
 

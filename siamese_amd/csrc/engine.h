@@ -143,6 +143,9 @@ struct EngineStats
     // originals produced.
     uint64_t refOpBytes = 0, outBytes = 0;
     uint64_t solveBytes = 0;   // the part of both done by the solve kernels
+    // host time of flush assembly, device waits, completion callbacks and
+    // returning released buffers to the free lists (nanoseconds)
+    uint64_t assembleNs = 0, waitNs = 0, completeNs = 0, reclaimNs = 0;
 
     void add(const EngineStats& o);
 };

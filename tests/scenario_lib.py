@@ -76,13 +76,13 @@ def replace(cfg, **kw):
 class BatchOptions(ctypes.Structure):
     _fields_ = [("steps", ctypes.c_uint32), ("warmup", ctypes.c_uint32),
                 ("verify", ctypes.c_uint32), ("device", ctypes.c_int32),
-                ("threads", ctypes.c_uint32)]
+                ("threads", ctypes.c_uint32), ("groups", ctypes.c_uint32)]
 
 
 class BatchReport(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("device_ms", ctypes.c_double),
                 ("exec_ms", ctypes.c_double), ("setup_seconds", ctypes.c_double),
-                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 10),
+                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 14),
                 ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64),
                 ("phase_seconds", ctypes.c_double * 5)]
 
@@ -123,13 +123,14 @@ def run_capi(library, cfg, threads=1, event_log=None):
     return res, sec.value, wall
 
 
-def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0):
+def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0, groups=1):
     """Run `cfg` through the device-resident batch API (lock-step rounds),
-    streams driven by `threads` host threads (0 = library default).
+    streams driven by `threads` host threads (0 = library default), split
+    into `groups` groups whose host work and device work alternate.
 
     Returns (results of the last run, BatchReport)."""
     res = (StreamResult * cfg.streams)()
-    opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads)
+    opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads, groups)
     rep = BatchReport()
     rc = lib().scenario_run_batch(library.encode(), ctypes.byref(cfg), res, ctypes.byref(opt),
                                   ctypes.byref(rep))
@@ -139,7 +140,7 @@ def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0
 
 
 ENGINE_KEYS = ("flushes launches ops terms solves ingests upload_bytes ref_op_bytes "
-               "out_bytes solve_bytes").split()
+               "out_bytes solve_bytes assemble_ns wait_ns complete_ns reclaim_ns").split()
 
 
 def engine_dict(report):
@@ -163,9 +164,9 @@ class BatchSession:
         if not self.handle:
             raise RuntimeError("scenario_batch_open(%s) failed" % library)
 
-    def run(self, steps=1, warmup=0, verify=False, threads=0):
+    def run(self, steps=1, warmup=0, verify=False, threads=0, groups=1):
         res = (StreamResult * self.cfg.streams)()
-        opt = BatchOptions(steps, warmup, 1 if verify else 0, -1, threads)
+        opt = BatchOptions(steps, warmup, 1 if verify else 0, -1, threads, groups)
         rep = BatchReport()
         rc = lib().scenario_batch_run(self.handle, res, ctypes.byref(opt), ctypes.byref(rep))
         if rc != 0:

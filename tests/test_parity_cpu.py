@@ -51,6 +51,18 @@ def test_hostsim_batch_matches_golden(name):
     assert rep.mismatches == 0
 
 
+@pytest.mark.parametrize("name", ["C2x64", "C1var", "edge_lag", "smoke_C4x8"])
+@pytest.mark.parametrize("threads,groups", [(1, 2), (4, 2), (8, 3)])
+def test_hostsim_batch_threads_and_pipelining(name, threads, groups):
+    """Streams driven from several host threads (per-thread engine shards)
+    and split into groups whose flushes overlap the other groups' host work
+    give the reference's results."""
+    cfg = golden.config(name)
+    res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True, threads=threads, groups=groups)
+    _check(name, res)
+    assert rep.mismatches == 0
+
+
 def test_hostsim_batch_length_only_digest():
     """hash_data=0 digests (used for the full-size GPU runs) also agree."""
     cfg = S.replace(golden.config("C4x256"), streams=32, hash_data=0)
