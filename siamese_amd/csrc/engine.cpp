@@ -701,8 +701,11 @@ void Engine::flush()
     for (int g = 0; g < 2; ++g)
         for (size_t pi = 0; pi < progs[g].size(); ++pi) {
             Program* p = progs[g][pi];
-            for (Completion& fn : p->callbacks_)
-                flight_.callbacks.emplace_back(resultBase[g][pi], std::move(fn));
+            if (!p->callbacks_.empty()) {
+                flight_.callbacks.emplace_back();
+                flight_.callbacks.back().first = resultBase[g][pi];
+                flight_.callbacks.back().second.swap(p->callbacks_);
+            }
             if (p->group_ & 2)
                 delete p;   // orphan of a freed instance (see ~Program)
             else
@@ -778,9 +781,14 @@ bool Engine::sync()
     for (const InFlight::Download& d : flight_.downloads)
         std::memcpy(d.host, downHost_ + d.off, d.bytes);
     const uint64_t t1 = now_ns();
+    // Completions of different programs touch different instances: run them
+    // in parallel, each program's in order.
     const uint32_t* results = (const uint32_t*)downHost_;
-    for (auto& cb : flight_.callbacks)
-        cb.second(results + cb.first);
+    pool().run(flight_.callbacks.size(), [&](size_t i) {
+        auto& cb = flight_.callbacks[i];
+        for (Completion& fn : cb.second)
+            fn(results + cb.first);
+    });
     flight_.callbacks.clear();
     flight_.downloads.clear();
     flight_.active = false;

@@ -228,7 +228,8 @@ private:
             uint32_t bytes;
         };
         std::vector<Download> downloads;
-        std::vector<std::pair<uint32_t, Completion>> callbacks;   // (results base, fn)
+        // per program: (results base, its completions in order)
+        std::vector<std::pair<uint32_t, std::vector<Completion>>> callbacks;
         bool active = false;
     } flight_;
     std::unique_ptr<WorkerPool> pool_;
