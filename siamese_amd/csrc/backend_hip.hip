@@ -158,17 +158,25 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
 // ---------------------------------------------------------------------------
 // Executor
 
-// One workgroup of kExecWaves waves per (instance segment, 1 KiB tile).  All
-// waves walk the segment's op list together; each op's terms are dealt
-// round-robin to the waves (wave w takes terms w, w+W, ...), every wave keeps
-// up to kExecDepth source loads in flight, and the partial sums meet in LDS.
-// Wave 0 then merges the destination's kept prefix/tail and stores; a
-// barrier orders the store before any later op of the segment reads it
-// (stores from one CU are visible to the CU's other waves after the
-// workgroup-scope fence of __syncthreads on gfx950).
+// One workgroup of kExecWaves waves per (instance segment, 1 KiB tile).
+//
+// The segment is one instruction stream (ops.h): each op's header and its
+// term descriptors are contiguous, and the workgroup keeps the current op's
+// block in an LDS ring while one coalesced load per thread prefetches the
+// next op's block, so no op waits on a descriptor round trip.  Each op's
+// terms are dealt round-robin to the waves (wave w takes terms w, w+W, ...),
+// every wave keeps up to kExecDepth source loads in flight, and the partial
+// sums meet in LDS.  Wave 0 merges the destination's kept prefix/tail and
+// stores; the barrier that rotates the ring also orders that store before
+// any later op of the segment reads it (stores from one CU are visible to
+// the CU's other waves after the workgroup-scope fence of __syncthreads).
 constexpr unsigned kExecWaves = 4;
+constexpr unsigned kExecThreads = 64 * kExecWaves;
 constexpr unsigned kExecDepth = 8;
-constexpr unsigned kExecSolo = 4;   // ops with <= this many terms run on wave 0 alone
+constexpr unsigned kExecSolo = 4;            // ops with <= this many terms run on wave 0 alone
+constexpr unsigned kRingWords = kExecThreads; // one prefetched word per thread
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ __forceinline__ uint4 term_value(uint4 x, uint32_t p, uint32_t len, uint32_t coeff)
 {
@@ -179,29 +187,41 @@ __device__ __forceinline__ uint4 term_value(uint4 x, uint32_t p, uint32_t len, u
     return x;
 }
 
-// Accumulate terms k0, k0+stride, ... of one op into acc0/acc1.
-__device__ __forceinline__ void gather_terms(const GfTerm* __restrict__ t, uint32_t nt, uint32_t k0,
-                                             uint32_t stride, uint32_t p, uint4& acc0, uint4& acc1)
+// Word `idx` of the current op's block: from the LDS ring while it lasts,
+// then straight from the stream (ops with more than kRingWords-2 terms).
+__device__ __forceinline__ uint4 op_word(const uint4* ring, const uint4* __restrict__ seg, uint32_t pos,
+                                         uint32_t idx)
+{
+    return idx < kRingWords ? ring[idx] : seg[pos + idx];
+}
+
+// Accumulate terms k0, k0+stride, ... of the current op into acc0/acc1.
+__device__ __forceinline__ void gather_terms(const uint4* ring, const uint4* __restrict__ seg,
+                                             uint32_t pos, uint32_t nt, uint32_t k0, uint32_t stride,
+                                             uint32_t p, uint4& acc0, uint4& acc1)
 {
     for (uint32_t k = k0; k < nt; k += stride * kExecDepth) {
-        GfTerm tt[kExecDepth];
+        uint32_t len[kExecDepth], ca[kExecDepth];
         uint4 v[kExecDepth];
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
             const uint32_t idx = k + u * stride;
             if (idx < nt) {   // wave-uniform
-                tt[u] = t[idx];
+                const uint4 w = op_word(ring, seg, pos, kOpWords + idx);
+                const uint64_t src = ((uint64_t)uni(w.y) << 32) | uni(w.x);
+                len[u] = uni(w.z);
+                ca[u] = uni(w.w);   // coeff | acc << 8
                 // lanes past the term's end load the term's first line (always
                 // mapped) and mask it away, so no load sits behind a branch
-                v[u] = ld16(tt[u].src + (p < tt[u].len ? p : 0));
+                v[u] = ld16(src + (p < len[u] ? p : 0));
             }
         }
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
             const uint32_t idx = k + u * stride;
             if (idx < nt) {
-                const uint4 x = term_value(v[u], p, tt[u].len, tt[u].coeff);
-                if (tt[u].acc)
+                const uint4 x = term_value(v[u], p, len[u], ca[u] & 0xff);
+                if (ca[u] & 0xff00)
                     acc1 = xor16(acc1, x);
                 else
                     acc0 = xor16(acc0, x);
@@ -210,65 +230,78 @@ __device__ __forceinline__ void gather_terms(const GfTerm* __restrict__ t, uint3
     }
 }
 
-__global__ __launch_bounds__(64 * kExecWaves) void k_exec(const GfOp* __restrict__ ops,
-                                                          const GfTerm* __restrict__ terms,
-                                                          const ExecItem* __restrict__ items)
+__global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
+                                                       const ExecItem* __restrict__ items)
 {
+    __shared__ uint4 ring[2][kRingWords];
     __shared__ uint4 part[kExecWaves - 1][64];
     const ExecItem it = items[blockIdx.x];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint4* seg = stream + it.streamBegin;
+    const uint32_t words = it.streamWords;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const uint32_t wave = tid >> 6;
     const uint32_t p = it.tileBase + lane * 16;
 
+    ring[0][tid] = tid < words ? seg[tid] : make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    uint32_t cur = 0, pos = 0;
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
-        const GfOp op = ops[it.opBegin + oi];
-        if (op.kind == OP_LITERAL) {
-            if (wave == 0) {
-                const uint32_t a = op.n, b = op.n + op.valid;
-                if (b > p && a < p + 16) {
-                    uint8_t* dst = reinterpret_cast<uint8_t*>(op.dst);
-                    for (uint32_t k = (a > p ? a : p); k < b && k < p + 16; ++k)
-                        dst[k] = op.lit[k - a];
-                }
-            }
-            __syncthreads();
-            continue;
-        }
-        if (it.tileBase >= op.n)
-            continue;   // op does not reach this tile (uniform over the workgroup)
+        const uint4* rb = ring[cur];
+        const uint4 h0 = rb[0], h1 = rb[1];   // GfOp: dst, n, valid | kind, mix, lit/terms
+        const uint64_t dst = ((uint64_t)uni(h0.y) << 32) | uni(h0.x);
+        const uint32_t n = uni(h0.z), valid = uni(h0.w);
+        const uint32_t kind = uni(h1.x), mix = uni(h1.y);
+        const uint32_t nt = kind == OP_LINCOMB ? uni(h1.w) : 0;
+        const uint32_t next = pos + kOpWords + nt;
+        // prefetch the next op's block while this one runs
+        uint4 pf = make_uint4(0, 0, 0, 0);
+        if (oi + 1 < it.opCount && next + tid < words)
+            pf = seg[next + tid];
 
-        const GfTerm* t = terms + op.termBegin;
-        const uint32_t nt = op.termCount;
-        const bool solo = nt <= kExecSolo;
-        uint4 acc0 = make_uint4(0, 0, 0, 0);
-        uint4 acc1 = make_uint4(0, 0, 0, 0);
-        if (!solo || wave == 0)
-            gather_terms(t, nt, solo ? 0 : wave, solo ? 1 : kExecWaves, p, acc0, acc1);
-        if (op.mix > 1)
-            acc1 = gf_mul16(acc1, op.mix);
-        uint4 out = xor16(acc0, acc1);
-        if (!solo) {
-            if (wave != 0)
-                part[wave - 1][lane] = out;
-            __syncthreads();
-        }
-        if (wave == 0) {
-            if (!solo) {
-#pragma unroll
-                for (unsigned w = 0; w + 1 < kExecWaves; ++w)
-                    out = xor16(out, part[w][lane]);
+        if (kind == OP_LITERAL) {
+            if (wave == 0 && n + valid > p && n < p + 16) {
+                const uint32_t lit[2] = {uni(h1.z), uni(h1.w)};
+                uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+                for (uint32_t k = (n > p ? n : p); k < n + valid && k < p + 16; ++k)
+                    d[k] = (uint8_t)(lit[(k - n) >> 2] >> (8 * ((k - n) & 3)));
             }
-            if (p < op.n) {
-                if (p < op.valid) {
-                    uint4 prior = ld16(op.dst + p);
-                    if (p + 16 > op.valid)
-                        prior = mask16(prior, (int)op.valid - (int)p);
+        } else if (it.tileBase < n) {   // uniform: the op reaches this tile
+            const bool solo = nt <= kExecSolo;
+            // wave 0 fetches what it merges at the end while the terms stream in
+            uint4 prior = make_uint4(0, 0, 0, 0), old = make_uint4(0, 0, 0, 0);
+            if (wave == 0 && p < n) {
+                if (p < valid)
+                    prior = ld16(dst + p);
+                if (p + 16 > n)
+                    old = ld16(dst + p);
+            }
+            uint4 acc0 = make_uint4(0, 0, 0, 0);
+            uint4 acc1 = make_uint4(0, 0, 0, 0);
+            if (!solo || wave == 0)
+                gather_terms(rb, seg, pos, nt, solo ? 0 : wave, solo ? 1 : kExecWaves, p, acc0, acc1);
+            if (mix > 1)
+                acc1 = gf_mul16(acc1, mix);
+            uint4 out = xor16(acc0, acc1);
+            if (!solo) {
+                if (wave != 0)
+                    part[wave - 1][lane] = out;
+                __syncthreads();
+            }
+            if (wave == 0 && p < n) {
+                if (!solo) {
+#pragma unroll
+                    for (unsigned w = 0; w + 1 < kExecWaves; ++w)
+                        out = xor16(out, part[w][lane]);
+                }
+                if (p < valid) {
+                    if (p + 16 > valid)
+                        prior = mask16(prior, (int)valid - (int)p);
                     out = xor16(out, prior);
                 }
-                if (p + 16 > op.n) {
+                if (p + 16 > n) {
                     // keep dst bytes at and beyond n
-                    const int nb = (int)op.n - (int)p;
-                    const uint4 old = ld16(op.dst + p);
+                    const int nb = (int)n - (int)p;
                     const uint4 keep = make_uint4(~byte_mask(nb), ~byte_mask(nb - 4),
                                                   ~byte_mask(nb - 8), ~byte_mask(nb - 12));
                     out = mask16(out, nb);
@@ -277,10 +310,13 @@ __global__ __launch_bounds__(64 * kExecWaves) void k_exec(const GfOp* __restrict
                     out.z |= old.z & keep.z;
                     out.w |= old.w & keep.w;
                 }
-                st16(op.dst + p, out);
+                st16(dst + p, out);
             }
         }
+        ring[cur ^ 1][tid] = pf;
         __syncthreads();
+        cur ^= 1;
+        pos = next;
     }
 }
 
@@ -406,37 +442,77 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 constexpr unsigned kSolveWaves = 4;
 constexpr unsigned kSolveLdsMaxRows = 120;
 
+// LDS bytes of the staged solve: row tiles, the transposed coefficient
+// matrix, per-row lengths and the result words.
+__host__ __device__ constexpr uint32_t solve_lds_bytes(uint32_t m)
+{
+    return m * 1024u + ((m * m + 15u) & ~15u) + m * 12u + (m + 1u) * 4u;
+}
+
 __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow* __restrict__ R,
                                const uint8_t* __restrict__ C, const uint32_t* __restrict__ res,
                                uint32_t tileBase)
 {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const uint32_t wave = tid >> 6;
     const uint32_t p = tileBase + lane * 16;
+    // Everything the sweeps consult goes to LDS first, so no step of the
+    // serial pivot chain waits on a global-memory round trip.
+    uint8_t* Ct = reinterpret_cast<uint8_t*>(X + m * 64);        // Ct[i*m + j] = C[j][i]
+    uint32_t* initB = reinterpret_cast<uint32_t*>(Ct + ((m * m + 15u) & ~15u));
+    uint32_t* lowL = initB + m;
+    uint32_t* finB = lowL + m;
+    uint32_t* rw = finB + m;                                     // result words
 
-    for (uint32_t j = wave; j < m; j += kSolveWaves) {
-        const uint32_t ib = R[j].initBytes;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (p < ib) {
-            v = ld16(R[j].buf + p);
-            if (p + 16 > ib)
-                v = mask16(v, (int)ib - (int)p);
+    for (uint32_t k = tid; k < m * m; k += 64 * kSolveWaves) {
+        const uint32_t j = k / m, i = k - j * m;
+        Ct[i * m + j] = C[k];
+    }
+    for (uint32_t j = tid; j < m; j += 64 * kSolveWaves) {
+        initB[j] = R[j].initBytes;
+        lowL[j] = R[j].lowerLen;
+        finB[j] = R[j].finalBytes;
+    }
+    for (uint32_t k = tid; k <= m; k += 64 * kSolveWaves)
+        rw[k] = res[k];
+    // row tiles: wave w stages rows w, w+W, ... four loads in flight per lane
+    for (uint32_t j0 = wave; j0 < m; j0 += 4 * kSolveWaves) {
+        uint4 v[4];
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+            const uint32_t j = j0 + u * kSolveWaves;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (j < m) {
+                const uint32_t ib = R[j].initBytes;
+                if (p < ib) {
+                    v[u] = ld16(R[j].buf + p);
+                    if (p + 16 > ib)
+                        v[u] = mask16(v[u], (int)ib - (int)p);
+                }
+            }
         }
-        X[j * 64 + lane] = v;
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+            const uint32_t j = j0 + u * kSolveWaves;
+            if (j < m)
+                X[j * 64 + lane] = v[u];
+        }
     }
     __syncthreads();
 
     // MultiplyLowerTriangle in pivot order (reference SiameseDecoder.cpp:1065-1104)
     for (uint32_t i = 0; i + 1 < m; ++i) {
-        const uint32_t L = R[i].lowerLen;
+        const uint32_t L = lowL[i];
         if (tileBase >= L)
             continue;   // uniform: row i contributes nothing to this tile
         uint4 src = X[i * 64 + lane];
         if (p + 16 > L)
             src = mask16(src, (int)L - (int)p);
+        const uint8_t* col = Ct + i * m;
         const uint32_t first = i + 1 + ((wave + kSolveWaves - (i + 1) % kSolveWaves) % kSolveWaves);
         for (uint32_t j = first; j < m; j += kSolveWaves) {
-            const uint32_t y = C[(size_t)j * m + i];
+            const uint32_t y = col[j];
             if (y)
                 X[j * 64 + lane] = xor16(X[j * 64 + lane], gf_mul16(src, y));
         }
@@ -444,23 +520,22 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
     }
 
     // BackSubstitution from the right-most column (reference :1106-1238)
-    const uint32_t ok = res[0];
+    const uint32_t ok = rw[0];
     uint32_t done = 0;
     for (int i = (int)m - 1; i >= 0 && done < ok; --i, ++done) {
-        const uint32_t w = res[1 + i];
+        const uint32_t w = rw[1 + i];
         const uint32_t bb = (w >> 29) + (w & kSolveLengthMask);
-        const uint32_t y = C[(size_t)i * m + i];
-        uint4 x = gf_mul16(X[i * 64 + lane], c_inv[y]);
+        const uint8_t* col = Ct + (uint32_t)i * m;
+        uint4 x = gf_mul16(X[i * 64 + lane], c_inv[col[i]]);
         x = mask16(x, (int)bb - (int)p); // zero beyond the recovered length
-        if ((uint32_t)i % kSolveWaves == wave && p < R[i].finalBytes)
+        if ((uint32_t)i % kSolveWaves == wave && p < finB[i])
             st16(R[i].buf + p, x);
         if (tileBase < bb) {
-            const uint32_t first = wave;
-            for (uint32_t j = first; j < (uint32_t)i; j += kSolveWaves) {
-                const uint32_t c = C[(size_t)j * m + i];
+            for (uint32_t j = wave; j < (uint32_t)i; j += kSolveWaves) {
+                const uint32_t c = col[j];
                 if (!c)
                     continue;
-                const uint32_t ab = bb < R[j].finalBytes ? bb : R[j].finalBytes;
+                const uint32_t ab = bb < finB[j] ? bb : finB[j];
                 const uint4 xs = mask16(x, (int)ab - (int)p);
                 X[j * 64 + lane] = xor16(X[j * 64 + lane], gf_mul16(xs, c));
             }
@@ -469,7 +544,7 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
     }
     // rows the back-substitution did not reach
     for (uint32_t j = wave; j + done < m; j += kSolveWaves)
-        if (p < R[j].finalBytes)
+        if (p < finB[j])
             st16(R[j].buf + p, X[j * 64 + lane]);
 }
 
@@ -562,7 +637,9 @@ namespace {
 hipStream_t g_stream = nullptr;
 bool g_ready = false;
 bool g_timing = false;
-uint32_t g_solveLdsRows = 64;   // raised at init if the device grants more dynamic LDS
+// largest m staged in LDS: 56 keeps solve_lds_bytes under the default 64 KiB
+// dynamic-LDS limit; raised at init when the device grants more
+uint32_t g_solveLdsRows = 56;
 double g_execMs = 0, g_totalMs = 0;
 
 struct EvPair
@@ -665,7 +742,7 @@ bool be_init(int device, const char** err)
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_inv), g_gf.inv, 256), "hipMemcpyToSymbol(inv)");
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_main),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kSolveLdsMaxRows * 64 * sizeof(uint4))) == hipSuccess)
+                            (int)solve_lds_bytes(kSolveLdsMaxRows)) == hipSuccess)
         g_solveLdsRows = kSolveLdsMaxRows;
     if (hipDeviceSynchronize() != hipSuccess) {
         *err = "device synchronisation failed during init";
@@ -729,10 +806,13 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count)
                        dim3(64 * kIngestWaves), 0, g_stream, descs, count);
 }
 
-void be_launch_exec(const GfOp* ops, const GfTerm* terms, const ExecItem* items, uint32_t count)
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count)
 {
+    if (count == 0)
+        return;
     Timed t(true);
-    hipLaunchKernelGGL(k_exec, dim3(count), dim3(64 * kExecWaves), 0, g_stream, ops, terms, items);
+    hipLaunchKernelGGL(k_exec, dim3(count), dim3(kExecThreads), 0, g_stream,
+                       static_cast<const uint4*>(stream), items);
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
@@ -752,8 +832,8 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
     Timed t(false);
     const uint32_t ldsRows = maxRows < g_solveLdsRows ? maxRows : g_solveLdsRows;
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
-                       (size_t)ldsRows * 64 * sizeof(uint4), g_stream, solves, rows, coef, results,
-                       items, ldsRows);
+                       (size_t)solve_lds_bytes(ldsRows), g_stream, solves, rows, coef, results, items,
+                       ldsRows);
 }
 
 bool be_sync()

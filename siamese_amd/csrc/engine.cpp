@@ -463,7 +463,7 @@ struct SegRef
 {
     Program* prog;
     uint32_t seg;
-    uint32_t opBase, termBase, itemBase;
+    uint32_t wordBase, words, itemBase;
 };
 
 struct ShardRef
@@ -513,7 +513,7 @@ void Engine::flush()
     std::vector<SolveRow> srows;
     std::vector<uint8_t> coef;
     std::vector<SolveItem> sitems;
-    size_t nOps = 0, nTerms = 0, nItems = 0;
+    size_t nOps = 0, nTerms = 0, nWords = 0, nItems = 0;
     for (int g = 0; g < 2; ++g) {
         size_t maxSegs = 0;
         for (Program* p : progs[g])
@@ -526,10 +526,12 @@ void Engine::flush()
                 const Program::Segment& s = p->segs_[k];
                 if (s.ops.empty())
                     continue;
-                segs.push_back(SegRef{p, (uint32_t)k, (uint32_t)nOps, (uint32_t)nTerms,
+                const size_t words = kOpWords * s.ops.size() + s.terms.size();
+                segs.push_back(SegRef{p, (uint32_t)k, (uint32_t)nWords, (uint32_t)words,
                                       (uint32_t)nItems});
                 nOps += s.ops.size();
                 nTerms += s.terms.size();
+                nWords += words;
                 nItems += (s.maxExtent + kTileBytes - 1) / kTileBytes;
             }
             ex.itemCount = nItems - ex.itemBegin;
@@ -574,10 +576,8 @@ void Engine::flush()
     off = align16(off + stageBytes);
     const size_t oIngD = off;
     off = align16(off + nIngest * sizeof(IngestDesc));
-    const size_t oOps = off;
-    off = align16(off + nOps * sizeof(GfOp));
-    const size_t oTerms = off;
-    off = align16(off + nTerms * sizeof(GfTerm));
+    const size_t oStream = off;
+    off = align16(off + nWords * 16);
     const size_t oItems = off;
     off = align16(off + nItems * sizeof(ExecItem));
     const size_t oSD = off;
@@ -612,19 +612,20 @@ void Engine::flush()
         if (t.kind == 0) {
             const SegRef& r = segs[t.a];
             const Program::Segment& s = r.prog->segs_[r.seg];
-            GfOp* ops = (GfOp*)(up + oOps) + r.opBase;
-            for (size_t i = 0; i < s.ops.size(); ++i) {
-                GfOp op = s.ops[i];
-                if (op.kind == OP_LINCOMB)
-                    op.termBegin += r.termBase;
-                ops[i] = op;
+            uint8_t* w = up + oStream + (size_t)r.wordBase * 16;
+            for (const GfOp& op : s.ops) {
+                std::memcpy(w, &op, sizeof(GfOp));
+                w += sizeof(GfOp);
+                if (op.kind == OP_LINCOMB && op.termCount) {
+                    const size_t bytes = (size_t)op.termCount * sizeof(GfTerm);
+                    std::memcpy(w, s.terms.data() + op.termBegin, bytes);
+                    w += bytes;
+                }
             }
-            std::memcpy((GfTerm*)(up + oTerms) + r.termBase, s.terms.data(),
-                        s.terms.size() * sizeof(GfTerm));
             ExecItem* items = (ExecItem*)(up + oItems) + r.itemBase;
             uint32_t n = 0;
             for (uint32_t tb = 0; tb < s.maxExtent; tb += kTileBytes)
-                items[n++] = ExecItem{r.opBase, (uint32_t)s.ops.size(), tb, 0};
+                items[n++] = ExecItem{r.wordBase, r.words, (uint32_t)s.ops.size(), tb};
         } else {
             const ShardRef& sr = srefs[t.a];
             const Shard& s = *sr.shard;
@@ -668,8 +669,8 @@ void Engine::flush()
     uint32_t* resultsDev = (uint32_t*)downDev_;
     for (const Phase& ph : phases) {
         if (ph.kind == Phase::EXEC) {
-            be_launch_exec((const GfOp*)(upDev_ + oOps), (const GfTerm*)(upDev_ + oTerms),
-                           (const ExecItem*)(upDev_ + oItems) + ph.itemBegin, (uint32_t)ph.itemCount);
+            be_launch_exec(upDev_ + oStream, (const ExecItem*)(upDev_ + oItems) + ph.itemBegin,
+                           (uint32_t)ph.itemCount);
         } else {
             const SolveDesc* sd = (const SolveDesc*)(upDev_ + oSD) + ph.solveBegin;
             be_launch_solve_prefix(sd, (const SolveRow*)(upDev_ + oSR), upDev_ + oCoef, resultsDev,

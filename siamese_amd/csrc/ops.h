@@ -56,13 +56,24 @@ struct GfOp
 static_assert(sizeof(GfOp) == 32, "GfOp layout");
 static_assert(sizeof(GfTerm) == 16, "GfTerm layout");
 
+/// On the device a segment is one instruction stream of 16-byte words: each
+/// op is its GfOp (2 words) followed, for OP_LINCOMB, by its termCount
+/// GfTerm words (termBegin is unused there).  A workgroup streams through it
+/// front to back, so one coalesced prefetch brings an op and its term list.
+constexpr unsigned kOpWords = sizeof(GfOp) / 16;
+
+inline uint32_t op_words(const GfOp& op)
+{
+    return kOpWords + (op.kind == OP_LINCOMB ? op.termCount : 0);
+}
+
 /// Executor work item: one (instance segment, byte tile).
 struct ExecItem
 {
-    uint32_t opBegin;
+    uint32_t streamBegin;  // first 16-byte word of the segment's stream
+    uint32_t streamWords;  // words in the segment's stream
     uint32_t opCount;
-    uint32_t tileBase;  // first byte of this tile
-    uint32_t pad;
+    uint32_t tileBase;     // first byte of this tile
 };
 
 /// Triangular solve of one decode (reference SiameseDecoder.cpp:1065-1238).

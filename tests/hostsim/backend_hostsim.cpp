@@ -88,10 +88,19 @@ int parse_prefix(const uint8_t* b, unsigned avail, unsigned* len)
 
 inline uint8_t* P(uint64_t a) { return reinterpret_cast<uint8_t*>(a); }
 
-void exec_tile(const GfOp* ops, const GfTerm* terms, const ExecItem& it)
+void exec_tile(const uint8_t* stream, const ExecItem& it)
 {
+    const uint8_t* w = stream + (size_t)it.streamBegin * 16;
+    const uint8_t* end = w + (size_t)it.streamWords * 16;
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
-        const GfOp& op = ops[it.opBegin + oi];
+        GfOp op;
+        std::memcpy(&op, w, sizeof(op));
+        const GfTerm* terms = reinterpret_cast<const GfTerm*>(w + sizeof(GfOp));
+        w += (size_t)op_words(op) * 16;
+        if (w > end)
+            std::abort(); // malformed stream
+        if (op.kind == OP_LINCOMB)
+            op.termBegin = 0; // terms follow the op in the stream
         const uint32_t t0 = it.tileBase, t1 = it.tileBase + kTileBytes;
         if (op.kind == OP_LITERAL) {
             for (uint32_t k = 0; k < op.valid; ++k) {
@@ -199,12 +208,12 @@ static bool noexec()
     return v == 1;
 }
 
-void be_launch_exec(const GfOp* ops, const GfTerm* terms, const ExecItem* items, uint32_t count)
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count)
 {
     if (noexec())
         return;
     for (uint32_t i = 0; i < count; ++i)
-        exec_tile(ops, terms, items[i]);
+        exec_tile(static_cast<const uint8_t*>(stream), items[i]);
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
