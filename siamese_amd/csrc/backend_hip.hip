@@ -502,8 +502,11 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
     __syncthreads();
 
     // MultiplyLowerTriangle in pivot order (reference SiameseDecoder.cpp:1065-1104)
+    // LDS values read by every lane alike are moved to scalar registers
+    // (uni), so the GF multiplier tables are fetched with scalar loads and
+    // the branches around the barriers are visibly uniform.
     for (uint32_t i = 0; i + 1 < m; ++i) {
-        const uint32_t L = lowL[i];
+        const uint32_t L = uni(lowL[i]);
         if (tileBase >= L)
             continue;   // uniform: row i contributes nothing to this tile
         uint4 src = X[i * 64 + lane];
@@ -512,7 +515,7 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
         const uint8_t* col = Ct + i * m;
         const uint32_t first = i + 1 + ((wave + kSolveWaves - (i + 1) % kSolveWaves) % kSolveWaves);
         for (uint32_t j = first; j < m; j += kSolveWaves) {
-            const uint32_t y = col[j];
+            const uint32_t y = uni(col[j]);
             if (y)
                 X[j * 64 + lane] = xor16(X[j * 64 + lane], gf_mul16(src, y));
         }
@@ -520,22 +523,23 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
     }
 
     // BackSubstitution from the right-most column (reference :1106-1238)
-    const uint32_t ok = rw[0];
+    const uint32_t ok = uni(rw[0]);
     uint32_t done = 0;
     for (int i = (int)m - 1; i >= 0 && done < ok; --i, ++done) {
-        const uint32_t w = rw[1 + i];
+        const uint32_t w = uni(rw[1 + i]);
         const uint32_t bb = (w >> 29) + (w & kSolveLengthMask);
         const uint8_t* col = Ct + (uint32_t)i * m;
-        uint4 x = gf_mul16(X[i * 64 + lane], c_inv[col[i]]);
+        uint4 x = gf_mul16(X[i * 64 + lane], c_inv[uni(col[i])]);
         x = mask16(x, (int)bb - (int)p); // zero beyond the recovered length
         if ((uint32_t)i % kSolveWaves == wave && p < finB[i])
             st16(R[i].buf + p, x);
         if (tileBase < bb) {
             for (uint32_t j = wave; j < (uint32_t)i; j += kSolveWaves) {
-                const uint32_t c = col[j];
+                const uint32_t c = uni(col[j]);
                 if (!c)
                     continue;
-                const uint32_t ab = bb < finB[j] ? bb : finB[j];
+                const uint32_t fj = uni(finB[j]);
+                const uint32_t ab = bb < fj ? bb : fj;
                 const uint4 xs = mask16(x, (int)ab - (int)p);
                 X[j * 64 + lane] = xor16(X[j * 64 + lane], gf_mul16(xs, c));
             }
