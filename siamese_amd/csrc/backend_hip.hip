@@ -195,22 +195,24 @@ __device__ __forceinline__ uint4 op_word(const uint4* ring, const uint4* __restr
     return idx < kRingWords ? ring[idx] : seg[pos + idx];
 }
 
-// Accumulate terms k0, k0+stride, ... of the current op into acc0/acc1.
-__device__ __forceinline__ void gather_terms(const uint4* ring, const uint4* __restrict__ seg,
-                                             uint32_t pos, uint32_t nt, uint32_t k0, uint32_t stride,
-                                             uint32_t p, uint4& acc0, uint4& acc1)
+// Accumulate terms k0, k0+stride, ... (k < nt) into acc0/acc1.  fetch(k,
+// src, len, ca) describes term k (ca = coeff | acc << 8) and returns false
+// for an absent term; every argument is wave-uniform, so the loads of up to
+// kExecDepth terms are issued back to back before the first one is used.
+template <class Fetch>
+__device__ __forceinline__ void gather(uint32_t nt, uint32_t k0, uint32_t stride, uint32_t p,
+                                       uint4& acc0, uint4& acc1, const Fetch& fetch)
 {
     for (uint32_t k = k0; k < nt; k += stride * kExecDepth) {
         uint32_t len[kExecDepth], ca[kExecDepth];
+        bool act[kExecDepth];
         uint4 v[kExecDepth];
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
             const uint32_t idx = k + u * stride;
-            if (idx < nt) {   // wave-uniform
-                const uint4 w = op_word(ring, seg, pos, kOpWords + idx);
-                const uint64_t src = ((uint64_t)uni(w.y) << 32) | uni(w.x);
-                len[u] = uni(w.z);
-                ca[u] = uni(w.w);   // coeff | acc << 8
+            uint64_t src = 0;
+            act[u] = idx < nt && fetch(idx, src, len[u], ca[u]);
+            if (act[u]) {
                 // lanes past the term's end load the term's first line (always
                 // mapped) and mask it away, so no load sits behind a branch
                 v[u] = ld16(src + (p < len[u] ? p : 0));
@@ -218,8 +220,7 @@ __device__ __forceinline__ void gather_terms(const uint4* ring, const uint4* __r
         }
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
-            const uint32_t idx = k + u * stride;
-            if (idx < nt) {
+            if (act[u]) {
                 const uint4 x = term_value(v[u], p, len[u], ca[u] & 0xff);
                 if (ca[u] & 0xff00)
                     acc1 = xor16(acc1, x);
@@ -230,11 +231,76 @@ __device__ __forceinline__ void gather_terms(const uint4* ring, const uint4* __r
     }
 }
 
+__device__ __forceinline__ void read_term(uint4 w, uint64_t& src, uint32_t& len)
+{
+    src = ((uint64_t)uni(w.y) << 32) | uni(w.x);
+    len = uni(w.z);
+}
+
+__device__ __forceinline__ uint32_t word_u16(uint4 w, uint32_t i)
+{
+    // 16-bit element i (0..7) of a 16-byte word
+    const uint32_t d = (i >> 1) == 0 ? w.x : (i >> 1) == 1 ? w.y : (i >> 1) == 2 ? w.z : w.w;
+    return (uni(d) >> (16 * (i & 1))) & 0xffff;
+}
+
+// Finish one linear combination on this lane's 16 bytes: merge the other
+// waves' partial sums (LDS), keep dst's prefix [0,valid) and tail [n, ...),
+// store, then write `litLen` literal bytes at dst+n.  `prior` and `old` were
+// loaded by wave 0 when the item started.
+__device__ __forceinline__ void finish_item(uint4 out, bool solo, uint4 (*part)[64], uint32_t wave,
+                                            uint32_t lane, uint32_t p, uint64_t dst, uint32_t n,
+                                            uint32_t valid, uint4 prior, uint4 old,
+                                            const uint32_t* lit, uint32_t litLen)
+{
+    if (!solo) {
+        if (wave != 0)
+            part[wave - 1][lane] = out;
+        __syncthreads();
+    }
+    if (wave != 0)
+        return;
+    if (p < n) {
+        if (!solo) {
+#pragma unroll
+            for (unsigned w = 0; w + 1 < kExecWaves; ++w)
+                out = xor16(out, part[w][lane]);
+        }
+        if (p < valid) {
+            if (p + 16 > valid)
+                prior = mask16(prior, (int)valid - (int)p);
+            out = xor16(out, prior);
+        }
+        if (p + 16 > n) {
+            // keep dst bytes at and beyond n
+            const int nb = (int)n - (int)p;
+            const uint4 keep = make_uint4(~byte_mask(nb), ~byte_mask(nb - 4), ~byte_mask(nb - 8),
+                                          ~byte_mask(nb - 12));
+            out = mask16(out, nb);
+            out.x |= old.x & keep.x;
+            out.y |= old.y & keep.y;
+            out.z |= old.z & keep.z;
+            out.w |= old.w & keep.w;
+        }
+        st16(dst + p, out);
+    }
+    if (litLen && n + litLen > p && n < p + 16) {
+        uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+        for (uint32_t k = (n > p ? n : p); k < n + litLen && k < p + 16; ++k)
+            d[k] = (uint8_t)(lit[(k - n) >> 2] >> (8 * ((k - n) & 3)));
+    }
+}
+
+constexpr unsigned kRowsTableLds = 256;   // table entries of an OP_ROWS batch kept in LDS
+constexpr unsigned kRowsSums = 24;
+
 __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
                                                        const ExecItem* __restrict__ items)
 {
     __shared__ uint4 ring[2][kRingWords];
     __shared__ uint4 part[kExecWaves - 1][64];
+    __shared__ uint4 sumsL[kRowsSums];
+    __shared__ uint4 tableL[kRowsTableLds];
     const ExecItem it = items[blockIdx.x];
     const uint4* seg = stream + it.streamBegin;
     const uint32_t words = it.streamWords;
@@ -246,15 +312,22 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     ring[0][tid] = tid < words ? seg[tid] : make_uint4(0, 0, 0, 0);
     __syncthreads();
     uint32_t cur = 0, pos = 0;
+    uint32_t rowsLeft = 0, tableBase = 0;   // state of the current OP_ROWS batch
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
         const uint4* rb = ring[cur];
-        const uint4 h0 = rb[0], h1 = rb[1];   // GfOp: dst, n, valid | kind, mix, lit/terms
+        const uint4 h0 = rb[0], h1 = rb[1];
         const uint64_t dst = ((uint64_t)uni(h0.y) << 32) | uni(h0.x);
         const uint32_t n = uni(h0.z), valid = uni(h0.w);
-        const uint32_t kind = uni(h1.x), mix = uni(h1.y);
-        const uint32_t nt = kind == OP_LINCOMB ? uni(h1.w) : 0;
-        const uint32_t next = pos + kOpWords + nt;
-        // prefetch the next op's block while this one runs
+        const uint32_t kind = rowsLeft ? (uint32_t)OP_ROW : uni(h1.x);
+        uint32_t itemWords = kOpWords;
+        if (kind == OP_LINCOMB)
+            itemWords += uni(h1.w);
+        else if (kind == OP_ROWS)
+            itemWords += uni(h1.w);   // S + T descriptor words
+        else if (kind == OP_ROW)
+            itemWords = kRowWords + ((uni(h1.x) >> 8) + kPicksPerWord - 1) / kPicksPerWord;
+        const uint32_t next = pos + itemWords;
+        // prefetch the next item's block while this one runs
         uint4 pf = make_uint4(0, 0, 0, 0);
         if (oi + 1 < it.opCount && next + tid < words)
             pf = seg[next + tid];
@@ -266,11 +339,20 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 for (uint32_t k = (n > p ? n : p); k < n + valid && k < p + 16; ++k)
                     d[k] = (uint8_t)(lit[(k - n) >> 2] >> (8 * ((k - n) & 3)));
             }
-        } else if (it.tileBase < n) {   // uniform: the op reaches this tile
-            const bool solo = nt <= kExecSolo;
-            // wave 0 fetches what it merges at the end while the terms stream in
+        } else if (kind == OP_ROWS) {
+            // batch prologue: stage the lane-sum descriptors and the first
+            // kRowsTableLds table entries; the rows follow as items
+            const uint32_t S = uni(h1.y), T = valid;
+            rowsLeft = n;
+            tableBase = pos + kOpWords + S;
+            if (tid < S)
+                sumsL[tid] = op_word(rb, seg, pos, kOpWords + tid);
+            if (tid < T && tid < kRowsTableLds)
+                tableL[tid] = op_word(rb, seg, pos, kOpWords + S + tid);
+        } else if (it.tileBase < n) {   // uniform: the item reaches this tile
             uint4 prior = make_uint4(0, 0, 0, 0), old = make_uint4(0, 0, 0, 0);
             if (wave == 0 && p < n) {
+                // what wave 0 merges at the end, fetched while the terms stream in
                 if (p < valid)
                     prior = ld16(dst + p);
                 if (p + 16 > n)
@@ -278,41 +360,61 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             }
             uint4 acc0 = make_uint4(0, 0, 0, 0);
             uint4 acc1 = make_uint4(0, 0, 0, 0);
-            if (!solo || wave == 0)
-                gather_terms(rb, seg, pos, nt, solo ? 0 : wave, solo ? 1 : kExecWaves, p, acc0, acc1);
+            uint32_t mix, litLen = 0;
+            uint32_t lit[2] = {0, 0};
+            bool solo;
+            if (kind == OP_LINCOMB) {
+                const uint32_t nt = uni(h1.w);
+                mix = uni(h1.y);
+                solo = nt <= kExecSolo;
+                if (!solo || wave == 0)
+                    gather(nt, solo ? 0 : wave, solo ? 1 : kExecWaves, p, acc0, acc1,
+                           [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                               const uint4 w = op_word(rb, seg, pos, kOpWords + k);
+                               read_term(w, src, len);
+                               ca = uni(w.w);
+                               return true;
+                           });
+            } else {
+                // OP_ROW: dense lane sums by mask bit, then the LDPC picks
+                const uint32_t npicks = uni(h1.x) >> 8;
+                const uint32_t mixLit = uni(h1.y);
+                const uint32_t mask0 = uni(h1.z), mask1 = uni(h1.w);
+                const uint4 h2 = rb[2];
+                mix = mixLit & 0xff;
+                litLen = mixLit >> 8;
+                lit[0] = uni(h2.x);
+                lit[1] = uni(h2.y);
+                solo = false;
+                // position b < 48: sum b % 24 into acc b / 24 (wave w: b = w mod 4)
+                gather(2 * kRowsSums, wave, kExecWaves, p, acc0, acc1,
+                       [&](uint32_t b, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                           const uint32_t sum = b < kRowsSums ? b : b - kRowsSums;
+                           const uint32_t m = b < kRowsSums ? mask0 : mask1;
+                           if (!((m >> sum) & 1))
+                               return false;
+                           read_term(sumsL[sum], src, len);
+                           ca = 1 | (b < kRowsSums ? 0u : 0x100u);
+                           return true;
+                       });
+                gather(npicks, wave, kExecWaves, p, acc0, acc1,
+                       [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                           const uint32_t pk =
+                               word_u16(op_word(rb, seg, pos, kRowWords + k / kPicksPerWord),
+                                        k % kPicksPerWord);
+                           const uint32_t ti = pk & 0x7fff;
+                           read_term(ti < kRowsTableLds ? tableL[ti] : seg[tableBase + ti], src, len);
+                           ca = 1 | ((pk >> 15) << 8);
+                           return true;
+                       });
+            }
             if (mix > 1)
                 acc1 = gf_mul16(acc1, mix);
-            uint4 out = xor16(acc0, acc1);
-            if (!solo) {
-                if (wave != 0)
-                    part[wave - 1][lane] = out;
-                __syncthreads();
-            }
-            if (wave == 0 && p < n) {
-                if (!solo) {
-#pragma unroll
-                    for (unsigned w = 0; w + 1 < kExecWaves; ++w)
-                        out = xor16(out, part[w][lane]);
-                }
-                if (p < valid) {
-                    if (p + 16 > valid)
-                        prior = mask16(prior, (int)valid - (int)p);
-                    out = xor16(out, prior);
-                }
-                if (p + 16 > n) {
-                    // keep dst bytes at and beyond n
-                    const int nb = (int)n - (int)p;
-                    const uint4 keep = make_uint4(~byte_mask(nb), ~byte_mask(nb - 4),
-                                                  ~byte_mask(nb - 8), ~byte_mask(nb - 12));
-                    out = mask16(out, nb);
-                    out.x |= old.x & keep.x;
-                    out.y |= old.y & keep.y;
-                    out.z |= old.z & keep.z;
-                    out.w |= old.w & keep.w;
-                }
-                st16(dst + p, out);
-            }
+            finish_item(xor16(acc0, acc1), solo, part, wave, lane, p, dst, n, valid, prior, old, lit,
+                        litLen);
         }
+        if (kind == OP_ROW)
+            --rowsLeft;
         ring[cur ^ 1][tid] = pf;
         __syncthreads();
         cur ^= 1;

@@ -621,12 +621,16 @@ SiameseResult DecoderCore::add_recovery_common(const RowMeta& m, int footer, uns
     static const uint8_t none[1] = {0};
     if (hostData)
         prog_.ingest_host(r->buf, hostData, payload, none, 0);
-    else if (producer) {
-        producer->lc_begin(r->buf.addr(), payload, 0);
-        producer->lc_term(devData, payload, 1);
-        producer->lc_end();
-    } else
-        prog_.ingest_device(r->buf, devData, payload, none, 0);
+    else {
+        // A device-resident packet may have been encoded in this very flush:
+        // copy it with an op of this (group-1) program, which runs after
+        // every encoder op of the flush.  Encoders give each packet a fresh
+        // buffer, so nothing overwrites it before the copy.
+        (void)producer;
+        prog_.lc_begin(r->buf.addr(), payload, 0);
+        prog_.lc_term(devData, payload, 1);
+        prog_.lc_end();
+    }
     r->bytes = payload;
     r->meta = m;
     r->elementStart = elementStart;
@@ -660,11 +664,12 @@ bool DecoderCore::add_single(const RowMeta& m, const uint8_t* headBytes, unsigne
         return false;
     if (hostData)
         prog_.ingest_host(s.buf, (const uint8_t*)hostData + headerBytes, length, hdr, h);
-    else if (producer && (unsigned)headerBytes == h) {
-        // Same byte alignment: an in-order copy on the producing program
-        producer->lc_begin(s.buf.addr(), h + length, 0);
-        producer->lc_term(devData, h + length, 1);
-        producer->lc_end();
+    else if ((unsigned)headerBytes == h) {
+        // Same byte alignment: a copy op of this program (see add_recovery_common)
+        (void)producer;
+        prog_.lc_begin(s.buf.addr(), h + length, 0);
+        prog_.lc_term(devData, h + length, 1);
+        prog_.lc_end();
     } else
         prog_.ingest_device(s.buf, devData + headerBytes, length, hdr, h);
     if (mirror_) {
@@ -1137,15 +1142,10 @@ bool DecoderCore::eliminate_original_data()
         }
         sumColumnCount_ = m.sumCount;
 
-        // decoder sums first (their ops precede this row's op)
-        struct DenseTerm
-        {
-            uint64_t src;
-            unsigned len;
-            uint8_t acc;
-        };
-        DenseTerm dense[kLanes * 2 * kSums];
-        unsigned nDense = 0;
+        // decoder sums first (their ops precede this row); the row selects
+        // them by mask bit lane*3 + sum
+        uint32_t mask[2] = {0, 0};
+        uint64_t opBytes = rb; // RX * product muladd
         for (unsigned lane = 0; lane < kLanes; ++lane) {
             const unsigned op = row_opcode(lane, m.row);
             for (unsigned bit = 0; bit < 2 * kSums; ++bit) {
@@ -1154,17 +1154,25 @@ bool DecoderCore::eliminate_original_data()
                 DevSum& s = get_sum(lane, bit % kSums, ee);
                 if (s.bytes > 0) {
                     materialize(s);
-                    dense[nDense++] = DenseTerm{s.buf.addr(), std::min(s.bytes, rb),
-                                                (uint8_t)(bit / kSums)};
+                    mask[bit / kSums] |= 1u << (lane * kSums + bit % kSums);
+                    opBytes += std::min(s.bytes, rb);
                 }
             }
         }
-        prog_.lc_begin(rec->buf.addr(), rb, rb, row_value(m.row));
-        uint64_t opBytes = rb; // RX * product muladd
-        for (unsigned k = 0; k < nDense; ++k) {
-            prog_.lc_term(dense[k].src, dense[k].len, 1, dense[k].acc);
-            opBytes += dense[k].len;
-        }
+        GfTerm sums[kLanes * kSums];
+        for (unsigned lane = 0; lane < kLanes; ++lane)
+            for (unsigned s = 0; s < kSums; ++s) {
+                const DevSum& d = sum(lane, s).d;
+                GfTerm& t = sums[lane * kSums + s];
+                t.src = d.buf.addr();
+                t.len = d.bytes;
+                t.coeff = 1;
+                t.acc = 0;
+                t.pad = 0;
+            }
+        // rows of one decode share the sums: one row of the program's batch
+        prog_.rows_begin(sums, kLanes * kSums, rec->buf.addr(), rb, rb, row_value(m.row), mask[0],
+                         mask[1]);
         Pcg32 prng;
         prng.seed(m.row, m.ldpcCount);
         const unsigned pairs = (m.ldpcCount + kPairRate - 1) / kPairRate;
@@ -1172,16 +1180,16 @@ bool DecoderCore::eliminate_original_data()
         for (unsigned k = 0; k < pairs; ++k) {
             const DecSlot& a = slot(es + mod(prng.next()));
             if (a.bytes > 0) {
-                prog_.lc_term(a.buf.addr(), std::min(a.bytes, rb), 1, 0);
+                prog_.rows_pick(a.buf.addr(), std::min(a.bytes, rb), 0);
                 opBytes += std::min(a.bytes, rb);
             }
             const DecSlot& b = slot(es + mod(prng.next()));
             if (b.bytes > 0) {
-                prog_.lc_term(b.buf.addr(), std::min(b.bytes, rb), 1, 1);
+                prog_.rows_pick(b.buf.addr(), std::min(b.bytes, rb), 1);
                 opBytes += std::min(b.bytes, rb);
             }
         }
-        prog_.lc_end();
+        prog_.rows_end();
         eng_->account(opBytes);
     }
     return !disabled_;

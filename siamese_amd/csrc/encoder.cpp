@@ -258,10 +258,13 @@ SiameseResult EncoderCore::get(SiameseOriginalPacket& packet)
 
 bool EncoderCore::ensure_recovery(unsigned bytes)
 {
-    if (recovery_.cap >= bytes)
-        return true;
+    // Every recovery packet gets a fresh buffer.  The previous one is
+    // recycled only after the flush that produced it completes, so a decoder
+    // that copies the packet later in the same flush (its own program, group
+    // 1) still reads it intact, and consecutive rows carry no write-after-
+    // read dependency through a shared buffer.
     eng_->release(recovery_);
-    recovery_ = eng_->alloc(bytes + bytes / 8);
+    recovery_ = eng_->alloc(bytes);
     if (!recovery_) {
         disabled_ = true;
         return false;
@@ -269,11 +272,13 @@ bool EncoderCore::ensure_recovery(unsigned bytes)
     return true;
 }
 
-void EncoderCore::finish_row(EncodeOut& out, const RowMeta& meta, unsigned payloadBytes)
+void EncoderCore::finish_row(EncodeOut& out, const RowMeta& meta, unsigned payloadBytes,
+                             bool footerWritten)
 {
     out.meta = meta;
     out.footerBytes = write_footer(meta, out.footer);
-    prog_.literal(recovery_.addr(), payloadBytes, out.footer, out.footerBytes);
+    if (!footerWritten)
+        prog_.literal(recovery_.addr(), payloadBytes, out.footer, out.footerBytes);
     out.buf = recovery_;
     out.bytes = payloadBytes + out.footerBytes;
     eng_->account(0, out.bytes);
@@ -388,15 +393,9 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
 
     // Dense part (:1046-1098): opcode bits 0-2 feed the row, 3-5 the product.
     // The lane sums are brought up to date first (their own ops precede the
-    // row's op in the program).
-    struct DenseTerm
-    {
-        uint64_t src;
-        unsigned len;
-        uint8_t acc;
-    };
-    DenseTerm dense[kLanes * 2 * kSums];
-    unsigned nDense = 0;
+    // row in the program); the row selects them by mask bit lane*3 + sum.
+    uint32_t mask[2] = {0, 0};
+    uint64_t opBytes = recoveryBytes; // final RX * product muladd
     for (unsigned lane = 0; lane < kLanes; ++lane) {
         const unsigned opcode = row_opcode(lane, row);
         for (unsigned bit = 0; bit < 2 * kSums; ++bit) {
@@ -405,20 +404,37 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
             DevSum& sum = get_sum(lane, bit % kSums, count_);
             if (disabled_)
                 return Siamese_Disabled;
-            if (sum.bytes > 0)
-                dense[nDense++] = DenseTerm{sum.buf.addr(), std::min(sum.bytes, recoveryBytes),
-                                            (uint8_t)(bit / kSums)};
+            if (sum.bytes > 0) {
+                mask[bit / kSums] |= 1u << (lane * kSums + bit % kSums);
+                opBytes += std::min(sum.bytes, recoveryBytes);
+            }
         }
     }
     sumEnd_ = count_;
+    GfTerm sums[kLanes * kSums];
+    for (unsigned lane = 0; lane < kLanes; ++lane)
+        for (unsigned s = 0; s < kSums; ++s) {
+            const DevSum& d = lanes_[lane].sum[s];
+            GfTerm& t = sums[lane * kSums + s];
+            t.src = d.buf.addr();
+            t.len = d.bytes;
+            t.coeff = 1;
+            t.acc = 0;
+            t.pad = 0;
+        }
 
-    // Recovery = row sums ^ RX * product  (:1232-1233), one fused device op
-    prog_.lc_begin(recovery_.addr(), recoveryBytes, 0, row_value(row));
-    uint64_t opBytes = recoveryBytes; // final RX * product muladd
-    for (unsigned k = 0; k < nDense; ++k) {
-        prog_.lc_term(dense[k].src, dense[k].len, 1, dense[k].acc);
-        opBytes += dense[k].len;
-    }
+    RowMeta m;
+    m.sumCount = sumEnd_ - sumStart_ + sumErased_;
+    m.ldpcCount = unacked();
+    m.columnStart = sumColumnStart_;
+    m.row = row;
+    uint8_t footer[kMaxFooterBytes];
+    const unsigned footerBytes = write_footer(m, footer);
+
+    // Recovery = row sums ^ RX * product (:1232-1233) and its footer: one row
+    // of the program's Siamese row batch (consecutive rows share the sums)
+    prog_.rows_begin(sums, kLanes * kSums, recovery_.addr(), recoveryBytes, 0, row_value(row),
+                     mask[0], mask[1], footer, footerBytes);
 
     // Sparse part (:1100-1144): ceil(n/16) PCG-chosen pairs
     const unsigned start = firstUnremoved_;
@@ -430,19 +446,14 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     for (unsigned i = 0; i < pairs; ++i) {
         const EncSlot& a = slot(start + mod(prng.next()));
         const EncSlot& b = slot(start + mod(prng.next()));
-        prog_.lc_term(a.buf.addr(), a.bytes, 1, 0);
-        prog_.lc_term(b.buf.addr(), b.bytes, 1, 1);
+        prog_.rows_pick(a.buf.addr(), a.bytes, 0);
+        prog_.rows_pick(b.buf.addr(), b.bytes, 1);
         opBytes += a.bytes + b.bytes;
     }
-    prog_.lc_end();
+    prog_.rows_end();
     eng_->account(opBytes);
 
-    RowMeta m;
-    m.sumCount = sumEnd_ - sumStart_ + sumErased_;
-    m.ldpcCount = unacked();
-    m.columnStart = sumColumnStart_;
-    m.row = row;
-    finish_row(out, m, recoveryBytes);
+    finish_row(out, m, recoveryBytes, true);
     return Siamese_Success;
 }
 

@@ -100,7 +100,8 @@ private:
     SiameseResult cauchy_row(EncodeOut& out);
     SiameseResult siamese_row(EncodeOut& out, unsigned row);
     bool ensure_recovery(unsigned bytes);
-    void finish_row(EncodeOut& out, const RowMeta& meta, unsigned payloadBytes);
+    void finish_row(EncodeOut& out, const RowMeta& meta, unsigned payloadBytes,
+                    bool footerWritten = false);
     void update_rto();
     SiameseResult retransmit_slot(EncSlot& s, SiameseOriginalPacket& out);
     AckState ack_;

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 
 namespace sgpu {
@@ -46,6 +47,7 @@ Program::~Program()
 {
     if (!shard_)
         return;
+    rows_close();
     // The instance goes away with work still queued (e.g. an encoder freed
     // right after its last recovery packet was handed to a decoder, whose
     // copy op lives in this program).  The queued ops still run: hand them
@@ -76,11 +78,15 @@ void Program::attach()
 
 void Program::new_segment()
 {
+    rows_close();
     if (nsegs_ == segs_.size())
         segs_.emplace_back();
     Segment& s = segs_[nsegs_++];
     s.ops.clear();
     s.terms.clear();
+    s.rowsData.clear();
+    s.rowsWords = 0;
+    s.rowsItems = 0;
     s.maxExtent = 0;
 }
 
@@ -89,6 +95,9 @@ void Program::reset_after_flush()
     for (size_t k = 0; k < nsegs_; ++k) {
         segs_[k].ops.clear();
         segs_[k].terms.clear();
+        segs_[k].rowsData.clear();
+        segs_[k].rowsWords = 0;
+        segs_[k].rowsItems = 0;
         segs_[k].maxExtent = 0;
     }
     nsegs_ = 0;
@@ -101,6 +110,7 @@ void Program::reset_after_flush()
 void Program::lc_begin(uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix)
 {
     touch();
+    rows_close();
     if (nsegs_ == 0)
         new_segment();
     Segment& s = segs_[nsegs_ - 1];
@@ -168,6 +178,7 @@ void Program::literal(uint64_t dst, uint32_t offset, const uint8_t* bytes, uint3
     if (len == 0)
         return;
     touch();
+    rows_close();
     if (nsegs_ == 0)
         new_segment();
     Segment& s = segs_[nsegs_ - 1];
@@ -225,6 +236,152 @@ void Program::on_complete(Completion fn)
 {
     touch();
     callbacks_.push_back(std::move(fn));
+}
+
+// ---- Siamese row batches ---------------------------------------------------
+
+void Program::rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, uint32_t n,
+                         uint32_t valid, uint8_t mix, uint32_t mask0, uint32_t mask1,
+                         const uint8_t* lit, uint32_t litLen)
+{
+    touch();
+    RowsBuild& b = rb_;
+    bool join = b.open && b.sumCount == sumCount && b.table.size() < kMaxRowsTable / 2;
+    for (unsigned k = 0; join && k < sumCount; ++k)
+        join = b.sums[k].src == sums[k].src && b.sums[k].len == sums[k].len;
+    if (!join) {
+        rows_close();
+        if (nsegs_ == 0)
+            new_segment();
+        b.open = true;
+        b.sumCount = sumCount;
+        std::memcpy(b.sums, sums, sumCount * sizeof(GfTerm));
+        b.rows = 0;
+        b.table.clear();
+        b.rowBytes.clear();
+        b.maxExtent = 0;
+        if (b.keys.empty()) {
+            b.keys.assign(1024, 0);
+            b.vals.assign(1024, 0);
+        } else {
+            std::fill(b.keys.begin(), b.keys.end(), 0);
+        }
+    }
+    RowHeader h;
+    std::memset(&h, 0, sizeof(h));
+    h.dst = dst;
+    h.n = n;
+    h.valid = valid < n ? valid : n;
+    h.kindPicks = OP_ROW;
+    h.mix = mix | (litLen << 8);
+    h.mask0 = mask0;
+    h.mask1 = mask1;
+    if (litLen)
+        std::memcpy(h.lit, lit, litLen);
+    b.curRow = b.rowBytes.size();
+    b.curPicks = 0;
+    b.rowBytes.resize(b.curRow + sizeof(RowHeader));
+    std::memcpy(b.rowBytes.data() + b.curRow, &h, sizeof(h));
+    ++b.rows;
+    if (n + litLen > b.maxExtent)
+        b.maxExtent = n + litLen;
+}
+
+uint16_t Program::rows_table_index(uint64_t src, uint32_t len)
+{
+    RowsBuild& b = rb_;
+    if (b.table.size() * 2 >= b.keys.size()) {
+        // grow the map (load factor <= 1/2)
+        std::vector<uint64_t> oldKeys;
+        std::vector<uint16_t> oldVals;
+        oldKeys.swap(b.keys);
+        oldVals.swap(b.vals);
+        b.keys.assign(oldKeys.size() * 2, 0);
+        b.vals.assign(oldKeys.size() * 2, 0);
+        const size_t mask = b.keys.size() - 1;
+        for (size_t i = 0; i < oldKeys.size(); ++i) {
+            if (!oldKeys[i])
+                continue;
+            size_t h = (oldKeys[i] >> 6) * 0x9E3779B97F4A7C15ULL >> 20;
+            while (b.keys[h & mask])
+                ++h;
+            b.keys[h & mask] = oldKeys[i];
+            b.vals[h & mask] = oldVals[i];
+        }
+    }
+    const size_t mask = b.keys.size() - 1;
+    size_t h = (src >> 6) * 0x9E3779B97F4A7C15ULL >> 20;
+    for (;; ++h) {
+        const uint64_t k = b.keys[h & mask];
+        if (k == src)
+            return b.vals[h & mask];
+        if (k == 0)
+            break;
+    }
+    const uint16_t idx = (uint16_t)b.table.size();
+    b.keys[h & mask] = src;
+    b.vals[h & mask] = idx;
+    GfTerm t;
+    t.src = src;
+    t.len = len;
+    t.coeff = 1;
+    t.acc = 0;
+    t.pad = 0;
+    b.table.push_back(t);
+    return idx;
+}
+
+void Program::rows_pick(uint64_t src, uint32_t len, uint32_t acc)
+{
+    RowsBuild& b = rb_;
+    if (len == 0)
+        return;
+    const uint16_t pick = (uint16_t)(rows_table_index(src, len) | (acc ? 0x8000u : 0u));
+    if (b.curPicks % kPicksPerWord == 0)
+        b.rowBytes.resize(b.rowBytes.size() + 16, 0);
+    const size_t at = b.rowBytes.size() - 16 + (b.curPicks % kPicksPerWord) * 2;
+    std::memcpy(b.rowBytes.data() + at, &pick, 2);
+    ++b.curPicks;
+}
+
+void Program::rows_end()
+{
+    RowsBuild& b = rb_;
+    uint32_t kp;
+    std::memcpy(&kp, b.rowBytes.data() + b.curRow + offsetof(RowHeader, kindPicks), 4);
+    kp |= b.curPicks << 8;
+    std::memcpy(b.rowBytes.data() + b.curRow + offsetof(RowHeader, kindPicks), &kp, 4);
+}
+
+void Program::rows_close()
+{
+    RowsBuild& b = rb_;
+    if (!b.open)
+        return;
+    b.open = false;
+    Segment& s = segs_[nsegs_ - 1];
+    const uint32_t S = b.sumCount, T = (uint32_t)b.table.size();
+    const uint32_t rowWords = (uint32_t)(b.rowBytes.size() / 16);
+    GfOp op;
+    std::memset(&op, 0, sizeof(op));
+    op.kind = OP_ROWS;
+    op.n = b.rows;
+    op.valid = T;
+    op.mix = S;
+    op.termBegin = (uint32_t)(s.rowsData.size() / 16);   // block offset in words
+    op.termCount = S + T;
+    op.dst = S + T + rowWords;                            // block words (host only)
+    s.ops.push_back(op);
+    const size_t at = s.rowsData.size();
+    s.rowsData.resize(at + (size_t)(S + T + rowWords) * 16);
+    uint8_t* w = s.rowsData.data() + at;
+    std::memcpy(w, b.sums, S * sizeof(GfTerm));
+    std::memcpy(w + S * 16, b.table.data(), T * sizeof(GfTerm));
+    std::memcpy(w + (S + T) * 16, b.rowBytes.data(), b.rowBytes.size());
+    s.rowsWords += S + T + rowWords;
+    s.rowsItems += b.rows;
+    if (b.maxExtent > s.maxExtent)
+        s.maxExtent = b.maxExtent;
 }
 
 // ---------------------------------------------------------------------------
@@ -496,8 +653,10 @@ void Engine::flush()
     // ---- 1. layout -----------------------------------------------------------
     std::vector<Program*> progs[2];
     for (Shard* s : shards)
-        for (Program* p : s->dirty)
+        for (Program* p : s->dirty) {
+            p->rows_close();
             progs[p->group_ & 1].push_back(p);
+        }
 
     uint32_t resultWords = 0;
     std::vector<uint32_t> resultBase[2];
@@ -526,7 +685,7 @@ void Engine::flush()
                 const Program::Segment& s = p->segs_[k];
                 if (s.ops.empty())
                     continue;
-                const size_t words = kOpWords * s.ops.size() + s.terms.size();
+                const size_t words = kOpWords * s.ops.size() + s.terms.size() + s.rowsWords;
                 segs.push_back(SegRef{p, (uint32_t)k, (uint32_t)nWords, (uint32_t)words,
                                       (uint32_t)nItems});
                 nOps += s.ops.size();
@@ -614,6 +773,16 @@ void Engine::flush()
             const Program::Segment& s = r.prog->segs_[r.seg];
             uint8_t* w = up + oStream + (size_t)r.wordBase * 16;
             for (const GfOp& op : s.ops) {
+                if (op.kind == OP_ROWS) {
+                    GfOp h = op;
+                    h.dst = 0;
+                    std::memcpy(w, &h, sizeof(GfOp));
+                    w += sizeof(GfOp);
+                    const size_t bytes = (size_t)op.dst * 16;   // block words (rows_close)
+                    std::memcpy(w, s.rowsData.data() + (size_t)op.termBegin * 16, bytes);
+                    w += bytes;
+                    continue;
+                }
                 std::memcpy(w, &op, sizeof(GfOp));
                 w += sizeof(GfOp);
                 if (op.kind == OP_LINCOMB && op.termCount) {
@@ -623,9 +792,10 @@ void Engine::flush()
                 }
             }
             ExecItem* items = (ExecItem*)(up + oItems) + r.itemBase;
+            const uint32_t nItems = (uint32_t)s.ops.size() + s.rowsItems;
             uint32_t n = 0;
             for (uint32_t tb = 0; tb < s.maxExtent; tb += kTileBytes)
-                items[n++] = ExecItem{r.wordBase, r.words, (uint32_t)s.ops.size(), tb};
+                items[n++] = ExecItem{r.wordBase, r.words, nItems, tb};
         } else {
             const ShardRef& sr = srefs[t.a];
             const Shard& s = *sr.shard;

@@ -55,6 +55,7 @@ public:
 
     /// LINCOMB: dst[i] = (i < valid ? dst[i] : 0) ^ acc0 ^ mix*acc1, i < n.
     void lc_begin(uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix = 0);
+    // (lc_term must follow lc_begin directly: it appends to the last op)
     void lc_term(uint64_t src, uint32_t len, uint8_t coeff, uint8_t acc = 0)
     {
         Segment& s = segs_[nsegs_ - 1];
@@ -97,6 +98,17 @@ public:
     /// Run `fn(results)` once the next flush has completed.
     void on_complete(Completion fn);
 
+    /// Siamese row batches (OP_ROWS, ops.h).  rows_begin() starts a row: it
+    /// joins the program's last op if that is an open batch over the same
+    /// `sums`, otherwise a new batch opens.  The row's LDPC picks follow
+    /// (rows_pick, in reference order), then rows_end().  Any other op
+    /// closes the batch.
+    void rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, uint32_t n,
+                    uint32_t valid, uint8_t mix, uint32_t mask0, uint32_t mask1,
+                    const uint8_t* lit = nullptr, uint32_t litLen = 0);
+    void rows_pick(uint64_t src, uint32_t len, uint32_t acc);
+    void rows_end();
+
     bool empty() const { return nsegs_ == 0 || (nsegs_ == 1 && segs_[0].ops.empty()); }
 
 private:
@@ -105,8 +117,28 @@ private:
     {
         std::vector<GfOp> ops;
         std::vector<GfTerm> terms;
+        std::vector<uint8_t> rowsData;   // closed OP_ROWS blocks (sums, table, rows)
+        uint32_t rowsWords = 0;          // stream words of those blocks (after headers)
+        uint32_t rowsItems = 0;          // row items they contain
         uint32_t maxExtent = 0;
     };
+    /// The OP_ROWS batch under construction (always the segment's last op).
+    struct RowsBuild
+    {
+        bool open = false;
+        GfTerm sums[24];
+        unsigned sumCount = 0;
+        unsigned rows = 0;
+        std::vector<GfTerm> table;
+        std::vector<uint64_t> keys;      // open-addressing map src -> table index
+        std::vector<uint16_t> vals;
+        std::vector<uint8_t> rowBytes;   // serialized row items
+        size_t curRow = 0;               // offset of the current row's header
+        unsigned curPicks = 0;
+        uint32_t maxExtent = 0;
+    };
+    void rows_close();
+    uint16_t rows_table_index(uint64_t src, uint32_t len);
     struct PendingSolve
     {
         SolveDesc desc;
@@ -131,6 +163,7 @@ private:
     std::vector<Segment> segs_;
     std::vector<PendingSolve> solves_;   // solve k follows segment k
     std::vector<Completion> callbacks_;
+    RowsBuild rb_;
 };
 
 /// Algorithmic byte accounting and flush counters.

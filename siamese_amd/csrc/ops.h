@@ -31,6 +31,8 @@ enum GfOpKind : uint32_t
 {
     OP_LINCOMB = 1,   // dst[0,n) = keep(dst,valid) ^ acc0 ^ mix*acc1
     OP_LITERAL = 2,   // dst[n, n+valid) = literal bytes (<= 8)
+    OP_ROWS = 3,      // a batch of Siamese rows sharing one set of lane sums
+    OP_ROW = 4,       // one row of the enclosing OP_ROWS batch (stream item)
 };
 
 /// One op.  For OP_LINCOMB:
@@ -62,9 +64,43 @@ static_assert(sizeof(GfTerm) == 16, "GfTerm layout");
 /// front to back, so one coalesced prefetch brings an op and its term list.
 constexpr unsigned kOpWords = sizeof(GfOp) / 16;
 
+/// OP_ROWS (Siamese rows, reference SiameseEncoder.cpp:1046-1144 and the
+/// decoder's elimination SiameseDecoder.cpp:937-1038).  Stream layout:
+///   GfOp header   kind=OP_ROWS, n = rows K, valid = table entries T,
+///                 mix = sum entries S, termCount = S + T
+///   S words       lane sums as GfTerm {src, len}; bit k of a row's masks
+///                 selects sums[k]
+///   T words       distinct source symbols picked by the rows' LDPC pairs,
+///                 as GfTerm {src, len}
+///   K row items, each RowHeader (2 words) + pick words:
+///     dst[0,n) = keep(dst,valid) ^ acc0 ^ mix * acc1, where acc0 gathers
+///     the sums of mask0 and the picks with acc=0, acc1 those of mask1 and
+///     the picks with acc=1; then `litLen` literal bytes (the recovery
+///     footer) at dst+n.  Picks are uint16 (table index | acc << 15), eight
+///     per word.
+/// All rows of a batch read the same sums, so the device touches each sum
+/// tile once per batch instead of once per row, and the host sends a few
+/// bytes per pick instead of a 16-byte term.
+struct RowHeader
+{
+    uint64_t dst;
+    uint32_t n;
+    uint32_t valid;
+    uint32_t kindPicks;   // OP_ROW | npicks << 8
+    uint32_t mix;         // RX multiplier of acc1 | litLen << 8
+    uint32_t mask0;       // 24-bit sum masks
+    uint32_t mask1;
+    uint8_t lit[8];       // literal bytes written at dst + n
+    uint32_t pad[2];
+};
+static_assert(sizeof(RowHeader) == 48, "RowHeader layout");
+constexpr unsigned kRowWords = sizeof(RowHeader) / 16;
+constexpr unsigned kPicksPerWord = 8;
+constexpr unsigned kMaxRowsTable = 0x7fff;   // table indices fit 15 bits
+
 inline uint32_t op_words(const GfOp& op)
 {
-    return kOpWords + (op.kind == OP_LINCOMB ? op.termCount : 0);
+    return kOpWords + ((op.kind == OP_LINCOMB || op.kind == OP_ROWS) ? op.termCount : 0);
 }
 
 /// Executor work item: one (instance segment, byte tile).

@@ -88,53 +88,110 @@ int parse_prefix(const uint8_t* b, unsigned avail, unsigned* len)
 
 inline uint8_t* P(uint64_t a) { return reinterpret_cast<uint8_t*>(a); }
 
+// One linear combination on one tile: dst[0,n) = keep(dst,valid) ^ acc0 ^
+// mix*acc1 with the terms (src, len, coeff, acc) given by `terms`.
+struct TileTerm
+{
+    uint64_t src;
+    uint32_t len;
+    uint8_t coeff, acc;
+};
+
+void lincomb_tile(uint64_t dstAddr, uint32_t n, uint32_t valid, uint32_t mix,
+                  const std::vector<TileTerm>& terms, uint32_t t0)
+{
+    const uint32_t t1 = t0 + kTileBytes;
+    const uint32_t end = n < t1 ? n : t1;
+    if (t0 >= end)
+        return;
+    const unsigned w = end - t0;
+    uint8_t acc0[kTileBytes], acc1[kTileBytes], tmp[kTileBytes];
+    std::memset(acc0, 0, w);
+    std::memset(acc1, 0, w);
+    for (const TileTerm& tm : terms) {
+        if (t0 >= tm.len)
+            continue;
+        const unsigned k = (tm.len < end ? tm.len : end) - t0;
+        std::memcpy(tmp, P(tm.src) + t0, k);
+        if (tm.coeff != 1)
+            mul_bytes(tmp, k, tm.coeff);
+        uint8_t* acc = tm.acc ? acc1 : acc0;
+        for (unsigned i = 0; i < k; ++i)
+            acc[i] ^= tmp[i];
+    }
+    if (mix > 1)
+        mul_bytes(acc1, w, (uint8_t)mix);
+    uint8_t* dst = P(dstAddr) + t0;
+    for (unsigned i = 0; i < w; ++i) {
+        const uint8_t prior = (t0 + i < valid) ? dst[i] : 0;
+        dst[i] = prior ^ acc0[i] ^ acc1[i];
+    }
+}
+
+void literal_tile(uint64_t dst, uint32_t at, const uint8_t* lit, uint32_t len, uint32_t t0)
+{
+    for (uint32_t k = 0; k < len; ++k) {
+        const uint32_t b = at + k;
+        if (b >= t0 && b < t0 + kTileBytes)
+            P(dst)[b] = lit[k];
+    }
+}
+
 void exec_tile(const uint8_t* stream, const ExecItem& it)
 {
     const uint8_t* w = stream + (size_t)it.streamBegin * 16;
     const uint8_t* end = w + (size_t)it.streamWords * 16;
+    const uint32_t t0 = it.tileBase;
+    std::vector<TileTerm> terms;
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
         GfOp op;
         std::memcpy(&op, w, sizeof(op));
-        const GfTerm* terms = reinterpret_cast<const GfTerm*>(w + sizeof(GfOp));
+        const uint8_t* body = w + sizeof(GfOp);
         w += (size_t)op_words(op) * 16;
         if (w > end)
             std::abort(); // malformed stream
-        if (op.kind == OP_LINCOMB)
-            op.termBegin = 0; // terms follow the op in the stream
-        const uint32_t t0 = it.tileBase, t1 = it.tileBase + kTileBytes;
         if (op.kind == OP_LITERAL) {
-            for (uint32_t k = 0; k < op.valid; ++k) {
-                const uint32_t b = op.n + k;
-                if (b >= t0 && b < t1)
-                    P(op.dst)[b] = op.lit[k];
+            literal_tile(op.dst, op.n, op.lit, op.valid, t0);
+            continue;
+        }
+        if (op.kind == OP_LINCOMB) {
+            terms.clear();
+            const GfTerm* tt = reinterpret_cast<const GfTerm*>(body);
+            for (uint32_t k = 0; k < op.termCount; ++k)
+                terms.push_back(TileTerm{tt[k].src, tt[k].len, tt[k].coeff, tt[k].acc});
+            lincomb_tile(op.dst, op.n, op.valid, op.mix, terms, t0);
+            continue;
+        }
+        if (op.kind != OP_ROWS)
+            std::abort();
+        // OP_ROWS: S sums, T table entries, then K row items (ops.h)
+        const GfTerm* sums = reinterpret_cast<const GfTerm*>(body);
+        const GfTerm* table = sums + op.mix;
+        for (uint32_t r = 0; r < op.n; ++r, ++oi) {
+            RowHeader h;
+            std::memcpy(&h, w, sizeof(h));
+            if ((h.kindPicks & 0xff) != OP_ROW)
+                std::abort();
+            const uint32_t npicks = h.kindPicks >> 8;
+            const uint16_t* picks = reinterpret_cast<const uint16_t*>(w + sizeof(RowHeader));
+            w += sizeof(RowHeader) + (size_t)((npicks + kPicksPerWord - 1) / kPicksPerWord) * 16;
+            if (w > end)
+                std::abort();
+            terms.clear();
+            for (uint32_t k = 0; k < op.mix; ++k) {
+                if (h.mask0 >> k & 1)
+                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 0});
+                if (h.mask1 >> k & 1)
+                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 1});
             }
-            continue;
-        }
-        const uint32_t end = op.n < t1 ? op.n : t1;
-        if (t0 >= end)
-            continue;
-        const unsigned w = end - t0;
-        uint8_t acc0[kTileBytes], acc1[kTileBytes], tmp[kTileBytes];
-        std::memset(acc0, 0, w);
-        std::memset(acc1, 0, w);
-        for (uint32_t k = 0; k < op.termCount; ++k) {
-            const GfTerm& tm = terms[op.termBegin + k];
-            if (t0 >= tm.len)
-                continue;
-            const unsigned n = (tm.len < end ? tm.len : end) - t0;
-            std::memcpy(tmp, P(tm.src) + t0, n);
-            if (tm.coeff != 1)
-                mul_bytes(tmp, n, tm.coeff);
-            uint8_t* acc = tm.acc ? acc1 : acc0;
-            for (unsigned i = 0; i < n; ++i)
-                acc[i] ^= tmp[i];
-        }
-        if (op.mix > 1)
-            mul_bytes(acc1, w, (uint8_t)op.mix);
-        uint8_t* dst = P(op.dst) + t0;
-        for (unsigned i = 0; i < w; ++i) {
-            const uint8_t prior = (t0 + i < op.valid) ? dst[i] : 0;
-            dst[i] = prior ^ acc0[i] ^ acc1[i];
+            for (uint32_t k = 0; k < npicks; ++k) {
+                const uint32_t idx = picks[k] & 0x7fff;
+                if (idx >= op.valid)
+                    std::abort();
+                terms.push_back(TileTerm{table[idx].src, table[idx].len, 1, (uint8_t)(picks[k] >> 15)});
+            }
+            lincomb_tile(h.dst, h.n, h.valid, h.mix & 0xff, terms, t0);
+            literal_tile(h.dst, h.n, h.lit, h.mix >> 8, t0);
         }
     }
 }
