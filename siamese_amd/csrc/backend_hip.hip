@@ -292,14 +292,12 @@ __device__ __forceinline__ void finish_item(uint4 out, bool solo, uint4 (*part)[
 }
 
 constexpr unsigned kRowsTableLds = 256;   // table entries of an OP_ROWS batch kept in LDS
-constexpr unsigned kRowsSums = 24;
 
 __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
                                                        const ExecItem* __restrict__ items)
 {
     __shared__ uint4 ring[2][kRingWords];
     __shared__ uint4 part[kExecWaves - 1][64];
-    __shared__ uint4 sumsL[kRowsSums];
     __shared__ uint4 tableL[kRowsTableLds];
     const ExecItem it = items[blockIdx.x];
     const uint4* seg = stream + it.streamBegin;
@@ -323,7 +321,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         if (kind == OP_LINCOMB)
             itemWords += uni(h1.w);
         else if (kind == OP_ROWS)
-            itemWords += uni(h1.w);   // S + T descriptor words
+            itemWords += uni(h1.w);   // table words
         else if (kind == OP_ROW)
             itemWords = kRowWords + ((uni(h1.x) >> 8) + kPicksPerWord - 1) / kPicksPerWord;
         const uint32_t next = pos + itemWords;
@@ -340,15 +338,12 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     d[k] = (uint8_t)(lit[(k - n) >> 2] >> (8 * ((k - n) & 3)));
             }
         } else if (kind == OP_ROWS) {
-            // batch prologue: stage the lane-sum descriptors and the first
-            // kRowsTableLds table entries; the rows follow as items
-            const uint32_t S = uni(h1.y), T = valid;
+            // batch prologue: stage the first kRowsTableLds table entries
+            // (lane sums first); the rows follow as items
             rowsLeft = n;
-            tableBase = pos + kOpWords + S;
-            if (tid < S)
-                sumsL[tid] = op_word(rb, seg, pos, kOpWords + tid);
-            if (tid < T && tid < kRowsTableLds)
-                tableL[tid] = op_word(rb, seg, pos, kOpWords + S + tid);
+            tableBase = pos + kOpWords;
+            if (tid < valid && tid < kRowsTableLds)
+                tableL[tid] = op_word(rb, seg, pos, kOpWords + tid);
         } else if (it.tileBase < n) {   // uniform: the item reaches this tile
             uint4 prior = make_uint4(0, 0, 0, 0), old = make_uint4(0, 0, 0, 0);
             if (wave == 0 && p < n) {
@@ -376,27 +371,15 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                return true;
                            });
             } else {
-                // OP_ROW: dense lane sums by mask bit, then the LDPC picks
+                // OP_ROW: the row's picks (selected lane sums, then LDPC pairs)
                 const uint32_t npicks = uni(h1.x) >> 8;
                 const uint32_t mixLit = uni(h1.y);
-                const uint32_t mask0 = uni(h1.z), mask1 = uni(h1.w);
                 const uint4 h2 = rb[2];
                 mix = mixLit & 0xff;
                 litLen = mixLit >> 8;
                 lit[0] = uni(h2.x);
                 lit[1] = uni(h2.y);
                 solo = false;
-                // position b < 48: sum b % 24 into acc b / 24 (wave w: b = w mod 4)
-                gather(2 * kRowsSums, wave, kExecWaves, p, acc0, acc1,
-                       [&](uint32_t b, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                           const uint32_t sum = b < kRowsSums ? b : b - kRowsSums;
-                           const uint32_t m = b < kRowsSums ? mask0 : mask1;
-                           if (!((m >> sum) & 1))
-                               return false;
-                           read_term(sumsL[sum], src, len);
-                           ca = 1 | (b < kRowsSums ? 0u : 0x100u);
-                           return true;
-                       });
                 gather(npicks, wave, kExecWaves, p, acc0, acc1,
                        [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
                            const uint32_t pk =
@@ -616,10 +599,23 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
             src = mask16(src, (int)L - (int)p);
         const uint8_t* col = Ct + i * m;
         const uint32_t first = i + 1 + ((wave + kSolveWaves - (i + 1) % kSolveWaves) % kSolveWaves);
-        for (uint32_t j = first; j < m; j += kSolveWaves) {
-            const uint32_t y = uni(col[j]);
-            if (y)
-                X[j * 64 + lane] = xor16(X[j * 64 + lane], gf_mul16(src, y));
+        // four independent row updates at a time, so the coefficient and
+        // table fetches of one overlap those of the others
+        for (uint32_t j0 = first; j0 < m; j0 += 4 * kSolveWaves) {
+            uint32_t y[4];
+            uint4 xr[4];
+#pragma unroll
+            for (unsigned u = 0; u < 4; ++u) {
+                const uint32_t j = j0 + u * kSolveWaves;
+                y[u] = j < m ? uni(col[j]) : 0;
+                xr[u] = j < m ? X[j * 64 + lane] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (unsigned u = 0; u < 4; ++u) {
+                const uint32_t j = j0 + u * kSolveWaves;
+                if (y[u])
+                    X[j * 64 + lane] = xor16(xr[u], gf_mul16(src, y[u]));
+            }
         }
         __syncthreads();
     }
@@ -636,14 +632,25 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
         if ((uint32_t)i % kSolveWaves == wave && p < finB[i])
             st16(R[i].buf + p, x);
         if (tileBase < bb) {
-            for (uint32_t j = wave; j < (uint32_t)i; j += kSolveWaves) {
-                const uint32_t c = uni(col[j]);
-                if (!c)
-                    continue;
-                const uint32_t fj = uni(finB[j]);
-                const uint32_t ab = bb < fj ? bb : fj;
-                const uint4 xs = mask16(x, (int)ab - (int)p);
-                X[j * 64 + lane] = xor16(X[j * 64 + lane], gf_mul16(xs, c));
+            for (uint32_t j0 = wave; j0 < (uint32_t)i; j0 += 4 * kSolveWaves) {
+                uint32_t c[4], fj[4];
+                uint4 xr[4];
+#pragma unroll
+                for (unsigned u = 0; u < 4; ++u) {
+                    const uint32_t j = j0 + u * kSolveWaves;
+                    c[u] = j < (uint32_t)i ? uni(col[j]) : 0;
+                    fj[u] = j < (uint32_t)i ? uni(finB[j]) : 0;
+                    xr[u] = j < (uint32_t)i ? X[j * 64 + lane] : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (unsigned u = 0; u < 4; ++u) {
+                    if (!c[u])
+                        continue;
+                    const uint32_t j = j0 + u * kSolveWaves;
+                    const uint32_t ab = bb < fj[u] ? bb : fj[u];
+                    const uint4 xs = mask16(x, (int)ab - (int)p);
+                    X[j * 64 + lane] = xor16(xr[u], gf_mul16(xs, c[u]));
+                }
             }
         }
         __syncthreads();

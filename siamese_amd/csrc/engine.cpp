@@ -257,7 +257,8 @@ void Program::rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, ui
         b.sumCount = sumCount;
         std::memcpy(b.sums, sums, sumCount * sizeof(GfTerm));
         b.rows = 0;
-        b.table.clear();
+        // the sums are the first table entries; LDPC sources follow
+        b.table.assign(sums, sums + sumCount);
         b.rowBytes.clear();
         b.maxExtent = 0;
         if (b.keys.empty()) {
@@ -274,8 +275,6 @@ void Program::rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, ui
     h.valid = valid < n ? valid : n;
     h.kindPicks = OP_ROW;
     h.mix = mix | (litLen << 8);
-    h.mask0 = mask0;
-    h.mask1 = mask1;
     if (litLen)
         std::memcpy(h.lit, lit, litLen);
     b.curRow = b.rowBytes.size();
@@ -285,6 +284,24 @@ void Program::rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, ui
     ++b.rows;
     if (n + litLen > b.maxExtent)
         b.maxExtent = n + litLen;
+    // dense part: the masked sums become picks of table entries 0..S-1, so a
+    // row is one list of (table index, accumulator) picks on the device
+    for (unsigned k = 0; k < sumCount; ++k) {
+        if (mask0 >> k & 1)
+            add_pick((uint16_t)k);
+        if (mask1 >> k & 1)
+            add_pick((uint16_t)(k | 0x8000u));
+    }
+}
+
+void Program::add_pick(uint16_t pick)
+{
+    RowsBuild& b = rb_;
+    if (b.curPicks % kPicksPerWord == 0)
+        b.rowBytes.resize(b.rowBytes.size() + 16, 0);
+    const size_t at = b.rowBytes.size() - 16 + (b.curPicks % kPicksPerWord) * 2;
+    std::memcpy(b.rowBytes.data() + at, &pick, 2);
+    ++b.curPicks;
 }
 
 uint16_t Program::rows_table_index(uint64_t src, uint32_t len)
@@ -333,15 +350,9 @@ uint16_t Program::rows_table_index(uint64_t src, uint32_t len)
 
 void Program::rows_pick(uint64_t src, uint32_t len, uint32_t acc)
 {
-    RowsBuild& b = rb_;
     if (len == 0)
         return;
-    const uint16_t pick = (uint16_t)(rows_table_index(src, len) | (acc ? 0x8000u : 0u));
-    if (b.curPicks % kPicksPerWord == 0)
-        b.rowBytes.resize(b.rowBytes.size() + 16, 0);
-    const size_t at = b.rowBytes.size() - 16 + (b.curPicks % kPicksPerWord) * 2;
-    std::memcpy(b.rowBytes.data() + at, &pick, 2);
-    ++b.curPicks;
+    add_pick((uint16_t)(rows_table_index(src, len) | (acc ? 0x8000u : 0u)));
 }
 
 void Program::rows_end()
@@ -360,25 +371,24 @@ void Program::rows_close()
         return;
     b.open = false;
     Segment& s = segs_[nsegs_ - 1];
-    const uint32_t S = b.sumCount, T = (uint32_t)b.table.size();
+    const uint32_t T = (uint32_t)b.table.size();   // sums + LDPC sources
     const uint32_t rowWords = (uint32_t)(b.rowBytes.size() / 16);
     GfOp op;
     std::memset(&op, 0, sizeof(op));
     op.kind = OP_ROWS;
     op.n = b.rows;
     op.valid = T;
-    op.mix = S;
+    op.mix = b.sumCount;
     op.termBegin = (uint32_t)(s.rowsData.size() / 16);   // block offset in words
-    op.termCount = S + T;
-    op.dst = S + T + rowWords;                            // block words (host only)
+    op.termCount = T;
+    op.dst = T + rowWords;                                // block words (host only)
     s.ops.push_back(op);
     const size_t at = s.rowsData.size();
-    s.rowsData.resize(at + (size_t)(S + T + rowWords) * 16);
+    s.rowsData.resize(at + (size_t)(T + rowWords) * 16);
     uint8_t* w = s.rowsData.data() + at;
-    std::memcpy(w, b.sums, S * sizeof(GfTerm));
-    std::memcpy(w + S * 16, b.table.data(), T * sizeof(GfTerm));
-    std::memcpy(w + (S + T) * 16, b.rowBytes.data(), b.rowBytes.size());
-    s.rowsWords += S + T + rowWords;
+    std::memcpy(w, b.table.data(), T * sizeof(GfTerm));
+    std::memcpy(w + T * 16, b.rowBytes.data(), b.rowBytes.size());
+    s.rowsWords += T + rowWords;
     s.rowsItems += b.rows;
     if (b.maxExtent > s.maxExtent)
         s.maxExtent = b.maxExtent;

@@ -139,6 +139,7 @@ private:
     };
     void rows_close();
     uint16_t rows_table_index(uint64_t src, uint32_t len);
+    void add_pick(uint16_t pick);
     struct PendingSolve
     {
         SolveDesc desc;

@@ -67,20 +67,17 @@ constexpr unsigned kOpWords = sizeof(GfOp) / 16;
 /// OP_ROWS (Siamese rows, reference SiameseEncoder.cpp:1046-1144 and the
 /// decoder's elimination SiameseDecoder.cpp:937-1038).  Stream layout:
 ///   GfOp header   kind=OP_ROWS, n = rows K, valid = table entries T,
-///                 mix = sum entries S, termCount = S + T
-///   S words       lane sums as GfTerm {src, len}; bit k of a row's masks
-///                 selects sums[k]
-///   T words       distinct source symbols picked by the rows' LDPC pairs,
-///                 as GfTerm {src, len}
-///   K row items, each RowHeader (2 words) + pick words:
-///     dst[0,n) = keep(dst,valid) ^ acc0 ^ mix * acc1, where acc0 gathers
-///     the sums of mask0 and the picks with acc=0, acc1 those of mask1 and
-///     the picks with acc=1; then `litLen` literal bytes (the recovery
-///     footer) at dst+n.  Picks are uint16 (table index | acc << 15), eight
-///     per word.
-/// All rows of a batch read the same sums, so the device touches each sum
-/// tile once per batch instead of once per row, and the host sends a few
-/// bytes per pick instead of a 16-byte term.
+///                 mix = lane-sum entries S, termCount = T
+///   T words       the source table as GfTerm {src, len}: the S lane sums
+///                 of the batch first, then every distinct symbol an LDPC
+///                 pair of some row picked
+///   K row items, each RowHeader (3 words) + pick words:
+///     dst[0,n) = keep(dst,valid) ^ acc0 ^ mix * acc1 over the row's picks
+///     (uint16 table index | acc << 15, eight per word: the sums its opcode
+///     selects, then its LDPC pairs), then `litLen` literal bytes (the
+///     recovery footer) at dst+n.
+/// All rows of a batch share one table, so the host sends 2 bytes per
+/// source instead of a 16-byte term, and the sums stay hot on the device.
 struct RowHeader
 {
     uint64_t dst;
@@ -88,8 +85,7 @@ struct RowHeader
     uint32_t valid;
     uint32_t kindPicks;   // OP_ROW | npicks << 8
     uint32_t mix;         // RX multiplier of acc1 | litLen << 8
-    uint32_t mask0;       // 24-bit sum masks
-    uint32_t mask1;
+    uint32_t reserved[2];
     uint8_t lit[8];       // literal bytes written at dst + n
     uint32_t pad[2];
 };
@@ -100,6 +96,7 @@ constexpr unsigned kMaxRowsTable = 0x7fff;   // table indices fit 15 bits
 
 inline uint32_t op_words(const GfOp& op)
 {
+    // (an OP_ROWS header's words cover its table; its rows follow as items)
     return kOpWords + ((op.kind == OP_LINCOMB || op.kind == OP_ROWS) ? op.termCount : 0);
 }
 

@@ -164,9 +164,8 @@ void exec_tile(const uint8_t* stream, const ExecItem& it)
         }
         if (op.kind != OP_ROWS)
             std::abort();
-        // OP_ROWS: S sums, T table entries, then K row items (ops.h)
-        const GfTerm* sums = reinterpret_cast<const GfTerm*>(body);
-        const GfTerm* table = sums + op.mix;
+        // OP_ROWS: T table entries (lane sums first), then K row items (ops.h)
+        const GfTerm* table = reinterpret_cast<const GfTerm*>(body);
         for (uint32_t r = 0; r < op.n; ++r, ++oi) {
             RowHeader h;
             std::memcpy(&h, w, sizeof(h));
@@ -178,12 +177,6 @@ void exec_tile(const uint8_t* stream, const ExecItem& it)
             if (w > end)
                 std::abort();
             terms.clear();
-            for (uint32_t k = 0; k < op.mix; ++k) {
-                if (h.mask0 >> k & 1)
-                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 0});
-                if (h.mask1 >> k & 1)
-                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 1});
-            }
             for (uint32_t k = 0; k < npicks; ++k) {
                 const uint32_t idx = picks[k] & 0x7fff;
                 if (idx >= op.valid)
