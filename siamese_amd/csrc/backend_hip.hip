@@ -524,7 +524,11 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 // traffic is one read and one write of each row instead of ~m of each.
 //
 // Global path (larger m): wave 0 alone, rows updated in place in HBM.
-constexpr unsigned kSolveWaves = 4;
+//
+// The staged rows take m KiB of LDS, so only one or two workgroups fit on a
+// CU: sixteen waves per workgroup keep four waves per SIMD to hide the LDS
+// and scalar-load latency of each row update.
+constexpr unsigned kSolveWaves = 16;
 constexpr unsigned kSolveLdsMaxRows = 120;
 
 // LDS bytes of the staged solve: row tiles, the transposed coefficient

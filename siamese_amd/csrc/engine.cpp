@@ -663,10 +663,11 @@ void Engine::flush()
     // ---- 1. layout -----------------------------------------------------------
     std::vector<Program*> progs[2];
     for (Shard* s : shards)
-        for (Program* p : s->dirty) {
-            p->rows_close();
+        for (Program* p : s->dirty)
             progs[p->group_ & 1].push_back(p);
-        }
+    // seal every open Siamese row batch (serialises its table and rows)
+    for (int g = 0; g < 2; ++g)
+        pool().run(progs[g].size(), [&](size_t i) { progs[g][i]->rows_close(); });
 
     uint32_t resultWords = 0;
     std::vector<uint32_t> resultBase[2];
