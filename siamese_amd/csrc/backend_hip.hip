@@ -49,38 +49,6 @@ __device__ __forceinline__ uint4 gf_mul16(uint4 v, uint32_t y)
     return r;
 }
 
-// Four packed bytes times 2 in GF(2^8) mod 0x14D (a carry out of bit 7
-// folds back as 0x4D).
-__device__ __forceinline__ uint32_t xtime4(uint32_t x)
-{
-    return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x4du);
-}
-
-// m[b] = x * 2^b, b = 0..7: the product of x by any y is then the XOR of
-// the multiples selected by y's bits (gf_mul_by), with no table fetch.
-__device__ __forceinline__ void gf_multiples(uint4 x, uint4 (&m)[8])
-{
-    m[0] = x;
-#pragma unroll
-    for (unsigned b = 1; b < 8; ++b)
-        m[b] = make_uint4(xtime4(m[b - 1].x), xtime4(m[b - 1].y), xtime4(m[b - 1].z),
-                          xtime4(m[b - 1].w));
-}
-
-__device__ __forceinline__ uint4 gf_mul_by(const uint4 (&m)[8], uint32_t y)
-{
-    uint4 r = make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (unsigned b = 0; b < 8; ++b) {
-        const uint32_t s = 0u - ((y >> b) & 1u);   // all ones if bit b of y is set
-        r.x ^= m[b].x & s;
-        r.y ^= m[b].y & s;
-        r.z ^= m[b].z & s;
-        r.w ^= m[b].w & s;
-    }
-    return r;
-}
-
 __device__ __forceinline__ uint32_t byte_mask(int n)
 {
     // mask of the low n bytes of a dword, n clamped to [0,4]
@@ -635,26 +603,22 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
             src = mask16(src, (int)L - (int)p);
         const uint8_t* col = Ct + i * m;
         const uint32_t first = i + 1 + ((wave + kSolveWaves - (i + 1) % kSolveWaves) % kSolveWaves);
-        if (first < m) {
-            // src * 2^b once per step; each row update is then an XOR of the
-            // multiples its coefficient's bits select (no table fetches)
-            uint4 mul[8];
-            gf_multiples(src, mul);
-            for (uint32_t j0 = first; j0 < m; j0 += 4 * kSolveWaves) {
-                uint32_t y[4];
-                uint4 xr[4];
+        // four independent row updates at a time, so the coefficient and
+        // table fetches of one overlap those of the others
+        for (uint32_t j0 = first; j0 < m; j0 += 4 * kSolveWaves) {
+            uint32_t y[4];
+            uint4 xr[4];
 #pragma unroll
-                for (unsigned u = 0; u < 4; ++u) {
-                    const uint32_t j = j0 + u * kSolveWaves;
-                    y[u] = j < m ? uni(col[j]) : 0;
-                    xr[u] = j < m ? X[j * 64 + lane] : make_uint4(0, 0, 0, 0);
-                }
+            for (unsigned u = 0; u < 4; ++u) {
+                const uint32_t j = j0 + u * kSolveWaves;
+                y[u] = j < m ? uni(col[j]) : 0;
+                xr[u] = j < m ? X[j * 64 + lane] : make_uint4(0, 0, 0, 0);
+            }
 #pragma unroll
-                for (unsigned u = 0; u < 4; ++u) {
-                    const uint32_t j = j0 + u * kSolveWaves;
-                    if (y[u])
-                        X[j * 64 + lane] = xor16(xr[u], gf_mul_by(mul, y[u]));
-                }
+            for (unsigned u = 0; u < 4; ++u) {
+                const uint32_t j = j0 + u * kSolveWaves;
+                if (y[u])
+                    X[j * 64 + lane] = xor16(xr[u], gf_mul16(src, y[u]));
             }
         }
         __syncthreads();
@@ -671,11 +635,7 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
         x = mask16(x, (int)bb - (int)p); // zero beyond the recovered length
         if ((uint32_t)i % kSolveWaves == wave && p < finB[i])
             st16(R[i].buf + p, x);
-        if (tileBase < bb && wave < (uint32_t)i) {
-            // x * 2^b once per step (masking commutes with the bytewise
-            // product, so each row masks the product to its own length)
-            uint4 mul[8];
-            gf_multiples(x, mul);
+        if (tileBase < bb) {
             for (uint32_t j0 = wave; j0 < (uint32_t)i; j0 += 4 * kSolveWaves) {
                 uint32_t c[4], fj[4];
                 uint4 xr[4];
@@ -692,8 +652,8 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
                         continue;
                     const uint32_t j = j0 + u * kSolveWaves;
                     const uint32_t ab = bb < fj[u] ? bb : fj[u];
-                    const uint4 prod = mask16(gf_mul_by(mul, c[u]), (int)ab - (int)p);
-                    X[j * 64 + lane] = xor16(xr[u], prod);
+                    const uint4 xs = mask16(x, (int)ab - (int)p);
+                    X[j * 64 + lane] = xor16(xr[u], gf_mul16(xs, c[u]));
                 }
             }
         }
