@@ -113,6 +113,20 @@ def run_rank(rank, world, local, args, library, use_cuda):
                         groups=args.groups)
     coll.barrier()
     elapsed = time.perf_counter() - t0
+
+    # End-to-end (PCIe-inclusive) leg, timed separately: the originals start
+    # in pinned host memory and every recovery packet and recovered original
+    # is copied back to the host.  Reported beside, never as, `value`.
+    e2e_elapsed = None
+    if args.e2e:
+        sess.run(steps=0, warmup=1, verify=False, threads=args.threads, groups=args.groups,
+                 e2e=True)
+        coll.barrier()
+        t1 = time.perf_counter()
+        _, rep_e2e = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
+                              groups=args.groups, e2e=True)
+        coll.barrier()
+        e2e_elapsed = time.perf_counter() - t1
     sess.close()
 
     eng = S.engine_dict(rep)
@@ -124,6 +138,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
     t_max, = coll.reduce([elapsed], "max")
     alg_total, payload_total, streams_total = coll.reduce(
         [float(alg_bytes), float(payload), float(cfg.streams)], "sum")
+    e2e_max = coll.reduce([e2e_elapsed], "max")[0] if e2e_elapsed is not None else None
     if rank != 0:
         return None
 
@@ -190,7 +205,17 @@ def run_rank(rank, world, local, args, library, use_cuda):
                     "(HIP events on the codec stream)",
         },
         "cpu_baseline": None,
+        "end_to_end": None,
     }
+    if e2e_max is not None:
+        line["end_to_end"] = {
+            "value": round(alg_total / e2e_max / 1e9, 3),
+            "unit": "GB/s",
+            "payload_GBps": round(payload_total / e2e_max / 1e9, 3),
+            "ms_per_step": round(e2e_max / steps * 1e3, 3),
+            "note": "originals H2D from pinned host memory each step; every recovery packet "
+                    "and recovered original D2H (PCIe-inclusive; not `value`)",
+        }
     if not args.no_cpu:
         threads = min(16, os.cpu_count() or 1)
         per_stream = alg_bytes / steps / args.streams
@@ -210,6 +235,8 @@ def main(argv=None):
                     help="host threads driving streams (0 = library default)")
     ap.add_argument("--groups", type=int, default=2,
                     help="stream groups alternating host and device work (1 = no overlap)")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false",
+                    help="skip the PCIe-inclusive end-to-end leg")
     ap.add_argument("--library", default=S.AMD_LIB, help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 

@@ -36,6 +36,8 @@ struct BatchOptions
     int32_t device;    ///< HIP device (-1 = current)
     uint32_t threads;  ///< host threads driving streams (0 = default)
     uint32_t groups;   ///< stream groups alternating host work and device work (0 = 1)
+    uint32_t e2e;      ///< originals start in pinned host memory (H2D each step) and every
+                       ///< recovery packet and recovered original is copied back (D2H)
 };
 
 struct BatchReport
@@ -80,6 +82,8 @@ struct Api
     int (*submit)(void);
     void* (*device_alloc)(size_t);
     void (*device_free)(void*);
+    void* (*host_alloc)(size_t);
+    void (*host_free)(void*);
     int (*h2d)(void*, const void*, size_t);
     int (*gather)(unsigned, const void* const*, const unsigned*, void*);
     void (*timing)(int, int, double*, double*);
@@ -112,6 +116,7 @@ bool load_api(const char* path, Api& a)
            bind(h, a.decoder_is_ready, "sgpu_decoder_is_ready") && bind(h, a.decode, "sgpu_decode") &&
            bind(h, a.decoder_get, "sgpu_decoder_get") && bind(h, a.flush, "sgpu_flush") && bind(h, a.submit, "sgpu_submit") &&
            bind(h, a.device_alloc, "sgpu_device_alloc") && bind(h, a.device_free, "sgpu_device_free") &&
+           bind(h, a.host_alloc, "sgpu_host_alloc") && bind(h, a.host_free, "sgpu_host_free") &&
            bind(h, a.h2d, "sgpu_h2d") && bind(h, a.gather, "sgpu_gather") &&
            bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats");
 }
@@ -150,6 +155,10 @@ struct Shared
     size_t stride;
     bool hashData;
     bool verify;
+    bool e2e = false;         // packets start and end in host memory (timed copies)
+    uint8_t* hostPayload = nullptr;   // pinned host copy of every original (e2e)
+    uint8_t* devBase = nullptr;       // its device-resident counterpart
+    size_t payloadBytes = 0;
     uint64_t checked = 0, mismatches = 0;
     std::unique_ptr<sgpu::WorkerPool> pool;
     unsigned groups = 1;
@@ -212,7 +221,8 @@ struct BatchCodec
 
     uint64_t rec_token(const Rec& r)
     {
-        if (sh->hashData)
+        // end-to-end mode: every recovery packet goes back to host memory
+        if (sh->hashData || sh->e2e)
             cur.push_back(Request{log, log->size(), r.pkt.DeviceData, r.bytes, 0, false, nullptr});
         return r.bytes;
     }
@@ -226,7 +236,7 @@ struct BatchCodec
                 std::fprintf(stderr, "pkt_token: id %u entry %d bytes %u want %u data %p\n", id,
                              p.entry != nullptr, bytes, want, data);
             *ok = false;
-        } else if (sh->hashData || sh->verify)
+        } else if (sh->hashData || sh->verify || sh->e2e)
             cur.push_back(Request{log, log->size(), data, bytes, id, true, ok});
         return bytes;
     }
@@ -262,7 +272,7 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
     for (const Request& r : reqs) {
         const uint8_t* d = host.data() + off;
         off += r.bytes;
-        if (r.isPacket) {
+        if (r.isPacket && (sh.verify || sh.hashData)) {
             expect.resize(r.bytes + 8);
             scen::fill_payload(r.id, expect.data(), r.bytes);
             ++sh.checked;
@@ -300,6 +310,8 @@ int run_once(Shared& sh, StreamResult* results, uint64_t* rounds, double* phase)
         phase[k] += std::chrono::duration<double>(now - t).count();
         t = now;
     };
+    if (sh.e2e && api.h2d(sh.devBase, sh.hostPayload, sh.payloadBytes) != 0)
+        return -3;   // the originals arrive in (pinned) host memory
     std::vector<BatchCodec> codecs(n);
     std::unique_ptr<BatchStream[]> streams(new BatchStream[n]);
     for_streams(sh, n, [&](size_t s) {
@@ -417,6 +429,7 @@ struct Session
     Api* api;
     ScenarioConfig cfg;
     uint8_t* dev = nullptr;
+    size_t payloadBytes = 0;
     Shared sh;
     double setupSeconds = 0;
 };
@@ -451,6 +464,7 @@ void* scenario_batch_open(const char* lib, const ScenarioConfig* cfg, int device
         delete ss;
         return nullptr;
     }
+    ss->payloadBytes = total * stride;
     const size_t chunkPackets = std::max<size_t>(1, (size_t)(64u << 20) / stride);
     std::vector<uint8_t> host(chunkPackets * stride);
     for (size_t base = 0; base < total; base += chunkPackets) {
@@ -482,6 +496,21 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
     std::memset(report, 0, sizeof(*report));
     report->setup_seconds = ss->setupSeconds;
     sh.checked = sh.mismatches = 0;
+    sh.e2e = opt->e2e != 0;
+    if (sh.e2e && !sh.hostPayload) {
+        // a pinned host image of the device payload area (untimed)
+        sh.payloadBytes = ss->payloadBytes;
+        sh.devBase = ss->dev;
+        sh.hostPayload = (uint8_t*)api.host_alloc(sh.payloadBytes);
+        if (!sh.hostPayload)
+            return -2;
+        const ScenarioConfig* c = &ss->cfg;
+        for (size_t k = 0; k < (size_t)c->streams * c->originals; ++k) {
+            const unsigned id = (unsigned)((size_t)c->first_stream * c->originals + k);
+            const unsigned b = c->payload_bytes ? c->payload_bytes : scen::variable_bytes(id);
+            scen::fill_payload(id, sh.hostPayload + k * sh.stride, b);
+        }
+    }
     int rc = 0;
     const unsigned runs = opt->warmup + opt->steps;
     for (unsigned r = 0; r < runs && rc == 0; ++r) {
@@ -525,6 +554,8 @@ void scenario_batch_close(void* session)
     if (!ss)
         return;
     ss->api->device_free(ss->dev);
+    if (ss->sh.hostPayload)
+        ss->api->host_free(ss->sh.hostPayload);
     delete ss;
 }
 

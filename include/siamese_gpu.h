@@ -84,6 +84,9 @@ SIAMESE_EXPORT int sgpu_submit(void);
 /// Device memory helpers for applications and the benchmark harness.
 SIAMESE_EXPORT void* sgpu_device_alloc(size_t bytes);
 SIAMESE_EXPORT void sgpu_device_free(void* p);
+/// Page-locked host memory (packet staging for DMA to and from the GPU).
+SIAMESE_EXPORT void* sgpu_host_alloc(size_t bytes);
+SIAMESE_EXPORT void sgpu_host_free(void* p);
 SIAMESE_EXPORT int sgpu_h2d(void* deviceDst, const void* hostSrc, size_t bytes);
 /// Gather `count` device ranges into one host buffer (concatenated in order).
 /// Runs immediately; queued-but-unflushed codec work is left untouched.

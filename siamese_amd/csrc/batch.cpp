@@ -210,6 +210,20 @@ SIAMESE_EXPORT void sgpu_device_free(void* p)
     be_dev_free(p);
 }
 
+SIAMESE_EXPORT void* sgpu_host_alloc(size_t bytes)
+{
+    if (!g_batchReady)
+        return nullptr;
+    Lock lock(Engine::global()->mutex());
+    return be_host_alloc(bytes);
+}
+
+SIAMESE_EXPORT void sgpu_host_free(void* p)
+{
+    Lock lock(Engine::global()->mutex());
+    be_host_free(p);
+}
+
 SIAMESE_EXPORT int sgpu_h2d(void* deviceDst, const void* hostSrc, size_t bytes)
 {
     Engine* eng = Engine::global();
