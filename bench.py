@@ -39,6 +39,21 @@ STREAMS_PER_GPU = 1024
 METRIC = "device-resident GB/s encode+decode, 1400B pkts @20% loss; % HBM peak"
 
 
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_traffic.json")
+TRAFFIC_NOTE = ("HBM bytes per k_exec launch from rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE "
+                "of `bench.py --steps 1 --warmup 1 --no-cpu --no-e2e` (profiles/r1_traffic.json, "
+                "tools/pmc_traffic.py); compare with exec_bytes_per_launch")
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM traffic of `kernel` from the committed PMC profile."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            return json.load(f)[kernel]["traffic_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def workload(rank, streams):
     return S.replace(S.CONFIGS["C4"], streams=streams, first_stream=rank * streams,
                      hash_data=0)
@@ -198,8 +213,11 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": None,
+            "traffic": pmc_traffic("sgpu::k_exec"),
+            "traffic_source": TRAFFIC_NOTE,
             "exec_bytes_per_step": exec_bytes // steps,
+            "exec_launches_per_step": eng["exec_launches"] / steps,
+            "exec_bytes_per_launch": exec_bytes // max(1, eng["exec_launches"]),
             "exec_ms_per_step": round(rep.exec_ms / steps, 4),
             "note": "achieved = k_exec's algorithmic bytes / summed k_exec launch time "
                     "(HIP events on the codec stream)",

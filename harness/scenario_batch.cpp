@@ -47,7 +47,7 @@ struct BatchReport
     double exec_ms;        ///< device time of the executor launches only
     double setup_seconds;  ///< payload generation + staging (untimed)
     uint64_t rounds;       ///< rounds (flushes) in the timed steps
-    uint64_t engine[14];   ///< engine counters over the timed steps (see sgpu_engine_stats)
+    uint64_t engine[15];   ///< engine counters over the timed steps (see sgpu_engine_stats)
     uint64_t checked;      ///< packets whose bytes were verified
     uint64_t mismatches;   ///< verification failures
     /// wall time of the timed steps split by phase: codec create, stream
@@ -60,7 +60,7 @@ struct BatchReport
 
 namespace {
 
-constexpr int kEngineStats = 14;
+constexpr int kEngineStats = 15;
 using Clock = std::chrono::steady_clock;
 
 struct Api
@@ -159,6 +159,7 @@ struct Shared
     uint8_t* hostPayload = nullptr;   // pinned host copy of every original (e2e)
     uint8_t* devBase = nullptr;       // its device-resident counterpart
     size_t payloadBytes = 0;
+    std::vector<uint8_t> landing;     // host buffer the packets are gathered into
     uint64_t checked = 0, mismatches = 0;
     std::unique_ptr<sgpu::WorkerPool> pool;
     unsigned groups = 1;
@@ -259,7 +260,10 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
         lens.push_back(r.bytes);
         total += r.bytes;
     }
-    std::vector<uint8_t> host(total + 16);
+    // the host side of the packets (kept across rounds: no page faults per round)
+    std::vector<uint8_t>& host = sh.landing;
+    if (host.size() < total + 16)
+        host.resize(total + 16);
     if (sh.api->gather((unsigned)reqs.size(), srcs.data(), lens.data(), host.data()) != 0) {
         for (const Request& r : reqs)
             if (r.ok)

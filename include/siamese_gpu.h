@@ -95,12 +95,13 @@ SIAMESE_EXPORT int sgpu_gather(unsigned count, const void* const* deviceSrcs, co
 
 /// Device timing of flushed work since the last reset (milliseconds).
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs);
-/// Engine counters (14 values): flushes, launches, ops, terms, solves,
+/// Engine counters (15 values): flushes, launches, ops, terms, solves,
 /// ingests, upload bytes, algorithmic op bytes, algorithmic output bytes,
 /// the part of the algorithmic bytes handled by the solve kernels, then host
 /// nanoseconds spent assembling flushes, waiting for the device,
-/// running completions, and reclaiming released buffers.
-SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out14);
+/// running completions, and reclaiming released buffers, then the number of
+/// executor launches.
+SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15);
 
 #ifdef __cplusplus
 }

@@ -252,13 +252,14 @@ SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* t
         be_timing_reset();
 }
 
-SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out14)
+SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15)
 {
     const EngineStats s = Engine::global()->stats();
-    const uint64_t v[14] = {s.flushes,    s.launches,    s.ops,        s.terms,    s.solves,
+    const uint64_t v[15] = {s.flushes,    s.launches,    s.ops,        s.terms,    s.solves,
                             s.ingests,    s.uploadBytes, s.refOpBytes, s.outBytes, s.solveBytes,
-                            s.assembleNs, s.waitNs,      s.completeNs, s.reclaimNs};
-    std::memcpy(out14, v, sizeof(v));
+                            s.assembleNs, s.waitNs,      s.completeNs, s.reclaimNs,
+                            s.execLaunches};
+    std::memcpy(out15, v, sizeof(v));
 }
 
 } // extern "C"

@@ -27,6 +27,7 @@ void EngineStats::add(const EngineStats& o)
     waitNs += o.waitNs;
     completeNs += o.completeNs;
     reclaimNs += o.reclaimNs;
+    execLaunches += o.execLaunches;
 }
 
 namespace {
@@ -852,6 +853,7 @@ void Engine::flush()
         if (ph.kind == Phase::EXEC) {
             be_launch_exec(upDev_ + oStream, (const ExecItem*)(upDev_ + oItems) + ph.itemBegin,
                            (uint32_t)ph.itemCount);
+            flushStats_.execLaunches++;
         } else {
             const SolveDesc* sd = (const SolveDesc*)(upDev_ + oSD) + ph.solveBegin;
             be_launch_solve_prefix(sd, (const SolveRow*)(upDev_ + oSR), upDev_ + oCoef, resultsDev,
@@ -944,13 +946,29 @@ bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* byt
     be_launch_ingest((const IngestDesc*)gUpDev_, count);
     be_d2h(gHost_, gDev_, total);
     const bool ok = be_sync();
-    uint8_t* out = (uint8_t*)hostOut;
-    size_t off = 0;
+    // unpack the 16-byte-aligned staging layout into the caller's buffer,
+    // in parallel chunks (this is the D2H leg of end-to-end packet flows)
+    constexpr unsigned kChunk = 2048;
+    std::vector<size_t> outOff((count + kChunk - 1) / kChunk + 1), inOff(outOff.size());
+    size_t o = 0, in = 0;
     for (unsigned i = 0; i < count; ++i) {
-        std::memcpy(out, gHost_ + off, bytes[i]);
-        out += bytes[i];
-        off = align16(off + bytes[i]);
+        if (i % kChunk == 0) {
+            outOff[i / kChunk] = o;
+            inOff[i / kChunk] = in;
+        }
+        o += bytes[i];
+        in = align16(in + bytes[i]);
     }
+    pool().run((count + kChunk - 1) / kChunk, [&](size_t c) {
+        uint8_t* out = (uint8_t*)hostOut + outOff[c];
+        size_t off = inOff[c];
+        const unsigned end = std::min<unsigned>(count, (unsigned)(c + 1) * kChunk);
+        for (unsigned i = (unsigned)c * kChunk; i < end; ++i) {
+            std::memcpy(out, gHost_ + off, bytes[i]);
+            out += bytes[i];
+            off = align16(off + bytes[i]);
+        }
+    });
     return ok;
 }
 

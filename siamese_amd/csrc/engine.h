@@ -180,6 +180,7 @@ struct EngineStats
     // host time of flush assembly, device waits, completion callbacks and
     // returning released buffers to the free lists (nanoseconds)
     uint64_t assembleNs = 0, waitNs = 0, completeNs = 0, reclaimNs = 0;
+    uint64_t execLaunches = 0;   // executor launches (part of `launches`)
 
     void add(const EngineStats& o);
 };
