@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <malloc.h>
 #include <memory>
 
 extern "C" {
@@ -453,6 +454,12 @@ void* scenario_batch_open(const char* lib, const ScenarioConfig* cfg, int device
     }
     if (g_api.init(device) != 0)
         return nullptr;
+    // Application-side allocator tuning: every step creates and frees
+    // thousands of codecs; keep freed heap memory in the process instead of
+    // returning it to the kernel and faulting it back in on the next step.
+    mallopt(M_MMAP_THRESHOLD, 32 << 20);
+    mallopt(M_TRIM_THRESHOLD, 1 << 30);
+    mallopt(M_TOP_PAD, 64 << 20);
     Session* ss = new Session;
     ss->api = &g_api;
     ss->cfg = *cfg;

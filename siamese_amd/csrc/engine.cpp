@@ -261,12 +261,14 @@ void Program::rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, ui
         // the sums are the first table entries; LDPC sources follow
         b.table.assign(sums, sums + sumCount);
         b.rowBytes.clear();
+        if (b.rowBytes.capacity() == 0)
+            b.rowBytes.reserve(16384);
         b.maxExtent = 0;
-        if (b.keys.empty()) {
-            b.keys.assign(1024, 0);
-            b.vals.assign(1024, 0);
-        } else {
-            std::fill(b.keys.begin(), b.keys.end(), 0);
+        // a new generation empties the source map without touching it
+        if (b.slotGen.empty() || ++b.gen == 0) {
+            b.slotGen.assign(b.slotGen.empty() ? 1024 : b.slotGen.size(), 0);
+            b.slotIdx.resize(b.slotGen.size());
+            b.gen = 1;
         }
     }
     RowHeader h;
@@ -298,8 +300,10 @@ void Program::rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, ui
 void Program::add_pick(uint16_t pick)
 {
     RowsBuild& b = rb_;
-    if (b.curPicks % kPicksPerWord == 0)
-        b.rowBytes.resize(b.rowBytes.size() + 16, 0);
+    if (b.curPicks % kPicksPerWord == 0) {
+        static const uint8_t zero[16] = {};
+        b.rowBytes.insert(b.rowBytes.end(), zero, zero + 16);
+    }
     const size_t at = b.rowBytes.size() - 16 + (b.curPicks % kPicksPerWord) * 2;
     std::memcpy(b.rowBytes.data() + at, &pick, 2);
     ++b.curPicks;
@@ -307,38 +311,36 @@ void Program::add_pick(uint16_t pick)
 
 uint16_t Program::rows_table_index(uint64_t src, uint32_t len)
 {
+    // Open-addressing map src -> table index.  A slot is live iff its
+    // generation is the batch's; the key is the table entry it points to.
     RowsBuild& b = rb_;
-    if (b.table.size() * 2 >= b.keys.size()) {
-        // grow the map (load factor <= 1/2)
-        std::vector<uint64_t> oldKeys;
-        std::vector<uint16_t> oldVals;
-        oldKeys.swap(b.keys);
-        oldVals.swap(b.vals);
-        b.keys.assign(oldKeys.size() * 2, 0);
-        b.vals.assign(oldKeys.size() * 2, 0);
-        const size_t mask = b.keys.size() - 1;
-        for (size_t i = 0; i < oldKeys.size(); ++i) {
-            if (!oldKeys[i])
-                continue;
-            size_t h = (oldKeys[i] >> 6) * 0x9E3779B97F4A7C15ULL >> 20;
-            while (b.keys[h & mask])
+    auto slot_of = [](uint64_t key) { return (size_t)((key >> 6) * 0x9E3779B97F4A7C15ULL >> 20); };
+    if ((b.table.size() - b.sumCount) * 2 >= b.slotGen.size()) {
+        // grow (load factor <= 1/2) and re-insert this batch's sources
+        b.slotGen.assign(b.slotGen.size() * 2, 0);
+        b.slotIdx.assign(b.slotGen.size(), 0);
+        b.gen = 1;
+        const size_t mask = b.slotGen.size() - 1;
+        for (size_t i = b.sumCount; i < b.table.size(); ++i) {
+            size_t h = slot_of(b.table[i].src);
+            while (b.slotGen[h & mask] == b.gen)
                 ++h;
-            b.keys[h & mask] = oldKeys[i];
-            b.vals[h & mask] = oldVals[i];
+            b.slotGen[h & mask] = b.gen;
+            b.slotIdx[h & mask] = (uint16_t)i;
         }
     }
-    const size_t mask = b.keys.size() - 1;
-    size_t h = (src >> 6) * 0x9E3779B97F4A7C15ULL >> 20;
+    const size_t mask = b.slotGen.size() - 1;
+    size_t h = slot_of(src);
     for (;; ++h) {
-        const uint64_t k = b.keys[h & mask];
-        if (k == src)
-            return b.vals[h & mask];
-        if (k == 0)
+        if (b.slotGen[h & mask] != b.gen)
             break;
+        const uint16_t i = b.slotIdx[h & mask];
+        if (b.table[i].src == src)
+            return i;
     }
     const uint16_t idx = (uint16_t)b.table.size();
-    b.keys[h & mask] = src;
-    b.vals[h & mask] = idx;
+    b.slotGen[h & mask] = b.gen;
+    b.slotIdx[h & mask] = idx;
     GfTerm t;
     t.src = src;
     t.len = len;

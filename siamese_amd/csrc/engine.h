@@ -130,8 +130,9 @@ private:
         unsigned sumCount = 0;
         unsigned rows = 0;
         std::vector<GfTerm> table;
-        std::vector<uint64_t> keys;      // open-addressing map src -> table index
-        std::vector<uint16_t> vals;
+        std::vector<uint32_t> slotGen;   // open-addressing map src -> table index:
+        std::vector<uint16_t> slotIdx;   // a slot is live iff slotGen == gen
+        uint32_t gen = 0;
         std::vector<uint8_t> rowBytes;   // serialized row items
         size_t curRow = 0;               // offset of the current row's header
         unsigned curPicks = 0;
