@@ -234,7 +234,8 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "note": "originals H2D from pinned host memory each step; every recovery packet "
                     "and recovered original D2H (PCIe-inclusive; not `value`)",
         }
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:
+        # the reference on the host cores, rank 0 at N=1 only
         threads = min(16, os.cpu_count() or 1)
         per_stream = alg_bytes / steps / args.streams
         line["cpu_baseline"] = cpu_baseline(args.cpu_streams, threads, per_stream)

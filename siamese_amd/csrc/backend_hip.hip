@@ -753,6 +753,20 @@ namespace {
 
 hipStream_t g_stream = nullptr;
 bool g_ready = false;
+int g_device = 0;
+
+// The HIP current device is per host thread, and codec calls (buffer
+// allocation) run on the application's threads: make each thread that
+// reaches the backend use the engine's device (one process per GPU, the
+// device chosen at init).
+inline void bind_device()
+{
+    thread_local int bound = -1;
+    if (bound != g_device) {
+        (void)hipSetDevice(g_device);
+        bound = g_device;
+    }
+}
 bool g_timing = false;
 // largest m staged in LDS: 56 keeps solve_lds_bytes under the default 64 KiB
 // dynamic-LDS limit; raised at init when the device grants more
@@ -786,6 +800,7 @@ struct Timed
     bool on;
     explicit Timed(bool exec) : on(g_timing)
     {
+        bind_device();
         if (on) {
             ev = take_events(exec);
             (void)hipEventRecord(ev.a, g_stream);
@@ -824,6 +839,7 @@ bool be_init(int device, const char** err)
     }
     int cur = 0;
     (void)hipGetDevice(&cur);
+    g_device = cur;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, cur) != hipSuccess) {
         *err = "hipGetDeviceProperties failed";
@@ -873,6 +889,7 @@ const char* be_name() { return "hip-gfx950"; }
 
 void* be_dev_alloc(size_t bytes)
 {
+    bind_device();
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess)
         return nullptr;
@@ -881,12 +898,14 @@ void* be_dev_alloc(size_t bytes)
 
 void be_dev_free(void* p)
 {
+    bind_device();
     if (p)
         (void)hipFree(p);
 }
 
 void* be_host_alloc(size_t bytes)
 {
+    bind_device();
     void* p = nullptr;
     if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess)
         return nullptr;
@@ -895,22 +914,26 @@ void* be_host_alloc(size_t bytes)
 
 void be_host_free(void* p)
 {
+    bind_device();
     if (p)
         (void)hipHostFree(p);
 }
 
 void be_h2d(void* dst, const void* src, size_t bytes)
 {
+    bind_device();
     check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g_stream), "H2D");
 }
 
 void be_d2h(void* dst, const void* src, size_t bytes)
 {
+    bind_device();
     check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, g_stream), "D2H");
 }
 
 void be_memset(void* dst, int value, size_t bytes)
 {
+    bind_device();
     check(hipMemsetAsync(dst, value, bytes, g_stream), "memset");
 }
 
@@ -955,6 +978,7 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
 
 bool be_sync()
 {
+    bind_device();
     const hipError_t e = hipStreamSynchronize(g_stream);
     if (e != hipSuccess) {
         check(e, "hipStreamSynchronize");
