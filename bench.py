@@ -195,6 +195,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "terms_per_step": eng["terms"] / steps,
             "algorithmic_bytes_per_step": alg_bytes // steps,
             "upload_bytes_per_step": eng["upload_bytes"] // steps,
+            "arena_growth_bytes": eng["arena_growth"],
             "rank0_digest": digest,
         },
         "host": {
@@ -245,10 +246,10 @@ def run_rank(rank, world, local, args, library, use_cuda):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--streams", type=int, default=STREAMS_PER_GPU)
-    ap.add_argument("--cpu-streams", type=int, default=4096)
+    ap.add_argument("--cpu-streams", type=int, default=16384)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--threads", type=int, default=0,
                     help="host threads driving streams (0 = library default)")

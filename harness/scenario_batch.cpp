@@ -48,7 +48,8 @@ struct BatchReport
     double exec_ms;        ///< device time of the executor launches only
     double setup_seconds;  ///< payload generation + staging (untimed)
     uint64_t rounds;       ///< rounds (flushes) in the timed steps
-    uint64_t engine[15];   ///< engine counters over the timed steps (see sgpu_engine_stats)
+    uint64_t engine[16];   ///< engine counters over the timed steps (see sgpu_engine_stats),
+                           ///< then the arena growth (sgpu_arena_bytes)
     uint64_t checked;      ///< packets whose bytes were verified
     uint64_t mismatches;   ///< verification failures
     /// wall time of the timed steps split by phase: codec create, stream
@@ -89,6 +90,7 @@ struct Api
     int (*gather)(unsigned, const void* const*, const unsigned*, void*);
     void (*timing)(int, int, double*, double*);
     void (*engine_stats)(uint64_t*);
+    uint64_t (*arena_bytes)(void);
 };
 
 template <class F>
@@ -119,7 +121,8 @@ bool load_api(const char* path, Api& a)
            bind(h, a.device_alloc, "sgpu_device_alloc") && bind(h, a.device_free, "sgpu_device_free") &&
            bind(h, a.host_alloc, "sgpu_host_alloc") && bind(h, a.host_free, "sgpu_host_free") &&
            bind(h, a.h2d, "sgpu_h2d") && bind(h, a.gather, "sgpu_gather") &&
-           bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats");
+           bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats") &&
+           bind(h, a.arena_bytes, "sgpu_arena_bytes");
 }
 
 struct Rec
@@ -533,8 +536,9 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         sh.groups = opt->groups ? opt->groups : 1;
         uint64_t rounds = 0;
         double phase[5] = {0, 0, 0, 0, 0};
-        uint64_t e0[kEngineStats], e1[kEngineStats];
+        uint64_t e0[kEngineStats + 1], e1[kEngineStats + 1];
         api.engine_stats(e0);
+        e0[kEngineStats] = api.arena_bytes();
         api.timing(timed ? 1 : 0, 1, nullptr, nullptr);
         const auto t1 = Clock::now();
         rc = run_once(sh, results, &rounds, phase);
@@ -542,6 +546,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         double execMs = 0, totalMs = 0;
         api.timing(0, 1, &execMs, &totalMs);
         api.engine_stats(e1);
+        e1[kEngineStats] = api.arena_bytes();
         if (timed) {
             report->seconds += dt;
             report->device_ms += totalMs;
@@ -549,7 +554,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
             report->rounds += rounds;
             for (int k = 0; k < 5; ++k)
                 report->phase_seconds[k] += phase[k];
-            for (int k = 0; k < kEngineStats; ++k)
+            for (int k = 0; k <= kEngineStats; ++k)
                 report->engine[k] += e1[k] - e0[k];
         }
     }

@@ -103,6 +103,10 @@ SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* t
 /// executor launches.
 SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15);
 
+/// Device bytes the engine's symbol arena has taken from hipMalloc so far
+/// (grows while warming up, then stays flat: buffers are recycled).
+SIAMESE_EXPORT uint64_t sgpu_arena_bytes(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include "backend.h"
+#include "codedef.h"
 #include "gf.h"
 
 #include <cstdio>
@@ -158,25 +159,56 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
 // ---------------------------------------------------------------------------
 // Executor
 
-// One workgroup of kExecWaves waves per (instance segment, 1 KiB tile).
+// One workgroup of kExecWaves waves per (instance segment, 2 KiB tile): lane
+// L owns bytes [16L, 16L+16) and [1024+16L, 1024+16L+16) of the tile, so a
+// 1400-byte symbol is one work item and every source costs a wave two
+// coalesced 16-byte loads per lane.
 //
 // The segment is one instruction stream (ops.h): each op's header and its
-// term descriptors are contiguous, and the workgroup keeps the current op's
-// block in an LDS ring while one coalesced load per thread prefetches the
-// next op's block, so no op waits on a descriptor round trip.  Each op's
-// terms are dealt round-robin to the waves (wave w takes terms w, w+W, ...),
-// every wave keeps up to kExecDepth source loads in flight, and the partial
-// sums meet in LDS.  Wave 0 merges the destination's kept prefix/tail and
-// stores; the barrier that rotates the ring also orders that store before
-// any later op of the segment reads it (stores from one CU are visible to
-// the CU's other waves after the workgroup-scope fence of __syncthreads).
+// words are contiguous, and the workgroup keeps the current op's first
+// kRingWords words in an LDS ring while one coalesced load per thread
+// prefetches the next op's, so no op waits on a descriptor round trip.
+//
+//   OP_LINCOMB  terms dealt round-robin to the waves (kExecDepth loads of
+//               each chunk in flight per wave), partial sums meet in LDS,
+//               wave 0 merges and stores.
+//   OP_ROWS     the batch's sums + window snapshot are staged in LDS; the
+//               lane-sum updates are dealt to the waves whole (each wave
+//               generates its own terms and CX coefficients), one barrier,
+//               then the rows are dealt to the waves whole: each wave draws
+//               the row's LDPC picks with PCG jump-ahead (one draw per lane),
+//               accumulates sums and picks, and stores the row and footer.
+//               Rows and updates never meet across waves, so the batch has
+//               two barriers however many rows it holds.
+// The barrier that rotates the ring also orders each op's stores before any
+// later op of the segment reads them (stores from one CU are visible to the
+// CU's other waves after the workgroup-scope fence of __syncthreads).
 constexpr unsigned kExecWaves = 4;
 constexpr unsigned kExecThreads = 64 * kExecWaves;
 constexpr unsigned kExecDepth = 8;
 constexpr unsigned kExecSolo = 4;            // ops with <= this many terms run on wave 0 alone
 constexpr unsigned kRingWords = kExecThreads; // one prefetched word per thread
+constexpr unsigned kRowsTableLds = 1024;      // sum + window entries of an OP_ROWS batch in LDS
+constexpr unsigned kChunk = 1024;             // byte distance of a lane's two chunks
+
+__constant__ uint64_t c_pcgA[65];   // A^j
+__constant__ uint64_t c_pcgG[65];   // sum_{t<j} A^t
+__constant__ uint8_t c_sqr[256];
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+struct Acc2
+{
+    uint4 a, b;   // chunk 0 (p) and chunk 1 (p + kChunk)
+};
+
+__device__ __forceinline__ Acc2 zero2()
+{
+    Acc2 r;
+    r.a = make_uint4(0, 0, 0, 0);
+    r.b = r.a;
+    return r;
+}
 
 __device__ __forceinline__ uint4 term_value(uint4 x, uint32_t p, uint32_t len, uint32_t coeff)
 {
@@ -188,47 +220,66 @@ __device__ __forceinline__ uint4 term_value(uint4 x, uint32_t p, uint32_t len, u
 }
 
 // Word `idx` of the current op's block: from the LDS ring while it lasts,
-// then straight from the stream (ops with more than kRingWords-2 terms).
+// then straight from the stream.
 __device__ __forceinline__ uint4 op_word(const uint4* ring, const uint4* __restrict__ seg, uint32_t pos,
                                          uint32_t idx)
 {
     return idx < kRingWords ? ring[idx] : seg[pos + idx];
 }
 
-// Accumulate terms k0, k0+stride, ... (k < nt) into acc0/acc1.  fetch(k,
-// src, len, ca) describes term k (ca = coeff | acc << 8) and returns false
-// for an absent term; every argument is wave-uniform, so the loads of up to
-// kExecDepth terms are issued back to back before the first one is used.
+// Accumulate terms [k0, k1).  fetch(k, src, len, ca) is called once per term
+// with increasing k and describes term k (ca = coeff | acc << 8); it returns
+// false for an absent term.  Fetches keep their descriptors in registers
+// (one term per lane, moved to scalars with readlane), so issuing a term
+// costs no memory round trip: the loads of up to kExecDepth terms (both
+// chunks) go out back to back before the first is used.  A chunk the term
+// does not reach is not loaded.
 template <class Fetch>
-__device__ __forceinline__ void gather(uint32_t nt, uint32_t k0, uint32_t stride, uint32_t p,
-                                       uint4& acc0, uint4& acc1, const Fetch& fetch)
+__device__ __forceinline__ void gather2(uint32_t k0, uint32_t k1, uint32_t tileBase, uint32_t p, Acc2& acc0,
+                                        Acc2& acc1, Fetch&& fetch)
 {
-    for (uint32_t k = k0; k < nt; k += stride * kExecDepth) {
+    const uint32_t p1 = p + kChunk;
+    for (uint32_t k = k0; k < k1; k += kExecDepth) {
         uint32_t len[kExecDepth], ca[kExecDepth];
         bool act[kExecDepth];
-        uint4 v[kExecDepth];
+        uint4 v0[kExecDepth], v1[kExecDepth];
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
-            const uint32_t idx = k + u * stride;
+            const uint32_t idx = k + u;
             uint64_t src = 0;
-            act[u] = idx < nt && fetch(idx, src, len[u], ca[u]);
+            act[u] = idx < k1 && fetch(idx, src, len[u], ca[u]) && tileBase < len[u];
             if (act[u]) {
                 // lanes past the term's end load the term's first line (always
-                // mapped) and mask it away, so no load sits behind a branch
-                v[u] = ld16(src + (p < len[u] ? p : 0));
+                // mapped) and mask it away, so no load sits behind a lane branch
+                v0[u] = ld16(src + (p < len[u] ? p : 0));
+                if (tileBase + kChunk < len[u])
+                    v1[u] = ld16(src + (p1 < len[u] ? p1 : 0));
             }
         }
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
             if (act[u]) {
-                const uint4 x = term_value(v[u], p, len[u], ca[u] & 0xff);
-                if (ca[u] & 0xff00)
-                    acc1 = xor16(acc1, x);
-                else
-                    acc0 = xor16(acc0, x);
+                const uint32_t c = ca[u] & 0xff;
+                const uint4 x0 = term_value(v0[u], p, len[u], c);
+                Acc2& acc = (ca[u] & 0xff00) ? acc1 : acc0;
+                acc.a = xor16(acc.a, x0);
+                if (tileBase + kChunk < len[u])
+                    acc.b = xor16(acc.b, term_value(v1[u], p1, len[u], c));
             }
         }
     }
+}
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+// term descriptor word held by lane j -> scalars
+__device__ __forceinline__ void lane_term(uint4 w, uint32_t j, uint64_t& src, uint32_t& len)
+{
+    src = ((uint64_t)rl(w.y, j) << 32) | rl(w.x, j);
+    len = rl(w.z, j);
 }
 
 __device__ __forceinline__ void read_term(uint4 w, uint64_t& src, uint32_t& len)
@@ -237,53 +288,44 @@ __device__ __forceinline__ void read_term(uint4 w, uint64_t& src, uint32_t& len)
     len = uni(w.z);
 }
 
-__device__ __forceinline__ uint32_t word_u16(uint4 w, uint32_t i)
+// dst[p, p+16) of an item: keep(dst, valid) ^ out for bytes < n, dst bytes
+// at and beyond n untouched.  `cur` is dst[p, p+16) as loaded at item start.
+__device__ __forceinline__ void store_item(uint4 out, uint32_t p, uint64_t dst, uint32_t n, uint32_t valid,
+                                           uint4 cur)
 {
-    // 16-bit element i (0..7) of a 16-byte word
-    const uint32_t d = (i >> 1) == 0 ? w.x : (i >> 1) == 1 ? w.y : (i >> 1) == 2 ? w.z : w.w;
-    return (uni(d) >> (16 * (i & 1))) & 0xffff;
+    if (p >= n)
+        return;
+    if (p < valid) {
+        uint4 prior = cur;
+        if (p + 16 > valid)
+            prior = mask16(prior, (int)valid - (int)p);
+        out = xor16(out, prior);
+    }
+    if (p + 16 > n) {
+        const int nb = (int)n - (int)p;
+        const uint4 keep = make_uint4(~byte_mask(nb), ~byte_mask(nb - 4), ~byte_mask(nb - 8),
+                                      ~byte_mask(nb - 12));
+        out = mask16(out, nb);
+        out.x |= cur.x & keep.x;
+        out.y |= cur.y & keep.y;
+        out.z |= cur.z & keep.z;
+        out.w |= cur.w & keep.w;
+    }
+    st16(dst + p, out);
 }
 
-// Finish one linear combination on this lane's 16 bytes: merge the other
-// waves' partial sums (LDS), keep dst's prefix [0,valid) and tail [n, ...),
-// store, then write `litLen` literal bytes at dst+n.  `prior` and `old` were
-// loaded by wave 0 when the item started.
-__device__ __forceinline__ void finish_item(uint4 out, bool solo, uint4 (*part)[64], uint32_t wave,
-                                            uint32_t lane, uint32_t p, uint64_t dst, uint32_t n,
-                                            uint32_t valid, uint4 prior, uint4 old,
-                                            const uint32_t* lit, uint32_t litLen)
+// what store_item needs of dst, loaded while the terms stream in
+__device__ __forceinline__ uint4 load_cur(uint32_t p, uint64_t dst, uint32_t n, uint32_t valid)
 {
-    if (!solo) {
-        if (wave != 0)
-            part[wave - 1][lane] = out;
-        __syncthreads();
-    }
-    if (wave != 0)
-        return;
-    if (p < n) {
-        if (!solo) {
-#pragma unroll
-            for (unsigned w = 0; w + 1 < kExecWaves; ++w)
-                out = xor16(out, part[w][lane]);
-        }
-        if (p < valid) {
-            if (p + 16 > valid)
-                prior = mask16(prior, (int)valid - (int)p);
-            out = xor16(out, prior);
-        }
-        if (p + 16 > n) {
-            // keep dst bytes at and beyond n
-            const int nb = (int)n - (int)p;
-            const uint4 keep = make_uint4(~byte_mask(nb), ~byte_mask(nb - 4), ~byte_mask(nb - 8),
-                                          ~byte_mask(nb - 12));
-            out = mask16(out, nb);
-            out.x |= old.x & keep.x;
-            out.y |= old.y & keep.y;
-            out.z |= old.z & keep.z;
-            out.w |= old.w & keep.w;
-        }
-        st16(dst + p, out);
-    }
+    if (p < n && (p < valid || p + 16 > n))
+        return ld16(dst + p);
+    return make_uint4(0, 0, 0, 0);
+}
+
+// `litLen` (<= 8) literal bytes at dst + n, written by the lanes owning them
+__device__ __forceinline__ void store_literal(uint32_t p, uint64_t dst, uint32_t n, uint32_t litLen,
+                                              const uint32_t* lit)
+{
     if (litLen && n + litLen > p && n < p + 16) {
         uint8_t* d = reinterpret_cast<uint8_t*>(dst);
         for (uint32_t k = (n > p ? n : p); k < n + litLen && k < p + 16; ++k)
@@ -291,113 +333,221 @@ __device__ __forceinline__ void finish_item(uint4 out, bool solo, uint4 (*part)[
     }
 }
 
-constexpr unsigned kRowsTableLds = 256;   // table entries of an OP_ROWS batch kept in LDS
+__device__ __forceinline__ uint32_t pcg_output(uint64_t s)
+{
+    const uint32_t xs = (uint32_t)(((s >> 18) ^ s) >> 27);
+    const uint32_t r = (uint32_t)(s >> 59);
+    return (xs >> r) | (xs << ((32u - r) & 31u));
+}
+
+// Sum or window entry i of the current OP_ROWS batch (per lane)
+__device__ __forceinline__ uint4 table_entry(const uint4* tableL, const uint4* __restrict__ seg,
+                                             uint32_t blockWord, uint32_t i)
+{
+    return i < kRowsTableLds ? tableL[i] : seg[blockWord + i];
+}
 
 __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
                                                        const ExecItem* __restrict__ items)
 {
     __shared__ uint4 ring[2][kRingWords];
-    __shared__ uint4 part[kExecWaves - 1][64];
+    __shared__ uint4 part[kExecWaves - 1][2][64];
     __shared__ uint4 tableL[kRowsTableLds];
+    __shared__ uint32_t cxL[kColumnValuePeriod];   // CX(c) | CX(c)^2 << 8 by c mod 253
     const ExecItem it = items[blockIdx.x];
     const uint4* seg = stream + it.streamBegin;
     const uint32_t words = it.streamWords;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     const uint32_t wave = tid >> 6;
-    const uint32_t p = it.tileBase + lane * 16;
+    const uint32_t tileBase = it.tileBase;
+    const uint32_t p = tileBase + lane * 16;
+    const uint32_t p1 = p + kChunk;
 
     ring[0][tid] = tid < words ? seg[tid] : make_uint4(0, 0, 0, 0);
+    for (uint32_t c = tid; c < kColumnValuePeriod; c += kExecThreads) {
+        const uint32_t cx = 3u + (c * 199u) % kColumnValuePeriod;   // SiameseCommon.h:89-93
+        cxL[c] = cx | ((uint32_t)c_sqr[cx] << 8);
+    }
     __syncthreads();
     uint32_t cur = 0, pos = 0;
-    uint32_t rowsLeft = 0, tableBase = 0;   // state of the current OP_ROWS batch
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
         const uint4* rb = ring[cur];
         const uint4 h0 = rb[0], h1 = rb[1];
         const uint64_t dst = ((uint64_t)uni(h0.y) << 32) | uni(h0.x);
         const uint32_t n = uni(h0.z), valid = uni(h0.w);
-        const uint32_t kind = rowsLeft ? (uint32_t)OP_ROW : uni(h1.x);
+        const uint32_t kind = uni(h1.x);
         uint32_t itemWords = kOpWords;
-        if (kind == OP_LINCOMB)
+        if (kind == OP_LINCOMB || kind == OP_ROWS)
             itemWords += uni(h1.w);
-        else if (kind == OP_ROWS)
-            itemWords += uni(h1.w);   // table words
-        else if (kind == OP_ROW)
-            itemWords = kRowWords + ((uni(h1.x) >> 8) + kPicksPerWord - 1) / kPicksPerWord;
         const uint32_t next = pos + itemWords;
-        // prefetch the next item's block while this one runs
+        // prefetch the next op's block while this one runs
         uint4 pf = make_uint4(0, 0, 0, 0);
         if (oi + 1 < it.opCount && next + tid < words)
             pf = seg[next + tid];
 
         if (kind == OP_LITERAL) {
-            if (wave == 0 && n + valid > p && n < p + 16) {
+            if (wave == 0) {
                 const uint32_t lit[2] = {uni(h1.z), uni(h1.w)};
-                uint8_t* d = reinterpret_cast<uint8_t*>(dst);
-                for (uint32_t k = (n > p ? n : p); k < n + valid && k < p + 16; ++k)
-                    d[k] = (uint8_t)(lit[(k - n) >> 2] >> (8 * ((k - n) & 3)));
+                store_literal(p, dst, n, valid, lit);
+                store_literal(p1, dst, n, valid, lit);
+            }
+        } else if (kind == OP_LINCOMB) {
+            if (tileBase < n) {   // uniform: the op reaches this tile
+                const uint32_t nt = uni(h1.w);
+                const uint32_t mix = uni(h1.y);
+                const bool solo = nt <= kExecSolo;
+                uint4 cur0 = make_uint4(0, 0, 0, 0), cur1 = cur0;
+                if (wave == 0) {
+                    cur0 = load_cur(p, dst, n, valid);
+                    cur1 = load_cur(p1, dst, n, valid);
+                }
+                Acc2 acc0 = zero2(), acc1 = zero2();
+                // wave w takes a contiguous share of the terms
+                const uint32_t a0 = solo ? 0 : nt * wave / kExecWaves;
+                const uint32_t a1 = solo ? (wave == 0 ? nt : 0) : nt * (wave + 1) / kExecWaves;
+                uint4 dv = make_uint4(0, 0, 0, 0);
+                gather2(a0, a1, tileBase, p, acc0, acc1,
+                        [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                            const uint32_t j = (k - a0) & 63u;
+                            if (j == 0) {
+                                const uint32_t idx = k + lane;
+                                dv = idx < a1 ? op_word(rb, seg, pos, kOpWords + idx) : make_uint4(0, 0, 0, 0);
+                            }
+                            lane_term(dv, j, src, len);
+                            ca = rl(dv.w, j);
+                            return true;
+                        });
+                if (mix > 1) {
+                    acc1.a = gf_mul16(acc1.a, mix);
+                    acc1.b = gf_mul16(acc1.b, mix);
+                }
+                uint4 out0 = xor16(acc0.a, acc1.a), out1 = xor16(acc0.b, acc1.b);
+                if (!solo) {
+                    if (wave != 0) {
+                        part[wave - 1][0][lane] = out0;
+                        part[wave - 1][1][lane] = out1;
+                    }
+                    __syncthreads();
+                    if (wave == 0) {
+#pragma unroll
+                        for (unsigned w = 0; w + 1 < kExecWaves; ++w) {
+                            out0 = xor16(out0, part[w][0][lane]);
+                            out1 = xor16(out1, part[w][1][lane]);
+                        }
+                    }
+                }
+                if (wave == 0) {
+                    store_item(out0, p, dst, n, valid, cur0);
+                    store_item(out1, p1, dst, n, valid, cur1);
+                }
             }
         } else if (kind == OP_ROWS) {
-            // batch prologue: stage the first kRowsTableLds table entries
-            // (lane sums first); the rows follow as items
-            rowsLeft = n;
-            tableBase = pos + kOpWords;
-            if (tid < valid && tid < kRowsTableLds)
-                tableL[tid] = op_word(rb, seg, pos, kOpWords + tid);
-        } else if (it.tileBase < n) {   // uniform: the item reaches this tile
-            uint4 prior = make_uint4(0, 0, 0, 0), old = make_uint4(0, 0, 0, 0);
-            if (wave == 0 && p < n) {
-                // what wave 0 merges at the end, fetched while the terms stream in
-                if (p < valid)
-                    prior = ld16(dst + p);
-                if (p + 16 > n)
-                    old = ld16(dst + p);
+            const uint32_t R = n, E = valid, U = uni(h1.y);
+            const uint32_t blk = pos + kOpWords;        // stream word of sum entry 0
+            const uint32_t T = kRowSums + E;
+            for (uint32_t i = tid; i < T && i < kRowsTableLds; i += kExecThreads)
+                tableL[i] = op_word(rb, seg, pos, kOpWords + i);
+            __syncthreads();
+
+            // phase A: lane-sum updates, one wave each
+            const uint32_t updWord = kOpWords + T;
+            for (uint32_t u = wave; u < U; u += kExecWaves) {
+                const uint4 w0 = op_word(rb, seg, pos, updWord + u * kUpdateWords);
+                const uint4 w1 = op_word(rb, seg, pos, updWord + u * kUpdateWords + 1);
+                const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                const uint32_t un = uni(w0.z), vs = uni(w0.w);
+                const uint32_t uvalid = vs & 0x3fffffffu, us = vs >> 30;
+                const uint32_t from = uni(w1.x), to = uni(w1.y);
+                if (tileBase >= un)
+                    continue;
+                const uint4 c0 = load_cur(p, udst, un, uvalid);
+                const uint4 c1 = load_cur(p1, udst, un, uvalid);
+                Acc2 acc0 = zero2(), acc1 = zero2();
+                const uint32_t cnt = to > from ? (to - from + kLanes - 1) / kLanes : 0;
+                uint4 ev = make_uint4(0, 0, 0, 0);
+                uint32_t cv = 1;
+                gather2(0, cnt, tileBase, p, acc0, acc1,
+                        [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                            const uint32_t j = k & 63u;
+                            if (j == 0) {
+                                // lane j: element from + 8 (k + j) and its coefficient
+                                const uint32_t e = from + (k + lane) * kLanes;
+                                ev = e < to ? table_entry(tableL, seg, blk, kRowSums + e)
+                                            : make_uint4(0, 0, 0, 0);
+                                const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
+                                cv = us == 0 ? 1u : (us == 1 ? (cx & 0xff) : (cx >> 8));
+                            }
+                            lane_term(ev, j, src, len);
+                            ca = rl(cv, j);
+                            return len != 0;
+                        });
+                store_item(acc0.a, p, udst, un, uvalid, c0);
+                store_item(acc0.b, p1, udst, un, uvalid, c1);
             }
-            uint4 acc0 = make_uint4(0, 0, 0, 0);
-            uint4 acc1 = make_uint4(0, 0, 0, 0);
-            uint32_t mix, litLen = 0;
-            uint32_t lit[2] = {0, 0};
-            bool solo;
-            if (kind == OP_LINCOMB) {
-                const uint32_t nt = uni(h1.w);
-                mix = uni(h1.y);
-                solo = nt <= kExecSolo;
-                if (!solo || wave == 0)
-                    gather(nt, solo ? 0 : wave, solo ? 1 : kExecWaves, p, acc0, acc1,
-                           [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                               const uint4 w = op_word(rb, seg, pos, kOpWords + k);
-                               read_term(w, src, len);
-                               ca = uni(w.w);
-                               return true;
-                           });
-            } else {
-                // OP_ROW: the row's picks (selected lane sums, then LDPC pairs)
-                const uint32_t npicks = uni(h1.x) >> 8;
-                const uint32_t mixLit = uni(h1.y);
-                const uint4 h2 = rb[2];
-                mix = mixLit & 0xff;
-                litLen = mixLit >> 8;
-                lit[0] = uni(h2.x);
-                lit[1] = uni(h2.y);
-                solo = false;
-                gather(npicks, wave, kExecWaves, p, acc0, acc1,
-                       [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                           const uint32_t pk =
-                               word_u16(op_word(rb, seg, pos, kRowWords + k / kPicksPerWord),
-                                        k % kPicksPerWord);
-                           const uint32_t ti = pk & 0x7fff;
-                           read_term(ti < kRowsTableLds ? tableL[ti] : seg[tableBase + ti], src, len);
-                           ca = 1 | ((pk >> 15) << 8);
-                           return true;
-                       });
+            __syncthreads();
+
+            // phase B: rows, one wave each; lane j < 24 holds sum entry j
+            const uint4 sumv = lane < kRowSums ? tableL[lane] : make_uint4(0, 0, 0, 0);
+            const uint32_t rowWord = updWord + U * kUpdateWords;
+            for (uint32_t r = wave; r < R; r += kExecWaves) {
+                const uint4 w0 = op_word(rb, seg, pos, rowWord + r * kRowWords);
+                const uint4 w1 = op_word(rb, seg, pos, rowWord + r * kRowWords + 1);
+                const uint4 w2 = op_word(rb, seg, pos, rowWord + r * kRowWords + 2);
+                const uint64_t rdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                const uint32_t rn = uni(w0.z), rvalid = uni(w0.w);
+                const uint32_t m0 = uni(w1.x), m1 = uni(w1.y), row = uni(w1.z), N = uni(w1.w);
+                const uint32_t off = uni(w2.x);
+                const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
+                const uint32_t litLen = m0 >> 24, mix = m1 >> 24;
+                if (tileBase < rn) {
+                    const uint4 c0 = load_cur(p, rdst, rn, rvalid);
+                    const uint4 c1 = load_cur(p1, rdst, rn, rvalid);
+                    Acc2 acc0 = zero2(), acc1 = zero2();
+                    // dense part: the sums the opcodes select (bit lane*3+s;
+                    // mask1 feeds the product)
+                    uint64_t bits = (uint64_t)(m0 & 0xffffffu) | ((uint64_t)(m1 & 0xffffffu) << 24);
+                    gather2(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
+                            [&](uint32_t, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                                const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+                                bits &= bits - 1;
+                                const uint32_t k = b < kRowSums ? b : b - kRowSums;
+                                lane_term(sumv, k, src, len);
+                                ca = 1u | ((b >= kRowSums ? 1u : 0u) << 8);
+                                return len != 0;
+                            });
+                    // sparse part: ceil(N/16) pairs of PCG.Seed(row, N) draws
+                    // (SiameseEncoder.cpp:1100-1144): lane j makes draw 64c+j by
+                    // jump-ahead and fetches its window entry
+                    if (N != 0) {
+                        const uint64_t inc = ((uint64_t)row << 1) | 1u;
+                        uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
+                        uint4 ev = make_uint4(0, 0, 0, 0);
+                        gather2(0, 2 * ((N + kPairRate - 1) / kPairRate), tileBase, p, acc0, acc1,
+                                [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                                    const uint32_t j = k & 63u;
+                                    if (j == 0) {
+                                        const uint64_t st = c_pcgA[lane] * sc + inc * c_pcgG[lane];
+                                        const uint32_t e = pcg_output(st) % N;
+                                        ev = table_entry(tableL, seg, blk, kRowSums + off + e);
+                                        sc = c_pcgA[64] * sc + inc * c_pcgG[64];
+                                    }
+                                    lane_term(ev, j, src, len);
+                                    ca = 1u | ((k & 1u) << 8);
+                                    return len != 0;
+                                });
+                    }
+                    if (mix > 1) {
+                        acc1.a = gf_mul16(acc1.a, mix);
+                        acc1.b = gf_mul16(acc1.b, mix);
+                    }
+                    store_item(xor16(acc0.a, acc1.a), p, rdst, rn, rvalid, c0);
+                    store_item(xor16(acc0.b, acc1.b), p1, rdst, rn, rvalid, c1);
+                }
+                store_literal(p, rdst, rn, litLen, lit);
+                store_literal(p1, rdst, rn, litLen, lit);
             }
-            if (mix > 1)
-                acc1 = gf_mul16(acc1, mix);
-            finish_item(xor16(acc0, acc1), solo, part, wave, lane, p, dst, n, valid, prior, old, lit,
-                        litLen);
         }
-        if (kind == OP_ROW)
-            --rowsLeft;
         ring[cur ^ 1][tid] = pf;
         __syncthreads();
         cur ^= 1;
@@ -873,6 +1023,17 @@ bool be_init(int device, const char** err)
     }
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_perm), perm, sizeof(perm)), "hipMemcpyToSymbol(perm)");
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_inv), g_gf.inv, 256), "hipMemcpyToSymbol(inv)");
+    check(hipMemcpyToSymbol(HIP_SYMBOL(c_sqr), g_gf.sqr, 256), "hipMemcpyToSymbol(sqr)");
+    // PCG jump-ahead: state after j draws = A^j s + inc * (A^0 + ... + A^(j-1))
+    uint64_t pa[65], pg[65];
+    pa[0] = 1;
+    pg[0] = 0;
+    for (unsigned j = 1; j <= 64; ++j) {
+        pa[j] = pa[j - 1] * kPcgMul;
+        pg[j] = pg[j - 1] * kPcgMul + 1;
+    }
+    check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgA), pa, sizeof(pa)), "hipMemcpyToSymbol(pcgA)");
+    check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgG), pg, sizeof(pg)), "hipMemcpyToSymbol(pcgG)");
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_main),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)solve_lds_bytes(kSolveLdsMaxRows)) == hipSuccess)

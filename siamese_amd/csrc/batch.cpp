@@ -262,4 +262,9 @@ SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15)
     std::memcpy(out15, v, sizeof(v));
 }
 
+SIAMESE_EXPORT uint64_t sgpu_arena_bytes(void)
+{
+    return Engine::global()->arena_bytes();
+}
+
 } // extern "C"

@@ -1,0 +1,60 @@
+// codedef.cpp -- cached LDPC pick sequences (see codedef.h).
+#include "codedef.h"
+
+#include <memory>
+#include <unordered_map>
+#include <vector>
+
+namespace sgpu {
+
+namespace {
+
+struct LdpcCache
+{
+    // (row, n) -> offsets; bounded so long single-stream runs (C3/C5, many
+    // distinct n) do not grow it without limit
+    std::unordered_map<uint64_t, std::unique_ptr<std::vector<uint32_t>>> map;
+    size_t bytes = 0;
+    std::vector<uint32_t> scratch;
+};
+
+void compute(unsigned row, unsigned n, std::vector<uint32_t>& out)
+{
+    const unsigned pairs = (n + kPairRate - 1) / kPairRate;
+    out.resize(2 * (size_t)pairs);
+    Pcg32 prng;
+    prng.seed(row, n);
+    const FastMod mod(n ? n : 1);
+    for (unsigned i = 0; i < 2 * pairs; ++i)
+        out[i] = mod(prng.next());
+}
+
+} // namespace
+
+const uint32_t* ldpc_offsets(unsigned row, unsigned n, unsigned* count)
+{
+    thread_local LdpcCache cache;
+    const uint64_t key = ((uint64_t)row << 32) | n;
+    auto it = cache.map.find(key);
+    if (it == cache.map.end()) {
+        constexpr size_t kMaxBytes = 64u << 20;
+        const size_t need = 8 * (size_t)((n + kPairRate - 1) / kPairRate);
+        if (need > kMaxBytes / 4) {
+            compute(row, n, cache.scratch);
+            *count = (unsigned)cache.scratch.size();
+            return cache.scratch.data();
+        }
+        if (cache.bytes + need > kMaxBytes) {
+            cache.map.clear();
+            cache.bytes = 0;
+        }
+        std::unique_ptr<std::vector<uint32_t>> v(new std::vector<uint32_t>);
+        compute(row, n, *v);
+        cache.bytes += need + 64;
+        it = cache.map.emplace(key, std::move(v)).first;
+    }
+    *count = (unsigned)it->second->size();
+    return it->second->data();
+}
+
+} // namespace sgpu

@@ -111,6 +111,15 @@ struct FastMod
     }
 };
 
+/// The LDPC pair picks of Siamese row `row` over a window of n columns
+/// (reference SiameseEncoder.cpp:1100-1144, SiameseDecoder.cpp:996-1051 and
+/// :2306-2339): PCG.Seed(row, n), then ceil(n/16) pairs of Next() % n, as
+/// 2*ceil(n/16) offsets in PCG order (even = row term, odd = product term).
+/// The same (row, n) recurs across rows of every stream and on both sides
+/// of the channel, so each host thread caches the sequences it computes.
+/// The pointer stays valid until the calling thread's next ldpc_offsets().
+const uint32_t* ldpc_offsets(unsigned row, unsigned n, unsigned* count);
+
 // ---- Metadata carried in every recovery footer (SiameseCommon.h:364-389) --
 struct RowMeta
 {

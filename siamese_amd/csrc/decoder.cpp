@@ -208,13 +208,30 @@ bool DecoderCore::grow_sum(DevSum& s, unsigned bytes)
     return true;
 }
 
-void DecoderCore::materialize(DevSum& s)
+void DecoderCore::cover(unsigned lo, unsigned hi)
 {
-    if (s.devValid >= s.bytes)
+    uint32_t from = hi;
+    WinEntry* w = prog_.rows_window(lo, hi, &from);
+    for (unsigned e = from; e < hi; ++e, ++w) {
+        const DecSlot& o = slot(e);
+        // lost originals read as absent (their `column` is a matrix column)
+        w->src = o.bytes ? o.buf.addr() : 0;
+        w->len = o.bytes;
+        w->column = o.bytes ? o.column : 0;
+    }
+}
+
+void DecoderCore::materialize(unsigned lane, unsigned s)
+{
+    // zero-fill [devValid, bytes): an update without terms in the row batch
+    DevSum& d = sum(lane, s).d;
+    if (d.devValid >= d.bytes)
         return;
-    prog_.lc_begin(s.buf.addr(), s.bytes, s.devValid);
-    prog_.lc_end();
-    s.devValid = s.bytes;
+    const unsigned at = sum(lane, s).elementEnd;
+    const unsigned lo = std::min(at, windowLo_);
+    cover(lo, lo);   // an open batch whose window starts at or below `at`
+    prog_.rows_update(lane * kSums + s, d.buf.addr(), d.bytes, d.devValid, s, at, at);
+    d.devValid = d.bytes;
 }
 
 static uint8_t sum_coeff(unsigned sumIndex, unsigned column)
@@ -234,32 +251,27 @@ DevSum& DecoderCore::get_sum(unsigned lane, unsigned s, unsigned elementEnd)
 
     unsigned newBytes = S.d.bytes;
     unsigned got = 0;
-    for (unsigned e = element; e < elementEnd; e += kLanes) {
-        const unsigned b = slot(e).bytes;
+    uint64_t opBytes = 0;
+    unsigned end = element;
+    for (; end < elementEnd; end += kLanes) {
+        const unsigned b = slot(end).bytes;
         if (b > 0) {
             newBytes = std::max(newBytes, b);
+            opBytes += b;
             ++got;
         }
     }
     if (got > 0) {
         if (!grow_sum(S.d, newBytes))
             return S.d;
-        prog_.lc_begin(S.d.buf.addr(), S.d.bytes, S.d.devValid);
-        uint64_t opBytes = 0;
-        for (unsigned e = element; e < elementEnd; e += kLanes) {
-            const DecSlot& o = slot(e);
-            if (o.bytes == 0)
-                continue;
-            prog_.lc_term(o.buf.addr(), o.bytes, sum_coeff(s, o.column));
-            opBytes += o.bytes;
-        }
-        prog_.lc_end();
+        // terms (received originals; lost ones are absent in the window)
+        // and their coefficients are generated on the device
+        cover(std::min(element, windowLo_), end - kLanes + 1);
+        prog_.rows_update(lane * kSums + s, S.d.buf.addr(), S.d.bytes, S.d.devValid, s, element, end);
         eng_->account(opBytes);
         S.d.devValid = S.d.bytes;
     }
-    while (element < elementEnd)
-        element += kLanes;
-    S.elementEnd = element;
+    S.elementEnd = end;
     return S.d;
 }
 
@@ -426,6 +438,8 @@ void DecoderCore::remove_elements()
         sumColumnCount_ = 0;
     }
 
+    // window indices shift below: close the open row batch first
+    prog_.rows_seal();
     for (unsigned i = 0; i < keptSub; ++i)
         subwindows_[i]->reset();
     std::rotate(subwindows_.begin(), subwindows_.begin() + keptSub, subwindows_.end());
@@ -989,18 +1003,13 @@ bool DecoderCore::generate_matrix()
         }
 
         // Sparse columns that landed on lost data
-        Pcg32 prng;
-        prng.seed(m.row, m.ldpcCount);
-        const unsigned pairs = (m.ldpcCount + kPairRate - 1) / kPairRate;
+        unsigned picks = 0;
+        const uint32_t* off = ldpc_offsets(m.row, m.ldpcCount, &picks);
         const size_t rowOff = (size_t)i * matStride_;
-        const FastMod mod(m.ldpcCount ? m.ldpcCount : 1);
-        for (unsigned k = 0; k < pairs; ++k) {
-            const DecSlot& a = slot(rec->elementStart + mod(prng.next()));
+        for (unsigned k = 0; k < picks; ++k) {
+            const DecSlot& a = slot(rec->elementStart + off[k]);
             if (a.bytes == 0 && a.column >= startCol && rowOff + a.column < matBytes)
-                mat_[rowOff + a.column] ^= 1;
-            const DecSlot& b = slot(rec->elementStart + mod(prng.next()));
-            if (b.bytes == 0 && b.column >= startCol && rowOff + b.column < matBytes)
-                mat_[rowOff + b.column] ^= rx;
+                mat_[rowOff + a.column] ^= (k & 1) ? rx : 1;
         }
     }
 
@@ -1142,8 +1151,9 @@ bool DecoderCore::eliminate_original_data()
         }
         sumColumnCount_ = m.sumCount;
 
-        // decoder sums first (their ops precede this row); the row selects
-        // them by mask bit lane*3 + sum
+        // decoder sums first (their updates precede the batch's rows); the
+        // row selects them by mask bit lane*3 + sum
+        windowLo_ = std::min(es, sumElementStart);
         uint32_t mask[2] = {0, 0};
         uint64_t opBytes = rb; // RX * product muladd
         for (unsigned lane = 0; lane < kLanes; ++lane) {
@@ -1153,45 +1163,35 @@ bool DecoderCore::eliminate_original_data()
                     continue;
                 DevSum& s = get_sum(lane, bit % kSums, ee);
                 if (s.bytes > 0) {
-                    materialize(s);
+                    materialize(lane, bit % kSums);
                     mask[bit / kSums] |= 1u << (lane * kSums + bit % kSums);
                     opBytes += std::min(s.bytes, rb);
                 }
             }
         }
-        GfTerm sums[kLanes * kSums];
+        WinEntry sums[kRowSums];
         for (unsigned lane = 0; lane < kLanes; ++lane)
             for (unsigned s = 0; s < kSums; ++s) {
                 const DevSum& d = sum(lane, s).d;
-                GfTerm& t = sums[lane * kSums + s];
+                WinEntry& t = sums[lane * kSums + s];
                 t.src = d.buf.addr();
                 t.len = d.bytes;
-                t.coeff = 1;
-                t.acc = 0;
-                t.pad = 0;
+                t.column = 0;
             }
+        // LDPC pairs over received originals, drawn on the device; the host
+        // walks the same draws only to count reference bytes
+        unsigned picks = 0;
+        const uint32_t* off = ldpc_offsets(m.row, m.ldpcCount, &picks);
+        for (unsigned k = 0; k < picks; ++k)
+            opBytes += std::min(slot(es + off[k]).bytes, rb);
         // rows of one decode share the sums: one row of the program's batch
-        prog_.rows_begin(sums, kLanes * kSums, rec->buf.addr(), rb, rb, row_value(m.row), mask[0],
-                         mask[1]);
-        Pcg32 prng;
-        prng.seed(m.row, m.ldpcCount);
-        const unsigned pairs = (m.ldpcCount + kPairRate - 1) / kPairRate;
-        const FastMod mod(m.ldpcCount ? m.ldpcCount : 1);
-        for (unsigned k = 0; k < pairs; ++k) {
-            const DecSlot& a = slot(es + mod(prng.next()));
-            if (a.bytes > 0) {
-                prog_.rows_pick(a.buf.addr(), std::min(a.bytes, rb), 0);
-                opBytes += std::min(a.bytes, rb);
-            }
-            const DecSlot& b = slot(es + mod(prng.next()));
-            if (b.bytes > 0) {
-                prog_.rows_pick(b.buf.addr(), std::min(b.bytes, rb), 1);
-                opBytes += std::min(b.bytes, rb);
-            }
-        }
-        prog_.rows_end();
+        cover(windowLo_, ee);
+        prog_.rows_row(sums, rec->buf.addr(), rb, rb, row_value(m.row), mask[0], mask[1], m.row,
+                       m.ldpcCount, es);
         eng_->account(opBytes);
     }
+    // the window snapshot must not see this decode's recoveries
+    prog_.rows_seal();
     return !disabled_;
 }
 

@@ -131,7 +131,9 @@ private:
     };
     Sum& sum(unsigned lane, unsigned s) { return lanes_[lane][s]; }
     bool grow_sum(DevSum& s, unsigned bytes);
-    void materialize(DevSum& s);
+    void materialize(unsigned lane, unsigned s);
+    void cover(unsigned lo, unsigned hi);   // row batch window covers [lo, hi)
+    unsigned windowLo_ = 0;                 // lowest element the current row references
     DevSum& get_sum(unsigned lane, unsigned s, unsigned elementEnd);
     bool start_sums(unsigned elementStart, unsigned bufferBytes);
     void reset_sums(unsigned elementStart);

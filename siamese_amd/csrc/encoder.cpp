@@ -154,6 +154,8 @@ void EncoderCore::remove_elements()
         sumStart_ = sumStart_ > removed ? sumStart_ - removed : 0;
     }
 
+    // window indices shift below: close the open row batch first
+    prog_.rows_seal();
     // Removed subwindows rotate to the back for reuse
     std::rotate(subwindows_.begin(), subwindows_.begin() + keptSub, subwindows_.end());
 
@@ -198,10 +200,23 @@ bool EncoderCore::grow_sum(DevSum& s, unsigned bytes)
     return true;
 }
 
+void EncoderCore::cover(unsigned lo, unsigned hi)
+{
+    uint32_t from = hi;
+    WinEntry* w = prog_.rows_window(lo, hi, &from);
+    for (unsigned e = from; e < hi; ++e, ++w) {
+        const EncSlot& o = slot(e);
+        w->src = o.buf.addr();
+        w->len = o.bytes;
+        w->column = o.column;
+    }
+}
+
 DevSum& EncoderCore::get_sum(unsigned lane, unsigned sumIndex, unsigned elementEnd)
 {
     // :359-418 -- lazily fold this lane's new originals into the running sum.
-    // Sum0 += X, Sum1 += CX*X, Sum2 += CX^2*X.
+    // Sum0 += X, Sum1 += CX*X, Sum2 += CX^2*X.  The terms and coefficients
+    // are generated on the device from the row batch's window snapshot.
     Lane& L = lanes_[lane];
     DevSum& sum = L.sum[sumIndex];
     unsigned element = L.next[sumIndex];
@@ -211,28 +226,21 @@ DevSum& EncoderCore::get_sum(unsigned lane, unsigned sumIndex, unsigned elementE
     unsigned newBytes = sum.bytes;
     if (L.longest > 0)
         newBytes = std::max(newBytes, L.longest);
-    for (unsigned e = element; e < elementEnd; e += kLanes)
-        newBytes = std::max(newBytes, slot(e).bytes);
+    uint64_t opBytes = 0; // one add/muladd per original in the reference
+    unsigned end = element;
+    for (; end < elementEnd; end += kLanes) {
+        const unsigned b = slot(end).bytes;
+        newBytes = std::max(newBytes, b);
+        opBytes += b;
+    }
     if (!grow_sum(sum, newBytes))
         return sum;
-    prog_.lc_begin(sum.buf.addr(), sum.bytes, sum.devValid);
-    uint64_t opBytes = 0;
-    do {
-        const EncSlot& o = slot(element);
-        uint8_t c = 1;
-        if (sumIndex > 0) {
-            c = column_value(o.column);
-            if (sumIndex == 2)
-                c = gf_sqr(c);
-        }
-        prog_.lc_term(o.buf.addr(), o.bytes, c);
-        opBytes += o.bytes; // one add/muladd per original in the reference
-        element += kLanes;
-    } while (element < elementEnd);
-    prog_.lc_end();
+    cover(std::min(element, std::min(sumStart_, firstUnremoved_)), end - kLanes + 1);
+    prog_.rows_update(lane * kSums + sumIndex, sum.buf.addr(), sum.bytes, sum.devValid, sumIndex,
+                      element, end);
     eng_->account(opBytes);
     sum.devValid = sum.bytes;
-    L.next[sumIndex] = element;
+    L.next[sumIndex] = end;
     return sum;
 }
 
@@ -411,16 +419,14 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
         }
     }
     sumEnd_ = count_;
-    GfTerm sums[kLanes * kSums];
+    WinEntry sums[kRowSums];
     for (unsigned lane = 0; lane < kLanes; ++lane)
         for (unsigned s = 0; s < kSums; ++s) {
             const DevSum& d = lanes_[lane].sum[s];
-            GfTerm& t = sums[lane * kSums + s];
+            WinEntry& t = sums[lane * kSums + s];
             t.src = d.buf.addr();
             t.len = d.bytes;
-            t.coeff = 1;
-            t.acc = 0;
-            t.pad = 0;
+            t.column = 0;
         }
 
     RowMeta m;
@@ -431,26 +437,20 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     uint8_t footer[kMaxFooterBytes];
     const unsigned footerBytes = write_footer(m, footer);
 
-    // Recovery = row sums ^ RX * product (:1232-1233) and its footer: one row
-    // of the program's Siamese row batch (consecutive rows share the sums)
-    prog_.rows_begin(sums, kLanes * kSums, recovery_.addr(), recoveryBytes, 0, row_value(row),
-                     mask[0], mask[1], footer, footerBytes);
-
-    // Sparse part (:1100-1144): ceil(n/16) PCG-chosen pairs
+    // Sparse part (:1100-1144): ceil(n/16) PCG-chosen pairs, drawn on the
+    // device; the host walks the same draws only to count reference bytes.
     const unsigned start = firstUnremoved_;
     const unsigned n = sumEnd_ - start;
-    Pcg32 prng;
-    prng.seed(row, n);
-    const unsigned pairs = (n + kPairRate - 1) / kPairRate;
-    const FastMod mod(n ? n : 1);
-    for (unsigned i = 0; i < pairs; ++i) {
-        const EncSlot& a = slot(start + mod(prng.next()));
-        const EncSlot& b = slot(start + mod(prng.next()));
-        prog_.rows_pick(a.buf.addr(), a.bytes, 0);
-        prog_.rows_pick(b.buf.addr(), b.bytes, 1);
-        opBytes += a.bytes + b.bytes;
-    }
-    prog_.rows_end();
+    unsigned picks = 0;
+    const uint32_t* off = ldpc_offsets(row, n, &picks);
+    for (unsigned i = 0; i < picks; ++i)
+        opBytes += slot(start + off[i]).bytes;
+
+    // Recovery = row sums ^ RX * product (:1232-1233) and its footer: one row
+    // of the program's Siamese row batch (consecutive rows share the sums)
+    cover(std::min(start, sumStart_), sumEnd_);
+    prog_.rows_row(sums, recovery_.addr(), recoveryBytes, 0, row_value(row), mask[0], mask[1], row,
+                   n, start, footer, footerBytes);
     eng_->account(opBytes);
 
     finish_row(out, m, recoveryBytes, true);

@@ -94,6 +94,7 @@ private:
     void remove_elements();
     /// Lazily accumulate lane sums up to elementEnd; returns the sum.
     DevSum& get_sum(unsigned lane, unsigned sumIndex, unsigned elementEnd);
+    void cover(unsigned lo, unsigned hi);   // row batch window covers [lo, hi)
     bool grow_sum(DevSum& s, unsigned bytes);
 
     SiameseResult single_row(EncodeOut& out);

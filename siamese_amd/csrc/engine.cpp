@@ -87,7 +87,6 @@ void Program::new_segment()
     s.terms.clear();
     s.rowsData.clear();
     s.rowsWords = 0;
-    s.rowsItems = 0;
     s.maxExtent = 0;
 }
 
@@ -98,7 +97,6 @@ void Program::reset_after_flush()
         segs_[k].terms.clear();
         segs_[k].rowsData.clear();
         segs_[k].rowsWords = 0;
-        segs_[k].rowsItems = 0;
         segs_[k].maxExtent = 0;
     }
     nsegs_ = 0;
@@ -241,130 +239,111 @@ void Program::on_complete(Completion fn)
 
 // ---- Siamese row batches ---------------------------------------------------
 
-void Program::rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, uint32_t n,
-                         uint32_t valid, uint8_t mix, uint32_t mask0, uint32_t mask1,
-                         const uint8_t* lit, uint32_t litLen)
+void Program::rows_open(uint32_t base, bool keepWindow)
 {
-    touch();
     RowsBuild& b = rb_;
-    bool join = b.open && b.sumCount == sumCount && b.table.size() < kMaxRowsTable / 2;
-    for (unsigned k = 0; join && k < sumCount; ++k)
-        join = b.sums[k].src == sums[k].src && b.sums[k].len == sums[k].len;
-    if (!join) {
-        rows_close();
-        if (nsegs_ == 0)
-            new_segment();
-        b.open = true;
-        b.sumCount = sumCount;
-        std::memcpy(b.sums, sums, sumCount * sizeof(GfTerm));
-        b.rows = 0;
-        // the sums are the first table entries; LDPC sources follow
-        b.table.assign(sums, sums + sumCount);
-        b.rowBytes.clear();
-        if (b.rowBytes.capacity() == 0)
-            b.rowBytes.reserve(16384);
-        b.maxExtent = 0;
-        // a new generation empties the source map without touching it
-        if (b.slotGen.empty() || ++b.gen == 0) {
-            b.slotGen.assign(b.slotGen.empty() ? 1024 : b.slotGen.size(), 0);
-            b.slotIdx.resize(b.slotGen.size());
-            b.gen = 1;
-        }
+    rows_close();
+    touch();
+    if (nsegs_ == 0)
+        new_segment();
+    b.open = true;
+    b.haveSums = false;
+    b.readMask = 0;
+    if (!keepWindow) {
+        b.base = base;
+        b.win.clear();
     }
-    RowHeader h;
-    std::memset(&h, 0, sizeof(h));
-    h.dst = dst;
-    h.n = n;
-    h.valid = valid < n ? valid : n;
-    h.kindPicks = OP_ROW;
-    h.mix = mix | (litLen << 8);
+    b.updates.clear();
+    for (int& u : b.updateOf)
+        u = -1;
+    b.rows.clear();
+    b.maxExtent = 0;
+}
+
+WinEntry* Program::rows_window(uint32_t lo, uint32_t hi, uint32_t* from)
+{
+    RowsBuild& b = rb_;
+    if (!b.open || lo < b.base)
+        rows_open(lo, false);
+    const uint32_t end = b.base + (uint32_t)b.win.size();
+    if (hi <= end) {
+        *from = hi;
+        return nullptr;
+    }
+    *from = end;
+    b.win.resize(hi - b.base);
+    return b.win.data() + (end - b.base);
+}
+
+void Program::rows_update(unsigned k, uint64_t dst, uint32_t n, uint32_t valid, unsigned s,
+                          uint32_t fromElement, uint32_t toElement)
+{
+    RowsBuild& b = rb_;
+    // a row of this batch already read sum k: the update belongs to a new
+    // batch over the same window (its rows run after this batch's rows)
+    if (b.readMask >> k & 1)
+        rows_open(b.base, true);
+    const uint32_t from = fromElement - b.base, to = toElement - b.base;
+    int& ui = b.updateOf[k];
+    if (ui >= 0) {
+        SumUpdate& u = b.updates[ui];
+        const uint64_t d = ((uint64_t)u.dstHi << 32) | u.dstLo;
+        if (d == dst && (u.to == from || from == to)) {
+            // continue the same sum: one update over the joined element range
+            if (from != to)
+                u.to = to;
+            if (n > u.n)
+                u.n = n;
+            if (n > b.maxExtent)
+                b.maxExtent = n;
+            return;
+        }
+        // a different buffer (the sum grew) or a gap: a fresh batch keeps
+        // the two updates in order
+        rows_open(b.base, true);
+    }
+    SumUpdate u;
+    std::memset(&u, 0, sizeof(u));
+    u.dstLo = (uint32_t)dst;
+    u.dstHi = (uint32_t)(dst >> 32);
+    u.n = n;
+    u.valid = valid < n ? valid : n;
+    u.s = s;
+    u.from = from;
+    u.to = to < from ? from : to;
+    b.updateOf[k] = (int)b.updates.size();
+    b.updates.push_back(u);
+    if (n > b.maxExtent)
+        b.maxExtent = n;
+}
+
+void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix,
+                       uint32_t mask0, uint32_t mask1, unsigned row, uint32_t ldpcN,
+                       uint32_t ldpcFirst, const uint8_t* lit, uint32_t litLen)
+{
+    RowsBuild& b = rb_;
+    if (b.haveSums && std::memcmp(b.sums, sums, sizeof(b.sums)) != 0)
+        rows_open(b.base, true);
+    if (!b.haveSums) {
+        std::memcpy(b.sums, sums, sizeof(b.sums));
+        b.haveSums = true;
+    }
+    RowItem r;
+    std::memset(&r, 0, sizeof(r));
+    r.dst = dst;
+    r.n = n;
+    r.valid = valid < n ? valid : n;
+    r.mask0 = mask0 | (litLen << 24);
+    r.mask1 = mask1 | ((uint32_t)mix << 24);
+    r.row = row;
+    r.ldpcN = ldpcN;
+    r.ldpcOff = ldpcFirst - b.base;
     if (litLen)
-        std::memcpy(h.lit, lit, litLen);
-    b.curRow = b.rowBytes.size();
-    b.curPicks = 0;
-    b.rowBytes.resize(b.curRow + sizeof(RowHeader));
-    std::memcpy(b.rowBytes.data() + b.curRow, &h, sizeof(h));
-    ++b.rows;
+        std::memcpy(r.lit, lit, litLen);
+    b.rows.push_back(r);
+    b.readMask |= mask0 | mask1;
     if (n + litLen > b.maxExtent)
         b.maxExtent = n + litLen;
-    // dense part: the masked sums become picks of table entries 0..S-1, so a
-    // row is one list of (table index, accumulator) picks on the device
-    for (unsigned k = 0; k < sumCount; ++k) {
-        if (mask0 >> k & 1)
-            add_pick((uint16_t)k);
-        if (mask1 >> k & 1)
-            add_pick((uint16_t)(k | 0x8000u));
-    }
-}
-
-void Program::add_pick(uint16_t pick)
-{
-    RowsBuild& b = rb_;
-    if (b.curPicks % kPicksPerWord == 0) {
-        static const uint8_t zero[16] = {};
-        b.rowBytes.insert(b.rowBytes.end(), zero, zero + 16);
-    }
-    const size_t at = b.rowBytes.size() - 16 + (b.curPicks % kPicksPerWord) * 2;
-    std::memcpy(b.rowBytes.data() + at, &pick, 2);
-    ++b.curPicks;
-}
-
-uint16_t Program::rows_table_index(uint64_t src, uint32_t len)
-{
-    // Open-addressing map src -> table index.  A slot is live iff its
-    // generation is the batch's; the key is the table entry it points to.
-    RowsBuild& b = rb_;
-    auto slot_of = [](uint64_t key) { return (size_t)((key >> 6) * 0x9E3779B97F4A7C15ULL >> 20); };
-    if ((b.table.size() - b.sumCount) * 2 >= b.slotGen.size()) {
-        // grow (load factor <= 1/2) and re-insert this batch's sources
-        b.slotGen.assign(b.slotGen.size() * 2, 0);
-        b.slotIdx.assign(b.slotGen.size(), 0);
-        b.gen = 1;
-        const size_t mask = b.slotGen.size() - 1;
-        for (size_t i = b.sumCount; i < b.table.size(); ++i) {
-            size_t h = slot_of(b.table[i].src);
-            while (b.slotGen[h & mask] == b.gen)
-                ++h;
-            b.slotGen[h & mask] = b.gen;
-            b.slotIdx[h & mask] = (uint16_t)i;
-        }
-    }
-    const size_t mask = b.slotGen.size() - 1;
-    size_t h = slot_of(src);
-    for (;; ++h) {
-        if (b.slotGen[h & mask] != b.gen)
-            break;
-        const uint16_t i = b.slotIdx[h & mask];
-        if (b.table[i].src == src)
-            return i;
-    }
-    const uint16_t idx = (uint16_t)b.table.size();
-    b.slotGen[h & mask] = b.gen;
-    b.slotIdx[h & mask] = idx;
-    GfTerm t;
-    t.src = src;
-    t.len = len;
-    t.coeff = 1;
-    t.acc = 0;
-    t.pad = 0;
-    b.table.push_back(t);
-    return idx;
-}
-
-void Program::rows_pick(uint64_t src, uint32_t len, uint32_t acc)
-{
-    if (len == 0)
-        return;
-    add_pick((uint16_t)(rows_table_index(src, len) | (acc ? 0x8000u : 0u)));
-}
-
-void Program::rows_end()
-{
-    RowsBuild& b = rb_;
-    uint32_t kp;
-    std::memcpy(&kp, b.rowBytes.data() + b.curRow + offsetof(RowHeader, kindPicks), 4);
-    kp |= b.curPicks << 8;
-    std::memcpy(b.rowBytes.data() + b.curRow + offsetof(RowHeader, kindPicks), &kp, 4);
 }
 
 void Program::rows_close()
@@ -373,26 +352,35 @@ void Program::rows_close()
     if (!b.open)
         return;
     b.open = false;
+    if (b.rows.empty() && b.updates.empty())
+        return;
+    if (!b.haveSums)
+        std::memset(b.sums, 0, sizeof(b.sums));
     Segment& s = segs_[nsegs_ - 1];
-    const uint32_t T = (uint32_t)b.table.size();   // sums + LDPC sources
-    const uint32_t rowWords = (uint32_t)(b.rowBytes.size() / 16);
+    const uint32_t E = (uint32_t)b.win.size();
+    const uint32_t U = (uint32_t)b.updates.size();
+    const uint32_t R = (uint32_t)b.rows.size();
+    const uint32_t words = kRowSums + E + U * kUpdateWords + R * kRowWords;
     GfOp op;
     std::memset(&op, 0, sizeof(op));
     op.kind = OP_ROWS;
-    op.n = b.rows;
-    op.valid = T;
-    op.mix = b.sumCount;
+    op.n = R;
+    op.valid = E;
+    op.mix = U;
     op.termBegin = (uint32_t)(s.rowsData.size() / 16);   // block offset in words
-    op.termCount = T;
-    op.dst = T + rowWords;                                // block words (host only)
+    op.termCount = words;
     s.ops.push_back(op);
     const size_t at = s.rowsData.size();
-    s.rowsData.resize(at + (size_t)(T + rowWords) * 16);
+    s.rowsData.resize(at + (size_t)words * 16);
     uint8_t* w = s.rowsData.data() + at;
-    std::memcpy(w, b.table.data(), T * sizeof(GfTerm));
-    std::memcpy(w + T * 16, b.rowBytes.data(), b.rowBytes.size());
-    s.rowsWords += T + rowWords;
-    s.rowsItems += b.rows;
+    std::memcpy(w, b.sums, sizeof(b.sums));
+    w += sizeof(b.sums);
+    std::memcpy(w, b.win.data(), (size_t)E * sizeof(WinEntry));
+    w += (size_t)E * sizeof(WinEntry);
+    std::memcpy(w, b.updates.data(), (size_t)U * sizeof(SumUpdate));
+    w += (size_t)U * sizeof(SumUpdate);
+    std::memcpy(w, b.rows.data(), (size_t)R * sizeof(RowItem));
+    s.rowsWords += words;
     if (b.maxExtent > s.maxExtent)
         s.maxExtent = b.maxExtent;
 }
@@ -489,22 +477,86 @@ size_t cap_class(uint32_t cap)
 
 } // namespace
 
-uint8_t* Engine::carve(uint32_t cap)
+namespace {
+constexpr size_t kChunkBytes = 64u << 20;    // one hipMalloc
+constexpr size_t kRegionBytes = 4u << 20;    // a shard's bump region
+constexpr size_t kMagazine = 64;             // buffers moved per depot transfer
+constexpr size_t kRefillBytes = 1u << 20;    // bytes carved per refill
+} // namespace
+
+uint8_t* Engine::carve_region(size_t bytes)
 {
-    const size_t kChunk = 64u << 20;
     std::lock_guard<std::mutex> g(arenaMu_);
-    if (cap > kChunk / 4)
-        return (uint8_t*)be_dev_alloc(cap);
-    if (chunks_.empty() || chunks_.back().used + cap > chunks_.back().size) {
-        uint8_t* base = (uint8_t*)be_dev_alloc(kChunk);
+    if (bytes > kChunkBytes / 4) {
+        arenaBytes_ += bytes;
+        return (uint8_t*)be_dev_alloc(bytes);
+    }
+    if (chunks_.empty() || chunks_.back().used + bytes > chunks_.back().size) {
+        uint8_t* base = (uint8_t*)be_dev_alloc(kChunkBytes);
         if (!base)
             return nullptr;
-        chunks_.push_back(Chunk{base, kChunk, 0});
+        arenaBytes_ += kChunkBytes;
+        chunks_.push_back(Chunk{base, kChunkBytes, 0});
     }
     Chunk& c = chunks_.back();
     uint8_t* p = c.base + c.used;
-    c.used += cap;
+    c.used += bytes;
     return p;
+}
+
+// Refill shard s's empty list of class `cls`: a magazine from the depot if
+// one is there, otherwise fresh buffers cut from the shard's bump region.
+bool Engine::refill(Shard& s, size_t cls, uint32_t cap)
+{
+    std::vector<uint8_t*>& list = s.freeLists[cls];
+    {
+        std::lock_guard<std::mutex> g(depotMu_);
+        if (cls < depot_.size() && depot_[cls].size() >= kMagazine) {
+            std::vector<uint8_t*>& d = depot_[cls];
+            list.insert(list.end(), d.end() - kMagazine, d.end());
+            d.resize(d.size() - kMagazine);
+            return true;
+        }
+    }
+    if (cap > kRegionBytes / 4) {
+        uint8_t* p = carve_region(cap);
+        if (!p)
+            return false;
+        list.push_back(p);
+        return true;
+    }
+    const size_t want = std::max<size_t>(1, std::min<size_t>(kMagazine, kRefillBytes / cap));
+    for (size_t k = 0; k < want; ++k) {
+        if (s.bumpLeft < cap) {
+            if (k > 0)
+                break;
+            uint8_t* r = carve_region(kRegionBytes);
+            if (!r)
+                return false;
+            s.bump = r;           // the rest of the old region is abandoned (< cap)
+            s.bumpLeft = kRegionBytes;
+        }
+        list.push_back(s.bump);
+        s.bump += cap;
+        s.bumpLeft -= cap;
+    }
+    return true;
+}
+
+// Return surplus free buffers of shard s to the depot in magazines.
+void Engine::spill(Shard& s)
+{
+    for (size_t cls = 0; cls < s.freeLists.size(); ++cls) {
+        std::vector<uint8_t*>& list = s.freeLists[cls];
+        if (list.size() <= 2 * kMagazine)
+            continue;
+        const size_t keep = kMagazine;
+        std::lock_guard<std::mutex> g(depotMu_);
+        if (cls >= depot_.size())
+            depot_.resize(cls + 1);
+        depot_[cls].insert(depot_[cls].end(), list.begin() + keep, list.end());
+        list.resize(keep);
+    }
 }
 
 DevBuf Engine::alloc(uint32_t bytes)
@@ -513,14 +565,12 @@ DevBuf Engine::alloc(uint32_t bytes)
     const uint32_t cap = round_cap(bytes);
     Shard& s = shard();
     const size_t cls = cap_class(cap);
-    if (cls < s.freeLists.size() && !s.freeLists[cls].empty()) {
-        b.ptr = s.freeLists[cls].back();
-        s.freeLists[cls].pop_back();
-    } else {
-        b.ptr = carve(cap);
-        if (!b.ptr)
-            return DevBuf();
-    }
+    if (cls >= s.freeLists.size())
+        s.freeLists.resize(cls + 1);
+    if (s.freeLists[cls].empty() && !refill(s, cls, cap))
+        return DevBuf();
+    b.ptr = s.freeLists[cls].back();
+    s.freeLists[cls].pop_back();
     b.cap = cap;
     s.inUse += cap;
     return b;
@@ -705,7 +755,7 @@ void Engine::flush()
                 nOps += s.ops.size();
                 nTerms += s.terms.size();
                 nWords += words;
-                nItems += (s.maxExtent + kTileBytes - 1) / kTileBytes;
+                nItems += (s.maxExtent + kExecTileBytes - 1) / kExecTileBytes;
             }
             ex.itemCount = nItems - ex.itemBegin;
             if (ex.itemCount)
@@ -788,11 +838,9 @@ void Engine::flush()
             uint8_t* w = up + oStream + (size_t)r.wordBase * 16;
             for (const GfOp& op : s.ops) {
                 if (op.kind == OP_ROWS) {
-                    GfOp h = op;
-                    h.dst = 0;
-                    std::memcpy(w, &h, sizeof(GfOp));
+                    std::memcpy(w, &op, sizeof(GfOp));
                     w += sizeof(GfOp);
-                    const size_t bytes = (size_t)op.dst * 16;   // block words (rows_close)
+                    const size_t bytes = (size_t)op.termCount * 16;   // block (rows_close)
                     std::memcpy(w, s.rowsData.data() + (size_t)op.termBegin * 16, bytes);
                     w += bytes;
                     continue;
@@ -806,9 +854,9 @@ void Engine::flush()
                 }
             }
             ExecItem* items = (ExecItem*)(up + oItems) + r.itemBase;
-            const uint32_t nItems = (uint32_t)s.ops.size() + s.rowsItems;
+            const uint32_t nItems = (uint32_t)s.ops.size();
             uint32_t n = 0;
-            for (uint32_t tb = 0; tb < s.maxExtent; tb += kTileBytes)
+            for (uint32_t tb = 0; tb < s.maxExtent; tb += kExecTileBytes)
                 items[n++] = ExecItem{r.wordBase, r.words, nItems, tb};
         } else {
             const ShardRef& sr = srefs[t.a];
@@ -1011,6 +1059,7 @@ bool Engine::sync()
             s->freeLists[cls].push_back(b.ptr);
         }
         s->flightFree.clear();
+        spill(*s);
     });
     const uint64_t t3 = now_ns();
     flushStats_.waitNs += t1 - t0;

@@ -98,16 +98,23 @@ public:
     /// Run `fn(results)` once the next flush has completed.
     void on_complete(Completion fn);
 
-    /// Siamese row batches (OP_ROWS, ops.h).  rows_begin() starts a row: it
-    /// joins the program's last op if that is an open batch over the same
-    /// `sums`, otherwise a new batch opens.  The row's LDPC picks follow
-    /// (rows_pick, in reference order), then rows_end().  Any other op
-    /// closes the batch.
-    void rows_begin(const GfTerm* sums, unsigned sumCount, uint64_t dst, uint32_t n,
-                    uint32_t valid, uint8_t mix, uint32_t mask0, uint32_t mask1,
-                    const uint8_t* lit = nullptr, uint32_t litLen = 0);
-    void rows_pick(uint64_t src, uint32_t len, uint32_t acc);
-    void rows_end();
+    /// Siamese row batches (OP_ROWS, ops.h).  A batch holds a snapshot of
+    /// the codec's window (elements [base, end)), lane-sum updates and rows.
+    /// Any other op closes the open batch.  Protocol for the owner:
+    ///   rows_window(lo, hi) -> entries to fill for elements it returns in
+    ///   [*from, hi) (a batch is opened at `lo` if none covers it);
+    ///   rows_update(...)    -> a lane-sum update over window elements;
+    ///   rows_row(...)       -> a row reading the 24 sums and the window.
+    /// Elements are the owner's window indices; the window of an open batch
+    /// must not change underneath it (owners seal before shifting indices).
+    WinEntry* rows_window(uint32_t lo, uint32_t hi, uint32_t* from);
+    void rows_update(unsigned sumIndex, uint64_t dst, uint32_t n, uint32_t valid, unsigned s,
+                     uint32_t fromElement, uint32_t toElement);
+    void rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix,
+                  uint32_t mask0, uint32_t mask1, unsigned row, uint32_t ldpcN,
+                  uint32_t ldpcFirst, const uint8_t* lit = nullptr, uint32_t litLen = 0);
+    /// Close the open batch (its window may change after this).
+    void rows_seal() { rows_close(); }
 
     bool empty() const { return nsegs_ == 0 || (nsegs_ == 1 && segs_[0].ops.empty()); }
 
@@ -117,30 +124,26 @@ private:
     {
         std::vector<GfOp> ops;
         std::vector<GfTerm> terms;
-        std::vector<uint8_t> rowsData;   // closed OP_ROWS blocks (sums, table, rows)
+        std::vector<uint8_t> rowsData;   // closed OP_ROWS blocks (ops.h layout)
         uint32_t rowsWords = 0;          // stream words of those blocks (after headers)
-        uint32_t rowsItems = 0;          // row items they contain
         uint32_t maxExtent = 0;
     };
     /// The OP_ROWS batch under construction (always the segment's last op).
     struct RowsBuild
     {
         bool open = false;
-        GfTerm sums[24];
-        unsigned sumCount = 0;
-        unsigned rows = 0;
-        std::vector<GfTerm> table;
-        std::vector<uint32_t> slotGen;   // open-addressing map src -> table index:
-        std::vector<uint16_t> slotIdx;   // a slot is live iff slotGen == gen
-        uint32_t gen = 0;
-        std::vector<uint8_t> rowBytes;   // serialized row items
-        size_t curRow = 0;               // offset of the current row's header
-        unsigned curPicks = 0;
+        bool haveSums = false;
+        WinEntry sums[kRowSums];
+        uint32_t readMask = 0;          // sums read by the batch's rows
+        uint32_t base = 0;              // window element of entry 0
+        std::vector<WinEntry> win;
+        std::vector<SumUpdate> updates;
+        int updateOf[kRowSums];         // index into updates, or -1
+        std::vector<RowItem> rows;
         uint32_t maxExtent = 0;
     };
     void rows_close();
-    uint16_t rows_table_index(uint64_t src, uint32_t len);
-    void add_pick(uint16_t pick);
+    void rows_open(uint32_t base, bool keepWindow);
     struct PendingSolve
     {
         SolveDesc desc;
@@ -199,6 +202,7 @@ public:
     DevBuf alloc(uint32_t bytes);
     void release(DevBuf& b);               // recycled after the next flush completes
     uint64_t bytes_in_use() const;
+    uint64_t arena_bytes() const { return arenaBytes_.load(std::memory_order_relaxed); }
 
     /// Copy `bytes` of device memory to host memory once the next flush has
     /// executed; the data is in place after sync().
@@ -234,13 +238,20 @@ private:
     void stage_host_ingest(const DevBuf& dst, const void* data, uint32_t bytes, const uint8_t* hdr,
                            uint32_t hdrLen);
     void add_ingest(const IngestDesc& d, int64_t hostStageOffset);
-    uint8_t* carve(uint32_t cap);
+    uint8_t* carve_region(size_t bytes);
+    bool refill(Shard& s, size_t cls, uint32_t cap);
+    void spill(Shard& s);
     WorkerPool& pool();
 
     bool ready_ = false;
     std::mutex mu_;
 
-    // ---- arena (chunks are carved under arenaMu_; free lists are per shard)
+    // ---- arena: 64 MiB hipMalloc chunks are cut into 4 MiB regions under
+    // arenaMu_; a shard bump-allocates buffers from its own region.  Free
+    // buffers live in per-shard lists by capacity class and move between
+    // shards in magazines of kMagazine through the depot (depotMu_), so a
+    // buffer released on one host thread is reused on another without a
+    // lock per buffer and the arena stops growing once warm.
     struct Chunk
     {
         uint8_t* base;
@@ -248,6 +259,9 @@ private:
     };
     std::mutex arenaMu_;
     std::vector<Chunk> chunks_;
+    std::atomic<uint64_t> arenaBytes_{0};
+    std::mutex depotMu_;
+    std::vector<std::vector<uint8_t*>> depot_;   // [class] -> free buffers
 
     // ---- shards (one per host thread that touched the engine)
     mutable std::mutex shardsMu_;
@@ -314,6 +328,8 @@ struct Shard
     std::vector<DevBuf> pendingFree;   // released since the last flush
     std::vector<DevBuf> flightFree;    // released before the flush in flight
     std::vector<std::vector<uint8_t*>> freeLists;   // by capacity class
+    uint8_t* bump = nullptr;                         // this shard's arena region
+    size_t bumpLeft = 0;
     int64_t inUse = 0;
     EngineStats stats;
 };

@@ -31,8 +31,7 @@ enum GfOpKind : uint32_t
 {
     OP_LINCOMB = 1,   // dst[0,n) = keep(dst,valid) ^ acc0 ^ mix*acc1
     OP_LITERAL = 2,   // dst[n, n+valid) = literal bytes (<= 8)
-    OP_ROWS = 3,      // a batch of Siamese rows sharing one set of lane sums
-    OP_ROW = 4,       // one row of the enclosing OP_ROWS batch (stream item)
+    OP_ROWS = 3,      // a batch of Siamese rows of one codec (sum updates, rows)
 };
 
 /// One op.  For OP_LINCOMB:
@@ -64,39 +63,74 @@ static_assert(sizeof(GfTerm) == 16, "GfTerm layout");
 /// front to back, so one coalesced prefetch brings an op and its term list.
 constexpr unsigned kOpWords = sizeof(GfOp) / 16;
 
-/// OP_ROWS (Siamese rows, reference SiameseEncoder.cpp:1046-1144 and the
-/// decoder's elimination SiameseDecoder.cpp:937-1038).  Stream layout:
-///   GfOp header   kind=OP_ROWS, n = rows K, valid = table entries T,
-///                 mix = lane-sum entries S, termCount = T
-///   T words       the source table as GfTerm {src, len}: the S lane sums
-///                 of the batch first, then every distinct symbol an LDPC
-///                 pair of some row picked
-///   K row items, each RowHeader (3 words) + pick words:
-///     dst[0,n) = keep(dst,valid) ^ acc0 ^ mix * acc1 over the row's picks
-///     (uint16 table index | acc << 15, eight per word: the sums its opcode
-///     selects, then its LDPC pairs), then `litLen` literal bytes (the
-///     recovery footer) at dst+n.
-/// All rows of a batch share one table, so the host sends 2 bytes per
-/// source instead of a 16-byte term, and the sums stay hot on the device.
-struct RowHeader
+/// OP_ROWS: a batch of Siamese rows of one codec (reference
+/// SiameseEncoder.cpp:1046-1144 and :359-418, the decoder's elimination
+/// SiameseDecoder.cpp:937-1063 and :1680-1739).  Everything symbol-sized is
+/// expanded on the device: the lane-sum updates generate their own terms and
+/// coefficients CX(column) / CX(column)^2 from a snapshot of the codec's
+/// window, and each row generates its LDPC pair picks from PCG(row, n).  The
+/// host sends O(1) words per row instead of a term per source.
+///
+/// Stream layout after the GfOp header (kind = OP_ROWS, n = rows R,
+/// valid = window entries E, mix = sum updates U, termCount = block words):
+///   24 words   WinEntry of the lane sums as the rows read them (lane*3 + s)
+///   E words    WinEntry of window elements [base, base+E): an absent
+///              (lost) element has len 0 and contributes nothing
+///   U words    SumUpdate, run before any row of the batch (no row of the
+///              batch reads a sum updated in it before the update; ops.h
+///              invariant kept by Program)
+///   R*3 words  RowItem
+struct WinEntry
+{
+    uint64_t src;
+    uint32_t len;
+    uint32_t column;     // packet number (selects CX for sum updates)
+};
+
+/// dst[0,n) = keep(dst,valid) ^ sum over elements e = from, from+8, ... < to
+/// of coeff(e) * window[e], coeff = 1, CX(column) or CX(column)^2 (s = 0..2).
+struct SumUpdate
+{
+    uint32_t dstLo, dstHi;
+    uint32_t n;
+    uint32_t valid : 30;
+    uint32_t s : 2;
+    uint32_t from;
+    uint32_t to;
+    uint32_t pad[2];
+};
+
+/// One Siamese row: dst[0,n) = keep(dst,valid) ^ acc0 ^ mix*acc1 where
+///   acc0 = sums selected by mask0 (bit lane*3+s) ^ window[ldpcOff + PCG_2i % ldpcN]
+///   acc1 = sums selected by mask1              ^ window[ldpcOff + PCG_2i+1 % ldpcN]
+/// over i < ceil(ldpcN/16) pairs of PCG.Seed(row, ldpcN) draws, then litLen
+/// footer bytes at dst + n.
+struct RowItem
 {
     uint64_t dst;
     uint32_t n;
     uint32_t valid;
-    uint32_t kindPicks;   // OP_ROW | npicks << 8
-    uint32_t mix;         // RX multiplier of acc1 | litLen << 8
-    uint32_t reserved[2];
-    uint8_t lit[8];       // literal bytes written at dst + n
-    uint32_t pad[2];
+    uint32_t mask0;      // bits 0..23; bits 24..31: litLen
+    uint32_t mask1;      // bits 0..23; bits 24..31: mix (RX)
+    uint32_t row;
+    uint32_t ldpcN;
+    uint32_t ldpcOff;
+    uint32_t pad;
+    uint8_t lit[8];
 };
-static_assert(sizeof(RowHeader) == 48, "RowHeader layout");
-constexpr unsigned kRowWords = sizeof(RowHeader) / 16;
-constexpr unsigned kPicksPerWord = 8;
-constexpr unsigned kMaxRowsTable = 0x7fff;   // table indices fit 15 bits
+static_assert(sizeof(WinEntry) == 16, "WinEntry layout");
+static_assert(sizeof(SumUpdate) == 32, "SumUpdate layout");
+static_assert(sizeof(RowItem) == 48, "RowItem layout");
+constexpr unsigned kRowSums = 24;                       // kLanes * kSums
+constexpr unsigned kUpdateWords = sizeof(SumUpdate) / 16;
+constexpr unsigned kRowWords = sizeof(RowItem) / 16;
+
+/// PCG-XSH-RR as the reference seeds it (SiameseTools.h:80-102).
+constexpr uint64_t kPcgMul = 6364136223846793005ULL;
 
 inline uint32_t op_words(const GfOp& op)
 {
-    // (an OP_ROWS header's words cover its table; its rows follow as items)
+    // (an OP_ROWS header's termCount is its whole block in words)
     return kOpWords + ((op.kind == OP_LINCOMB || op.kind == OP_ROWS) ? op.termCount : 0);
 }
 
@@ -157,6 +191,7 @@ struct IngestDesc
     uint8_t hdr[8];
 };
 
-constexpr unsigned kTileBytes = 1024;   // 64 lanes x 16 bytes
+constexpr unsigned kTileBytes = 1024;       // solve tiles: 64 lanes x 16 bytes
+constexpr unsigned kExecTileBytes = 2048;   // executor tiles: 64 lanes x 2 x 16 bytes
 
 } // namespace sgpu

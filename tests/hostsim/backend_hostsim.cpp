@@ -9,6 +9,7 @@
 // so a wrong op stream or table fails the same parity tests the GPU runs.
 #include "../../siamese_amd/csrc/backend.h"
 #include "../../siamese_amd/csrc/gf.h"
+#include "../../siamese_amd/csrc/codedef.h"
 
 #include <cstdlib>
 #include <cstring>
@@ -100,12 +101,12 @@ struct TileTerm
 void lincomb_tile(uint64_t dstAddr, uint32_t n, uint32_t valid, uint32_t mix,
                   const std::vector<TileTerm>& terms, uint32_t t0)
 {
-    const uint32_t t1 = t0 + kTileBytes;
+    const uint32_t t1 = t0 + kExecTileBytes;
     const uint32_t end = n < t1 ? n : t1;
     if (t0 >= end)
         return;
     const unsigned w = end - t0;
-    uint8_t acc0[kTileBytes], acc1[kTileBytes], tmp[kTileBytes];
+    uint8_t acc0[kExecTileBytes], acc1[kExecTileBytes], tmp[kExecTileBytes];
     std::memset(acc0, 0, w);
     std::memset(acc1, 0, w);
     for (const TileTerm& tm : terms) {
@@ -132,7 +133,7 @@ void literal_tile(uint64_t dst, uint32_t at, const uint8_t* lit, uint32_t len, u
 {
     for (uint32_t k = 0; k < len; ++k) {
         const uint32_t b = at + k;
-        if (b >= t0 && b < t0 + kTileBytes)
+        if (b >= t0 && b < t0 + kExecTileBytes)
             P(dst)[b] = lit[k];
     }
 }
@@ -164,27 +165,54 @@ void exec_tile(const uint8_t* stream, const ExecItem& it)
         }
         if (op.kind != OP_ROWS)
             std::abort();
-        // OP_ROWS: T table entries (lane sums first), then K row items (ops.h)
-        const GfTerm* table = reinterpret_cast<const GfTerm*>(body);
-        for (uint32_t r = 0; r < op.n; ++r, ++oi) {
-            RowHeader h;
-            std::memcpy(&h, w, sizeof(h));
-            if ((h.kindPicks & 0xff) != OP_ROW)
-                std::abort();
-            const uint32_t npicks = h.kindPicks >> 8;
-            const uint16_t* picks = reinterpret_cast<const uint16_t*>(w + sizeof(RowHeader));
-            w += sizeof(RowHeader) + (size_t)((npicks + kPicksPerWord - 1) / kPicksPerWord) * 16;
-            if (w > end)
-                std::abort();
+        // OP_ROWS (ops.h): sums, window, sum updates, rows
+        const uint32_t E = op.valid, U = op.mix, R = op.n;
+        const WinEntry* sums = reinterpret_cast<const WinEntry*>(body);
+        const WinEntry* win = sums + kRowSums;
+        const SumUpdate* ups = reinterpret_cast<const SumUpdate*>(win + E);
+        const RowItem* rows = reinterpret_cast<const RowItem*>(ups + U);
+        if (reinterpret_cast<const uint8_t*>(rows + R) != w)
+            std::abort(); // malformed block
+        for (uint32_t u = 0; u < U; ++u) {
+            const SumUpdate& up = ups[u];
             terms.clear();
-            for (uint32_t k = 0; k < npicks; ++k) {
-                const uint32_t idx = picks[k] & 0x7fff;
-                if (idx >= op.valid)
+            for (uint32_t e = up.from; e < up.to; e += kLanes) {
+                if (e >= E)
                     std::abort();
-                terms.push_back(TileTerm{table[idx].src, table[idx].len, 1, (uint8_t)(picks[k] >> 15)});
+                const WinEntry& x = win[e];
+                if (x.len == 0)
+                    continue;
+                uint8_t c = 1;
+                if (up.s > 0) {
+                    c = column_value(x.column);
+                    if (up.s == 2)
+                        c = gf_sqr(c);
+                }
+                terms.push_back(TileTerm{x.src, x.len, c, 0});
             }
-            lincomb_tile(h.dst, h.n, h.valid, h.mix & 0xff, terms, t0);
-            literal_tile(h.dst, h.n, h.lit, h.mix >> 8, t0);
+            lincomb_tile(((uint64_t)up.dstHi << 32) | up.dstLo, up.n, up.valid, 0, terms, t0);
+        }
+        for (uint32_t r = 0; r < R; ++r) {
+            const RowItem& h = rows[r];
+            terms.clear();
+            for (unsigned k = 0; k < kRowSums; ++k) {
+                if ((h.mask0 >> k & 1) && sums[k].len)
+                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 0});
+                if ((h.mask1 >> k & 1) && sums[k].len)
+                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 1});
+            }
+            Pcg32 prng;
+            prng.seed(h.row, h.ldpcN);
+            const uint32_t pairs = (h.ldpcN + kPairRate - 1) / kPairRate;
+            for (uint32_t i = 0; i < 2 * pairs; ++i) {
+                const uint32_t e = h.ldpcOff + prng.next() % h.ldpcN;
+                if (e >= E)
+                    std::abort();
+                if (win[e].len)
+                    terms.push_back(TileTerm{win[e].src, win[e].len, 1, (uint8_t)(i & 1)});
+            }
+            lincomb_tile(h.dst, h.n, h.valid, h.mask1 >> 24, terms, t0);
+            literal_tile(h.dst, h.n, h.lit, h.mask0 >> 24, t0);
         }
     }
 }
