@@ -28,7 +28,9 @@ void be_memset(void* dst, int value, size_t bytes);
 /// One wave per descriptor (count descriptors), looping over its tiles.
 void be_launch_ingest(const IngestDesc* descs, uint32_t count);
 /// `stream`: the instruction words of every segment (see ExecItem).
-void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count);
+/// `acct`: device counter the executor adds the reference's source bytes of
+/// the terms it expands itself (sum updates, LDPC picks) to (ops.h).
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct);
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
                             uint32_t* results, uint32_t count);
 /// maxRows: largest m among the solves this launch covers (sizes LDS staging).

@@ -210,10 +210,13 @@ __device__ __forceinline__ Acc2 zero2()
     return r;
 }
 
+// A term's bytes in [len, align16(len)) are zero in memory (every writer
+// zero-fills the tail of its last 16-byte lane, ops.h), so only lanes wholly
+// past the term's end need clearing: one select per dword, no byte masks.
 __device__ __forceinline__ uint4 term_value(uint4 x, uint32_t p, uint32_t len, uint32_t coeff)
 {
-    if (p + 16 > len)
-        x = mask16(x, (int)len - (int)p);
+    if (p >= len)
+        x = make_uint4(0, 0, 0, 0);
     if (coeff != 1)
         x = gf_mul16(x, coeff);
     return x;
@@ -288,8 +291,10 @@ __device__ __forceinline__ void read_term(uint4 w, uint64_t& src, uint32_t& len)
     len = uni(w.z);
 }
 
-// dst[p, p+16) of an item: keep(dst, valid) ^ out for bytes < n, dst bytes
-// at and beyond n untouched.  `cur` is dst[p, p+16) as loaded at item start.
+// dst[p, p+16) of an item: keep(dst, valid) ^ out for bytes < n, zero for
+// bytes in [n, p+16) (the zero tail every term reader relies on), nothing
+// stored for lanes at or past n.  `cur` is dst[p, p+16) as loaded at item
+// start when p < valid.
 __device__ __forceinline__ void store_item(uint4 out, uint32_t p, uint64_t dst, uint32_t n, uint32_t valid,
                                            uint4 cur)
 {
@@ -301,23 +306,15 @@ __device__ __forceinline__ void store_item(uint4 out, uint32_t p, uint64_t dst, 
             prior = mask16(prior, (int)valid - (int)p);
         out = xor16(out, prior);
     }
-    if (p + 16 > n) {
-        const int nb = (int)n - (int)p;
-        const uint4 keep = make_uint4(~byte_mask(nb), ~byte_mask(nb - 4), ~byte_mask(nb - 8),
-                                      ~byte_mask(nb - 12));
-        out = mask16(out, nb);
-        out.x |= cur.x & keep.x;
-        out.y |= cur.y & keep.y;
-        out.z |= cur.z & keep.z;
-        out.w |= cur.w & keep.w;
-    }
+    if (p + 16 > n)
+        out = mask16(out, (int)n - (int)p);
     st16(dst + p, out);
 }
 
 // what store_item needs of dst, loaded while the terms stream in
 __device__ __forceinline__ uint4 load_cur(uint32_t p, uint64_t dst, uint32_t n, uint32_t valid)
 {
-    if (p < n && (p < valid || p + 16 > n))
+    if (p < n && p < valid)
         return ld16(dst + p);
     return make_uint4(0, 0, 0, 0);
 }
@@ -348,7 +345,8 @@ __device__ __forceinline__ uint4 table_entry(const uint4* tableL, const uint4* _
 }
 
 __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
-                                                       const ExecItem* __restrict__ items)
+                                                       const ExecItem* __restrict__ items,
+                                                       unsigned long long* __restrict__ acct)
 {
     __shared__ uint4 ring[2][kRingWords];
     __shared__ uint4 part[kExecWaves - 1][2][64];
@@ -467,6 +465,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 const uint32_t cnt = to > from ? (to - from + kLanes - 1) / kLanes : 0;
                 uint4 ev = make_uint4(0, 0, 0, 0);
                 uint32_t cv = 1;
+                uint32_t refBytes = 0;   // reference source bytes (one add/muladd per original)
                 gather2(0, cnt, tileBase, p, acc0, acc1,
                         [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
                             const uint32_t j = k & 63u;
@@ -480,10 +479,13 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             }
                             lane_term(ev, j, src, len);
                             ca = rl(cv, j);
+                            refBytes += len;
                             return len != 0;
                         });
                 store_item(acc0.a, p, udst, un, uvalid, c0);
                 store_item(acc0.b, p1, udst, un, uvalid, c1);
+                if (tileBase == 0 && lane == 0 && refBytes)
+                    atomicAdd(acct, (unsigned long long)refBytes);
             }
             __syncthreads();
 
@@ -519,6 +521,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     // sparse part: ceil(N/16) pairs of PCG.Seed(row, N) draws
                     // (SiameseEncoder.cpp:1100-1144): lane j makes draw 64c+j by
                     // jump-ahead and fetches its window entry
+                    uint32_t refBytes = 0;   // reference source bytes of the pairs
                     if (N != 0) {
                         const uint64_t inc = ((uint64_t)row << 1) | 1u;
                         uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
@@ -534,9 +537,12 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                     }
                                     lane_term(ev, j, src, len);
                                     ca = 1u | ((k & 1u) << 8);
+                                    refBytes += len < rn ? len : rn;
                                     return len != 0;
                                 });
                     }
+                    if (tileBase == 0 && lane == 0 && refBytes)
+                        atomicAdd(acct, (unsigned long long)refBytes);
                     if (mix > 1) {
                         acc1.a = gf_mul16(acc1.a, mix);
                         acc1.b = gf_mul16(acc1.b, mix);
@@ -1107,13 +1113,14 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count)
                        dim3(64 * kIngestWaves), 0, g_stream, descs, count);
 }
 
-void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count)
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct)
 {
     if (count == 0)
         return;
     Timed t(true);
     hipLaunchKernelGGL(k_exec, dim3(count), dim3(kExecThreads), 0, g_stream,
-                       static_cast<const uint4*>(stream), items);
+                       static_cast<const uint4*>(stream), items,
+                       reinterpret_cast<unsigned long long*>(acct));
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,

@@ -251,24 +251,22 @@ DevSum& DecoderCore::get_sum(unsigned lane, unsigned s, unsigned elementEnd)
 
     unsigned newBytes = S.d.bytes;
     unsigned got = 0;
-    uint64_t opBytes = 0;
     unsigned end = element;
     for (; end < elementEnd; end += kLanes) {
         const unsigned b = slot(end).bytes;
         if (b > 0) {
             newBytes = std::max(newBytes, b);
-            opBytes += b;
             ++got;
         }
     }
     if (got > 0) {
         if (!grow_sum(S.d, newBytes))
             return S.d;
-        // terms (received originals; lost ones are absent in the window)
-        // and their coefficients are generated on the device
+        // terms (received originals; lost ones are absent in the window),
+        // their coefficients and their reference source bytes are generated
+        // on the device
         cover(std::min(element, windowLo_), end - kLanes + 1);
         prog_.rows_update(lane * kSums + s, S.d.buf.addr(), S.d.bytes, S.d.devValid, s, element, end);
-        eng_->account(opBytes);
         S.d.devValid = S.d.bytes;
     }
     S.elementEnd = end;
@@ -1178,12 +1176,8 @@ bool DecoderCore::eliminate_original_data()
                 t.len = d.bytes;
                 t.column = 0;
             }
-        // LDPC pairs over received originals, drawn on the device; the host
-        // walks the same draws only to count reference bytes
-        unsigned picks = 0;
-        const uint32_t* off = ldpc_offsets(m.row, m.ldpcCount, &picks);
-        for (unsigned k = 0; k < picks; ++k)
-            opBytes += std::min(slot(es + off[k]).bytes, rb);
+        // LDPC pairs over received originals: drawn (and their reference
+        // source bytes counted) on the device
         // rows of one decode share the sums: one row of the program's batch
         cover(windowLo_, ee);
         prog_.rows_row(sums, rec->buf.addr(), rb, rb, row_value(m.row), mask[0], mask[1], m.row,

@@ -223,22 +223,20 @@ DevSum& EncoderCore::get_sum(unsigned lane, unsigned sumIndex, unsigned elementE
     if (element >= elementEnd)
         return sum;
 
-    unsigned newBytes = sum.bytes;
-    if (L.longest > 0)
-        newBytes = std::max(newBytes, L.longest);
-    uint64_t opBytes = 0; // one add/muladd per original in the reference
-    unsigned end = element;
-    for (; end < elementEnd; end += kLanes) {
-        const unsigned b = slot(end).bytes;
-        newBytes = std::max(newBytes, b);
-        opBytes += b;
-    }
+    // The sum grows to the longest original it covers.  L.longest bounds
+    // every element of the lane from FirstUnremoved on; older (acknowledged)
+    // elements are checked one by one.
+    unsigned newBytes = std::max(sum.bytes, L.longest);
+    const unsigned end = element + ((elementEnd - element + kLanes - 1) / kLanes) * kLanes;
+    for (unsigned e = element; e < end && e < firstUnremoved_; e += kLanes)
+        newBytes = std::max(newBytes, slot(e).bytes);
     if (!grow_sum(sum, newBytes))
         return sum;
+    // reference source bytes (one add/muladd per original) are counted by
+    // the device as it expands the update
     cover(std::min(element, std::min(sumStart_, firstUnremoved_)), end - kLanes + 1);
     prog_.rows_update(lane * kSums + sumIndex, sum.buf.addr(), sum.bytes, sum.devValid, sumIndex,
                       element, end);
-    eng_->account(opBytes);
     sum.devValid = sum.bytes;
     L.next[sumIndex] = end;
     return sum;
@@ -438,13 +436,9 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     const unsigned footerBytes = write_footer(m, footer);
 
     // Sparse part (:1100-1144): ceil(n/16) PCG-chosen pairs, drawn on the
-    // device; the host walks the same draws only to count reference bytes.
+    // device, which also counts their reference source bytes
     const unsigned start = firstUnremoved_;
     const unsigned n = sumEnd_ - start;
-    unsigned picks = 0;
-    const uint32_t* off = ldpc_offsets(row, n, &picks);
-    for (unsigned i = 0; i < picks; ++i)
-        opBytes += slot(start + off[i]).bytes;
 
     // Recovery = row sums ^ RX * product (:1232-1233) and its footer: one row
     // of the program's Siamese row batch (consecutive rows share the sums)

@@ -880,8 +880,10 @@ void Engine::flush()
         std::memcpy(up + oSI, sitems.data(), sitems.size() * sizeof(SolveItem));
     }
 
-    // download area: results first, then each requested range
-    size_t dOff = align16((size_t)resultWords * 4);
+    // download area: the executor's byte counter (kAcctBytes), the solve
+    // results, then each requested range
+    constexpr size_t kAcctBytes = 16;
+    size_t dOff = align16(kAcctBytes + (size_t)resultWords * 4);
     flight_.downloads.clear();
     std::vector<Shard::Download> dls;
     for (Shard* s : shards)
@@ -890,19 +892,20 @@ void Engine::flush()
             dls.push_back(d);
             dOff = align16(dOff + d.bytes);
         }
-    if (dOff)
-        ensure_down(dOff);
+    ensure_down(dOff);
 
     // ---- 3. launch -----------------------------------------------------------
     if (upBytes)
         be_h2d(upDev_, upHost_, upBytes);
     if (nIngest)
         be_launch_ingest((const IngestDesc*)(upDev_ + oIngD), (uint32_t)nIngest);
-    uint32_t* resultsDev = (uint32_t*)downDev_;
+    uint64_t* acctDev = (uint64_t*)downDev_;
+    uint32_t* resultsDev = (uint32_t*)(downDev_ + kAcctBytes);
+    be_memset(acctDev, 0, sizeof(uint64_t));
     for (const Phase& ph : phases) {
         if (ph.kind == Phase::EXEC) {
             be_launch_exec(upDev_ + oStream, (const ExecItem*)(upDev_ + oItems) + ph.itemBegin,
-                           (uint32_t)ph.itemCount);
+                           (uint32_t)ph.itemCount, acctDev);
             flushStats_.execLaunches++;
         } else {
             const SolveDesc* sd = (const SolveDesc*)(upDev_ + oSD) + ph.solveBegin;
@@ -915,8 +918,7 @@ void Engine::flush()
                                  (uint32_t)ph.itemCount, ph.maxRows);
         }
     }
-    if (resultWords)
-        be_d2h(downHost_, resultsDev, (size_t)resultWords * 4);
+    be_d2h(downHost_, downDev_, kAcctBytes + (size_t)resultWords * 4);
     for (size_t i = 0; i < dls.size(); ++i)
         be_d2h(downHost_ + flight_.downloads[i].off, (const void*)(uintptr_t)dls[i].dev,
                dls[i].bytes);
@@ -1033,7 +1035,11 @@ bool Engine::sync()
     const uint64_t t1 = now_ns();
     // Completions of different programs touch different instances: run them
     // in parallel, each program's in order.
-    const uint32_t* results = (const uint32_t*)downHost_;
+    // bytes the executor counted for the terms it expanded itself
+    uint64_t acct = 0;
+    std::memcpy(&acct, downHost_, sizeof(acct));
+    flushStats_.refOpBytes += acct;
+    const uint32_t* results = (const uint32_t*)(downHost_ + 16);
     pool().run(flight_.callbacks.size(), [&](size_t i) {
         auto& cb = flight_.callbacks[i];
         for (Completion& fn : cb.second)

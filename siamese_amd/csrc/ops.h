@@ -37,7 +37,11 @@ enum GfOpKind : uint32_t
 /// One op.  For OP_LINCOMB:
 ///   for i < n:  dst[i] = (i < valid ? dst[i] : 0) ^ sum_{acc0 terms} c*src[i]
 ///                        ^ mix * sum_{acc1 terms} c*src[i]
-///   bytes of dst at i >= n are left untouched.
+///   bytes of dst in [n, align16(n)) become zero and bytes at and beyond
+///   align16(n) are left untouched.  Every symbol buffer therefore reads as
+///   zero between its length and the end of its last 16-byte lane (k_ingest
+///   and the solve keep the same rule), which the executor relies on when it
+///   reads a term of length len < n.
 /// For OP_LITERAL: writes `valid` (<= 8) bytes taken from `lit` at dst + n.
 struct GfOp
 {

@@ -112,7 +112,11 @@ void lincomb_tile(uint64_t dstAddr, uint32_t n, uint32_t valid, uint32_t mix,
     for (const TileTerm& tm : terms) {
         if (t0 >= tm.len)
             continue;
-        const unsigned k = (tm.len < end ? tm.len : end) - t0;
+        // read through the end of the term's last 16-byte lane, as the kernel
+        // does: those bytes must be zero in memory (ops.h), and garbage there
+        // shows up as a parity failure here
+        const uint32_t lenA = (tm.len + 15) & ~15u;
+        const unsigned k = (lenA < end ? lenA : end) - t0;
         std::memcpy(tmp, P(tm.src) + t0, k);
         if (tm.coeff != 1)
             mul_bytes(tmp, k, tm.coeff);
@@ -127,6 +131,11 @@ void lincomb_tile(uint64_t dstAddr, uint32_t n, uint32_t valid, uint32_t mix,
         const uint8_t prior = (t0 + i < valid) ? dst[i] : 0;
         dst[i] = prior ^ acc0[i] ^ acc1[i];
     }
+    // the kernel zero-fills the rest of the last 16-byte lane (ops.h)
+    const uint32_t tailEnd = (n + 15) & ~15u;
+    for (uint32_t b = n; b < tailEnd; ++b)
+        if (b >= t0 && b < t1)
+            P(dstAddr)[b] = 0;
 }
 
 void literal_tile(uint64_t dst, uint32_t at, const uint8_t* lit, uint32_t len, uint32_t t0)
@@ -138,7 +147,7 @@ void literal_tile(uint64_t dst, uint32_t at, const uint8_t* lit, uint32_t len, u
     }
 }
 
-void exec_tile(const uint8_t* stream, const ExecItem& it)
+void exec_tile(const uint8_t* stream, const ExecItem& it, uint64_t* acct)
 {
     const uint8_t* w = stream + (size_t)it.streamBegin * 16;
     const uint8_t* end = w + (size_t)it.streamWords * 16;
@@ -189,6 +198,8 @@ void exec_tile(const uint8_t* stream, const ExecItem& it)
                         c = gf_sqr(c);
                 }
                 terms.push_back(TileTerm{x.src, x.len, c, 0});
+                if (t0 == 0)
+                    *acct += x.len;   // the reference's source bytes (device-counted)
             }
             lincomb_tile(((uint64_t)up.dstHi << 32) | up.dstLo, up.n, up.valid, 0, terms, t0);
         }
@@ -210,6 +221,8 @@ void exec_tile(const uint8_t* stream, const ExecItem& it)
                     std::abort();
                 if (win[e].len)
                     terms.push_back(TileTerm{win[e].src, win[e].len, 1, (uint8_t)(i & 1)});
+                if (t0 == 0)
+                    *acct += win[e].len < h.n ? win[e].len : h.n;
             }
             lincomb_tile(h.dst, h.n, h.valid, h.mask1 >> 24, terms, t0);
             literal_tile(h.dst, h.n, h.lit, h.mask0 >> 24, t0);
@@ -286,12 +299,12 @@ static bool noexec()
     return v == 1;
 }
 
-void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count)
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct)
 {
     if (noexec())
         return;
     for (uint32_t i = 0; i < count; ++i)
-        exec_tile(static_cast<const uint8_t*>(stream), items[i]);
+        exec_tile(static_cast<const uint8_t*>(stream), items[i], acct);
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
@@ -389,6 +402,8 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
             const uint8_t inv = g_inv[C[(size_t)i * m + i]];
             for (uint32_t b = t0; b < fb; ++b)
                 P(R[i].buf)[b] = b < bb ? gf_mul(P(R[i].buf)[b], inv) : 0;
+            for (uint32_t b = fb > t0 ? fb : t0; b < clip((bb + 15) & ~15u); ++b)
+                P(R[i].buf)[b] = 0;   // the kernel stores whole 16-byte lanes
             for (uint32_t j = 0; j < (uint32_t)i; ++j) {
                 const uint8_t c = C[(size_t)j * m + i];
                 if (!c)
