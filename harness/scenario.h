@@ -190,6 +190,12 @@ struct Stream
     StreamResult* res = nullptr;
     unsigned global = 0;          // global stream index
     std::vector<uint64_t> log;    // event log
+    bool logOn = true;            // keep the log (digests); off in timed bench steps
+    void note(uint64_t e)
+    {
+        if (logOn)
+            log.push_back(e);
+    }
 
     Pcg loss;
     Phase phase = ADD;
@@ -209,6 +215,8 @@ struct Stream
         res = r;
         global = globalIndex;
         std::memset(res, 0, sizeof(*res));
+        if (logOn)
+            log.reserve(4 * cfg->originals + 64);
         loss.seed(cfg->seed, global);
         buf.resize(cfg->payload_bytes ? cfg->payload_bytes + 8 : 1208);
         phase = ADD;
@@ -235,11 +243,11 @@ struct Stream
             Pkt p;
             const int r = codec->dec_get(nextExpected, &p);
             if (r != 0) {
-                log.push_back(ev(EV_GET, r, nextExpected));
+                note(ev(EV_GET, r, nextExpected));
                 return r == 2; // NeedMoreData is the normal stop
             }
-            log.push_back(ev(EV_GET, 0, nextExpected));
-            log.push_back(codec->pkt_token(p, packet_id(nextExpected), &dataOk));
+            note(ev(EV_GET, 0, nextExpected));
+            note(codec->pkt_token(p, packet_id(nextExpected), &dataOk));
             ++nextExpected;
             ++res->delivered;
         }
@@ -251,14 +259,14 @@ struct Stream
     {
         Rec rec;
         const int r = codec->encode(&rec);
-        log.push_back(ev(EV_ENCODE, r));
+        note(ev(EV_ENCODE, r));
         if (r == 2)
             return; // nothing to encode yet
         if (r != 0) {
             fail(2);
             return;
         }
-        log.push_back(codec->rec_token(rec));
+        note(codec->rec_token(rec));
         ++res->encodes;
         res->recovery_bytes += rec.bytes;
         const bool lost = (loss.next() % 100) < cfg->recovery_loss_pct;
@@ -267,7 +275,7 @@ struct Stream
             return;
         }
         const int a = codec->dec_add_recovery(rec);
-        log.push_back(ev(EV_DEC_ADD_REC, a));
+        note(ev(EV_DEC_ADD_REC, a));
         if (a != 0) {
             fail(2);
             return;
@@ -295,7 +303,7 @@ struct Stream
             }
             unsigned num = 0;
             const int r = codec->enc_add(id, host, bytes, &num);
-            log.push_back(ev(EV_ENC_ADD, r, num));
+            note(ev(EV_ENC_ADD, r, num));
             if (r != 0) {
                 fail(2);
                 return false;
@@ -307,7 +315,7 @@ struct Stream
                 ++res->originals_lost;
             } else {
                 const int a = codec->dec_add_original(id, num, host, bytes);
-                log.push_back(ev(EV_DEC_ADD_ORIG, a, num));
+                note(ev(EV_DEC_ADD_ORIG, a, num));
                 if (a != 0 && a != 4) {
                     fail(2);
                     return false;
@@ -331,7 +339,7 @@ struct Stream
             return codec->wants_yield_after_encode();
         case DECODE_LOOP: {
             const int ready = codec->is_ready();
-            log.push_back(ev(EV_IS_READY, ready));
+            note(ev(EV_IS_READY, ready));
             if (ready != 0) {
                 phase = tailMode ? TAIL : ACK;
                 return false;
@@ -339,7 +347,7 @@ struct Stream
             decoded.clear();
             ++res->decode_calls;
             const int r = codec->decode(&decoded);
-            log.push_back(ev(EV_DECODE, r, (uint64_t)decoded.size()));
+            note(ev(EV_DECODE, r, (uint64_t)decoded.size()));
             if (r == 2) {
                 ++res->decode_fail;
                 return false;
@@ -353,8 +361,8 @@ struct Stream
         }
         case DECODED: {
             for (const Pkt& p : decoded) {
-                log.push_back(ev(EV_DECODED_PKT, 0, p.num));
-                log.push_back(codec->pkt_token(p, packet_id(p.num), &dataOk));
+                note(ev(EV_DECODED_PKT, 0, p.num));
+                note(codec->pkt_token(p, packet_id(p.num), &dataOk));
                 ++res->recovered;
             }
             decoded.clear();
@@ -368,12 +376,12 @@ struct Stream
             tailMode = (phase == TAIL);
             if (cfg->ack_policy == 1) {
                 const int r = codec->enc_remove_before(nextExpected);
-                log.push_back(ev(EV_REMOVE, r, nextExpected));
+                note(ev(EV_REMOVE, r, nextExpected));
             } else if (cfg->ack_policy == 2) {
                 const unsigned lag = (lastNum - nextExpected) & 0x3fffff;
                 if (lag >= cfg->ack_lag && lag < 0x200000) {
                     const int r = codec->enc_remove_before(nextExpected);
-                    log.push_back(ev(EV_REMOVE, r, nextExpected));
+                    note(ev(EV_REMOVE, r, nextExpected));
                 }
             }
             return false;
@@ -400,6 +408,8 @@ struct Stream
     {
         if (!dataOk && res->status == 0)
             res->status = 3;
+        if (!logOn)
+            return;   // no digest without a log
         Fnv f;
         for (uint64_t e : log)
             f.u64(e);

@@ -39,6 +39,7 @@ struct BatchOptions
     uint32_t groups;   ///< stream groups alternating host work and device work (0 = 1)
     uint32_t e2e;      ///< originals start in pinned host memory (H2D each step) and every
                        ///< recovery packet and recovered original is copied back (D2H)
+    uint32_t digest;   ///< keep event logs and digests on unverified runs too
 };
 
 struct BatchReport
@@ -167,6 +168,7 @@ struct Shared
     uint64_t checked = 0, mismatches = 0;
     std::unique_ptr<sgpu::WorkerPool> pool;
     unsigned groups = 1;
+    bool digest = true;   // per-stream digests (event logs) also on unverified runs
 };
 
 struct BatchCodec
@@ -327,6 +329,8 @@ int run_once(Shared& sh, StreamResult* results, uint64_t* rounds, double* phase)
         codecs[s].enc = api.encoder_create();
         codecs[s].dec = api.decoder_create();
         codecs[s].log = &streams[s].log;
+        // the event log only feeds digests: timed bench steps run without it
+        streams[s].logOn = sh.verify || sh.hashData || sh.digest;
         streams[s].init(cfg, &codecs[s], &results[s], cfg->first_stream + (unsigned)s);
         if (!codecs[s].enc || !codecs[s].dec)
             streams[s].fail(2);
@@ -530,6 +534,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
     for (unsigned r = 0; r < runs && rc == 0; ++r) {
         const bool timed = r >= opt->warmup;
         sh.verify = opt->verify && r == 0;
+        sh.digest = opt->digest != 0;
         const unsigned threads = opt->threads ? opt->threads : sgpu::WorkerPool::default_threads();
         if (!sh.pool || sh.pool->size() != threads)
             sh.pool.reset(new sgpu::WorkerPool(threads));

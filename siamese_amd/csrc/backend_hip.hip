@@ -16,9 +16,13 @@
 
 #include "backend.h"
 #include "codedef.h"
+#include "placement.h"
+#include "pool.h"
 #include "gf.h"
 
+#include <cctype>
 #include <cstdio>
+#include <string>
 #include <cstring>
 #include <vector>
 
@@ -1004,6 +1008,35 @@ bool be_init(int device, const char** err)
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
         *err = "device is not gfx950 (MI355X); kernels are built for gfx950 only";
         return false;
+    }
+    // Host threads next to the device: the NUMA node of its PCI function,
+    // a slice per device on that node (placement.h).
+    {
+        char bus[64] = {0};
+        auto node_of = [](const char* b) {
+            std::string s(b);
+            for (char& c : s)
+                c = (char)std::tolower((unsigned char)c);
+            FILE* f = std::fopen(("/sys/bus/pci/devices/" + s + "/numa_node").c_str(), "r");
+            int node = -1;
+            if (f) {
+                if (std::fscanf(f, "%d", &node) != 1)
+                    node = -1;
+                std::fclose(f);
+            }
+            return node;
+        };
+        if (hipDeviceGetPCIBusId(bus, sizeof(bus), cur) == hipSuccess) {
+            const int myNode = node_of(bus);
+            unsigned slice = 0;
+            for (int d = 0; d < cur; ++d) {
+                char other[64] = {0};
+                if (hipDeviceGetPCIBusId(other, sizeof(other), d) == hipSuccess &&
+                    node_of(other) == myNode)
+                    ++slice;
+            }
+            place_near_device(bus, slice, WorkerPool::default_threads());
+        }
     }
     if (hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking) != hipSuccess) {
         *err = "hipStreamCreate failed";

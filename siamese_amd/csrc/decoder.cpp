@@ -121,7 +121,7 @@ bool DecoderCore::grow_window(unsigned end)
 {
     const unsigned needed = (end + kLanes + kSubwindow - 1) / kSubwindow;
     while (subwindows_.size() < needed)
-        subwindows_.emplace_back(new DecSubwindow);
+        subwindows_.emplace_back(ObjPool<DecSubwindow>::get());
     if (end > count_)
         count_ = end;
     return true;
@@ -462,10 +462,22 @@ void DecoderCore::remove_elements()
 // ---------------------------------------------------------------------------
 // Recovery packet list (:2567-2666)
 
+void DecSubwindowRecycle::operator()(DecSubwindow* w) const
+{
+    w->reset();
+    for (DecSlot& s : w->slot) {
+        s.buf = DevBuf();
+        s.header = 0;
+        s.host.clear();
+    }
+    ObjPool<DecSubwindow>::put(w);
+}
+
 void DecoderCore::free_packet(RecPacket* r)
 {
     eng_->release(r->buf);
-    delete r;
+    *r = RecPacket();
+    ObjPool<RecPacket>::put(r);
 }
 
 void DecoderCore::list_insert(RecPacket* r, bool outOfOrder)
@@ -623,10 +635,10 @@ SiameseResult DecoderCore::add_recovery_common(const RowMeta& m, int footer, uns
         return Siamese_Success;
     }
 
-    RecPacket* r = new RecPacket;
+    RecPacket* r = ObjPool<RecPacket>::get();
     r->buf = eng_->alloc(payload + payload / 16);
     if (!r->buf) {
-        delete r;
+        ObjPool<RecPacket>::put(r);
         disabled_ = true;
         return Siamese_Disabled;
     }

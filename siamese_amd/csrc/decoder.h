@@ -17,6 +17,7 @@
 #include "codedef.h"
 #include "encoder.h"
 #include "engine.h"
+#include "objpool.h"
 #include "../../include/siamese.h"
 
 #include <memory>
@@ -50,6 +51,14 @@ struct DecSubwindow
         }
     }
 };
+
+/// unique_ptr deleter: subwindows go back to the thread's pool, emptied
+/// (their buffers were released by the owner).
+struct DecSubwindowRecycle
+{
+    void operator()(DecSubwindow* w) const;
+};
+using DecSubwindowPtr = std::unique_ptr<DecSubwindow, DecSubwindowRecycle>;
 
 struct RecPacket
 {
@@ -179,7 +188,7 @@ private:
     unsigned count_ = 0;
     unsigned columnStart_ = 0;
     unsigned nextExpected_ = 0;
-    std::vector<std::unique_ptr<DecSubwindow>> subwindows_;
+    std::vector<DecSubwindowPtr> subwindows_;
     Sum lanes_[kLanes][kSums];
     unsigned sumColumnStart_ = 0;
     unsigned sumColumnCount_ = 0;

@@ -43,7 +43,7 @@ SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc
 
     // Keep one lane-width of spare slots ahead of the last subwindow (:108-118)
     if (element + kLanes >= subwindows_.size() * kSubwindow)
-        subwindows_.emplace_back(new EncSubwindow);
+        subwindows_.emplace_back(ObjPool<EncSubwindow>::get());
 
     if (count_ > 0)
         ++count_;

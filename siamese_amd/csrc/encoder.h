@@ -10,6 +10,7 @@
 #include "arq.h"
 #include "codedef.h"
 #include "engine.h"
+#include "objpool.h"
 #include "../../include/siamese.h"
 
 #include <memory>
@@ -31,6 +32,23 @@ struct EncSubwindow
 {
     EncSlot slot[kSubwindow];
 };
+
+/// unique_ptr deleter: subwindows go back to the thread's pool, emptied
+/// (their buffers were released by the owner).
+struct EncSubwindowRecycle
+{
+    void operator()(EncSubwindow* w) const
+    {
+        for (EncSlot& s : w->slot) {
+            s.buf = DevBuf();
+            s.bytes = s.column = s.header = 0;
+            s.lastSend = 0;
+            s.host.clear();
+        }
+        ObjPool<EncSubwindow>::put(w);
+    }
+};
+using EncSubwindowPtr = std::unique_ptr<EncSubwindow, EncSubwindowRecycle>;
 
 /// Running sum of one (lane, sum-index) in HBM.
 struct DevSum
@@ -112,7 +130,7 @@ private:
     bool mirror_;
     bool disabled_ = false;
 
-    std::vector<std::unique_ptr<EncSubwindow>> subwindows_;
+    std::vector<EncSubwindowPtr> subwindows_;
     unsigned nextColumn_ = 0;
     unsigned count_ = 0;
     unsigned columnStart_ = 0;

@@ -44,10 +44,52 @@ uint64_t now_ns()
 // ---------------------------------------------------------------------------
 // Program
 
+std::vector<Program::Store>& Program::spare_stores()
+{
+    thread_local std::vector<Store> spare;
+    return spare;
+}
+
+void Program::take_store()
+{
+    std::vector<Store>& spare = spare_stores();
+    if (spare.empty())
+        return;
+    Store& st = spare.back();
+    segs_.swap(st.segs);
+    rb_.win.swap(st.win);
+    rb_.updates.swap(st.updates);
+    rb_.rows.swap(st.rows);
+    spare.pop_back();
+}
+
+void Program::stash_store()
+{
+    std::vector<Store>& spare = spare_stores();
+    if (spare.size() >= 4096)
+        return;
+    for (Segment& g : segs_) {
+        g.ops.clear();
+        g.terms.clear();
+        g.rowsData.clear();
+    }
+    rb_.win.clear();
+    rb_.updates.clear();
+    rb_.rows.clear();
+    spare.emplace_back();
+    Store& st = spare.back();
+    st.segs.swap(segs_);
+    st.win.swap(rb_.win);
+    st.updates.swap(rb_.updates);
+    st.rows.swap(rb_.rows);
+}
+
 Program::~Program()
 {
-    if (!shard_)
+    if (!shard_) {
+        stash_store();
         return;
+    }
     rows_close();
     // The instance goes away with work still queued (e.g. an encoder freed
     // right after its last recovery packet was handed to a decoder, whose

@@ -46,7 +46,7 @@ using Completion = std::function<void(const uint32_t* results)>;
 class Program
 {
 public:
-    Program(Engine* e, int group) : eng_(e), group_(group) {}
+    Program(Engine* e, int group) : eng_(e), group_(group) { take_store(); }
     ~Program();
     Program(const Program&) = delete;
     Program& operator=(const Program&) = delete;
@@ -144,6 +144,18 @@ private:
     };
     void rows_close();
     void rows_open(uint32_t base, bool keepWindow);
+    // The containers of programs that went away are kept per host thread and
+    // handed to new programs, so a fresh codec starts with warm capacity.
+    struct Store
+    {
+        std::vector<Segment> segs;
+        std::vector<WinEntry> win;
+        std::vector<SumUpdate> updates;
+        std::vector<RowItem> rows;
+    };
+    static std::vector<Store>& spare_stores();
+    void take_store();
+    void stash_store();
     struct PendingSolve
     {
         SolveDesc desc;

@@ -77,7 +77,7 @@ class BatchOptions(ctypes.Structure):
     _fields_ = [("steps", ctypes.c_uint32), ("warmup", ctypes.c_uint32),
                 ("verify", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("threads", ctypes.c_uint32), ("groups", ctypes.c_uint32),
-                ("e2e", ctypes.c_uint32)]
+                ("e2e", ctypes.c_uint32), ("digest", ctypes.c_uint32)]
 
 
 class BatchReport(ctypes.Structure):
@@ -134,7 +134,7 @@ def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0
 
     Returns (results of the last run, BatchReport)."""
     res = (StreamResult * cfg.streams)()
-    opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads, groups, 1 if e2e else 0)
+    opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads, groups, 1 if e2e else 0, 1)
     rep = BatchReport()
     rc = lib().scenario_run_batch(library.encode(), ctypes.byref(cfg), res, ctypes.byref(opt),
                                   ctypes.byref(rep))
@@ -169,10 +169,12 @@ class BatchSession:
         if not self.handle:
             raise RuntimeError("scenario_batch_open(%s) failed" % library)
 
-    def run(self, steps=1, warmup=0, verify=False, threads=0, groups=1, e2e=False):
+    def run(self, steps=1, warmup=0, verify=False, threads=0, groups=1, e2e=False, digest=True):
+        """digest=False: timed runs skip the per-stream event logs (results
+        then carry no digest; take it from a verified run)."""
         res = (StreamResult * self.cfg.streams)()
         opt = BatchOptions(steps, warmup, 1 if verify else 0, -1, threads, groups,
-                           1 if e2e else 0)
+                           1 if e2e else 0, 1 if digest else 0)
         rep = BatchReport()
         rc = lib().scenario_batch_run(self.handle, res, ctypes.byref(opt), ctypes.byref(rep))
         if rc != 0:

@@ -37,12 +37,15 @@ def main():
     path = sys.argv[1]
     flt = None
     callers = None
+    lines = False
     top = 40
     args = sys.argv[2:]
     while args:
         a = args.pop(0)
         if a == "--filter":
             flt = args.pop(0)
+        elif a == "--lines":
+            lines = True
         elif a == "--callers":
             callers = args.pop(0)
         elif a == "--top":
@@ -55,6 +58,36 @@ def main():
                 samples.append(parts[1:])
     frames = {fr for s in samples for fr in s}
     names = symbolize(frames)
+    if lines:
+        # self samples of the filtered stacks by innermost source line
+        # (inlined frames resolved), e.g. --filter sgpu_encoder_free --lines
+        loc = collections.Counter()
+        pcs = collections.defaultdict(list)
+        for s in samples:
+            syms = [names[fr] for fr in s]
+            if flt and not any(flt in x for x in syms):
+                continue
+            if s:
+                pcs[s[0]].append(1)
+        by_obj = collections.defaultdict(list)
+        for fr in pcs:
+            obj, off = fr.rsplit(":", 1)
+            by_obj[obj].append(off)
+        for obj, offs in by_obj.items():
+            out = subprocess.run(["addr2line", "-a", "-i", "-e", obj] + ["0x" + o for o in offs],
+                                 capture_output=True, text=True).stdout.splitlines()
+            cur = None
+            for ln in out:
+                if ln.startswith("0x"):
+                    cur = obj + ":" + ("%x" % int(ln, 16))
+                    first = True
+                    continue
+                if cur and first:
+                    loc[ln.rsplit("/", 1)[-1]] += len(pcs.get(cur, []))
+                    first = False
+        for k, v in loc.most_common(top):
+            print("%6d  %s" % (v, k))
+        return
     if callers:
         chains = collections.Counter()
         for s in samples:
