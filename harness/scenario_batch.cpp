@@ -309,126 +309,186 @@ void for_streams(Shared& sh, size_t count, const F& fn)
     });
 }
 
-int run_once(Shared& sh, StreamResult* results, uint64_t* rounds, double* phase)
+// One job = one contiguous group of a step's streams.  Jobs flow through a
+// pipeline so that the host work of one job overlaps the device work of the
+// previous flush: every iteration advances the jobs whose device work has
+// completed (round two and later: deliveries after a decode), starts the next
+// job (round one: adds, encodes, decodes), and submits.  sgpu_submit()
+// completes the previous flush before launching the new one, so work queued
+// before submit k is final once submit k+1 has returned.
+struct Job
+{
+    unsigned step = 0, begin = 0, end = 0;
+    std::vector<BatchCodec> codecs;
+    std::unique_ptr<BatchStream[]> streams;
+    std::vector<unsigned> live;     // indices into codecs/streams
+    uint64_t readyAfter = 0;        // submits after which its device work is final
+};
+
+int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* rounds,
+                 double* phase)
 {
     const Api& api = *sh.api;
     const ScenarioConfig* cfg = sh.cfg;
     const unsigned n = cfg->streams;
+    const unsigned G = std::max(1u, std::min(sh.groups, n));
     auto t = Clock::now();
+    // SCENARIO_TIMELINE=1: one stderr line per phase (debugging aid)
+    static const bool timeline = std::getenv("SCENARIO_TIMELINE") != nullptr;
+    const auto t00 = t;
+    int curJob = -1;
     auto lap = [&](int k) {
         const auto now = Clock::now();
         phase[k] += std::chrono::duration<double>(now - t).count();
+        if (timeline)
+            std::fprintf(stderr, "tl %8.3f %8.3f ms  %s j%d\n",
+                         std::chrono::duration<double>(t - t00).count() * 1e3,
+                         std::chrono::duration<double>(now - t).count() * 1e3,
+                         k == 0 ? "create" : k == 1 ? "step" : k == 2 ? "flush" : k == 3 ? "resolve" : "finish",
+                         curJob);
         t = now;
     };
-    if (sh.e2e && api.h2d(sh.devBase, sh.hostPayload, sh.payloadBytes) != 0)
-        return -3;   // the originals arrive in (pinned) host memory
-    std::vector<BatchCodec> codecs(n);
-    std::unique_ptr<BatchStream[]> streams(new BatchStream[n]);
-    for_streams(sh, n, [&](size_t s) {
-        codecs[s].sh = &sh;
-        codecs[s].enc = api.encoder_create();
-        codecs[s].dec = api.decoder_create();
-        codecs[s].log = &streams[s].log;
-        // the event log only feeds digests: timed bench steps run without it
-        streams[s].logOn = sh.verify || sh.hashData || sh.digest;
-        streams[s].init(cfg, &codecs[s], &results[s], cfg->first_stream + (unsigned)s);
-        if (!codecs[s].enc || !codecs[s].dec)
-            streams[s].fail(2);
-    });
-    lap(0);
-    // Streams are split into `groups` contiguous groups.  With one group a
-    // round is: step every live stream, then flush and wait.  With two, the
-    // groups alternate: a group's flush is submitted without waiting and
-    // the other group's host work runs while it executes on the device; the
-    // next submit completes it first (sgpu_submit semantics), before that
-    // group steps again.
-    const unsigned G = std::max(1u, std::min(sh.groups, n));
-    auto group_begin = [&](unsigned g) { return (unsigned)((uint64_t)n * g / G); };
-    // requests of group g's streams that wait for device bytes
-    auto take = [&](unsigned g, bool prev) {
+    auto take = [](Job& J, bool prev) {
         std::vector<Request> reqs;
-        for (unsigned s = group_begin(g); s < group_begin(g + 1); ++s) {
-            std::vector<Request>& q = prev ? codecs[s].prev : codecs[s].cur;
+        for (BatchCodec& c : J.codecs) {
+            std::vector<Request>& q = prev ? c.prev : c.cur;
             reqs.insert(reqs.end(), q.begin(), q.end());
             q.clear();
         }
         return reqs;
     };
-    std::vector<std::vector<unsigned>> live(G);
-    for (unsigned g = 0; g < G; ++g)
-        for (unsigned s = group_begin(g); s < group_begin(g + 1); ++s)
-            live[g].push_back(s);
-    int rc = 0;
-    int inflight = -1;   // group whose flush was submitted last and may still run
-    for (bool any = true; any && rc == 0;) {
-        any = false;
-        for (unsigned g = 0; g < G && rc == 0; ++g) {
-            std::vector<unsigned>& lv = live[g];
-            if (lv.empty())
-                continue;
-            any = true;
-            if (inflight == (int)g) {
-                // no other group submitted since: complete this group's flush
-                if (api.flush() != 0)
-                    rc = -3;
-                inflight = -1;
-                lap(2);
+    // advance every live stream of J until it yields; finished streams free
+    // their codecs right away (their state is still hot); digests wait for
+    // the job's last device bytes (retirement)
+    auto advance = [&](Job& J) {
+        for_streams(sh, J.live.size(), [&](size_t k) {
+            const unsigned i = J.live[k];
+            BatchStream& st = J.streams[i];
+            while (!st.done())
+                if (st.step())
+                    break;
+            // (a stream with device bytes still to read keeps its codecs, and
+            // so its buffers, until the job retires)
+            BatchCodec& c = J.codecs[i];
+            if (st.done() && c.cur.empty() && c.prev.empty()) {
+                api.encoder_free(c.enc);
+                api.decoder_free(c.dec);
+                c.enc = nullptr;
+                c.dec = nullptr;
             }
-            // Every live stream advances until it yields; streams are
-            // independent, so the host threads drive them concurrently.
-            for_streams(sh, lv.size(), [&](size_t k) {
-                BatchStream& st = streams[lv[k]];
-                while (!st.done())
-                    if (st.step())
-                        break;
-            });
-            lap(1);
-            // bytes produced by this group's previous flush are final now
-            std::vector<Request> reqs = take(g, true);
+        });
+        J.live.erase(std::remove_if(J.live.begin(), J.live.end(),
+                                    [&](unsigned i) { return J.streams[i].done(); }),
+                     J.live.end());
+        for (BatchCodec& c : J.codecs)
+            std::swap(c.prev, c.cur);
+    };
+    auto dump = [&](Job& J) {
+        // debugging aid: SCENARIO_DUMP="<stream index>:<path>" writes that
+        // stream's event log (same format as scenario_run_capi's)
+        const char* d = std::getenv("SCENARIO_DUMP");
+        if (!d || J.step + 1 != nsteps)
+            return;
+        const unsigned idx = (unsigned)std::strtoul(d, nullptr, 10);
+        const char* path = std::strchr(d, ':');
+        if (path && idx >= J.begin && idx < J.end)
+            if (FILE* f = std::fopen(path + 1, "w")) {
+                for (uint64_t e : J.streams[idx - J.begin].log)
+                    std::fprintf(f, "%016llx\n", (unsigned long long)e);
+                std::fclose(f);
+            }
+    };
+
+    const unsigned jobs = nsteps * G;
+    std::vector<std::unique_ptr<Job>> active;
+    uint64_t seq = 0;
+    unsigned next = 0;
+    int rc = 0;
+    while (rc == 0 && (next < jobs || !active.empty())) {
+        // 1. jobs whose device work is final: resolve, advance, retire
+        for (auto& jp : active) {
+            Job& J = *jp;
+            if (seq < J.readyAfter)
+                continue;
+            curJob = (int)(J.step * G + J.begin);
+            std::vector<Request> reqs = take(J, true);
             resolve_requests(sh, reqs);
             lap(3);
-            if ((G == 1 ? api.flush() : api.submit()) != 0)
-                rc = -3;
-            inflight = G == 1 ? -1 : (int)g;
-            lap(2);
-            ++*rounds;
-            for (unsigned s = group_begin(g); s < group_begin(g + 1); ++s)
-                std::swap(codecs[s].prev, codecs[s].cur);
-            lv.erase(std::remove_if(lv.begin(), lv.end(),
-                                    [&](unsigned s) { return streams[s].done(); }),
-                     lv.end());
+            if (!J.live.empty()) {
+                advance(J);
+                J.readyAfter = seq + 2;
+                lap(1);
+            }
         }
+        for (size_t k = 0; k < active.size();) {
+            Job& J = *active[k];
+            if (J.live.empty() && seq >= J.readyAfter) {
+                std::vector<Request> reqs = take(J, true);
+                resolve_requests(sh, reqs);
+                reqs = take(J, false);
+                resolve_requests(sh, reqs);
+                for_streams(sh, J.end - J.begin, [&](size_t i) {
+                    J.streams[i].finish();
+                    api.encoder_free(J.codecs[i].enc);   // (null if freed already)
+                    api.decoder_free(J.codecs[i].dec);
+                    J.codecs[i].enc = nullptr;
+                    J.codecs[i].dec = nullptr;
+                });
+                dump(J);
+                active.erase(active.begin() + (long)k);
+                lap(4);
+            } else {
+                ++k;
+            }
+        }
+        // 2. start the next job (round one) while the pipeline is shallow
+        if (next < jobs && active.size() < 3) {
+            std::unique_ptr<Job> jp(new Job);
+            Job& J = *jp;
+            J.step = next / G;
+            const unsigned g = next % G;
+            J.begin = (unsigned)((uint64_t)n * g / G);
+            J.end = (unsigned)((uint64_t)n * (g + 1) / G);
+            curJob = (int)next;
+            ++next;
+            // the originals arrive in (pinned) host memory with each step
+            if (sh.e2e && g == 0 && api.h2d(sh.devBase, sh.hostPayload, sh.payloadBytes) != 0) {
+                rc = -3;
+                break;
+            }
+            const unsigned cnt = J.end - J.begin;
+            J.codecs.resize(cnt);
+            J.streams.reset(new BatchStream[cnt]);
+            for_streams(sh, cnt, [&](size_t i) {
+                BatchCodec& c = J.codecs[i];
+                c.sh = &sh;
+                c.enc = api.encoder_create();
+                c.dec = api.decoder_create();
+                c.log = &J.streams[i].log;
+                // the event log only feeds digests: timed bench steps run without it
+                J.streams[i].logOn = sh.verify || sh.hashData || sh.digest;
+                J.streams[i].init(cfg, &c, &results[J.begin + i], cfg->first_stream + J.begin + (unsigned)i);
+                if (!c.enc || !c.dec)
+                    J.streams[i].fail(2);
+            });
+            for (unsigned i = 0; i < cnt; ++i)
+                J.live.push_back(i);
+            lap(0);
+            advance(J);
+            J.readyAfter = seq + 2;
+            lap(1);
+            active.push_back(std::move(jp));
+        }
+        // 3. launch what the jobs queued (completing the previous flush first)
+        if (api.submit() != 0)
+            rc = -3;
+        ++seq;
+        ++*rounds;
+        lap(2);
     }
     if (api.flush() != 0)
         rc = -3;
     lap(2);
-    for (unsigned g = 0; g < G; ++g) {
-        std::vector<Request> reqs = take(g, true);
-        resolve_requests(sh, reqs);
-        reqs = take(g, false);
-        resolve_requests(sh, reqs);
-    }
-    lap(3);
-    for_streams(sh, n, [&](size_t s) {
-        streams[s].finish();
-        api.encoder_free(codecs[s].enc);
-        api.decoder_free(codecs[s].dec);
-    });
-    // debugging aid: SCENARIO_DUMP="<stream index>:<path>" writes that
-    // stream's event log (same format as scenario_run_capi's)
-    if (const char* dump = std::getenv("SCENARIO_DUMP")) {
-        const unsigned idx = (unsigned)std::strtoul(dump, nullptr, 10);
-        const char* path = std::strchr(dump, ':');
-        if (path && idx < n) {
-            if (FILE* f = std::fopen(path + 1, "w")) {
-                for (uint64_t e : streams[idx].log)
-                    std::fprintf(f, "%016llx\n", (unsigned long long)e);
-                std::fclose(f);
-            }
-        }
-    }
-    api.flush();
-    lap(4);
     return rc;
 }
 
@@ -530,8 +590,11 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         }
     }
     int rc = 0;
-    const unsigned runs = opt->warmup + opt->steps;
-    for (unsigned r = 0; r < runs && rc == 0; ++r) {
+    // warm-up runs one at a time (the first may verify every byte); then all
+    // timed steps as one pipeline, so one step's device tail overlaps the
+    // next step's host work
+    const unsigned passes = opt->warmup + (opt->steps ? 1 : 0);
+    for (unsigned r = 0; r < passes && rc == 0; ++r) {
         const bool timed = r >= opt->warmup;
         sh.verify = opt->verify && r == 0;
         sh.digest = opt->digest != 0;
@@ -546,7 +609,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         e0[kEngineStats] = api.arena_bytes();
         api.timing(timed ? 1 : 0, 1, nullptr, nullptr);
         const auto t1 = Clock::now();
-        rc = run_once(sh, results, &rounds, phase);
+        rc = run_pipeline(sh, results, timed ? opt->steps : 1, &rounds, phase);
         const double dt = std::chrono::duration<double>(Clock::now() - t1).count();
         double execMs = 0, totalMs = 0;
         api.timing(0, 1, &execMs, &totalMs);
