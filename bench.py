@@ -266,7 +266,7 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_cuda = args.library == S.AMD_LIB
+    use_cuda = os.path.basename(args.library).startswith("libsiamese_amd")
     line = run_rank(rank, world, local, args, args.library, use_cuda)
     if line is not None:
         print(json.dumps(line), flush=True)

@@ -891,9 +891,9 @@ bool DecoderCore::matrix_resize(unsigned rows, unsigned columns, bool initialize
     if (initialize) {
         matAllocRows_ = rows + 4;
         matStride_ = stride;
-        mat_.resize((size_t)matAllocRows_ * matStride_);
+        mat_.resize((size_t)matAllocRows_ * matStride_ + kRowSlack);
     } else if (!(rows <= matAllocRows_ && columns <= matStride_)) {
-        std::vector<uint8_t> nm((size_t)(rows + 4) * stride);
+        std::vector<uint8_t> nm((size_t)(rows + 4) * stride + kRowSlack);
         const unsigned copy = std::min(matCols_, columns);
         if (matCols_ > 0)
             for (unsigned i = 0; i < matRows_; ++i)
@@ -912,6 +912,9 @@ void DecoderCore::populate_columns(unsigned oldColumns, unsigned newColumns)
     if (oldColumns >= newColumns)
         return;
     cols_.resize(newColumns);
+    colLane_.resize(newColumns + kRowSlack);
+    colCx_.resize(newColumns + kRowSlack);
+    colCx2_.resize(newColumns + kRowSlack);
     unsigned elementStart = prevNextCheckStart_;
     prevNextCheckStart_ = region_.nextCheckStart;
     const unsigned elementEnd = region_.nextCheckStart;
@@ -935,6 +938,9 @@ void DecoderCore::populate_columns(unsigned oldColumns, unsigned newColumns)
                 const uint8_t cx2 = gf_sqr(c.cx);
                 for (unsigned k = 0; k < 8; ++k)
                     c.comb[k] = (uint8_t)((k & 1) ^ ((k & 2) ? c.cx : 0) ^ ((k & 4) ? cx2 : 0));
+                colLane_[column] = (uint8_t)(c.column % kLanes);
+                colCx_[column] = c.cx;
+                colCx2_[column] = cx2;
                 c.original->column = column; // lost slot -> matrix column
                 if (++column >= newColumns)
                     return;
@@ -998,19 +1004,20 @@ bool DecoderCore::generate_matrix()
         // select {1, CX, CX^2} for the row sum, the high three the same for
         // the product, which is scaled by RX:  v = comb[op&7] ^ RX*comb[op>>3]
         const uint8_t rx = row_value(m.row);
-        const uint8_t* mulRx = g_gf.mul[rx];
-        unsigned opcodes[kLanes];
-        for (unsigned lane = 0; lane < kLanes; ++lane)
-            opcodes[lane] = row_opcode(lane, m.row);
-        for (unsigned j = startCol; j < columns; ++j) {
-            const ColInfo& c = cols_[j];
-            if (column_sub(c.column, m.columnStart) >= m.sumCount) {
-                std::memset(row + j, 0, columns - j);
-                break;
-            }
-            const unsigned op = opcodes[c.column % kLanes];
-            row[j] = (uint8_t)(c.comb[op & 7] ^ mulRx[c.comb[op >> 3]]);
+        uint8_t opLo[kLanes], opHi[kLanes];
+        for (unsigned lane = 0; lane < kLanes; ++lane) {
+            const unsigned op = row_opcode(lane, m.row);
+            opLo[lane] = (uint8_t)(op & 7);
+            opHi[lane] = (uint8_t)(op >> 3);
         }
+        unsigned jEnd = startCol;
+        while (jEnd < columns && column_sub(cols_[jEnd].column, m.columnStart) < m.sumCount)
+            ++jEnd;
+        if (jEnd > startCol)
+            gf_dense_row(row + startCol, colLane_.data() + startCol, colCx_.data() + startCol,
+                         colCx2_.data() + startCol, opLo, opHi, rx, jEnd - startCol);
+        if (jEnd < columns)
+            std::memset(row + jEnd, 0, columns - jEnd);
 
         // Sparse columns that landed on lost data
         unsigned picks = 0;

@@ -230,6 +230,10 @@ private:
     };
     std::vector<RowInfo> rows_;
     std::vector<ColInfo> cols_;
+    // per matrix column, for the vector row builder (gf_dense_row): lane,
+    // CX and CX^2, each padded by kRowSlack bytes
+    static constexpr unsigned kRowSlack = 32;
+    std::vector<uint8_t> colLane_, colCx_, colCx2_;
     unsigned prevNextCheckStart_ = 0;
     std::vector<uint8_t> mat_;
     unsigned matRows_ = 0, matCols_ = 0, matAllocRows_ = 0, matStride_ = 0;

@@ -64,35 +64,74 @@ bool gf_init()
     return true;
 }
 
+namespace {
+
+// bytes [0, k) of a 32-byte vector selected (k in 1..32)
+inline __m256i head_mask(unsigned k)
+{
+    const __m256i iota = _mm256_setr_epi8(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17,
+                                          18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31);
+    return _mm256_cmpgt_epi8(_mm256_set1_epi8((char)k), iota);
+}
+
+inline __m256i gf_mul32(__m256i x, __m256i tlo, __m256i thi)
+{
+    const __m256i m0f = _mm256_set1_epi8(0x0f);
+    const __m256i lo = _mm256_and_si256(x, m0f);
+    const __m256i hi = _mm256_and_si256(_mm256_srli_epi64(x, 4), m0f);
+    return _mm256_xor_si256(_mm256_shuffle_epi8(tlo, lo), _mm256_shuffle_epi8(thi, hi));
+}
+
+} // namespace
+
 void gf_muladd_row(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n)
 {
     if (y == 0 || n == 0)
         return;
-    unsigned i = 0;
-    if (y == 1) {
-        for (; i + 32 <= n; i += 32) {
-            __m256i a = _mm256_loadu_si256((const __m256i*)(dst + i));
-            __m256i b = _mm256_loadu_si256((const __m256i*)(src + i));
-            _mm256_storeu_si256((__m256i*)(dst + i), _mm256_xor_si256(a, b));
-        }
-        for (; i < n; ++i)
-            dst[i] ^= src[i];
-        return;
-    }
     const __m256i tlo = _mm256_broadcastsi128_si256(_mm_load_si128((const __m128i*)g_gf.nib_lo[y]));
     const __m256i thi = _mm256_broadcastsi128_si256(_mm_load_si128((const __m128i*)g_gf.nib_hi[y]));
-    const __m256i m0f = _mm256_set1_epi8(0x0f);
-    for (; i + 32 <= n; i += 32) {
-        __m256i x = _mm256_loadu_si256((const __m256i*)(src + i));
-        __m256i lo = _mm256_and_si256(x, m0f);
-        __m256i hi = _mm256_and_si256(_mm256_srli_epi64(x, 4), m0f);
-        __m256i p = _mm256_xor_si256(_mm256_shuffle_epi8(tlo, lo), _mm256_shuffle_epi8(thi, hi));
-        __m256i d = _mm256_loadu_si256((const __m256i*)(dst + i));
-        _mm256_storeu_si256((__m256i*)(dst + i), _mm256_xor_si256(d, p));
+    for (unsigned i = 0; i < n; i += 32) {
+        const __m256i x = _mm256_loadu_si256((const __m256i*)(src + i));
+        const __m256i d = _mm256_loadu_si256((const __m256i*)(dst + i));
+        const __m256i p = y == 1 ? x : gf_mul32(x, tlo, thi);
+        __m256i r = _mm256_xor_si256(d, p);
+        if (n - i < 32)
+            r = _mm256_blendv_epi8(d, r, head_mask(n - i));
+        _mm256_storeu_si256((__m256i*)(dst + i), r);
     }
-    const uint8_t* row = g_gf.mul[y];
-    for (; i < n; ++i)
-        dst[i] ^= row[src[i]];
+}
+
+void gf_dense_row(uint8_t* out, const uint8_t* lane, const uint8_t* cx, const uint8_t* cx2,
+                  const uint8_t opLo[8], const uint8_t opHi[8], uint8_t rx, unsigned n)
+{
+    uint8_t lo16[16] = {0}, hi16[16] = {0};
+    for (unsigned l = 0; l < 8; ++l) {
+        lo16[l] = opLo[l];
+        hi16[l] = opHi[l];
+    }
+    const __m256i tLo = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)lo16));
+    const __m256i tHi = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)hi16));
+    const __m256i rlo = _mm256_broadcastsi128_si256(_mm_load_si128((const __m128i*)g_gf.nib_lo[rx]));
+    const __m256i rhi = _mm256_broadcastsi128_si256(_mm_load_si128((const __m128i*)g_gf.nib_hi[rx]));
+    const __m256i one = _mm256_set1_epi8(1), two = _mm256_set1_epi8(2), four = _mm256_set1_epi8(4);
+    // comb(k) for the selector vector k
+    auto comb = [&](__m256i k, __m256i c1, __m256i c2) {
+        const __m256i b0 = _mm256_and_si256(k, one);
+        const __m256i b1 = _mm256_cmpeq_epi8(_mm256_and_si256(k, two), two);
+        const __m256i b2 = _mm256_cmpeq_epi8(_mm256_and_si256(k, four), four);
+        return _mm256_xor_si256(b0, _mm256_xor_si256(_mm256_and_si256(b1, c1), _mm256_and_si256(b2, c2)));
+    };
+    for (unsigned j = 0; j < n; j += 32) {
+        const __m256i L = _mm256_loadu_si256((const __m256i*)(lane + j));
+        const __m256i c1 = _mm256_loadu_si256((const __m256i*)(cx + j));
+        const __m256i c2 = _mm256_loadu_si256((const __m256i*)(cx2 + j));
+        const __m256i v = _mm256_xor_si256(comb(_mm256_shuffle_epi8(tLo, L), c1, c2),
+                                           gf_mul32(comb(_mm256_shuffle_epi8(tHi, L), c1, c2), rlo, rhi));
+        __m256i r = v;
+        if (n - j < 32)
+            r = _mm256_blendv_epi8(_mm256_loadu_si256((const __m256i*)(out + j)), v, head_mask(n - j));
+        _mm256_storeu_si256((__m256i*)(out + j), r);
+    }
 }
 
 } // namespace sgpu

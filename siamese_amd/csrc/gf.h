@@ -34,6 +34,17 @@ inline uint8_t gf_sqr(uint8_t x) { return g_gf.sqr[x]; }
 inline uint8_t gf_div(uint8_t x, uint8_t y) { return y ? g_gf.mul[g_gf.inv[y]][x] : 0; }
 
 /// dst[i] ^= y * src[i] for i < n (host rows of the coefficient matrix).
+/// The tail is done with a blended 32-byte vector, so both buffers must stay
+/// readable and dst writable up to 31 bytes past n (bytes there are
+/// rewritten unchanged).
 void gf_muladd_row(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n);
+
+/// Dense Siamese coefficients of one recovery row for `n` lost columns
+/// (reference SiameseDecoder.cpp:2278-2300): out[j] = comb(opLo[lane[j]]) ^
+/// RX * comb(opHi[lane[j]]) with comb(k) = (k&1) ^ (k&2 ? cx[j] : 0) ^
+/// (k&4 ? cx2[j] : 0).  opLo/opHi: the row's opcode bits 0-2 / 3-5 per lane.
+/// All arrays readable (out writable, rewritten unchanged) 31 bytes past n.
+void gf_dense_row(uint8_t* out, const uint8_t* lane, const uint8_t* cx, const uint8_t* cx2,
+                  const uint8_t opLo[8], const uint8_t opHi[8], uint8_t rx, unsigned n);
 
 } // namespace sgpu
