@@ -863,11 +863,14 @@ SiameseResult DecoderCore::decode(SiameseOriginalPacket** packetsOut, unsigned* 
 
 SiameseResult DecoderCore::decode_region()
 {
+    geBytes_ = 0;   // (generate_matrix may resume an elimination)
     if (!generate_matrix()) {
         disabled_ = true;
         return Siamese_Disabled;
     }
-    if (!gaussian_elimination()) {
+    const bool solved = gaussian_elimination();
+    eng_->account(geBytes_);
+    if (!solved) {
         region_.solveFailed = true;
         stats_[SiameseDecoderStats_SolveFailCount]++;
         return Siamese_NeedMoreData;
@@ -1047,8 +1050,10 @@ bool DecoderCore::eliminate_row(const uint8_t* geRow, uint8_t* remRow, unsigned 
         return false;
     const uint8_t y = gf_div(valJ, valI);
     remRow[pivot] = y;
-    if (end > pivot + 1)
+    if (end > pivot + 1) {
         gf_muladd_row(remRow + pivot + 1, geRow + pivot + 1, y, end - pivot - 1);
+        geBytes_ += end - pivot - 1;   // the reference's MulAddRows muladd (:504-520)
+    }
     return true;
 }
 

@@ -239,6 +239,7 @@ private:
     unsigned matRows_ = 0, matCols_ = 0, matAllocRows_ = 0, matStride_ = 0;
     std::vector<unsigned> pivots_;
     unsigned geResume_ = 0;
+    uint64_t geBytes_ = 0;   // coefficient bytes the elimination multiplied (accounting)
 
     unsigned latestColumn_ = 0;
 
