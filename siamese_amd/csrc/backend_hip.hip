@@ -380,7 +380,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         const uint32_t n = uni(h0.z), valid = uni(h0.w);
         const uint32_t kind = uni(h1.x);
         uint32_t itemWords = kOpWords;
-        if (kind == OP_LINCOMB || kind == OP_ROWS)
+        if (kind == OP_LINCOMB || kind == OP_ROWS || kind == OP_COPIES)
             itemWords += uni(h1.w);
         const uint32_t next = pos + itemWords;
         // prefetch the next op's block while this one runs
@@ -556,6 +556,38 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 }
                 store_literal(p, rdst, rn, litLen, lit);
                 store_literal(p1, rdst, rn, litLen, lit);
+            }
+        } else if (kind == OP_COPIES) {
+            // kCopyBatch copies per wave at a time, all their loads in flight
+            // before the first store; sources carry their zero tails
+            constexpr unsigned kCopyBatch = 4;
+            for (uint32_t c0 = wave * kCopyBatch; c0 < n; c0 += kExecWaves * kCopyBatch) {
+                uint64_t d[kCopyBatch];
+                uint32_t l[kCopyBatch];
+                uint4 v0[kCopyBatch], v1[kCopyBatch];
+#pragma unroll
+                for (unsigned u = 0; u < kCopyBatch; ++u) {
+                    l[u] = 0;
+                    if (c0 + u < n) {
+                        const uint4 w0 = op_word(rb, seg, pos, kOpWords + (c0 + u) * kCopyWords);
+                        const uint4 w1 = op_word(rb, seg, pos, kOpWords + (c0 + u) * kCopyWords + 1);
+                        d[u] = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                        const uint64_t s = ((uint64_t)uni(w0.w) << 32) | uni(w0.z);
+                        l[u] = uni(w1.x);
+                        if (tileBase < l[u]) {
+                            v0[u] = ld16(s + (p < l[u] ? p : 0));
+                            if (tileBase + kChunk < l[u])
+                                v1[u] = ld16(s + (p1 < l[u] ? p1 : 0));
+                        }
+                    }
+                }
+#pragma unroll
+                for (unsigned u = 0; u < kCopyBatch; ++u) {
+                    if (p < l[u])
+                        st16(d[u] + p, p + 16 > l[u] ? mask16(v0[u], (int)l[u] - (int)p) : v0[u]);
+                    if (p1 < l[u])
+                        st16(d[u] + p1, p1 + 16 > l[u] ? mask16(v1[u], (int)l[u] - (int)p1) : v1[u]);
+                }
             }
         }
         ring[cur ^ 1][tid] = pf;

@@ -649,11 +649,10 @@ SiameseResult DecoderCore::add_recovery_common(const RowMeta& m, int footer, uns
         // A device-resident packet may have been encoded in this very flush:
         // copy it with an op of this (group-1) program, which runs after
         // every encoder op of the flush.  Encoders give each packet a fresh
-        // buffer, so nothing overwrites it before the copy.
+        // buffer, so nothing overwrites it before the copy, and this program
+        // never writes it, so the copy can share a batch with others.
         (void)producer;
-        prog_.lc_begin(r->buf.addr(), payload, 0);
-        prog_.lc_term(devData, payload, 1);
-        prog_.lc_end();
+        prog_.copy(r->buf.addr(), devData, payload);
     }
     r->bytes = payload;
     r->meta = m;
@@ -691,9 +690,7 @@ bool DecoderCore::add_single(const RowMeta& m, const uint8_t* headBytes, unsigne
     else if ((unsigned)headerBytes == h) {
         // Same byte alignment: a copy op of this program (see add_recovery_common)
         (void)producer;
-        prog_.lc_begin(s.buf.addr(), h + length, 0);
-        prog_.lc_term(devData, h + length, 1);
-        prog_.lc_end();
+        prog_.copy(s.buf.addr(), devData, h + length);
     } else
         prog_.ingest_device(s.buf, devData + headerBytes, length, hdr, h);
     if (mirror_) {

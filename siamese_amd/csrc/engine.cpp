@@ -388,8 +388,45 @@ void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t 
         b.maxExtent = n + litLen;
 }
 
+void Program::copy(uint64_t dst, uint64_t src, uint32_t len)
+{
+    if (len == 0)
+        return;
+    touch();
+    if (copies_.empty()) {
+        rows_close();
+        if (nsegs_ == 0)
+            new_segment();
+    }
+    CopyItem c;
+    std::memset(&c, 0, sizeof(c));
+    c.dst = dst;
+    c.src = src;
+    c.len = len;
+    copies_.push_back(c);
+    Segment& g = segs_[nsegs_ - 1];
+    if (len > g.maxExtent)
+        g.maxExtent = len;
+}
+
 void Program::rows_close()
 {
+    if (!copies_.empty()) {
+        // seal the open copy batch
+        Segment& g = segs_[nsegs_ - 1];
+        GfOp op;
+        std::memset(&op, 0, sizeof(op));
+        op.kind = OP_COPIES;
+        op.n = (uint32_t)copies_.size();
+        op.termBegin = (uint32_t)(g.rowsData.size() / 16);
+        op.termCount = (uint32_t)copies_.size() * kCopyWords;
+        g.ops.push_back(op);
+        const size_t at = g.rowsData.size();
+        g.rowsData.resize(at + copies_.size() * sizeof(CopyItem));
+        std::memcpy(g.rowsData.data() + at, copies_.data(), copies_.size() * sizeof(CopyItem));
+        g.rowsWords += op.termCount;
+        copies_.clear();
+    }
     RowsBuild& b = rb_;
     if (!b.open)
         return;
@@ -879,7 +916,7 @@ void Engine::flush()
             const Program::Segment& s = r.prog->segs_[r.seg];
             uint8_t* w = up + oStream + (size_t)r.wordBase * 16;
             for (const GfOp& op : s.ops) {
-                if (op.kind == OP_ROWS) {
+                if (op.kind == OP_ROWS || op.kind == OP_COPIES) {
                     std::memcpy(w, &op, sizeof(GfOp));
                     w += sizeof(GfOp);
                     const size_t bytes = (size_t)op.termCount * 16;   // block (rows_close)

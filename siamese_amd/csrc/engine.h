@@ -116,6 +116,11 @@ public:
     /// Close the open batch (its window may change after this).
     void rows_seal() { rows_close(); }
 
+    /// dst[0,len) = src[0,len) (zero tail), one of a batch of independent
+    /// copies (OP_COPIES): the destinations are fresh buffers no other op of
+    /// the batch touches.
+    void copy(uint64_t dst, uint64_t src, uint32_t len);
+
     bool empty() const { return nsegs_ == 0 || (nsegs_ == 1 && segs_[0].ops.empty()); }
 
 private:
@@ -142,8 +147,9 @@ private:
         std::vector<RowItem> rows;
         uint32_t maxExtent = 0;
     };
-    void rows_close();
+    void rows_close();   // closes the open OP_ROWS or OP_COPIES batch
     void rows_open(uint32_t base, bool keepWindow);
+    std::vector<CopyItem> copies_;   // the open OP_COPIES batch (segment's last op)
     // The containers of programs that went away are kept per host thread and
     // handed to new programs, so a fresh codec starts with warm capacity.
     struct Store

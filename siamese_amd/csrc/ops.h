@@ -32,6 +32,7 @@ enum GfOpKind : uint32_t
     OP_LINCOMB = 1,   // dst[0,n) = keep(dst,valid) ^ acc0 ^ mix*acc1
     OP_LITERAL = 2,   // dst[n, n+valid) = literal bytes (<= 8)
     OP_ROWS = 3,      // a batch of Siamese rows of one codec (sum updates, rows)
+    OP_COPIES = 4,    // independent copies dst[0,len) = src[0,len)
 };
 
 /// One op.  For OP_LINCOMB:
@@ -129,13 +130,29 @@ constexpr unsigned kRowSums = 24;                       // kLanes * kSums
 constexpr unsigned kUpdateWords = sizeof(SumUpdate) / 16;
 constexpr unsigned kRowWords = sizeof(RowItem) / 16;
 
+/// OP_COPIES: n independent copies (the decoder taking in recovery packets,
+/// reference SiameseDecoder.cpp:437), one CopyItem word pair each after the
+/// GfOp header (termCount = 2n).  dst[0,len) = src[0,len) with the zero tail
+/// of every write; copies of one batch never overlap, so the executor deals
+/// them to its waves without barriers.
+struct CopyItem
+{
+    uint64_t dst;
+    uint64_t src;
+    uint32_t len;
+    uint32_t pad[3];
+};
+static_assert(sizeof(CopyItem) == 32, "CopyItem layout");
+constexpr unsigned kCopyWords = sizeof(CopyItem) / 16;
+
 /// PCG-XSH-RR as the reference seeds it (SiameseTools.h:80-102).
 constexpr uint64_t kPcgMul = 6364136223846793005ULL;
 
 inline uint32_t op_words(const GfOp& op)
 {
     // (an OP_ROWS header's termCount is its whole block in words)
-    return kOpWords + ((op.kind == OP_LINCOMB || op.kind == OP_ROWS) ? op.termCount : 0);
+    return kOpWords +
+           ((op.kind == OP_LINCOMB || op.kind == OP_ROWS || op.kind == OP_COPIES) ? op.termCount : 0);
 }
 
 /// Executor work item: one (instance segment, byte tile).

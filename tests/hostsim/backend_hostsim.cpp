@@ -172,6 +172,17 @@ void exec_tile(const uint8_t* stream, const ExecItem& it, uint64_t* acct)
             lincomb_tile(op.dst, op.n, op.valid, op.mix, terms, t0);
             continue;
         }
+        if (op.kind == OP_COPIES) {
+            const CopyItem* cs = reinterpret_cast<const CopyItem*>(body);
+            if (reinterpret_cast<const uint8_t*>(cs + op.n) != w)
+                std::abort(); // malformed block
+            for (uint32_t c = 0; c < op.n; ++c) {
+                const uint32_t end16 = (cs[c].len + 15) & ~15u;
+                for (uint32_t b = t0; b < t0 + kExecTileBytes && b < end16; ++b)
+                    P(cs[c].dst)[b] = b < cs[c].len ? P(cs[c].src)[b] : 0;
+            }
+            continue;
+        }
         if (op.kind != OP_ROWS)
             std::abort();
         // OP_ROWS (ops.h): sums, window, sum updates, rows
