@@ -559,7 +559,8 @@ size_t cap_class(uint32_t cap)
 namespace {
 constexpr size_t kChunkBytes = 64u << 20;    // one hipMalloc
 constexpr size_t kRegionBytes = 4u << 20;    // a shard's bump region
-constexpr size_t kMagazine = 64;             // buffers moved per depot transfer
+constexpr size_t kMagazine = 512;            // buffers moved per depot transfer
+constexpr size_t kKeepFree = 8 * kMagazine;  // free buffers of a class a shard keeps through a reclaim
 constexpr size_t kRefillBytes = 1u << 20;    // bytes carved per refill
 } // namespace
 
@@ -590,10 +591,11 @@ bool Engine::refill(Shard& s, size_t cls, uint32_t cap)
     std::vector<uint8_t*>& list = s.freeLists[cls];
     {
         std::lock_guard<std::mutex> g(depotMu_);
-        if (cls < depot_.size() && depot_[cls].size() >= kMagazine) {
+        if (cls < depot_.size() && !depot_[cls].empty()) {
             std::vector<uint8_t*>& d = depot_[cls];
-            list.insert(list.end(), d.end() - kMagazine, d.end());
-            d.resize(d.size() - kMagazine);
+            const size_t take = std::min(kMagazine, d.size());
+            list.insert(list.end(), d.end() - take, d.end());
+            d.resize(d.size() - take);
             return true;
         }
     }
@@ -627,9 +629,9 @@ void Engine::spill(Shard& s)
 {
     for (size_t cls = 0; cls < s.freeLists.size(); ++cls) {
         std::vector<uint8_t*>& list = s.freeLists[cls];
-        if (list.size() <= 2 * kMagazine)
+        if (list.size() <= kKeepFree + kMagazine)
             continue;
-        const size_t keep = kMagazine;
+        const size_t keep = kKeepFree;
         std::lock_guard<std::mutex> g(depotMu_);
         if (cls >= depot_.size())
             depot_.resize(cls + 1);
