@@ -187,7 +187,10 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
 // The barrier that rotates the ring also orders each op's stores before any
 // later op of the segment reads them (stores from one CU are visible to the
 // CU's other waves after the workgroup-scope fence of __syncthreads).
-constexpr unsigned kExecWaves = 4;
+#ifndef SGPU_EXEC_WAVES
+#define SGPU_EXEC_WAVES 8
+#endif
+constexpr unsigned kExecWaves = SGPU_EXEC_WAVES;   // 8 measured best of 4/8/16 (16 spills)
 constexpr unsigned kExecThreads = 64 * kExecWaves;
 constexpr unsigned kExecDepth = 8;
 constexpr unsigned kExecSolo = 4;            // ops with <= this many terms run on wave 0 alone
