@@ -721,9 +721,12 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 // Global path (larger m): wave 0 alone, rows updated in place in HBM.
 //
 // The staged rows take m KiB of LDS, so only one or two workgroups fit on a
-// CU: sixteen waves per workgroup keep four waves per SIMD to hide the LDS
-// and scalar-load latency of each row update.
-constexpr unsigned kSolveWaves = 16;
+// CU.  Eight waves per workgroup measured best (A/B of 4/8/16: 16 waves put
+// more waves on each pivot step's barrier than its few row updates use).
+#ifndef SGPU_SOLVE_WAVES
+#define SGPU_SOLVE_WAVES 8
+#endif
+constexpr unsigned kSolveWaves = SGPU_SOLVE_WAVES;
 constexpr unsigned kSolveLdsMaxRows = 120;
 
 // LDS bytes of the staged solve: row tiles, the transposed coefficient
