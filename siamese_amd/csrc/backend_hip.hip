@@ -92,8 +92,11 @@ __device__ __forceinline__ void st16(uint64_t addr, uint4 v)
 // lane's 16 bytes straddle two aligned 16-byte source words: both are loaded
 // (coalesced) and recombined with v_alignbyte_b32.  The word offset and byte
 // shift are uniform per symbol, so the selection is a uniform branch, not a
-// register-indexed gather.  Only 16-byte-aligned words holding at least one
-// source byte are loaded (never past the source's last page).
+// register-indexed gather.  Every lane takes the same path: only aligned
+// words holding at least one source byte are loaded (an aligned 16-byte word
+// never crosses a page), the prefix bytes are merged into lane 0 and bytes
+// past the symbol are masked to zero.  Two tiles' loads are in flight before
+// their stores.
 constexpr unsigned kIngestWaves = 4;
 
 __device__ __forceinline__ uint32_t pick(const uint32_t* w, unsigned q, unsigned r, unsigned k)
@@ -110,53 +113,57 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
     const uint32_t lane = threadIdx.x & 63;
     const IngestDesc d = descs[di];
     const uint32_t total = d.hdrLen + d.bytes;
-    const uint64_t dst = d.dst;
     // source address that lines up with dst byte 0
     const uint64_t base = d.src - d.hdrLen;
     const unsigned sh = (unsigned)(base & 15u);
     const unsigned q = sh >> 2, r = sh & 3;
     const uint64_t srcEnd = d.src + d.bytes;
+    const uint32_t h0 = d.hdr[0] | (d.hdr[1] << 8) | (d.hdr[2] << 16) | ((uint32_t)d.hdr[3] << 24);
+    const uint32_t h1 = d.hdr[4] | (d.hdr[5] << 8) | (d.hdr[6] << 16) | ((uint32_t)d.hdr[7] << 24);
 
-    for (uint32_t t = 0; t < total; t += kTileBytes) {
-        const uint32_t p = t + lane * 16;
-        if (p >= total)
-            break;
-        uint4 out;
-        if (p >= d.hdrLen && p + 16 <= total) {
+    for (uint32_t t = 0; t < total; t += 2 * kTileBytes) {
+        uint4 out[2];
+#pragma unroll
+        for (unsigned u = 0; u < 2; ++u) {
+            const uint32_t p = t + u * kTileBytes + lane * 16;
+            out[u] = make_uint4(0, 0, 0, 0);
+            if (p >= total)
+                continue;
             const uint64_t a = (base + p) & ~(uint64_t)15;
-            const uint4 lo = ld16(a);
-            const uint4 hi = (sh != 0 && a + 16 < srcEnd) ? ld16(a + 16) : make_uint4(0, 0, 0, 0);
+            const bool any = d.bytes != 0;
+            const uint4 lo = (any && a < srcEnd && a + 16 > d.src) ? ld16(a) : make_uint4(0, 0, 0, 0);
+            const uint4 hi = (any && sh != 0 && a + 16 < srcEnd) ? ld16(a + 16) : make_uint4(0, 0, 0, 0);
             const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
             switch (q) {   // wave-uniform
             case 0:
-                out = make_uint4(pick(w, 0, r, 0), pick(w, 0, r, 1), pick(w, 0, r, 2), pick(w, 0, r, 3));
+                out[u] = make_uint4(pick(w, 0, r, 0), pick(w, 0, r, 1), pick(w, 0, r, 2), pick(w, 0, r, 3));
                 break;
             case 1:
-                out = make_uint4(pick(w, 1, r, 0), pick(w, 1, r, 1), pick(w, 1, r, 2), pick(w, 1, r, 3));
+                out[u] = make_uint4(pick(w, 1, r, 0), pick(w, 1, r, 1), pick(w, 1, r, 2), pick(w, 1, r, 3));
                 break;
             case 2:
-                out = make_uint4(pick(w, 2, r, 0), pick(w, 2, r, 1), pick(w, 2, r, 2), pick(w, 2, r, 3));
+                out[u] = make_uint4(pick(w, 2, r, 0), pick(w, 2, r, 1), pick(w, 2, r, 2), pick(w, 2, r, 3));
                 break;
             default:
-                out = make_uint4(pick(w, 3, r, 0), pick(w, 3, r, 1), pick(w, 3, r, 2), pick(w, 3, r, 3));
+                out[u] = make_uint4(pick(w, 3, r, 0), pick(w, 3, r, 1), pick(w, 3, r, 2), pick(w, 3, r, 3));
                 break;
             }
-        } else {
-            // the header lane and the last partial lane: byte by byte
-            const uint8_t* src = reinterpret_cast<const uint8_t*>(d.src);
-            uint32_t v[4] = {0, 0, 0, 0};
-            for (uint32_t k = 0; k < 16; ++k) {
-                const uint32_t pk = p + k;
-                uint32_t b = 0;
-                if (pk < d.hdrLen)
-                    b = d.hdr[pk];
-                else if (pk < total)
-                    b = src[pk - d.hdrLen];
-                v[k >> 2] |= b << (8 * (k & 3));
-            }
-            out = make_uint4(v[0], v[1], v[2], v[3]);
         }
-        st16(dst + p, out);
+#pragma unroll
+        for (unsigned u = 0; u < 2; ++u) {
+            const uint32_t p = t + u * kTileBytes + lane * 16;
+            if (p >= total)
+                continue;
+            uint4 v = out[u];
+            if (p == 0) {   // the length prefix (at most 8 bytes) over source bytes
+                const uint32_t m0 = byte_mask((int)d.hdrLen), m1 = byte_mask((int)d.hdrLen - 4);
+                v.x = (v.x & ~m0) | (h0 & m0);
+                v.y = (v.y & ~m1) | (h1 & m1);
+            }
+            if (p + 16 > total)
+                v = mask16(v, (int)total - (int)p);
+            st16(d.dst + p, v);
+        }
     }
 }
 
