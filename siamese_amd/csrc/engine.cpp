@@ -814,8 +814,15 @@ void Engine::flush()
     std::vector<SegRef> segs;
     std::vector<Phase> phases;
     std::vector<SolveDesc> sdescs;
-    std::vector<SolveRow> srows;
-    std::vector<uint8_t> coef;
+    // solve rows and coefficients are copied straight into the upload by the
+    // assembly tasks (SolveRef: where each pending solve's data goes)
+    struct SolveRef
+    {
+        const Program::PendingSolve* ps;
+        size_t rowBase, coefBase;
+    };
+    std::vector<SolveRef> srefsSolve;
+    size_t nSolveRows = 0, nCoef = 0;
     std::vector<SolveItem> sitems;
     size_t nOps = 0, nTerms = 0, nWords = 0, nItems = 0;
     for (int g = 0; g < 2; ++g) {
@@ -850,10 +857,11 @@ void Engine::flush()
                 const Program::PendingSolve& ps = p->solves_[k];
                 SolveDesc d = ps.desc;
                 d.result += resultBase[g][pi];
-                d.rowBegin = (uint32_t)srows.size();
-                d.coefOffset = coef.size();
-                srows.insert(srows.end(), ps.rows.begin(), ps.rows.end());
-                coef.insert(coef.end(), ps.coef.begin(), ps.coef.end());
+                d.rowBegin = (uint32_t)nSolveRows;
+                d.coefOffset = nCoef;
+                srefsSolve.push_back(SolveRef{&ps, nSolveRows, nCoef});
+                nSolveRows += ps.rows.size();
+                nCoef += ps.coef.size();
                 const uint32_t sidx = (uint32_t)sdescs.size();
                 sdescs.push_back(d);
                 sv.maxRows = std::max(sv.maxRows, d.m);
@@ -887,9 +895,9 @@ void Engine::flush()
     const size_t oSD = off;
     off = align16(off + sdescs.size() * sizeof(SolveDesc));
     const size_t oSR = off;
-    off = align16(off + srows.size() * sizeof(SolveRow));
+    off = align16(off + nSolveRows * sizeof(SolveRow));
     const size_t oCoef = off;
-    off = align16(off + coef.size());
+    off = align16(off + nCoef);
     const size_t oSI = off;
     off = align16(off + sitems.size() * sizeof(SolveItem));
     const size_t upBytes = off;
@@ -900,14 +908,17 @@ void Engine::flush()
     uint8_t* up = upHost_;
     const uint64_t stageDev = (uint64_t)(uintptr_t)(upDev_ + oStage);
     constexpr size_t kIngestChunk = 16384;
+    constexpr size_t kSolveChunk = 64;
     struct Task
     {
-        int kind;   // 0 = segment, 1 = ingest chunk
+        int kind;   // 0 = segment, 1 = ingest chunk, 2 = solve chunk
         size_t a, b;
     };
     std::vector<Task> tasks;
     for (size_t i = 0; i < segs.size(); ++i)
         tasks.push_back(Task{0, i, 0});
+    for (size_t i = 0; i < srefsSolve.size(); i += kSolveChunk)
+        tasks.push_back(Task{2, i, 0});
     for (size_t si = 0; si < srefs.size(); ++si)
         for (size_t c = 0; c < srefs[si].shard->ingest.size(); c += kIngestChunk)
             tasks.push_back(Task{1, si, c});
@@ -939,6 +950,14 @@ void Engine::flush()
             uint32_t n = 0;
             for (uint32_t tb = 0; tb < s.maxExtent; tb += kExecTileBytes)
                 items[n++] = ExecItem{r.wordBase, r.words, nItems, tb};
+        } else if (t.kind == 2) {
+            const size_t end = std::min(srefsSolve.size(), t.a + kSolveChunk);
+            for (size_t i = t.a; i < end; ++i) {
+                const SolveRef& r = srefsSolve[i];
+                std::memcpy(up + oSR + r.rowBase * sizeof(SolveRow), r.ps->rows.data(),
+                            r.ps->rows.size() * sizeof(SolveRow));
+                std::memcpy(up + oCoef + r.coefBase, r.ps->coef.data(), r.ps->coef.size());
+            }
         } else {
             const ShardRef& sr = srefs[t.a];
             const Shard& s = *sr.shard;
@@ -956,8 +975,6 @@ void Engine::flush()
     });
     if (!sdescs.empty()) {
         std::memcpy(up + oSD, sdescs.data(), sdescs.size() * sizeof(SolveDesc));
-        std::memcpy(up + oSR, srows.data(), srows.size() * sizeof(SolveRow));
-        std::memcpy(up + oCoef, coef.data(), coef.size());
         std::memcpy(up + oSI, sitems.data(), sitems.size() * sizeof(SolveItem));
     }
 
