@@ -39,9 +39,9 @@ STREAMS_PER_GPU = 1024
 METRIC = "device-resident GB/s encode+decode, 1400B pkts @20% loss; % HBM peak"
 
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_s7_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_s8_traffic.json")
 TRAFFIC_NOTE = ("HBM bytes per k_exec launch from rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE "
-                "of `bench.py --steps 1 --warmup 1 --no-cpu --no-e2e` (profiles/r1_s7_traffic.json, "
+                "of `bench.py --steps 1 --warmup 1 --no-cpu --no-e2e` (profiles/r1_s8_traffic.json, "
                 "tools/pmc_traffic.py); compare with exec_bytes_per_launch")
 
 

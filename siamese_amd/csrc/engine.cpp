@@ -9,6 +9,11 @@
 #include <cstddef>
 #include <cstring>
 
+// dispatch each exec phase's segments longest op list first (see flush)
+#ifndef SGPU_EXEC_LPT
+#define SGPU_EXEC_LPT 1
+#endif
+
 namespace sgpu {
 
 void EngineStats::add(const EngineStats& o)
@@ -831,6 +836,7 @@ void Engine::flush()
             maxSegs = std::max(maxSegs, p->nsegs_);
         for (size_t k = 0; k < maxSegs; ++k) {
             Phase ex{Phase::EXEC, nItems, 0, 0, 0, 0};
+            const size_t segBegin = segs.size();
             for (Program* p : progs[g]) {
                 if (k >= p->nsegs_)
                     continue;
@@ -845,6 +851,25 @@ void Engine::flush()
                 nWords += words;
                 nItems += (s.maxExtent + kExecTileBytes - 1) / kExecTileBytes;
             }
+#if SGPU_EXEC_LPT
+            // Longest op lists first: workgroups are dispatched in blockIdx
+            // order and a launch runs in about two rounds of one workgroup per
+            // CU, so the short segments fill the second round's tail.
+            {
+                std::vector<uint32_t> order(segs.size() - segBegin);
+                for (uint32_t i = 0; i < order.size(); ++i)
+                    order[i] = i;
+                std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+                    return segs[segBegin + a].words > segs[segBegin + b].words;
+                });
+                uint32_t ib = (uint32_t)ex.itemBegin;
+                for (uint32_t i : order) {
+                    SegRef& r = segs[segBegin + i];
+                    r.itemBase = ib;
+                    ib += (r.prog->segs_[r.seg].maxExtent + kExecTileBytes - 1) / kExecTileBytes;
+                }
+            }
+#endif
             ex.itemCount = nItems - ex.itemBegin;
             if (ex.itemCount)
                 phases.push_back(ex);
@@ -868,6 +893,13 @@ void Engine::flush()
                 for (uint32_t t = 0; t < d.maxBytes; t += kTileBytes)
                     sitems.push_back(SolveItem{sidx, t});
             }
+#if SGPU_EXEC_LPT
+            // largest solves first (the serial pivot chain grows with m)
+            std::stable_sort(sitems.begin() + sv.itemBegin, sitems.end(),
+                             [&](const SolveItem& a, const SolveItem& b) {
+                                 return sdescs[a.solve].m > sdescs[b.solve].m;
+                             });
+#endif
             sv.itemCount = sitems.size() - sv.itemBegin;
             sv.solveCount = sdescs.size() - sv.solveBegin;
             if (sv.solveCount)
