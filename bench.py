@@ -22,10 +22,21 @@ roofline = the executor kernel k_exec: its share of the algorithmic bytes over
 cpu_baseline = the upstream reference (oracle/_ref, built from
          /root/reference's own sources) on the host cores, same workload on a
          bounded sample of streams.
+legs   = (N=1 only) the other BASELINE configs on one GPU -- C2 (1024 streams,
+         Cauchy/parity path), C3 (one 8192-packet stream) and C5 (one stream of
+         16000 x 64 KiB) -- each with the reference on the host cores beside it.
+
+Multi-GPU: `bench.py --gpus N` (no WORLD_SIZE in the environment) starts N
+rank processes itself, one per GPU, from a parent that never touches the GPU;
+under torch.distributed.run the ranks come from the environment.  Barrier and
+max/sum reductions use gloo on the host: no RCCL anywhere (there is no
+data-path exchange between stream shards).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,20 +49,18 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 STREAMS_PER_GPU = 1024
 METRIC = "device-resident GB/s encode+decode, 1400B pkts @20% loss; % HBM peak"
 
-
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_s8_traffic.json")
-TRAFFIC_NOTE = ("HBM bytes per k_exec launch from rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE "
-                "of `bench.py --steps 1 --warmup 1 --no-cpu --no-e2e` (profiles/r1_s8_traffic.json, "
-                "tools/pmc_traffic.py); compare with exec_bytes_per_launch")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2_traffic.json")
 
 
 def pmc_traffic(kernel):
-    """Per-launch HBM traffic of `kernel` from the committed PMC profile."""
+    """Per-launch HBM traffic of `kernel` from the committed PMC profile
+    (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py)."""
     try:
         with open(TRAFFIC_JSON) as f:
-            return json.load(f)[kernel]["traffic_bytes"]
+            d = json.load(f)
+        return d[kernel]["traffic_bytes"], d.get("_source", TRAFFIC_JSON)
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 def workload(rank, streams):
@@ -59,71 +68,147 @@ def workload(rank, streams):
                      hash_data=0)
 
 
-def cpu_baseline(sample_streams, threads, alg_bytes_per_stream):
-    """Reference codec on the host cores over a bounded sample of the same workload."""
+def cpu_baseline(cfg, threads, alg_bytes, sample):
+    """The reference codec on the host cores over `cfg` (a bounded sample of
+    the workload whose algorithmic bytes are `alg_bytes`)."""
     if not os.path.exists(S.REF_LIB):
         return None
-    cfg = S.replace(S.CONFIGS["C4"], streams=sample_streams, first_stream=0, hash_data=0)
     res, _, wall = S.run_capi(S.REF_LIB, cfg, threads=threads)
     payload = sum(r.payload_bytes for r in res)
     return {
-        "value": round(alg_bytes_per_stream * sample_streams / wall / 1e9, 3),
+        "value": round(alg_bytes / wall / 1e9, 3),
         "unit": "GB/s",
         "payload_GBps": round(payload / wall / 1e9, 3),
         "cores": threads,
         "kind": "reference",
-        "sample": "%d C4 streams (256 x 1400 B, 20%% loss, block mode) on %d threads, %.2f s"
-                  % (sample_streams, threads, wall),
+        "sample": "%s on %d thread%s, %.2f s" % (sample, threads, "s" if threads > 1 else "",
+                                                 wall),
     }
 
 
 class Collective:
-    """Barrier + reductions over ranks (torch.distributed), or a no-op at N=1."""
+    """Barrier + reductions over ranks on the host (gloo), or no-ops at N=1."""
 
-    def __init__(self, world, use_cuda):
-        import torch
-        self.torch = torch
+    def __init__(self, world):
         self.world = world
-        self.use_cuda = use_cuda
         self.dist = None
         if world > 1:
             import torch.distributed as dist
             self.dist = dist
             if not dist.is_initialized():
-                dist.init_process_group("nccl" if use_cuda else "gloo")
+                dist.init_process_group("gloo")
 
     def barrier(self):
         if self.dist is not None:
             self.dist.barrier()
-        if self.use_cuda:
-            self.torch.cuda.synchronize()
 
     def reduce(self, values, op):
-        t = self.torch.tensor(values, dtype=self.torch.float64,
-                              device="cuda" if self.use_cuda else "cpu")
-        if self.dist is not None:
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max"
-                                 else self.dist.ReduceOp.SUM)
+        if self.dist is None:
+            return [float(v) for v in values]
+        import torch
+        t = torch.tensor(values, dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max"
+                             else self.dist.ReduceOp.SUM)
         return [float(x) for x in t.tolist()]
+
+    def close(self):
+        if self.dist is not None and self.dist.is_initialized():
+            self.dist.destroy_process_group()
+
+
+def engine_bytes(rep):
+    eng = S.engine_dict(rep)
+    return eng, eng["ref_op_bytes"] + eng["out_bytes"]
+
+
+def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu_sample):
+    """One extra BASELINE config on one GPU: a verified warm-up, then `runs`
+    timed runs; the reference on the host beside it."""
+    sess = S.BatchSession(library, cfg, device=device)
+    try:
+        res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=1)
+        if rep.mismatches or any(r.status for r in res):
+            raise RuntimeError("bench leg %s: verification failed" % name)
+        res, rep = sess.run(steps=runs, warmup=0, verify=False, threads=threads, groups=1,
+                            digest=False)
+    finally:
+        sess.close()
+    eng, alg = engine_bytes(rep)
+    payload = sum(r.payload_bytes for r in res) * runs
+    sec = rep.seconds
+    exec_s = rep.exec_ms / 1e3
+    exec_bytes = alg - eng["solve_bytes"]
+    out = {
+        "workload": "%d stream%s x %d originals x %d B, %d%% loss" % (
+            cfg.streams, "s" if cfg.streams > 1 else "", cfg.originals, cfg.payload_bytes,
+            cfg.loss_pct),
+        "runs": runs,
+        "ms_per_run": round(sec / runs * 1e3, 3),
+        "value": round(alg / sec / 1e9, 3),
+        "unit": "GB/s",
+        "payload_GBps": round(payload / sec / 1e9, 3),
+        "device_ms_per_run": round(rep.device_ms / runs, 3),
+        "rounds_per_run": rep.rounds / runs,
+        "algorithmic_bytes_per_run": alg // runs,
+        "roofline": {
+            "bound": "hbm", "kernel": "k_exec",
+            "achieved": round(exec_bytes / exec_s / 1e9, 2) if exec_s > 0 else None,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(exec_bytes / exec_s / 1e9 / HBM_PEAK_GBPS, 4) if exec_s > 0 else None,
+        },
+        "cpu_baseline": None,
+    }
+    if cpu_cfg is not None:
+        # algorithmic bytes of the sample: the library's count scaled by payload
+        per_payload = alg / max(1, payload)
+        sample_payload = cpu_cfg.streams * cpu_cfg.originals * cpu_cfg.payload_bytes
+        out["cpu_baseline"] = cpu_baseline(cpu_cfg, cpu_threads, per_payload * sample_payload,
+                                           cpu_sample)
+    return out
+
+
+def legs(library, device, threads, use_cpu):
+    cpu_threads = min(16, os.cpu_count() or 1)
+    specs = [
+        # C2: 1024 streams, Cauchy/parity path; reference on all host cores
+        ("C2", S.replace(S.CONFIGS["C2"], hash_data=0), 3,
+         S.replace(S.CONFIGS["C2"], hash_data=0), cpu_threads,
+         "the full C2 (1024 streams x 256 x 1400 B)"),
+        # C3: one stream; reference on one core (an instance is single-threaded)
+        ("C3", S.replace(S.CONFIGS["C3"], hash_data=0), 2,
+         S.replace(S.CONFIGS["C3"], hash_data=0), 1, "the full C3 (1 stream x 8192 x 1400 B)"),
+        # C5: one stream of 64 KiB symbols; reference on one core over the
+        # first 2000 originals (the whole stream takes it ~15 s)
+        ("C5", S.replace(S.CONFIGS["C5"], hash_data=0), 1,
+         S.replace(S.CONFIGS["C5"], hash_data=0, originals=2000), 1,
+         "C5's first 2000 originals (1 stream x 2000 x 64 KiB)"),
+    ]
+    out = {}
+    for name, cfg, runs, cpu_cfg, cpu_thr, sample in specs:
+        out[name] = run_leg(name, library, cfg, device, threads, runs,
+                            cpu_cfg if use_cpu else None, cpu_thr, sample)
+    return out
 
 
 def run_rank(rank, world, local, args, library, use_cuda):
     """One rank's share: returns the JSON line on rank 0, None elsewhere."""
-    import torch
-    if use_cuda:
-        torch.cuda.set_device(local)
-    coll = Collective(world, use_cuda)
+    coll = Collective(world)
     cfg = workload(rank, args.streams)
-    sess = S.BatchSession(library, cfg, device=local if use_cuda else -1)
+    device = local if use_cuda else -1
+    sess = S.BatchSession(library, cfg, device=device)
     # untimed warm-up; its first run checks every recovered byte against the payload
-    res, rep = sess.run(steps=0, warmup=max(1, args.warmup), verify=True, threads=args.threads,
-                        groups=args.groups)
+    res, rep = sess.run(steps=0, warmup=1, verify=True, threads=args.threads, groups=args.groups)
     if rep.mismatches or any(r.status for r in res):
         raise RuntimeError("bench: verification failed: %d byte mismatches, status %s"
                            % (rep.mismatches, S.summary(res)["status"]))
     # determinism fingerprint of the (verified) workload; the timed steps
     # repeat it exactly but keep no event logs
     verified_digests = S.digests(res)
+    # then W untimed steps pipelined exactly like the timed ones, so the
+    # buffer arena reaches the timed loop's high-water mark before timing
+    if args.warmup > 0:
+        sess.run(steps=args.warmup, warmup=0, verify=False, threads=args.threads,
+                 groups=args.groups, digest=False)
 
     coll.barrier()
     t0 = time.perf_counter()
@@ -137,18 +222,17 @@ def run_rank(rank, world, local, args, library, use_cuda):
     # is copied back to the host.  Reported beside, never as, `value`.
     e2e_elapsed = None
     if args.e2e:
-        sess.run(steps=0, warmup=1, verify=False, threads=args.threads, groups=args.groups,
-                 e2e=True)
+        sess.run(steps=max(1, args.warmup), warmup=0, verify=False, threads=args.threads,
+                 groups=args.groups, e2e=True, digest=False)
         coll.barrier()
         t1 = time.perf_counter()
-        _, rep_e2e = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
-                              groups=args.groups, e2e=True, digest=False)
+        sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
+                 groups=args.groups, e2e=True, digest=False)
         coll.barrier()
         e2e_elapsed = time.perf_counter() - t1
     sess.close()
 
-    eng = S.engine_dict(rep)
-    alg_bytes = eng["ref_op_bytes"] + eng["out_bytes"]
+    eng, alg_bytes = engine_bytes(rep)
     payload = sum(r.payload_bytes for r in res) * args.steps
     digest = 0
     for d in verified_digests:
@@ -157,6 +241,11 @@ def run_rank(rank, world, local, args, library, use_cuda):
     alg_total, payload_total, streams_total = coll.reduce(
         [float(alg_bytes), float(payload), float(cfg.streams)], "sum")
     e2e_max = coll.reduce([e2e_elapsed], "max")[0] if e2e_elapsed is not None else None
+    extra = None
+    if rank == 0 and world == 1 and args.legs:
+        extra = legs(library, device, args.threads, not args.no_cpu)
+    coll.barrier()
+    coll.close()
     if rank != 0:
         return None
 
@@ -165,6 +254,9 @@ def run_rank(rank, world, local, args, library, use_cuda):
     exec_bytes = alg_bytes - eng["solve_bytes"]
     achieved = (exec_bytes / exec_s / 1e9) if exec_s > 0 else 0.0
     steps = args.steps
+    launches = max(1, eng["exec_launches"])
+    traffic, traffic_src = pmc_traffic("sgpu::k_exec")
+    exec_ms_per_launch = rep.exec_ms / launches
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -186,7 +278,8 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "originals": 256,
             "payload_bytes": 1400,
             "loss_pct": 20,
-            "parallelism": "independent streams sharded by index (weak scaling)",
+            "parallelism": "independent streams sharded by index (weak scaling), "
+                           "one process per GPU, gloo host barrier",
         },
         "payload_GBps": round(payload_total / t_max / 1e9, 3),
         "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
@@ -195,7 +288,6 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "device_ms_per_step": round(rep.device_ms / steps, 3),
             "rounds_per_step": rep.rounds / steps,
             "launches_per_step": eng["launches"] / steps,
-            "terms_per_step": eng["terms"] / steps,
             "algorithmic_bytes_per_step": alg_bytes // steps,
             "upload_bytes_per_step": eng["upload_bytes"] // steps,
             "arena_growth_bytes": eng["arena_growth"],
@@ -217,17 +309,24 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": pmc_traffic("sgpu::k_exec"),
-            "traffic_source": TRAFFIC_NOTE,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "traffic_GBps": (round(traffic / (exec_ms_per_launch / 1e3) / 1e9, 2)
+                             if traffic and exec_ms_per_launch > 0 else None),
+            "traffic_frac": (round(traffic / (exec_ms_per_launch / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
+                             if traffic and exec_ms_per_launch > 0 else None),
             "exec_bytes_per_step": exec_bytes // steps,
             "exec_launches_per_step": eng["exec_launches"] / steps,
-            "exec_bytes_per_launch": exec_bytes // max(1, eng["exec_launches"]),
-            "exec_ms_per_step": round(rep.exec_ms / steps, 4),
-            "note": "achieved = k_exec's algorithmic bytes / summed k_exec launch time "
-                    "(HIP events on the codec stream)",
+            "exec_bytes_per_launch": exec_bytes // launches,
+            "exec_ms_per_launch": round(exec_ms_per_launch, 4),
+            "note": "achieved/frac = k_exec's ALGORITHMIC bytes per launch / its average launch "
+                    "time (HIP events on the codec stream, this run); traffic = measured HBM "
+                    "bytes per launch (rocprofv3 PMC, traffic_source) and traffic_GBps/"
+                    "traffic_frac = that over this run's launch time",
         },
         "cpu_baseline": None,
         "end_to_end": None,
+        "legs": extra,
     }
     if e2e_max is not None:
         line["end_to_end"] = {
@@ -239,14 +338,54 @@ def run_rank(rank, world, local, args, library, use_cuda):
                     "and recovered original D2H (PCIe-inclusive; not `value`)",
         }
     if not args.no_cpu and world == 1:
-        # the reference on the host cores, rank 0 at N=1 only
+        # the reference on the host cores, rank 0 at N=1 only, on a bounded
+        # sample of C4 streams
         threads = min(16, os.cpu_count() or 1)
         per_stream = alg_bytes / steps / args.streams
-        line["cpu_baseline"] = cpu_baseline(args.cpu_streams, threads, per_stream)
+        sample_cfg = S.replace(S.CONFIGS["C4"], streams=args.cpu_streams, first_stream=0,
+                               hash_data=0)
+        line["cpu_baseline"] = cpu_baseline(
+            sample_cfg, threads, per_stream * args.cpu_streams,
+            "%d C4 streams (256 x 1400 B, 20%% loss, block mode)" % args.cpu_streams)
     return line
 
 
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """Start n rank processes (one per GPU) and wait for them.  The parent
+    makes no GPU call; each child binds GPU `LOCAL_RANK` itself."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                   SIAMESE_AMD_DEVICE=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rc = 0
+    try:
+        for p in procs:
+            p.wait()
+            rc = rc or p.returncode
+            if p.returncode:
+                for q in procs:
+                    if q.poll() is None:
+                        q.kill()   # exact PIDs of our own children
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+                q.wait()
+    return rc
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -260,9 +399,13 @@ def main(argv=None):
                     help="stream groups alternating host and device work (1 = no overlap)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip the PCIe-inclusive end-to-end leg")
+    ap.add_argument("--no-legs", dest="legs", action="store_false",
+                    help="skip the C2/C3/C5 legs (N=1)")
     ap.add_argument("--library", default=S.AMD_LIB, help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -270,11 +413,8 @@ def main(argv=None):
     line = run_rank(rank, world, local, args, args.library, use_cuda)
     if line is not None:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        if dist.is_initialized():
-            dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -226,7 +226,7 @@ void EncoderCore::update_rto()
 
 SiameseResult EncoderCore::acknowledge(const uint8_t* data, unsigned bytes, unsigned& nextExpectedOut)
 {
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     unsigned next = 0;
     const int h = get_packetnum_head(data, (int)bytes, &next);
@@ -281,7 +281,7 @@ SiameseResult EncoderCore::retransmit(SiameseOriginalPacket& out)
 {
     out.Data = nullptr;
     out.DataBytes = 0;
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     if (unacked() == 0) {
         ack_.foundOldest = false;
@@ -377,7 +377,7 @@ unsigned DecoderCore::find_next_got(unsigned start)
 
 SiameseResult DecoderCore::acknowledgement(uint8_t* buffer, unsigned byteLimit, unsigned& usedBytes)
 {
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     const unsigned count = count_;
     if (count == 0) {

@@ -192,8 +192,7 @@ SIAMESE_EXPORT int sgpu_submit(void)
 {
     Engine* eng = Engine::global();
     Lock lock(eng->mutex());
-    eng->flush();
-    return 0;
+    return eng->flush() ? 0 : -1;
 }
 
 SIAMESE_EXPORT void* sgpu_device_alloc(size_t bytes)
@@ -228,7 +227,8 @@ SIAMESE_EXPORT int sgpu_h2d(void* deviceDst, const void* hostSrc, size_t bytes)
 {
     Engine* eng = Engine::global();
     Lock lock(eng->mutex());
-    eng->sync();
+    if (!eng->sync())
+        return -1;
     be_h2d(deviceDst, hostSrc, bytes);
     return be_sync() ? 0 : -1;
 }

@@ -130,7 +130,7 @@ bool DecoderCore::grow_window(unsigned end)
 SiameseResult DecoderCore::add_original(const SiameseOriginalPacket& packet, uint64_t deviceSrc)
 {
     // :1467-1536
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     const unsigned element = column_to_element(packet.PacketNum);
     if (column_delta_negative(element)) {
@@ -548,7 +548,7 @@ void DecoderCore::list_delete_before(unsigned element)
 
 SiameseResult DecoderCore::add_recovery(const SiameseRecoveryPacket& packet)
 {
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     RowMeta m;
     const int footer = read_footer(packet.Data, packet.DataBytes, &m);
@@ -561,7 +561,7 @@ SiameseResult DecoderCore::add_recovery(const SiameseRecoveryPacket& packet)
 
 SiameseResult DecoderCore::add_recovery_device(const DeviceRecovery& rec)
 {
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     RowMeta m;
     // The footer sits at the end of the packet; the producer handed us a
@@ -753,7 +753,7 @@ void DecoderCore::region_reset()
 
 bool DecoderCore::check_recovery_possible()
 {
-    if (disabled_)
+    if (dead())
         return false;
     RecPacket* r;
     unsigned nextCheck, recCount, lost;
@@ -805,7 +805,7 @@ SiameseResult DecoderCore::is_ready()
 
 SiameseResult DecoderCore::decode(SiameseOriginalPacket** packetsOut, unsigned* countOut)
 {
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     if (hasRecovered_) {
         hasRecovered_ = false;
@@ -1379,7 +1379,7 @@ void DecoderCore::download_recovered()
 
 SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
 {
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     const unsigned element = column_to_element(packet.PacketNum);
     if (element >= count_ || slot(element).bytes == 0) {
@@ -1389,8 +1389,7 @@ SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
     }
     if (slot(element).pending) {
         // Exact length still on the device: finish the outstanding work.
-        eng_->flush_and_sync();
-        if (disabled_)
+        if (!eng_->flush_and_sync() || dead())
             return Siamese_Disabled;
     }
     DecSlot& s = slot(element);

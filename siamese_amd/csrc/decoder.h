@@ -104,12 +104,14 @@ public:
     /// ARQ: siamese_decoder_ack (arq.cpp)
     SiameseResult acknowledgement(uint8_t* buffer, unsigned byteLimit, unsigned& usedBytes);
 
-    bool disabled() const { return disabled_; }
+    /// Disabled: this instance failed (sticky), or the device did (Engine::failed).
+    bool disabled() const { return dead(); }
+    bool dead() const { return disabled_ || eng_->failed(); }
     /// Packet present in the window (received or recovered, length may be pending)
     bool has(unsigned packetNum)
     {
         const unsigned e = column_to_element(packetNum);
-        return !disabled_ && e < count_ && slot(e).bytes > 0;
+        return !dead() && e < count_ && slot(e).bytes > 0;
     }
     /// True while a queued solve has not been resolved by a completed flush.
     bool has_pending() const { return pendingSolves_ > 0; }

@@ -32,7 +32,7 @@ EncoderCore::~EncoderCore()
 SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc)
 {
     // :85-161
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     if (remaining_slots() == 0)
         return Siamese_MaxPacketsReached;
@@ -105,7 +105,7 @@ void EncoderCore::start_window(unsigned column)
 void EncoderCore::remove_before(unsigned firstKeptColumn)
 {
     // :183-216
-    if (disabled_)
+    if (dead())
         return;
     const unsigned element = column_to_element(firstKeptColumn);
     if (element >= count_) {
@@ -244,7 +244,7 @@ DevSum& EncoderCore::get_sum(unsigned lane, unsigned sumIndex, unsigned elementE
 
 SiameseResult EncoderCore::get(SiameseOriginalPacket& packet)
 {
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     const unsigned element = column_to_element(packet.PacketNum);
     if (element >= count_ || slot(element).bytes == 0) {
@@ -295,7 +295,7 @@ void EncoderCore::finish_row(EncodeOut& out, const RowMeta& meta, unsigned paylo
 SiameseResult EncoderCore::encode(EncodeOut& out)
 {
     // :1146-1254
-    if (disabled_)
+    if (dead())
         return Siamese_Disabled;
     if (count_ == 0) {
         out.bytes = 0;
@@ -408,7 +408,7 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
             if (!(opcode & (1u << bit)))
                 continue;
             DevSum& sum = get_sum(lane, bit % kSums, count_);
-            if (disabled_)
+            if (dead())
                 return Siamese_Disabled;
             if (sum.bytes > 0) {
                 mask[bit / kSums] |= 1u << (lane * kSums + bit % kSums);

@@ -90,7 +90,9 @@ public:
     SiameseResult acknowledge(const uint8_t* data, unsigned bytes, unsigned& nextExpectedOut);
     SiameseResult retransmit(SiameseOriginalPacket& out);
 
-    bool disabled() const { return disabled_; }
+    /// Disabled: this instance failed (sticky), or the device did (Engine::failed).
+    bool disabled() const { return dead(); }
+    bool dead() const { return disabled_ || eng_->failed(); }
     uint64_t stat(unsigned i) const { return stats_[i]; }
 
 private:

@@ -780,10 +780,12 @@ struct ShardRef
 
 } // namespace
 
-void Engine::flush()
+bool Engine::flush()
 {
-    if (flight_.active)
-        sync();
+    if (flight_.active && !sync())
+        return false;
+    if (failed())
+        return false;
 
     std::vector<Shard*> shards;
     {
@@ -796,7 +798,7 @@ void Engine::flush()
         any = any || !s->dirty.empty() || !s->ingest.empty() || !s->downloads.empty() ||
               !s->pendingFree.empty();
     if (!any)
-        return;
+        return true;
     const uint64_t t0 = now_ns();
 
     // ---- 1. layout -----------------------------------------------------------
@@ -1087,12 +1089,15 @@ void Engine::flush()
         s->flightFree.swap(s->pendingFree);
         s->pendingFree.clear();
     }
+    return true;
 }
 
 bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut)
 {
-    if (flight_.active)
-        sync();
+    if (flight_.active && !sync())
+        return false;
+    if (failed())
+        return false;
     if (count == 0)
         return true;
     std::vector<IngestDesc> descs(count);
@@ -1128,6 +1133,10 @@ bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* byt
     be_launch_ingest((const IngestDesc*)gUpDev_, count);
     be_d2h(gHost_, gDev_, total);
     const bool ok = be_sync();
+    if (!ok) {
+        failed_.store(true, std::memory_order_relaxed);
+        return false;
+    }
     // unpack the 16-byte-aligned staging layout into the caller's buffer,
     // in parallel chunks (this is the D2H leg of end-to-end packet flows)
     constexpr unsigned kChunk = 2048;
@@ -1160,6 +1169,17 @@ bool Engine::sync()
         return true;
     const uint64_t t0 = now_ns();
     const bool ok = be_sync();
+    if (!ok) {
+        // The results buffer and downloads of this flush are not valid:
+        // deliver nothing, keep the flush's released buffers out of reuse,
+        // and fail every instance from now on.
+        failed_.store(true, std::memory_order_relaxed);
+        flight_.callbacks.clear();
+        flight_.downloads.clear();
+        flight_.active = false;
+        flushStats_.waitNs += now_ns() - t0;
+        return false;
+    }
     for (const InFlight::Download& d : flight_.downloads)
         std::memcpy(d.host, downHost_ + d.off, d.bytes);
     const uint64_t t1 = now_ns();
@@ -1201,7 +1221,7 @@ bool Engine::sync()
     flushStats_.waitNs += t1 - t0;
     flushStats_.completeNs += t2 - t1;
     flushStats_.reclaimNs += t3 - t2;
-    return ok;
+    return true;
 }
 
 } // namespace sgpu

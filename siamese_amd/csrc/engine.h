@@ -226,13 +226,22 @@ public:
     /// executed; the data is in place after sync().
     void download(void* hostDst, uint64_t devSrc, uint32_t bytes);
 
-    void flush();
+    /// Launch all queued work (completing the flush in flight first).
+    /// Returns false once the device has failed.
+    bool flush();
+    /// Wait for the flush in flight and run its completions.  On a device
+    /// failure nothing of that flush is delivered (no downloads, no
+    /// completions), the engine is marked failed, and every instance reports
+    /// Siamese_Disabled from then on (sticky, like the reference's
+    /// EmergencyDisabled, siamese.h:147-150).
     bool sync();
     bool flush_and_sync()
     {
-        flush();
-        return sync();
+        const bool ok = flush();
+        return sync() && ok;
     }
+    /// A device operation failed; the engine accepts no further work.
+    bool failed() const { return failed_.load(std::memory_order_relaxed); }
     bool pending() const;
 
     /// Copy device ranges into one host buffer right now (after completing
@@ -262,6 +271,7 @@ private:
     WorkerPool& pool();
 
     bool ready_ = false;
+    std::atomic<bool> failed_{false};
     std::mutex mu_;
 
     // ---- arena: 64 MiB hipMalloc chunks are cut into 4 MiB regions under

@@ -427,7 +427,19 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
     }
 }
 
-bool be_sync() { return true; }
+// HOSTSIM_FAIL_SYNC=N: the N-th be_sync (1-based) and every later one
+// report a device fault (tests of the sticky Disabled path).
+bool be_sync()
+{
+    static long failAt = -2;
+    static long calls = 0;
+    if (failAt == -2) {
+        const char* v = std::getenv("HOSTSIM_FAIL_SYNC");
+        failAt = v ? std::atol(v) : -1;
+    }
+    ++calls;
+    return failAt < 1 || calls < failAt;
+}
 void be_timing_enable(bool) {}
 void be_timing_reset() {}
 double be_timing_exec_ms() { return 0; }

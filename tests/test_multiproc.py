@@ -12,14 +12,39 @@ import scenario_lib as S
 ROOT = S.ROOT
 
 
+BENCH_ARGS = ["--library", S.SIM_LIB, "--streams", "6", "--steps", "1", "--warmup", "1",
+              "--no-cpu", "--no-legs"]
+
+
+def _clean_env():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_bench_gpus_2_spawns_two_ranks():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts its own two rank
+    processes (the driver's SCALE run) and reports the 2-rank aggregate."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] +
+                       BENCH_ARGS, env=_clean_env(), capture_output=True, text=True,
+                       timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout   # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["streams_total"] == 12
+    assert "gloo" in line["config"]["parallelism"]
+
+
 def test_two_rank_gloo_bench_shards_streams():
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29517")
+    env = dict(_clean_env(), MASTER_ADDR="127.0.0.1", MASTER_PORT="29517")
     procs = []
     for rank in range(2):
         e = dict(env, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank))
         procs.append(subprocess.Popen(
-            [sys.executable, os.path.join(ROOT, "bench.py"), "--library", S.SIM_LIB,
-             "--streams", "6", "--steps", "1", "--warmup", "1", "--no-cpu"],
+            [sys.executable, os.path.join(ROOT, "bench.py")] + BENCH_ARGS,
             env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=600) for p in procs]
     for p, (o, err) in zip(procs, outs):
