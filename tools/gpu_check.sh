@@ -9,5 +9,5 @@ tail -2 gpurun_out/gputests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
     || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
-timeout -k 10 240 python bench.py "$@" > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
+timeout -k 10 500 python bench.py "$@" > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
 python tools/bench_summary.py bench gpurun_out/bench.log

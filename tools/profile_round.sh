@@ -7,10 +7,10 @@ TAG=${1:-cur}
 D=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-B="bench.py --steps 3 --warmup 1 --no-cpu --no-e2e"
+B="bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-legs"
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o trace -- python3 $B > $D/bench_trace.log 2>&1
-B1="bench.py --steps 1 --warmup 1 --no-cpu --no-e2e"
+B1="bench.py --steps 1 --warmup 1 --no-cpu --no-e2e --no-legs"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $D -o pmc_fetch -- python3 $B1 > /dev/null 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $D -o pmc_write -- python3 $B1 > /dev/null 2>&1
-python3 tools/pmc_traffic.py $(ls $D/pmc_fetch*counter_collection.csv | head -n1) $(ls $D/pmc_write*counter_collection.csv | head -n1) $D/traffic.json > /dev/null
+python3 tools/pmc_traffic.py $(ls $D/pmc_fetch*counter_collection.csv | head -n1) $(ls $D/pmc_write*counter_collection.csv | head -n1) $D/traffic.json "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per k_exec launch, bench.py --steps 1 --no-legs, round 2 tag $TAG" > /dev/null
 ls -R $D | head -n 40
