@@ -6,15 +6,19 @@
 #include "decoder.h"
 #include "encoder.h"
 
-#include <chrono>
+#include <ctime>
 #include <cstring>
 
 namespace sgpu {
 
 uint64_t now_msec()
 {
-    using namespace std::chrono;
-    return (uint64_t)duration_cast<milliseconds>(steady_clock::now().time_since_epoch()).count();
+    // Every add stamps its original (reference SiameseEncoder.cpp:142); the
+    // coarse monotonic clock is a memory read (no vDSO/TSC round trip) and
+    // its tick is far below the millisecond-scale RTO arithmetic it feeds.
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC_COARSE, &ts);
+    return (uint64_t)ts.tv_sec * 1000u + (uint64_t)ts.tv_nsec / 1000000u;
 }
 
 unsigned put_nack_range(unsigned relativeStart, unsigned lossCountM1, uint8_t* out)

@@ -29,7 +29,31 @@ void compute(unsigned row, unsigned n, std::vector<uint32_t>& out)
         out[i] = mod(prng.next());
 }
 
+struct RowSelectTable
+{
+    RowSelect t[256];
+    RowSelectTable()
+    {
+        for (unsigned row = 0; row < 256; ++row) {
+            RowSelect& r = t[row];
+            r.mask[0] = r.mask[1] = 0;
+            for (unsigned lane = 0; lane < kLanes; ++lane) {
+                const unsigned op = row_opcode(lane, row);
+                r.opLo[lane] = (uint8_t)(op & 7);
+                r.opHi[lane] = (uint8_t)(op >> 3);
+                for (unsigned bit = 0; bit < 2 * kSums; ++bit)
+                    if (op & (1u << bit))
+                        r.mask[bit / kSums] |= 1u << (lane * kSums + bit % kSums);
+            }
+        }
+    }
+};
+
+const RowSelectTable g_rowSelect;
+
 } // namespace
+
+const RowSelect& row_select(unsigned row) { return g_rowSelect.t[row & 255]; }
 
 const uint32_t* ldpc_offsets(unsigned row, unsigned n, unsigned* count)
 {

@@ -68,6 +68,19 @@ inline unsigned row_opcode(unsigned lane, unsigned row)
     return op ? op : 16u;
 }
 
+/// The opcodes of one Siamese row, precomputed for every row number: the
+/// sums they select as masks of bit lane*3 + s (mask[0] feeds the recovery
+/// row from opcode bits 0..2, mask[1] the product from bits 3..5;
+/// SiameseEncoder.cpp:1046-1098) and the raw 3-bit halves per lane (the
+/// decoder's matrix rows, SiameseDecoder.cpp:2180-2260).
+struct RowSelect
+{
+    uint32_t mask[2];
+    uint8_t opLo[kLanes], opHi[kLanes];
+};
+/// row < 256 (Siamese rows use 0..254; a footer can carry any byte)
+const RowSelect& row_select(unsigned row);
+
 // Cauchy element 1/(X_r ^ Y_c), X_r = r + 64, Y_c = c (SiameseCommon.h:212-218)
 inline uint8_t cauchy_element(unsigned row, unsigned column)
 {

@@ -982,6 +982,26 @@ bool DecoderCore::generate_matrix()
 
     const unsigned startRow = (columns <= oldColumns) ? oldRows : 0;
     const size_t matBytes = mat_.size();
+
+    // The sparse picks only land on lost slots: one pass over the elements
+    // the new rows span gives each its matrix column (kNoColumn: received),
+    // so the picks below read a small dense array instead of window slots.
+    constexpr uint32_t kNoColumn = ~0u;
+    unsigned pickLo = ~0u, pickHi = 0;
+    for (unsigned i = startRow; i < rows; ++i) {
+        const RecPacket* rec = rows_[i].rec;
+        if (rec->meta.sumCount <= kCauchyThreshold)
+            continue;
+        pickLo = std::min(pickLo, rec->elementStart);
+        pickHi = std::max(pickHi, rec->elementStart + rec->meta.ldpcCount);
+    }
+    if (pickHi > pickLo) {
+        pickCol_.resize(pickHi - pickLo);
+        for (unsigned e = pickLo; e < pickHi; ++e) {
+            const DecSlot& a = slot(e);
+            pickCol_[e - pickLo] = a.bytes == 0 ? a.column : kNoColumn;
+        }
+    }
     for (unsigned i = startRow; i < rows; ++i) {
         uint8_t* row = mrow(i);
         const RecPacket* rec = rows_[i].rec;
@@ -1004,12 +1024,9 @@ bool DecoderCore::generate_matrix()
         // select {1, CX, CX^2} for the row sum, the high three the same for
         // the product, which is scaled by RX:  v = comb[op&7] ^ RX*comb[op>>3]
         const uint8_t rx = row_value(m.row);
-        uint8_t opLo[kLanes], opHi[kLanes];
-        for (unsigned lane = 0; lane < kLanes; ++lane) {
-            const unsigned op = row_opcode(lane, m.row);
-            opLo[lane] = (uint8_t)(op & 7);
-            opHi[lane] = (uint8_t)(op >> 3);
-        }
+        const RowSelect& sel = row_select(m.row);
+        const uint8_t* opLo = sel.opLo;
+        const uint8_t* opHi = sel.opHi;
         unsigned jEnd = startCol;
         while (jEnd < columns && column_sub(cols_[jEnd].column, m.columnStart) < m.sumCount)
             ++jEnd;
@@ -1023,10 +1040,11 @@ bool DecoderCore::generate_matrix()
         unsigned picks = 0;
         const uint32_t* off = ldpc_offsets(m.row, m.ldpcCount, &picks);
         const size_t rowOff = (size_t)i * matStride_;
+        const uint32_t* pc = pickCol_.data() + (rec->elementStart - pickLo);
         for (unsigned k = 0; k < picks; ++k) {
-            const DecSlot& a = slot(rec->elementStart + off[k]);
-            if (a.bytes == 0 && a.column >= startCol && rowOff + a.column < matBytes)
-                mat_[rowOff + a.column] ^= (k & 1) ? rx : 1;
+            const uint32_t c = pc[off[k]];
+            if (c != kNoColumn && c >= startCol && rowOff + c < matBytes)
+                mat_[rowOff + c] ^= (k & 1) ? rx : 1;
         }
     }
 
@@ -1133,6 +1151,15 @@ bool DecoderCore::pivoted_ge(unsigned pivot)
 bool DecoderCore::eliminate_original_data()
 {
     const unsigned rows = region_.recoveryCount;
+    // the current run of rows with one sum range (see below)
+    bool haveRun = false;
+    unsigned runStart = 0, runCount = 0, runEnd = 0, runBytes = 0, runSumStart = 0;
+    uint32_t fresh = 0;   // sums brought up to runEnd during this run
+    // the 24 sums as rows read them, rebuilt only after a sum may have changed
+    WinEntry sums[kRowSums];
+    uint32_t clip[kRowSums];   // min(sum bytes, row bytes): reference source bytes
+    uint32_t present = 0;      // sums holding bytes
+    bool tableStale = true;
     for (unsigned ri = 0; ri < rows; ++ri) {
         if (!rows_[ri].used)
             continue;
@@ -1156,47 +1183,70 @@ bool DecoderCore::eliminate_original_data()
             continue;
         }
 
+        // Rows of one decode usually share their sum range (a block of
+        // Siamese rows: same ColumnStart/SumCount/end/length).  The restart
+        // below is then a no-op for every row after the first, and only sums
+        // no earlier row of the run brought up to `ee` need the lazy walk.
+        const bool sameRun = haveRun && m.columnStart == runStart && m.sumCount == runCount &&
+                             ee == runEnd && rb == runBytes && recoveredColumns_.empty();
         unsigned sumElementStart = column_to_element(m.columnStart);
-        if (m.columnStart != sumColumnStart_ || m.sumCount < sumColumnCount_) {
-            if (sumElementStart >= count_)
-                return false;
-            reset_sums(sumElementStart);
-            sumColumnStart_ = m.columnStart;
-        } else {
-            if (sumElementStart >= count_)
-                sumElementStart = 0;
-            if (!start_sums(sumElementStart, rb))
-                return false;
+        if (!sameRun) {
+            if (m.columnStart != sumColumnStart_ || m.sumCount < sumColumnCount_) {
+                if (sumElementStart >= count_)
+                    return false;
+                reset_sums(sumElementStart);
+                sumColumnStart_ = m.columnStart;
+            } else {
+                if (sumElementStart >= count_)
+                    sumElementStart = 0;
+                if (!start_sums(sumElementStart, rb))
+                    return false;
+            }
+            sumColumnCount_ = m.sumCount;
+            haveRun = true;
+            runStart = m.columnStart;
+            runCount = m.sumCount;
+            runEnd = ee;
+            runBytes = rb;
+            fresh = 0;
+            tableStale = true;
+            runSumStart = sumElementStart;
         }
-        sumColumnCount_ = m.sumCount;
 
         // decoder sums first (their updates precede the batch's rows); the
         // row selects them by mask bit lane*3 + sum
-        windowLo_ = std::min(es, sumElementStart);
-        uint32_t mask[2] = {0, 0};
-        uint64_t opBytes = rb; // RX * product muladd
-        for (unsigned lane = 0; lane < kLanes; ++lane) {
-            const unsigned op = row_opcode(lane, m.row);
-            for (unsigned bit = 0; bit < 2 * kSums; ++bit) {
-                if (!(op & (1u << bit)))
-                    continue;
-                DevSum& s = get_sum(lane, bit % kSums, ee);
-                if (s.bytes > 0) {
-                    materialize(lane, bit % kSums);
-                    mask[bit / kSums] |= 1u << (lane * kSums + bit % kSums);
-                    opBytes += std::min(s.bytes, rb);
-                }
-            }
+        windowLo_ = std::min(es, runSumStart);
+        const RowSelect& sel = row_select(m.row);
+        const uint32_t want = sel.mask[0] | sel.mask[1];
+        uint32_t need = want & ~fresh;
+        if (need)
+            tableStale = true;   // a sum may grow below: rebuild the table
+        for (; need; need &= need - 1) {
+            const unsigned k = (unsigned)__builtin_ctz(need);
+            if (get_sum(k / kSums, k % kSums, ee).bytes > 0)
+                materialize(k / kSums, k % kSums);
         }
-        WinEntry sums[kRowSums];
-        for (unsigned lane = 0; lane < kLanes; ++lane)
-            for (unsigned s = 0; s < kSums; ++s) {
-                const DevSum& d = sum(lane, s).d;
-                WinEntry& t = sums[lane * kSums + s];
+        fresh |= want;
+        if (tableStale) {
+            tableStale = false;
+            present = 0;
+            for (unsigned k = 0; k < kRowSums; ++k) {
+                const DevSum& d = sum(k / kSums, k % kSums).d;
+                WinEntry& t = sums[k];
                 t.src = d.buf.addr();
                 t.len = d.bytes;
                 t.column = 0;
+                if (d.bytes > 0)
+                    present |= 1u << k;
+                clip[k] = std::min(d.bytes, rb);
             }
+        }
+        uint64_t opBytes = rb;  // RX * product muladd
+        for (uint32_t b = sel.mask[0] & present; b; b &= b - 1)
+            opBytes += clip[__builtin_ctz(b)];
+        for (uint32_t b = sel.mask[1] & present; b; b &= b - 1)
+            opBytes += clip[__builtin_ctz(b)];
+        const uint32_t mask[2] = {sel.mask[0] & present, sel.mask[1] & present};
         // LDPC pairs over received originals: drawn (and their reference
         // source bytes counted) on the device
         // rows of one decode share the sums: one row of the program's batch

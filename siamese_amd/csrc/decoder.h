@@ -236,6 +236,7 @@ private:
     // CX and CX^2, each padded by kRowSlack bytes
     static constexpr unsigned kRowSlack = 32;
     std::vector<uint8_t> colLane_, colCx_, colCx2_;
+    std::vector<uint32_t> pickCol_;   // generate_matrix: matrix column per element (or none)
     unsigned prevNextCheckStart_ = 0;
     std::vector<uint8_t> mat_;
     unsigned matRows_ = 0, matCols_ = 0, matAllocRows_ = 0, matStride_ = 0;

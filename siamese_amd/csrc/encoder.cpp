@@ -77,6 +77,7 @@ SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc
 
     nextColumn_ = column_add(nextColumn_, 1);
 
+    staleSums_ |= 7u << (column % kLanes * kSums);
     Lane& lane = lanes_[column % kLanes];
     if (lane.longest < s.bytes)
         lane.longest = s.bytes;
@@ -100,6 +101,8 @@ void EncoderCore::start_window(unsigned column)
     longest_ = 0;
     for (Lane& l : lanes_)
         l.longest = 0;
+    staleSums_ = kAllSums;
+    sumTableStale_ = true;
 }
 
 void EncoderCore::remove_before(unsigned firstKeptColumn)
@@ -132,6 +135,8 @@ void EncoderCore::reset_sums(unsigned elementStart)
     sumEnd_ = elementStart;
     sumColumnStart_ = element_to_column(elementStart);
     sumErased_ = 0;
+    staleSums_ = kAllSums;
+    sumTableStale_ = true;
 }
 
 void EncoderCore::remove_elements()
@@ -162,6 +167,8 @@ void EncoderCore::remove_elements()
     count_ -= removed;
     columnStart_ = element_to_column(removed);
     firstUnremoved_ -= removed;
+    staleSums_ = kAllSums;
+    sumTableStale_ = true;
 
     unsigned longest = 0;
     unsigned laneLongest[kLanes] = {0};
@@ -400,32 +407,41 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     // Dense part (:1046-1098): opcode bits 0-2 feed the row, 3-5 the product.
     // The lane sums are brought up to date first (their own ops precede the
     // row in the program); the row selects them by mask bit lane*3 + sum.
-    uint32_t mask[2] = {0, 0};
-    uint64_t opBytes = recoveryBytes; // final RX * product muladd
-    for (unsigned lane = 0; lane < kLanes; ++lane) {
-        const unsigned opcode = row_opcode(lane, row);
-        for (unsigned bit = 0; bit < 2 * kSums; ++bit) {
-            if (!(opcode & (1u << bit)))
-                continue;
-            DevSum& sum = get_sum(lane, bit % kSums, count_);
-            if (dead())
-                return Siamese_Disabled;
-            if (sum.bytes > 0) {
-                mask[bit / kSums] |= 1u << (lane * kSums + bit % kSums);
-                opBytes += std::min(sum.bytes, recoveryBytes);
-            }
-        }
+    // Only sums that may have fallen behind since they were last folded
+    // (staleSums_) are visited, so consecutive rows over an unchanged window
+    // skip the lazy-update walk.
+    const RowSelect& sel = row_select(row);
+    const uint32_t want = sel.mask[0] | sel.mask[1];
+    uint32_t need = want & staleSums_;
+    if (need)
+        sumTableStale_ = true;   // a sum may grow below
+    for (; need; need &= need - 1) {
+        const unsigned k = (unsigned)__builtin_ctz(need);
+        get_sum(k / kSums, k % kSums, count_);
+        if (dead())
+            return Siamese_Disabled;
     }
-    sumEnd_ = count_;
-    WinEntry sums[kRowSums];
-    for (unsigned lane = 0; lane < kLanes; ++lane)
-        for (unsigned s = 0; s < kSums; ++s) {
-            const DevSum& d = lanes_[lane].sum[s];
-            WinEntry& t = sums[lane * kSums + s];
+    staleSums_ &= ~want;
+    if (sumTableStale_) {
+        // the 24 sums as the rows read them (rebuilt only after a change)
+        sumTableStale_ = false;
+        sumPresent_ = 0;
+        for (unsigned k = 0; k < kRowSums; ++k) {
+            const DevSum& d = lanes_[k / kSums].sum[k % kSums];
+            WinEntry& t = sumTable_[k];
             t.src = d.buf.addr();
             t.len = d.bytes;
             t.column = 0;
+            if (d.bytes > 0)
+                sumPresent_ |= 1u << k;
         }
+    }
+    const uint32_t mask[2] = {sel.mask[0] & sumPresent_, sel.mask[1] & sumPresent_};
+    uint64_t opBytes = recoveryBytes; // final RX * product muladd
+    for (unsigned h = 0; h < 2; ++h)
+        for (uint32_t b = mask[h]; b; b &= b - 1)
+            opBytes += std::min(sumTable_[__builtin_ctz(b)].len, recoveryBytes);
+    sumEnd_ = count_;
 
     RowMeta m;
     m.sumCount = sumEnd_ - sumStart_ + sumErased_;
@@ -443,7 +459,7 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     // Recovery = row sums ^ RX * product (:1232-1233) and its footer: one row
     // of the program's Siamese row batch (consecutive rows share the sums)
     cover(std::min(start, sumStart_), sumEnd_);
-    prog_.rows_row(sums, recovery_.addr(), recoveryBytes, 0, row_value(row), mask[0], mask[1], row,
+    prog_.rows_row(sumTable_, recovery_.addr(), recoveryBytes, 0, row_value(row), mask[0], mask[1], row,
                    n, start, footer, footerBytes);
     eng_->account(opBytes);
 

@@ -147,6 +147,15 @@ private:
         unsigned longest = 0;
     } lanes_[kLanes];
 
+    // sums (bit lane*3 + s) that may lag the window: set when an original
+    // lands in their lane or the sums restart, cleared once a row folds them
+    static constexpr uint32_t kAllSums = (1u << kRowSums) - 1;
+    uint32_t staleSums_ = kAllSums;
+    // the sums as rows read them (WinEntry per bit), valid unless stale
+    WinEntry sumTable_[kRowSums];
+    uint32_t sumPresent_ = 0;   // sums holding bytes
+    bool sumTableStale_ = true;
+
     DevBuf recovery_;          // reused recovery packet buffer
     unsigned nextRow_ = 0;
     unsigned nextParityColumn_ = 0;

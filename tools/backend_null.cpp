@@ -1,0 +1,98 @@
+// tools/backend_null.cpp -- PROFILING AID ONLY (never shipped, never tested
+// against).  A backend.h implementation whose launches do no symbol work, so
+// a bench run on the CPU measures the host control plane alone: stepping
+// codecs, flush assembly and completions.
+//
+// The control plane only reads one thing back from the device: the
+// recovered length words of each solve.  Here every solve reports all m rows
+// valid with a 2-byte prefix and NULLSIM_LEN payload bytes (default 1400), so
+// fixed-size workloads (C4, C2, C3) take the same control flow as on the GPU.
+// Symbol bytes are garbage: run bench.py with verification off
+// (--no-verify is implied by the digest-free timed steps).
+#include "../siamese_amd/csrc/backend.h"
+#include "../siamese_amd/csrc/gf.h"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace sgpu {
+
+namespace {
+
+// the last upload: device range -> host source (launch arguments point into it)
+const uint8_t* g_upHost = nullptr;
+uint8_t* g_upDev = nullptr;
+size_t g_upBytes = 0;
+uint32_t g_len = 1400;
+
+template <class T>
+const T* host_view(const T* dev)
+{
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(dev);
+    if (p >= g_upDev && p < g_upDev + g_upBytes)
+        return reinterpret_cast<const T*>(g_upHost + (p - g_upDev));
+    return dev;
+}
+
+} // namespace
+
+bool be_init(int, const char** err)
+{
+    if (!gf_init()) {
+        *err = "gf_init failed";
+        return false;
+    }
+    if (const char* s = std::getenv("NULLSIM_LEN"))
+        g_len = (uint32_t)std::strtoul(s, nullptr, 10);
+    return true;
+}
+
+const char* be_name() { return "null (profiling only)"; }
+
+void* be_dev_alloc(size_t bytes)
+{
+    void* p = nullptr;
+    if (posix_memalign(&p, 256, bytes) != 0)
+        return nullptr;
+    return p;
+}
+void be_dev_free(void* p) { std::free(p); }
+void* be_host_alloc(size_t bytes) { return be_dev_alloc(bytes); }
+void be_host_free(void* p) { std::free(p); }
+void be_h2d(void* dst, const void* src, size_t bytes)
+{
+    // a DMA on the GPU: remember the mapping instead of copying
+    g_upDev = (uint8_t*)dst;
+    g_upHost = (const uint8_t*)src;
+    g_upBytes = bytes;
+}
+void be_d2h(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
+void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
+
+void be_launch_ingest(const IngestDesc*, uint32_t) {}
+void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*) {}
+
+void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow*, const uint8_t*,
+                            uint32_t* results, uint32_t count)
+{
+    const SolveDesc* sd = host_view(solves);
+    for (uint32_t s = 0; s < count; ++s) {
+        uint32_t* out = results + sd[s].result;
+        out[0] = sd[s].m;
+        for (uint32_t i = 0; i < sd[s].m; ++i)
+            out[1 + i] = (2u << 29) | g_len;
+    }
+}
+
+void be_launch_solve_main(const SolveDesc*, const SolveRow*, const uint8_t*, const uint32_t*,
+                          const SolveItem*, uint32_t, uint32_t)
+{
+}
+
+bool be_sync() { return true; }
+void be_timing_enable(bool) {}
+void be_timing_reset() {}
+double be_timing_exec_ms() { return 0; }
+double be_timing_total_ms() { return 0; }
+
+} // namespace sgpu
