@@ -396,7 +396,7 @@ def main(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--threads", type=int, default=0,
                     help="host threads driving streams (0 = library default)")
-    ap.add_argument("--groups", type=int, default=2,
+    ap.add_argument("--groups", type=int, default=4,
                     help="stream groups alternating host and device work (1 = no overlap)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip the PCIe-inclusive end-to-end leg")

@@ -83,6 +83,10 @@ struct Api
     SiameseResult (*decoder_get)(SgpuDecoder, SiameseOriginalPacket*);
     int (*flush)(void);
     int (*submit)(void);
+    long long (*enqueue)(void);
+    int (*wait)(long long);
+    int (*query)(long long);
+    void (*parallel_for)(unsigned, void (*)(void*, unsigned), void*);
     void* (*device_alloc)(size_t);
     void (*device_free)(void*);
     void* (*host_alloc)(size_t);
@@ -119,6 +123,9 @@ bool load_api(const char* path, Api& a)
            bind(h, a.decoder_add_recovery, "sgpu_decoder_add_recovery") &&
            bind(h, a.decoder_is_ready, "sgpu_decoder_is_ready") && bind(h, a.decode, "sgpu_decode") &&
            bind(h, a.decoder_get, "sgpu_decoder_get") && bind(h, a.flush, "sgpu_flush") && bind(h, a.submit, "sgpu_submit") &&
+           bind(h, a.enqueue, "sgpu_enqueue") && bind(h, a.wait, "sgpu_wait") &&
+           bind(h, a.query, "sgpu_query") &&
+           bind(h, a.parallel_for, "sgpu_parallel_for") &&
            bind(h, a.device_alloc, "sgpu_device_alloc") && bind(h, a.device_free, "sgpu_device_free") &&
            bind(h, a.host_alloc, "sgpu_host_alloc") && bind(h, a.host_free, "sgpu_host_free") &&
            bind(h, a.h2d, "sgpu_h2d") && bind(h, a.gather, "sgpu_gather") &&
@@ -297,32 +304,43 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
     reqs.clear();
 }
 
-// fn(i) for i in [0, count), blocks of a few streams per pool task
+// fn(i) for i in [0, count), blocks of a few streams per pool task: on the
+// library's host threads (sgpu_parallel_for) unless the run asked for its
+// own thread count
 template <class F>
 void for_streams(Shared& sh, size_t count, const F& fn)
 {
     constexpr size_t kBlock = 4;
-    sh.pool->run((count + kBlock - 1) / kBlock, [&](size_t b) {
+    const size_t blocks = (count + kBlock - 1) / kBlock;
+    auto body = [&](size_t b) {
         const size_t end = std::min(count, (b + 1) * kBlock);
         for (size_t i = b * kBlock; i < end; ++i)
             fn(i);
-    });
+    };
+    if (sh.pool) {
+        sh.pool->run(blocks, body);
+        return;
+    }
+    using Body = decltype(body);
+    sh.api->parallel_for((unsigned)blocks,
+                         [](void* ctx, unsigned b) { (*static_cast<const Body*>(ctx))(b); },
+                         (void*)&body);
 }
 
 // One job = one contiguous group of a step's streams.  Jobs flow through a
-// pipeline so that the host work of one job overlaps the device work of the
-// previous flush: every iteration advances the jobs whose device work has
-// completed (round two and later: deliveries after a decode), starts the next
-// job (round one: adds, encodes, decodes), and submits.  sgpu_submit()
-// completes the previous flush before launching the new one, so work queued
-// before submit k is final once submit k+1 has returned.
+// pipeline so that the host work of one job overlaps the device work (and
+// the library's launch and completion work) of the others: every iteration
+// takes each active job in turn, waits for its last submission, advances its
+// streams (round two and later: deliveries after a decode) and submits
+// again without waiting (sgpu_enqueue); a new job (round one: adds, encodes,
+// decodes) starts while the pipeline is shallow.
 struct Job
 {
     unsigned step = 0, begin = 0, end = 0;
     std::vector<BatchCodec> codecs;
     std::unique_ptr<BatchStream[]> streams;
     std::vector<unsigned> live;     // indices into codecs/streams
-    uint64_t readyAfter = 0;        // submits after which its device work is final
+    long long ticket = 0;           // its latest submission
 };
 
 int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* rounds,
@@ -341,8 +359,8 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
         const auto now = Clock::now();
         phase[k] += std::chrono::duration<double>(now - t).count();
         if (timeline)
-            std::fprintf(stderr, "tl %8.3f %8.3f ms  %s j%d\n",
-                         std::chrono::duration<double>(t - t00).count() * 1e3,
+            std::fprintf(stderr, "tl %10.3f %8.3f ms  %s j%d\n",
+                         std::chrono::duration<double>(t.time_since_epoch()).count() * 1e3,
                          std::chrono::duration<double>(now - t).count() * 1e3,
                          k == 0 ? "create" : k == 1 ? "step" : k == 2 ? "flush" : k == 3 ? "resolve" : "finish",
                          curJob);
@@ -383,6 +401,13 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
         for (BatchCodec& c : J.codecs)
             std::swap(c.prev, c.cur);
     };
+    auto submit = [&](Job& J) {
+        J.ticket = api.enqueue();
+        if (timeline)
+            std::fprintf(stderr, "tl submit j%d t%lld live %zu\n", curJob, J.ticket, J.live.size());
+        ++*rounds;
+        return J.ticket >= 0;
+    };
     auto dump = [&](Job& J) {
         // debugging aid: SCENARIO_DUMP="<stream index>:<path>" writes that
         // stream's event log (same format as scenario_run_capi's)
@@ -400,49 +425,56 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
     };
 
     const unsigned jobs = nsteps * G;
+    const size_t depth = G + 1;   // jobs in flight
     std::vector<std::unique_ptr<Job>> active;
-    uint64_t seq = 0;
     unsigned next = 0;
     int rc = 0;
+    // Host work is done whenever some is available: a job whose submission
+    // has completed is advanced (or retired), a new job starts (round one,
+    // the bulk of a step's host work) while the pipeline is shallow; the
+    // thread blocks only when neither is possible.
     while (rc == 0 && (next < jobs || !active.empty())) {
-        // 1. jobs whose device work is final: resolve, advance, retire
-        for (auto& jp : active) {
-            Job& J = *jp;
-            if (seq < J.readyAfter)
-                continue;
+        bool did = false;
+        for (size_t k = 0; k < active.size() && rc == 0;) {
+            Job& J = *active[k];
             curJob = (int)(J.step * G + J.begin);
+            const int q = api.query(J.ticket);
+            if (q < 0) {
+                rc = -3;
+                break;
+            }
+            if (q == 0) {
+                ++k;
+                continue;
+            }
+            did = true;
             std::vector<Request> reqs = take(J, true);
             resolve_requests(sh, reqs);
             lap(3);
             if (!J.live.empty()) {
                 advance(J);
-                J.readyAfter = seq + 2;
                 lap(1);
-            }
-        }
-        for (size_t k = 0; k < active.size();) {
-            Job& J = *active[k];
-            if (J.live.empty() && seq >= J.readyAfter) {
-                std::vector<Request> reqs = take(J, true);
-                resolve_requests(sh, reqs);
-                reqs = take(J, false);
-                resolve_requests(sh, reqs);
-                for_streams(sh, J.end - J.begin, [&](size_t i) {
-                    J.streams[i].finish();
-                    api.encoder_free(J.codecs[i].enc);   // (null if freed already)
-                    api.decoder_free(J.codecs[i].dec);
-                    J.codecs[i].enc = nullptr;
-                    J.codecs[i].dec = nullptr;
-                });
-                dump(J);
-                active.erase(active.begin() + (long)k);
-                lap(4);
-            } else {
+                if (!submit(J))
+                    rc = -3;
+                lap(2);
                 ++k;
+                continue;
             }
+            reqs = take(J, false);
+            resolve_requests(sh, reqs);
+            for_streams(sh, J.end - J.begin, [&](size_t i) {
+                J.streams[i].finish();
+                api.encoder_free(J.codecs[i].enc);   // (null if freed already)
+                api.decoder_free(J.codecs[i].dec);
+                J.codecs[i].enc = nullptr;
+                J.codecs[i].dec = nullptr;
+            });
+            dump(J);
+            active.erase(active.begin() + (long)k);
+            lap(4);
         }
-        // 2. start the next job (round one) while the pipeline is shallow
-        if (next < jobs && active.size() < 3) {
+        if (rc == 0 && next < jobs && active.size() < depth) {
+            did = true;
             std::unique_ptr<Job> jp(new Job);
             Job& J = *jp;
             J.step = next / G;
@@ -475,16 +507,18 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 J.live.push_back(i);
             lap(0);
             advance(J);
-            J.readyAfter = seq + 2;
             lap(1);
+            if (!submit(J))
+                rc = -3;
+            lap(2);
             active.push_back(std::move(jp));
         }
-        // 3. launch what the jobs queued (completing the previous flush first)
-        if (api.submit() != 0)
-            rc = -3;
-        ++seq;
-        ++*rounds;
-        lap(2);
+        if (rc == 0 && !did && !active.empty()) {
+            // nothing to do until the oldest submission completes
+            if (api.wait(active.front()->ticket) != 0)
+                rc = -3;
+            lap(2);
+        }
     }
     if (api.flush() != 0)
         rc = -3;
@@ -598,9 +632,11 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         const bool timed = r >= opt->warmup;
         sh.verify = opt->verify && r == 0;
         sh.digest = opt->digest != 0;
-        const unsigned threads = opt->threads ? opt->threads : sgpu::WorkerPool::default_threads();
-        if (!sh.pool || sh.pool->size() != threads)
-            sh.pool.reset(new sgpu::WorkerPool(threads));
+        // streams run on the library's host threads unless a count is requested
+        if (opt->threads == 0)
+            sh.pool.reset();
+        else if (!sh.pool || sh.pool->size() != opt->threads)
+            sh.pool.reset(new sgpu::WorkerPool(opt->threads));
         sh.groups = opt->groups ? opt->groups : 1;
         uint64_t rounds = 0;
         double phase[5] = {0, 0, 0, 0, 0};

@@ -21,9 +21,16 @@
     Threading: instances may be driven from many host threads at once, each
     instance by one thread at a time (handing a recovery packet to a decoder
     also touches the encoder that produced it).  Per-instance calls take no
-    global lock.  sgpu_init, sgpu_flush, sgpu_submit, sgpu_gather, sgpu_h2d,
-    and sgpu_decoder_get on a packet whose length is still pending (it
-    flushes) must not run concurrently with any other call.
+    global lock.  sgpu_init, sgpu_flush, sgpu_submit, sgpu_enqueue,
+    sgpu_gather, sgpu_h2d, and sgpu_decoder_get on a packet whose length is
+    still pending (it flushes) must not run concurrently with any other call.
+
+    Pipelined submission: sgpu_enqueue() hands all queued work to the
+    library's launcher thread and returns a ticket at once; sgpu_wait(ticket)
+    returns when that submission (and every earlier one) has run on the GPU
+    and its results are delivered.  sgpu_wait may run while other threads
+    drive instances; an instance with work in a submission must not be called
+    again until that submission has been waited for.
 */
 #ifndef SIAMESE_GPU_H
 #define SIAMESE_GPU_H
@@ -78,8 +85,23 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_has(SgpuDecoder decoder, unsigned pack
 
 /// Submit all queued device work of every instance and wait for it.
 SIAMESE_EXPORT int sgpu_flush(void);
-/// Submit without waiting (the next sgpu_flush completes it).
+/// Submit, then complete the previous submission (one submission in flight).
 SIAMESE_EXPORT int sgpu_submit(void);
+/// Submit without waiting: returns the submission's ticket (>= 0; 0 when
+/// nothing was ever queued), -1 once the device has failed.
+SIAMESE_EXPORT long long sgpu_enqueue(void);
+/// Wait for submission `ticket` and every earlier one; nonzero on a device
+/// failure (sticky: every instance reports Siamese_Disabled afterwards).
+SIAMESE_EXPORT int sgpu_wait(long long ticket);
+/// Non-blocking: 1 if submission `ticket` has completed (as sgpu_wait would
+/// return), 0 if it is still in flight, -1 once the device has failed.
+SIAMESE_EXPORT int sgpu_query(long long ticket);
+/// Run fn(ctx, i) for i in [0, count) on the library's host worker threads
+/// (the caller takes part) and return when all calls are done.  Lets an
+/// application drive many instances on the threads the library placed next
+/// to the GPU.
+SIAMESE_EXPORT void sgpu_parallel_for(unsigned count, void (*fn)(void* ctx, unsigned index),
+                                      void* ctx);
 
 /// Device memory helpers for applications and the benchmark harness.
 SIAMESE_EXPORT void* sgpu_device_alloc(size_t bytes);

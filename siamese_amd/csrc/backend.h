@@ -31,8 +31,11 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count);
 /// `acct`: device counter the executor adds the reference's source bytes of
 /// the terms it expands itself (sum updates, LDPC picks) to (ops.h).
 void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct);
+/// `acct`: acct[0] += the reference's source bytes of each back-substitution
+/// step the solve completes (SiameseDecoder.cpp:1131-1212), acct[1] += the
+/// recovered bytes it outputs.
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                            uint32_t* results, uint32_t count);
+                            uint32_t* results, uint32_t count, uint64_t* acct);
 /// maxRows: largest m among the solves this launch covers (sizes LDS staging).
 void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
                           const uint32_t* results, const SolveItem* items, uint32_t count,
@@ -40,6 +43,13 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
 
 /// Block until all queued work has finished.  Returns false on a device fault.
 bool be_sync();
+
+/// A marker after all work queued so far.  be_fence_wait blocks (sleeping,
+/// not spinning) until the device has passed it, returns false on a device
+/// fault, and releases it.  The launcher thread creates fences, the
+/// completer thread waits for them.
+void* be_fence();
+bool be_fence_wait(void* fence);
 
 /// Device-time accounting: every executor/solve launch is bracketed with
 /// events; these return the accumulated milliseconds since the last reset.

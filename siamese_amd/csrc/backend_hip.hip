@@ -24,6 +24,8 @@
 #include <cstdio>
 #include <string>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <vector>
 
 namespace sgpu {
@@ -649,7 +651,8 @@ __device__ __forceinline__ int parse_prefix(uint32_t w, uint32_t avail, uint32_t
 __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict__ solves,
                                                      const SolveRow* __restrict__ rows,
                                                      const uint8_t* __restrict__ coef,
-                                                     uint32_t* __restrict__ results)
+                                                     uint32_t* __restrict__ results,
+                                                     unsigned long long* __restrict__ acct)
 {
     __shared__ uint32_t P[256];
     __shared__ uint32_t X;
@@ -679,8 +682,12 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
         __syncthreads();
     }
 
-    // BackSubstitution on bytes 0..3 (reference SiameseDecoder.cpp:1106-1238)
+    // BackSubstitution on bytes 0..3 (reference SiameseDecoder.cpp:1106-1238).
+    // Each completed step also counts the reference's source bytes: the
+    // diagonal scaling of max(32 clipped, recovered) bytes and one muladd of
+    // min(recovered, row) bytes per earlier row it eliminates (:1131-1212).
     uint32_t ok = 0;
+    unsigned long long opAcc = 0, outAcc = 0;
     for (int i = (int)m - 1; i >= 0; --i) {
         if (lane == 0) {
             const uint32_t fb = R[i].finalBytes;
@@ -695,6 +702,8 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
                 out[1 + i] = ((uint32_t)h << 29) | len;
                 bb = (uint32_t)h + len;
                 X = x & byte_mask((int)bb);
+                opAcc += lc > bb ? lc : bb;
+                outAcc += bb;
             }
         }
         __syncthreads();
@@ -707,12 +716,17 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
             if (c) {
                 const uint32_t ab = b < R[j].finalBytes ? b : R[j].finalBytes;
                 P[j] ^= gf_mul_dword(xi & byte_mask((int)ab), c);
+                opAcc += ab;
             }
         }
         __syncthreads();
     }
     if (lane == 0)
         out[0] = ok;
+    if (opAcc)
+        atomicAdd(&acct[0], opAcc);
+    if (outAcc)
+        atomicAdd(&acct[1], outAcc);
 }
 
 // k_solve_main: one workgroup of kSolveWaves waves per (solve, 1 KiB tile).
@@ -983,18 +997,27 @@ struct EvPair
     hipEvent_t a, b;
     bool exec;
 };
-std::vector<EvPair> g_evFree, g_evUsed;
+// Launches come from the engine's launcher thread, fence waits from its
+// completer thread: the event lists are shared under g_evMu.
+std::mutex g_evMu;
+std::vector<EvPair> g_evFree;
+std::deque<EvPair> g_evUsed;
+std::vector<hipEvent_t> g_fenceFree;
 
 EvPair take_events(bool exec)
 {
     EvPair e;
-    if (!g_evFree.empty()) {
-        e = g_evFree.back();
-        g_evFree.pop_back();
-    } else {
-        (void)hipEventCreate(&e.a);
-        (void)hipEventCreate(&e.b);
+    {
+        std::lock_guard<std::mutex> g(g_evMu);
+        if (!g_evFree.empty()) {
+            e = g_evFree.back();
+            g_evFree.pop_back();
+            e.exec = exec;
+            return e;
+        }
     }
+    (void)hipEventCreate(&e.a);
+    (void)hipEventCreate(&e.b);
     e.exec = exec;
     return e;
 }
@@ -1015,10 +1038,30 @@ struct Timed
     {
         if (on) {
             (void)hipEventRecord(ev.b, g_stream);
+            std::lock_guard<std::mutex> g(g_evMu);
             g_evUsed.push_back(ev);
         }
     }
 };
+
+// Fold the timing events that have completed (in stream order) into the
+// totals.  all = true after a full stream synchronisation.
+void harvest_timing(bool all)
+{
+    std::lock_guard<std::mutex> g(g_evMu);
+    while (!g_evUsed.empty()) {
+        const EvPair& ev = g_evUsed.front();
+        if (!all && hipEventQuery(ev.b) != hipSuccess)
+            break;
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ev.a, ev.b);
+        g_totalMs += ms;
+        if (ev.exec)
+            g_execMs += ms;
+        g_evFree.push_back(ev);
+        g_evUsed.pop_front();
+    }
+}
 
 void check(hipError_t e, const char* what)
 {
@@ -1202,11 +1245,11 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                            uint32_t* results, uint32_t count)
+                            uint32_t* results, uint32_t count, uint64_t* acct)
 {
     Timed t(false);
     hipLaunchKernelGGL(k_solve_prefix, dim3(count), dim3(64), 0, g_stream, solves, rows, coef,
-                       results);
+                       results, reinterpret_cast<unsigned long long*>(acct));
 }
 
 void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
@@ -1230,15 +1273,42 @@ bool be_sync()
         check(e, "hipStreamSynchronize");
         return false;
     }
-    for (const EvPair& ev : g_evUsed) {
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, ev.a, ev.b);
-        g_totalMs += ms;
-        if (ev.exec)
-            g_execMs += ms;
-        g_evFree.push_back(ev);
+    harvest_timing(true);
+    return true;
+}
+
+void* be_fence()
+{
+    bind_device();
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_evMu);
+        if (!g_fenceFree.empty()) {
+            e = g_fenceFree.back();
+            g_fenceFree.pop_back();
+        }
     }
-    g_evUsed.clear();
+    if (!e && hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    if (hipEventRecord(e, g_stream) != hipSuccess)
+        return nullptr;
+    return e;
+}
+
+bool be_fence_wait(void* fence)
+{
+    bind_device();
+    if (!fence)
+        return false;
+    hipEvent_t e = static_cast<hipEvent_t>(fence);
+    const hipError_t r = hipEventSynchronize(e);
+    if (r != hipSuccess) {
+        check(r, "hipEventSynchronize");
+        return false;
+    }
+    harvest_timing(false);
+    std::lock_guard<std::mutex> g(g_evMu);
+    g_fenceFree.push_back(e);
     return true;
 }
 

@@ -8,6 +8,7 @@
 #include "decoder.h"
 #include "encoder.h"
 #include "engine.h"
+#include "pool.h"
 
 #include <cstdio>
 #include <cstring>
@@ -193,6 +194,37 @@ SIAMESE_EXPORT int sgpu_submit(void)
     Engine* eng = Engine::global();
     Lock lock(eng->mutex());
     return eng->flush() ? 0 : -1;
+}
+
+SIAMESE_EXPORT long long sgpu_enqueue(void)
+{
+    Engine* eng = Engine::global();
+    Lock lock(eng->mutex());
+    const uint64_t t = eng->enqueue();
+    return eng->failed() ? -1 : (long long)t;
+}
+
+SIAMESE_EXPORT int sgpu_wait(long long ticket)
+{
+    // no engine lock: other threads keep driving instances meanwhile
+    if (ticket < 0)
+        return -1;
+    return Engine::global()->wait((uint64_t)ticket) ? 0 : -1;
+}
+
+SIAMESE_EXPORT int sgpu_query(long long ticket)
+{
+    Engine* eng = Engine::global();
+    if (ticket < 0 || eng->failed())
+        return -1;
+    return eng->done((uint64_t)ticket) ? 1 : 0;
+}
+
+SIAMESE_EXPORT void sgpu_parallel_for(unsigned count, void (*fn)(void* ctx, unsigned index), void* ctx)
+{
+    if (!fn)
+        return;
+    Engine::global()->pool().run(count, [&](size_t i) { fn(ctx, (unsigned)i); });
 }
 
 SIAMESE_EXPORT void* sgpu_device_alloc(size_t bytes)

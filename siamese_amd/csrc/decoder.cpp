@@ -1349,25 +1349,9 @@ SiameseResult DecoderCore::solve_and_substitute()
     std::weak_ptr<int> alive = alive_;
     const uint64_t serial = decodeSerial_;
     pendingSolves_++;
-    Engine* eng = eng_;
-    std::vector<unsigned> finals(len.begin(), len.end());
-    prog_.on_complete([this, alive, fixes, base, m, serial, coef, finals, eng](const uint32_t* results) {
-        // Back-substitution bytes of the reference (:1131-1212) need the
-        // recovered lengths, so they are counted once those are known.
-        const unsigned ok = results[base];
-        uint64_t opBytes = 0, outBytes = 0;
-        for (unsigned k = 0; k < ok && k < m; ++k) {
-            const unsigned i = m - 1 - k;
-            const uint32_t w = results[base + 1 + i];
-            const unsigned bb = (w >> 29) + (w & kSolveLengthMask);
-            const unsigned lc = std::min(32u, finals[i]);
-            opBytes += std::max(lc, bb);
-            outBytes += bb;
-            for (unsigned j = 0; j < i; ++j)
-                if (coef[(size_t)j * m + i])
-                    opBytes += std::min(bb, finals[j]);
-        }
-        eng->account(opBytes, outBytes, true);
+    // (the back-substitution's reference source bytes need the recovered
+    // lengths: the solve kernel counts them, SiameseDecoder.cpp:1131-1212)
+    prog_.on_complete([this, alive, fixes, base, m, serial](const uint32_t* results) {
         if (alive.expired())
             return;
         resolve_solve(results, base, m, fixes, serial);

@@ -1,4 +1,5 @@
-// engine.cpp -- arena, programs and flush (see engine.h).
+// engine.cpp -- arena, programs and the asynchronous flush pipeline (see
+// engine.h).
 #include "engine.h"
 #include "backend.h"
 #include "pool.h"
@@ -7,9 +8,10 @@
 #include <chrono>
 #include <cstdio>
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 
-// dispatch each exec phase's segments longest op list first (see flush)
+// dispatch each exec phase's segments longest op list first (see launch_batch)
 #ifndef SGPU_EXEC_LPT
 #define SGPU_EXEC_LPT 1
 #endif
@@ -44,72 +46,158 @@ uint64_t now_ns()
         .count();
 }
 
+inline size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+
 } // namespace
+
+// ---------------------------------------------------------------------------
+// ProgramBody
+
+namespace {
+std::mutex g_bodyMu;
+std::vector<ProgramBody*> g_bodies;   // cleared bodies ready for reuse
+} // namespace
+
+ProgramBody* ProgramBody::get()
+{
+    {
+        std::lock_guard<std::mutex> g(g_bodyMu);
+        if (!g_bodies.empty()) {
+            ProgramBody* b = g_bodies.back();
+            g_bodies.pop_back();
+            return b;
+        }
+    }
+    return new ProgramBody;
+}
+
+void ProgramBody::put(ProgramBody* b)
+{
+    b->clear();
+    std::lock_guard<std::mutex> g(g_bodyMu);
+    if (g_bodies.size() < (1u << 15))
+        g_bodies.push_back(b);
+    else
+        delete b;
+}
+
+void ProgramBody::clear()
+{
+    for (size_t k = 0; k < nsegs; ++k)
+        segs[k].clear();
+    nsegs = 0;
+    resultWords = 0;
+    solves.clear();
+    callbacks.clear();
+    rb.open = false;
+    rb.win.clear();
+    rb.updates.clear();
+    rb.rows.clear();
+    copies.clear();
+}
+
+void ProgramBody::new_segment()
+{
+    rows_close();
+    if (nsegs == segs.size())
+        segs.emplace_back();
+    segs[nsegs++].clear();
+}
+
+void ProgramBody::rows_open(uint32_t base, bool keepWindow)
+{
+    rows_close();
+    if (nsegs == 0)
+        new_segment();
+    rb.open = true;
+    rb.haveSums = false;
+    rb.readMask = 0;
+    if (!keepWindow) {
+        rb.base = base;
+        rb.win.clear();
+    }
+    rb.updates.clear();
+    for (int& u : rb.updateOf)
+        u = -1;
+    rb.rows.clear();
+    rb.maxExtent = 0;
+}
+
+void ProgramBody::rows_close()
+{
+    if (!copies.empty()) {
+        // seal the open copy batch
+        Segment& g = segs[nsegs - 1];
+        GfOp op;
+        std::memset(&op, 0, sizeof(op));
+        op.kind = OP_COPIES;
+        op.n = (uint32_t)copies.size();
+        op.termBegin = (uint32_t)(g.rowsData.size() / 16);
+        op.termCount = (uint32_t)copies.size() * kCopyWords;
+        g.ops.push_back(op);
+        const size_t at = g.rowsData.size();
+        g.rowsData.resize(at + copies.size() * sizeof(CopyItem));
+        std::memcpy(g.rowsData.data() + at, copies.data(), copies.size() * sizeof(CopyItem));
+        g.rowsWords += op.termCount;
+        copies.clear();
+    }
+    RowsBuild& b = rb;
+    if (!b.open)
+        return;
+    b.open = false;
+    if (b.rows.empty() && b.updates.empty())
+        return;
+    if (!b.haveSums)
+        std::memset(b.sums, 0, sizeof(b.sums));
+    Segment& s = segs[nsegs - 1];
+    const uint32_t E = (uint32_t)b.win.size();
+    const uint32_t U = (uint32_t)b.updates.size();
+    const uint32_t R = (uint32_t)b.rows.size();
+    const uint32_t words = kRowSums + E + U * kUpdateWords + R * kRowWords;
+    GfOp op;
+    std::memset(&op, 0, sizeof(op));
+    op.kind = OP_ROWS;
+    op.n = R;
+    op.valid = E;
+    op.mix = U;
+    op.termBegin = (uint32_t)(s.rowsData.size() / 16);   // block offset in words
+    op.termCount = words;
+    s.ops.push_back(op);
+    const size_t at = s.rowsData.size();
+    s.rowsData.resize(at + (size_t)words * 16);
+    uint8_t* w = s.rowsData.data() + at;
+    std::memcpy(w, b.sums, sizeof(b.sums));
+    w += sizeof(b.sums);
+    std::memcpy(w, b.win.data(), (size_t)E * sizeof(WinEntry));
+    w += (size_t)E * sizeof(WinEntry);
+    std::memcpy(w, b.updates.data(), (size_t)U * sizeof(SumUpdate));
+    w += (size_t)U * sizeof(SumUpdate);
+    std::memcpy(w, b.rows.data(), (size_t)R * sizeof(RowItem));
+    s.rowsWords += words;
+    if (b.maxExtent > s.maxExtent)
+        s.maxExtent = b.maxExtent;
+}
 
 // ---------------------------------------------------------------------------
 // Program
 
-std::vector<Program::Store>& Program::spare_stores()
-{
-    thread_local std::vector<Store> spare;
-    return spare;
-}
-
-void Program::take_store()
-{
-    std::vector<Store>& spare = spare_stores();
-    if (spare.empty())
-        return;
-    Store& st = spare.back();
-    segs_.swap(st.segs);
-    rb_.win.swap(st.win);
-    rb_.updates.swap(st.updates);
-    rb_.rows.swap(st.rows);
-    spare.pop_back();
-}
-
-void Program::stash_store()
-{
-    std::vector<Store>& spare = spare_stores();
-    if (spare.size() >= 4096)
-        return;
-    for (Segment& g : segs_) {
-        g.ops.clear();
-        g.terms.clear();
-        g.rowsData.clear();
-    }
-    rb_.win.clear();
-    rb_.updates.clear();
-    rb_.rows.clear();
-    spare.emplace_back();
-    Store& st = spare.back();
-    st.segs.swap(segs_);
-    st.win.swap(rb_.win);
-    st.updates.swap(rb_.updates);
-    st.rows.swap(rb_.rows);
-}
-
 Program::~Program()
 {
     if (!shard_) {
-        stash_store();
+        if (b_)
+            ProgramBody::put(b_);
         return;
     }
-    rows_close();
     // The instance goes away with work still queued (e.g. an encoder freed
     // right after its last recovery packet was handed to a decoder, whose
-    // copy op lives in this program).  The queued ops still run: hand them
-    // to an orphan program the engine deletes after the next flush.  The
+    // copy op lives in this program).  The queued ops still run: hand the
+    // body to an orphan program the next submission takes and deletes.  The
     // buffers they touch were released by the instance and are not reused
-    // before that flush completes.
-    Program* orphan = new Program(eng_, group_);
+    // before that submission completes.
+    Program* orphan = new Program(eng_, group_ | 2);   // bit 1: delete when submitted
     orphan->shard_ = shard_;
-    orphan->resultWords_ = resultWords_;
-    orphan->nsegs_ = nsegs_;
-    orphan->segs_.swap(segs_);
-    orphan->solves_.swap(solves_);
-    orphan->callbacks_.swap(callbacks_);
-    orphan->group_ = group_ | 2;   // bit 1: delete after flush
+    orphan->b_ = b_;
+    b_ = nullptr;
     std::lock_guard<std::mutex> g(shard_->mu);
     auto it = std::find(shard_->dirty.begin(), shard_->dirty.end(), this);
     if (it != shard_->dirty.end())
@@ -118,48 +206,22 @@ Program::~Program()
 
 void Program::attach()
 {
+    if (!b_)
+        b_ = ProgramBody::get();
+    b_->group = group_ & 1;
     Shard& s = eng_->shard();
     shard_ = &s;
     std::lock_guard<std::mutex> g(s.mu);
     s.dirty.push_back(this);
 }
 
-void Program::new_segment()
-{
-    rows_close();
-    if (nsegs_ == segs_.size())
-        segs_.emplace_back();
-    Segment& s = segs_[nsegs_++];
-    s.ops.clear();
-    s.terms.clear();
-    s.rowsData.clear();
-    s.rowsWords = 0;
-    s.maxExtent = 0;
-}
-
-void Program::reset_after_flush()
-{
-    for (size_t k = 0; k < nsegs_; ++k) {
-        segs_[k].ops.clear();
-        segs_[k].terms.clear();
-        segs_[k].rowsData.clear();
-        segs_[k].rowsWords = 0;
-        segs_[k].maxExtent = 0;
-    }
-    nsegs_ = 0;
-    solves_.clear();
-    callbacks_.clear();
-    resultWords_ = 0;
-    shard_ = nullptr;
-}
-
 void Program::lc_begin(uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix)
 {
     touch();
-    rows_close();
-    if (nsegs_ == 0)
-        new_segment();
-    Segment& s = segs_[nsegs_ - 1];
+    b_->rows_close();
+    if (b_->nsegs == 0)
+        b_->new_segment();
+    ProgramBody::Segment& s = b_->segs[b_->nsegs - 1];
     GfOp op;
     op.dst = dst;
     op.n = n;
@@ -173,7 +235,7 @@ void Program::lc_begin(uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix)
 
 void Program::lc_end()
 {
-    Segment& s = segs_[nsegs_ - 1];
+    ProgramBody::Segment& s = b_->segs[b_->nsegs - 1];
     GfOp& op = s.ops.back();
     // An op that keeps all of dst and adds nothing is a no-op.
     if (op.termCount == 0 && op.valid >= op.n) {
@@ -224,10 +286,10 @@ void Program::literal(uint64_t dst, uint32_t offset, const uint8_t* bytes, uint3
     if (len == 0)
         return;
     touch();
-    rows_close();
-    if (nsegs_ == 0)
-        new_segment();
-    Segment& s = segs_[nsegs_ - 1];
+    b_->rows_close();
+    if (b_->nsegs == 0)
+        b_->new_segment();
+    ProgramBody::Segment& s = b_->segs[b_->nsegs - 1];
     GfOp op;
     std::memset(&op, 0, sizeof(op));
     op.dst = dst;
@@ -250,66 +312,47 @@ void Program::ingest_device(const DevBuf& dst, uint64_t src, uint32_t bytes, con
                             uint32_t hdrLen)
 {
     IngestDesc d;
-    std::memset(&d, 0, sizeof(d));
     d.dst = dst.addr();
     d.src = src;
     d.bytes = bytes;
     d.hdrLen = hdrLen;
-    std::memcpy(d.hdr, hdr, hdrLen);
+    uint64_t h = 0;
+    std::memcpy(&h, hdr, hdrLen < 8 ? hdrLen : 8);
+    std::memcpy(d.hdr, &h, 8);
     eng_->add_ingest(d, -1);
 }
 
 uint32_t Program::solve(const std::vector<SolveRow>& rows, const uint8_t* coef, uint32_t maxBytes)
 {
     touch();
-    if (nsegs_ == 0)
-        new_segment(); // the segment preceding this solve
-    PendingSolve ps;
+    if (b_->nsegs == 0)
+        b_->new_segment(); // the segment preceding this solve
+    ProgramBody::PendingSolve ps;
     std::memset(&ps.desc, 0, sizeof(ps.desc));
     ps.desc.m = (uint32_t)rows.size();
     ps.desc.maxBytes = maxBytes;
-    ps.desc.result = resultWords_;
-    resultWords_ += ps.desc.m + 1;
+    ps.desc.result = b_->resultWords;
+    b_->resultWords += ps.desc.m + 1;
     ps.rows = rows;
     ps.coef.assign(coef, coef + rows.size() * rows.size());
     const uint32_t r = ps.desc.result;
-    solves_.push_back(std::move(ps));
-    new_segment(); // ops after the solve go to the next segment
+    b_->solves.push_back(std::move(ps));
+    b_->new_segment(); // ops after the solve go to the next segment
     return r;
 }
 
 void Program::on_complete(Completion fn)
 {
     touch();
-    callbacks_.push_back(std::move(fn));
+    b_->callbacks.push_back(std::move(fn));
 }
 
 // ---- Siamese row batches ---------------------------------------------------
 
-void Program::rows_open(uint32_t base, bool keepWindow)
-{
-    RowsBuild& b = rb_;
-    rows_close();
-    touch();
-    if (nsegs_ == 0)
-        new_segment();
-    b.open = true;
-    b.haveSums = false;
-    b.readMask = 0;
-    if (!keepWindow) {
-        b.base = base;
-        b.win.clear();
-    }
-    b.updates.clear();
-    for (int& u : b.updateOf)
-        u = -1;
-    b.rows.clear();
-    b.maxExtent = 0;
-}
-
 WinEntry* Program::rows_window(uint32_t lo, uint32_t hi, uint32_t* from)
 {
-    RowsBuild& b = rb_;
+    touch();
+    ProgramBody::RowsBuild& b = b_->rb;
     if (!b.open || lo < b.base)
         rows_open(lo, false);
     const uint32_t end = b.base + (uint32_t)b.win.size();
@@ -325,7 +368,7 @@ WinEntry* Program::rows_window(uint32_t lo, uint32_t hi, uint32_t* from)
 void Program::rows_update(unsigned k, uint64_t dst, uint32_t n, uint32_t valid, unsigned s,
                           uint32_t fromElement, uint32_t toElement)
 {
-    RowsBuild& b = rb_;
+    ProgramBody::RowsBuild& b = b_->rb;
     // a row of this batch already read sum k: the update belongs to a new
     // batch over the same window (its rows run after this batch's rows)
     if (b.readMask >> k & 1)
@@ -368,7 +411,7 @@ void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t 
                        uint32_t mask0, uint32_t mask1, unsigned row, uint32_t ldpcN,
                        uint32_t ldpcFirst, const uint8_t* lit, uint32_t litLen)
 {
-    RowsBuild& b = rb_;
+    ProgramBody::RowsBuild& b = b_->rb;
     if (b.haveSums && std::memcmp(b.sums, sums, sizeof(b.sums)) != 0)
         rows_open(b.base, true);
     if (!b.haveSums) {
@@ -398,75 +441,42 @@ void Program::copy(uint64_t dst, uint64_t src, uint32_t len)
     if (len == 0)
         return;
     touch();
-    if (copies_.empty()) {
-        rows_close();
-        if (nsegs_ == 0)
-            new_segment();
+    if (b_->copies.empty()) {
+        b_->rows_close();
+        if (b_->nsegs == 0)
+            b_->new_segment();
     }
     CopyItem c;
     std::memset(&c, 0, sizeof(c));
     c.dst = dst;
     c.src = src;
     c.len = len;
-    copies_.push_back(c);
-    Segment& g = segs_[nsegs_ - 1];
+    b_->copies.push_back(c);
+    ProgramBody::Segment& g = b_->segs[b_->nsegs - 1];
     if (len > g.maxExtent)
         g.maxExtent = len;
 }
 
-void Program::rows_close()
+// ---------------------------------------------------------------------------
+// Shard queues
+
+bool Shard::Queues::empty() const
 {
-    if (!copies_.empty()) {
-        // seal the open copy batch
-        Segment& g = segs_[nsegs_ - 1];
-        GfOp op;
-        std::memset(&op, 0, sizeof(op));
-        op.kind = OP_COPIES;
-        op.n = (uint32_t)copies_.size();
-        op.termBegin = (uint32_t)(g.rowsData.size() / 16);
-        op.termCount = (uint32_t)copies_.size() * kCopyWords;
-        g.ops.push_back(op);
-        const size_t at = g.rowsData.size();
-        g.rowsData.resize(at + copies_.size() * sizeof(CopyItem));
-        std::memcpy(g.rowsData.data() + at, copies_.data(), copies_.size() * sizeof(CopyItem));
-        g.rowsWords += op.termCount;
-        copies_.clear();
-    }
-    RowsBuild& b = rb_;
-    if (!b.open)
-        return;
-    b.open = false;
-    if (b.rows.empty() && b.updates.empty())
-        return;
-    if (!b.haveSums)
-        std::memset(b.sums, 0, sizeof(b.sums));
-    Segment& s = segs_[nsegs_ - 1];
-    const uint32_t E = (uint32_t)b.win.size();
-    const uint32_t U = (uint32_t)b.updates.size();
-    const uint32_t R = (uint32_t)b.rows.size();
-    const uint32_t words = kRowSums + E + U * kUpdateWords + R * kRowWords;
-    GfOp op;
-    std::memset(&op, 0, sizeof(op));
-    op.kind = OP_ROWS;
-    op.n = R;
-    op.valid = E;
-    op.mix = U;
-    op.termBegin = (uint32_t)(s.rowsData.size() / 16);   // block offset in words
-    op.termCount = words;
-    s.ops.push_back(op);
-    const size_t at = s.rowsData.size();
-    s.rowsData.resize(at + (size_t)words * 16);
-    uint8_t* w = s.rowsData.data() + at;
-    std::memcpy(w, b.sums, sizeof(b.sums));
-    w += sizeof(b.sums);
-    std::memcpy(w, b.win.data(), (size_t)E * sizeof(WinEntry));
-    w += (size_t)E * sizeof(WinEntry);
-    std::memcpy(w, b.updates.data(), (size_t)U * sizeof(SumUpdate));
-    w += (size_t)U * sizeof(SumUpdate);
-    std::memcpy(w, b.rows.data(), (size_t)R * sizeof(RowItem));
-    s.rowsWords += words;
-    if (b.maxExtent > s.maxExtent)
-        s.maxExtent = b.maxExtent;
+    if (!ingest.empty() || !downloads.empty())
+        return false;
+    for (const auto& r : released)
+        if (!r.empty())
+            return false;
+    return true;
+}
+
+void Shard::Queues::clear()
+{
+    ingest.clear();
+    hostStage.clear();
+    downloads.clear();
+    for (auto& r : released)
+        r.clear();
 }
 
 // ---------------------------------------------------------------------------
@@ -478,7 +488,7 @@ Engine* Engine::global()
     return &e;
 }
 
-Engine::~Engine() = default;
+Engine::~Engine() { stop_threads(); }
 
 bool Engine::init(int device, const char** err)
 {
@@ -486,6 +496,7 @@ bool Engine::init(int device, const char** err)
         return true;
     if (!be_init(device, err))
         return false;
+    start_threads();
     ready_ = true;
     return true;
 }
@@ -505,6 +516,8 @@ Shard& Engine::shard()
 
 WorkerPool& Engine::pool()
 {
+    static std::mutex m;
+    std::lock_guard<std::mutex> g(m);
     if (!pool_)
         pool_.reset(new WorkerPool(WorkerPool::default_threads()));
     return *pool_;
@@ -521,7 +534,11 @@ void Engine::account(uint64_t opBytes, uint64_t outBytes, bool inSolve)
 
 EngineStats Engine::stats() const
 {
-    EngineStats t = flushStats_;
+    EngineStats t;
+    {
+        std::lock_guard<std::mutex> g(const_cast<std::mutex&>(statsMu_));
+        t = flushStats_;
+    }
     std::lock_guard<std::mutex> g(shardsMu_);
     for (const auto& s : shards_)
         t.add(s->stats);
@@ -559,14 +576,12 @@ size_t cap_class(uint32_t cap)
     return 188 + cap / 65536 - 3;
 }
 
-} // namespace
-
-namespace {
 constexpr size_t kChunkBytes = 64u << 20;    // one hipMalloc
 constexpr size_t kRegionBytes = 4u << 20;    // a shard's bump region
-constexpr size_t kMagazine = 512;            // buffers moved per depot transfer
-constexpr size_t kKeepFree = 8 * kMagazine;  // free buffers of a class a shard keeps through a reclaim
+constexpr size_t kMagazine = 512;            // buffers cut per refill at most
+constexpr size_t kMaxMagazine = 512;         // buffers per depot magazine at most (bounds what a shard hoards)
 constexpr size_t kRefillBytes = 1u << 20;    // bytes carved per refill
+
 } // namespace
 
 uint8_t* Engine::carve_region(size_t bytes)
@@ -589,19 +604,19 @@ uint8_t* Engine::carve_region(size_t bytes)
     return p;
 }
 
-// Refill shard s's empty list of class `cls`: a magazine from the depot if
-// one is there, otherwise fresh buffers cut from the shard's bump region.
+// Refill shard s's empty list of class `cls`: a magazine of buffers a
+// completed submission returned, otherwise fresh buffers cut from the shard's
+// bump region.
 bool Engine::refill(Shard& s, size_t cls, uint32_t cap)
 {
     std::vector<uint8_t*>& list = s.freeLists[cls];
     {
         std::lock_guard<std::mutex> g(depotMu_);
         if (cls < depot_.size() && !depot_[cls].empty()) {
-            std::vector<uint8_t*>& d = depot_[cls];
-            const size_t take = std::min(kMagazine, d.size());
-            list.insert(list.end(), d.end() - take, d.end());
-            d.resize(d.size() - take);
-            return true;
+            list.swap(depot_[cls].back());
+            depot_[cls].pop_back();
+            if (!list.empty())
+                return true;
         }
     }
     if (cap > kRegionBytes / 4) {
@@ -629,22 +644,6 @@ bool Engine::refill(Shard& s, size_t cls, uint32_t cap)
     return true;
 }
 
-// Return surplus free buffers of shard s to the depot in magazines.
-void Engine::spill(Shard& s)
-{
-    for (size_t cls = 0; cls < s.freeLists.size(); ++cls) {
-        std::vector<uint8_t*>& list = s.freeLists[cls];
-        if (list.size() <= kKeepFree + kMagazine)
-            continue;
-        const size_t keep = kKeepFree;
-        std::lock_guard<std::mutex> g(depotMu_);
-        if (cls >= depot_.size())
-            depot_.resize(cls + 1);
-        depot_[cls].insert(depot_[cls].end(), list.begin() + keep, list.end());
-        list.resize(keep);
-    }
-}
-
 DevBuf Engine::alloc(uint32_t bytes)
 {
     DevBuf b;
@@ -666,7 +665,10 @@ void Engine::release(DevBuf& b)
 {
     if (b.ptr) {
         Shard& s = shard();
-        s.pendingFree.push_back(b);
+        const size_t cls = cap_class(b.cap);
+        if (cls >= s.q.released.size())
+            s.q.released.resize(cls + 1);
+        s.q.released[cls].push_back(b.ptr);
         s.inUse -= b.cap;
     }
     b = DevBuf();
@@ -675,7 +677,7 @@ void Engine::release(DevBuf& b)
 void Engine::download(void* hostDst, uint64_t devSrc, uint32_t bytes)
 {
     if (bytes)
-        shard().downloads.push_back(Shard::Download{hostDst, devSrc, bytes});
+        shard().q.downloads.push_back(Shard::Download{hostDst, devSrc, bytes});
 }
 
 void Engine::stage_host_ingest(const DevBuf& dst, const void* data, uint32_t bytes,
@@ -683,79 +685,79 @@ void Engine::stage_host_ingest(const DevBuf& dst, const void* data, uint32_t byt
 {
     // Stage hdr || data contiguously so the device copy is aligned.
     Shard& s = shard();
-    const size_t off = (s.hostStage.size() + 15) & ~(size_t)15;
-    s.hostStage.resize(off + hdrLen + bytes);
-    std::memcpy(s.hostStage.data() + off, hdr, hdrLen);
-    std::memcpy(s.hostStage.data() + off + hdrLen, data, bytes);
+    const size_t off = (s.q.hostStage.size() + 15) & ~(size_t)15;
+    s.q.hostStage.resize(off + hdrLen + bytes);
+    std::memcpy(s.q.hostStage.data() + off, hdr, hdrLen);
+    std::memcpy(s.q.hostStage.data() + off + hdrLen, data, bytes);
     IngestDesc d;
     std::memset(&d, 0, sizeof(d));
     d.dst = dst.addr();
     d.src = 0;
     d.bytes = hdrLen + bytes;
     d.hdrLen = 0;
-    add_ingest(d, (int64_t)off);
+    s.q.ingest.push_back(Shard::IngestRec{d, (int64_t)off});
 }
 
 void Engine::add_ingest(const IngestDesc& d, int64_t hostStageOffset)
 {
-    Shard& s = shard();
-    s.ingest.push_back(Shard::IngestRec{d, hostStageOffset});
+    shard().q.ingest.push_back(Shard::IngestRec{d, hostStageOffset});
 }
 
 bool Engine::pending() const
 {
     std::lock_guard<std::mutex> g(shardsMu_);
     for (const auto& s : shards_)
-        if (!s->dirty.empty() || !s->ingest.empty() || !s->downloads.empty())
+        if (!s->dirty.empty() || !s->q.empty())
             return true;
     return false;
 }
 
-void Engine::ensure_up(size_t bytes)
+void Engine::ensure_up(XferSet& x, size_t bytes)
 {
-    if (bytes <= upCap_)
+    if (bytes <= x.upCap)
         return;
-    size_t cap = upCap_ ? upCap_ : (1u << 20);
+    size_t cap = x.upCap ? x.upCap : (1u << 20);
     while (cap < bytes)
         cap *= 2;
-    if (upHost_)
-        be_host_free(upHost_);
-    if (upDev_)
-        be_dev_free(upDev_);
-    upHost_ = (uint8_t*)be_host_alloc(cap);
-    upDev_ = (uint8_t*)be_dev_alloc(cap);
-    upCap_ = cap;
+    if (x.upHost)
+        be_host_free(x.upHost);
+    if (x.upDev)
+        be_dev_free(x.upDev);
+    x.upHost = (uint8_t*)be_host_alloc(cap);
+    x.upDev = (uint8_t*)be_dev_alloc(cap);
+    x.upCap = cap;
 }
 
-void Engine::ensure_down(size_t bytes)
+void Engine::ensure_down(XferSet& x, size_t bytes)
 {
-    if (bytes <= downCap_)
+    if (bytes <= x.downCap)
         return;
-    size_t cap = downCap_ ? downCap_ : (1u << 20);
+    size_t cap = x.downCap ? x.downCap : (1u << 20);
     while (cap < bytes)
         cap *= 2;
-    if (downHost_)
-        be_host_free(downHost_);
-    if (downDev_)
-        be_dev_free(downDev_);
-    downHost_ = (uint8_t*)be_host_alloc(cap);
-    downDev_ = (uint8_t*)be_dev_alloc(cap);
-    downCap_ = cap;
+    if (x.downHost)
+        be_host_free(x.downHost);
+    if (x.downDev)
+        be_dev_free(x.downDev);
+    x.downHost = (uint8_t*)be_host_alloc(cap);
+    x.downDev = (uint8_t*)be_dev_alloc(cap);
+    x.downCap = cap;
 }
 
 // ---------------------------------------------------------------------------
-// Engine: flush
+// Engine: the flush pipeline
 //
-// 1. A sequential pass over the queued programs fixes every segment's place
-//    in the upload (ops, terms, work items) and every solve's place in the
-//    result array.
-// 2. The pool copies segments, ingest descriptors and staged host payloads
-//    into the pinned upload buffer in parallel.
-// 3. One H2D copy, then ingest, executor and solve launches in phase order.
+// enqueue (caller, exclusive): swap out every queued program body and every
+//   shard's queues into a Batch, hand it to the launcher.
+// launcher thread: lay the batch out (every segment's place in the upload,
+//   every solve's place in the result array), copy it into the pinned upload
+//   buffer of its transfer set, then one H2D copy, the ingest, executor and
+//   solve launches in phase order, the D2H of results and downloads, and a
+//   fence.
+// completer thread: wait for the fence, deliver downloads, run completions,
+//   return released buffers to the depot and the bodies/queues for reuse.
 
 namespace {
-
-inline size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
 
 struct Phase
 {
@@ -767,87 +769,261 @@ struct Phase
 
 struct SegRef
 {
-    Program* prog;
-    uint32_t seg;
+    const ProgramBody::Segment* seg;
     uint32_t wordBase, words, itemBase;
-};
-
-struct ShardRef
-{
-    Shard* shard;
-    size_t descBase, stageBase;
 };
 
 } // namespace
 
-bool Engine::flush()
+struct Batch
 {
-    if (flight_.active && !sync())
-        return false;
-    if (failed())
-        return false;
+    uint64_t ticket = 0;
+    std::vector<ProgramBody*> bodies[2];   // by group
+    std::vector<Shard::Queues> queues;     // detached shard queues
+    std::vector<Shard*> queueOwner;
+    unsigned set = 0;                      // transfer set (ticket % kSets)
+    // layout (enqueue -> launcher)
+    std::vector<Phase> phases;
+    size_t upBytes = 0, nIngest = 0;
+    size_t oIngD = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0;
+    uint32_t resultWords = 0;
+    std::vector<const Shard::Download*> dls;
+    EngineStats st;
+    // launcher -> completer
+    void* fence = nullptr;
+    bool launched = false;
+    std::vector<uint32_t> resultBase[2];
+    struct Download
+    {
+        void* host;
+        size_t off;
+        uint32_t bytes;
+    };
+    std::vector<Download> downloads;
+};
 
+namespace {
+
+// SGPU_TIMELINE=1: one stderr line per pipeline event (debugging aid)
+const bool g_timeline = std::getenv("SGPU_TIMELINE") != nullptr;
+void tl(const char* what, uint64_t ticket)
+{
+    if (g_timeline)
+        std::fprintf(stderr, "eng %10.3f ms  %s t%llu\n", (double)now_ns() / 1e6, what,
+                     (unsigned long long)ticket);
+}
+
+// the download area starts with the byte counters: the executor's expanded
+// terms, then the solve's back-substitution source bytes and output bytes
+constexpr size_t kAcctBytes = 32;
+
+// below this many stream words a submission is assembled on the calling
+// thread alone (the drop-in API's per-call flushes)
+constexpr size_t kParallelWords = 1u << 16;
+
+} // namespace
+
+void Engine::start_threads()
+{
+    stop_ = false;
+    launcher_ = std::thread([this] { launcher_loop(); });
+    completer_ = std::thread([this] { completer_loop(); });
+}
+
+void Engine::stop_threads()
+{
+    {
+        std::lock_guard<std::mutex> g(qMu_);
+        stop_ = true;
+    }
+    launchCv_.notify_all();
+    completeCv_.notify_all();
+    setCv_.notify_all();
+    doneCv_.notify_all();
+    if (launcher_.joinable())
+        launcher_.join();
+    if (completer_.joinable())
+        completer_.join();
+}
+
+uint64_t Engine::enqueue()
+{
+    if (failed())
+        return 0;
     std::vector<Shard*> shards;
     {
         std::lock_guard<std::mutex> g(shardsMu_);
         for (auto& s : shards_)
             shards.push_back(s.get());
     }
-    bool any = false;
-    for (Shard* s : shards)
-        any = any || !s->dirty.empty() || !s->ingest.empty() || !s->downloads.empty() ||
-              !s->pendingFree.empty();
-    if (!any)
-        return true;
-    const uint64_t t0 = now_ns();
-
-    // ---- 1. layout -----------------------------------------------------------
-    std::vector<Program*> progs[2];
-    for (Shard* s : shards)
-        for (Program* p : s->dirty)
-            progs[p->group_ & 1].push_back(p);
-    // seal every open Siamese row batch (serialises its table and rows)
-    for (int g = 0; g < 2; ++g)
-        pool().run(progs[g].size(), [&](size_t i) { progs[g][i]->rows_close(); });
-
-    uint32_t resultWords = 0;
-    std::vector<uint32_t> resultBase[2];
-    for (int g = 0; g < 2; ++g)
-        for (Program* p : progs[g]) {
-            resultBase[g].push_back(resultWords);
-            resultWords += p->resultWords_;
+    Batch* b = nullptr;
+    for (Shard* s : shards) {
+        if (s->dirty.empty() && s->q.empty())
+            continue;
+        if (!b)
+            b = new Batch;
+        for (Program* p : s->dirty) {
+            ProgramBody* body = p->b_;
+            p->b_ = nullptr;
+            p->shard_ = nullptr;
+            if (body) {
+                if (body->empty() && body->callbacks.empty())
+                    ProgramBody::put(body);
+                else
+                    b->bodies[body->group].push_back(body);
+            }
+            if (p->group_ & 2)
+                delete p;   // orphan of a freed instance (see ~Program)
         }
+        s->dirty.clear();
+        if (!s->q.empty()) {
+            Shard::Queues next;
+            {
+                std::lock_guard<std::mutex> g(s->mu);
+                if (!s->spare.empty()) {
+                    next = std::move(s->spare.back());
+                    s->spare.pop_back();
+                }
+            }
+            b->queues.push_back(std::move(s->q));
+            b->queueOwner.push_back(s);
+            s->q = std::move(next);
+        }
+    }
+    if (!b)
+        return nextTicket_;   // nothing queued: the latest submission covers everything
+    const uint64_t ticket = ++nextTicket_;
+    tl("enqueue", ticket);
+    b->ticket = ticket;
+    b->set = (unsigned)(ticket % kSets);
+    {
+        // this ticket's transfer set must be free (its previous user done)
+        std::unique_lock<std::mutex> lk(qMu_);
+        setCv_.wait(lk, [&] { return stop_ || sets_[b->set].busyTicket == 0; });
+        sets_[b->set].busyTicket = ticket;
+    }
+    assemble_batch(*b);
+    tl("assembled", ticket);
+    {
+        std::lock_guard<std::mutex> g(qMu_);
+        toLaunch_.push_back(b);   // (b belongs to the pipeline from here on)
+    }
+    launchCv_.notify_one();
+    return ticket;
+}
+
+bool Engine::wait(uint64_t ticket)
+{
+    std::unique_lock<std::mutex> lk(qMu_);
+    doneCv_.wait(lk, [&] { return stop_ || doneTicket_ >= ticket; });
+    return !failed();
+}
+
+bool Engine::flush()
+{
+    const uint64_t prev = nextTicket_;
+    enqueue();
+    // complete what was in flight before this submission (one flush in flight)
+    return wait(prev) && !failed();
+}
+
+void Engine::launcher_loop()
+{
+    for (;;) {
+        Batch* b = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(qMu_);
+            launchCv_.wait(lk, [&] { return stop_ || !toLaunch_.empty(); });
+            if (stop_)
+                return;
+            b = toLaunch_.front();
+            toLaunch_.pop_front();
+        }
+        tl("launch begin", b->ticket);
+        if (!failed())
+            launch_batch(*b);
+        tl("launch end", b->ticket);
+        {
+            std::lock_guard<std::mutex> g(qMu_);
+            toComplete_.push_back(b);
+        }
+        completeCv_.notify_one();
+    }
+}
+
+// Lay the batch out and copy it into its pinned upload buffer (caller's
+// thread, in parallel on the worker pool for large batches):
+//   1. every open Siamese row batch is sealed (parallel over bodies);
+//   2. a sequential pass fixes every segment's place in the upload and its
+//      work items, and every solve's place in the result array;
+//   3. segments, solve data and ingest descriptors are copied (parallel).
+void Engine::assemble_batch(Batch& bt)
+{
+    const uint64_t t0 = now_ns();
+    XferSet& xs = sets_[bt.set];
+    EngineStats& st = bt.st;
+    size_t totalBodies = bt.bodies[0].size() + bt.bodies[1].size();
+    size_t approxWords = 0;
+    for (const Shard::Queues& q : bt.queues)
+        approxWords += q.ingest.size() * 2;
+    for (int g = 0; g < 2; ++g)
+        for (ProgramBody* p : bt.bodies[g])
+            for (size_t k = 0; k < p->nsegs; ++k)
+                approxWords += p->segs[k].ops.size() * 2 + p->segs[k].terms.size() +
+                               p->segs[k].rowsWords + p->rb.win.size() + p->rb.rows.size() * 3;
+    const bool parallel = approxWords >= kParallelWords;
+    auto run = [&](size_t n, const std::function<void(size_t)>& fn) {
+        if (parallel)
+            pool().run(n, fn);
+        else
+            for (size_t i = 0; i < n; ++i)
+                fn(i);
+    };
+
+    // ---- 1. seal -------------------------------------------------------------
+    run((totalBodies + 31) / 32, [&](size_t c) {
+        for (size_t i = c * 32; i < std::min(totalBodies, c * 32 + 32); ++i) {
+            const size_t n0 = bt.bodies[0].size();
+            (i < n0 ? bt.bodies[0][i] : bt.bodies[1][i - n0])->rows_close();
+        }
+    });
+
+    // ---- 2. layout -----------------------------------------------------------
+    uint32_t resultWords = 0;
+    for (int g = 0; g < 2; ++g)
+        for (ProgramBody* p : bt.bodies[g]) {
+            bt.resultBase[g].push_back(resultWords);
+            resultWords += p->resultWords;
+        }
+    bt.resultWords = resultWords;
 
     std::vector<SegRef> segs;
-    std::vector<Phase> phases;
+    std::vector<Phase>& phases = bt.phases;
     std::vector<SolveDesc> sdescs;
-    // solve rows and coefficients are copied straight into the upload by the
-    // assembly tasks (SolveRef: where each pending solve's data goes)
     struct SolveRef
     {
-        const Program::PendingSolve* ps;
+        const ProgramBody::PendingSolve* ps;
         size_t rowBase, coefBase;
     };
-    std::vector<SolveRef> srefsSolve;
+    std::vector<SolveRef> srefs;
     size_t nSolveRows = 0, nCoef = 0;
     std::vector<SolveItem> sitems;
     size_t nOps = 0, nTerms = 0, nWords = 0, nItems = 0;
     for (int g = 0; g < 2; ++g) {
         size_t maxSegs = 0;
-        for (Program* p : progs[g])
-            maxSegs = std::max(maxSegs, p->nsegs_);
+        for (ProgramBody* p : bt.bodies[g])
+            maxSegs = std::max(maxSegs, p->nsegs);
         for (size_t k = 0; k < maxSegs; ++k) {
             Phase ex{Phase::EXEC, nItems, 0, 0, 0, 0};
             const size_t segBegin = segs.size();
-            for (Program* p : progs[g]) {
-                if (k >= p->nsegs_)
+            for (ProgramBody* p : bt.bodies[g]) {
+                if (k >= p->nsegs)
                     continue;
-                const Program::Segment& s = p->segs_[k];
+                const ProgramBody::Segment& s = p->segs[k];
                 if (s.ops.empty())
                     continue;
                 const size_t words = kOpWords * s.ops.size() + s.terms.size() + s.rowsWords;
-                segs.push_back(SegRef{p, (uint32_t)k, (uint32_t)nWords, (uint32_t)words,
-                                      (uint32_t)nItems});
+                segs.push_back(SegRef{&s, (uint32_t)nWords, (uint32_t)words, (uint32_t)nItems});
                 nOps += s.ops.size();
                 nTerms += s.terms.size();
                 nWords += words;
@@ -855,20 +1031,15 @@ bool Engine::flush()
             }
 #if SGPU_EXEC_LPT
             // Longest op lists first: workgroups are dispatched in blockIdx
-            // order and a launch runs in about two rounds of one workgroup per
-            // CU, so the short segments fill the second round's tail.
+            // order and a launch runs in a few rounds of workgroups per CU,
+            // so the short segments fill the last round's tail.
             {
-                std::vector<uint32_t> order(segs.size() - segBegin);
-                for (uint32_t i = 0; i < order.size(); ++i)
-                    order[i] = i;
-                std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-                    return segs[segBegin + a].words > segs[segBegin + b].words;
-                });
+                std::stable_sort(segs.begin() + (long)segBegin, segs.end(),
+                                 [](const SegRef& a, const SegRef& b) { return a.words > b.words; });
                 uint32_t ib = (uint32_t)ex.itemBegin;
-                for (uint32_t i : order) {
-                    SegRef& r = segs[segBegin + i];
-                    r.itemBase = ib;
-                    ib += (r.prog->segs_[r.seg].maxExtent + kExecTileBytes - 1) / kExecTileBytes;
+                for (size_t i = segBegin; i < segs.size(); ++i) {
+                    segs[i].itemBase = ib;
+                    ib += (segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes;
                 }
             }
 #endif
@@ -877,16 +1048,16 @@ bool Engine::flush()
                 phases.push_back(ex);
 
             Phase sv{Phase::SOLVE, sitems.size(), 0, sdescs.size(), 0, 0};
-            for (size_t pi = 0; pi < progs[g].size(); ++pi) {
-                Program* p = progs[g][pi];
-                if (k >= p->solves_.size())
+            for (size_t pi = 0; pi < bt.bodies[g].size(); ++pi) {
+                const ProgramBody* p = bt.bodies[g][pi];
+                if (k >= p->solves.size())
                     continue;
-                const Program::PendingSolve& ps = p->solves_[k];
+                const ProgramBody::PendingSolve& ps = p->solves[k];
                 SolveDesc d = ps.desc;
-                d.result += resultBase[g][pi];
+                d.result += bt.resultBase[g][pi];
                 d.rowBegin = (uint32_t)nSolveRows;
                 d.coefOffset = nCoef;
-                srefsSolve.push_back(SolveRef{&ps, nSolveRows, nCoef});
+                srefs.push_back(SolveRef{&ps, nSolveRows, nCoef});
                 nSolveRows += ps.rows.size();
                 nCoef += ps.coef.size();
                 const uint32_t sidx = (uint32_t)sdescs.size();
@@ -897,7 +1068,7 @@ bool Engine::flush()
             }
 #if SGPU_EXEC_LPT
             // largest solves first (the serial pivot chain grows with m)
-            std::stable_sort(sitems.begin() + sv.itemBegin, sitems.end(),
+            std::stable_sort(sitems.begin() + (long)sv.itemBegin, sitems.end(),
                              [&](const SolveItem& a, const SolveItem& b) {
                                  return sdescs[a.solve].m > sdescs[b.solve].m;
                              });
@@ -909,194 +1080,270 @@ bool Engine::flush()
         }
     }
 
-    std::vector<ShardRef> srefs;
     size_t nIngest = 0, stageBytes = 0;
-    for (Shard* s : shards) {
-        srefs.push_back(ShardRef{s, nIngest, stageBytes});
-        nIngest += s->ingest.size();
-        stageBytes = align16(stageBytes + s->hostStage.size());
+    std::vector<size_t> descBase, stageBase;
+    for (const Shard::Queues& q : bt.queues) {
+        descBase.push_back(nIngest);
+        stageBase.push_back(stageBytes);
+        nIngest += q.ingest.size();
+        stageBytes = align16(stageBytes + q.hostStage.size());
     }
+    bt.nIngest = nIngest;
 
     size_t off = 0;
     const size_t oStage = off;
     off = align16(off + stageBytes);
-    const size_t oIngD = off;
+    bt.oIngD = off;
     off = align16(off + nIngest * sizeof(IngestDesc));
-    const size_t oStream = off;
+    bt.oStream = off;
     off = align16(off + nWords * 16);
-    const size_t oItems = off;
+    bt.oItems = off;
     off = align16(off + nItems * sizeof(ExecItem));
-    const size_t oSD = off;
+    bt.oSD = off;
     off = align16(off + sdescs.size() * sizeof(SolveDesc));
-    const size_t oSR = off;
+    bt.oSR = off;
     off = align16(off + nSolveRows * sizeof(SolveRow));
-    const size_t oCoef = off;
+    bt.oCoef = off;
     off = align16(off + nCoef);
-    const size_t oSI = off;
+    bt.oSI = off;
     off = align16(off + sitems.size() * sizeof(SolveItem));
-    const size_t upBytes = off;
-    if (upBytes)
-        ensure_up(upBytes);
+    bt.upBytes = off;
+    if (bt.upBytes)
+        ensure_up(xs, bt.upBytes);
 
-    // ---- 2. parallel assembly into the pinned upload buffer ----------------
-    uint8_t* up = upHost_;
-    const uint64_t stageDev = (uint64_t)(uintptr_t)(upDev_ + oStage);
-    constexpr size_t kIngestChunk = 16384;
+    // ---- 3. copy into the pinned upload buffer -------------------------------
+    uint8_t* up = xs.upHost;
+    const uint64_t stageDev = (uint64_t)(uintptr_t)(xs.upDev + oStage);
+    constexpr size_t kSegChunk = 16;
+    constexpr size_t kIngestChunk = 8192;
     constexpr size_t kSolveChunk = 64;
     struct Task
     {
-        int kind;   // 0 = segment, 1 = ingest chunk, 2 = solve chunk
+        int kind;   // 0 = segments, 1 = ingest chunk, 2 = solves
         size_t a, b;
     };
     std::vector<Task> tasks;
-    for (size_t i = 0; i < segs.size(); ++i)
-        tasks.push_back(Task{0, i, 0});
-    for (size_t i = 0; i < srefsSolve.size(); i += kSolveChunk)
-        tasks.push_back(Task{2, i, 0});
-    for (size_t si = 0; si < srefs.size(); ++si)
-        for (size_t c = 0; c < srefs[si].shard->ingest.size(); c += kIngestChunk)
-            tasks.push_back(Task{1, si, c});
-    pool().run(tasks.size(), [&](size_t ti) {
+    for (size_t i = 0; i < segs.size(); i += kSegChunk)
+        tasks.push_back(Task{0, i, std::min(segs.size(), i + kSegChunk)});
+    for (size_t i = 0; i < srefs.size(); i += kSolveChunk)
+        tasks.push_back(Task{2, i, std::min(srefs.size(), i + kSolveChunk)});
+    for (size_t qi = 0; qi < bt.queues.size(); ++qi)
+        for (size_t c = 0; c < std::max<size_t>(1, bt.queues[qi].ingest.size()); c += kIngestChunk)
+            tasks.push_back(Task{1, qi, c});
+    run(tasks.size(), [&](size_t ti) {
         const Task& t = tasks[ti];
         if (t.kind == 0) {
-            const SegRef& r = segs[t.a];
-            const Program::Segment& s = r.prog->segs_[r.seg];
-            uint8_t* w = up + oStream + (size_t)r.wordBase * 16;
-            for (const GfOp& op : s.ops) {
-                if (op.kind == OP_ROWS || op.kind == OP_COPIES) {
+            for (size_t si = t.a; si < t.b; ++si) {
+                const SegRef& r = segs[si];
+                const ProgramBody::Segment& s = *r.seg;
+                uint8_t* w = up + bt.oStream + (size_t)r.wordBase * 16;
+                for (const GfOp& op : s.ops) {
                     std::memcpy(w, &op, sizeof(GfOp));
                     w += sizeof(GfOp);
-                    const size_t bytes = (size_t)op.termCount * 16;   // block (rows_close)
-                    std::memcpy(w, s.rowsData.data() + (size_t)op.termBegin * 16, bytes);
-                    w += bytes;
-                    continue;
+                    if (op.kind == OP_ROWS || op.kind == OP_COPIES) {
+                        const size_t bytes = (size_t)op.termCount * 16;   // block (rows_close)
+                        std::memcpy(w, s.rowsData.data() + (size_t)op.termBegin * 16, bytes);
+                        w += bytes;
+                    } else if (op.kind == OP_LINCOMB && op.termCount) {
+                        const size_t bytes = (size_t)op.termCount * sizeof(GfTerm);
+                        std::memcpy(w, s.terms.data() + op.termBegin, bytes);
+                        w += bytes;
+                    }
                 }
-                std::memcpy(w, &op, sizeof(GfOp));
-                w += sizeof(GfOp);
-                if (op.kind == OP_LINCOMB && op.termCount) {
-                    const size_t bytes = (size_t)op.termCount * sizeof(GfTerm);
-                    std::memcpy(w, s.terms.data() + op.termBegin, bytes);
-                    w += bytes;
-                }
+                ExecItem* items = (ExecItem*)(up + bt.oItems) + r.itemBase;
+                const uint32_t nOpsSeg = (uint32_t)s.ops.size();
+                uint32_t n = 0;
+                for (uint32_t tb = 0; tb < s.maxExtent; tb += kExecTileBytes)
+                    items[n++] = ExecItem{r.wordBase, r.words, nOpsSeg, tb};
             }
-            ExecItem* items = (ExecItem*)(up + oItems) + r.itemBase;
-            const uint32_t nItems = (uint32_t)s.ops.size();
-            uint32_t n = 0;
-            for (uint32_t tb = 0; tb < s.maxExtent; tb += kExecTileBytes)
-                items[n++] = ExecItem{r.wordBase, r.words, nItems, tb};
         } else if (t.kind == 2) {
-            const size_t end = std::min(srefsSolve.size(), t.a + kSolveChunk);
-            for (size_t i = t.a; i < end; ++i) {
-                const SolveRef& r = srefsSolve[i];
-                std::memcpy(up + oSR + r.rowBase * sizeof(SolveRow), r.ps->rows.data(),
+            for (size_t i = t.a; i < t.b; ++i) {
+                const SolveRef& r = srefs[i];
+                std::memcpy(up + bt.oSR + r.rowBase * sizeof(SolveRow), r.ps->rows.data(),
                             r.ps->rows.size() * sizeof(SolveRow));
-                std::memcpy(up + oCoef + r.coefBase, r.ps->coef.data(), r.ps->coef.size());
+                std::memcpy(up + bt.oCoef + r.coefBase, r.ps->coef.data(), r.ps->coef.size());
             }
         } else {
-            const ShardRef& sr = srefs[t.a];
-            const Shard& s = *sr.shard;
-            const size_t end = std::min(s.ingest.size(), t.b + kIngestChunk);
-            IngestDesc* descs = (IngestDesc*)(up + oIngD) + sr.descBase;
+            const Shard::Queues& q = bt.queues[t.a];
+            IngestDesc* descs = (IngestDesc*)(up + bt.oIngD) + descBase[t.a];
+            const size_t end = std::min(q.ingest.size(), t.b + kIngestChunk);
             for (size_t i = t.b; i < end; ++i) {
-                IngestDesc d = s.ingest[i].d;
-                if (s.ingest[i].hostOffset >= 0)
-                    d.src = stageDev + sr.stageBase + (uint64_t)s.ingest[i].hostOffset;
+                IngestDesc d = q.ingest[i].d;
+                if (q.ingest[i].hostOffset >= 0)
+                    d.src = stageDev + stageBase[t.a] + (uint64_t)q.ingest[i].hostOffset;
                 descs[i] = d;
             }
-            if (t.b == 0 && !s.hostStage.empty())
-                std::memcpy(up + oStage + sr.stageBase, s.hostStage.data(), s.hostStage.size());
+            if (t.b == 0 && !q.hostStage.empty())
+                std::memcpy(up + oStage + stageBase[t.a], q.hostStage.data(), q.hostStage.size());
         }
     });
     if (!sdescs.empty()) {
-        std::memcpy(up + oSD, sdescs.data(), sdescs.size() * sizeof(SolveDesc));
-        std::memcpy(up + oSI, sitems.data(), sitems.size() * sizeof(SolveItem));
+        std::memcpy(up + bt.oSD, sdescs.data(), sdescs.size() * sizeof(SolveDesc));
+        std::memcpy(up + bt.oSI, sitems.data(), sitems.size() * sizeof(SolveItem));
     }
 
-    // download area: the executor's byte counter (kAcctBytes), the solve
-    // results, then each requested range
-    constexpr size_t kAcctBytes = 16;
+    // download area: the byte counters (kAcctBytes), the solve results, then
+    // each requested range
     size_t dOff = align16(kAcctBytes + (size_t)resultWords * 4);
-    flight_.downloads.clear();
-    std::vector<Shard::Download> dls;
-    for (Shard* s : shards)
-        for (const Shard::Download& d : s->downloads) {
-            flight_.downloads.push_back(InFlight::Download{d.host, dOff, d.bytes});
-            dls.push_back(d);
+    for (const Shard::Queues& q : bt.queues)
+        for (const Shard::Download& d : q.downloads) {
+            bt.downloads.push_back(Batch::Download{d.host, dOff, d.bytes});
+            bt.dls.push_back(&d);
             dOff = align16(dOff + d.bytes);
         }
-    ensure_down(dOff);
+    ensure_down(xs, dOff);
 
-    // ---- 3. launch -----------------------------------------------------------
-    if (upBytes)
-        be_h2d(upDev_, upHost_, upBytes);
-    if (nIngest)
-        be_launch_ingest((const IngestDesc*)(upDev_ + oIngD), (uint32_t)nIngest);
-    uint64_t* acctDev = (uint64_t*)downDev_;
-    uint32_t* resultsDev = (uint32_t*)(downDev_ + kAcctBytes);
-    be_memset(acctDev, 0, sizeof(uint64_t));
-    for (const Phase& ph : phases) {
+    st.flushes = 1;
+    st.launches = phases.size() + (nIngest ? 1 : 0);
+    st.ops = nOps;
+    st.terms = nTerms;
+    st.solves = sdescs.size();
+    st.ingests = nIngest;
+    st.uploadBytes = bt.upBytes;
+    st.assembleNs = now_ns() - t0;
+}
+
+void Engine::launch_batch(Batch& bt)
+{
+    XferSet& xs = sets_[bt.set];
+    EngineStats& st = bt.st;
+    if (bt.upBytes)
+        be_h2d(xs.upDev, xs.upHost, bt.upBytes);
+    if (bt.nIngest)
+        be_launch_ingest((const IngestDesc*)(xs.upDev + bt.oIngD), (uint32_t)bt.nIngest);
+    uint64_t* acctDev = (uint64_t*)xs.downDev;
+    uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
+    be_memset(acctDev, 0, 3 * sizeof(uint64_t));
+    for (const Phase& ph : bt.phases) {
         if (ph.kind == Phase::EXEC) {
-            be_launch_exec(upDev_ + oStream, (const ExecItem*)(upDev_ + oItems) + ph.itemBegin,
+            be_launch_exec(xs.upDev + bt.oStream, (const ExecItem*)(xs.upDev + bt.oItems) + ph.itemBegin,
                            (uint32_t)ph.itemCount, acctDev);
-            flushStats_.execLaunches++;
+            st.execLaunches++;
         } else {
-            const SolveDesc* sd = (const SolveDesc*)(upDev_ + oSD) + ph.solveBegin;
-            be_launch_solve_prefix(sd, (const SolveRow*)(upDev_ + oSR), upDev_ + oCoef, resultsDev,
-                                   (uint32_t)ph.solveCount);
+            const SolveDesc* sd = (const SolveDesc*)(xs.upDev + bt.oSD) + ph.solveBegin;
+            be_launch_solve_prefix(sd, (const SolveRow*)(xs.upDev + bt.oSR), xs.upDev + bt.oCoef,
+                                   resultsDev, (uint32_t)ph.solveCount, acctDev + 1);
             // solve items index solves globally; pass the global desc base
-            be_launch_solve_main((const SolveDesc*)(upDev_ + oSD), (const SolveRow*)(upDev_ + oSR),
-                                 upDev_ + oCoef, resultsDev,
-                                 (const SolveItem*)(upDev_ + oSI) + ph.itemBegin,
+            be_launch_solve_main((const SolveDesc*)(xs.upDev + bt.oSD),
+                                 (const SolveRow*)(xs.upDev + bt.oSR), xs.upDev + bt.oCoef, resultsDev,
+                                 (const SolveItem*)(xs.upDev + bt.oSI) + ph.itemBegin,
                                  (uint32_t)ph.itemCount, ph.maxRows);
         }
     }
-    be_d2h(downHost_, downDev_, kAcctBytes + (size_t)resultWords * 4);
-    for (size_t i = 0; i < dls.size(); ++i)
-        be_d2h(downHost_ + flight_.downloads[i].off, (const void*)(uintptr_t)dls[i].dev,
-               dls[i].bytes);
+    be_d2h(xs.downHost, xs.downDev, kAcctBytes + (size_t)bt.resultWords * 4);
+    for (size_t i = 0; i < bt.dls.size(); ++i)
+        be_d2h(xs.downHost + bt.downloads[i].off, (const void*)(uintptr_t)bt.dls[i]->dev,
+               bt.dls[i]->bytes);
+    bt.fence = be_fence();
+    bt.launched = true;
+    std::lock_guard<std::mutex> g(statsMu_);
+    flushStats_.add(st);
+}
 
-    // ---- bookkeeping -----------------------------------------------------------
-    flushStats_.flushes++;
-    flushStats_.launches += phases.size() + (nIngest ? 1 : 0);
-    flushStats_.ops += nOps;
-    flushStats_.terms += nTerms;
-    flushStats_.solves += sdescs.size();
-    flushStats_.ingests += nIngest;
-    flushStats_.uploadBytes += upBytes;
-    flushStats_.assembleNs += now_ns() - t0;
-
-    flight_.callbacks.clear();
-    for (int g = 0; g < 2; ++g)
-        for (size_t pi = 0; pi < progs[g].size(); ++pi) {
-            Program* p = progs[g][pi];
-            if (!p->callbacks_.empty()) {
-                flight_.callbacks.emplace_back();
-                flight_.callbacks.back().first = resultBase[g][pi];
-                flight_.callbacks.back().second.swap(p->callbacks_);
-            }
-            if (p->group_ & 2)
-                delete p;   // orphan of a freed instance (see ~Program)
-            else
-                p->reset_after_flush();
+void Engine::completer_loop()
+{
+    for (;;) {
+        Batch* b = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(qMu_);
+            completeCv_.wait(lk, [&] { return stop_ || !toComplete_.empty(); });
+            if (stop_)
+                return;
+            b = toComplete_.front();
+            toComplete_.pop_front();
         }
-    flight_.active = true;
-    for (Shard* s : shards) {
-        s->dirty.clear();
-        s->ingest.clear();
-        s->hostStage.clear();
-        s->downloads.clear();
-        // buffers released before this flush may be reused once it completes
-        s->flightFree.swap(s->pendingFree);
-        s->pendingFree.clear();
+        tl("complete begin", b->ticket);
+        complete_batch(*b);
+        tl("complete end", b->ticket);
+        {
+            std::lock_guard<std::mutex> g(qMu_);
+            sets_[b->set].busyTicket = 0;
+            doneTicket_ = b->ticket;
+        }
+        setCv_.notify_all();
+        doneCv_.notify_all();
+        delete b;
     }
-    return true;
+}
+
+void Engine::complete_batch(Batch& bt)
+{
+    const uint64_t t0 = now_ns();
+    EngineStats st;
+    const bool ok = bt.launched && be_fence_wait(bt.fence) && !failed();
+    const uint64_t t1 = now_ns();
+    tl("fence passed", bt.ticket);
+    st.waitNs = t1 - t0;
+    if (!ok) {
+        // The results buffer and downloads of this submission are not valid:
+        // deliver nothing, keep its released buffers out of reuse, and fail
+        // every instance from now on.
+        failed_.store(true, std::memory_order_relaxed);
+        for (int g = 0; g < 2; ++g)
+            for (ProgramBody* p : bt.bodies[g]) {
+                p->callbacks.clear();
+                ProgramBody::put(p);
+            }
+        std::lock_guard<std::mutex> g(statsMu_);
+        flushStats_.add(st);
+        return;
+    }
+    const XferSet& xs = sets_[bt.set];
+    for (const Batch::Download& d : bt.downloads)
+        std::memcpy(d.host, xs.downHost + d.off, d.bytes);
+    // bytes the kernels counted: terms the executor expanded itself, and the
+    // solves' back-substitution (source bytes, recovered bytes)
+    uint64_t acct[3];
+    std::memcpy(acct, xs.downHost, sizeof(acct));
+    st.refOpBytes += acct[0] + acct[1];
+    st.outBytes += acct[2];
+    st.solveBytes += acct[1] + acct[2];
+    const uint32_t* results = (const uint32_t*)(xs.downHost + kAcctBytes);
+    for (int g = 0; g < 2; ++g)
+        for (size_t i = 0; i < bt.bodies[g].size(); ++i) {
+            ProgramBody* p = bt.bodies[g][i];
+            for (Completion& fn : p->callbacks)
+                fn(results + bt.resultBase[g][i]);
+            ProgramBody::put(p);
+        }
+    const uint64_t t2 = now_ns();
+    st.completeNs = t2 - t1;
+    // Released buffers are free once this submission (and so every earlier
+    // one) has run: they go back to the depot as magazines, and the emptied
+    // queues back to their shard.
+    for (size_t qi = 0; qi < bt.queues.size(); ++qi) {
+        Shard::Queues& q = bt.queues[qi];
+        for (size_t cls = 0; cls < q.released.size(); ++cls) {
+            std::vector<uint8_t*>& r = q.released[cls];
+            if (r.empty())
+                continue;
+            std::lock_guard<std::mutex> g(depotMu_);
+            if (cls >= depot_.size())
+                depot_.resize(cls + 1);
+            if (r.size() <= kMaxMagazine) {
+                depot_[cls].emplace_back();
+                depot_[cls].back().swap(r);
+            } else {
+                for (size_t k = 0; k < r.size(); k += kMaxMagazine)
+                    depot_[cls].emplace_back(r.begin() + (long)k,
+                                             r.begin() + (long)std::min(r.size(), k + kMaxMagazine));
+                r.clear();
+            }
+        }
+        q.clear();
+        Shard* s = bt.queueOwner[qi];
+        std::lock_guard<std::mutex> g(s->mu);
+        if (s->spare.size() < 4)
+            s->spare.push_back(std::move(q));
+    }
+    st.reclaimNs = now_ns() - t2;
+    std::lock_guard<std::mutex> g(statsMu_);
+    flushStats_.add(st);
 }
 
 bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut)
 {
-    if (flight_.active && !sync())
-        return false;
-    if (failed())
+    if (!sync())
         return false;
     if (count == 0)
         return true;
@@ -1161,67 +1408,6 @@ bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* byt
         }
     });
     return ok;
-}
-
-bool Engine::sync()
-{
-    if (!flight_.active)
-        return true;
-    const uint64_t t0 = now_ns();
-    const bool ok = be_sync();
-    if (!ok) {
-        // The results buffer and downloads of this flush are not valid:
-        // deliver nothing, keep the flush's released buffers out of reuse,
-        // and fail every instance from now on.
-        failed_.store(true, std::memory_order_relaxed);
-        flight_.callbacks.clear();
-        flight_.downloads.clear();
-        flight_.active = false;
-        flushStats_.waitNs += now_ns() - t0;
-        return false;
-    }
-    for (const InFlight::Download& d : flight_.downloads)
-        std::memcpy(d.host, downHost_ + d.off, d.bytes);
-    const uint64_t t1 = now_ns();
-    // Completions of different programs touch different instances: run them
-    // in parallel, each program's in order.
-    // bytes the executor counted for the terms it expanded itself
-    uint64_t acct = 0;
-    std::memcpy(&acct, downHost_, sizeof(acct));
-    flushStats_.refOpBytes += acct;
-    const uint32_t* results = (const uint32_t*)(downHost_ + 16);
-    pool().run(flight_.callbacks.size(), [&](size_t i) {
-        auto& cb = flight_.callbacks[i];
-        for (Completion& fn : cb.second)
-            fn(results + cb.first);
-    });
-    flight_.callbacks.clear();
-    flight_.downloads.clear();
-    flight_.active = false;
-    const uint64_t t2 = now_ns();
-    std::vector<Shard*> shards;
-    {
-        std::lock_guard<std::mutex> g(shardsMu_);
-        for (auto& s : shards_)
-            shards.push_back(s.get());
-    }
-    // each shard's released buffers go back to its own free lists
-    pool().run(shards.size(), [&](size_t i) {
-        Shard* s = shards[i];
-        for (const DevBuf& b : s->flightFree) {
-            const size_t cls = cap_class(b.cap);
-            if (cls >= s->freeLists.size())
-                s->freeLists.resize(cls + 1);
-            s->freeLists[cls].push_back(b.ptr);
-        }
-        s->flightFree.clear();
-        spill(*s);
-    });
-    const uint64_t t3 = now_ns();
-    flushStats_.waitNs += t1 - t0;
-    flushStats_.completeNs += t2 - t1;
-    flushStats_.reclaimNs += t3 - t2;
-    return true;
 }
 
 } // namespace sgpu

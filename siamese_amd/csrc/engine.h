@@ -1,23 +1,33 @@
 // engine.h -- device-side resources of the codec: an arena of symbol
-// buffers in HBM, per-instance op programs, and the flush that turns all
-// pending programs into a handful of kernel launches.
+// buffers in HBM, per-instance op programs, and the asynchronous flush
+// pipeline that turns all pending programs into a handful of kernel launches.
 //
 // Threading: codec instances may be driven concurrently from different host
 // threads (one thread per instance at a time).  Everything an instance call
 // touches in the engine lives in the calling thread's Shard (buffer free
 // lists, ingest queue, downloads, statistics) or in the instance's own
-// Program, so per-instance calls take no global lock.  flush()/sync()/
-// gather() are exclusive: the caller guarantees no instance call runs
-// concurrently with them (the siamese_gpu.h contract).
+// Program, so per-instance calls take no global lock.
+//
+// Flushes are pipelined: enqueue() detaches every
+// queued program body and per-thread queue in O(programs) pointer swaps and
+// returns a ticket; a launcher thread lays the work out, uploads it and
+// launches the kernels; a completer thread waits for the device and runs the
+// completions.  enqueue() is exclusive with instance calls; wait(ticket) is
+// not, so host threads keep driving other instances while a flush is
+// assembled, runs on the GPU and completes.  An instance with work in a
+// submission is not called again until that submission has been waited for.
 #pragma once
 
 #include "ops.h"
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace sgpu {
@@ -35,10 +45,72 @@ struct DevBuf
 
 class Engine;
 struct Shard;
+struct Batch;
 
 /// Completion callback of a flush; `results` is the solve-result word array
 /// as seen by the program that registered it (indices returned by solve()).
 using Completion = std::function<void(const uint32_t* results)>;
+
+/// Everything a program has queued since it was last detached.  Bodies move
+/// whole into a flush (an O(1) swap) and come back to a shared pool once the
+/// flush has been laid out and completed, keeping their capacity.
+struct ProgramBody
+{
+    struct Segment
+    {
+        std::vector<GfOp> ops;
+        std::vector<GfTerm> terms;
+        std::vector<uint8_t> rowsData;   // closed OP_ROWS / OP_COPIES blocks (ops.h layout)
+        uint32_t rowsWords = 0;          // stream words of those blocks (after headers)
+        uint32_t maxExtent = 0;
+        void clear()
+        {
+            ops.clear();
+            terms.clear();
+            rowsData.clear();
+            rowsWords = 0;
+            maxExtent = 0;
+        }
+    };
+    /// The OP_ROWS batch under construction (always the segment's last op).
+    struct RowsBuild
+    {
+        bool open = false;
+        bool haveSums = false;
+        WinEntry sums[kRowSums];
+        uint32_t readMask = 0;          // sums read by the batch's rows
+        uint32_t base = 0;              // window element of entry 0
+        std::vector<WinEntry> win;
+        std::vector<SumUpdate> updates;
+        int updateOf[kRowSums];         // index into updates, or -1
+        std::vector<RowItem> rows;
+        uint32_t maxExtent = 0;
+    };
+    struct PendingSolve
+    {
+        SolveDesc desc;
+        std::vector<SolveRow> rows;
+        std::vector<uint8_t> coef;
+    };
+
+    int group = 0;
+    uint32_t resultWords = 0;   // result words reserved in this body
+    size_t nsegs = 0;           // segments in use (capacity is kept)
+    std::vector<Segment> segs;
+    std::vector<PendingSolve> solves;   // solve k follows segment k
+    std::vector<Completion> callbacks;
+    RowsBuild rb;
+    std::vector<CopyItem> copies;       // the open OP_COPIES batch (segment's last op)
+
+    bool empty() const { return nsegs == 0 || (nsegs == 1 && segs[0].ops.empty() && copies.empty() && !rb.open); }
+    void new_segment();
+    void rows_open(uint32_t base, bool keepWindow);
+    void rows_close();   // closes the open OP_ROWS or OP_COPIES batch
+    void clear();        // back to the freshly constructed state (capacity kept)
+
+    static ProgramBody* get();
+    static void put(ProgramBody* b);
+};
 
 /// Ops of one codec instance since the last flush.  Segments are separated
 /// by triangular solves; `group` orders instances inside a flush (group 0 =
@@ -46,7 +118,7 @@ using Completion = std::function<void(const uint32_t* results)>;
 class Program
 {
 public:
-    Program(Engine* e, int group) : eng_(e), group_(group) { take_store(); }
+    Program(Engine* e, int group) : eng_(e), group_(group) {}
     ~Program();
     Program(const Program&) = delete;
     Program& operator=(const Program&) = delete;
@@ -58,7 +130,7 @@ public:
     // (lc_term must follow lc_begin directly: it appends to the last op)
     void lc_term(uint64_t src, uint32_t len, uint8_t coeff, uint8_t acc = 0)
     {
-        Segment& s = segs_[nsegs_ - 1];
+        ProgramBody::Segment& s = b_->segs[b_->nsegs - 1];
         GfOp& op = s.ops.back();
         if (len > op.n)
             len = op.n;
@@ -95,7 +167,7 @@ public:
     /// (valid in this program's completion callbacks of the flush that runs it).
     uint32_t solve(const std::vector<SolveRow>& rows, const uint8_t* coef, uint32_t maxBytes);
 
-    /// Run `fn(results)` once the next flush has completed.
+    /// Run `fn(results)` once the flush holding this program's work completes.
     void on_complete(Completion fn);
 
     /// Siamese row batches (OP_ROWS, ops.h).  A batch holds a snapshot of
@@ -114,79 +186,33 @@ public:
                   uint32_t mask0, uint32_t mask1, unsigned row, uint32_t ldpcN,
                   uint32_t ldpcFirst, const uint8_t* lit = nullptr, uint32_t litLen = 0);
     /// Close the open batch (its window may change after this).
-    void rows_seal() { rows_close(); }
+    void rows_seal()
+    {
+        if (b_)
+            b_->rows_close();
+    }
 
     /// dst[0,len) = src[0,len) (zero tail), one of a batch of independent
     /// copies (OP_COPIES): the destinations are fresh buffers no other op of
     /// the batch touches.
     void copy(uint64_t dst, uint64_t src, uint32_t len);
 
-    bool empty() const { return nsegs_ == 0 || (nsegs_ == 1 && segs_[0].ops.empty()); }
+    bool empty() const { return !b_ || b_->empty(); }
 
 private:
     friend class Engine;
-    struct Segment
-    {
-        std::vector<GfOp> ops;
-        std::vector<GfTerm> terms;
-        std::vector<uint8_t> rowsData;   // closed OP_ROWS blocks (ops.h layout)
-        uint32_t rowsWords = 0;          // stream words of those blocks (after headers)
-        uint32_t maxExtent = 0;
-    };
-    /// The OP_ROWS batch under construction (always the segment's last op).
-    struct RowsBuild
-    {
-        bool open = false;
-        bool haveSums = false;
-        WinEntry sums[kRowSums];
-        uint32_t readMask = 0;          // sums read by the batch's rows
-        uint32_t base = 0;              // window element of entry 0
-        std::vector<WinEntry> win;
-        std::vector<SumUpdate> updates;
-        int updateOf[kRowSums];         // index into updates, or -1
-        std::vector<RowItem> rows;
-        uint32_t maxExtent = 0;
-    };
-    void rows_close();   // closes the open OP_ROWS or OP_COPIES batch
-    void rows_open(uint32_t base, bool keepWindow);
-    std::vector<CopyItem> copies_;   // the open OP_COPIES batch (segment's last op)
-    // The containers of programs that went away are kept per host thread and
-    // handed to new programs, so a fresh codec starts with warm capacity.
-    struct Store
-    {
-        std::vector<Segment> segs;
-        std::vector<WinEntry> win;
-        std::vector<SumUpdate> updates;
-        std::vector<RowItem> rows;
-    };
-    static std::vector<Store>& spare_stores();
-    void take_store();
-    void stash_store();
-    struct PendingSolve
-    {
-        SolveDesc desc;
-        std::vector<SolveRow> rows;
-        std::vector<uint8_t> coef;
-    };
-
     void touch()
     {
         if (!shard_)
             attach();
     }
     void attach();
-    void new_segment();
-    void reset_after_flush();
+    void rows_open(uint32_t base, bool keepWindow) { b_->rows_open(base, keepWindow); }
 
     Engine* eng_;
     int group_;
     Shard* shard_ = nullptr;     // shard this program is queued in (null: clean)
-    uint32_t resultWords_ = 0;   // result words reserved since the last flush
-    size_t nsegs_ = 0;           // segments in use (capacity is kept across flushes)
-    std::vector<Segment> segs_;
-    std::vector<PendingSolve> solves_;   // solve k follows segment k
-    std::vector<Completion> callbacks_;
-    RowsBuild rb_;
+    ProgramBody* b_ = nullptr;   // the queued work (null until the first op)
 };
 
 /// Algorithmic byte accounting and flush counters.
@@ -199,8 +225,9 @@ struct EngineStats
     // originals produced.
     uint64_t refOpBytes = 0, outBytes = 0;
     uint64_t solveBytes = 0;   // the part of both done by the solve kernels
-    // host time of flush assembly, device waits, completion callbacks and
-    // returning released buffers to the free lists (nanoseconds)
+    // host time of flush assembly (launcher thread), device waits and
+    // completion callbacks (completer thread), and returning released
+    // buffers to the arena (nanoseconds)
     uint64_t assembleNs = 0, waitNs = 0, completeNs = 0, reclaimNs = 0;
     uint64_t execLaunches = 0;   // executor launches (part of `launches`)
 
@@ -223,29 +250,42 @@ public:
     uint64_t arena_bytes() const { return arenaBytes_.load(std::memory_order_relaxed); }
 
     /// Copy `bytes` of device memory to host memory once the next flush has
-    /// executed; the data is in place after sync().
+    /// executed; the data is in place after that flush has been waited for.
     void download(void* hostDst, uint64_t devSrc, uint32_t bytes);
 
-    /// Launch all queued work (completing the flush in flight first).
-    /// Returns false once the device has failed.
+    /// Detach all queued work and hand it to the launcher.  Exclusive with
+    /// instance calls.  Returns the submission's ticket (> 0), or 0 once the
+    /// device has failed.
+    uint64_t enqueue();
+    /// Wait until submission `ticket` (and every earlier one) has completed.
+    /// On a device failure nothing of the failed submission is delivered (no
+    /// downloads, no completions), the engine is marked failed, and every
+    /// instance reports Siamese_Disabled from then on (sticky, like the
+    /// reference's EmergencyDisabled, siamese.h:147-150).
+    bool wait(uint64_t ticket);
+    /// Non-blocking: has submission `ticket` completed?
+    bool done(uint64_t ticket)
+    {
+        std::lock_guard<std::mutex> g(qMu_);
+        return doneTicket_ >= ticket;
+    }
+    /// Ticket of the latest submission.
+    uint64_t last_ticket() const { return nextTicket_; }
+    /// Submit, then complete the previous submission (one flush in flight).
     bool flush();
-    /// Wait for the flush in flight and run its completions.  On a device
-    /// failure nothing of that flush is delivered (no downloads, no
-    /// completions), the engine is marked failed, and every instance reports
-    /// Siamese_Disabled from then on (sticky, like the reference's
-    /// EmergencyDisabled, siamese.h:147-150).
-    bool sync();
+    /// Complete every submission.
+    bool sync() { return wait(nextTicket_); }
     bool flush_and_sync()
     {
-        const bool ok = flush();
-        return sync() && ok;
+        const uint64_t t = enqueue();
+        return wait(t) && t != 0;
     }
     /// A device operation failed; the engine accepts no further work.
     bool failed() const { return failed_.load(std::memory_order_relaxed); }
     bool pending() const;
 
     /// Copy device ranges into one host buffer right now (after completing
-    /// any flush in flight).  Queued, unflushed work is not touched.
+    /// every submission).  Queued, unsubmitted work is not touched.
     bool gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut);
 
     /// Serialises the drop-in siamese.h entry points and the exclusive
@@ -260,6 +300,10 @@ public:
     /// The calling thread's shard.
     Shard& shard();
 
+    /// The engine's host worker pool (also offered to applications,
+    /// sgpu_parallel_for).
+    WorkerPool& pool();
+
 private:
     friend class Program;
     void stage_host_ingest(const DevBuf& dst, const void* data, uint32_t bytes, const uint8_t* hdr,
@@ -267,8 +311,15 @@ private:
     void add_ingest(const IngestDesc& d, int64_t hostStageOffset);
     uint8_t* carve_region(size_t bytes);
     bool refill(Shard& s, size_t cls, uint32_t cap);
-    void spill(Shard& s);
-    WorkerPool& pool();
+
+    // ---- flush pipeline
+    void launcher_loop();
+    void completer_loop();
+    void assemble_batch(Batch& b);
+    void launch_batch(Batch& b);
+    void complete_batch(Batch& b);
+    void start_threads();
+    void stop_threads();
 
     bool ready_ = false;
     std::atomic<bool> failed_{false};
@@ -276,10 +327,10 @@ private:
 
     // ---- arena: 64 MiB hipMalloc chunks are cut into 4 MiB regions under
     // arenaMu_; a shard bump-allocates buffers from its own region.  Free
-    // buffers live in per-shard lists by capacity class and move between
-    // shards in magazines of kMagazine through the depot (depotMu_), so a
-    // buffer released on one host thread is reused on another without a
-    // lock per buffer and the arena stops growing once warm.
+    // buffers live in per-shard lists by capacity class; a completed flush
+    // returns its released buffers to the depot (depotMu_) in magazines,
+    // which shards take whole when their list runs dry, so the arena stops
+    // growing once warm.
     struct Chunk
     {
         uint8_t* base;
@@ -289,38 +340,38 @@ private:
     std::vector<Chunk> chunks_;
     std::atomic<uint64_t> arenaBytes_{0};
     std::mutex depotMu_;
-    std::vector<std::vector<uint8_t*>> depot_;   // [class] -> free buffers
+    std::vector<std::vector<std::vector<uint8_t*>>> depot_;   // [class] -> magazines
 
     // ---- shards (one per host thread that touched the engine)
     mutable std::mutex shardsMu_;
     std::vector<std::unique_ptr<Shard>> shards_;
 
-    // ---- flush-level state (exclusive)
+    // ---- flush pipeline state
+    std::mutex statsMu_;
     EngineStats flushStats_;
-    struct InFlight
-    {
-        struct Download
-        {
-            void* host;
-            size_t off;
-            uint32_t bytes;
-        };
-        std::vector<Download> downloads;
-        // per program: (results base, its completions in order)
-        std::vector<std::pair<uint32_t, std::vector<Completion>>> callbacks;
-        bool active = false;
-    } flight_;
+    uint64_t nextTicket_ = 0;                       // last ticket handed out (enqueue only)
+    std::mutex qMu_;
+    std::condition_variable launchCv_, completeCv_, doneCv_, setCv_;
+    std::deque<Batch*> toLaunch_, toComplete_;
+    uint64_t doneTicket_ = 0;                       // every ticket <= this has completed
+    bool stop_ = false;
+    std::thread launcher_, completer_;
     std::unique_ptr<WorkerPool> pool_;
 
-    // transfer buffers (grown on demand)
-    uint8_t* upHost_ = nullptr;
-    uint8_t* upDev_ = nullptr;
-    size_t upCap_ = 0;
-    uint8_t* downHost_ = nullptr;
-    uint8_t* downDev_ = nullptr;   // device-side gather area for downloads + results
-    size_t downCap_ = 0;
-    void ensure_up(size_t bytes);
-    void ensure_down(size_t bytes);
+    // transfer buffer sets: one per submission in flight (ticket % kSets)
+    static constexpr unsigned kSets = 4;
+    struct XferSet
+    {
+        uint8_t* upHost = nullptr;
+        uint8_t* upDev = nullptr;
+        size_t upCap = 0;
+        uint8_t* downHost = nullptr;
+        uint8_t* downDev = nullptr;   // device-side gather area for downloads + results
+        size_t downCap = 0;
+        uint64_t busyTicket = 0;      // submission using it (0: free)
+    } sets_[kSets];
+    void ensure_up(XferSet& x, size_t bytes);
+    void ensure_down(XferSet& x, size_t bytes);
 
     // gather buffers (separate from the flush buffers)
     uint8_t* gUpHost_ = nullptr;
@@ -332,7 +383,7 @@ private:
 };
 
 /// Per-host-thread engine state.  Only its owning thread touches it between
-/// flushes, except `dirty`, which a program's destructor may edit from
+/// submissions, except `dirty`, which a program's destructor may edit from
 /// another thread (guarded by `mu`).
 struct Shard
 {
@@ -347,16 +398,23 @@ struct Shard
         uint64_t dev;
         uint32_t bytes;
     };
+    /// What a submission takes from the shard (swapped out whole).
+    struct Queues
+    {
+        std::vector<IngestRec> ingest;
+        std::vector<uint8_t> hostStage;
+        std::vector<Download> downloads;
+        std::vector<std::vector<uint8_t*>> released;   // by capacity class
+        bool empty() const;
+        void clear();
+    };
 
     std::mutex mu;
     std::vector<Program*> dirty;
-    std::vector<IngestRec> ingest;
-    std::vector<uint8_t> hostStage;
-    std::vector<Download> downloads;
-    std::vector<DevBuf> pendingFree;   // released since the last flush
-    std::vector<DevBuf> flightFree;    // released before the flush in flight
+    Queues q;
+    std::vector<Queues> spare;                      // recycled by completed submissions (mu)
     std::vector<std::vector<uint8_t*>> freeLists;   // by capacity class
-    uint8_t* bump = nullptr;                         // this shard's arena region
+    uint8_t* bump = nullptr;                        // this shard's arena region
     size_t bumpLeft = 0;
     int64_t inUse = 0;
     EngineStats stats;

@@ -3,8 +3,19 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 namespace sgpu {
+
+namespace {
+// SIAMESE_AMD_WORKER_NICE overrides (0 = same priority as the engine threads)
+const int kWorkerNice = [] {
+    const char* v = std::getenv("SIAMESE_AMD_WORKER_NICE");
+    return v ? std::atoi(v) : 10;
+}();
+} // namespace
 
 unsigned WorkerPool::default_threads()
 {
@@ -20,7 +31,13 @@ unsigned WorkerPool::default_threads()
 WorkerPool::WorkerPool(unsigned threads)
 {
     for (unsigned i = 1; i < threads; ++i)
-        workers_.emplace_back([this] { loop(); });
+        workers_.emplace_back([this] {
+            // Workers yield the CPU to the engine's launcher and completer
+            // threads (nice 0), which sit on the device's critical path:
+            // a nice-10 worker is preempted as soon as either wakes up.
+            (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), kWorkerNice);
+            loop();
+        });
 }
 
 WorkerPool::~WorkerPool()

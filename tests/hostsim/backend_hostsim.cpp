@@ -11,6 +11,7 @@
 #include "../../siamese_amd/csrc/gf.h"
 #include "../../siamese_amd/csrc/codedef.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -319,7 +320,7 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                            uint32_t* results, uint32_t count)
+                            uint32_t* results, uint32_t count, uint64_t* acct)
 {
     for (uint32_t s = 0; s < count; ++s) {
         const SolveDesc& sd = solves[s];
@@ -360,11 +361,14 @@ void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const
             out[1 + i] = ((uint32_t)h << 29) | len;
             const uint32_t bb = (uint32_t)h + len;
             ++ok;
+            acct[0] += lc > bb ? lc : bb;
+            acct[1] += bb;
             for (uint32_t j = 0; j < (uint32_t)i; ++j) {
                 const uint8_t c = C[(size_t)j * m + i];
                 if (!c)
                     continue;
                 const uint32_t ab = bb < R[j].finalBytes ? bb : R[j].finalBytes;
+                acct[0] += ab;
                 for (uint32_t b = 0; b < 4 && b < ab; ++b)
                     pre[j * 4 + b] ^= gf_mul(x[b], c);
             }
@@ -431,15 +435,18 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
 // report a device fault (tests of the sticky Disabled path).
 bool be_sync()
 {
-    static long failAt = -2;
-    static long calls = 0;
+    static std::atomic<long> failAt{-2};
+    static std::atomic<long> calls{0};
     if (failAt == -2) {
         const char* v = std::getenv("HOSTSIM_FAIL_SYNC");
         failAt = v ? std::atol(v) : -1;
     }
-    ++calls;
-    return failAt < 1 || calls < failAt;
+    const long c = ++calls;
+    return failAt < 1 || c < failAt;
 }
+// fences are synchronisations too (they count toward HOSTSIM_FAIL_SYNC)
+void* be_fence() { return reinterpret_cast<void*>(1); }
+bool be_fence_wait(void*) { return be_sync(); }
 void be_timing_enable(bool) {}
 void be_timing_reset() {}
 double be_timing_exec_ms() { return 0; }

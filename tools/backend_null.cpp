@@ -73,7 +73,7 @@ void be_launch_ingest(const IngestDesc*, uint32_t) {}
 void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*) {}
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow*, const uint8_t*,
-                            uint32_t* results, uint32_t count)
+                            uint32_t* results, uint32_t count, uint64_t*)
 {
     const SolveDesc* sd = host_view(solves);
     for (uint32_t s = 0; s < count; ++s) {
@@ -90,6 +90,8 @@ void be_launch_solve_main(const SolveDesc*, const SolveRow*, const uint8_t*, con
 }
 
 bool be_sync() { return true; }
+void* be_fence() { return reinterpret_cast<void*>(1); }
+bool be_fence_wait(void*) { return true; }
 void be_timing_enable(bool) {}
 void be_timing_reset() {}
 double be_timing_exec_ms() { return 0; }
