@@ -28,12 +28,20 @@ inline unsigned first_clear(uint64_t bits, unsigned from)
 } // namespace
 
 DecoderCore::DecoderCore(Engine* eng, bool hostMirror)
-    : eng_(eng), prog_(eng, 1), mirror_(hostMirror), alive_(std::make_shared<int>(0))
+    : eng_(eng), prog_(eng, 1), mirror_(hostMirror)
 {
 }
 
 DecoderCore::~DecoderCore()
 {
+    if (pendingSolves_ > 0) {
+        // Completions must not reach a freed decoder: drop the ones still
+        // queued in our program, and let submitted ones finish first (the
+        // siamese_gpu.h contract has the caller wait before freeing; this
+        // covers callers that do not).
+        prog_.drop_callbacks();
+        eng_->wait(eng_->last_ticket());
+    }
     for (RecPacket* r = head_; r;) {
         RecPacket* n = r->next;
         free_packet(r);
@@ -1266,13 +1274,17 @@ bool DecoderCore::eliminate_original_data()
 SiameseResult DecoderCore::solve_and_substitute()
 {
     const unsigned m = region_.lostCount;
-    std::vector<RecPacket*> pr(m);
-    std::vector<unsigned> len(m);
+    // (scratch vectors are members: a decode allocates nothing once warm)
+    std::vector<RecPacket*>& pr = scratchRec_;
+    std::vector<unsigned>& len = scratchLen_;
+    std::vector<SolveRow>& desc = scratchRows_;
+    pr.resize(m);
+    len.resize(m);
     for (unsigned i = 0; i < m; ++i) {
         pr[i] = rows_[pivots_[i]].rec;
         len[i] = pr[i]->bytes;
     }
-    std::vector<SolveRow> desc(m);
+    desc.resize(m);
     for (unsigned i = 0; i < m; ++i) {
         std::memset(&desc[i], 0, sizeof(SolveRow));
         desc[i].initBytes = len[i];
@@ -1312,7 +1324,8 @@ SiameseResult DecoderCore::solve_and_substitute()
         desc[i].finalBytes = len[i];
         maxBytes = std::max(maxBytes, len[i]);
     }
-    std::vector<uint8_t> coef((size_t)m * m);
+    std::vector<uint8_t>& coef = scratchCoef_;
+    coef.resize((size_t)m * m);
     for (unsigned j = 0; j < m; ++j)
         std::memcpy(coef.data() + (size_t)j * m, mrow(pivots_[j]), m);
 
@@ -1322,8 +1335,19 @@ SiameseResult DecoderCore::solve_and_substitute()
     // the outputs (lengths patched in resolve()).
     recovered_.resize(m);
     ++decodeSerial_;
-    std::vector<Fix> fixes;
-    fixes.reserve(m);
+    // a free slot for this solve's completion state
+    unsigned slot = 0;
+    while (slot < pend_.size() && pend_[slot].live)
+        ++slot;
+    if (slot == pend_.size())
+        pend_.emplace_back();
+    PendingDecode& pd = pend_[slot];
+    pd.live = true;
+    pd.base = base;
+    pd.m = m;
+    pd.serial = decodeSerial_;
+    std::vector<Fix>& fixes = pd.fixes;
+    fixes.clear();
     bool advanced = false;
     for (int ci = (int)m - 1; ci >= 0; --ci) {
         RecPacket* r = pr[ci];
@@ -1346,16 +1370,11 @@ SiameseResult DecoderCore::solve_and_substitute()
         fixes.push_back(Fix{o, o->buf.ptr, (uint32_t)ci, (unsigned)ci, len[ci]});
     }
     lastDecoded_ = fixes;
-    std::weak_ptr<int> alive = alive_;
-    const uint64_t serial = decodeSerial_;
     pendingSolves_++;
     // (the back-substitution's reference source bytes need the recovered
-    // lengths: the solve kernel counts them, SiameseDecoder.cpp:1131-1212)
-    prog_.on_complete([this, alive, fixes, base, m, serial](const uint32_t* results) {
-        if (alive.expired())
-            return;
-        resolve_solve(results, base, m, fixes, serial);
-    });
+    // lengths: the solve kernel counts them, SiameseDecoder.cpp:1131-1212).
+    // The callback holds two words, so std::function keeps it inline.
+    prog_.on_complete([this, slot](const uint32_t* results) { resolve_solve(results, slot); });
 
     if (!advanced) {
         disabled_ = true;
@@ -1369,13 +1388,15 @@ SiameseResult DecoderCore::solve_and_substitute()
     return Siamese_Success;
 }
 
-void DecoderCore::resolve_solve(const uint32_t* results, uint32_t base, unsigned m,
-                                const std::vector<Fix>& fixes, uint64_t serial)
+void DecoderCore::resolve_solve(const uint32_t* results, unsigned slot)
 {
+    PendingDecode& pd = pend_[slot];
+    const uint32_t base = pd.base;
+    const unsigned m = pd.m;
     const unsigned okCount = results[base];
     if (okCount < m)
         disabled_ = true; // corrupt length prefix (reference :1142-1154)
-    for (const Fix& f : fixes) {
+    for (const Fix& f : pd.fixes) {
         const unsigned ci = f.outIndex;
         if (ci + okCount < m)
             continue; // not reached before the failure
@@ -1390,12 +1411,13 @@ void DecoderCore::resolve_solve(const uint32_t* results, uint32_t base, unsigned
             if (mirror_ && s->host.size() < s->bytes)
                 s->host.resize(s->bytes);
         }
-        if (serial == decodeSerial_ && ci < recovered_.size()) {
+        if (pd.serial == decodeSerial_ && ci < recovered_.size()) {
             SiameseOriginalPacket& out = recovered_[ci];
             out.DataBytes = len;
             out.Data = (mirror_ ? s->host.data() : f.buf) + hdr;
         }
     }
+    pd.live = false;
     pendingSolves_--;
 }
 

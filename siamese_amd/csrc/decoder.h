@@ -255,10 +255,23 @@ private:
         unsigned outIndex;     // index into recovered_
         unsigned bound;        // upper bound on the length (row length)
     };
-    void resolve_solve(const uint32_t* results, uint32_t base, unsigned m,
-                       const std::vector<Fix>& fixes, uint64_t serial);
+    /// A queued solve whose completion has not run yet (slots are reused).
+    struct PendingDecode
+    {
+        std::vector<Fix> fixes;
+        uint32_t base = 0;
+        unsigned m = 0;
+        uint64_t serial = 0;
+        bool live = false;
+    };
+    void resolve_solve(const uint32_t* results, unsigned slot);
+    std::vector<PendingDecode> pend_;
     std::vector<Fix> lastDecoded_;
-    std::shared_ptr<int> alive_;     // lets completion callbacks outlive us safely
+    // scratch of solve_and_substitute (reused across decodes)
+    std::vector<RecPacket*> scratchRec_;
+    std::vector<unsigned> scratchLen_;
+    std::vector<SolveRow> scratchRows_;
+    std::vector<uint8_t> scratchCoef_;
     uint64_t decodeSerial_ = 0;
     unsigned pendingSolves_ = 0;
 

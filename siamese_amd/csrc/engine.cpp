@@ -87,7 +87,7 @@ void ProgramBody::clear()
         segs[k].clear();
     nsegs = 0;
     resultWords = 0;
-    solves.clear();
+    nsolves = 0;   // (their vectors keep their capacity)
     callbacks.clear();
     rb.open = false;
     rb.win.clear();
@@ -327,16 +327,17 @@ uint32_t Program::solve(const std::vector<SolveRow>& rows, const uint8_t* coef, 
     touch();
     if (b_->nsegs == 0)
         b_->new_segment(); // the segment preceding this solve
-    ProgramBody::PendingSolve ps;
+    if (b_->nsolves == b_->solves.size())
+        b_->solves.emplace_back();
+    ProgramBody::PendingSolve& ps = b_->solves[b_->nsolves++];
     std::memset(&ps.desc, 0, sizeof(ps.desc));
     ps.desc.m = (uint32_t)rows.size();
     ps.desc.maxBytes = maxBytes;
     ps.desc.result = b_->resultWords;
     b_->resultWords += ps.desc.m + 1;
-    ps.rows = rows;
+    ps.rows.assign(rows.begin(), rows.end());
     ps.coef.assign(coef, coef + rows.size() * rows.size());
     const uint32_t r = ps.desc.result;
-    b_->solves.push_back(std::move(ps));
     b_->new_segment(); // ops after the solve go to the next segment
     return r;
 }
@@ -1050,7 +1051,7 @@ void Engine::assemble_batch(Batch& bt)
             Phase sv{Phase::SOLVE, sitems.size(), 0, sdescs.size(), 0, 0};
             for (size_t pi = 0; pi < bt.bodies[g].size(); ++pi) {
                 const ProgramBody* p = bt.bodies[g][pi];
-                if (k >= p->solves.size())
+                if (k >= p->nsolves)
                     continue;
                 const ProgramBody::PendingSolve& ps = p->solves[k];
                 SolveDesc d = ps.desc;

@@ -97,7 +97,8 @@ struct ProgramBody
     uint32_t resultWords = 0;   // result words reserved in this body
     size_t nsegs = 0;           // segments in use (capacity is kept)
     std::vector<Segment> segs;
-    std::vector<PendingSolve> solves;   // solve k follows segment k
+    std::vector<PendingSolve> solves;   // solve k follows segment k (nsolves in use)
+    size_t nsolves = 0;
     std::vector<Completion> callbacks;
     RowsBuild rb;
     std::vector<CopyItem> copies;       // the open OP_COPIES batch (segment's last op)
@@ -169,6 +170,12 @@ public:
 
     /// Run `fn(results)` once the flush holding this program's work completes.
     void on_complete(Completion fn);
+    /// Forget the completions of work not yet submitted (owner going away).
+    void drop_callbacks()
+    {
+        if (b_)
+            b_->callbacks.clear();
+    }
 
     /// Siamese row batches (OP_ROWS, ops.h).  A batch holds a snapshot of
     /// the codec's window (elements [base, end)), lane-sum updates and rows.
