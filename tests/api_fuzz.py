@@ -96,12 +96,66 @@ def run(lib, seed, steps=1500, max_bytes=1500):
     return log
 
 
+def run_arq(lib, seed, rounds=3, sleep_s=0.65):
+    """ARQ scenario past the retransmission timeout (reference
+    SiameseEncoder.cpp:835-1044, :514-800): originals over a lossy link, the
+    decoder's NACK acknowledgement fed to the encoder, then after sleeping
+    beyond any RTO (500 ms initial, 1.5 x max RTT >= 20 ms later) every
+    retransmission the encoder offers, with its bytes, some of them
+    delivered.  Retransmit is only called right after a sleep, so the
+    sequence does not depend on how long the calls themselves take."""
+    import time
+    rnd = random.Random(seed)
+    enc = lib.Encoder()
+    dec = lib.Decoder()
+    log = []
+    sent = {}
+    for _ in range(rounds):
+        loss = rnd.choice([0.1, 0.2, 0.35])
+        for _ in range(rnd.randint(20, 90)):
+            n = rnd.choice([1, 40, 700, 1400, rnd.randint(1, 1500)])
+            data = bytes(rnd.getrandbits(8) for _ in range(n))
+            rc, num = enc.add_raw(data)
+            log.append(("add", rc, num))
+            if rc != Success:
+                continue
+            sent[num] = data
+            if rnd.random() >= loss:
+                log.append(("add_orig", dec.add_original(num, data)))
+        if rnd.random() < 0.5:
+            rc, rec = enc.encode_raw()
+            log.append(("encode", rc, _h(rec)))
+            if rec is not None:
+                log.append(("add_rec", dec.add_recovery(rec)))
+        rc, msg = dec.ack()
+        log.append(("dec_ack", rc, _h(msg)))
+        if msg:
+            log.append(("enc_ack",) + enc.ack(msg))
+        time.sleep(sleep_s)
+        for _ in range(400):
+            rc, r = enc.retransmit()
+            log.append(("retransmit", rc, None if r is None else (r[0], _h(r[1]))))
+            if rc != Success:
+                break
+            assert r[1] == sent.get(r[0]), "retransmitted packet %d corrupt" % r[0]
+            if rnd.random() < 0.7:
+                log.append(("add_orig", dec.add_original(r[0], r[1])))
+        if rnd.random() < 0.3 and sent:
+            num = rnd.randrange(0, len(sent))
+            log.append(("remove_before", num, enc.remove_before(num)))
+    log.append(("enc_stats", enc.stats()[:8]))
+    log.append(("dec_stats", dec.stats()[:10]))
+    enc.close()
+    dec.close()
+    return log
+
+
 def normalise(log):
     import json
     return json.loads(json.dumps(log))
 
 
-def run_isolated(library_path, seed, steps=1500):
+def run_isolated(library_path, seed, steps=1500, scenario="run"):
     """Run the scenario in a child process (the reference can crash on some
     sequences); returns the normalised log or None if the child died."""
     import json
@@ -109,10 +163,11 @@ def run_isolated(library_path, seed, steps=1500):
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
+    args = "%d, %d" % (seed, steps) if scenario == "run" else "%d" % seed
     code = ("import sys, json; sys.path[:0] = [%r, %r]; import api_fuzz; "
             "from siamese_amd.binding import SiameseLib; "
-            "print(json.dumps(api_fuzz.run(SiameseLib(%r).init(), %d, %d)))"
-            % (here, os.path.dirname(here), library_path, seed, steps))
+            "print(json.dumps(api_fuzz.%s(SiameseLib(%r).init(), %s)))"
+            % (here, os.path.dirname(here), scenario, library_path, args))
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
     if p.returncode != 0:
         return None

@@ -33,6 +33,17 @@ def test_random_call_sequences(ref, sim, seed):
     assert api_fuzz.first_difference(a, b) is None
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_retransmit_after_rto(ref, sim, seed):
+    """Retransmissions past the RTO (NACK-driven and oldest-first) carry the
+    same packets and bytes as the reference's (SiameseEncoder.cpp:877-1044)."""
+    a = api_fuzz.run_isolated(S.REF_LIB, seed, scenario="run_arq")
+    b = api_fuzz.normalise(api_fuzz.run_arq(sim, seed))
+    assert a is not None
+    assert any(e[0] == "retransmit" and e[1] == Success for e in a), "no retransmission exercised"
+    assert api_fuzz.first_difference(a, b) is None
+
+
 def test_argument_validation(ref, sim):
     for lib in (ref, sim):
         L = lib.L

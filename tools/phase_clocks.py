@@ -1,0 +1,25 @@
+#!/usr/bin/env python3
+"""Per-phase shader clocks of k_exec's OP_ROWS path (profiling build:
+tools/build_variant.sh phase -DSGPU_PHASE_CLOCKS).  Runs a short C4 bench
+through the variant library, then prints the clocks per workgroup-op.
+usage: python tools/phase_clocks.py siamese_amd/libsiamese_amd_phase.so"""
+import ctypes
+import sys
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+lib = sys.argv[1]
+bench.main(["--library", lib, "--steps", "3", "--warmup", "1", "--no-cpu", "--no-e2e", "--no-legs"])
+L = ctypes.CDLL(os.path.abspath(lib))
+out = (ctypes.c_ulonglong * 16)()
+L.sgpu_debug_phase_clocks(out)
+ops = max(1, out[8])
+names = ["block load", "stage window", "sum updates", "stage sums", "plan", "rows"]
+print("OP_ROWS workgroup-ops %d, rows %.1f, updates %.1f, window %.1f, staged %.1f per op"
+      % (out[8], out[9] / ops, out[10] / ops, out[11] / ops, out[12] / ops))
+for k, nm in enumerate(names):
+    print("  %-14s %10.0f clocks per op" % (nm, out[k] / ops))
+print("kernel: %d workgroups, %.0f clocks each" % (out[7], out[6] / max(1, out[7])))
