@@ -30,7 +30,10 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count);
 /// `stream`: the instruction words of every segment (see ExecItem).
 /// `acct`: device counter the executor adds the reference's source bytes of
 /// the terms it expands itself (sum updates, LDPC picks) to (ops.h).
-void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct);
+/// `maxWindow`: the largest OP_ROWS window (entries) among the launched
+/// segments, kNoRows when none has a row batch (sizes the LDS stage).
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct,
+                    uint32_t maxWindow);
 /// `acct`: acct[0] += the reference's source bytes of each back-substitution
 /// step the solve completes (SiameseDecoder.cpp:1131-1212), acct[1] += the
 /// recovered bytes it outputs.

@@ -21,6 +21,7 @@
 #include "gf.h"
 
 #include <cctype>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <cstring>
@@ -44,6 +45,28 @@ __device__ __forceinline__ uint32_t gf_mul_dword(uint32_t x, uint32_t y)
     const uint32_t c = (x >> 6) & 0x03030303u;
     return __builtin_amdgcn_perm(t[1], t[0], a) ^ __builtin_amdgcn_perm(t[3], t[2], b) ^
            __builtin_amdgcn_perm(0u, t[4], c);
+}
+
+// the same multiply with y's three lookup words already in registers (per
+// lane, or moved to scalars with readlane), so no table fetch sits in a loop
+struct GfTab
+{
+    uint32_t a0, a1, b0, b1, c;
+};
+
+__device__ __forceinline__ GfTab gf_tab(uint32_t y)
+{
+    const uint32_t* t = c_perm[y];
+    return GfTab{t[0], t[1], t[2], t[3], t[4]};
+}
+
+__device__ __forceinline__ uint32_t gf_mul_tab(uint32_t x, const GfTab& t)
+{
+    const uint32_t a = x & 0x07070707u;
+    const uint32_t b = (x >> 3) & 0x07070707u;
+    const uint32_t c = (x >> 6) & 0x03030303u;
+    return __builtin_amdgcn_perm(t.a1, t.a0, a) ^ __builtin_amdgcn_perm(t.b1, t.b0, b) ^
+           __builtin_amdgcn_perm(0u, t.c, c);
 }
 
 __device__ __forceinline__ uint4 gf_mul16(uint4 v, uint32_t y)
@@ -171,71 +194,101 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
 
 // ---------------------------------------------------------------------------
 // Executor
-
-// One workgroup of kExecWaves waves per (instance segment, 2 KiB tile): lane
-// L owns bytes [16L, 16L+16) and [1024+16L, 1024+16L+16) of the tile, so a
-// 1400-byte symbol is one work item and every source costs a wave two
-// coalesced 16-byte loads per lane.
+//
+// One workgroup of kExecWaves waves per (instance segment, 256-byte tile):
+// lane L owns bytes [4L, 4L+4) of the tile, so a 1402-byte symbol spans six
+// work items and a 64 KiB symbol 256, and every source costs a wave one
+// 256-byte coalesced load (global_load_dword) or LDS read.
 //
 // The segment is one instruction stream (ops.h): each op's header and its
 // words are contiguous, and the workgroup keeps the current op's first
 // kRingWords words in an LDS ring while one coalesced load per thread
 // prefetches the next op's, so no op waits on a descriptor round trip.
 //
-//   OP_LINCOMB  terms dealt round-robin to the waves (kExecDepth loads of
-//               each chunk in flight per wave), partial sums meet in LDS,
-//               wave 0 merges and stores.
-//   OP_ROWS     the batch's sums + window snapshot are staged in LDS; the
-//               lane-sum updates are dealt to the waves whole (each wave
-//               generates its own terms and CX coefficients), one barrier,
-//               then the rows are dealt to the waves whole: each wave draws
-//               the row's LDPC picks with PCG jump-ahead (one draw per lane),
-//               accumulates sums and picks, and stores the row and footer.
-//               Rows and updates never meet across waves, so the batch has
-//               two barriers however many rows it holds.
+//   OP_LINCOMB  terms dealt to the waves in contiguous shares (kExecDepth
+//               loads in flight per wave), partial sums meet in LDS, wave 0
+//               merges and stores.
+//   OP_ROWS     the batch's window snapshot is staged in LDS: the tile's 256
+//               bytes of up to `stage` window symbols (one coalesced
+//               bulk load), so every later read of a symbol by the batch's
+//               sum updates and rows is an LDS read instead of an HBM/L2
+//               round trip.  The lane-sum updates are dealt to the waves
+//               whole (each wave generates its element terms and CX
+//               coefficients), one barrier, then the rows: with at least as
+//               many rows as waves each wave takes whole rows; with fewer,
+//               each row's LDPC picks are split across W/R waves (PCG
+//               jump-ahead to each part's first draw) and the partial sums
+//               meet in LDS, so a single large row (C3/C5) still keeps every
+//               wave busy.
+//   OP_COPIES   independent copies dealt to the waves, four at a time.
 // The barrier that rotates the ring also orders each op's stores before any
 // later op of the segment reads them (stores from one CU are visible to the
 // CU's other waves after the workgroup-scope fence of __syncthreads).
 #ifndef SGPU_EXEC_WAVES
-#define SGPU_EXEC_WAVES 8
+#define SGPU_EXEC_WAVES 16
 #endif
-constexpr unsigned kExecWaves = SGPU_EXEC_WAVES;   // 8 measured best of 4/8/16 (16 spills)
+constexpr unsigned kExecWaves = SGPU_EXEC_WAVES;
 constexpr unsigned kExecThreads = 64 * kExecWaves;
-constexpr unsigned kExecDepth = 8;
+constexpr unsigned kExecDepth = 16;          // term loads in flight per wave
 constexpr unsigned kExecSolo = 4;            // ops with <= this many terms run on wave 0 alone
-constexpr unsigned kRingWords = kExecThreads; // one prefetched word per thread
-constexpr unsigned kRowsTableLds = 1024;      // sum + window entries of an OP_ROWS batch in LDS
-constexpr unsigned kChunk = 1024;             // byte distance of a lane's two chunks
+constexpr unsigned kRingWords = 256;         // prefetched words per op (threads < 256 fetch one)
+constexpr unsigned kRowsTableLds = 1024;     // sum + window descriptors of an OP_ROWS batch in LDS
+constexpr unsigned kPlanCap = 8192;          // planned row terms (LDS slot indices) per batch
+constexpr unsigned kPlanRows = 256;          // rows of a batch that get a plan
+constexpr uint32_t kNoPlan = 0xffffffffu;    // row not planned: general path, counts its bytes
+constexpr uint32_t kPlanGeneral = 0xfffffffeu;   // planned and counted, but reads memory
+static_assert(kExecTileBytes == 256, "executor tile = 64 lanes x 4 bytes");
 
 __constant__ uint64_t c_pcgA[65];   // A^j
 __constant__ uint64_t c_pcgG[65];   // sum_{t<j} A^t
+__constant__ uint64_t c_pcgJA[32];  // A^(2^k)
+__constant__ uint64_t c_pcgJG[32];  // sum_{t<2^k} A^t
 __constant__ uint8_t c_sqr[256];
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-struct Acc2
-{
-    uint4 a, b;   // chunk 0 (p) and chunk 1 (p + kChunk)
-};
+#ifdef SGPU_PHASE_CLOCKS
+// profiling build only: shader clocks per OP_ROWS phase, summed over
+// workgroups as seen by thread 0 (tools/phase_clocks.py reads them)
+__device__ unsigned long long g_phaseClk[16];
+#define PHASE_MARK(k, t)                                                             \
+    do {                                                                             \
+        if (tid == 0) {                                                              \
+            const unsigned long long now_ = clock64();                               \
+            atomicAdd(&g_phaseClk[k], now_ - (t));                                   \
+            (t) = now_;                                                              \
+        }                                                                            \
+    } while (0)
+#else
+#define PHASE_MARK(k, t) (void)0
+#endif
 
-__device__ __forceinline__ Acc2 zero2()
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
 {
-    Acc2 r;
-    r.a = make_uint4(0, 0, 0, 0);
-    r.b = r.a;
-    return r;
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+__device__ __forceinline__ uint32_t ld4(uint64_t addr)
+{
+    return *reinterpret_cast<const uint32_t*>(addr);
+}
+
+__device__ __forceinline__ void st4(uint64_t addr, uint32_t v)
+{
+    *reinterpret_cast<uint32_t*>(addr) = v;
 }
 
 // A term's bytes in [len, align16(len)) are zero in memory (every writer
 // zero-fills the tail of its last 16-byte lane, ops.h), so only lanes wholly
-// past the term's end need clearing: one select per dword, no byte masks.
-__device__ __forceinline__ uint4 term_value(uint4 x, uint32_t p, uint32_t len, uint32_t coeff)
+// past the term's end need clearing.
+__device__ __forceinline__ uint32_t term_load(uint64_t src, uint32_t len, uint32_t p)
 {
-    if (p >= len)
-        x = make_uint4(0, 0, 0, 0);
-    if (coeff != 1)
-        x = gf_mul16(x, coeff);
-    return x;
+    return p < len ? ld4(src + p) : 0u;
+}
+
+__device__ __forceinline__ uint32_t term_mul(uint32_t x, uint32_t coeff)
+{
+    return coeff == 1 ? x : gf_mul_dword(x, coeff);
 }
 
 // Word `idx` of the current op's block: from the LDS ring while it lasts,
@@ -248,50 +301,35 @@ __device__ __forceinline__ uint4 op_word(const uint4* ring, const uint4* __restr
 
 // Accumulate terms [k0, k1).  fetch(k, src, len, ca) is called once per term
 // with increasing k and describes term k (ca = coeff | acc << 8); it returns
-// false for an absent term.  Fetches keep their descriptors in registers
-// (one term per lane, moved to scalars with readlane), so issuing a term
-// costs no memory round trip: the loads of up to kExecDepth terms (both
-// chunks) go out back to back before the first is used.  A chunk the term
-// does not reach is not loaded.
+// false for an absent term.  The loads of up to kExecDepth terms go out back
+// to back before the first is used; a term that ends before the tile is not
+// loaded.
 template <class Fetch>
-__device__ __forceinline__ void gather2(uint32_t k0, uint32_t k1, uint32_t tileBase, uint32_t p, Acc2& acc0,
-                                        Acc2& acc1, Fetch&& fetch)
+__device__ __forceinline__ void gather(uint32_t k0, uint32_t k1, uint32_t tileBase, uint32_t p,
+                                       uint32_t& acc0, uint32_t& acc1, Fetch&& fetch)
 {
-    const uint32_t p1 = p + kChunk;
     for (uint32_t k = k0; k < k1; k += kExecDepth) {
-        uint32_t len[kExecDepth], ca[kExecDepth];
+        uint32_t v[kExecDepth], ca[kExecDepth];
         bool act[kExecDepth];
-        uint4 v0[kExecDepth], v1[kExecDepth];
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
             const uint32_t idx = k + u;
             uint64_t src = 0;
-            act[u] = idx < k1 && fetch(idx, src, len[u], ca[u]) && tileBase < len[u];
-            if (act[u]) {
-                // lanes past the term's end load the term's first line (always
-                // mapped) and mask it away, so no load sits behind a lane branch
-                v0[u] = ld16(src + (p < len[u] ? p : 0));
-                if (tileBase + kChunk < len[u])
-                    v1[u] = ld16(src + (p1 < len[u] ? p1 : 0));
-            }
+            uint32_t len = 0;
+            act[u] = idx < k1 && fetch(idx, src, len, ca[u]) && tileBase < len;
+            v[u] = act[u] ? term_load(src, len, p) : 0u;
         }
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
             if (act[u]) {
-                const uint32_t c = ca[u] & 0xff;
-                const uint4 x0 = term_value(v0[u], p, len[u], c);
-                Acc2& acc = (ca[u] & 0xff00) ? acc1 : acc0;
-                acc.a = xor16(acc.a, x0);
-                if (tileBase + kChunk < len[u])
-                    acc.b = xor16(acc.b, term_value(v1[u], p1, len[u], c));
+                const uint32_t x = term_mul(v[u], ca[u] & 0xff);
+                if (ca[u] & 0xff00)
+                    acc1 ^= x;
+                else
+                    acc0 ^= x;
             }
         }
     }
-}
-
-__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
-{
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
 
 // term descriptor word held by lane j -> scalars
@@ -301,47 +339,70 @@ __device__ __forceinline__ void lane_term(uint4 w, uint32_t j, uint64_t& src, ui
     len = rl(w.z, j);
 }
 
-__device__ __forceinline__ void read_term(uint4 w, uint64_t& src, uint32_t& len)
+__device__ __forceinline__ uint32_t align16u(uint32_t v) { return (v + 15u) & ~15u; }
+
+// dst[p, p+4) of an item: keep(dst, valid) ^ out for bytes < n, zero for
+// bytes in [n, align16(n)) (the zero tail every term reader relies on),
+// nothing stored past that.  `cur` is dst[p, p+4) as loaded at item start.
+__device__ __forceinline__ void store_item(uint32_t out, uint32_t p, uint64_t dst, uint32_t n, uint32_t valid,
+                                           uint32_t cur)
 {
-    src = ((uint64_t)uni(w.y) << 32) | uni(w.x);
-    len = uni(w.z);
+    if (p >= align16u(n))
+        return;
+    if (p >= n) {
+        st4(dst + p, 0u);
+        return;
+    }
+    if (p < valid)
+        out ^= cur & byte_mask((int)valid - (int)p);
+    st4(dst + p, out & byte_mask((int)n - (int)p));
 }
 
-// dst[p, p+16) of an item: keep(dst, valid) ^ out for bytes < n, zero for
-// bytes in [n, p+16) (the zero tail every term reader relies on), nothing
-// stored for lanes at or past n.  `cur` is dst[p, p+16) as loaded at item
-// start when p < valid.
-__device__ __forceinline__ void store_item(uint4 out, uint32_t p, uint64_t dst, uint32_t n, uint32_t valid,
-                                           uint4 cur)
+// store_item for a 16-byte lane (the quad layout of planned rows: lane
+// holds bytes [p, p+16) of the tile)
+__device__ __forceinline__ void store_item16(uint4 out, uint32_t p, uint64_t dst, uint32_t n, uint32_t valid,
+                                             uint4 cur)
 {
-    if (p >= n)
+    if (p >= align16u(n))
         return;
-    if (p < valid) {
-        uint4 prior = cur;
-        if (p + 16 > valid)
-            prior = mask16(prior, (int)valid - (int)p);
-        out = xor16(out, prior);
-    }
-    if (p + 16 > n)
-        out = mask16(out, (int)n - (int)p);
-    st16(dst + p, out);
+    if (p < valid)
+        out = xor16(out, mask16(cur, (int)valid - (int)p));
+    *reinterpret_cast<uint4*>(dst + p) = mask16(out, (int)n - (int)p);
+}
+
+__device__ __forceinline__ uint4 load_cur16(uint32_t p, uint64_t dst, uint32_t n, uint32_t valid)
+{
+    return (p < n && p < valid) ? *reinterpret_cast<const uint4*>(dst + p) : make_uint4(0, 0, 0, 0);
+}
+
+// the four quads (16-lane groups) of a wave hold partial sums of one tile:
+// fold them so every quad holds the total
+__device__ __forceinline__ uint4 quad_fold(uint4 v)
+{
+    v.x ^= __shfl_xor(v.x, 16, 64);
+    v.y ^= __shfl_xor(v.y, 16, 64);
+    v.z ^= __shfl_xor(v.z, 16, 64);
+    v.w ^= __shfl_xor(v.w, 16, 64);
+    v.x ^= __shfl_xor(v.x, 32, 64);
+    v.y ^= __shfl_xor(v.y, 32, 64);
+    v.z ^= __shfl_xor(v.z, 32, 64);
+    v.w ^= __shfl_xor(v.w, 32, 64);
+    return v;
 }
 
 // what store_item needs of dst, loaded while the terms stream in
-__device__ __forceinline__ uint4 load_cur(uint32_t p, uint64_t dst, uint32_t n, uint32_t valid)
+__device__ __forceinline__ uint32_t load_cur(uint32_t p, uint64_t dst, uint32_t n, uint32_t valid)
 {
-    if (p < n && p < valid)
-        return ld16(dst + p);
-    return make_uint4(0, 0, 0, 0);
+    return (p < n && p < valid) ? ld4(dst + p) : 0u;
 }
 
 // `litLen` (<= 8) literal bytes at dst + n, written by the lanes owning them
 __device__ __forceinline__ void store_literal(uint32_t p, uint64_t dst, uint32_t n, uint32_t litLen,
                                               const uint32_t* lit)
 {
-    if (litLen && n + litLen > p && n < p + 16) {
+    if (litLen && n + litLen > p && n < p + 4) {
         uint8_t* d = reinterpret_cast<uint8_t*>(dst);
-        for (uint32_t k = (n > p ? n : p); k < n + litLen && k < p + 16; ++k)
+        for (uint32_t k = (n > p ? n : p); k < n + litLen && k < p + 4; ++k)
             d[k] = (uint8_t)(lit[(k - n) >> 2] >> (8 * ((k - n) & 3)));
     }
 }
@@ -353,32 +414,107 @@ __device__ __forceinline__ uint32_t pcg_output(uint64_t s)
     return (xs >> r) | (xs << ((32u - r) & 31u));
 }
 
-// Sum or window entry i of the current OP_ROWS batch (per lane)
+// PCG state after d more draws from state s (uniform): the draws compose as
+// powers of one affine map, applied per set bit of d.
+__device__ __forceinline__ uint64_t pcg_jump(uint64_t s, uint64_t inc, uint32_t d)
+{
+    for (uint32_t k = 0; d; ++k, d >>= 1)
+        if (d & 1u)
+            s = c_pcgJA[k] * s + inc * c_pcgJG[k];
+    return s;
+}
+
+// Sum or window descriptor i of the current OP_ROWS batch (per lane)
 __device__ __forceinline__ uint4 table_entry(const uint4* tableL, const uint4* __restrict__ seg,
                                              uint32_t blockWord, uint32_t i)
 {
     return i < kRowsTableLds ? tableL[i] : seg[blockWord + i];
 }
 
+// One Siamese row's LDPC picks [d0, d1) of PCG.Seed(row, N) (pair index
+// d / 2; even draws feed acc0, odd acc1), from the staged window where it
+// holds the element and from memory otherwise.  Returns the reference source
+// bytes of the picks (SiameseEncoder.cpp:1100-1144 adds min(len, rowBytes)).
+__device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t off, uint32_t d0,
+                                              uint32_t d1, uint32_t rn, uint32_t tileBase, uint32_t p,
+                                              uint32_t lane, uint64_t pcgA, uint64_t pcgG,
+                                              const uint32_t* stage, uint32_t staged,
+                                              const uint4* tableL, const uint4* __restrict__ seg,
+                                              uint32_t blk, uint32_t& acc0, uint32_t& acc1)
+// (window element e < staged lives in stage slot kRowSums + e)
+{
+    const uint64_t inc = ((uint64_t)row << 1) | 1u;
+    uint64_t sc = pcg_jump((inc + N) * kPcgMul + inc, inc, d0);   // state after Seed(), then d0 draws
+    uint32_t refBytes = 0;
+    for (uint32_t c = d0; c < d1; c += 64) {
+        // lane j: draw c + j -> window element e and its descriptor
+        const uint64_t st = pcgA * sc + inc * pcgG;
+        const uint32_t e = off + pcg_output(st) % N;
+        const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
+        sc = c_pcgA[64] * sc + inc * c_pcgG[64];
+        const uint32_t cnt = d1 - c < 64 ? d1 - c : 64;
+        for (uint32_t j0 = 0; j0 < cnt; j0 += kExecDepth) {
+            uint32_t v[kExecDepth];
+#pragma unroll
+            for (unsigned u = 0; u < kExecDepth; ++u) {
+                const uint32_t j = j0 + u;
+                v[u] = 0;
+                if (j < cnt) {
+                    const uint32_t ej = rl(e, j);
+                    uint64_t src;
+                    uint32_t len;
+                    lane_term(ev, j, src, len);
+                    refBytes += len < rn ? len : rn;
+                    if (ej < staged)
+                        v[u] = stage[(kRowSums + ej) * 64 + lane];
+                    else if (tileBase < len)
+                        v[u] = term_load(src, len, p);
+                }
+            }
+#pragma unroll
+            for (unsigned u = 0; u < kExecDepth; ++u) {
+                if (((c + j0 + u) & 1u) == 0)
+                    acc0 ^= v[u];
+                else
+                    acc1 ^= v[u];
+            }
+        }
+    }
+    return refBytes;
+}
+
 __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
                                                        const ExecItem* __restrict__ items,
-                                                       unsigned long long* __restrict__ acct)
+                                                       unsigned long long* __restrict__ acct,
+                                                       uint32_t stageSlots)
 {
     __shared__ uint4 ring[2][kRingWords];
-    __shared__ uint4 part[kExecWaves - 1][2][64];
+    __shared__ __attribute__((aligned(16))) uint32_t part[kExecWaves][2][64];
     __shared__ uint4 tableL[kRowsTableLds];
     __shared__ uint32_t cxL[kColumnValuePeriod];   // CX(c) | CX(c)^2 << 8 by c mod 253
+    __shared__ uint16_t plan[kPlanCap];            // rows' terms as stage slots
+    __shared__ uint2 rowInfo[kPlanRows];           // plan offset (or kNoPlan/kPlanGeneral), n0 | n1 << 16
+    // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
+    // window element e < stageCap (stageSlots x 64 dwords in all)
+    extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
+    const uint32_t stageCap = stageSlots > kRowSums ? stageSlots - kRowSums : 0;
     const ExecItem it = items[blockIdx.x];
     const uint4* seg = stream + it.streamBegin;
     const uint32_t words = it.streamWords;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
-    const uint32_t wave = tid >> 6;
+    const uint32_t wave = uni(tid >> 6);   // (uniform: keeps wave-derived loops scalar)
     const uint32_t tileBase = it.tileBase;
-    const uint32_t p = tileBase + lane * 16;
-    const uint32_t p1 = p + kChunk;
+    const uint32_t p = tileBase + lane * 4;
+    // PCG jump-ahead by this lane's index (A^lane, sum_{t<lane} A^t)
+    const uint64_t pcgA = c_pcgA[lane], pcgG = c_pcgG[lane];
+    const uint64_t pcgA64 = c_pcgA[64], pcgG64 = c_pcgG[64];
+#ifdef SGPU_PHASE_CLOCKS
+    unsigned long long kclk = clock64();
+#endif
 
-    ring[0][tid] = tid < words ? seg[tid] : make_uint4(0, 0, 0, 0);
+    if (tid < kRingWords)
+        ring[0][tid] = tid < words ? seg[tid] : make_uint4(0, 0, 0, 0);
     for (uint32_t c = tid; c < kColumnValuePeriod; c += kExecThreads) {
         const uint32_t cx = 3u + (c * 199u) % kColumnValuePeriod;   // SiameseCommon.h:89-93
         cxL[c] = cx | ((uint32_t)c_sqr[cx] << 8);
@@ -397,215 +533,501 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         const uint32_t next = pos + itemWords;
         // prefetch the next op's block while this one runs
         uint4 pf = make_uint4(0, 0, 0, 0);
-        if (oi + 1 < it.opCount && next + tid < words)
+        if (tid < kRingWords && oi + 1 < it.opCount && next + tid < words)
             pf = seg[next + tid];
 
         if (kind == OP_LITERAL) {
             if (wave == 0) {
                 const uint32_t lit[2] = {uni(h1.z), uni(h1.w)};
                 store_literal(p, dst, n, valid, lit);
-                store_literal(p1, dst, n, valid, lit);
             }
         } else if (kind == OP_LINCOMB) {
-            if (tileBase < n) {   // uniform: the op reaches this tile
+            if (tileBase < align16u(n)) {   // uniform: the op reaches this tile
                 const uint32_t nt = uni(h1.w);
                 const uint32_t mix = uni(h1.y);
                 const bool solo = nt <= kExecSolo;
-                uint4 cur0 = make_uint4(0, 0, 0, 0), cur1 = cur0;
-                if (wave == 0) {
-                    cur0 = load_cur(p, dst, n, valid);
-                    cur1 = load_cur(p1, dst, n, valid);
-                }
-                Acc2 acc0 = zero2(), acc1 = zero2();
+                const uint32_t c0 = wave == 0 ? load_cur(p, dst, n, valid) : 0u;
+                uint32_t acc0 = 0, acc1 = 0;
                 // wave w takes a contiguous share of the terms
                 const uint32_t a0 = solo ? 0 : nt * wave / kExecWaves;
                 const uint32_t a1 = solo ? (wave == 0 ? nt : 0) : nt * (wave + 1) / kExecWaves;
                 uint4 dv = make_uint4(0, 0, 0, 0);
-                gather2(a0, a1, tileBase, p, acc0, acc1,
-                        [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                            const uint32_t j = (k - a0) & 63u;
-                            if (j == 0) {
-                                const uint32_t idx = k + lane;
-                                dv = idx < a1 ? op_word(rb, seg, pos, kOpWords + idx) : make_uint4(0, 0, 0, 0);
-                            }
-                            lane_term(dv, j, src, len);
-                            ca = rl(dv.w, j);
-                            return true;
-                        });
-                if (mix > 1) {
-                    acc1.a = gf_mul16(acc1.a, mix);
-                    acc1.b = gf_mul16(acc1.b, mix);
-                }
-                uint4 out0 = xor16(acc0.a, acc1.a), out1 = xor16(acc0.b, acc1.b);
+                gather(a0, a1, tileBase, p, acc0, acc1,
+                       [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                           const uint32_t j = (k - a0) & 63u;
+                           if (j == 0) {
+                               const uint32_t idx = k + lane;
+                               dv = idx < a1 ? op_word(rb, seg, pos, kOpWords + idx) : make_uint4(0, 0, 0, 0);
+                           }
+                           lane_term(dv, j, src, len);
+                           ca = rl(dv.w, j);
+                           return true;
+                       });
+                uint32_t out = acc0 ^ (mix > 1 ? gf_mul_dword(acc1, mix) : acc1);
                 if (!solo) {
-                    if (wave != 0) {
-                        part[wave - 1][0][lane] = out0;
-                        part[wave - 1][1][lane] = out1;
-                    }
+                    if (wave != 0)
+                        part[wave][0][lane] = out;
                     __syncthreads();
                     if (wave == 0) {
 #pragma unroll
-                        for (unsigned w = 0; w + 1 < kExecWaves; ++w) {
-                            out0 = xor16(out0, part[w][0][lane]);
-                            out1 = xor16(out1, part[w][1][lane]);
-                        }
+                        for (unsigned w = 1; w < kExecWaves; ++w)
+                            out ^= part[w][0][lane];
                     }
                 }
-                if (wave == 0) {
-                    store_item(out0, p, dst, n, valid, cur0);
-                    store_item(out1, p1, dst, n, valid, cur1);
-                }
+                if (wave == 0)
+                    store_item(out, p, dst, n, valid, c0);
             }
         } else if (kind == OP_ROWS) {
+#ifdef SGPU_PHASE_CLOCKS
+            unsigned long long tclk = clock64();
+#endif
             const uint32_t R = n, E = valid, U = uni(h1.y);
             const uint32_t blk = pos + kOpWords;        // stream word of sum entry 0
             const uint32_t T = kRowSums + E;
-            for (uint32_t i = tid; i < T && i < kRowsTableLds; i += kExecThreads)
+            // the whole block (descriptors, updates, rows) to LDS: every
+            // later header read is an LDS read, not a memory round trip
+            const uint32_t blockWords = uni(h1.w);
+            for (uint32_t i = tid; i < blockWords && i < kRowsTableLds; i += kExecThreads)
                 tableL[i] = op_word(rb, seg, pos, kOpWords + i);
             __syncthreads();
+            PHASE_MARK(0, tclk);
 
-            // phase A: lane-sum updates, one wave each
-            const uint32_t updWord = kOpWords + T;
-            for (uint32_t u = wave; u < U; u += kExecWaves) {
-                const uint4 w0 = op_word(rb, seg, pos, updWord + u * kUpdateWords);
-                const uint4 w1 = op_word(rb, seg, pos, updWord + u * kUpdateWords + 1);
-                const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                const uint32_t un = uni(w0.z), vs = uni(w0.w);
-                const uint32_t uvalid = vs & 0x3fffffffu, us = vs >> 30;
-                const uint32_t from = uni(w1.x), to = uni(w1.y);
-                if (tileBase >= un)
-                    continue;
-                const uint4 c0 = load_cur(p, udst, un, uvalid);
-                const uint4 c1 = load_cur(p1, udst, un, uvalid);
-                Acc2 acc0 = zero2(), acc1 = zero2();
-                const uint32_t cnt = to > from ? (to - from + kLanes - 1) / kLanes : 0;
-                uint4 ev = make_uint4(0, 0, 0, 0);
-                uint32_t cv = 1;
-                uint32_t refBytes = 0;   // reference source bytes (one add/muladd per original)
-                gather2(0, cnt, tileBase, p, acc0, acc1,
-                        [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                            const uint32_t j = k & 63u;
-                            if (j == 0) {
-                                // lane j: element from + 8 (k + j) and its coefficient
-                                const uint32_t e = from + (k + lane) * kLanes;
-                                ev = e < to ? table_entry(tableL, seg, blk, kRowSums + e)
-                                            : make_uint4(0, 0, 0, 0);
-                                const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
-                                cv = us == 0 ? 1u : (us == 1 ? (cx & 0xff) : (cx >> 8));
-                            }
-                            lane_term(ev, j, src, len);
-                            ca = rl(cv, j);
-                            refBytes += len;
-                            return len != 0;
-                        });
-                store_item(acc0.a, p, udst, un, uvalid, c0);
-                store_item(acc0.b, p1, udst, un, uvalid, c1);
-                if (tileBase == 0 && lane == 0 && refBytes)
-                    atomicAdd(acct, (unsigned long long)refBytes);
+            // stage this tile of window elements [0, staged) into slots 24.. :
+            // thread t loads 16 bytes of element t/16 per pass, four passes in
+            // flight at once; bytes past an element's length (absent
+            // elements: all of them) read zero
+            const uint32_t staged = E < stageCap ? E : stageCap;
+            constexpr unsigned kPass = kExecThreads / 16;   // elements per pass
+            const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
+            for (uint32_t e0 = tid / 16; e0 < staged; e0 += 4 * kPass) {
+                uint4 v[4];
+#pragma unroll
+                for (unsigned u = 0; u < 4; ++u) {
+                    const uint32_t e = e0 + u * kPass;
+                    v[u] = make_uint4(0, 0, 0, 0);
+                    if (e < staged) {
+                        const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
+                        const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+                        if (tileBase + q16 < d.z)
+                            v[u] = *reinterpret_cast<const uint4*>(src + tileBase + q16);
+                    }
+                }
+#pragma unroll
+                for (unsigned u = 0; u < 4; ++u) {
+                    const uint32_t e = e0 + u * kPass;
+                    if (e < staged)
+                        *reinterpret_cast<uint4*>(&stage[(kRowSums + e) * 64 + q16 / 4]) = v[u];
+                }
             }
             __syncthreads();
+            PHASE_MARK(1, tclk);
 
-            // phase B: rows, one wave each; lane j < 24 holds sum entry j
-            const uint4 sumv = lane < kRowSums ? tableL[lane] : make_uint4(0, 0, 0, 0);
+            // phase A: lane-sum updates (SiameseEncoder.cpp:359-418,
+            // SiameseDecoder.cpp:1680-1739): element e = from, from+8, ... < to,
+            // coefficient 1, CX or CX^2 of its column.  With fewer updates
+            // than waves each update's elements are split across Q = W / U
+            // waves whose partial sums meet in LDS.  Lane j holds element j's
+            // descriptor (reference source bytes counted per lane) and its
+            // coefficient's multiply table, moved to scalars with readlane;
+            // the element reads of 16 elements go out back to back.
+            const uint32_t updWord = kOpWords + T;
+            const uint32_t Q = (U == 0 || U >= kExecWaves) ? 1u : kExecWaves / U;
+            const uint32_t uUnits = Q == 1 ? U : U * Q;
+            for (uint32_t unit = wave; unit < uUnits; unit += kExecWaves) {
+                const uint32_t u = Q == 1 ? unit : unit / Q;
+                const uint32_t uq = Q == 1 ? 0 : unit % Q;
+                const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
+                const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords);
+                const uint32_t un = uni(w0.z), vs = uni(w0.w);
+                const uint32_t us = vs >> 30;
+                const uint32_t from = uni(w1.x), to = uni(w1.y);
+                uint32_t acc = 0;
+                if (tileBase < align16u(un)) {
+                    const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
+                    const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
+                    uint32_t refBytes = 0;   // this lane's elements (one add/muladd per original)
+                    for (uint32_t c = k0; c < k1; c += 64) {
+                        const uint32_t e = from + (c + lane) * kLanes;
+                        const uint4 ev = c + lane < k1 ? table_entry(tableL, seg, blk, kRowSums + e)
+                                                       : make_uint4(0, 0, 0, 0);
+                        const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
+                        const GfTab tab = gf_tab(us == 1 ? (cx & 0xff) : (cx >> 8));
+                        refBytes += ev.z;
+                        const uint32_t cnt = k1 - c < 64 ? k1 - c : 64;
+                        for (uint32_t j0 = 0; j0 < cnt; j0 += 16) {
+                            uint32_t v[16];
+#pragma unroll
+                            for (unsigned k = 0; k < 16; ++k) {
+                                const uint32_t j = j0 + k;
+                                const uint32_t ej = from + (c + j) * kLanes;
+                                v[k] = 0;
+                                if (j < cnt) {
+                                    if (ej < staged) {
+                                        v[k] = stage[(kRowSums + ej) * 64 + lane];
+                                    } else {
+                                        uint64_t src;
+                                        uint32_t len;
+                                        lane_term(ev, j, src, len);
+                                        if (tileBase < len)
+                                            v[k] = term_load(src, len, p);
+                                    }
+                                }
+                            }
+#pragma unroll
+                            for (unsigned k = 0; k < 16; ++k) {
+                                const uint32_t j = j0 + k;
+                                if (j < cnt) {
+                                    if (us == 0) {
+                                        acc ^= v[k];
+                                    } else {
+                                        const GfTab t{rl(tab.a0, j), rl(tab.a1, j), rl(tab.b0, j),
+                                                      rl(tab.b1, j), rl(tab.c, j)};
+                                        acc ^= gf_mul_tab(v[k], t);
+                                    }
+                                }
+                            }
+                        }
+                    }
+                    if (tileBase == 0 && refBytes)
+                        atomicAdd(acct, (unsigned long long)refBytes);
+                }
+                if (Q > 1) {
+                    part[wave][0][lane] = acc;
+                } else if (tileBase < align16u(un)) {
+                    const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                    const uint32_t uvalid = vs & 0x3fffffffu;
+                    store_item(acc, p, udst, un, uvalid, load_cur(p, udst, un, uvalid));
+                }
+            }
+            if (Q > 1) {
+                __syncthreads();
+                if (wave < uUnits && wave % Q == 0) {
+                    const uint32_t u = wave / Q;
+                    const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
+                    const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                    const uint32_t un = uni(w0.z), uvalid = uni(w0.w) & 0x3fffffffu;
+                    if (tileBase < align16u(un)) {
+                        const uint32_t cu = load_cur(p, udst, un, uvalid);
+                        uint32_t acc = 0;
+                        for (uint32_t k = 0; k < Q; ++k)
+                            acc ^= part[wave + k][0][lane];
+                        store_item(acc, p, udst, un, uvalid, cu);
+                    }
+                }
+            }
+            __syncthreads();
+            PHASE_MARK(2, tclk);
+
+            // stage the 24 lane sums as the rows read them (after the updates
+            // above: this workgroup's own stores, visible after the barrier)
+            const bool sumsStaged = stageSlots >= kRowSums;
+            if (sumsStaged && tid < kRowSums * 16) {
+                const uint32_t k = tid / 16;
+                const uint4 d = tableL[k];
+                const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (tileBase + q16 < d.z)
+                    v = *reinterpret_cast<const uint4*>(src + tileBase + q16);
+                *reinterpret_cast<uint4*>(&stage[k * 64 + q16 / 4]) = v;
+            }
+
+            // phase B0: each row's terms as stage slots (the plan).  Row
+            // sizes: its selected sums plus one slot per LDPC draw; offsets by
+            // a prefix sum over rows (wave 0).  The draws are made here, lane
+            // parallel (and their reference source bytes counted); a row with
+            // a draw outside the staged window keeps reading memory.
             const uint32_t rowWord = updWord + U * kUpdateWords;
-            for (uint32_t r = wave; r < R; r += kExecWaves) {
-                const uint4 w0 = op_word(rb, seg, pos, rowWord + r * kRowWords);
-                const uint4 w1 = op_word(rb, seg, pos, rowWord + r * kRowWords + 1);
-                const uint4 w2 = op_word(rb, seg, pos, rowWord + r * kRowWords + 2);
+            const uint32_t planned = R < kPlanRows ? R : kPlanRows;
+            PHASE_MARK(3, tclk);
+            if (wave == 0) {
+                uint32_t carry = 0;
+                for (uint32_t r0 = 0; r0 < planned; r0 += 64) {
+                    const uint32_t r = r0 + lane;
+                    uint32_t size = 0;
+                    uint4 w1 = make_uint4(0, 0, 0, 0);
+                    if (r < planned) {
+                        w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
+                        const uint32_t pairs = (w1.w + kPairRate - 1) / kPairRate;
+                        size = __builtin_popcount(w1.x & 0xffffffu) + __builtin_popcount(w1.y & 0xffffffu) +
+                               2 * pairs;
+                    }
+                    uint32_t incl = size;
+#pragma unroll
+                    for (unsigned d = 1; d < 64; d <<= 1) {
+                        const uint32_t t = __shfl_up(incl, d, 64);
+                        if (lane >= d)
+                            incl += t;
+                    }
+                    const uint32_t offs = carry + incl - size;
+                    if (r < planned) {
+                        const uint32_t pairs = (w1.w + kPairRate - 1) / kPairRate;
+                        const uint32_t n0 = __builtin_popcount(w1.x & 0xffffffu) + pairs;
+                        const uint32_t n1 = __builtin_popcount(w1.y & 0xffffffu) + pairs;
+                        rowInfo[r] = make_uint2(sumsStaged && offs + size <= kPlanCap ? offs : kNoPlan,
+                                                n0 | (n1 << 16));
+                    }
+                    carry += __shfl(incl, 63, 64);
+                }
+            }
+            __syncthreads();
+            for (uint32_t r = wave; r < planned; r += kExecWaves) {
+                const uint2 info = rowInfo[r];
+                const uint32_t off0 = uni(info.x);
+                if (off0 == kNoPlan)
+                    continue;
+                const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
+                const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
+                const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords);
+                const uint32_t rn = uni(w0.z);
+                const uint32_t m0 = uni(w1.x) & 0xffffffu, m1 = uni(w1.y) & 0xffffffu;
+                const uint32_t row = uni(w1.z), N = uni(w1.w), woff = uni(w2.x);
+                const uint32_t n0 = uni(info.y) & 0xffffu;
+                const uint32_t pc0 = __builtin_popcount(m0), pc1 = __builtin_popcount(m1);
+                const uint32_t off1 = off0 + n0;
+                // sums: lane k < 24 places slot k if its bit is set
+                if (lane < kRowSums) {
+                    const uint32_t below = (1u << lane) - 1u;
+                    if (m0 >> lane & 1u)
+                        plan[off0 + __builtin_popcount(m0 & below)] = (uint16_t)lane;
+                    if (m1 >> lane & 1u)
+                        plan[off1 + __builtin_popcount(m1 & below)] = (uint16_t)lane;
+                }
+                // draws: even -> row list, odd -> product list
+                bool general = false;
+                uint32_t refBytes = 0;
+                if (N != 0) {
+                    const uint32_t D = 2 * ((N + kPairRate - 1) / kPairRate);
+                    const uint64_t inc = ((uint64_t)row << 1) | 1u;
+                    uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
+                    // x % N through a double reciprocal: the quotient estimate
+                    // is within one for 32-bit x, then corrected exactly
+                    const double invN = 1.0 / (double)N;
+                    for (uint32_t c = 0; c < D; c += 64) {
+                        const uint32_t d = c + lane;
+                        const uint64_t st = pcgA * sc + inc * pcgG;
+                        sc = pcgA64 * sc + inc * pcgG64;
+                        if (d < D) {
+                            const uint32_t x = pcg_output(st);
+                            const uint32_t qn = (uint32_t)((double)x * invN);
+                            int64_t rr = (int64_t)x - (int64_t)qn * N;
+                            rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
+                            const uint32_t e = woff + (uint32_t)rr;
+                            const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e).z;
+                            refBytes += len < rn ? len : rn;
+                            general |= e >= staged;
+                            const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
+                            plan[at] = (uint16_t)(e < staged ? kRowSums + e : 0);
+                        }
+                    }
+                }
+                if (tileBase == 0 && refBytes)
+                    atomicAdd(acct, (unsigned long long)refBytes);
+                const bool anyGeneral = __any(general ? 1 : 0);
+                if (anyGeneral && lane == 0)
+                    rowInfo[r].x = kPlanGeneral;
+            }
+            __syncthreads();
+            PHASE_MARK(4, tclk);
+
+            // phase B1: rows.  R >= W: wave w takes rows w, w+W, ...; R < W:
+            // row r's terms are split into P = W / R parts, unit w = (w / P,
+            // w % P), and the parts meet in LDS.  A planned row XORs stage
+            // slots; the others read sums and undrawn-from-LDS picks from
+            // memory.  lane j < 24 holds sum entry j.
+            const uint4 sumv = lane < kRowSums ? tableL[lane] : make_uint4(0, 0, 0, 0);
+            const uint32_t P = R >= kExecWaves ? 1u : kExecWaves / R;
+            const uint32_t units = P == 1 ? R : R * P;
+            for (uint32_t unit = wave; unit < units; unit += kExecWaves) {
+                const uint32_t r = P == 1 ? unit : unit / P;
+                const uint32_t q = P == 1 ? 0 : unit % P;
+                const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
+                const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
+                const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords);
                 const uint64_t rdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
                 const uint32_t rn = uni(w0.z), rvalid = uni(w0.w);
                 const uint32_t m0 = uni(w1.x), m1 = uni(w1.y), row = uni(w1.z), N = uni(w1.w);
                 const uint32_t off = uni(w2.x);
-                const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
-                const uint32_t litLen = m0 >> 24, mix = m1 >> 24;
-                if (tileBase < rn) {
-                    const uint4 c0 = load_cur(p, rdst, rn, rvalid);
-                    const uint4 c1 = load_cur(p1, rdst, rn, rvalid);
-                    Acc2 acc0 = zero2(), acc1 = zero2();
-                    // dense part: the sums the opcodes select (bit lane*3+s;
-                    // mask1 feeds the product)
-                    uint64_t bits = (uint64_t)(m0 & 0xffffffu) | ((uint64_t)(m1 & 0xffffffu) << 24);
-                    gather2(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
-                            [&](uint32_t, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                                const uint32_t b = (uint32_t)__builtin_ctzll(bits);
-                                bits &= bits - 1;
-                                const uint32_t k = b < kRowSums ? b : b - kRowSums;
-                                lane_term(sumv, k, src, len);
-                                ca = 1u | ((b >= kRowSums ? 1u : 0u) << 8);
-                                return len != 0;
-                            });
-                    // sparse part: ceil(N/16) pairs of PCG.Seed(row, N) draws
-                    // (SiameseEncoder.cpp:1100-1144): lane j makes draw 64c+j by
-                    // jump-ahead and fetches its window entry
-                    uint32_t refBytes = 0;   // reference source bytes of the pairs
-                    if (N != 0) {
-                        const uint64_t inc = ((uint64_t)row << 1) | 1u;
-                        uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
-                        uint4 ev = make_uint4(0, 0, 0, 0);
-                        gather2(0, 2 * ((N + kPairRate - 1) / kPairRate), tileBase, p, acc0, acc1,
-                                [&](uint32_t k, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                                    const uint32_t j = k & 63u;
-                                    if (j == 0) {
-                                        const uint64_t st = c_pcgA[lane] * sc + inc * c_pcgG[lane];
-                                        const uint32_t e = pcg_output(st) % N;
-                                        ev = table_entry(tableL, seg, blk, kRowSums + off + e);
-                                        sc = c_pcgA[64] * sc + inc * c_pcgG[64];
-                                    }
-                                    lane_term(ev, j, src, len);
-                                    ca = 1u | ((k & 1u) << 8);
-                                    refBytes += len < rn ? len : rn;
-                                    return len != 0;
-                                });
+                const uint32_t mix = m1 >> 24;
+                const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
+                const uint32_t pinfo = uni(info.x);
+#ifdef SGPU_PHASE_CLOCKS
+                unsigned long long rclk = clock64();
+#endif
+                // dst as kept (decoder rows) and the product's multiply table,
+                // fetched before the terms stream in
+                const bool plannedRow = pinfo < kPlanGeneral;
+                const uint32_t p16 = tileBase + (lane & 15u) * 16u;
+                const uint32_t c0 = (P == 1 && !plannedRow && tileBase < align16u(rn)) ? load_cur(p, rdst, rn, rvalid) : 0u;
+                const uint4 c0q = (P == 1 && plannedRow && tileBase < align16u(rn) && lane < 16)
+                                      ? load_cur16(p16, rdst, rn, rvalid) : make_uint4(0, 0, 0, 0);
+                const GfTab mixTab = gf_tab(mix);
+                uint32_t acc0 = 0, acc1 = 0;
+                uint4 acc0q = make_uint4(0, 0, 0, 0), acc1q = acc0q;   // planned rows (quad layout)
+                bool quadRow = false;
+                if (tileBase < align16u(rn)) {
+                    if (pinfo < kPlanGeneral) {
+                        // planned: XOR of stage slots, the part's share of each
+                        // list, in the quad layout: quad g of the wave takes
+                        // terms g, g+4, ... and lane l holds bytes 16*(l%16)..
+                        // of the tile, so one 16-byte LDS read per lane moves
+                        // four terms; the quads are folded at the end.
+                        const uint32_t n0 = uni(info.y) & 0xffffu, n1 = uni(info.y) >> 16;
+                        const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
+                        for (unsigned h = 0; h < 2; ++h) {
+                            const uint32_t nl = h ? n1 : n0;
+                            const uint32_t base = pinfo + (h ? n0 : 0);
+                            const uint32_t i0 = base + nl * q / P, i1 = base + nl * (q + 1) / P;
+                            uint4 a = make_uint4(0, 0, 0, 0);
+                            for (uint32_t t = i0; t < i1; t += 16) {
+                                uint4 v[4];
+#pragma unroll
+                                for (unsigned k = 0; k < 4; ++k) {
+                                    const uint32_t ti = t + 4 * k + g;
+                                    v[k] = make_uint4(0, 0, 0, 0);
+                                    if (ti < i1)
+                                        v[k] = *reinterpret_cast<const uint4*>(&stage[(uint32_t)plan[ti] * 64 + b4]);
+                                }
+#pragma unroll
+                                for (unsigned k = 0; k < 4; ++k)
+                                    a = xor16(a, v[k]);
+                            }
+                            a = quad_fold(a);
+                            if (h)
+                                acc1q = a;
+                            else
+                                acc0q = a;
+                        }
+                        quadRow = true;
+                    } else {
+                        // dense part (part 0): the sums the opcodes select (bit
+                        // lane*3+s; mask1 feeds the product)
+                        if (q == 0) {
+                            uint64_t bits = (uint64_t)(m0 & 0xffffffu) | ((uint64_t)(m1 & 0xffffffu) << 24);
+                            gather(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
+                                   [&](uint32_t, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                                       const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+                                       bits &= bits - 1;
+                                       const uint32_t k = b < kRowSums ? b : b - kRowSums;
+                                       lane_term(sumv, k, src, len);
+                                       ca = 1u | ((b >= kRowSums ? 1u : 0u) << 8);
+                                       return len != 0;
+                                   });
+                        }
+                        // sparse part: this unit's share of the 2*ceil(N/16) draws
+                        // (pairs stay whole: even draw -> row, odd -> product)
+                        if (N != 0) {
+                            const uint32_t pairs = (N + kPairRate - 1) / kPairRate;
+                            const uint32_t d0 = 2 * (pairs * q / P), d1 = 2 * (pairs * (q + 1) / P);
+                            const uint32_t refBytes = row_picks(row, N, off, d0, d1, rn, tileBase, p, lane, pcgA,
+                                                                pcgG, stage, staged, tableL, seg, blk, acc0, acc1);
+                            // (a planned row's draws were counted by its plan)
+                            if (pinfo == kNoPlan && tileBase == 0 && lane == 0 && refBytes)
+                                atomicAdd(acct, (unsigned long long)refBytes);
+                        }
                     }
-                    if (tileBase == 0 && lane == 0 && refBytes)
-                        atomicAdd(acct, (unsigned long long)refBytes);
-                    if (mix > 1) {
-                        acc1.a = gf_mul16(acc1.a, mix);
-                        acc1.b = gf_mul16(acc1.b, mix);
-                    }
-                    store_item(xor16(acc0.a, acc1.a), p, rdst, rn, rvalid, c0);
-                    store_item(xor16(acc0.b, acc1.b), p1, rdst, rn, rvalid, c1);
                 }
-                store_literal(p, rdst, rn, litLen, lit);
-                store_literal(p1, rdst, rn, litLen, lit);
+                if (P > 1) {
+                    // partials in the dword layout (lane l: bytes 4l..); a
+                    // quad-layout row's quad 0 writes the same bytes as 16-byte words
+                    if (quadRow) {
+                        if (lane < 16) {
+                            *reinterpret_cast<uint4*>(&part[wave][0][lane * 4]) = acc0q;
+                            *reinterpret_cast<uint4*>(&part[wave][1][lane * 4]) = acc1q;
+                        }
+                    } else {
+                        part[wave][0][lane] = acc0;
+                        part[wave][1][lane] = acc1;
+                    }
+                } else if (quadRow) {
+                    if (tileBase < align16u(rn) && lane < 16)
+                        store_item16(xor16(acc0q, mix > 1 ? gf_mul16(acc1q, mix) : acc1q), p16, rdst, rn,
+                                     rvalid, c0q);
+                    PHASE_MARK(14, rclk);
+                    const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
+                    store_literal(p, rdst, rn, m0 >> 24, lit);
+                    PHASE_MARK(15, rclk);
+                } else {
+                    if (tileBase < align16u(rn))
+                        store_item(acc0 ^ (mix > 1 ? gf_mul_tab(acc1, mixTab) : acc1), p, rdst, rn, rvalid, c0);
+                    PHASE_MARK(14, rclk);
+                    const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
+                    store_literal(p, rdst, rn, m0 >> 24, lit);
+                    PHASE_MARK(15, rclk);
+                }
+            }
+            if (P > 1) {
+                __syncthreads();
+                if (wave < units && wave % P == 0) {
+                    const uint32_t r = wave / P;
+                    const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
+                    const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
+                    const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords);
+                    const uint64_t rdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                    const uint32_t rn = uni(w0.z), rvalid = uni(w0.w);
+                    const uint32_t m0 = uni(w1.x), mix = uni(w1.y) >> 24;
+                    uint32_t acc0 = 0, acc1 = 0;
+                    for (uint32_t k = 0; k < P; ++k) {
+                        acc0 ^= part[wave + k][0][lane];
+                        acc1 ^= part[wave + k][1][lane];
+                    }
+                    if (tileBase < align16u(rn)) {
+                        const uint32_t c0 = load_cur(p, rdst, rn, rvalid);
+                        store_item(acc0 ^ (mix > 1 ? gf_mul_dword(acc1, mix) : acc1), p, rdst, rn, rvalid, c0);
+                    }
+                    const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
+                    store_literal(p, rdst, rn, m0 >> 24, lit);
+                }
+            }
+            PHASE_MARK(5, tclk);
+            if (tid == 0) {
+#ifdef SGPU_PHASE_CLOCKS
+                atomicAdd(&g_phaseClk[8], 1ull);
+                atomicAdd(&g_phaseClk[9], (unsigned long long)R);
+                atomicAdd(&g_phaseClk[10], (unsigned long long)U);
+                atomicAdd(&g_phaseClk[11], (unsigned long long)E);
+                atomicAdd(&g_phaseClk[12], (unsigned long long)staged);
+#endif
             }
         } else if (kind == OP_COPIES) {
             // kCopyBatch copies per wave at a time, all their loads in flight
             // before the first store; sources carry their zero tails
             constexpr unsigned kCopyBatch = 4;
-            for (uint32_t c0 = wave * kCopyBatch; c0 < n; c0 += kExecWaves * kCopyBatch) {
+            for (uint32_t k0 = wave * kCopyBatch; k0 < n; k0 += kExecWaves * kCopyBatch) {
                 uint64_t d[kCopyBatch];
-                uint32_t l[kCopyBatch];
-                uint4 v0[kCopyBatch], v1[kCopyBatch];
+                uint32_t l[kCopyBatch], v[kCopyBatch];
 #pragma unroll
                 for (unsigned u = 0; u < kCopyBatch; ++u) {
                     l[u] = 0;
-                    if (c0 + u < n) {
-                        const uint4 w0 = op_word(rb, seg, pos, kOpWords + (c0 + u) * kCopyWords);
-                        const uint4 w1 = op_word(rb, seg, pos, kOpWords + (c0 + u) * kCopyWords + 1);
+                    v[u] = 0;
+                    if (k0 + u < n) {
+                        const uint4 w0 = op_word(rb, seg, pos, kOpWords + (k0 + u) * kCopyWords);
+                        const uint4 w1 = op_word(rb, seg, pos, kOpWords + (k0 + u) * kCopyWords + 1);
                         d[u] = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
                         const uint64_t s = ((uint64_t)uni(w0.w) << 32) | uni(w0.z);
                         l[u] = uni(w1.x);
-                        if (tileBase < l[u]) {
-                            v0[u] = ld16(s + (p < l[u] ? p : 0));
-                            if (tileBase + kChunk < l[u])
-                                v1[u] = ld16(s + (p1 < l[u] ? p1 : 0));
-                        }
+                        v[u] = term_load(s, l[u], p);
                     }
                 }
 #pragma unroll
                 for (unsigned u = 0; u < kCopyBatch; ++u) {
                     if (p < l[u])
-                        st16(d[u] + p, p + 16 > l[u] ? mask16(v0[u], (int)l[u] - (int)p) : v0[u]);
-                    if (p1 < l[u])
-                        st16(d[u] + p1, p1 + 16 > l[u] ? mask16(v1[u], (int)l[u] - (int)p1) : v1[u]);
+                        st4(d[u] + p, v[u] & byte_mask((int)l[u] - (int)p));
+                    else if (p < align16u(l[u]))
+                        st4(d[u] + p, 0u);
                 }
             }
         }
-        ring[cur ^ 1][tid] = pf;
+        if (tid < kRingWords)
+            ring[cur ^ 1][tid] = pf;
         __syncthreads();
         cur ^= 1;
         pos = next;
+    }
+    PHASE_MARK(6, kclk);
+    if (tid == 0) {
+#ifdef SGPU_PHASE_CLOCKS
+        atomicAdd(&g_phaseClk[7], 1ull);
+#endif
     }
 }
 
@@ -990,6 +1412,10 @@ bool g_timing = false;
 // largest m staged in LDS: 56 keeps solve_lds_bytes under the default 64 KiB
 // dynamic-LDS limit; raised at init when the device grants more
 uint32_t g_solveLdsRows = 56;
+// window elements an OP_ROWS batch stages in LDS per tile (256 B each, beside
+// the 24 sums); sized at init to the LDS the kernel's static arrays leave
+// free; SGPU_STAGE overrides (0 = read every element from memory)
+uint32_t g_stageCap = 0;
 double g_execMs = 0, g_totalMs = 0;
 
 struct EvPair
@@ -1160,6 +1586,32 @@ bool be_init(int device, const char** err)
         pg[j] = pg[j - 1] * kPcgMul + 1;
     }
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgA), pa, sizeof(pa)), "hipMemcpyToSymbol(pcgA)");
+    // jumps of 2^k draws: A^(2^k) and sum_{t<2^k} A^t
+    uint64_t ja[32], jg[32];
+    ja[0] = kPcgMul;
+    jg[0] = 1;
+    for (unsigned k = 1; k < 32; ++k) {
+        jg[k] = jg[k - 1] * ja[k - 1] + jg[k - 1];
+        ja[k] = ja[k - 1] * ja[k - 1];
+    }
+    check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgJA), ja, sizeof(ja)), "hipMemcpyToSymbol(pcgJA)");
+    check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgJG), jg, sizeof(jg)), "hipMemcpyToSymbol(pcgJG)");
+    {
+        hipFuncAttributes fa;
+        size_t staticLds = 64u * 1024u;
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_exec)) == hipSuccess)
+            staticLds = fa.sharedSizeBytes;
+        const size_t ldsPerCu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor
+                                                                : 160u * 1024u;
+        const size_t dyn = ldsPerCu > staticLds ? ldsPerCu - staticLds : 0;
+        g_stageCap = dyn / kExecTileBytes > kRowSums ? (uint32_t)(dyn / kExecTileBytes) - kRowSums : 0;
+        if (const char* sc = std::getenv("SGPU_STAGE"))
+            g_stageCap = std::min<uint32_t>(g_stageCap, (uint32_t)std::atoi(sc));
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exec),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)((kRowSums + g_stageCap) * kExecTileBytes)) != hipSuccess)
+            g_stageCap = 48u * 1024u / kExecTileBytes - kRowSums;
+    }
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgG), pg, sizeof(pg)), "hipMemcpyToSymbol(pcgG)");
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_main),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1174,6 +1626,15 @@ bool be_init(int device, const char** err)
 }
 
 const char* be_name() { return "hip-gfx950"; }
+
+#ifdef SGPU_PHASE_CLOCKS
+extern "C" __attribute__((visibility("default"))) void sgpu_debug_phase_clocks(unsigned long long* out16)
+{
+    bind_device();
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phaseClk), 16 * sizeof(unsigned long long));
+}
+#endif
 
 void* be_dev_alloc(size_t bytes)
 {
@@ -1234,14 +1695,20 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count)
                        dim3(64 * kIngestWaves), 0, g_stream, descs, count);
 }
 
-void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct)
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct,
+                    uint32_t maxWindow)
 {
     if (count == 0)
         return;
     Timed t(true);
-    hipLaunchKernelGGL(k_exec, dim3(count), dim3(kExecThreads), 0, g_stream,
-                       static_cast<const uint4*>(stream), items,
-                       reinterpret_cast<unsigned long long*>(acct));
+    // LDS stage: the 24 sums plus the largest OP_ROWS window of the launch,
+    // up to the device's budget (none for launches without row batches)
+    uint32_t slots = 0;
+    if (maxWindow != kNoRows)
+        slots = kRowSums + (maxWindow < g_stageCap ? maxWindow : g_stageCap);
+    hipLaunchKernelGGL(k_exec, dim3(count), dim3(kExecThreads), (size_t)slots * kExecTileBytes,
+                       g_stream, static_cast<const uint4*>(stream), items,
+                       reinterpret_cast<unsigned long long*>(acct), slots);
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,

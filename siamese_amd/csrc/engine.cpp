@@ -765,7 +765,7 @@ struct Phase
     enum Kind { EXEC, SOLVE } kind;
     size_t itemBegin, itemCount;    // exec items or solve items
     size_t solveBegin, solveCount;  // solve descs (SOLVE)
-    uint32_t maxRows;               // largest m among them (SOLVE)
+    uint32_t maxRows;               // largest m among them (SOLVE); largest OP_ROWS window (EXEC)
 };
 
 struct SegRef
@@ -1015,7 +1015,7 @@ void Engine::assemble_batch(Batch& bt)
         for (ProgramBody* p : bt.bodies[g])
             maxSegs = std::max(maxSegs, p->nsegs);
         for (size_t k = 0; k < maxSegs; ++k) {
-            Phase ex{Phase::EXEC, nItems, 0, 0, 0, 0};
+            Phase ex{Phase::EXEC, nItems, 0, 0, 0, kNoRows};
             const size_t segBegin = segs.size();
             for (ProgramBody* p : bt.bodies[g]) {
                 if (k >= p->nsegs)
@@ -1023,6 +1023,9 @@ void Engine::assemble_batch(Batch& bt)
                 const ProgramBody::Segment& s = p->segs[k];
                 if (s.ops.empty())
                     continue;
+                for (const GfOp& op : s.ops)
+                    if (op.kind == OP_ROWS)
+                        ex.maxRows = ex.maxRows == kNoRows ? op.valid : std::max(ex.maxRows, op.valid);
                 const size_t words = kOpWords * s.ops.size() + s.terms.size() + s.rowsWords;
                 segs.push_back(SegRef{&s, (uint32_t)nWords, (uint32_t)words, (uint32_t)nItems});
                 nOps += s.ops.size();
@@ -1218,7 +1221,7 @@ void Engine::launch_batch(Batch& bt)
     for (const Phase& ph : bt.phases) {
         if (ph.kind == Phase::EXEC) {
             be_launch_exec(xs.upDev + bt.oStream, (const ExecItem*)(xs.upDev + bt.oItems) + ph.itemBegin,
-                           (uint32_t)ph.itemCount, acctDev);
+                           (uint32_t)ph.itemCount, acctDev, ph.maxRows);
             st.execLaunches++;
         } else {
             const SolveDesc* sd = (const SolveDesc*)(xs.upDev + bt.oSD) + ph.solveBegin;

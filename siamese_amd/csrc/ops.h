@@ -213,6 +213,7 @@ struct IngestDesc
 };
 
 constexpr unsigned kTileBytes = 1024;       // solve tiles: 64 lanes x 16 bytes
-constexpr unsigned kExecTileBytes = 2048;   // executor tiles: 64 lanes x 2 x 16 bytes
+constexpr uint32_t kNoRows = 0xffffffffu;   // be_launch_exec: no OP_ROWS in the launch
+constexpr unsigned kExecTileBytes = 256;    // executor tiles: 64 lanes x 4 bytes
 
 } // namespace sgpu

@@ -311,7 +311,7 @@ static bool noexec()
     return v == 1;
 }
 
-void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct)
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct, uint32_t)
 {
     if (noexec())
         return;

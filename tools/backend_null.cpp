@@ -70,7 +70,7 @@ void be_d2h(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, by
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
 void be_launch_ingest(const IngestDesc*, uint32_t) {}
-void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*) {}
+void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*, uint32_t) {}
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow*, const uint8_t*,
                             uint32_t* results, uint32_t count, uint64_t*)
