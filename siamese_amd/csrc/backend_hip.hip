@@ -34,6 +34,12 @@ namespace sgpu {
 // ---------------------------------------------------------------------------
 // Device tables
 
+// device (global) address space: plain global_load/store rather than flat
+// ones, which would also count against lgkmcnt and make every LDS wait wait
+// for outstanding memory loads
+#define GMEM __attribute__((address_space(1)))
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __constant__ uint32_t c_perm[256][8];   // per constant y: {Ta0,Ta1,Tb0,Tb1,Tc,0,0,0}
 __constant__ uint8_t c_inv[256];
 
@@ -60,6 +66,13 @@ __device__ __forceinline__ GfTab gf_tab(uint32_t y)
     return GfTab{t[0], t[1], t[2], t[3], t[4]};
 }
 
+// from the workgroup's LDS copy of c_perm (a0 a1 b0 b1 | c)
+__device__ __forceinline__ GfTab gf_tab_l(const uint4* permL, const uint32_t* permC, uint32_t y)
+{
+    const uint4 t = permL[y];
+    return GfTab{t.x, t.y, t.z, t.w, permC[y]};
+}
+
 __device__ __forceinline__ uint32_t gf_mul_tab(uint32_t x, const GfTab& t)
 {
     const uint32_t a = x & 0x07070707u;
@@ -77,6 +90,11 @@ __device__ __forceinline__ uint4 gf_mul16(uint4 v, uint32_t y)
     r.z = gf_mul_dword(v.z, y);
     r.w = gf_mul_dword(v.w, y);
     return r;
+}
+
+__device__ __forceinline__ uint4 gf_mul16_tab(uint4 v, const GfTab& t)
+{
+    return make_uint4(gf_mul_tab(v.x, t), gf_mul_tab(v.y, t), gf_mul_tab(v.z, t), gf_mul_tab(v.w, t));
 }
 
 __device__ __forceinline__ uint32_t byte_mask(int n)
@@ -101,12 +119,13 @@ __device__ __forceinline__ uint4 xor16(uint4 a, uint4 b)
 
 __device__ __forceinline__ uint4 ld16(uint64_t addr)
 {
-    return *reinterpret_cast<const uint4*>(addr);
+    const u32x4 r = *reinterpret_cast<const GMEM u32x4*>(addr);
+    return make_uint4(r.x, r.y, r.z, r.w);
 }
 
 __device__ __forceinline__ void st16(uint64_t addr, uint4 v)
 {
-    *reinterpret_cast<uint4*>(addr) = v;
+    *reinterpret_cast<GMEM u32x4*>(addr) = u32x4{v.x, v.y, v.z, v.w};
 }
 
 // ---------------------------------------------------------------------------
@@ -224,6 +243,12 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
 // The barrier that rotates the ring also orders each op's stores before any
 // later op of the segment reads them (stores from one CU are visible to the
 // CU's other waves after the workgroup-scope fence of __syncthreads).
+#ifndef SGPU_PLAN_OVERLAP
+#define SGPU_PLAN_OVERLAP 0
+#endif
+#ifndef SGPU_UPD_SPLIT
+#define SGPU_UPD_SPLIT 0
+#endif
 #ifndef SGPU_EXEC_WAVES
 #define SGPU_EXEC_WAVES 16
 #endif
@@ -247,10 +272,21 @@ __constant__ uint8_t c_sqr[256];
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// add a per-lane count to the workgroup's LDS counter: one atomic per wave
+// (a global atomic per lane serialises at one L2 address across the grid)
+__device__ __forceinline__ void acct_wave(unsigned long long* acctL, uint32_t v)
+{
+#pragma unroll
+    for (unsigned d = 32; d >= 1; d >>= 1)
+        v += __shfl_xor(v, d, 64);
+    if ((threadIdx.x & 63) == 0 && v)
+        atomicAdd(acctL, (unsigned long long)v);
+}
+
 #ifdef SGPU_PHASE_CLOCKS
 // profiling build only: shader clocks per OP_ROWS phase, summed over
 // workgroups as seen by thread 0 (tools/phase_clocks.py reads them)
-__device__ unsigned long long g_phaseClk[16];
+__device__ unsigned long long g_phaseClk[32];
 #define PHASE_MARK(k, t)                                                             \
     do {                                                                             \
         if (tid == 0) {                                                              \
@@ -259,8 +295,16 @@ __device__ unsigned long long g_phaseClk[16];
             (t) = now_;                                                              \
         }                                                                            \
     } while (0)
+#define PHASE_ADD(k, v)                                                              \
+    do {                                                                             \
+        if ((threadIdx.x & 63) == 0)                                                 \
+            atomicAdd(&g_phaseClk[k], (unsigned long long)(v));                      \
+    } while (0)
+#define PHASE_CLK() clock64()
 #else
 #define PHASE_MARK(k, t) (void)0
+#define PHASE_ADD(k, v) (void)0
+#define PHASE_CLK() 0ull
 #endif
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
@@ -270,12 +314,12 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
 
 __device__ __forceinline__ uint32_t ld4(uint64_t addr)
 {
-    return *reinterpret_cast<const uint32_t*>(addr);
+    return *reinterpret_cast<const GMEM uint32_t*>(addr);
 }
 
 __device__ __forceinline__ void st4(uint64_t addr, uint32_t v)
 {
-    *reinterpret_cast<uint32_t*>(addr) = v;
+    *reinterpret_cast<GMEM uint32_t*>(addr) = v;
 }
 
 // A term's bytes in [len, align16(len)) are zero in memory (every writer
@@ -296,7 +340,7 @@ __device__ __forceinline__ uint32_t term_mul(uint32_t x, uint32_t coeff)
 __device__ __forceinline__ uint4 op_word(const uint4* ring, const uint4* __restrict__ seg, uint32_t pos,
                                          uint32_t idx)
 {
-    return idx < kRingWords ? ring[idx] : seg[pos + idx];
+    return idx < kRingWords ? ring[idx] : ld16((uint64_t)(seg + pos + idx));
 }
 
 // Accumulate terms [k0, k1).  fetch(k, src, len, ca) is called once per term
@@ -367,12 +411,12 @@ __device__ __forceinline__ void store_item16(uint4 out, uint32_t p, uint64_t dst
         return;
     if (p < valid)
         out = xor16(out, mask16(cur, (int)valid - (int)p));
-    *reinterpret_cast<uint4*>(dst + p) = mask16(out, (int)n - (int)p);
+    st16(dst + p, mask16(out, (int)n - (int)p));
 }
 
 __device__ __forceinline__ uint4 load_cur16(uint32_t p, uint64_t dst, uint32_t n, uint32_t valid)
 {
-    return (p < n && p < valid) ? *reinterpret_cast<const uint4*>(dst + p) : make_uint4(0, 0, 0, 0);
+    return (p < n && p < valid) ? ld16(dst + p) : make_uint4(0, 0, 0, 0);
 }
 
 // the four quads (16-lane groups) of a wave hold partial sums of one tile:
@@ -401,7 +445,7 @@ __device__ __forceinline__ void store_literal(uint32_t p, uint64_t dst, uint32_t
                                               const uint32_t* lit)
 {
     if (litLen && n + litLen > p && n < p + 4) {
-        uint8_t* d = reinterpret_cast<uint8_t*>(dst);
+        GMEM uint8_t* d = reinterpret_cast<GMEM uint8_t*>(dst);
         for (uint32_t k = (n > p ? n : p); k < n + litLen && k < p + 4; ++k)
             d[k] = (uint8_t)(lit[(k - n) >> 2] >> (8 * ((k - n) & 3)));
     }
@@ -428,7 +472,7 @@ __device__ __forceinline__ uint64_t pcg_jump(uint64_t s, uint64_t inc, uint32_t 
 __device__ __forceinline__ uint4 table_entry(const uint4* tableL, const uint4* __restrict__ seg,
                                              uint32_t blockWord, uint32_t i)
 {
-    return i < kRowsTableLds ? tableL[i] : seg[blockWord + i];
+    return i < kRowsTableLds ? tableL[i] : ld16((uint64_t)(seg + blockWord + i));
 }
 
 // One Siamese row's LDPC picks [d0, d1) of PCG.Seed(row, N) (pair index
@@ -494,6 +538,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint32_t cxL[kColumnValuePeriod];   // CX(c) | CX(c)^2 << 8 by c mod 253
     __shared__ uint16_t plan[kPlanCap];            // rows' terms as stage slots
     __shared__ uint2 rowInfo[kPlanRows];           // plan offset (or kNoPlan/kPlanGeneral), n0 | n1 << 16
+    __shared__ unsigned long long acctL;          // reference source bytes counted by this workgroup
+    __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
+    __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
     // window element e < stageCap (stageSlots x 64 dwords in all)
     extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
@@ -514,10 +561,16 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
 #endif
 
     if (tid < kRingWords)
-        ring[0][tid] = tid < words ? seg[tid] : make_uint4(0, 0, 0, 0);
+        ring[0][tid] = tid < words ? ld16((uint64_t)(seg + tid)) : make_uint4(0, 0, 0, 0);
     for (uint32_t c = tid; c < kColumnValuePeriod; c += kExecThreads) {
         const uint32_t cx = 3u + (c * 199u) % kColumnValuePeriod;   // SiameseCommon.h:89-93
         cxL[c] = cx | ((uint32_t)c_sqr[cx] << 8);
+    }
+    if (tid == 0)
+        acctL = 0;
+    if (tid < 256) {
+        permL[tid] = make_uint4(c_perm[tid][0], c_perm[tid][1], c_perm[tid][2], c_perm[tid][3]);
+        permC[tid] = c_perm[tid][4];
     }
     __syncthreads();
     uint32_t cur = 0, pos = 0;
@@ -534,7 +587,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         // prefetch the next op's block while this one runs
         uint4 pf = make_uint4(0, 0, 0, 0);
         if (tid < kRingWords && oi + 1 < it.opCount && next + tid < words)
-            pf = seg[next + tid];
+            pf = ld16((uint64_t)(seg + next + tid));
 
         if (kind == OP_LITERAL) {
             if (wave == 0) {
@@ -592,14 +645,112 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             __syncthreads();
             PHASE_MARK(0, tclk);
 
-            // stage this tile of window elements [0, staged) into slots 24.. :
-            // thread t loads 16 bytes of element t/16 per pass, four passes in
-            // flight at once; bytes past an element's length (absent
-            // elements: all of them) read zero
+            // every wave: issue its loads of this tile of window elements
+            // [0, staged) (thread t: 16 bytes of element t/16 per pass, four
+            // passes in flight; bytes past an element's length -- absent
+            // elements: all of them -- read zero), build its rows' term plans
+            // (phase B0, from the descriptors alone) while they fly, then
+            // write them to stage slots 24..
             const uint32_t staged = E < stageCap ? E : stageCap;
-            constexpr unsigned kPass = kExecThreads / 16;   // elements per pass
             const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
-            for (uint32_t e0 = tid / 16; e0 < staged; e0 += 4 * kPass) {
+            const bool sumsStaged = stageSlots >= kRowSums;
+            const uint32_t updWord = kOpWords + T;
+            const uint32_t rowWord = updWord + U * kUpdateWords;
+            const uint32_t planned = R < kPlanRows ? R : kPlanRows;
+            constexpr unsigned kPass = kExecThreads / 16;   // elements per pass
+            uint32_t* updAcc = &part[0][0][0];              // U <= 24 update accumulators of 64 dwords
+            static_assert(kExecWaves * 2 >= kRowSums, "update accumulators fit part[]");
+            for (uint32_t i = tid; i < U * 64; i += kExecThreads)
+                updAcc[i] = 0;
+            auto build_plan = [&]() {
+                // plan: row sizes are its selected sums plus one slot per
+                // LDPC draw, offsets a prefix sum over rows (each wave scans
+                // them all and keeps the rows it owns, r = wave mod W); the
+                // draws are made lane parallel (and their reference source
+                // bytes counted); a row with a draw outside the staged
+                // window keeps reading memory
+                uint32_t carry = 0;
+                for (uint32_t r0 = 0; r0 < planned; r0 += 64) {
+                    const uint32_t r = r0 + lane;
+                    uint32_t size = 0, n01 = 0;
+                    if (r < planned) {
+                        const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
+                        const uint32_t pairs = (w1.w + kPairRate - 1) / kPairRate;
+                        const uint32_t n0 = __builtin_popcount(w1.x & 0xffffffu) + pairs;
+                        const uint32_t n1 = __builtin_popcount(w1.y & 0xffffffu) + pairs;
+                        size = n0 + n1;
+                        n01 = n0 | (n1 << 16);
+                    }
+                    uint32_t incl = size;
+    #pragma unroll
+                    for (unsigned d = 1; d < 64; d <<= 1) {
+                        const uint32_t t = __shfl_up(incl, d, 64);
+                        if (lane >= d)
+                            incl += t;
+                    }
+                    const uint32_t offs = carry + incl - size;
+                    if (r < planned && r % kExecWaves == wave)
+                        rowInfo[r] = make_uint2(sumsStaged && offs + size <= kPlanCap ? offs : kNoPlan, n01);
+                    carry += __shfl(incl, 63, 64);
+                }
+                for (uint32_t r = wave; r < planned; r += kExecWaves) {
+                    const uint2 info = rowInfo[r];   // (this wave's own write)
+                    const uint32_t off0 = uni(info.x);
+                    if (off0 == kNoPlan)
+                        continue;
+                    const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
+                    const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
+                    const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords);
+                    const uint32_t rn = uni(w0.z);
+                    const uint32_t m0 = uni(w1.x) & 0xffffffu, m1 = uni(w1.y) & 0xffffffu;
+                    const uint32_t row = uni(w1.z), N = uni(w1.w), woff = uni(w2.x);
+                    const uint32_t n0 = uni(info.y) & 0xffffu;
+                    const uint32_t pc0 = __builtin_popcount(m0), pc1 = __builtin_popcount(m1);
+                    const uint32_t off1 = off0 + n0;
+                    // sums: lane k < 24 places slot k if its bit is set
+                    if (lane < kRowSums) {
+                        const uint32_t below = (1u << lane) - 1u;
+                        if (m0 >> lane & 1u)
+                            plan[off0 + __builtin_popcount(m0 & below)] = (uint16_t)lane;
+                        if (m1 >> lane & 1u)
+                            plan[off1 + __builtin_popcount(m1 & below)] = (uint16_t)lane;
+                    }
+                    // draws: even -> row list, odd -> product list
+                    bool general = false;
+                    uint32_t refBytes = 0;
+                    if (N != 0) {
+                        const uint32_t D = 2 * ((N + kPairRate - 1) / kPairRate);
+                        const uint64_t inc = ((uint64_t)row << 1) | 1u;
+                        uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
+                        // x % N through a double reciprocal: the quotient estimate
+                        // is within one for 32-bit x, then corrected exactly
+                        const double invN = 1.0 / (double)N;
+                        for (uint32_t c = 0; c < D; c += 64) {
+                            const uint32_t d = c + lane;
+                            const uint64_t st = pcgA * sc + inc * pcgG;
+                            sc = pcgA64 * sc + inc * pcgG64;
+                            if (d < D) {
+                                const uint32_t x = pcg_output(st);
+                                const uint32_t qn = (uint32_t)((double)x * invN);
+                                int64_t rr = (int64_t)x - (int64_t)qn * N;
+                                rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
+                                const uint32_t e = woff + (uint32_t)rr;
+                                const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e).z;
+                                refBytes += len < rn ? len : rn;
+                                general |= e >= staged;
+                                const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
+                                plan[at] = (uint16_t)(e < staged ? kRowSums + e : 0);
+                            }
+                        }
+                    }
+                    if (tileBase == 0)
+                        acct_wave(&acctL, refBytes);
+                    const bool anyGeneral = __any(general ? 1 : 0);
+                    if (anyGeneral && lane == 0)
+                        rowInfo[r].x = kPlanGeneral;
+                }
+            };
+            for (uint32_t e0 = tid / 16, first = 1; first || e0 < staged; e0 += 4 * kPass) {
                 uint4 v[4];
 #pragma unroll
                 for (unsigned u = 0; u < 4; ++u) {
@@ -609,8 +760,13 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
                         const uint64_t src = ((uint64_t)d.y << 32) | d.x;
                         if (tileBase + q16 < d.z)
-                            v[u] = *reinterpret_cast<const uint4*>(src + tileBase + q16);
+                            v[u] = ld16(src + tileBase + q16);
                     }
+                }
+                if (first) {
+                    first = 0;
+                    if (SGPU_PLAN_OVERLAP)
+                        build_plan();
                 }
 #pragma unroll
                 for (unsigned u = 0; u < 4; ++u) {
@@ -619,39 +775,54 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         *reinterpret_cast<uint4*>(&stage[(kRowSums + e) * 64 + q16 / 4]) = v[u];
                 }
             }
+            if (!SGPU_PLAN_OVERLAP)
+                build_plan();
             __syncthreads();
             PHASE_MARK(1, tclk);
 
             // phase A: lane-sum updates (SiameseEncoder.cpp:359-418,
             // SiameseDecoder.cpp:1680-1739): element e = from, from+8, ... < to,
-            // coefficient 1, CX or CX^2 of its column.  With fewer updates
-            // than waves each update's elements are split across Q = W / U
-            // waves whose partial sums meet in LDS.  Lane j holds element j's
-            // descriptor (reference source bytes counted per lane) and its
-            // coefficient's multiply table, moved to scalars with readlane;
-            // the element reads of 16 elements go out back to back.
-            const uint32_t updWord = kOpWords + T;
-            const uint32_t Q = (U == 0 || U >= kExecWaves) ? 1u : kExecWaves / U;
-            const uint32_t uUnits = Q == 1 ? U : U * Q;
+            // coefficient 1, CX or CX^2 of its column.  Each update's elements
+            // are split into Q parts (U*Q ~ 3 units per wave) whose partial
+            // sums meet in LDS accumulators (XOR atomics); wave u then stores
+            // update u.  Lane j holds element j's descriptor (reference source
+            // bytes counted per lane) and its coefficient's multiply table,
+            // moved to scalars with readlane; the element reads of 16 elements
+            // go out back to back.
+            const uint32_t Q = U == 0 ? 1u
+                               : SGPU_UPD_SPLIT ? (SGPU_UPD_SPLIT * kExecWaves + U - 1) / U
+                                                : (U >= kExecWaves ? 1u : kExecWaves / U);
+            const uint32_t uUnits = U * Q;
+            // the update this wave stores: its dst as kept, fetched now
+            uint64_t sdst = 0;
+            uint32_t sn = 0, svalid = 0, scur = 0;
+            if (wave < U) {
+                const uint4 w0 = table_entry(tableL, seg, blk, updWord + wave * kUpdateWords - kOpWords);
+                sdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                sn = uni(w0.z);
+                svalid = uni(w0.w) & 0x3fffffffu;
+                if (tileBase < align16u(sn))
+                    scur = load_cur(p, sdst, sn, svalid);
+            }
             for (uint32_t unit = wave; unit < uUnits; unit += kExecWaves) {
-                const uint32_t u = Q == 1 ? unit : unit / Q;
-                const uint32_t uq = Q == 1 ? 0 : unit % Q;
+                [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
+                const uint32_t u = unit / Q;
+                const uint32_t uq = unit % Q;
                 const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
                 const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords);
-                const uint32_t un = uni(w0.z), vs = uni(w0.w);
-                const uint32_t us = vs >> 30;
+                const uint32_t un = uni(w0.z), us = uni(w0.w) >> 30;
                 const uint32_t from = uni(w1.x), to = uni(w1.y);
-                uint32_t acc = 0;
-                if (tileBase < align16u(un)) {
-                    const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
-                    const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
+                const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
+                const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
+                if (tileBase < align16u(un) && k0 < k1) {
+                    uint32_t acc = 0;
                     uint32_t refBytes = 0;   // this lane's elements (one add/muladd per original)
                     for (uint32_t c = k0; c < k1; c += 64) {
                         const uint32_t e = from + (c + lane) * kLanes;
                         const uint4 ev = c + lane < k1 ? table_entry(tableL, seg, blk, kRowSums + e)
                                                        : make_uint4(0, 0, 0, 0);
                         const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
-                        const GfTab tab = gf_tab(us == 1 ? (cx & 0xff) : (cx >> 8));
+                        const GfTab tab = gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8));
                         refBytes += ev.z;
                         const uint32_t cnt = k1 - c < 64 ? k1 - c : 64;
                         for (uint32_t j0 = 0; j0 < cnt; j0 += 16) {
@@ -688,144 +859,38 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             }
                         }
                     }
-                    if (tileBase == 0 && refBytes)
-                        atomicAdd(acct, (unsigned long long)refBytes);
+                    if (tileBase == 0)
+                        acct_wave(&acctL, refBytes);
+                    atomicXor(&updAcc[u * 64 + lane], acc);
                 }
-                if (Q > 1) {
-                    part[wave][0][lane] = acc;
-                } else if (tileBase < align16u(un)) {
-                    const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                    const uint32_t uvalid = vs & 0x3fffffffu;
-                    store_item(acc, p, udst, un, uvalid, load_cur(p, udst, un, uvalid));
-                }
+                if (wave == 0)
+                    PHASE_ADD(19, PHASE_CLK() - uclk0);
             }
-            if (Q > 1) {
-                __syncthreads();
-                if (wave < uUnits && wave % Q == 0) {
-                    const uint32_t u = wave / Q;
-                    const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
-                    const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                    const uint32_t un = uni(w0.z), uvalid = uni(w0.w) & 0x3fffffffu;
-                    if (tileBase < align16u(un)) {
-                        const uint32_t cu = load_cur(p, udst, un, uvalid);
-                        uint32_t acc = 0;
-                        for (uint32_t k = 0; k < Q; ++k)
-                            acc ^= part[wave + k][0][lane];
-                        store_item(acc, p, udst, un, uvalid, cu);
-                    }
-                }
+            __syncthreads();
+            if (wave < U && tileBase < align16u(sn))
+                store_item(updAcc[wave * 64 + lane], p, sdst, sn, svalid, scur);
+            for (uint32_t u = wave + kExecWaves; u < U; u += kExecWaves) {
+                const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
+                const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                const uint32_t un = uni(w0.z), uvalid = uni(w0.w) & 0x3fffffffu;
+                if (tileBase < align16u(un))
+                    store_item(updAcc[u * 64 + lane], p, udst, un, uvalid, load_cur(p, udst, un, uvalid));
             }
             __syncthreads();
             PHASE_MARK(2, tclk);
 
             // stage the 24 lane sums as the rows read them (after the updates
             // above: this workgroup's own stores, visible after the barrier)
-            const bool sumsStaged = stageSlots >= kRowSums;
             if (sumsStaged && tid < kRowSums * 16) {
                 const uint32_t k = tid / 16;
                 const uint4 d = tableL[k];
                 const uint64_t src = ((uint64_t)d.y << 32) | d.x;
                 uint4 v = make_uint4(0, 0, 0, 0);
                 if (tileBase + q16 < d.z)
-                    v = *reinterpret_cast<const uint4*>(src + tileBase + q16);
+                    v = ld16(src + tileBase + q16);
                 *reinterpret_cast<uint4*>(&stage[k * 64 + q16 / 4]) = v;
             }
-
-            // phase B0: each row's terms as stage slots (the plan).  Row
-            // sizes: its selected sums plus one slot per LDPC draw; offsets by
-            // a prefix sum over rows (wave 0).  The draws are made here, lane
-            // parallel (and their reference source bytes counted); a row with
-            // a draw outside the staged window keeps reading memory.
-            const uint32_t rowWord = updWord + U * kUpdateWords;
-            const uint32_t planned = R < kPlanRows ? R : kPlanRows;
             PHASE_MARK(3, tclk);
-            if (wave == 0) {
-                uint32_t carry = 0;
-                for (uint32_t r0 = 0; r0 < planned; r0 += 64) {
-                    const uint32_t r = r0 + lane;
-                    uint32_t size = 0;
-                    uint4 w1 = make_uint4(0, 0, 0, 0);
-                    if (r < planned) {
-                        w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
-                        const uint32_t pairs = (w1.w + kPairRate - 1) / kPairRate;
-                        size = __builtin_popcount(w1.x & 0xffffffu) + __builtin_popcount(w1.y & 0xffffffu) +
-                               2 * pairs;
-                    }
-                    uint32_t incl = size;
-#pragma unroll
-                    for (unsigned d = 1; d < 64; d <<= 1) {
-                        const uint32_t t = __shfl_up(incl, d, 64);
-                        if (lane >= d)
-                            incl += t;
-                    }
-                    const uint32_t offs = carry + incl - size;
-                    if (r < planned) {
-                        const uint32_t pairs = (w1.w + kPairRate - 1) / kPairRate;
-                        const uint32_t n0 = __builtin_popcount(w1.x & 0xffffffu) + pairs;
-                        const uint32_t n1 = __builtin_popcount(w1.y & 0xffffffu) + pairs;
-                        rowInfo[r] = make_uint2(sumsStaged && offs + size <= kPlanCap ? offs : kNoPlan,
-                                                n0 | (n1 << 16));
-                    }
-                    carry += __shfl(incl, 63, 64);
-                }
-            }
-            __syncthreads();
-            for (uint32_t r = wave; r < planned; r += kExecWaves) {
-                const uint2 info = rowInfo[r];
-                const uint32_t off0 = uni(info.x);
-                if (off0 == kNoPlan)
-                    continue;
-                const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
-                const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
-                const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords);
-                const uint32_t rn = uni(w0.z);
-                const uint32_t m0 = uni(w1.x) & 0xffffffu, m1 = uni(w1.y) & 0xffffffu;
-                const uint32_t row = uni(w1.z), N = uni(w1.w), woff = uni(w2.x);
-                const uint32_t n0 = uni(info.y) & 0xffffu;
-                const uint32_t pc0 = __builtin_popcount(m0), pc1 = __builtin_popcount(m1);
-                const uint32_t off1 = off0 + n0;
-                // sums: lane k < 24 places slot k if its bit is set
-                if (lane < kRowSums) {
-                    const uint32_t below = (1u << lane) - 1u;
-                    if (m0 >> lane & 1u)
-                        plan[off0 + __builtin_popcount(m0 & below)] = (uint16_t)lane;
-                    if (m1 >> lane & 1u)
-                        plan[off1 + __builtin_popcount(m1 & below)] = (uint16_t)lane;
-                }
-                // draws: even -> row list, odd -> product list
-                bool general = false;
-                uint32_t refBytes = 0;
-                if (N != 0) {
-                    const uint32_t D = 2 * ((N + kPairRate - 1) / kPairRate);
-                    const uint64_t inc = ((uint64_t)row << 1) | 1u;
-                    uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
-                    // x % N through a double reciprocal: the quotient estimate
-                    // is within one for 32-bit x, then corrected exactly
-                    const double invN = 1.0 / (double)N;
-                    for (uint32_t c = 0; c < D; c += 64) {
-                        const uint32_t d = c + lane;
-                        const uint64_t st = pcgA * sc + inc * pcgG;
-                        sc = pcgA64 * sc + inc * pcgG64;
-                        if (d < D) {
-                            const uint32_t x = pcg_output(st);
-                            const uint32_t qn = (uint32_t)((double)x * invN);
-                            int64_t rr = (int64_t)x - (int64_t)qn * N;
-                            rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
-                            const uint32_t e = woff + (uint32_t)rr;
-                            const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e).z;
-                            refBytes += len < rn ? len : rn;
-                            general |= e >= staged;
-                            const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
-                            plan[at] = (uint16_t)(e < staged ? kRowSums + e : 0);
-                        }
-                    }
-                }
-                if (tileBase == 0 && refBytes)
-                    atomicAdd(acct, (unsigned long long)refBytes);
-                const bool anyGeneral = __any(general ? 1 : 0);
-                if (anyGeneral && lane == 0)
-                    rowInfo[r].x = kPlanGeneral;
-            }
             __syncthreads();
             PHASE_MARK(4, tclk);
 
@@ -860,7 +925,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 const uint32_t c0 = (P == 1 && !plannedRow && tileBase < align16u(rn)) ? load_cur(p, rdst, rn, rvalid) : 0u;
                 const uint4 c0q = (P == 1 && plannedRow && tileBase < align16u(rn) && lane < 16)
                                       ? load_cur16(p16, rdst, rn, rvalid) : make_uint4(0, 0, 0, 0);
-                const GfTab mixTab = gf_tab(mix);
+                const GfTab mixTab = gf_tab_l(permL, permC, mix);
                 uint32_t acc0 = 0, acc1 = 0;
                 uint4 acc0q = make_uint4(0, 0, 0, 0), acc1q = acc0q;   // planned rows (quad layout)
                 bool quadRow = false;
@@ -922,7 +987,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                                                 pcgG, stage, staged, tableL, seg, blk, acc0, acc1);
                             // (a planned row's draws were counted by its plan)
                             if (pinfo == kNoPlan && tileBase == 0 && lane == 0 && refBytes)
-                                atomicAdd(acct, (unsigned long long)refBytes);
+                                atomicAdd(&acctL, (unsigned long long)refBytes);
                         }
                     }
                 }
@@ -940,7 +1005,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     }
                 } else if (quadRow) {
                     if (tileBase < align16u(rn) && lane < 16)
-                        store_item16(xor16(acc0q, mix > 1 ? gf_mul16(acc1q, mix) : acc1q), p16, rdst, rn,
+                        store_item16(xor16(acc0q, mix > 1 ? gf_mul16_tab(acc1q, mixTab) : acc1q), p16, rdst, rn,
                                      rvalid, c0q);
                     PHASE_MARK(14, rclk);
                     const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
@@ -1023,6 +1088,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         cur ^= 1;
         pos = next;
     }
+    // (the last op's barrier ordered every wave's count)
+    if (tid == 0 && acctL)
+        atomicAdd(acct, acctL);
     PHASE_MARK(6, kclk);
     if (tid == 0) {
 #ifdef SGPU_PHASE_CLOCKS
@@ -1037,7 +1105,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
 __device__ __forceinline__ uint32_t ld4_masked(uint64_t addr, uint32_t bytes)
 {
     // first four bytes of a row, bytes at/after `bytes` read as zero
-    const uint32_t v = *reinterpret_cast<const uint32_t*>(addr);
+    const uint32_t v = *reinterpret_cast<const GMEM uint32_t*>(addr);
     return v & byte_mask((int)bytes);
 }
 
@@ -1145,9 +1213,15 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
     }
     if (lane == 0)
         out[0] = ok;
-    if (opAcc)
+    // one atomic per wave (per-lane global atomics serialise at one address)
+#pragma unroll
+    for (unsigned d = 32; d >= 1; d >>= 1) {
+        opAcc += __shfl_xor(opAcc, d, 64);
+        outAcc += __shfl_xor(outAcc, d, 64);
+    }
+    if (lane == 0 && opAcc)
         atomicAdd(&acct[0], opAcc);
-    if (outAcc)
+    if (lane == 0 && outAcc)
         atomicAdd(&acct[1], outAcc);
 }
 
@@ -1628,11 +1702,11 @@ bool be_init(int device, const char** err)
 const char* be_name() { return "hip-gfx950"; }
 
 #ifdef SGPU_PHASE_CLOCKS
-extern "C" __attribute__((visibility("default"))) void sgpu_debug_phase_clocks(unsigned long long* out16)
+extern "C" __attribute__((visibility("default"))) void sgpu_debug_phase_clocks(unsigned long long* out32)
 {
     bind_device();
     (void)hipDeviceSynchronize();
-    (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phaseClk), 16 * sizeof(unsigned long long));
+    (void)hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_phaseClk), 32 * sizeof(unsigned long long));
 }
 #endif
 

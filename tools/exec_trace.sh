@@ -6,7 +6,7 @@ TAG=$1; shift
 D=$GRAFT_REPO_ROOT/gpurun_out/et_$TAG
 mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-env "$@" timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-legs > $D/bench.log 2>&1
+env "$@" timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-legs ${LIB:+--library $LIB} > $D/bench.log 2>&1
 python3 - $D <<'PY'
 import csv, sys, glob, statistics
 d = sys.argv[1]

@@ -14,14 +14,16 @@ import bench  # noqa: E402
 lib = sys.argv[1]
 bench.main(["--library", lib, "--steps", "3", "--warmup", "1", "--no-cpu", "--no-e2e", "--no-legs"])
 L = ctypes.CDLL(os.path.abspath(lib))
-out = (ctypes.c_ulonglong * 16)()
+out = (ctypes.c_ulonglong * 32)()
 L.sgpu_debug_phase_clocks(out)
 ops = max(1, out[8])
-names = ["block load", "stage window", "sum updates", "stage sums", "plan", "rows"]
+names = ["block load", "stage+plan", "sum updates", "stage sums", "sums barrier", "rows"]
 print("OP_ROWS workgroup-ops %d, rows %.1f, updates %.1f, window %.1f, staged %.1f per op"
       % (out[8], out[9] / ops, out[10] / ops, out[11] / ops, out[12] / ops))
 for k, nm in enumerate(names):
     print("  %-14s %10.0f clocks per op" % (nm, out[k] / ops))
 print("  rows detail (wave 0): planned XOR %.0f, mix+store %.0f, literal %.0f clocks per op"
       % (out[13] / ops, out[14] / ops, out[15] / ops))
+print("  detail (wave 0): update unit %.0f, plan scan %.0f, plan draws %.0f clocks per op"
+      % (out[19] / ops, out[20] / ops, out[21] / ops))
 print("kernel: %d workgroups, %.0f clocks each" % (out[7], out[6] / max(1, out[7])))
