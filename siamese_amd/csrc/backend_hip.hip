@@ -272,6 +272,14 @@ __constant__ uint8_t c_sqr[256];
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// v, as a value the compiler cannot prove loop invariant (so loads indexed by
+// it are not hoisted out of the loop and kept live in registers)
+__device__ __forceinline__ uint32_t opaque(uint32_t v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 // add a per-lane count to the workgroup's LDS counter: one atomic per wave
 // (a global atomic per lane serialises at one L2 address across the grid)
 __device__ __forceinline__ void acct_wave(unsigned long long* acctL, uint32_t v)
@@ -419,6 +427,25 @@ __device__ __forceinline__ uint4 load_cur16(uint32_t p, uint64_t dst, uint32_t n
     return (p < n && p < valid) ? ld16(dst + p) : make_uint4(0, 0, 0, 0);
 }
 
+__device__ __forceinline__ uint4 lds16(const uint32_t* base, uint32_t word)
+{
+    return *reinterpret_cast<const uint4*>(base + word);
+}
+
+__device__ __forceinline__ uint4 and16(uint4 v, uint32_t m)
+{
+    return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+
+// lane K of each 16-lane row (quad) to the whole row: DPP row_newbcast, a
+// VALU move (no LDS round trip)
+template <unsigned K>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v)
+{
+    static_assert(K < 16, "row lane");
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + K, 0xf, 0xf, false);
+}
+
 // the four quads (16-lane groups) of a wave hold partial sums of one tile:
 // fold them so every quad holds the total
 __device__ __forceinline__ uint4 quad_fold(uint4 v)
@@ -441,13 +468,14 @@ __device__ __forceinline__ uint32_t load_cur(uint32_t p, uint64_t dst, uint32_t 
 }
 
 // `litLen` (<= 8) literal bytes at dst + n, written by the lanes owning them
+// (the lane owns bytes [p, p + width) of the tile)
 __device__ __forceinline__ void store_literal(uint32_t p, uint64_t dst, uint32_t n, uint32_t litLen,
-                                              const uint32_t* lit)
+                                              uint32_t lit0, uint32_t lit1, uint32_t width = 4)
 {
-    if (litLen && n + litLen > p && n < p + 4) {
+    if (litLen && n + litLen > p && n < p + width) {
         GMEM uint8_t* d = reinterpret_cast<GMEM uint8_t*>(dst);
-        for (uint32_t k = (n > p ? n : p); k < n + litLen && k < p + 4; ++k)
-            d[k] = (uint8_t)(lit[(k - n) >> 2] >> (8 * ((k - n) & 3)));
+        for (uint32_t k = (n > p ? n : p); k < n + litLen && k < p + width; ++k)
+            d[k] = (uint8_t)(((k - n) >= 4 ? lit1 : lit0) >> (8 * ((k - n) & 3)));
     }
 }
 
@@ -539,6 +567,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint16_t plan[kPlanCap];            // rows' terms as stage slots
     __shared__ uint2 rowInfo[kPlanRows];           // plan offset (or kNoPlan/kPlanGeneral), n0 | n1 << 16
     __shared__ unsigned long long acctL;          // reference source bytes counted by this workgroup
+    __shared__ uint32_t generalRows;               // a row of this OP_ROWS batch has no plan
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
@@ -548,33 +577,36 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     const ExecItem it = items[blockIdx.x];
     const uint4* seg = stream + it.streamBegin;
     const uint32_t words = it.streamWords;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63;
-    const uint32_t wave = uni(tid >> 6);   // (uniform: keeps wave-derived loops scalar)
+    const uint32_t wave = uni(threadIdx.x >> 6);   // (uniform: keeps wave-derived loops scalar)
     const uint32_t tileBase = it.tileBase;
-    const uint32_t p = tileBase + lane * 4;
-    // PCG jump-ahead by this lane's index (A^lane, sum_{t<lane} A^t)
-    const uint64_t pcgA = c_pcgA[lane], pcgG = c_pcgG[lane];
-    const uint64_t pcgA64 = c_pcgA[64], pcgG64 = c_pcgG[64];
 #ifdef SGPU_PHASE_CLOCKS
     unsigned long long kclk = clock64();
 #endif
 
-    if (tid < kRingWords)
-        ring[0][tid] = tid < words ? ld16((uint64_t)(seg + tid)) : make_uint4(0, 0, 0, 0);
-    for (uint32_t c = tid; c < kColumnValuePeriod; c += kExecThreads) {
+    {
+        const uint32_t tid = threadIdx.x;
+        if (tid < kRingWords)
+            ring[0][tid] = tid < words ? ld16((uint64_t)(seg + tid)) : make_uint4(0, 0, 0, 0);
+        for (uint32_t c = tid; c < kColumnValuePeriod; c += kExecThreads) {
         const uint32_t cx = 3u + (c * 199u) % kColumnValuePeriod;   // SiameseCommon.h:89-93
-        cxL[c] = cx | ((uint32_t)c_sqr[cx] << 8);
-    }
-    if (tid == 0)
-        acctL = 0;
-    if (tid < 256) {
-        permL[tid] = make_uint4(c_perm[tid][0], c_perm[tid][1], c_perm[tid][2], c_perm[tid][3]);
-        permC[tid] = c_perm[tid][4];
+            cxL[c] = cx | ((uint32_t)c_sqr[cx] << 8);
+        }
+        if (tid == 0)
+            acctL = 0;
+        if (tid < 256) {
+            permL[tid] = make_uint4(c_perm[tid][0], c_perm[tid][1], c_perm[tid][2], c_perm[tid][3]);
+            permC[tid] = c_perm[tid][4];
+        }
     }
     __syncthreads();
     uint32_t cur = 0, pos = 0;
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
+        // the thread index, opaque per op: lane-derived addresses are then
+        // computed where they are used instead of hoisted out of the op loop,
+        // where dozens of them would hold VGPRs through every phase
+        const uint32_t tid = opaque(threadIdx.x);
+        const uint32_t lane = tid & 63;
+        const uint32_t p = tileBase + lane * 4;
         const uint4* rb = ring[cur];
         const uint4 h0 = rb[0], h1 = rb[1];
         const uint64_t dst = ((uint64_t)uni(h0.y) << 32) | uni(h0.x);
@@ -591,8 +623,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
 
         if (kind == OP_LITERAL) {
             if (wave == 0) {
-                const uint32_t lit[2] = {uni(h1.z), uni(h1.w)};
-                store_literal(p, dst, n, valid, lit);
+                store_literal(p, dst, n, valid, uni(h1.z), uni(h1.w));
             }
         } else if (kind == OP_LINCOMB) {
             if (tileBase < align16u(n)) {   // uniform: the op reaches this tile
@@ -642,6 +673,13 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             const uint32_t blockWords = uni(h1.w);
             for (uint32_t i = tid; i < blockWords && i < kRowsTableLds; i += kExecThreads)
                 tableL[i] = op_word(rb, seg, pos, kOpWords + i);
+            if (tid == 0)
+                generalRows = 0;
+            // the next op's prefetched block goes to the ring now (the ring's
+            // other half is free: the previous op ended with a barrier), so
+            // it holds no registers through the batch
+            if (tid < kRingWords)
+                ring[cur ^ 1][tid] = pf;
             __syncthreads();
             PHASE_MARK(0, tclk);
 
@@ -665,7 +703,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             auto build_plan = [&]() {
                 // plan: row sizes are its selected sums plus one slot per
                 // LDPC draw, offsets a prefix sum over rows (each wave scans
-                // them all and keeps the rows it owns, r = wave mod W); the
+                // them all and keeps the rows it owns, r/2 = wave mod W); the
                 // draws are made lane parallel (and their reference source
                 // bytes counted); a row with a draw outside the staged
                 // window keeps reading memory
@@ -689,65 +727,79 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             incl += t;
                     }
                     const uint32_t offs = carry + incl - size;
-                    if (r < planned && r % kExecWaves == wave)
-                        rowInfo[r] = make_uint2(sumsStaged && offs + size <= kPlanCap ? offs : kNoPlan, n01);
+                    if (r < planned && (r >> 1) % kExecWaves == wave) {
+                        const bool fits = sumsStaged && offs + size <= kPlanCap;
+                        rowInfo[r] = make_uint2(fits ? offs : kNoPlan, n01);
+                        if (!fits)
+                            generalRows = 1;
+                    }
                     carry += __shfl(incl, 63, 64);
                 }
-                for (uint32_t r = wave; r < planned; r += kExecWaves) {
-                    const uint2 info = rowInfo[r];   // (this wave's own write)
-                    const uint32_t off0 = uni(info.x);
-                    if (off0 == kNoPlan)
+                // draws, two rows per wave at a time: lanes 32h..32h+31 take
+                // row 2i+h (this wave's own rowInfo writes above)
+                const uint32_t h = lane >> 5, hl = lane & 31u;
+                for (uint32_t r2 = 2 * wave; r2 < planned; r2 += 2 * kExecWaves) {
+                    const uint32_t r = r2 + h;
+                    const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
+                    const bool act = info.x != kNoPlan;
+                    if (!__any(act ? 1 : 0))
                         continue;
-                    const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
-                    const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
-                    const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords);
-                    const uint32_t rn = uni(w0.z);
-                    const uint32_t m0 = uni(w1.x) & 0xffffffu, m1 = uni(w1.y) & 0xffffffu;
-                    const uint32_t row = uni(w1.z), N = uni(w1.w), woff = uni(w2.x);
-                    const uint32_t n0 = uni(info.y) & 0xffffu;
+                    const uint4 z4 = make_uint4(0, 0, 0, 0);
+                    const uint4 w0 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords) : z4;
+                    const uint4 w1 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords) : z4;
+                    const uint4 w2 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords) : z4;
+                    const uint32_t rn = w0.z;
+                    const uint32_t m0 = w1.x & 0xffffffu, m1 = w1.y & 0xffffffu;
+                    const uint32_t row = w1.z, N = act ? w1.w : 0u, woff = w2.x;
+                    const uint32_t off0 = info.x, off1 = info.x + (info.y & 0xffffu);
                     const uint32_t pc0 = __builtin_popcount(m0), pc1 = __builtin_popcount(m1);
-                    const uint32_t off1 = off0 + n0;
-                    // sums: lane k < 24 places slot k if its bit is set
-                    if (lane < kRowSums) {
-                        const uint32_t below = (1u << lane) - 1u;
-                        if (m0 >> lane & 1u)
-                            plan[off0 + __builtin_popcount(m0 & below)] = (uint16_t)lane;
-                        if (m1 >> lane & 1u)
-                            plan[off1 + __builtin_popcount(m1 & below)] = (uint16_t)lane;
+                    // sums: lane k < 24 of the half places slot k if its bit is set
+                    if (act && hl < kRowSums) {
+                        const uint32_t below = (1u << hl) - 1u;
+                        if (m0 >> hl & 1u)
+                            plan[off0 + __builtin_popcount(m0 & below)] = (uint16_t)hl;
+                        if (m1 >> hl & 1u)
+                            plan[off1 + __builtin_popcount(m1 & below)] = (uint16_t)hl;
                     }
                     // draws: even -> row list, odd -> product list
+                    const uint32_t D = N ? 2 * ((N + kPairRate - 1) / kPairRate) : 0u;
+                    uint32_t Dmax = max(D, (uint32_t)__shfl_xor(D, 32, 64));
+                    Dmax = uni(Dmax);
                     bool general = false;
                     uint32_t refBytes = 0;
-                    if (N != 0) {
-                        const uint32_t D = 2 * ((N + kPairRate - 1) / kPairRate);
-                        const uint64_t inc = ((uint64_t)row << 1) | 1u;
-                        uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
-                        // x % N through a double reciprocal: the quotient estimate
-                        // is within one for 32-bit x, then corrected exactly
-                        const double invN = 1.0 / (double)N;
-                        for (uint32_t c = 0; c < D; c += 64) {
-                            const uint32_t d = c + lane;
-                            const uint64_t st = pcgA * sc + inc * pcgG;
-                            sc = pcgA64 * sc + inc * pcgG64;
-                            if (d < D) {
-                                const uint32_t x = pcg_output(st);
-                                const uint32_t qn = (uint32_t)((double)x * invN);
-                                int64_t rr = (int64_t)x - (int64_t)qn * N;
-                                rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
-                                const uint32_t e = woff + (uint32_t)rr;
-                                const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e).z;
-                                refBytes += len < rn ? len : rn;
-                                general |= e >= staged;
-                                const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
-                                plan[at] = (uint16_t)(e < staged ? kRowSums + e : 0);
-                            }
+                    const uint64_t inc = ((uint64_t)row << 1) | 1u;
+                    uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
+                    // x % N through a double reciprocal: the quotient estimate
+                    // is within one for 32-bit x, then corrected exactly
+                    const double invN = N ? 1.0 / (double)N : 0.0;
+                    // (an opaque lane index keeps these loads in the loop: hoisted
+                    // out of the op loop they would hold 4 VGPRs through every phase)
+                    const uint32_t jl = opaque(hl);
+                    const uint64_t ja = c_pcgA[jl], jg = c_pcgG[jl];
+                    for (uint32_t c = 0; c < Dmax; c += 32) {
+                        const uint32_t d = c + hl;
+                        const uint64_t st = ja * sc + inc * jg;
+                        sc = c_pcgA[32] * sc + inc * c_pcgG[32];
+                        if (d < D) {
+                            const uint32_t x = pcg_output(st);
+                            const uint32_t qn = (uint32_t)((double)x * invN);
+                            int64_t rr = (int64_t)x - (int64_t)qn * N;
+                            rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
+                            const uint32_t e = woff + (uint32_t)rr;
+                            const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e).z;
+                            refBytes += len < rn ? len : rn;
+                            general |= e >= staged;
+                            const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
+                            plan[at] = (uint16_t)(e < staged ? kRowSums + e : 0);
                         }
                     }
                     if (tileBase == 0)
                         acct_wave(&acctL, refBytes);
-                    const bool anyGeneral = __any(general ? 1 : 0);
-                    if (anyGeneral && lane == 0)
+                    const uint64_t gb = __ballot(general ? 1 : 0);
+                    if (hl == 0 && act && (uint32_t)(gb >> (32 * h)) != 0) {
                         rowInfo[r].x = kPlanGeneral;
+                        generalRows = 1;
+                    }
                 }
             };
             for (uint32_t e0 = tid / 16, first = 1; first || e0 < staged; e0 += 4 * kPass) {
@@ -894,14 +946,93 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             __syncthreads();
             PHASE_MARK(4, tclk);
 
-            // phase B1: rows.  R >= W: wave w takes rows w, w+W, ...; R < W:
-            // row r's terms are split into P = W / R parts, unit w = (w / P,
-            // w % P), and the parts meet in LDS.  A planned row XORs stage
-            // slots; the others read sums and undrawn-from-LDS picks from
-            // memory.  lane j < 24 holds sum entry j.
+            // phase B1a: planned rows, four per wave at a time: quad g of the
+            // wave (lanes 16g..16g+15) takes row 4t+g, and lane l holds bytes
+            // 16*(l%16).. of the tile, so one 16-byte LDS read per lane moves
+            // one term of each of four rows and every per-row step (the
+            // descriptors, the RX product, the stores) is paid once per four
+            // rows.
+            {
+                const uint32_t nq = (planned + 3) / 4;
+                const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
+                const uint32_t p16 = tileBase + (lane & 15u) * 16u;
+                for (uint32_t task = wave; task < nq; task += kExecWaves) {
+#ifdef SGPU_PHASE_CLOCKS
+                    unsigned long long qclk = clock64();
+#endif
+                    const uint32_t r = task * 4 + g;
+                    const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
+                    const bool act = info.x < kPlanGeneral;
+                    if (!__any(act ? 1 : 0))
+                        continue;
+                    const uint4 z4 = make_uint4(0, 0, 0, 0);
+                    const uint4 w0 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords) : z4;
+                    const uint4 w1 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords) : z4;
+                    const uint4 w2 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords) : z4;
+                    const uint64_t rdst = ((uint64_t)w0.y << 32) | w0.x;
+                    const uint32_t rn = w0.z, rvalid = w0.w;
+                    const uint32_t mix = w1.y >> 24;
+                    const bool live = act && tileBase < align16u(rn);
+                    // dst as kept (decoder rows), fetched before the terms stream in
+                    const uint4 cur = live ? load_cur16(p16, rdst, rn, rvalid) : z4;
+                    const GfTab tab = gf_tab_l(permL, permC, mix > 1 ? mix : 1u);
+                    const uint32_t off0 = info.x, n0 = live ? (info.y & 0xffffu) : 0u;
+                    const uint32_t off1 = info.x + (info.y & 0xffffu), n1 = live ? (info.y >> 16) : 0u;
+                    uint32_t most = n0 > n1 ? n0 : n1;
+                    most = max(most, (uint32_t)__shfl_xor(most, 16, 64));
+                    most = uni(max(most, (uint32_t)__shfl_xor(most, 32, 64)));
+                    PHASE_MARK(13, qclk);
+                    uint4 a0 = z4, a1 = z4;
+                    // 16 terms at a time: lane i of a quad reads plan entry
+                    // t+i of its row's lists, a row broadcast (DPP) hands
+                    // entry j to the whole quad, 4 terms of each list in flight
+                    for (uint32_t t = 0; t < most; t += 16) {
+                        const uint32_t i = t + (lane & 15u);
+                        const uint32_t s0 = i < n0 ? (uint32_t)plan[off0 + i] : 0u;
+                        const uint32_t s1 = i < n1 ? (uint32_t)plan[off1 + i] : 0u;
+                        const uint32_t rem0 = n0 > t ? n0 - t : 0u, rem1 = n1 > t ? n1 - t : 0u;
+                        const uint32_t left = most - t;   // (uniform)
+                        uint4 v0[4], v1[4];
+    // (terms past a list's end read slot 0 and are masked off: a select
+    // between an LDS read and a constant would become a flat load)
+#define SGPU_QUAD_LOAD(J)                                                                                   \
+    v0[(J) & 3] = and16(lds16(stage, row_bcast<(J)>(s0) * 64 + b4), (J) < rem0 ? ~0u : 0u);              \
+    v1[(J) & 3] = and16(lds16(stage, row_bcast<(J)>(s1) * 64 + b4), (J) < rem1 ? ~0u : 0u);
+#define SGPU_QUAD_XOR()                                                                                     \
+    a0 = xor16(xor16(a0, xor16(v0[0], v0[1])), xor16(v0[2], v0[3]));                                      \
+    a1 = xor16(xor16(a1, xor16(v1[0], v1[1])), xor16(v1[2], v1[3]));
+                        SGPU_QUAD_LOAD(0) SGPU_QUAD_LOAD(1) SGPU_QUAD_LOAD(2) SGPU_QUAD_LOAD(3) SGPU_QUAD_XOR()
+                        if (left > 4) {
+                            SGPU_QUAD_LOAD(4) SGPU_QUAD_LOAD(5) SGPU_QUAD_LOAD(6) SGPU_QUAD_LOAD(7) SGPU_QUAD_XOR()
+                        }
+                        if (left > 8) {
+                            SGPU_QUAD_LOAD(8) SGPU_QUAD_LOAD(9) SGPU_QUAD_LOAD(10) SGPU_QUAD_LOAD(11) SGPU_QUAD_XOR()
+                        }
+                        if (left > 12) {
+                            SGPU_QUAD_LOAD(12) SGPU_QUAD_LOAD(13) SGPU_QUAD_LOAD(14) SGPU_QUAD_LOAD(15) SGPU_QUAD_XOR()
+                        }
+#undef SGPU_QUAD_LOAD
+#undef SGPU_QUAD_XOR
+                    }
+                    PHASE_MARK(14, qclk);
+                    if (live)
+                        store_item16(xor16(a0, gf_mul16_tab(a1, tab)), p16, rdst, rn, rvalid, cur);
+                    if (act) {
+                        store_literal(p16, rdst, rn, w1.x >> 24, w2.z, w2.w, 16);
+                    }
+                    PHASE_MARK(15, qclk);
+                }
+            }
+
+            // phase B1b: rows without a plan (a draw outside the staged
+            // window, or past the plan's capacity).  R >= W: wave w takes rows
+            // w, w+W, ...; R < W: row r's terms are split into P = W / R parts,
+            // unit w = (w / P, w % P), and the parts meet in LDS.  They read
+            // sums and undrawn-from-LDS picks from memory; lane j < 24 holds
+            // sum entry j.
             const uint4 sumv = lane < kRowSums ? tableL[lane] : make_uint4(0, 0, 0, 0);
             const uint32_t P = R >= kExecWaves ? 1u : kExecWaves / R;
-            const uint32_t units = P == 1 ? R : R * P;
+            const uint32_t units = (R > planned || uni(generalRows)) ? (P == 1 ? R : R * P) : 0u;
             for (uint32_t unit = wave; unit < units; unit += kExecWaves) {
                 const uint32_t r = P == 1 ? unit : unit / P;
                 const uint32_t q = P == 1 ? 0 : unit % P;
@@ -915,114 +1046,58 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 const uint32_t mix = m1 >> 24;
                 const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
                 const uint32_t pinfo = uni(info.x);
+                if (pinfo < kPlanGeneral)
+                    continue;   // (phase B1a)
 #ifdef SGPU_PHASE_CLOCKS
                 unsigned long long rclk = clock64();
 #endif
                 // dst as kept (decoder rows) and the product's multiply table,
                 // fetched before the terms stream in
-                const bool plannedRow = pinfo < kPlanGeneral;
-                const uint32_t p16 = tileBase + (lane & 15u) * 16u;
-                const uint32_t c0 = (P == 1 && !plannedRow && tileBase < align16u(rn)) ? load_cur(p, rdst, rn, rvalid) : 0u;
-                const uint4 c0q = (P == 1 && plannedRow && tileBase < align16u(rn) && lane < 16)
-                                      ? load_cur16(p16, rdst, rn, rvalid) : make_uint4(0, 0, 0, 0);
+                const uint32_t c0 = (P == 1 && tileBase < align16u(rn)) ? load_cur(p, rdst, rn, rvalid) : 0u;
                 const GfTab mixTab = gf_tab_l(permL, permC, mix);
                 uint32_t acc0 = 0, acc1 = 0;
-                uint4 acc0q = make_uint4(0, 0, 0, 0), acc1q = acc0q;   // planned rows (quad layout)
-                bool quadRow = false;
                 if (tileBase < align16u(rn)) {
-                    if (pinfo < kPlanGeneral) {
-                        // planned: XOR of stage slots, the part's share of each
-                        // list, in the quad layout: quad g of the wave takes
-                        // terms g, g+4, ... and lane l holds bytes 16*(l%16)..
-                        // of the tile, so one 16-byte LDS read per lane moves
-                        // four terms; the quads are folded at the end.
-                        const uint32_t n0 = uni(info.y) & 0xffffu, n1 = uni(info.y) >> 16;
-                        const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
-                        for (unsigned h = 0; h < 2; ++h) {
-                            const uint32_t nl = h ? n1 : n0;
-                            const uint32_t base = pinfo + (h ? n0 : 0);
-                            const uint32_t i0 = base + nl * q / P, i1 = base + nl * (q + 1) / P;
-                            uint4 a = make_uint4(0, 0, 0, 0);
-                            for (uint32_t t = i0; t < i1; t += 16) {
-                                uint4 v[4];
-#pragma unroll
-                                for (unsigned k = 0; k < 4; ++k) {
-                                    const uint32_t ti = t + 4 * k + g;
-                                    v[k] = make_uint4(0, 0, 0, 0);
-                                    if (ti < i1)
-                                        v[k] = *reinterpret_cast<const uint4*>(&stage[(uint32_t)plan[ti] * 64 + b4]);
-                                }
-#pragma unroll
-                                for (unsigned k = 0; k < 4; ++k)
-                                    a = xor16(a, v[k]);
-                            }
-                            a = quad_fold(a);
-                            if (h)
-                                acc1q = a;
-                            else
-                                acc0q = a;
-                        }
-                        quadRow = true;
-                    } else {
-                        // dense part (part 0): the sums the opcodes select (bit
-                        // lane*3+s; mask1 feeds the product)
-                        if (q == 0) {
-                            uint64_t bits = (uint64_t)(m0 & 0xffffffu) | ((uint64_t)(m1 & 0xffffffu) << 24);
-                            gather(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
-                                   [&](uint32_t, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                                       const uint32_t b = (uint32_t)__builtin_ctzll(bits);
-                                       bits &= bits - 1;
-                                       const uint32_t k = b < kRowSums ? b : b - kRowSums;
-                                       lane_term(sumv, k, src, len);
-                                       ca = 1u | ((b >= kRowSums ? 1u : 0u) << 8);
-                                       return len != 0;
-                                   });
-                        }
-                        // sparse part: this unit's share of the 2*ceil(N/16) draws
-                        // (pairs stay whole: even draw -> row, odd -> product)
-                        if (N != 0) {
-                            const uint32_t pairs = (N + kPairRate - 1) / kPairRate;
-                            const uint32_t d0 = 2 * (pairs * q / P), d1 = 2 * (pairs * (q + 1) / P);
-                            const uint32_t refBytes = row_picks(row, N, off, d0, d1, rn, tileBase, p, lane, pcgA,
-                                                                pcgG, stage, staged, tableL, seg, blk, acc0, acc1);
-                            // (a planned row's draws were counted by its plan)
-                            if (pinfo == kNoPlan && tileBase == 0 && lane == 0 && refBytes)
-                                atomicAdd(&acctL, (unsigned long long)refBytes);
-                        }
+                    // dense part (part 0): the sums the opcodes select (bit
+                    // lane*3+s; mask1 feeds the product)
+                    if (q == 0) {
+                        uint64_t bits = (uint64_t)(m0 & 0xffffffu) | ((uint64_t)(m1 & 0xffffffu) << 24);
+                        gather(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
+                               [&](uint32_t, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                                   const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+                                   bits &= bits - 1;
+                                   const uint32_t k = b < kRowSums ? b : b - kRowSums;
+                                   lane_term(sumv, k, src, len);
+                                   ca = 1u | ((b >= kRowSums ? 1u : 0u) << 8);
+                                   return len != 0;
+                               });
+                    }
+                    // sparse part: this unit's share of the 2*ceil(N/16) draws
+                    // (pairs stay whole: even draw -> row, odd -> product)
+                    if (N != 0) {
+                        const uint32_t pairs = (N + kPairRate - 1) / kPairRate;
+                        const uint32_t d0 = 2 * (pairs * q / P), d1 = 2 * (pairs * (q + 1) / P);
+                        const uint32_t refBytes = row_picks(row, N, off, d0, d1, rn, tileBase, p, lane,
+                                                            c_pcgA[opaque(lane)], c_pcgG[opaque(lane)], stage, staged, tableL, seg, blk, acc0, acc1);
+                        // (a planned row's draws were counted by its plan)
+                        if (pinfo == kNoPlan && tileBase == 0 && lane == 0 && refBytes)
+                            atomicAdd(&acctL, (unsigned long long)refBytes);
                     }
                 }
                 if (P > 1) {
-                    // partials in the dword layout (lane l: bytes 4l..); a
-                    // quad-layout row's quad 0 writes the same bytes as 16-byte words
-                    if (quadRow) {
-                        if (lane < 16) {
-                            *reinterpret_cast<uint4*>(&part[wave][0][lane * 4]) = acc0q;
-                            *reinterpret_cast<uint4*>(&part[wave][1][lane * 4]) = acc1q;
-                        }
-                    } else {
-                        part[wave][0][lane] = acc0;
-                        part[wave][1][lane] = acc1;
-                    }
-                } else if (quadRow) {
-                    if (tileBase < align16u(rn) && lane < 16)
-                        store_item16(xor16(acc0q, mix > 1 ? gf_mul16_tab(acc1q, mixTab) : acc1q), p16, rdst, rn,
-                                     rvalid, c0q);
-                    PHASE_MARK(14, rclk);
-                    const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
-                    store_literal(p, rdst, rn, m0 >> 24, lit);
-                    PHASE_MARK(15, rclk);
+                    part[wave][0][lane] = acc0;
+                    part[wave][1][lane] = acc1;
                 } else {
                     if (tileBase < align16u(rn))
                         store_item(acc0 ^ (mix > 1 ? gf_mul_tab(acc1, mixTab) : acc1), p, rdst, rn, rvalid, c0);
                     PHASE_MARK(14, rclk);
-                    const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
-                    store_literal(p, rdst, rn, m0 >> 24, lit);
+                    store_literal(p, rdst, rn, m0 >> 24, uni(w2.z), uni(w2.w));
                     PHASE_MARK(15, rclk);
                 }
             }
-            if (P > 1) {
+            if (P > 1 && units) {
                 __syncthreads();
-                if (wave < units && wave % P == 0) {
+                if (wave < units && wave % P == 0 &&
+                    !(wave / P < planned && uni(rowInfo[wave / P].x) < kPlanGeneral)) {
                     const uint32_t r = wave / P;
                     const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
                     const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
@@ -1039,8 +1114,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         const uint32_t c0 = load_cur(p, rdst, rn, rvalid);
                         store_item(acc0 ^ (mix > 1 ? gf_mul_dword(acc1, mix) : acc1), p, rdst, rn, rvalid, c0);
                     }
-                    const uint32_t lit[2] = {uni(w2.z), uni(w2.w)};
-                    store_literal(p, rdst, rn, m0 >> 24, lit);
+                    store_literal(p, rdst, rn, m0 >> 24, uni(w2.z), uni(w2.w));
                 }
             }
             PHASE_MARK(5, tclk);
@@ -1082,13 +1156,14 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 }
             }
         }
-        if (tid < kRingWords)
+        if (kind != OP_ROWS && tid < kRingWords)
             ring[cur ^ 1][tid] = pf;
         __syncthreads();
         cur ^= 1;
         pos = next;
     }
     // (the last op's barrier ordered every wave's count)
+    const uint32_t tid = threadIdx.x;
     if (tid == 0 && acctL)
         atomicAdd(acct, acctL);
     PHASE_MARK(6, kclk);

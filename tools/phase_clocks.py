@@ -22,7 +22,7 @@ print("OP_ROWS workgroup-ops %d, rows %.1f, updates %.1f, window %.1f, staged %.
       % (out[8], out[9] / ops, out[10] / ops, out[11] / ops, out[12] / ops))
 for k, nm in enumerate(names):
     print("  %-14s %10.0f clocks per op" % (nm, out[k] / ops))
-print("  rows detail (wave 0): planned XOR %.0f, mix+store %.0f, literal %.0f clocks per op"
+print("  rows detail (wave 0 quad tasks): descriptors %.0f, terms %.0f, stores %.0f clocks per op"
       % (out[13] / ops, out[14] / ops, out[15] / ops))
 print("  detail (wave 0): update unit %.0f, plan scan %.0f, plan draws %.0f clocks per op"
       % (out[19] / ops, out[20] / ops, out[21] / ops))
