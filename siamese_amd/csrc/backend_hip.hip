@@ -243,12 +243,6 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
 // The barrier that rotates the ring also orders each op's stores before any
 // later op of the segment reads them (stores from one CU are visible to the
 // CU's other waves after the workgroup-scope fence of __syncthreads).
-#ifndef SGPU_PLAN_OVERLAP
-#define SGPU_PLAN_OVERLAP 0
-#endif
-#ifndef SGPU_UPD_SPLIT
-#define SGPU_UPD_SPLIT 0
-#endif
 #ifndef SGPU_EXEC_WAVES
 #define SGPU_EXEC_WAVES 16
 #endif
@@ -410,6 +404,15 @@ __device__ __forceinline__ void store_item(uint32_t out, uint32_t p, uint64_t ds
     st4(dst + p, out & byte_mask((int)n - (int)p));
 }
 
+// the dword store_item writes at p < align16(n) (keep(cur, valid) ^ out,
+// zero past n)
+__device__ __forceinline__ uint32_t item_value(uint32_t out, uint32_t p, uint32_t n, uint32_t valid, uint32_t cur)
+{
+    if (p < valid)
+        out ^= cur & byte_mask((int)valid - (int)p);
+    return out & byte_mask((int)n - (int)p);
+}
+
 // store_item for a 16-byte lane (the quad layout of planned rows: lane
 // holds bytes [p, p+16) of the tile)
 __device__ __forceinline__ void store_item16(uint4 out, uint32_t p, uint64_t dst, uint32_t n, uint32_t valid,
@@ -568,6 +571,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint2 rowInfo[kPlanRows];           // plan offset (or kNoPlan/kPlanGeneral), n0 | n1 << 16
     __shared__ unsigned long long acctL;          // reference source bytes counted by this workgroup
     __shared__ uint32_t generalRows;               // a row of this OP_ROWS batch has no plan
+    __shared__ uint32_t sumsDirty;                 // a staged lane sum must be re-read after the updates
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
@@ -683,30 +687,86 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             __syncthreads();
             PHASE_MARK(0, tclk);
 
-            // every wave: issue its loads of this tile of window elements
-            // [0, staged) (thread t: 16 bytes of element t/16 per pass, four
-            // passes in flight; bytes past an element's length -- absent
-            // elements: all of them -- read zero), build its rows' term plans
-            // (phase B0, from the descriptors alone) while they fly, then
-            // write them to stage slots 24..
+            // phase S: stage this tile of the 24 lane sums (slots 0..23, as
+            // they stand before the batch's updates) and of window elements
+            // [0, staged) (slots 24..): table entry x is stage slot x.  Thread
+            // t loads 16 bytes of entry t/16 per pass, four passes in flight;
+            // bytes past an entry's length (absent elements: all of them)
+            // read zero.
             const uint32_t staged = E < stageCap ? E : stageCap;
             const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
             const bool sumsStaged = stageSlots >= kRowSums;
             const uint32_t updWord = kOpWords + T;
             const uint32_t rowWord = updWord + U * kUpdateWords;
             const uint32_t planned = R < kPlanRows ? R : kPlanRows;
-            constexpr unsigned kPass = kExecThreads / 16;   // elements per pass
+            constexpr unsigned kPass = kExecThreads / 16;   // entries per pass
             uint32_t* updAcc = &part[0][0][0];              // U <= 24 update accumulators of 64 dwords
             static_assert(kExecWaves * 2 >= kRowSums, "update accumulators fit part[]");
             for (uint32_t i = tid; i < U * 64; i += kExecThreads)
                 updAcc[i] = 0;
-            auto build_plan = [&]() {
-                // plan: row sizes are its selected sums plus one slot per
-                // LDPC draw, offsets a prefix sum over rows (each wave scans
-                // them all and keeps the rows it owns, r/2 = wave mod W); the
-                // draws are made lane parallel (and their reference source
-                // bytes counted); a row with a draw outside the staged
-                // window keeps reading memory
+            if (tid == 0)
+                sumsDirty = 0;
+            {
+                const uint32_t entries = sumsStaged ? kRowSums + staged : 0u;
+                for (uint32_t x0 = tid / 16; x0 < entries; x0 += 4 * kPass) {
+                    uint4 v[4];
+#pragma unroll
+                    for (unsigned u = 0; u < 4; ++u) {
+                        const uint32_t x = x0 + u * kPass;
+                        v[u] = make_uint4(0, 0, 0, 0);
+                        if (x < entries) {
+                            const uint4 d = table_entry(tableL, seg, blk, x);
+                            const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+                            if (tileBase + q16 < d.z)
+                                v[u] = ld16(src + tileBase + q16);
+                        }
+                    }
+#pragma unroll
+                    for (unsigned u = 0; u < 4; ++u) {
+                        const uint32_t x = x0 + u * kPass;
+                        if (x < entries)
+                            *reinterpret_cast<uint4*>(&stage[x * 64 + q16 / 4]) = v[u];
+                    }
+                }
+            }
+            __syncthreads();
+            PHASE_MARK(1, tclk);
+
+            // phase A + B0: the lane-sum updates and the rows' term plans,
+            // dealt to the waves as units: unit < U*Q is part unit%Q of update
+            // unit/Q, the rest are row pairs of the plan.
+            //
+            // Updates (SiameseEncoder.cpp:359-418, SiameseDecoder.cpp:
+            // 1680-1739): element e = from, from+8, ... < to, coefficient 1, CX
+            // or CX^2 of its column.  Staged elements go four per wave
+            // instruction (quad g of the wave takes element 4j+g, lane l bytes
+            // 16*(l%16).., each lane with its element's multiply table from
+            // LDS); an update reaching past the stage falls back to the dword
+            // layout (lane j holds element j's descriptor and table, moved to
+            // scalars with readlane) with memory reads.  Partial sums meet in
+            // LDS accumulators (XOR atomics).
+            //
+            // Plan: row sizes are its selected sums plus one slot per LDPC
+            // draw, offsets a prefix sum over rows (every wave scans them all
+            // and keeps the rows whose pair it owns); the draws are made lane
+            // parallel, two rows per wave (lanes 32h.. take row 2i+h), and
+            // their reference source bytes counted; a row with a draw outside
+            // the staged window keeps reading memory (phase B1b).
+            const uint32_t Q = U == 0 ? 1u : (U >= kExecWaves ? 1u : kExecWaves / U);
+            const uint32_t uUnits = U * Q;
+            const uint32_t nPairs = sumsStaged ? (planned + 1) / 2 : 0u;
+            // the update this wave stores: its dst as kept, fetched now
+            uint64_t sdst = 0;
+            uint32_t sn = 0, svalid = 0, scur = 0;
+            if (wave < U) {
+                const uint4 w0 = table_entry(tableL, seg, blk, updWord + wave * kUpdateWords - kOpWords);
+                sdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                sn = uni(w0.z);
+                svalid = uni(w0.w) & 0x3fffffffu;
+                if (tileBase < align16u(sn))
+                    scur = load_cur(p, sdst, sn, svalid);
+            }
+            if (nPairs) {
                 uint32_t carry = 0;
                 for (uint32_t r0 = 0; r0 < planned; r0 += 64) {
                     const uint32_t r = r0 + lane;
@@ -720,27 +780,117 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         n01 = n0 | (n1 << 16);
                     }
                     uint32_t incl = size;
-    #pragma unroll
+#pragma unroll
                     for (unsigned d = 1; d < 64; d <<= 1) {
                         const uint32_t t = __shfl_up(incl, d, 64);
                         if (lane >= d)
                             incl += t;
                     }
                     const uint32_t offs = carry + incl - size;
-                    if (r < planned && (r >> 1) % kExecWaves == wave) {
-                        const bool fits = sumsStaged && offs + size <= kPlanCap;
+                    if (r < planned && (uUnits + (r >> 1)) % kExecWaves == wave) {
+                        const bool fits = offs + size <= kPlanCap;
                         rowInfo[r] = make_uint2(fits ? offs : kNoPlan, n01);
                         if (!fits)
                             generalRows = 1;
                     }
                     carry += __shfl(incl, 63, 64);
                 }
-                // draws, two rows per wave at a time: lanes 32h..32h+31 take
-                // row 2i+h (this wave's own rowInfo writes above)
-                const uint32_t h = lane >> 5, hl = lane & 31u;
-                for (uint32_t r2 = 2 * wave; r2 < planned; r2 += 2 * kExecWaves) {
-                    const uint32_t r = r2 + h;
-                    const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
+            }
+            const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
+            for (uint32_t unit = wave; unit < uUnits + nPairs; unit += kExecWaves) {
+                if (unit < uUnits) {
+                    [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
+                    const uint32_t u = unit / Q;
+                    const uint32_t uq = unit % Q;
+                    const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
+                    const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords);
+                    const uint32_t un = uni(w0.z), us = uni(w0.w) >> 30;
+                    const uint32_t from = uni(w1.x), to = uni(w1.y);
+                    const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
+                    const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
+                    if (tileBase < align16u(un) && k0 < k1) {
+                        uint32_t refBytes = 0;   // reference source bytes (one add/muladd per original)
+                        if (from + (k1 - 1) * kLanes < staged) {
+                            // quad layout, two elements per quad in flight
+                            uint4 a = make_uint4(0, 0, 0, 0);
+                            for (uint32_t kk = k0; kk < k1; kk += 8) {
+                                uint4 v[2];
+#pragma unroll
+                                for (unsigned j = 0; j < 2; ++j) {
+                                    const uint32_t k = kk + 4 * j + g;
+                                    const bool act = k < k1;
+                                    const uint32_t e = from + (act ? k : k0) * kLanes;
+                                    const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
+                                    if (act && (lane & 15u) == 0)
+                                        refBytes += ev.z;
+                                    v[j] = and16(lds16(stage, (kRowSums + e) * 64 + b4), act ? ~0u : 0u);
+                                    if (us != 0) {
+                                        const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
+                                        v[j] = gf_mul16_tab(v[j], gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8)));
+                                    }
+                                }
+                                a = xor16(a, xor16(v[0], v[1]));
+                            }
+                            atomicXor(&updAcc[u * 64 + b4 + 0], a.x);
+                            atomicXor(&updAcc[u * 64 + b4 + 1], a.y);
+                            atomicXor(&updAcc[u * 64 + b4 + 2], a.z);
+                            atomicXor(&updAcc[u * 64 + b4 + 3], a.w);
+                        } else {
+                            uint32_t acc = 0;
+                            for (uint32_t c = k0; c < k1; c += 64) {
+                                const uint32_t e = from + (c + lane) * kLanes;
+                                const uint4 ev = c + lane < k1 ? table_entry(tableL, seg, blk, kRowSums + e)
+                                                               : make_uint4(0, 0, 0, 0);
+                                const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
+                                const GfTab tab = gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8));
+                                refBytes += ev.z;
+                                const uint32_t cnt = k1 - c < 64 ? k1 - c : 64;
+                                for (uint32_t j0 = 0; j0 < cnt; j0 += 16) {
+                                    uint32_t v[16];
+#pragma unroll
+                                    for (unsigned k = 0; k < 16; ++k) {
+                                        const uint32_t j = j0 + k;
+                                        const uint32_t ej = from + (c + j) * kLanes;
+                                        v[k] = 0;
+                                        if (j < cnt) {
+                                            if (ej < staged) {
+                                                v[k] = stage[(kRowSums + ej) * 64 + lane];
+                                            } else {
+                                                uint64_t src;
+                                                uint32_t len;
+                                                lane_term(ev, j, src, len);
+                                                if (tileBase < len)
+                                                    v[k] = term_load(src, len, p);
+                                            }
+                                        }
+                                    }
+#pragma unroll
+                                    for (unsigned k = 0; k < 16; ++k) {
+                                        const uint32_t j = j0 + k;
+                                        if (j < cnt) {
+                                            if (us == 0) {
+                                                acc ^= v[k];
+                                            } else {
+                                                const GfTab t{rl(tab.a0, j), rl(tab.a1, j), rl(tab.b0, j),
+                                                              rl(tab.b1, j), rl(tab.c, j)};
+                                                acc ^= gf_mul_tab(v[k], t);
+                                            }
+                                        }
+                                    }
+                                }
+                            }
+                            atomicXor(&updAcc[u * 64 + lane], acc);
+                        }
+                        if (tileBase == 0)
+                            acct_wave(&acctL, refBytes);
+                    }
+                    if (wave == 0)
+                        PHASE_ADD(19, PHASE_CLK() - uclk0);
+                } else {
+                    [[maybe_unused]] const unsigned long long pclk0 = PHASE_CLK();
+                    const uint32_t h = lane >> 5, hl = lane & 31u;
+                    const uint32_t r = 2 * (unit - uUnits) + h;
+                    const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);   // (own write)
                     const bool act = info.x != kNoPlan;
                     if (!__any(act ? 1 : 0))
                         continue;
@@ -800,150 +950,59 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         rowInfo[r].x = kPlanGeneral;
                         generalRows = 1;
                     }
+                    if (wave == 0)
+                        PHASE_ADD(20, PHASE_CLK() - pclk0);
                 }
-            };
-            for (uint32_t e0 = tid / 16, first = 1; first || e0 < staged; e0 += 4 * kPass) {
-                uint4 v[4];
-#pragma unroll
-                for (unsigned u = 0; u < 4; ++u) {
-                    const uint32_t e = e0 + u * kPass;
-                    v[u] = make_uint4(0, 0, 0, 0);
-                    if (e < staged) {
-                        const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
-                        const uint64_t src = ((uint64_t)d.y << 32) | d.x;
-                        if (tileBase + q16 < d.z)
-                            v[u] = ld16(src + tileBase + q16);
-                    }
-                }
-                if (first) {
-                    first = 0;
-                    if (SGPU_PLAN_OVERLAP)
-                        build_plan();
-                }
-#pragma unroll
-                for (unsigned u = 0; u < 4; ++u) {
-                    const uint32_t e = e0 + u * kPass;
-                    if (e < staged)
-                        *reinterpret_cast<uint4*>(&stage[(kRowSums + e) * 64 + q16 / 4]) = v[u];
-                }
-            }
-            if (!SGPU_PLAN_OVERLAP)
-                build_plan();
-            __syncthreads();
-            PHASE_MARK(1, tclk);
-
-            // phase A: lane-sum updates (SiameseEncoder.cpp:359-418,
-            // SiameseDecoder.cpp:1680-1739): element e = from, from+8, ... < to,
-            // coefficient 1, CX or CX^2 of its column.  Each update's elements
-            // are split into Q parts (U*Q ~ 3 units per wave) whose partial
-            // sums meet in LDS accumulators (XOR atomics); wave u then stores
-            // update u.  Lane j holds element j's descriptor (reference source
-            // bytes counted per lane) and its coefficient's multiply table,
-            // moved to scalars with readlane; the element reads of 16 elements
-            // go out back to back.
-            const uint32_t Q = U == 0 ? 1u
-                               : SGPU_UPD_SPLIT ? (SGPU_UPD_SPLIT * kExecWaves + U - 1) / U
-                                                : (U >= kExecWaves ? 1u : kExecWaves / U);
-            const uint32_t uUnits = U * Q;
-            // the update this wave stores: its dst as kept, fetched now
-            uint64_t sdst = 0;
-            uint32_t sn = 0, svalid = 0, scur = 0;
-            if (wave < U) {
-                const uint4 w0 = table_entry(tableL, seg, blk, updWord + wave * kUpdateWords - kOpWords);
-                sdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                sn = uni(w0.z);
-                svalid = uni(w0.w) & 0x3fffffffu;
-                if (tileBase < align16u(sn))
-                    scur = load_cur(p, sdst, sn, svalid);
-            }
-            for (uint32_t unit = wave; unit < uUnits; unit += kExecWaves) {
-                [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
-                const uint32_t u = unit / Q;
-                const uint32_t uq = unit % Q;
-                const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
-                const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords);
-                const uint32_t un = uni(w0.z), us = uni(w0.w) >> 30;
-                const uint32_t from = uni(w1.x), to = uni(w1.y);
-                const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
-                const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
-                if (tileBase < align16u(un) && k0 < k1) {
-                    uint32_t acc = 0;
-                    uint32_t refBytes = 0;   // this lane's elements (one add/muladd per original)
-                    for (uint32_t c = k0; c < k1; c += 64) {
-                        const uint32_t e = from + (c + lane) * kLanes;
-                        const uint4 ev = c + lane < k1 ? table_entry(tableL, seg, blk, kRowSums + e)
-                                                       : make_uint4(0, 0, 0, 0);
-                        const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
-                        const GfTab tab = gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8));
-                        refBytes += ev.z;
-                        const uint32_t cnt = k1 - c < 64 ? k1 - c : 64;
-                        for (uint32_t j0 = 0; j0 < cnt; j0 += 16) {
-                            uint32_t v[16];
-#pragma unroll
-                            for (unsigned k = 0; k < 16; ++k) {
-                                const uint32_t j = j0 + k;
-                                const uint32_t ej = from + (c + j) * kLanes;
-                                v[k] = 0;
-                                if (j < cnt) {
-                                    if (ej < staged) {
-                                        v[k] = stage[(kRowSums + ej) * 64 + lane];
-                                    } else {
-                                        uint64_t src;
-                                        uint32_t len;
-                                        lane_term(ev, j, src, len);
-                                        if (tileBase < len)
-                                            v[k] = term_load(src, len, p);
-                                    }
-                                }
-                            }
-#pragma unroll
-                            for (unsigned k = 0; k < 16; ++k) {
-                                const uint32_t j = j0 + k;
-                                if (j < cnt) {
-                                    if (us == 0) {
-                                        acc ^= v[k];
-                                    } else {
-                                        const GfTab t{rl(tab.a0, j), rl(tab.a1, j), rl(tab.b0, j),
-                                                      rl(tab.b1, j), rl(tab.c, j)};
-                                        acc ^= gf_mul_tab(v[k], t);
-                                    }
-                                }
-                            }
-                        }
-                    }
-                    if (tileBase == 0)
-                        acct_wave(&acctL, refBytes);
-                    atomicXor(&updAcc[u * 64 + lane], acc);
-                }
-                if (wave == 0)
-                    PHASE_ADD(19, PHASE_CLK() - uclk0);
-            }
-            __syncthreads();
-            if (wave < U && tileBase < align16u(sn))
-                store_item(updAcc[wave * 64 + lane], p, sdst, sn, svalid, scur);
-            for (uint32_t u = wave + kExecWaves; u < U; u += kExecWaves) {
-                const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
-                const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                const uint32_t un = uni(w0.z), uvalid = uni(w0.w) & 0x3fffffffu;
-                if (tileBase < align16u(un))
-                    store_item(updAcc[u * 64 + lane], p, udst, un, uvalid, load_cur(p, udst, un, uvalid));
             }
             __syncthreads();
             PHASE_MARK(2, tclk);
 
-            // stage the 24 lane sums as the rows read them (after the updates
-            // above: this workgroup's own stores, visible after the barrier)
-            if (sumsStaged && tid < kRowSums * 16) {
-                const uint32_t k = tid / 16;
-                const uint4 d = tableL[k];
-                const uint64_t src = ((uint64_t)d.y << 32) | d.x;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (tileBase + q16 < d.z)
-                    v = ld16(src + tileBase + q16);
-                *reinterpret_cast<uint4*>(&stage[k * 64 + q16 / 4]) = v;
+            // update stores.  Update u's sum (SumUpdate.sum = k)
+            // also refreshes stage slot k straight from registers when it is
+            // the buffer the rows read and the stored bytes cover the staged
+            // ones; anything else marks the stage stale and the sums are
+            // re-read from memory after a barrier.
+            for (uint32_t u = wave; u < U; u += kExecWaves) {
+                const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
+                const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords);
+                const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                const uint32_t un = uni(w0.z), uvalid = uni(w0.w) & 0x3fffffffu;
+                if (tileBase >= align16u(un))
+                    continue;   // (this tile of the sum is unchanged, as staged)
+                const uint32_t cu = u == wave ? scur : load_cur(p, udst, un, uvalid);
+                const uint32_t out = item_value(updAcc[u * 64 + lane], p, un, uvalid, cu);
+                if (p < align16u(un))
+                    st4(udst + p, out);
+                const uint32_t k = uni(w1.z);
+                bool direct = false;
+                if (k < kRowSums && sumsStaged) {
+                    const uint4 d = tableL[k];
+                    const uint64_t src = ((uint64_t)uni(d.y) << 32) | uni(d.x);
+                    const uint32_t len = uni(d.z);
+                    direct = src == udst && align16u(len) <= align16u(un);
+                    if (direct)
+                        stage[k * 64 + lane] = p < align16u(len) ? out : 0u;
+                }
+                if (!direct && nPairs && lane == 0)   // (no plan: no row reads the stage)
+                    sumsDirty = 1;
             }
-            PHASE_MARK(3, tclk);
             __syncthreads();
+            PHASE_MARK(3, tclk);
+            if (tid == 0)
+                PHASE_ADD(21, sumsDirty ? 1 : 0);
+            if (sumsStaged && uni(sumsDirty)) {
+                // (this workgroup's own stores, visible after the barrier)
+                if (tid < kRowSums * 16) {
+                    const uint32_t k = tid / 16;
+                    const uint4 d = tableL[k];
+                    const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+                    uint4 v = make_uint4(0, 0, 0, 0);
+                    if (tileBase + q16 < d.z)
+                        v = ld16(src + tileBase + q16);
+                    *reinterpret_cast<uint4*>(&stage[k * 64 + q16 / 4]) = v;
+                }
+                __syncthreads();
+            }
             PHASE_MARK(4, tclk);
 
             // phase B1a: planned rows, four per wave at a time: quad g of the

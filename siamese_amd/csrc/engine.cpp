@@ -402,6 +402,7 @@ void Program::rows_update(unsigned k, uint64_t dst, uint32_t n, uint32_t valid, 
     u.s = s;
     u.from = from;
     u.to = to < from ? from : to;
+    u.sum = k;   // (the executor refreshes that sum's stage slot from the update)
     b.updateOf[k] = (int)b.updates.size();
     b.updates.push_back(u);
     if (n > b.maxExtent)

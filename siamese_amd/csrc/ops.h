@@ -102,7 +102,8 @@ struct SumUpdate
     uint32_t s : 2;
     uint32_t from;
     uint32_t to;
-    uint32_t pad[2];
+    uint32_t sum;        // which of the 24 lane sums the rows read (lane*3+s) dst is
+    uint32_t pad;
 };
 
 /// One Siamese row: dst[0,n) = keep(dst,valid) ^ acc0 ^ mix*acc1 where

@@ -24,6 +24,6 @@ for k, nm in enumerate(names):
     print("  %-14s %10.0f clocks per op" % (nm, out[k] / ops))
 print("  rows detail (wave 0 quad tasks): descriptors %.0f, terms %.0f, stores %.0f clocks per op"
       % (out[13] / ops, out[14] / ops, out[15] / ops))
-print("  detail (wave 0): update unit %.0f, plan scan %.0f, plan draws %.0f clocks per op"
-      % (out[19] / ops, out[20] / ops, out[21] / ops))
+print("  detail (wave 0): update units %.0f, plan pairs %.0f clocks per op; stage re-read in %.1f%% of ops"
+      % (out[19] / ops, out[20] / ops, 100.0 * out[21] / ops))
 print("kernel: %d workgroups, %.0f clocks each" % (out[7], out[6] / max(1, out[7])))
