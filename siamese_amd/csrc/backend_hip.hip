@@ -575,9 +575,11 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
-    // window element e < stageCap (stageSlots x 64 dwords in all)
+    // window element e < stageCap; slot stageSlots: zeros ((stageSlots + 1)
+    // x 64 dwords in all)
     extern __shared__ __attribute__((aligned(16))) uint32_t stage[];
     const uint32_t stageCap = stageSlots > kRowSums ? stageSlots - kRowSums : 0;
+    const uint32_t zeroSlot = stageSlots;   // (one more slot, all zero, for masked reads)
     const ExecItem it = items[blockIdx.x];
     const uint4* seg = stream + it.streamBegin;
     const uint32_t words = it.streamWords;
@@ -597,6 +599,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         }
         if (tid == 0)
             acctL = 0;
+        if (stageSlots && tid < 64)
+            stage[zeroSlot * 64 + tid] = 0;
         if (tid < 256) {
             permL[tid] = make_uint4(c_perm[tid][0], c_perm[tid][1], c_perm[tid][2], c_perm[tid][3]);
             permC[tid] = c_perm[tid][4];
@@ -811,25 +815,33 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     if (tileBase < align16u(un) && k0 < k1) {
                         uint32_t refBytes = 0;   // reference source bytes (one add/muladd per original)
                         if (from + (k1 - 1) * kLanes < staged) {
-                            // quad layout, two elements per quad in flight
+                            // quad layout, four elements per quad in flight
+                            // (elements past the range read the zero slot)
                             uint4 a = make_uint4(0, 0, 0, 0);
-                            for (uint32_t kk = k0; kk < k1; kk += 8) {
-                                uint4 v[2];
+                            for (uint32_t kk = k0; kk < k1; kk += 16) {
+                                uint32_t slot[4], y[4];
 #pragma unroll
-                                for (unsigned j = 0; j < 2; ++j) {
+                                for (unsigned j = 0; j < 4; ++j) {
                                     const uint32_t k = kk + 4 * j + g;
                                     const bool act = k < k1;
                                     const uint32_t e = from + (act ? k : k0) * kLanes;
                                     const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
                                     if (act && (lane & 15u) == 0)
                                         refBytes += ev.z;
-                                    v[j] = and16(lds16(stage, (kRowSums + e) * 64 + b4), act ? ~0u : 0u);
-                                    if (us != 0) {
-                                        const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
-                                        v[j] = gf_mul16_tab(v[j], gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8)));
-                                    }
+                                    slot[j] = act ? kRowSums + e : zeroSlot;
+                                    const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
+                                    y[j] = us == 1 ? (cx & 0xff) : (cx >> 8);
                                 }
-                                a = xor16(a, xor16(v[0], v[1]));
+                                uint4 v[4];
+#pragma unroll
+                                for (unsigned j = 0; j < 4; ++j)
+                                    v[j] = lds16(stage, slot[j] * 64 + b4);
+                                if (us != 0) {
+#pragma unroll
+                                    for (unsigned j = 0; j < 4; ++j)
+                                        v[j] = gf_mul16_tab(v[j], gf_tab_l(permL, permC, y[j]));
+                                }
+                                a = xor16(xor16(a, xor16(v[0], v[1])), xor16(v[2], v[3]));
                             }
                             atomicXor(&updAcc[u * 64 + b4 + 0], a.x);
                             atomicXor(&updAcc[u * 64 + b4 + 1], a.y);
@@ -973,17 +985,23 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 const uint32_t out = item_value(updAcc[u * 64 + lane], p, un, uvalid, cu);
                 if (p < align16u(un))
                     st4(udst + p, out);
+                // (slot k holds the buffer the rows read as sum k; an update of
+                // another buffer -- the rows of this batch do not read the sum,
+                // it grew after they took their table -- leaves it as staged)
                 const uint32_t k = uni(w1.z);
-                bool direct = false;
+                bool stale = k >= kRowSums;
                 if (k < kRowSums && sumsStaged) {
                     const uint4 d = tableL[k];
                     const uint64_t src = ((uint64_t)uni(d.y) << 32) | uni(d.x);
                     const uint32_t len = uni(d.z);
-                    direct = src == udst && align16u(len) <= align16u(un);
-                    if (direct)
-                        stage[k * 64 + lane] = p < align16u(len) ? out : 0u;
+                    if (src == udst) {
+                        if (align16u(len) <= align16u(un))
+                            stage[k * 64 + lane] = p < align16u(len) ? out : 0u;
+                        else
+                            stale = true;
+                    }
                 }
-                if (!direct && nPairs && lane == 0)   // (no plan: no row reads the stage)
+                if (stale && nPairs && lane == 0)   // (no plan: no row reads the stage)
                     sumsDirty = 1;
             }
             __syncthreads();
@@ -1045,33 +1063,34 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     // 16 terms at a time: lane i of a quad reads plan entry
                     // t+i of its row's lists, a row broadcast (DPP) hands
                     // entry j to the whole quad, 4 terms of each list in flight
+                    // (no masking after the reads, so they go out together)
                     for (uint32_t t = 0; t < most; t += 16) {
                         const uint32_t i = t + (lane & 15u);
-                        const uint32_t s0 = i < n0 ? (uint32_t)plan[off0 + i] : 0u;
-                        const uint32_t s1 = i < n1 ? (uint32_t)plan[off1 + i] : 0u;
-                        const uint32_t rem0 = n0 > t ? n0 - t : 0u, rem1 = n1 > t ? n1 - t : 0u;
+                        // (entries past a list's end name the zero slot)
+                        const uint32_t s0 = i < n0 ? (uint32_t)plan[off0 + i] : zeroSlot;
+                        const uint32_t s1 = i < n1 ? (uint32_t)plan[off1 + i] : zeroSlot;
                         const uint32_t left = most - t;   // (uniform)
-                        uint4 v0[4], v1[4];
-    // (terms past a list's end read slot 0 and are masked off: a select
-    // between an LDS read and a constant would become a flat load)
-#define SGPU_QUAD_LOAD(J)                                                                                   \
-    v0[(J) & 3] = and16(lds16(stage, row_bcast<(J)>(s0) * 64 + b4), (J) < rem0 ? ~0u : 0u);              \
-    v1[(J) & 3] = and16(lds16(stage, row_bcast<(J)>(s1) * 64 + b4), (J) < rem1 ? ~0u : 0u);
-#define SGPU_QUAD_XOR()                                                                                     \
-    a0 = xor16(xor16(a0, xor16(v0[0], v0[1])), xor16(v0[2], v0[3]));                                      \
-    a1 = xor16(xor16(a1, xor16(v1[0], v1[1])), xor16(v1[2], v1[3]));
-                        SGPU_QUAD_LOAD(0) SGPU_QUAD_LOAD(1) SGPU_QUAD_LOAD(2) SGPU_QUAD_LOAD(3) SGPU_QUAD_XOR()
-                        if (left > 4) {
-                            SGPU_QUAD_LOAD(4) SGPU_QUAD_LOAD(5) SGPU_QUAD_LOAD(6) SGPU_QUAD_LOAD(7) SGPU_QUAD_XOR()
-                        }
-                        if (left > 8) {
-                            SGPU_QUAD_LOAD(8) SGPU_QUAD_LOAD(9) SGPU_QUAD_LOAD(10) SGPU_QUAD_LOAD(11) SGPU_QUAD_XOR()
-                        }
-                        if (left > 12) {
-                            SGPU_QUAD_LOAD(12) SGPU_QUAD_LOAD(13) SGPU_QUAD_LOAD(14) SGPU_QUAD_LOAD(15) SGPU_QUAD_XOR()
-                        }
-#undef SGPU_QUAD_LOAD
-#undef SGPU_QUAD_XOR
+#define SGPU_QUAD_GROUP(J)                                                                                  \
+    {                                                                                                       \
+        const uint4 x0 = lds16(stage, row_bcast<(J)>(s0) * 64 + b4);                                        \
+        const uint4 x1 = lds16(stage, row_bcast<(J) + 1>(s0) * 64 + b4);                                    \
+        const uint4 x2 = lds16(stage, row_bcast<(J) + 2>(s0) * 64 + b4);                                    \
+        const uint4 x3 = lds16(stage, row_bcast<(J) + 3>(s0) * 64 + b4);                                    \
+        const uint4 y0 = lds16(stage, row_bcast<(J)>(s1) * 64 + b4);                                        \
+        const uint4 y1 = lds16(stage, row_bcast<(J) + 1>(s1) * 64 + b4);                                    \
+        const uint4 y2 = lds16(stage, row_bcast<(J) + 2>(s1) * 64 + b4);                                    \
+        const uint4 y3 = lds16(stage, row_bcast<(J) + 3>(s1) * 64 + b4);                                    \
+        a0 = xor16(xor16(a0, xor16(x0, x1)), xor16(x2, x3));                                                \
+        a1 = xor16(xor16(a1, xor16(y0, y1)), xor16(y2, y3));                                                \
+    }
+                        SGPU_QUAD_GROUP(0)
+                        if (left > 4)
+                            SGPU_QUAD_GROUP(4)
+                        if (left > 8)
+                            SGPU_QUAD_GROUP(8)
+                        if (left > 12)
+                            SGPU_QUAD_GROUP(12)
+#undef SGPU_QUAD_GROUP
                     }
                     PHASE_MARK(14, qclk);
                     if (live)
@@ -1812,13 +1831,14 @@ bool be_init(int device, const char** err)
         const size_t ldsPerCu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor
                                                                 : 160u * 1024u;
         const size_t dyn = ldsPerCu > staticLds ? ldsPerCu - staticLds : 0;
-        g_stageCap = dyn / kExecTileBytes > kRowSums ? (uint32_t)(dyn / kExecTileBytes) - kRowSums : 0;
+        // (the sums, the window and one zero slot)
+        g_stageCap = dyn / kExecTileBytes > kRowSums + 1 ? (uint32_t)(dyn / kExecTileBytes) - kRowSums - 1 : 0;
         if (const char* sc = std::getenv("SGPU_STAGE"))
             g_stageCap = std::min<uint32_t>(g_stageCap, (uint32_t)std::atoi(sc));
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exec),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)((kRowSums + g_stageCap) * kExecTileBytes)) != hipSuccess)
-            g_stageCap = 48u * 1024u / kExecTileBytes - kRowSums;
+                                (int)((kRowSums + g_stageCap + 1) * kExecTileBytes)) != hipSuccess)
+            g_stageCap = 48u * 1024u / kExecTileBytes - kRowSums - 1;
     }
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgG), pg, sizeof(pg)), "hipMemcpyToSymbol(pcgG)");
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_main),
@@ -1914,7 +1934,7 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
     uint32_t slots = 0;
     if (maxWindow != kNoRows)
         slots = kRowSums + (maxWindow < g_stageCap ? maxWindow : g_stageCap);
-    hipLaunchKernelGGL(k_exec, dim3(count), dim3(kExecThreads), (size_t)slots * kExecTileBytes,
+    hipLaunchKernelGGL(k_exec, dim3(count), dim3(kExecThreads), (size_t)(slots ? slots + 1 : 0) * kExecTileBytes,
                        g_stream, static_cast<const uint4*>(stream), items,
                        reinterpret_cast<unsigned long long*>(acct), slots);
 }
