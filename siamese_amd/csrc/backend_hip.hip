@@ -1388,7 +1388,11 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 // rows left unsolved (a corrupt length prefix) are stored at the end.  HBM
 // traffic is one read and one write of each row instead of ~m of each.
 //
-// Global path (larger m): wave 0 alone, rows updated in place in HBM.
+// Narrow LDS path (m > kSolveWideMaxRows): the same sweeps on 256-byte tiles
+// (solve_tile_narrow below), up to the 255-column limit.
+//
+// Global path (only when the device refuses the large dynamic-LDS grant):
+// wave 0 alone, rows updated in place in HBM.
 //
 // The staged rows take m KiB of LDS, so only one or two workgroups fit on a
 // CU.  Eight waves per workgroup measured best (A/B of 4/8/16: 16 waves put
@@ -1397,7 +1401,7 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 #define SGPU_SOLVE_WAVES 8
 #endif
 constexpr unsigned kSolveWaves = SGPU_SOLVE_WAVES;
-constexpr unsigned kSolveLdsMaxRows = 120;
+constexpr unsigned kSolveLdsMaxRows = 255;   // kMaximumLossRecoveryCount (SiameseCommon.h:80)
 
 // LDS bytes of the staged solve: row tiles, the transposed coefficient
 // matrix, per-row lengths and the result words.
@@ -1533,6 +1537,158 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
             st16(R[j].buf + p, X[j * 64 + lane]);
 }
 
+// Narrow LDS path (kSolveWideMaxRows < m <= 255): 256-byte tiles, so the m
+// row tiles (<= 64 KiB) and the m x m coefficients (<= 64 KiB) fit one
+// workgroup's LDS together.  A row tile is 16 lanes x 16 bytes: lane = 16 q
+// + c holds chunk c of one of four rows per wave (row slot 4 w + q, 32 slots
+// per workgroup), so each row update's multiplier differs per quad and comes
+// from the workgroup's LDS copy of the multiply tables.  Same sweeps, same
+// barriers and same stores as the 1 KiB path.
+__host__ __device__ constexpr uint32_t solve_narrow_lds_bytes(uint32_t m)
+{
+    return m * kSolveNarrowTileBytes + ((m * m + 15u) & ~15u) + 256u * 20u + m * 12u + (m + 1u) * 4u;
+}
+
+__device__ void solve_tile_narrow(uint4* __restrict__ X, uint32_t m, const SolveRow* __restrict__ R,
+                                  const uint8_t* __restrict__ C, const uint32_t* __restrict__ res,
+                                  uint32_t tileBase)
+{
+    constexpr uint32_t kChunks = kSolveNarrowTileBytes / 16;   // 16 lanes per row
+    constexpr uint32_t kSlots = kSolveWaves * (64 / kChunks);  // rows in flight per workgroup
+    const uint32_t tid = threadIdx.x;
+    const uint32_t c = tid & (kChunks - 1);
+    const uint32_t slot = tid / kChunks;
+    const uint32_t p = tileBase + c * 16;
+    uint4* permL = X + m * kChunks;                                  // c_perm words 0..3
+    uint32_t* permC = reinterpret_cast<uint32_t*>(permL + 256);      // c_perm word 4
+    uint8_t* Ct = reinterpret_cast<uint8_t*>(permC + 256);           // Ct[i*m + j] = C[j][i]
+    uint32_t* initB = reinterpret_cast<uint32_t*>(Ct + ((m * m + 15u) & ~15u));
+    uint32_t* lowL = initB + m;
+    uint32_t* finB = lowL + m;
+    uint32_t* rw = finB + m;
+
+    for (uint32_t y = tid; y < 256; y += 64 * kSolveWaves) {
+        const uint32_t* t = c_perm[y];
+        permL[y] = make_uint4(t[0], t[1], t[2], t[3]);
+        permC[y] = t[4];
+    }
+    for (uint32_t k = tid; k < m * m; k += 64 * kSolveWaves) {
+        const uint32_t j = k / m, i = k - j * m;
+        Ct[i * m + j] = C[k];
+    }
+    for (uint32_t j = tid; j < m; j += 64 * kSolveWaves) {
+        initB[j] = R[j].initBytes;
+        lowL[j] = R[j].lowerLen;
+        finB[j] = R[j].finalBytes;
+    }
+    for (uint32_t k = tid; k <= m; k += 64 * kSolveWaves)
+        rw[k] = res[k];
+    // row tiles, bytes past each row's initial length as zero; four loads
+    // in flight per lane
+    for (uint32_t j0 = slot; j0 < m; j0 += 4 * kSlots) {
+        uint4 v[4];
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+            const uint32_t j = j0 + u * kSlots;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (j < m) {
+                const uint32_t ib = R[j].initBytes;
+                if (p < ib) {
+                    v[u] = ld16(R[j].buf + p);
+                    if (p + 16 > ib)
+                        v[u] = mask16(v[u], (int)ib - (int)p);
+                }
+            }
+        }
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+            const uint32_t j = j0 + u * kSlots;
+            if (j < m)
+                X[j * kChunks + c] = v[u];
+        }
+    }
+    __syncthreads();
+
+    // MultiplyLowerTriangle in pivot order (reference SiameseDecoder.cpp:1065-1104)
+    for (uint32_t i = 0; i + 1 < m; ++i) {
+        const uint32_t L = uni(lowL[i]);
+        if (tileBase >= L)
+            continue;   // uniform: row i contributes nothing to this tile
+        uint4 src = X[i * kChunks + c];
+        if (p + 16 > L)
+            src = mask16(src, (int)L - (int)p);
+        const uint8_t* col = Ct + i * m;
+        const uint32_t first = i + 1 + ((slot + kSlots - (i + 1) % kSlots) % kSlots);
+        for (uint32_t j0 = first; j0 < m; j0 += 2 * kSlots) {
+            uint32_t y[2];
+            uint4 xr[2];
+#pragma unroll
+            for (unsigned u = 0; u < 2; ++u) {
+                const uint32_t j = j0 + u * kSlots;
+                y[u] = j < m ? col[j] : 0;
+                xr[u] = j < m ? X[j * kChunks + c] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (unsigned u = 0; u < 2; ++u) {
+                const uint32_t j = j0 + u * kSlots;
+                if (y[u])
+                    X[j * kChunks + c] = xor16(xr[u], gf_mul16_tab(src, gf_tab_l(permL, permC, y[u])));
+            }
+        }
+        __syncthreads();
+    }
+
+    // BackSubstitution from the right-most column (reference :1106-1238)
+    const uint32_t ok = uni(rw[0]);
+    uint32_t done = 0;
+    for (int i = (int)m - 1; i >= 0 && done < ok; --i, ++done) {
+        const uint32_t w = uni(rw[1 + i]);
+        const uint32_t bb = (w >> 29) + (w & kSolveLengthMask);
+        const uint8_t* col = Ct + (uint32_t)i * m;
+        uint4 x = gf_mul16(X[i * kChunks + c], c_inv[uni(col[i])]);
+        x = mask16(x, (int)bb - (int)p); // zero beyond the recovered length
+        if (slot == (uint32_t)i % kSlots && p < finB[i])
+            st16(R[i].buf + p, x);
+        if (tileBase < bb) {
+            for (uint32_t j0 = slot; j0 < (uint32_t)i; j0 += 2 * kSlots) {
+                uint32_t cj[2], fj[2];
+                uint4 xr[2];
+#pragma unroll
+                for (unsigned u = 0; u < 2; ++u) {
+                    const uint32_t j = j0 + u * kSlots;
+                    cj[u] = j < (uint32_t)i ? col[j] : 0;
+                    fj[u] = j < (uint32_t)i ? finB[j] : 0;
+                    xr[u] = j < (uint32_t)i ? X[j * kChunks + c] : make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (unsigned u = 0; u < 2; ++u) {
+                    if (!cj[u])
+                        continue;
+                    const uint32_t j = j0 + u * kSlots;
+                    const uint32_t ab = bb < fj[u] ? bb : fj[u];
+                    const uint4 xs = mask16(x, (int)ab - (int)p);
+                    X[j * kChunks + c] = xor16(xr[u], gf_mul16_tab(xs, gf_tab_l(permL, permC, cj[u])));
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // rows the back-substitution did not reach
+    for (uint32_t j = slot; j + done < m; j += kSlots)
+        if (p < finB[j])
+            st16(R[j].buf + p, X[j * kChunks + c]);
+}
+
+// bytes of dynamic LDS a solve launch needs for its largest m
+__host__ __device__ constexpr uint32_t solve_launch_lds_bytes(uint32_t maxRows)
+{
+    return maxRows > kSolveWideMaxRows
+               ? (solve_narrow_lds_bytes(maxRows) > solve_lds_bytes(kSolveWideMaxRows)
+                      ? solve_narrow_lds_bytes(maxRows)
+                      : solve_lds_bytes(kSolveWideMaxRows))
+               : solve_lds_bytes(maxRows);
+}
+
 __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const SolveDesc* __restrict__ solves, const SolveRow* __restrict__ rows,
     const uint8_t* __restrict__ coef, const uint32_t* __restrict__ results,
@@ -1545,14 +1701,20 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const SolveRow* R = rows + sd.rowBegin;
     const uint8_t* C = coef + sd.coefOffset;
     const uint32_t* res = results + sd.result;
-    if (m <= ldsRows) {
+    if (m <= ldsRows && m <= kSolveWideMaxRows) {
         solve_tile_lds(X, m, R, C, res, it.tileBase);
+        return;
+    }
+    if (m <= ldsRows) {
+        solve_tile_narrow(X, m, R, C, res, it.tileBase);
         return;
     }
     if (threadIdx.x >= 64)
         return;
+    // (the item's tile: 1 KiB, or 256 B for m > kSolveWideMaxRows)
+    const uint32_t tileEnd = it.tileBase + (m > kSolveWideMaxRows ? kSolveNarrowTileBytes : kTileBytes);
     const uint32_t p = it.tileBase + threadIdx.x * 16;
-    if (p >= sd.maxBytes)
+    if (p >= sd.maxBytes || p >= tileEnd)
         return;
 
     // Zero the region each row grows into (GrowZeroPadded) up front.
@@ -1637,7 +1799,8 @@ inline void bind_device()
 }
 bool g_timing = false;
 // largest m staged in LDS: 56 keeps solve_lds_bytes under the default 64 KiB
-// dynamic-LDS limit; raised at init when the device grants more
+// dynamic-LDS limit; raised at init to 255 (1 KiB tiles up to m = 120,
+// 256-byte tiles above) when the device grants ~140 KiB
 uint32_t g_solveLdsRows = 56;
 // window elements an OP_ROWS batch stages in LDS per tile (256 B each, beside
 // the 24 sums); sized at init to the LDS the kernel's static arrays leave
@@ -1843,7 +2006,7 @@ bool be_init(int device, const char** err)
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgG), pg, sizeof(pg)), "hipMemcpyToSymbol(pcgG)");
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_main),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)solve_lds_bytes(kSolveLdsMaxRows)) == hipSuccess)
+                            (int)solve_launch_lds_bytes(kSolveLdsMaxRows)) == hipSuccess)
         g_solveLdsRows = kSolveLdsMaxRows;
     if (hipDeviceSynchronize() != hipSuccess) {
         *err = "device synchronisation failed during init";
@@ -1956,7 +2119,7 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
     Timed t(false);
     const uint32_t ldsRows = maxRows < g_solveLdsRows ? maxRows : g_solveLdsRows;
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
-                       (size_t)solve_lds_bytes(ldsRows), g_stream, solves, rows, coef, results, items,
+                       (size_t)solve_launch_lds_bytes(ldsRows), g_stream, solves, rows, coef, results, items,
                        ldsRows);
 }
 

@@ -1068,7 +1068,8 @@ void Engine::assemble_batch(Batch& bt)
                 const uint32_t sidx = (uint32_t)sdescs.size();
                 sdescs.push_back(d);
                 sv.maxRows = std::max(sv.maxRows, d.m);
-                for (uint32_t t = 0; t < d.maxBytes; t += kTileBytes)
+                const uint32_t tb = solve_tile_bytes(d.m);
+                for (uint32_t t = 0; t < d.maxBytes; t += tb)
                     sitems.push_back(SolveItem{sidx, t});
             }
 #if SGPU_EXEC_LPT

@@ -214,6 +214,15 @@ struct IngestDesc
 };
 
 constexpr unsigned kTileBytes = 1024;       // solve tiles: 64 lanes x 16 bytes
+/// Solves with more rows than this stage 256-byte tiles (16 lanes x 16 bytes
+/// per row, four rows per wave) so all m <= 255 rows and the m x m
+/// coefficients still fit one workgroup's LDS.
+constexpr unsigned kSolveWideMaxRows = 120;
+constexpr unsigned kSolveNarrowTileBytes = 256;
+inline unsigned solve_tile_bytes(uint32_t m)
+{
+    return m > kSolveWideMaxRows ? kSolveNarrowTileBytes : kTileBytes;
+}
 constexpr uint32_t kNoRows = 0xffffffffu;   // be_launch_exec: no OP_ROWS in the launch
 constexpr unsigned kExecTileBytes = 256;    // executor tiles: 64 lanes x 4 bytes
 

@@ -389,12 +389,11 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
         const SolveRow* R = rows + sd.rowBegin;
         const uint8_t* C = coef + sd.coefOffset;
         const uint32_t* res = results + sd.result;
-        const uint32_t t0 = items[it].tileBase, t1 = t0 + kTileBytes;
+        const uint32_t t0 = items[it].tileBase, t1 = t0 + solve_tile_bytes(m);
         auto clip = [&](uint32_t v) { return v < t1 ? v : t1; };
         for (uint32_t j = 0; j < m; ++j)
             for (uint32_t b = (R[j].initBytes > t0 ? R[j].initBytes : t0); b < clip(R[j].finalBytes); ++b)
                 P(R[j].buf)[b] = 0;
-        std::vector<uint8_t> tmp(kTileBytes);
         for (uint32_t i = 0; i + 1 < m; ++i) {
             const uint32_t L = clip(R[i].lowerLen);
             if (t0 >= L)
