@@ -128,6 +128,10 @@ SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15);
 /// Device bytes the engine's symbol arena has taken from hipMalloc so far
 /// (grows while warming up, then stays flat: buffers are recycled).
 SIAMESE_EXPORT uint64_t sgpu_arena_bytes(void);
+/// Keep at least `bytes` of untouched arena memory in reserve (allocated now,
+/// counted in sgpu_arena_bytes), so later growth of the working set takes it
+/// instead of calling hipMalloc inside a latency-sensitive phase.
+SIAMESE_EXPORT int sgpu_arena_reserve(size_t bytes);
 
 #ifdef __cplusplus
 }

@@ -34,6 +34,9 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count);
 /// segments, kNoRows when none has a row batch (sizes the LDS stage).
 void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct,
                     uint32_t maxWindow);
+/// Wide rows' LDPC picks (ops.h LdpcItem), one workgroup per item; adds the
+/// reference's source bytes of the picks (min(len, n) each) to acct[0].
+void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct);
 /// `acct`: acct[0] += the reference's source bytes of each back-substitution
 /// step the solve completes (SiameseDecoder.cpp:1131-1212), acct[1] += the
 /// recovered bytes it outputs.
@@ -53,6 +56,22 @@ bool be_sync();
 /// completer thread waits for them.
 void* be_fence();
 bool be_fence_wait(void* fence);
+
+/// Transfer streams beside the codec stream (end-to-end packet flows).
+/// be_stage_h2d copies host -> device on the staging stream right away (the
+/// caller guarantees that no unfinished submission touches dst) and returns
+/// a mark; be_wait_mark makes the codec stream wait for it on the device
+/// (the host never blocks); be_mark_release recycles it once that wait has
+/// been queued.  Null mark: the copy could not be queued.
+void* be_stage_h2d(void* dst, const void* src, size_t bytes);
+void be_wait_mark(void* mark);
+void be_mark_release(void* mark);
+/// Gather on the gather stream: upload `count` ingest descriptors (from
+/// pinned descsHost to descsDev), pack their sources into devStage, copy
+/// `bytes` of it to hostOut, and wait for the gather stream only (not for
+/// in-flight codec work).  False on a device fault.
+bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, const void* devStage,
+               void* hostOut, size_t bytes);
 
 /// Device-time accounting: every executor/solve launch is bracketed with
 /// events; these return the accumulated milliseconds since the last reset.

@@ -558,6 +558,97 @@ __device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t
     return refBytes;
 }
 
+// k_ldpc: the LDPC picks of wide rows (ops.h LdpcItem), one workgroup of
+// kLdpcWaves waves per item = (row, 1 KiB tile, kLdpcPairsPerItem pairs).
+// Wave w takes a contiguous share of the item's draws: lane j generates draw
+// c + j (PCG jump-ahead, as the executor does) and loads that element's
+// descriptor, then the wave streams the elements' 16-byte lanes eight loads
+// at a time, even draws into a0 and odd into a1 (SiameseEncoder.cpp:
+// 1100-1144; the decoder's rows SiameseDecoder.cpp:996-1051 draw the same
+// way).  The waves meet in LDS and the tile is XORed into the row's zeroed
+// scratch pair with one atomic per dword: the items of one row are spread
+// over the whole chip instead of running inside the codec's one workgroup
+// per tile.
+constexpr unsigned kLdpcWaves = 4;
+constexpr unsigned kLdpcDepth = 8;
+
+__global__ __launch_bounds__(64 * kLdpcWaves) void k_ldpc(const LdpcItem* __restrict__ items,
+                                                          unsigned long long* __restrict__ acct)
+{
+    __shared__ uint4 part[kLdpcWaves][2][64];
+    const LdpcItem it = items[blockIdx.x];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uni(threadIdx.x >> 6);
+    const uint32_t p = it.tileBase + lane * 16u;
+    const uint32_t pairs = it.pair1 - it.pair0;
+    const uint32_t d0 = 2u * (it.pair0 + pairs * wave / kLdpcWaves);
+    const uint32_t d1 = 2u * (it.pair0 + pairs * (wave + 1) / kLdpcWaves);
+    const uint64_t inc = ((uint64_t)it.row << 1) | 1u;
+    uint64_t sc = pcg_jump((inc + it.N) * kPcgMul + inc, inc, d0);   // after Seed(), then d0 draws
+    const uint64_t pa = c_pcgA[lane], pg = c_pcgG[lane];
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    uint32_t refBytes = 0;
+    for (uint32_t c = d0; c < d1; c += 64) {
+        const uint64_t st = pa * sc + inc * pg;
+        sc = c_pcgA[64] * sc + inc * c_pcgG[64];
+        const uint32_t cnt = d1 - c < 64 ? d1 - c : 64;   // (uniform)
+        const uint32_t e = it.off + pcg_output(st) % it.N;
+        const uint4 ev = lane < cnt ? ld16(it.win + (uint64_t)e * 16u) : make_uint4(0, 0, 0, 0);
+        refBytes += ev.z < it.n ? ev.z : it.n;
+        for (uint32_t j0 = 0; j0 < cnt; j0 += kLdpcDepth) {
+            uint4 v[kLdpcDepth];
+#pragma unroll
+            for (unsigned u = 0; u < kLdpcDepth; ++u) {
+                const uint32_t j = j0 + u;
+                v[u] = make_uint4(0, 0, 0, 0);
+                if (j < cnt) {
+                    const uint64_t src = ((uint64_t)rl(ev.y, j) << 32) | rl(ev.x, j);
+                    const uint32_t len = rl(ev.z, j);
+                    // (bytes in [len, align16(len)) are zero in memory)
+                    if (p < len)
+                        v[u] = ld16(src + p);
+                }
+            }
+#pragma unroll
+            for (unsigned u = 0; u < kLdpcDepth; u += 2) {
+                a0 = xor16(a0, v[u]);       // (c and j0 are even: draw parity = u's)
+                a1 = xor16(a1, v[u + 1]);
+            }
+        }
+    }
+    part[wave][0][lane] = a0;
+    part[wave][1][lane] = a1;
+    if (it.tileBase == 0) {
+        // the reference's source bytes of these draws, once per row (tile 0)
+        unsigned long long rb = refBytes;
+#pragma unroll
+        for (unsigned d = 32; d >= 1; d >>= 1)
+            rb += __shfl_xor(rb, d, 64);
+        if (lane == 0 && rb)
+            atomicAdd(acct, rb);
+    }
+    __syncthreads();
+    if (wave == 0) {
+        uint4 s0 = part[0][0][lane], s1 = part[0][1][lane];
+#pragma unroll
+        for (unsigned w = 1; w < kLdpcWaves; ++w) {
+            s0 = xor16(s0, part[w][0][lane]);
+            s1 = xor16(s1, part[w][1][lane]);
+        }
+        // (scratch tiles are whole: span is a multiple of the tile)
+        uint32_t* l0 = reinterpret_cast<uint32_t*>(it.dst + p);
+        uint32_t* l1 = reinterpret_cast<uint32_t*>(it.dst + it.span + p);
+        if (s0.x) atomicXor(l0 + 0, s0.x);
+        if (s0.y) atomicXor(l0 + 1, s0.y);
+        if (s0.z) atomicXor(l0 + 2, s0.z);
+        if (s0.w) atomicXor(l0 + 3, s0.w);
+        if (s1.x) atomicXor(l1 + 0, s1.x);
+        if (s1.y) atomicXor(l1 + 1, s1.y);
+        if (s1.z) atomicXor(l1 + 2, s1.z);
+        if (s1.w) atomicXor(l1 + 3, s1.w);
+    }
+}
+
 __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
                                                        const ExecItem* __restrict__ items,
                                                        unsigned long long* __restrict__ acct,
@@ -777,7 +868,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     uint32_t size = 0, n01 = 0;
                     if (r < planned) {
                         const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
-                        const uint32_t pairs = (w1.w + kPairRate - 1) / kPairRate;
+                        // (a wide row reads its two k_ldpc sums as one pair)
+                        const uint32_t pairs = (w1.x & kRowWide) ? 1u : (w1.w + kPairRate - 1) / kPairRate;
                         const uint32_t n0 = __builtin_popcount(w1.x & 0xffffffu) + pairs;
                         const uint32_t n1 = __builtin_popcount(w1.y & 0xffffffu) + pairs;
                         size = n0 + n1;
@@ -923,8 +1015,11 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         if (m1 >> hl & 1u)
                             plan[off1 + __builtin_popcount(m1 & below)] = (uint16_t)hl;
                     }
-                    // draws: even -> row list, odd -> product list
-                    const uint32_t D = N ? 2 * ((N + kPairRate - 1) / kPairRate) : 0u;
+                    // draws: even -> row list, odd -> product list; a wide
+                    // row's two "draws" are its k_ldpc sums L0 / L1 at
+                    // window entries woff, woff + 1 (counted by k_ldpc)
+                    const bool wide = act && (w1.x & kRowWide) != 0;
+                    const uint32_t D = N ? 2 * ((N + kPairRate - 1) / kPairRate) : (wide ? 2u : 0u);
                     uint32_t Dmax = max(D, (uint32_t)__shfl_xor(D, 32, 64));
                     Dmax = uni(Dmax);
                     bool general = false;
@@ -943,13 +1038,17 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         const uint64_t st = ja * sc + inc * jg;
                         sc = c_pcgA[32] * sc + inc * c_pcgG[32];
                         if (d < D) {
-                            const uint32_t x = pcg_output(st);
-                            const uint32_t qn = (uint32_t)((double)x * invN);
-                            int64_t rr = (int64_t)x - (int64_t)qn * N;
-                            rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
-                            const uint32_t e = woff + (uint32_t)rr;
+                            uint32_t e = woff + d;
+                            if (!wide) {
+                                const uint32_t x = pcg_output(st);
+                                const uint32_t qn = (uint32_t)((double)x * invN);
+                                int64_t rr = (int64_t)x - (int64_t)qn * N;
+                                rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
+                                e = woff + (uint32_t)rr;
+                            }
                             const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e).z;
-                            refBytes += len < rn ? len : rn;
+                            if (!wide)
+                                refBytes += len < rn ? len : rn;
                             general |= e >= staged;
                             const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
                             plan[at] = (uint16_t)(e < staged ? kRowSums + e : 0);
@@ -1096,7 +1195,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     if (live)
                         store_item16(xor16(a0, gf_mul16_tab(a1, tab)), p16, rdst, rn, rvalid, cur);
                     if (act) {
-                        store_literal(p16, rdst, rn, w1.x >> 24, w2.z, w2.w, 16);
+                        store_literal(p16, rdst, rn, row_lit_len(w1.x), w2.z, w2.w, 16);
                     }
                     PHASE_MARK(15, qclk);
                 }
@@ -1151,6 +1250,27 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     }
                     // sparse part: this unit's share of the 2*ceil(N/16) draws
                     // (pairs stay whole: even draw -> row, odd -> product)
+                    if ((m0 & kRowWide) && q == 0) {
+                        // a wide row's k_ldpc sums L0 -> acc0, L1 -> acc1
+#pragma unroll
+                        for (uint32_t k = 0; k < 2; ++k) {
+                            const uint32_t e = off + k;
+                            uint32_t v = 0;
+                            if (e < staged) {
+                                v = stage[(kRowSums + e) * 64 + lane];
+                            } else {
+                                const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
+                                const uint64_t src = ((uint64_t)uni(ev.y) << 32) | uni(ev.x);
+                                const uint32_t len = uni(ev.z);
+                                if (tileBase < len)
+                                    v = term_load(src, len, p);
+                            }
+                            if (k == 0)
+                                acc0 ^= v;
+                            else
+                                acc1 ^= v;
+                        }
+                    }
                     if (N != 0) {
                         const uint32_t pairs = (N + kPairRate - 1) / kPairRate;
                         const uint32_t d0 = 2 * (pairs * q / P), d1 = 2 * (pairs * (q + 1) / P);
@@ -1168,7 +1288,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     if (tileBase < align16u(rn))
                         store_item(acc0 ^ (mix > 1 ? gf_mul_tab(acc1, mixTab) : acc1), p, rdst, rn, rvalid, c0);
                     PHASE_MARK(14, rclk);
-                    store_literal(p, rdst, rn, m0 >> 24, uni(w2.z), uni(w2.w));
+                    store_literal(p, rdst, rn, row_lit_len(m0), uni(w2.z), uni(w2.w));
                     PHASE_MARK(15, rclk);
                 }
             }
@@ -1192,7 +1312,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         const uint32_t c0 = load_cur(p, rdst, rn, rvalid);
                         store_item(acc0 ^ (mix > 1 ? gf_mul_dword(acc1, mix) : acc1), p, rdst, rn, rvalid, c0);
                     }
-                    store_literal(p, rdst, rn, m0 >> 24, uni(w2.z), uni(w2.w));
+                    store_literal(p, rdst, rn, row_lit_len(m0), uni(w2.z), uni(w2.w));
                 }
             }
             PHASE_MARK(5, tclk);
@@ -1782,6 +1902,8 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
 namespace {
 
 hipStream_t g_stream = nullptr;
+hipStream_t g_stageStream = nullptr;    // application H2D staging (be_stage_h2d)
+hipStream_t g_gatherStream = nullptr;   // gathers of completed results (be_gather)
 bool g_ready = false;
 int g_device = 0;
 
@@ -1946,6 +2068,11 @@ bool be_init(int device, const char** err)
         *err = "hipStreamCreate failed";
         return false;
     }
+    if (hipStreamCreateWithFlags(&g_stageStream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&g_gatherStream, hipStreamNonBlocking) != hipSuccess) {
+        *err = "hipStreamCreate (transfer streams) failed";
+        return false;
+    }
     if (!gf_init()) {
         *err = "GF(256) table self-check failed";
         return false;
@@ -2102,6 +2229,15 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
                        reinterpret_cast<unsigned long long*>(acct), slots);
 }
 
+void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
+{
+    if (count == 0)
+        return;
+    Timed t(true);   // (part of the executor's work: counted as exec time)
+    hipLaunchKernelGGL(k_ldpc, dim3(count), dim3(64 * kLdpcWaves), 0, g_stream, items,
+                       reinterpret_cast<unsigned long long*>(acct));
+}
+
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
                             uint32_t* results, uint32_t count, uint64_t* acct)
 {
@@ -2121,6 +2257,61 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
                        (size_t)solve_launch_lds_bytes(ldsRows), g_stream, solves, rows, coef, results, items,
                        ldsRows);
+}
+
+void* be_stage_h2d(void* dst, const void* src, size_t bytes)
+{
+    bind_device();
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_evMu);
+        if (!g_fenceFree.empty()) {
+            e = g_fenceFree.back();
+            g_fenceFree.pop_back();
+        }
+    }
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g_stageStream) != hipSuccess ||
+        hipEventRecord(e, g_stageStream) != hipSuccess)
+        return nullptr;
+    return e;
+}
+
+void be_wait_mark(void* mark)
+{
+    bind_device();
+    if (mark)
+        check(hipStreamWaitEvent(g_stream, static_cast<hipEvent_t>(mark), 0), "hipStreamWaitEvent");
+}
+
+void be_mark_release(void* mark)
+{
+    if (!mark)
+        return;
+    std::lock_guard<std::mutex> g(g_evMu);
+    g_fenceFree.push_back(static_cast<hipEvent_t>(mark));
+}
+
+bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, const void* devStage,
+               void* hostOut, size_t bytes)
+{
+    bind_device();
+    if (count == 0)
+        return true;
+    if (hipMemcpyAsync(descsDev, descsHost, (size_t)count * sizeof(IngestDesc), hipMemcpyHostToDevice,
+                       g_gatherStream) != hipSuccess)
+        return false;
+    hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves), dim3(64 * kIngestWaves),
+                       0, g_gatherStream, static_cast<const IngestDesc*>(descsDev), count);
+    if (hipMemcpyAsync(hostOut, devStage, bytes, hipMemcpyDeviceToHost, g_gatherStream) != hipSuccess)
+        return false;
+    const hipError_t e = hipStreamSynchronize(g_gatherStream);
+    if (e != hipSuccess) {
+        check(e, "hipStreamSynchronize(gather)");
+        return false;
+    }
+    return true;
 }
 
 bool be_sync()

@@ -299,4 +299,11 @@ SIAMESE_EXPORT uint64_t sgpu_arena_bytes(void)
     return Engine::global()->arena_bytes();
 }
 
+SIAMESE_EXPORT int sgpu_arena_reserve(size_t bytes)
+{
+    if (!g_batchReady)
+        return -1;
+    return Engine::global()->reserve(bytes) ? 0 : -1;
+}
+
 } // extern "C"

@@ -2,6 +2,7 @@
 // engine.h).
 #include "engine.h"
 #include "backend.h"
+#include "codedef.h"
 #include "pool.h"
 
 #include <algorithm>
@@ -150,6 +151,27 @@ void ProgramBody::rows_close()
     if (!b.haveSums)
         std::memset(b.sums, 0, sizeof(b.sums));
     Segment& s = segs[nsegs - 1];
+    // wide rows: their LDPC picks run in k_ldpc (ops.h); the row reads the
+    // two results as window entries appended after the snapshot (for this
+    // block only: a batch opened with keepWindow continues the snapshot)
+    const size_t winKept = b.win.size();
+    for (RowItem& r : b.rows) {
+        if (r.ldpcN < kLdpcSplitMin)
+            continue;
+        const uint32_t entry = (uint32_t)b.win.size();
+        const uint32_t pairs = (r.ldpcN + kPairRate - 1) / kPairRate;
+        s.wide.push_back(Segment::Wide{(uint32_t)s.ops.size(), entry, r.n, r.row, r.ldpcN, r.ldpcOff});
+        s.wideItems += ((r.n + kLdpcTileBytes - 1) / kLdpcTileBytes) *
+                       ((pairs + kLdpcPairsPerItem - 1) / kLdpcPairsPerItem);
+        s.wideBytes += 2 * (uint64_t)((r.n + kLdpcTileBytes - 1) / kLdpcTileBytes * kLdpcTileBytes);
+        WinEntry z;
+        std::memset(&z, 0, sizeof(z));
+        b.win.push_back(z);   // (addresses patched at assembly)
+        b.win.push_back(z);
+        r.ldpcN = 0;
+        r.ldpcOff = entry;
+        r.mask0 |= kRowWide;
+    }
     const uint32_t E = (uint32_t)b.win.size();
     const uint32_t U = (uint32_t)b.updates.size();
     const uint32_t R = (uint32_t)b.rows.size();
@@ -173,6 +195,7 @@ void ProgramBody::rows_close()
     std::memcpy(w, b.updates.data(), (size_t)U * sizeof(SumUpdate));
     w += (size_t)U * sizeof(SumUpdate);
     std::memcpy(w, b.rows.data(), (size_t)R * sizeof(RowItem));
+    b.win.resize(winKept);
     s.rowsWords += words;
     if (b.maxExtent > s.maxExtent)
         s.maxExtent = b.maxExtent;
@@ -594,16 +617,39 @@ uint8_t* Engine::carve_region(size_t bytes)
         return (uint8_t*)be_dev_alloc(bytes);
     }
     if (chunks_.empty() || chunks_.back().used + bytes > chunks_.back().size) {
-        uint8_t* base = (uint8_t*)be_dev_alloc(kChunkBytes);
-        if (!base)
-            return nullptr;
-        arenaBytes_ += kChunkBytes;
-        chunks_.push_back(Chunk{base, kChunkBytes, 0});
+        if (!spare_.empty()) {
+            // a chunk reserved ahead (reserve()): no hipMalloc here
+            chunks_.push_back(spare_.back());
+            spare_.pop_back();
+        } else {
+            uint8_t* base = (uint8_t*)be_dev_alloc(kChunkBytes);
+            if (!base)
+                return nullptr;
+            arenaBytes_ += kChunkBytes;
+            chunks_.push_back(Chunk{base, kChunkBytes, 0});
+        }
     }
     Chunk& c = chunks_.back();
     uint8_t* p = c.base + c.used;
     c.used += bytes;
     return p;
+}
+
+bool Engine::reserve(size_t bytes)
+{
+    std::lock_guard<std::mutex> g(arenaMu_);
+    size_t have = 0;
+    for (const Chunk& c : spare_)
+        have += c.size;
+    while (have < bytes) {
+        uint8_t* base = (uint8_t*)be_dev_alloc(kChunkBytes);
+        if (!base)
+            return false;
+        arenaBytes_ += kChunkBytes;
+        spare_.push_back(Chunk{base, kChunkBytes, 0});
+        have += kChunkBytes;
+    }
+    return true;
 }
 
 // Refill shard s's empty list of class `cls`: a magazine of buffers a
@@ -730,6 +776,19 @@ void Engine::ensure_up(XferSet& x, size_t bytes)
     x.upCap = cap;
 }
 
+void Engine::ensure_wide(XferSet& x, size_t bytes)
+{
+    if (bytes <= x.wideCap)
+        return;
+    size_t cap = x.wideCap ? x.wideCap : (1u << 20);
+    while (cap < bytes)
+        cap *= 2;
+    if (x.wideDev)
+        be_dev_free(x.wideDev);
+    x.wideDev = (uint8_t*)be_dev_alloc(cap);
+    x.wideCap = cap;
+}
+
 void Engine::ensure_down(XferSet& x, size_t bytes)
 {
     if (bytes <= x.downCap)
@@ -767,12 +826,15 @@ struct Phase
     size_t itemBegin, itemCount;    // exec items or solve items
     size_t solveBegin, solveCount;  // solve descs (SOLVE)
     uint32_t maxRows;               // largest m among them (SOLVE); largest OP_ROWS window (EXEC)
+    size_t wideBegin = 0, wideCount = 0;   // k_ldpc items run before the exec launch (EXEC)
 };
 
 struct SegRef
 {
     const ProgramBody::Segment* seg;
     uint32_t wordBase, words, itemBase;
+    uint32_t wideBase = 0;          // first k_ldpc item of its wide rows
+    uint64_t wideOff = 0;           // their scratch (bytes into the set's wideDev)
 };
 
 } // namespace
@@ -787,7 +849,8 @@ struct Batch
     // layout (enqueue -> launcher)
     std::vector<Phase> phases;
     size_t upBytes = 0, nIngest = 0;
-    size_t oIngD = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0;
+    size_t oIngD = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
+    uint64_t wideBytes = 0;                // k_ldpc scratch to zero before the first exec launch
     uint32_t resultWords = 0;
     std::vector<const Shard::Download*> dls;
     EngineStats st;
@@ -802,6 +865,7 @@ struct Batch
         uint32_t bytes;
     };
     std::vector<Download> downloads;
+    std::vector<void*> marks;              // staged copies its device work waits for
 };
 
 namespace {
@@ -898,6 +962,10 @@ uint64_t Engine::enqueue()
     tl("enqueue", ticket);
     b->ticket = ticket;
     b->set = (unsigned)(ticket % kSets);
+    {
+        std::lock_guard<std::mutex> g(qMu_);
+        b->marks.swap(pendingMarks_);
+    }
     {
         // this ticket's transfer set must be free (its previous user done)
         std::unique_lock<std::mutex> lk(qMu_);
@@ -1010,7 +1078,8 @@ void Engine::assemble_batch(Batch& bt)
     std::vector<SolveRef> srefs;
     size_t nSolveRows = 0, nCoef = 0;
     std::vector<SolveItem> sitems;
-    size_t nOps = 0, nTerms = 0, nWords = 0, nItems = 0;
+    size_t nOps = 0, nTerms = 0, nWords = 0, nItems = 0, nWide = 0;
+    uint64_t wideBytes = 0;
     for (int g = 0; g < 2; ++g) {
         size_t maxSegs = 0;
         for (ProgramBody* p : bt.bodies[g])
@@ -1028,7 +1097,7 @@ void Engine::assemble_batch(Batch& bt)
                     if (op.kind == OP_ROWS)
                         ex.maxRows = ex.maxRows == kNoRows ? op.valid : std::max(ex.maxRows, op.valid);
                 const size_t words = kOpWords * s.ops.size() + s.terms.size() + s.rowsWords;
-                segs.push_back(SegRef{&s, (uint32_t)nWords, (uint32_t)words, (uint32_t)nItems});
+                segs.push_back(SegRef{&s, (uint32_t)nWords, (uint32_t)words, (uint32_t)nItems, 0, 0});
                 nOps += s.ops.size();
                 nTerms += s.terms.size();
                 nWords += words;
@@ -1049,6 +1118,17 @@ void Engine::assemble_batch(Batch& bt)
             }
 #endif
             ex.itemCount = nItems - ex.itemBegin;
+            ex.wideBegin = nWide;
+            for (size_t i = segBegin; i < segs.size(); ++i) {
+                const ProgramBody::Segment& s = *segs[i].seg;
+                if (s.wide.empty())
+                    continue;
+                segs[i].wideBase = (uint32_t)nWide;
+                segs[i].wideOff = wideBytes;
+                nWide += s.wideItems;
+                wideBytes += s.wideBytes;
+            }
+            ex.wideCount = nWide - ex.wideBegin;
             if (ex.itemCount)
                 phases.push_back(ex);
 
@@ -1113,9 +1193,14 @@ void Engine::assemble_batch(Batch& bt)
     off = align16(off + nCoef);
     bt.oSI = off;
     off = align16(off + sitems.size() * sizeof(SolveItem));
+    bt.oWide = off;
+    off = align16(off + nWide * sizeof(LdpcItem));
     bt.upBytes = off;
     if (bt.upBytes)
         ensure_up(xs, bt.upBytes);
+    bt.wideBytes = wideBytes;
+    if (wideBytes)
+        ensure_wide(xs, wideBytes);
 
     // ---- 3. copy into the pinned upload buffer -------------------------------
     uint8_t* up = xs.upHost;
@@ -1143,12 +1228,45 @@ void Engine::assemble_batch(Batch& bt)
                 const SegRef& r = segs[si];
                 const ProgramBody::Segment& s = *r.seg;
                 uint8_t* w = up + bt.oStream + (size_t)r.wordBase * 16;
-                for (const GfOp& op : s.ops) {
+                size_t wi = 0;                                      // next wide row
+                LdpcItem* wItem = (LdpcItem*)(up + bt.oWide) + r.wideBase;
+                uint64_t wOff = r.wideOff;
+                for (uint32_t oi = 0; oi < (uint32_t)s.ops.size(); ++oi) {
+                    const GfOp& op = s.ops[oi];
                     std::memcpy(w, &op, sizeof(GfOp));
                     w += sizeof(GfOp);
                     if (op.kind == OP_ROWS || op.kind == OP_COPIES) {
                         const size_t bytes = (size_t)op.termCount * 16;   // block (rows_close)
                         std::memcpy(w, s.rowsData.data() + (size_t)op.termBegin * 16, bytes);
+                        // wide rows of this batch: their scratch pair as the
+                        // appended window entries, and their k_ldpc items
+                        const uint64_t winDev = (uint64_t)(uintptr_t)(xs.upDev + (w - up)) + kRowSums * 16;
+                        for (; wi < s.wide.size() && s.wide[wi].op == oi; ++wi) {
+                            const ProgramBody::Segment::Wide& x = s.wide[wi];
+                            const uint32_t span = (x.n + kLdpcTileBytes - 1) / kLdpcTileBytes * kLdpcTileBytes;
+                            const uint64_t dst = (uint64_t)(uintptr_t)xs.wideDev + wOff;
+                            wOff += 2 * (uint64_t)span;
+                            WinEntry* e = reinterpret_cast<WinEntry*>(w + (size_t)(kRowSums + x.entry) * 16);
+                            e[0].src = dst;
+                            e[0].len = x.n;
+                            e[1].src = dst + span;
+                            e[1].len = x.n;
+                            const uint32_t pairs = (x.N + kPairRate - 1) / kPairRate;
+                            for (uint32_t t = 0; t < x.n; t += kLdpcTileBytes)
+                                for (uint32_t p0 = 0; p0 < pairs; p0 += kLdpcPairsPerItem) {
+                                    LdpcItem& it = *wItem++;
+                                    it.win = winDev;
+                                    it.dst = dst;
+                                    it.span = span;
+                                    it.n = x.n;
+                                    it.row = x.row;
+                                    it.N = x.N;
+                                    it.off = x.off;
+                                    it.tileBase = t;
+                                    it.pair0 = p0;
+                                    it.pair1 = std::min(pairs, p0 + kLdpcPairsPerItem);
+                                }
+                        }
                         w += bytes;
                     } else if (op.kind == OP_LINCOMB && op.termCount) {
                         const size_t bytes = (size_t)op.termCount * sizeof(GfTerm);
@@ -1213,6 +1331,12 @@ void Engine::launch_batch(Batch& bt)
 {
     XferSet& xs = sets_[bt.set];
     EngineStats& st = bt.st;
+    // originals the application staged on the transfer stream (stage_in)
+    for (void* m : bt.marks) {
+        be_wait_mark(m);
+        be_mark_release(m);
+    }
+    bt.marks.clear();
     if (bt.upBytes)
         be_h2d(xs.upDev, xs.upHost, bt.upBytes);
     if (bt.nIngest)
@@ -1220,8 +1344,13 @@ void Engine::launch_batch(Batch& bt)
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
     be_memset(acctDev, 0, 3 * sizeof(uint64_t));
+    if (bt.wideBytes)
+        be_memset(xs.wideDev, 0, bt.wideBytes);
     for (const Phase& ph : bt.phases) {
         if (ph.kind == Phase::EXEC) {
+            if (ph.wideCount)
+                be_launch_ldpc((const LdpcItem*)(xs.upDev + bt.oWide) + ph.wideBegin, (uint32_t)ph.wideCount,
+                               acctDev);
             be_launch_exec(xs.upDev + bt.oStream, (const ExecItem*)(xs.upDev + bt.oItems) + ph.itemBegin,
                            (uint32_t)ph.itemCount, acctDev, ph.maxRows);
             st.execLaunches++;
@@ -1345,6 +1474,65 @@ void Engine::complete_batch(Batch& bt)
     st.reclaimNs = now_ns() - t2;
     std::lock_guard<std::mutex> g(statsMu_);
     flushStats_.add(st);
+}
+
+bool Engine::stage_in(void* dst, const void* src, size_t bytes)
+{
+    if (failed())
+        return false;
+    void* m = be_stage_h2d(dst, src, bytes);
+    if (!m)
+        return false;
+    std::lock_guard<std::mutex> g(qMu_);
+    pendingMarks_.push_back(m);
+    return true;
+}
+
+bool Engine::gather_completed(unsigned count, const void* const* srcs, const unsigned* bytes,
+                              void* pinnedOut)
+{
+    if (failed())
+        return false;
+    if (count == 0)
+        return true;
+    std::lock_guard<std::mutex> g(gatherMu_);
+    const size_t upBytes = count * sizeof(IngestDesc);
+    size_t total = 0;
+    for (unsigned i = 0; i < count; ++i)
+        total = align16(total + bytes[i]);
+    auto grow = [](uint8_t*& h, uint8_t*& d, size_t& cap, size_t need, bool host) {
+        if (need <= cap)
+            return;
+        size_t c = cap ? cap : (1u << 20);
+        while (c < need)
+            c *= 2;
+        if (h)
+            be_host_free(h);
+        if (d)
+            be_dev_free(d);
+        h = host ? (uint8_t*)be_host_alloc(c) : nullptr;
+        d = (uint8_t*)be_dev_alloc(c);
+        cap = c;
+    };
+    uint8_t* noHost = nullptr;
+    grow(cUpHost_, cUpDev_, cUpCap_, upBytes, true);
+    grow(noHost, cDev_, cCap_, total, false);
+    if (!cUpHost_ || !cUpDev_ || !cDev_)
+        return false;
+    IngestDesc* descs = reinterpret_cast<IngestDesc*>(cUpHost_);
+    size_t off = 0;
+    for (unsigned i = 0; i < count; ++i) {
+        std::memset(&descs[i], 0, sizeof(IngestDesc));
+        descs[i].src = (uint64_t)(uintptr_t)srcs[i];
+        descs[i].bytes = bytes[i];
+        descs[i].dst = (uint64_t)(uintptr_t)cDev_ + off;
+        off = align16(off + bytes[i]);
+    }
+    if (!be_gather(descs, cUpDev_, count, cDev_, pinnedOut, total)) {
+        failed_.store(true, std::memory_order_relaxed);
+        return false;
+    }
+    return true;
 }
 
 bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut)

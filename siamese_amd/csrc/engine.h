@@ -63,6 +63,17 @@ struct ProgramBody
         std::vector<uint8_t> rowsData;   // closed OP_ROWS / OP_COPIES blocks (ops.h layout)
         uint32_t rowsWords = 0;          // stream words of those blocks (after headers)
         uint32_t maxExtent = 0;
+        /// Wide rows of the closed OP_ROWS blocks, whose LDPC picks k_ldpc
+        /// computes (ops.h LdpcItem): filled in at flush assembly.
+        struct Wide
+        {
+            uint32_t op;       // index into ops (the OP_ROWS header)
+            uint32_t entry;    // window index of its L0 entry (L1 follows)
+            uint32_t n, row, N, off;
+        };
+        std::vector<Wide> wide;
+        uint32_t wideItems = 0;          // k_ldpc items of those rows
+        uint64_t wideBytes = 0;          // scratch bytes of those rows
         void clear()
         {
             ops.clear();
@@ -70,6 +81,9 @@ struct ProgramBody
             rowsData.clear();
             rowsWords = 0;
             maxExtent = 0;
+            wide.clear();
+            wideItems = 0;
+            wideBytes = 0;
         }
     };
     /// The OP_ROWS batch under construction (always the segment's last op).
@@ -255,6 +269,10 @@ public:
     void release(DevBuf& b);               // recycled after the next flush completes
     uint64_t bytes_in_use() const;
     uint64_t arena_bytes() const { return arenaBytes_.load(std::memory_order_relaxed); }
+    /// Keep at least `bytes` of untouched arena chunks in reserve, so later
+    /// growth takes them instead of calling hipMalloc (an application calls
+    /// this before a latency-sensitive phase).  False if hipMalloc fails.
+    bool reserve(size_t bytes);
 
     /// Copy `bytes` of device memory to host memory once the next flush has
     /// executed; the data is in place after that flush has been waited for.
@@ -294,6 +312,15 @@ public:
     /// Copy device ranges into one host buffer right now (after completing
     /// every submission).  Queued, unsubmitted work is not touched.
     bool gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut);
+    /// Gather ranges written by COMPLETED submissions into pinned host memory
+    /// on the gather stream, without waiting for submissions in flight.
+    /// Range i lands at the 16-byte aligned running offset (see
+    /// sgpu_gather_completed).
+    bool gather_completed(unsigned count, const void* const* srcs, const unsigned* bytes, void* pinnedOut);
+    /// Host -> device copy on the staging stream, issued now; every later
+    /// submission's device work waits for it (the host does not).  The caller
+    /// guarantees that no unfinished submission touches dst.
+    bool stage_in(void* dst, const void* src, size_t bytes);
 
     /// Serialises the drop-in siamese.h entry points and the exclusive
     /// siamese_gpu.h calls.
@@ -345,6 +372,7 @@ private:
     };
     std::mutex arenaMu_;
     std::vector<Chunk> chunks_;
+    std::vector<Chunk> spare_;   // reserved ahead, not yet carved
     std::atomic<uint64_t> arenaBytes_{0};
     std::mutex depotMu_;
     std::vector<std::vector<std::vector<uint8_t*>>> depot_;   // [class] -> magazines
@@ -360,6 +388,8 @@ private:
     std::mutex qMu_;
     std::condition_variable launchCv_, completeCv_, doneCv_, setCv_;
     std::deque<Batch*> toLaunch_, toComplete_;
+    std::vector<void*> pendingMarks_;               // staged copies the next submission waits for (qMu_)
+    std::mutex gatherMu_;
     uint64_t doneTicket_ = 0;                       // every ticket <= this has completed
     bool stop_ = false;
     std::thread launcher_, completer_;
@@ -376,8 +406,11 @@ private:
         uint8_t* downDev = nullptr;   // device-side gather area for downloads + results
         size_t downCap = 0;
         uint64_t busyTicket = 0;      // submission using it (0: free)
+        uint8_t* wideDev = nullptr;   // k_ldpc scratch (zeroed per submission)
+        size_t wideCap = 0;
     } sets_[kSets];
     void ensure_up(XferSet& x, size_t bytes);
+    void ensure_wide(XferSet& x, size_t bytes);
     void ensure_down(XferSet& x, size_t bytes);
 
     // gather buffers (separate from the flush buffers)
@@ -387,6 +420,12 @@ private:
     uint8_t* gHost_ = nullptr;
     uint8_t* gDev_ = nullptr;
     size_t gCap_ = 0;
+    // gather_completed buffers (gatherMu_)
+    uint8_t* cUpHost_ = nullptr;
+    uint8_t* cUpDev_ = nullptr;
+    size_t cUpCap_ = 0;
+    uint8_t* cDev_ = nullptr;
+    size_t cCap_ = 0;
 };
 
 /// Per-host-thread engine state.  Only its owning thread touches it between

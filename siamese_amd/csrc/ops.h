@@ -116,7 +116,7 @@ struct RowItem
     uint64_t dst;
     uint32_t n;
     uint32_t valid;
-    uint32_t mask0;      // bits 0..23; bits 24..31: litLen
+    uint32_t mask0;      // bits 0..23; bits 24..30: litLen; bit 31: kRowWide
     uint32_t mask1;      // bits 0..23; bits 24..31: mix (RX)
     uint32_t row;
     uint32_t ldpcN;
@@ -124,12 +124,45 @@ struct RowItem
     uint32_t pad;
     uint8_t lit[8];
 };
+/// RowItem.mask0 bit 31: a wide row whose LDPC sums k_ldpc computed
+/// (LdpcItem): ldpcN = 0, and window entries ldpcOff / ldpcOff + 1 hold L0 /
+/// L1, added to acc0 / acc1 as two draws would be.
+constexpr uint32_t kRowWide = 1u << 31;
+inline constexpr uint32_t row_lit_len(uint32_t mask0) { return (mask0 >> 24) & 0x7fu; }
 static_assert(sizeof(WinEntry) == 16, "WinEntry layout");
 static_assert(sizeof(SumUpdate) == 32, "SumUpdate layout");
 static_assert(sizeof(RowItem) == 48, "RowItem layout");
 constexpr unsigned kRowSums = 24;                       // kLanes * kSums
 constexpr unsigned kUpdateWords = sizeof(SumUpdate) / 16;
 constexpr unsigned kRowWords = sizeof(RowItem) / 16;
+
+/// Wide rows (ldpcN >= kLdpcSplitMin): the O(window) LDPC part of a row is
+/// too much for the one workgroup per tile that runs the codec's op list, so
+/// k_ldpc computes it first, spread over the whole chip: item k covers pairs
+/// [pair0, pair1) of PCG.Seed(row, N) on one 1 KiB tile and XORs
+///   L0 = sum of the even draws' window elements  into dst[0, n)
+///   L1 = sum of the odd draws' window elements   into dst[span, span + n)
+/// (a zeroed scratch area; items of one row meet by atomic XOR).  The row in
+/// the OP_ROWS block then carries kRowWide, ldpcN = 0 and ldpcOff = the
+/// window index of two entries appended to the batch's window that name L0
+/// and L1, and adds them to acc0 and acc1 like two draws.  The same bytes
+/// meet in a different order, which GF(2^8) addition (XOR) does not see.
+struct LdpcItem
+{
+    uint64_t win;        // device address of the batch's window entry 0 (WinEntry[])
+    uint64_t dst;        // L0 at dst, L1 at dst + span
+    uint32_t span;
+    uint32_t n;          // row bytes
+    uint32_t row;
+    uint32_t N;          // PCG.Seed(row, N); element = off + draw % N
+    uint32_t off;
+    uint32_t tileBase;
+    uint32_t pair0, pair1;
+};
+static_assert(sizeof(LdpcItem) == 48, "LdpcItem layout");
+constexpr uint32_t kLdpcSplitMin = 512;      // ldpcN from which a row's picks go to k_ldpc
+constexpr uint32_t kLdpcPairsPerItem = 32;   // pairs per k_ldpc item
+constexpr uint32_t kLdpcTileBytes = 1024;    // k_ldpc tile: 64 lanes x 16 bytes
 
 /// OP_COPIES: n independent copies (the decoder taking in recovery packets,
 /// reference SiameseDecoder.cpp:437), one CopyItem word pair each after the

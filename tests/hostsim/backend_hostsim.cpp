@@ -224,6 +224,15 @@ void exec_tile(const uint8_t* stream, const ExecItem& it, uint64_t* acct)
                 if ((h.mask1 >> k & 1) && sums[k].len)
                     terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 1});
             }
+            if (h.mask0 & kRowWide) {
+                // L0 / L1 of a wide row (k_ldpc), as two draws
+                for (uint32_t i = 0; i < 2; ++i) {
+                    const WinEntry& x = win[h.ldpcOff + i];
+                    if (h.ldpcOff + i >= E)
+                        std::abort();
+                    terms.push_back(TileTerm{x.src, x.len, 1, (uint8_t)i});
+                }
+            }
             Pcg32 prng;
             prng.seed(h.row, h.ldpcN);
             const uint32_t pairs = (h.ldpcN + kPairRate - 1) / kPairRate;
@@ -237,7 +246,7 @@ void exec_tile(const uint8_t* stream, const ExecItem& it, uint64_t* acct)
                     *acct += win[e].len < h.n ? win[e].len : h.n;
             }
             lincomb_tile(h.dst, h.n, h.valid, h.mask1 >> 24, terms, t0);
-            literal_tile(h.dst, h.n, h.lit, h.mask0 >> 24, t0);
+            literal_tile(h.dst, h.n, h.lit, row_lit_len(h.mask0), t0);
         }
     }
 }
@@ -317,6 +326,29 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
         return;
     for (uint32_t i = 0; i < count; ++i)
         exec_tile(static_cast<const uint8_t*>(stream), items[i], acct);
+}
+
+void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
+{
+    if (noexec())
+        return;
+    for (uint32_t k = 0; k < count; ++k) {
+        const LdpcItem& it = items[k];
+        const WinEntry* win = reinterpret_cast<const WinEntry*>((uintptr_t)it.win);
+        Pcg32 prng;
+        prng.seed(it.row, it.N);
+        for (uint32_t d = 0; d < 2 * it.pair0; ++d)
+            (void)prng.next();
+        const uint32_t t1 = it.tileBase + kLdpcTileBytes;
+        for (uint32_t d = 2 * it.pair0; d < 2 * it.pair1; ++d) {
+            const WinEntry& x = win[it.off + prng.next() % it.N];
+            if (it.tileBase == 0)
+                *acct += x.len < it.n ? x.len : it.n;
+            uint8_t* dst = P(it.dst + ((d & 1) ? it.span : 0));
+            for (uint32_t b = it.tileBase; b < t1 && b < x.len; ++b)
+                dst[b] ^= P(x.src)[b];
+        }
+    }
 }
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
@@ -428,6 +460,22 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
             }
         }
     }
+}
+
+void* be_stage_h2d(void* dst, const void* src, size_t bytes)
+{
+    std::memcpy(dst, src, bytes);
+    return reinterpret_cast<void*>(1);
+}
+void be_wait_mark(void*) {}
+void be_mark_release(void*) {}
+bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, const void* devStage,
+               void* hostOut, size_t bytes)
+{
+    std::memcpy(descsDev, descsHost, (size_t)count * sizeof(IngestDesc));
+    be_launch_ingest(static_cast<const IngestDesc*>(descsDev), count);
+    std::memcpy(hostOut, devStage, bytes);
+    return true;
 }
 
 // HOSTSIM_FAIL_SYNC=N: the N-th be_sync (1-based) and every later one

@@ -71,6 +71,7 @@ void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, byt
 
 void be_launch_ingest(const IngestDesc*, uint32_t) {}
 void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*, uint32_t) {}
+void be_launch_ldpc(const LdpcItem*, uint32_t, uint64_t*) {}
 
 void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow*, const uint8_t*,
                             uint32_t* results, uint32_t count, uint64_t*)
@@ -87,6 +88,22 @@ void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow*, const uint
 void be_launch_solve_main(const SolveDesc*, const SolveRow*, const uint8_t*, const uint32_t*,
                           const SolveItem*, uint32_t, uint32_t)
 {
+}
+
+void* be_stage_h2d(void* dst, const void* src, size_t bytes)
+{
+    std::memcpy(dst, src, bytes);
+    return reinterpret_cast<void*>(1);
+}
+void be_wait_mark(void*) {}
+void be_mark_release(void*) {}
+bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, const void* devStage,
+               void* hostOut, size_t bytes)
+{
+    std::memcpy(descsDev, descsHost, (size_t)count * sizeof(IngestDesc));
+    (void)count;
+    std::memcpy(hostOut, devStage, bytes);
+    return true;
 }
 
 bool be_sync() { return true; }
