@@ -37,15 +37,15 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
 /// Wide rows' LDPC picks (ops.h LdpcItem), one workgroup per item; adds the
 /// reference's source bytes of the picks (min(len, n) each) to acct[0].
 void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct);
-/// `acct`: acct[0] += the reference's source bytes of each back-substitution
-/// step the solve completes (SiameseDecoder.cpp:1131-1212), acct[1] += the
-/// recovered bytes it outputs.
-void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                            uint32_t* results, uint32_t count, uint64_t* acct);
-/// maxRows: largest m among the solves this launch covers (sizes LDS staging).
-void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                          const uint32_t* results, const SolveItem* items, uint32_t count,
-                          uint32_t maxRows);
+/// The triangular solves (reference SiameseDecoder.cpp:1065-1238), one
+/// workgroup per SolveItem: every tile first solves bytes 0..3 of its rows
+/// to learn the recovered lengths, the tile-0 item writes them to `results`
+/// and adds acct[0] += the reference's source bytes of each
+/// back-substitution step the solve completes (:1131-1212), acct[1] += the
+/// recovered bytes it outputs.  maxRows: largest m among the solves (sizes
+/// the LDS staging).
+void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
+                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct);
 
 /// Block until all queued work has finished.  Returns false on a device fault.
 bool be_sync();

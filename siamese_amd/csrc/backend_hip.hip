@@ -21,6 +21,7 @@
 #include "gf.h"
 
 #include <cctype>
+#include <chrono>
 #include <cstdlib>
 #include <cstdio>
 #include <string>
@@ -513,10 +514,11 @@ __device__ __forceinline__ uint4 table_entry(const uint4* tableL, const uint4* _
 __device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t off, uint32_t d0,
                                               uint32_t d1, uint32_t rn, uint32_t tileBase, uint32_t p,
                                               uint32_t lane, uint64_t pcgA, uint64_t pcgG,
-                                              const uint32_t* stage, uint32_t staged,
+                                              const uint32_t* stage, uint32_t stageLo, uint32_t staged,
                                               const uint4* tableL, const uint4* __restrict__ seg,
                                               uint32_t blk, uint32_t& acc0, uint32_t& acc1)
-// (window element e < staged lives in stage slot kRowSums + e)
+// (window element e in [stageLo, stageLo + staged) lives in stage slot
+// kRowSums + e - stageLo)
 {
     const uint64_t inc = ((uint64_t)row << 1) | 1u;
     uint64_t sc = pcg_jump((inc + N) * kPcgMul + inc, inc, d0);   // state after Seed(), then d0 draws
@@ -540,8 +542,8 @@ __device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t
                     uint32_t len;
                     lane_term(ev, j, src, len);
                     refBytes += len < rn ? len : rn;
-                    if (ej < staged)
-                        v[u] = stage[(kRowSums + ej) * 64 + lane];
+                    if (ej - stageLo < staged)
+                        v[u] = stage[(kRowSums + ej - stageLo) * 64 + lane];
                     else if (tileBase < len)
                         v[u] = term_load(src, len, p);
                 }
@@ -788,7 +790,10 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             // t loads 16 bytes of entry t/16 per pass, four passes in flight;
             // bytes past an entry's length (absent elements: all of them)
             // read zero.
-            const uint32_t staged = E < stageCap ? E : stageCap;
+            // (the host points the stage at the elements the batch reads:
+            // GfOp.dst low word = stageLo, ops.h)
+            const uint32_t stageLo = uni(h0.x) < E ? uni(h0.x) : E;
+            const uint32_t staged = E - stageLo < stageCap ? E - stageLo : stageCap;
             const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
             const bool sumsStaged = stageSlots >= kRowSums;
             const uint32_t updWord = kOpWords + T;
@@ -810,7 +815,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         const uint32_t x = x0 + u * kPass;
                         v[u] = make_uint4(0, 0, 0, 0);
                         if (x < entries) {
-                            const uint4 d = table_entry(tableL, seg, blk, x);
+                            const uint4 d = table_entry(tableL, seg, blk, x < kRowSums ? x : x + stageLo);
                             const uint64_t src = ((uint64_t)d.y << 32) | d.x;
                             if (tileBase + q16 < d.z)
                                 v[u] = ld16(src + tileBase + q16);
@@ -906,7 +911,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
                     if (tileBase < align16u(un) && k0 < k1) {
                         uint32_t refBytes = 0;   // reference source bytes (one add/muladd per original)
-                        if (from + (k1 - 1) * kLanes < staged) {
+                        if (from + k0 * kLanes >= stageLo && from + (k1 - 1) * kLanes - stageLo < staged) {
                             // quad layout, four elements per quad in flight
                             // (elements past the range read the zero slot)
                             uint4 a = make_uint4(0, 0, 0, 0);
@@ -920,7 +925,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                     const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
                                     if (act && (lane & 15u) == 0)
                                         refBytes += ev.z;
-                                    slot[j] = act ? kRowSums + e : zeroSlot;
+                                    slot[j] = act ? kRowSums + e - stageLo : zeroSlot;
                                     const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
                                     y[j] = us == 1 ? (cx & 0xff) : (cx >> 8);
                                 }
@@ -957,8 +962,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                         const uint32_t ej = from + (c + j) * kLanes;
                                         v[k] = 0;
                                         if (j < cnt) {
-                                            if (ej < staged) {
-                                                v[k] = stage[(kRowSums + ej) * 64 + lane];
+                                            if (ej - stageLo < staged) {
+                                                v[k] = stage[(kRowSums + ej - stageLo) * 64 + lane];
                                             } else {
                                                 uint64_t src;
                                                 uint32_t len;
@@ -1049,9 +1054,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e).z;
                             if (!wide)
                                 refBytes += len < rn ? len : rn;
-                            general |= e >= staged;
+                            general |= e - stageLo >= staged;
                             const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
-                            plan[at] = (uint16_t)(e < staged ? kRowSums + e : 0);
+                            plan[at] = (uint16_t)(e - stageLo < staged ? kRowSums + e - stageLo : 0);
                         }
                     }
                     if (tileBase == 0)
@@ -1256,8 +1261,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         for (uint32_t k = 0; k < 2; ++k) {
                             const uint32_t e = off + k;
                             uint32_t v = 0;
-                            if (e < staged) {
-                                v = stage[(kRowSums + e) * 64 + lane];
+                            if (e - stageLo < staged) {
+                                v = stage[(kRowSums + e - stageLo) * 64 + lane];
                             } else {
                                 const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
                                 const uint64_t src = ((uint64_t)uni(ev.y) << 32) | uni(ev.x);
@@ -1275,7 +1280,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         const uint32_t pairs = (N + kPairRate - 1) / kPairRate;
                         const uint32_t d0 = 2 * (pairs * q / P), d1 = 2 * (pairs * (q + 1) / P);
                         const uint32_t refBytes = row_picks(row, N, off, d0, d1, rn, tileBase, p, lane,
-                                                            c_pcgA[opaque(lane)], c_pcgG[opaque(lane)], stage, staged, tableL, seg, blk, acc0, acc1);
+                                                            c_pcgA[opaque(lane)], c_pcgG[opaque(lane)], stage, stageLo, staged, tableL, seg, blk, acc0, acc1);
                         // (a planned row's draws were counted by its plan)
                         if (pinfo == kNoPlan && tileBase == 0 && lane == 0 && refBytes)
                             atomicAdd(&acctL, (unsigned long long)refBytes);
@@ -1411,48 +1416,50 @@ __device__ __forceinline__ int parse_prefix(uint32_t w, uint32_t avail, uint32_t
     return 4;
 }
 
-__global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict__ solves,
-                                                     const SolveRow* __restrict__ rows,
-                                                     const uint8_t* __restrict__ coef,
-                                                     uint32_t* __restrict__ results,
-                                                     unsigned long long* __restrict__ acct)
+// The solve's bytes 0..3 (the recovered length prefixes), by the first wave
+// of a k_solve_main workgroup while the others wait at the same barriers:
+// MultiplyLowerTriangle and BackSubstitution on one dword per row (reference
+// SiameseDecoder.cpp:1065-1238) give each row's header length and length, or
+// stop at the first corrupt prefix.  rw[0] = rows recovered from the right,
+// rw[1 + i] = (header << 29) | length.  Every tile of a solve computes the
+// same words (two dozen cycles per row pair against the tile's own sweeps)
+// from the rows' first 16 bytes as copied before the solve (SolveDesc.head),
+// so the solve needs no separate launch; the tile-0 workgroup publishes them
+// (`out`) with the byte counts: the diagonal scaling of max(32 clipped,
+// recovered) bytes and one muladd of min(recovered, row) bytes per earlier
+// row each completed step eliminates (:1131-1212).
+__device__ void solve_prefix_block(uint32_t m, const SolveRow* __restrict__ R, uint64_t head,
+                                   const uint8_t* __restrict__ C,
+                                   uint32_t* __restrict__ rw, uint32_t* __restrict__ P, uint32_t* __restrict__ sh,
+                                   uint32_t* __restrict__ out, unsigned long long* __restrict__ acct)
 {
-    __shared__ uint32_t P[256];
-    __shared__ uint32_t X;
-    __shared__ uint32_t bb;
-    __shared__ int stop;
-    const SolveDesc sd = solves[blockIdx.x];
-    const uint32_t m = sd.m;
-    const SolveRow* R = rows + sd.rowBegin;
-    const uint8_t* C = coef + sd.coefOffset;
-    uint32_t* out = results + sd.result;
-    const uint32_t lane = threadIdx.x;
-
-    for (uint32_t j = lane; j < m; j += 64)
-        P[j] = ld4_masked(R[j].buf, R[j].initBytes);
-    if (lane == 0)
-        stop = 0;
+    // sh[0] = X, sh[1] = bb, sh[2] = stop
+    const uint32_t tid = threadIdx.x;
+    const bool w0 = tid < 64;
+    const uint32_t lane = tid & 63u;
+    if (w0) {
+        for (uint32_t j = lane; j < m; j += 64)
+            P[j] = ld4_masked(head + (uint64_t)j * 16u, R[j].initBytes);   // (not R[j].buf: tile 0 may
+                                                                           // have stored the solved row)
+        if (lane == 0)
+            sh[2] = 0;
+    }
     __syncthreads();
-
-    // MultiplyLowerTriangle on bytes 0..3 (reference SiameseDecoder.cpp:1065-1104)
     for (uint32_t i = 0; i + 1 < m; ++i) {
-        const uint32_t src = P[i] & byte_mask((int)R[i].lowerLen);
-        for (uint32_t j = i + 1 + lane; j < m; j += 64) {
-            const uint32_t y = C[(size_t)j * m + i];
-            if (y)
-                P[j] ^= gf_mul_dword(src, y);
+        if (w0) {
+            const uint32_t src = P[i] & byte_mask((int)R[i].lowerLen);
+            for (uint32_t j = i + 1 + lane; j < m; j += 64) {
+                const uint32_t y = C[(size_t)j * m + i];
+                if (y)
+                    P[j] ^= gf_mul_dword(src, y);
+            }
         }
         __syncthreads();
     }
-
-    // BackSubstitution on bytes 0..3 (reference SiameseDecoder.cpp:1106-1238).
-    // Each completed step also counts the reference's source bytes: the
-    // diagonal scaling of max(32 clipped, recovered) bytes and one muladd of
-    // min(recovered, row) bytes per earlier row it eliminates (:1131-1212).
     uint32_t ok = 0;
     unsigned long long opAcc = 0, outAcc = 0;
     for (int i = (int)m - 1; i >= 0; --i) {
-        if (lane == 0) {
+        if (tid == 0) {
             const uint32_t fb = R[i].finalBytes;
             const uint32_t lc = fb < 32 ? fb : 32;
             const uint32_t y = C[(size_t)i * m + i];
@@ -1460,42 +1467,54 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
             uint32_t len = 0;
             const int h = parse_prefix(x, lc, &len);
             if (h < 1 || len == 0 || (uint32_t)h + len > fb) {
-                stop = 1;
+                sh[2] = 1;
             } else {
-                out[1 + i] = ((uint32_t)h << 29) | len;
-                bb = (uint32_t)h + len;
-                X = x & byte_mask((int)bb);
-                opAcc += lc > bb ? lc : bb;
-                outAcc += bb;
+                rw[1 + i] = ((uint32_t)h << 29) | len;
+                sh[1] = (uint32_t)h + len;
+                sh[0] = x & byte_mask((int)((uint32_t)h + len));
+                opAcc += lc > sh[1] ? lc : sh[1];
+                outAcc += sh[1];
             }
         }
         __syncthreads();
-        if (stop)
+        if (sh[2])
             break;
         ++ok;
-        const uint32_t xi = X, b = bb;
-        for (uint32_t j = lane; j < (uint32_t)i; j += 64) {
-            const uint32_t c = C[(size_t)j * m + i];
-            if (c) {
-                const uint32_t ab = b < R[j].finalBytes ? b : R[j].finalBytes;
-                P[j] ^= gf_mul_dword(xi & byte_mask((int)ab), c);
-                opAcc += ab;
+        if (w0) {
+            const uint32_t xi = sh[0], b = sh[1];
+            for (uint32_t j = lane; j < (uint32_t)i; j += 64) {
+                const uint32_t c = C[(size_t)j * m + i];
+                if (c) {
+                    const uint32_t ab = b < R[j].finalBytes ? b : R[j].finalBytes;
+                    P[j] ^= gf_mul_dword(xi & byte_mask((int)ab), c);
+                    opAcc += ab;
+                }
             }
         }
         __syncthreads();
     }
-    if (lane == 0)
-        out[0] = ok;
-    // one atomic per wave (per-lane global atomics serialise at one address)
-#pragma unroll
-    for (unsigned d = 32; d >= 1; d >>= 1) {
-        opAcc += __shfl_xor(opAcc, d, 64);
-        outAcc += __shfl_xor(outAcc, d, 64);
+    if (tid == 0)
+        rw[0] = ok;
+    if (w0) {
+        // rows not reached keep word 0 (as the host reads them)
+        for (uint32_t j = lane; j + ok < m; j += 64)
+            rw[1 + j] = 0;
     }
-    if (lane == 0 && opAcc)
-        atomicAdd(&acct[0], opAcc);
-    if (lane == 0 && outAcc)
-        atomicAdd(&acct[1], outAcc);
+    __syncthreads();
+    if (out && w0) {
+        for (uint32_t k = lane; k <= m; k += 64)
+            out[k] = rw[k];
+        // one atomic per wave (per-lane global atomics serialise at one address)
+#pragma unroll
+        for (unsigned d = 32; d >= 1; d >>= 1) {
+            opAcc += __shfl_xor(opAcc, d, 64);
+            outAcc += __shfl_xor(outAcc, d, 64);
+        }
+        if (lane == 0 && opAcc)
+            atomicAdd(&acct[0], opAcc);
+        if (lane == 0 && outAcc)
+            atomicAdd(&acct[1], outAcc);
+    }
 }
 
 // k_solve_main: one workgroup of kSolveWaves waves per (solve, 1 KiB tile).
@@ -1811,16 +1830,23 @@ __host__ __device__ constexpr uint32_t solve_launch_lds_bytes(uint32_t maxRows)
 
 __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const SolveDesc* __restrict__ solves, const SolveRow* __restrict__ rows,
-    const uint8_t* __restrict__ coef, const uint32_t* __restrict__ results,
-    const SolveItem* __restrict__ items, uint32_t ldsRows)
+    const uint8_t* __restrict__ coef, uint32_t* __restrict__ results,
+    const SolveItem* __restrict__ items, uint32_t ldsRows, unsigned long long* __restrict__ acct)
 {
     extern __shared__ uint4 X[];
+    __shared__ uint32_t rwS[kSolveLdsMaxRows + 1];   // the solve's result words (prefix pass)
+    __shared__ uint32_t prefP[kSolveLdsMaxRows + 1];
+    __shared__ uint32_t prefSh[4];
     const SolveItem it = items[blockIdx.x];
     const SolveDesc sd = solves[it.solve];
     const uint32_t m = sd.m;
     const SolveRow* R = rows + sd.rowBegin;
     const uint8_t* C = coef + sd.coefOffset;
-    const uint32_t* res = results + sd.result;
+    if (m > kSolveLdsMaxRows)
+        return;   // (the host never queues m > 255: kMaximumLossRecoveryCount)
+    solve_prefix_block(m, R, sd.head, C, rwS, prefP, prefSh, it.tileBase == 0 ? results + sd.result : nullptr,
+                       acct);
+    const uint32_t* res = rwS;
     if (m <= ldsRows && m <= kSolveWideMaxRows) {
         solve_tile_lds(X, m, R, C, res, it.tileBase);
         return;
@@ -2238,17 +2264,8 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
                        reinterpret_cast<unsigned long long*>(acct));
 }
 
-void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                            uint32_t* results, uint32_t count, uint64_t* acct)
-{
-    Timed t(false);
-    hipLaunchKernelGGL(k_solve_prefix, dim3(count), dim3(64), 0, g_stream, solves, rows, coef,
-                       results, reinterpret_cast<unsigned long long*>(acct));
-}
-
-void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
-                          const uint32_t* results, const SolveItem* items, uint32_t count,
-                          uint32_t maxRows)
+void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
+                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct)
 {
     if (count == 0)
         return;
@@ -2256,7 +2273,7 @@ void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const u
     const uint32_t ldsRows = maxRows < g_solveLdsRows ? maxRows : g_solveLdsRows;
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
                        (size_t)solve_launch_lds_bytes(ldsRows), g_stream, solves, rows, coef, results, items,
-                       ldsRows);
+                       ldsRows, reinterpret_cast<unsigned long long*>(acct));
 }
 
 void* be_stage_h2d(void* dst, const void* src, size_t bytes)
@@ -2350,7 +2367,23 @@ bool be_fence_wait(void* fence)
     if (!fence)
         return false;
     hipEvent_t e = static_cast<hipEvent_t>(fence);
-    const hipError_t r = hipEventSynchronize(e);
+    // Poll first: a blocking-sync wait sleeps until an interrupt wakes the
+    // thread, tens of microseconds a flush on the latency-bound single-stream
+    // path (C3); the completer is a dedicated thread, so it spins up to
+    // kFenceSpinUs before it sleeps.
+    constexpr int64_t kFenceSpinUs = 2000;
+    hipError_t r = hipEventQuery(e);
+    if (r == hipErrorNotReady) {
+        const auto t0 = std::chrono::steady_clock::now();
+        do {
+            __builtin_ia32_pause();
+            r = hipEventQuery(e);
+        } while (r == hipErrorNotReady &&
+                 std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0)
+                         .count() < kFenceSpinUs);
+    }
+    if (r == hipErrorNotReady)
+        r = hipEventSynchronize(e);
     if (r != hipSuccess) {
         check(r, "hipEventSynchronize");
         return false;

@@ -176,8 +176,18 @@ void ProgramBody::rows_close()
     const uint32_t U = (uint32_t)b.updates.size();
     const uint32_t R = (uint32_t)b.rows.size();
     const uint32_t words = kRowSums + E + U * kUpdateWords + R * kRowWords;
+    // the executor stages window elements from the first one the batch reads
+    // (updates, LDPC draws, wide rows' sums), not from the window's start
+    uint32_t stageLo = E;
+    for (const SumUpdate& u : b.updates)
+        if (u.to > u.from)
+            stageLo = std::min(stageLo, u.from);
+    for (const RowItem& r : b.rows)
+        if (r.ldpcN || (r.mask0 & kRowWide))
+            stageLo = std::min(stageLo, r.ldpcOff);
     GfOp op;
     std::memset(&op, 0, sizeof(op));
+    op.dst = stageLo;   // (OP_ROWS has no dst of its own)
     op.kind = OP_ROWS;
     op.n = R;
     op.valid = E;
@@ -352,8 +362,18 @@ uint32_t Program::solve(const std::vector<SolveRow>& rows, const uint8_t* coef, 
         b_->new_segment(); // the segment preceding this solve
     if (b_->nsolves == b_->solves.size())
         b_->solves.emplace_back();
+    // each row's first 16 bytes as the solve will find them, for the length
+    // prefix pass every tile of the solve runs (SolveDesc.head)
+    DevBuf head = eng_->alloc((uint32_t)rows.size() * 16u);
+    if (head) {
+        for (size_t i = 0; i < rows.size(); ++i)
+            copy(head.addr() + i * 16, rows[i].buf, std::min<uint32_t>(16u, rows[i].initBytes));
+        b_->rows_close();   // (seal the copy batch into this segment)
+    }
     ProgramBody::PendingSolve& ps = b_->solves[b_->nsolves++];
     std::memset(&ps.desc, 0, sizeof(ps.desc));
+    ps.desc.head = head.addr();
+    eng_->release(head);   // (reused only after this submission completes)
     ps.desc.m = (uint32_t)rows.size();
     ps.desc.maxBytes = maxBytes;
     ps.desc.result = b_->resultWords;
@@ -803,6 +823,8 @@ void Engine::ensure_down(XferSet& x, size_t bytes)
     x.downHost = (uint8_t*)be_host_alloc(cap);
     x.downDev = (uint8_t*)be_dev_alloc(cap);
     x.downCap = cap;
+    x.acctZero = true;
+    x.acctPrev[0] = x.acctPrev[1] = x.acctPrev[2] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -850,7 +872,8 @@ struct Batch
     std::vector<Phase> phases;
     size_t upBytes = 0, nIngest = 0;
     size_t oIngD = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
-    uint64_t wideBytes = 0;                // k_ldpc scratch to zero before the first exec launch
+    uint64_t wideBase = 0;                 // this submission's k_ldpc scratch: bytes into the ring
+    bool wideZero = false;                 // the ring wrapped: zero it before the first exec launch
     uint32_t resultWords = 0;
     std::vector<const Shard::Download*> dls;
     EngineStats st;
@@ -1148,9 +1171,12 @@ void Engine::assemble_batch(Batch& bt)
                 const uint32_t sidx = (uint32_t)sdescs.size();
                 sdescs.push_back(d);
                 sv.maxRows = std::max(sv.maxRows, d.m);
+                // (tile 0 always runs: it publishes the solve's result words)
                 const uint32_t tb = solve_tile_bytes(d.m);
-                for (uint32_t t = 0; t < d.maxBytes; t += tb)
+                uint32_t t = 0;
+                do
                     sitems.push_back(SolveItem{sidx, t});
+                while ((t += tb) < d.maxBytes);
             }
 #if SGPU_EXEC_LPT
             // largest solves first (the serial pivot chain grows with m)
@@ -1198,9 +1224,17 @@ void Engine::assemble_batch(Batch& bt)
     bt.upBytes = off;
     if (bt.upBytes)
         ensure_up(xs, bt.upBytes);
-    bt.wideBytes = wideBytes;
-    if (wideBytes)
-        ensure_wide(xs, wideBytes);
+    if (wideBytes) {
+        // k_ldpc scratch comes from the set's ring, which is zeroed as a whole
+        // when it wraps (not per submission: most flushes then need no memset)
+        if (xs.wideUsed + wideBytes > xs.wideCap) {
+            ensure_wide(xs, std::max<size_t>(wideBytes, 16u << 20));
+            xs.wideUsed = 0;
+            bt.wideZero = true;
+        }
+        bt.wideBase = xs.wideUsed;
+        xs.wideUsed += wideBytes;
+    }
 
     // ---- 3. copy into the pinned upload buffer -------------------------------
     uint8_t* up = xs.upHost;
@@ -1230,7 +1264,7 @@ void Engine::assemble_batch(Batch& bt)
                 uint8_t* w = up + bt.oStream + (size_t)r.wordBase * 16;
                 size_t wi = 0;                                      // next wide row
                 LdpcItem* wItem = (LdpcItem*)(up + bt.oWide) + r.wideBase;
-                uint64_t wOff = r.wideOff;
+                uint64_t wOff = bt.wideBase + r.wideOff;
                 for (uint32_t oi = 0; oi < (uint32_t)s.ops.size(); ++oi) {
                     const GfOp& op = s.ops[oi];
                     std::memcpy(w, &op, sizeof(GfOp));
@@ -1343,26 +1377,33 @@ void Engine::launch_batch(Batch& bt)
         be_launch_ingest((const IngestDesc*)(xs.upDev + bt.oIngD), (uint32_t)bt.nIngest);
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
-    be_memset(acctDev, 0, 3 * sizeof(uint64_t));
-    if (bt.wideBytes)
-        be_memset(xs.wideDev, 0, bt.wideBytes);
+    if (xs.acctZero) {
+        be_memset(acctDev, 0, 3 * sizeof(uint64_t));
+        xs.acctZero = false;
+    }
+    if (bt.wideZero)
+        be_memset(xs.wideDev, 0, xs.wideCap);
+    // k_ldpc items of every exec phase before the first solve go in one
+    // launch (they read only window elements that exist before the flush's
+    // first solve); a phase after a solve launches its own
+    size_t wideDone = 0;
+    for (size_t k = 0; k < bt.phases.size() && bt.phases[k].kind == Phase::EXEC; ++k)
+        wideDone = bt.phases[k].wideBegin + bt.phases[k].wideCount;
+    if (wideDone)
+        be_launch_ldpc((const LdpcItem*)(xs.upDev + bt.oWide), (uint32_t)wideDone, acctDev);
     for (const Phase& ph : bt.phases) {
         if (ph.kind == Phase::EXEC) {
-            if (ph.wideCount)
+            if (ph.wideCount && ph.wideBegin >= wideDone)
                 be_launch_ldpc((const LdpcItem*)(xs.upDev + bt.oWide) + ph.wideBegin, (uint32_t)ph.wideCount,
                                acctDev);
             be_launch_exec(xs.upDev + bt.oStream, (const ExecItem*)(xs.upDev + bt.oItems) + ph.itemBegin,
                            (uint32_t)ph.itemCount, acctDev, ph.maxRows);
             st.execLaunches++;
         } else {
-            const SolveDesc* sd = (const SolveDesc*)(xs.upDev + bt.oSD) + ph.solveBegin;
-            be_launch_solve_prefix(sd, (const SolveRow*)(xs.upDev + bt.oSR), xs.upDev + bt.oCoef,
-                                   resultsDev, (uint32_t)ph.solveCount, acctDev + 1);
             // solve items index solves globally; pass the global desc base
-            be_launch_solve_main((const SolveDesc*)(xs.upDev + bt.oSD),
-                                 (const SolveRow*)(xs.upDev + bt.oSR), xs.upDev + bt.oCoef, resultsDev,
-                                 (const SolveItem*)(xs.upDev + bt.oSI) + ph.itemBegin,
-                                 (uint32_t)ph.itemCount, ph.maxRows);
+            be_launch_solve((const SolveDesc*)(xs.upDev + bt.oSD), (const SolveRow*)(xs.upDev + bt.oSR),
+                            xs.upDev + bt.oCoef, resultsDev, (const SolveItem*)(xs.upDev + bt.oSI) + ph.itemBegin,
+                            (uint32_t)ph.itemCount, ph.maxRows, acctDev + 1);
         }
     }
     be_d2h(xs.downHost, xs.downDev, kAcctBytes + (size_t)bt.resultWords * 4);
@@ -1423,13 +1464,18 @@ void Engine::complete_batch(Batch& bt)
         flushStats_.add(st);
         return;
     }
-    const XferSet& xs = sets_[bt.set];
+    XferSet& xs = sets_[bt.set];
     for (const Batch::Download& d : bt.downloads)
         std::memcpy(d.host, xs.downHost + d.off, d.bytes);
     // bytes the kernels counted: terms the executor expanded itself, and the
-    // solves' back-substitution (source bytes, recovered bytes)
-    uint64_t acct[3];
-    std::memcpy(acct, xs.downHost, sizeof(acct));
+    // solves' back-substitution (source bytes, recovered bytes); the device
+    // counters of a transfer set only grow
+    uint64_t acct[3], cur[3];
+    std::memcpy(cur, xs.downHost, sizeof(cur));
+    for (int k = 0; k < 3; ++k) {
+        acct[k] = cur[k] - xs.acctPrev[k];
+        xs.acctPrev[k] = cur[k];
+    }
     st.refOpBytes += acct[0] + acct[1];
     st.outBytes += acct[2];
     st.solveBytes += acct[1] + acct[2];

@@ -406,8 +406,13 @@ private:
         uint8_t* downDev = nullptr;   // device-side gather area for downloads + results
         size_t downCap = 0;
         uint64_t busyTicket = 0;      // submission using it (0: free)
-        uint8_t* wideDev = nullptr;   // k_ldpc scratch (zeroed per submission)
+        uint8_t* wideDev = nullptr;   // k_ldpc scratch ring (see ensure_wide)
         size_t wideCap = 0;
+        size_t wideUsed = 0;          // bytes of the ring dirtied since it was zeroed
+        // the device byte counters at the head of downDev only grow (no
+        // memset per submission): each completion takes the difference
+        uint64_t acctPrev[3] = {0, 0, 0};
+        bool acctZero = false;        // fresh downDev: zero the counters first
     } sets_[kSets];
     void ensure_up(XferSet& x, size_t bytes);
     void ensure_wide(XferSet& x, size_t bytes);

@@ -77,7 +77,9 @@ constexpr unsigned kOpWords = sizeof(GfOp) / 16;
 /// host sends O(1) words per row instead of a term per source.
 ///
 /// Stream layout after the GfOp header (kind = OP_ROWS, n = rows R,
-/// valid = window entries E, mix = sum updates U, termCount = block words):
+/// valid = window entries E, mix = sum updates U, termCount = block words,
+/// dst = stageLo: the first window element the batch reads, where the
+/// executor's LDS stage of the window starts):
 ///   24 words   WinEntry of the lane sums as the rows read them (lane*3 + s)
 ///   E words    WinEntry of window elements [base, base+E): an absent
 ///              (lost) element has len 0 and contributes nothing
@@ -208,6 +210,10 @@ struct SolveDesc
     uint64_t coefOffset; // byte offset into coefficient array
     uint32_t result;     // index into the uint32 result array (m+1 words)
     uint32_t maxBytes;   // max finalBytes over rows (tile count)
+    uint64_t head;       // m x 16 bytes: each row's first 16 bytes as the solve
+                         // starts (copied by the segment before it), so every
+                         // tile can solve the length prefixes while tile 0
+                         // overwrites the rows
 };
 
 struct SolveRow

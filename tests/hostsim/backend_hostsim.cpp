@@ -351,7 +351,7 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
     }
 }
 
-void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
+static void solve_prefix(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
                             uint32_t* results, uint32_t count, uint64_t* acct)
 {
     for (uint32_t s = 0; s < count; ++s) {
@@ -409,7 +409,7 @@ void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow* rows, const
     }
 }
 
-void be_launch_solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
+static void solve_main(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef,
                           const uint32_t* results, const SolveItem* items, uint32_t count,
                           uint32_t)
 {
@@ -498,5 +498,16 @@ void be_timing_enable(bool) {}
 void be_timing_reset() {}
 double be_timing_exec_ms() { return 0; }
 double be_timing_total_ms() { return 0; }
+
+void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
+                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct)
+{
+    // the device fuses both passes; here the prefix of each solve (its tile-0
+    // item), then every tile
+    for (uint32_t k = 0; k < count; ++k)
+        if (items[k].tileBase == 0)
+            solve_prefix(solves + items[k].solve, rows, coef, results, 1, acct);
+    solve_main(solves, rows, coef, results, items, count, maxRows);
+}
 
 } // namespace sgpu

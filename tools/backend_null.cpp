@@ -73,7 +73,7 @@ void be_launch_ingest(const IngestDesc*, uint32_t) {}
 void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*, uint32_t) {}
 void be_launch_ldpc(const LdpcItem*, uint32_t, uint64_t*) {}
 
-void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow*, const uint8_t*,
+static void solve_prefix(const SolveDesc* solves, const SolveRow*, const uint8_t*,
                             uint32_t* results, uint32_t count, uint64_t*)
 {
     const SolveDesc* sd = host_view(solves);
@@ -85,7 +85,7 @@ void be_launch_solve_prefix(const SolveDesc* solves, const SolveRow*, const uint
     }
 }
 
-void be_launch_solve_main(const SolveDesc*, const SolveRow*, const uint8_t*, const uint32_t*,
+static void solve_main(const SolveDesc*, const SolveRow*, const uint8_t*, const uint32_t*,
                           const SolveItem*, uint32_t, uint32_t)
 {
 }
@@ -113,5 +113,17 @@ void be_timing_enable(bool) {}
 void be_timing_reset() {}
 double be_timing_exec_ms() { return 0; }
 double be_timing_total_ms() { return 0; }
+
+void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
+                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct)
+{
+    // the device fuses both passes; here the prefix of each solve (its tile-0
+    // item), then every tile
+    const SolveItem* it = host_view(items);
+    for (uint32_t k = 0; k < count; ++k)
+        if (it[k].tileBase == 0)
+            solve_prefix(solves + it[k].solve, rows, coef, results, 1, acct);
+    solve_main(solves, rows, coef, results, items, count, maxRows);
+}
 
 } // namespace sgpu
