@@ -223,8 +223,13 @@ def run_rank(rank, world, local, args, library, use_cuda):
     # is copied back to the host.  Reported beside, never as, `value`.
     e2e_elapsed = None
     if args.e2e:
-        sess.run(steps=max(1, args.warmup), warmup=0, verify=False, threads=args.threads,
-                 groups=args.groups, e2e=True, digest=False)
+        # (pipelined warm-up over both alternating device copies, every
+        # recovered byte checked against the payloads)
+        res_e, rep_e = sess.run(steps=max(2, args.warmup), warmup=0, verify=args.verify,
+                                threads=args.threads, groups=args.groups, e2e=True, digest=False)
+        if args.verify and (rep_e.mismatches or any(r.status for r in res_e)):
+            raise RuntimeError("bench: end-to-end verification failed: %d byte mismatches"
+                               % rep_e.mismatches)
         coll.barrier()
         t1 = time.perf_counter()
         sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,

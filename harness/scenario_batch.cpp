@@ -93,6 +93,8 @@ struct Api
     void (*host_free)(void*);
     int (*h2d)(void*, const void*, size_t);
     int (*gather)(unsigned, const void* const*, const unsigned*, void*);
+    int (*h2d_async)(void*, const void*, size_t);
+    int (*gather_completed)(unsigned, const void* const*, const unsigned*, void*);
     void (*timing)(int, int, double*, double*);
     void (*engine_stats)(uint64_t*);
     uint64_t (*arena_bytes)(void);
@@ -130,6 +132,7 @@ bool load_api(const char* path, Api& a)
            bind(h, a.device_alloc, "sgpu_device_alloc") && bind(h, a.device_free, "sgpu_device_free") &&
            bind(h, a.host_alloc, "sgpu_host_alloc") && bind(h, a.host_free, "sgpu_host_free") &&
            bind(h, a.h2d, "sgpu_h2d") && bind(h, a.gather, "sgpu_gather") &&
+           bind(h, a.h2d_async, "sgpu_h2d_async") && bind(h, a.gather_completed, "sgpu_gather_completed") &&
            bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats") &&
            bind(h, a.arena_bytes, "sgpu_arena_bytes") && bind(h, a.arena_reserve, "sgpu_arena_reserve");
 }
@@ -164,15 +167,18 @@ struct Shared
 {
     const Api* api;
     const ScenarioConfig* cfg;
-    uint8_t* payload;        // all originals, device-resident
+    uint8_t* payload;        // all originals, device-resident (indexed by global payload id)
+    uint8_t* payload2 = nullptr;   // e2e: the second device copy (steps alternate, see run_pipeline)
     size_t stride;
     bool hashData;
     bool verify;
     bool e2e = false;         // packets start and end in host memory (timed copies)
     uint8_t* hostPayload = nullptr;   // pinned host copy of every original (e2e)
-    uint8_t* devBase = nullptr;       // its device-resident counterpart
+    uint8_t* devBase = nullptr;       // its device-resident counterparts
+    uint8_t* devBase2 = nullptr;
     size_t payloadBytes = 0;
-    std::vector<uint8_t> landing;     // host buffer the packets are gathered into
+    uint8_t* landing = nullptr;       // pinned host buffer the packets are gathered into
+    size_t landingCap = 0;
     uint64_t checked = 0, mismatches = 0;
     std::unique_ptr<sgpu::WorkerPool> pool;
     unsigned groups = 1;
@@ -182,12 +188,13 @@ struct Shared
 struct BatchCodec
 {
     Shared* sh;
+    const uint8_t* payload = nullptr;   // the step's device copy of the originals
     SgpuEncoder enc = nullptr;
     SgpuDecoder dec = nullptr;
     std::vector<uint64_t>* log = nullptr;
     std::vector<Request> cur, prev;   // tokens waiting for device bytes
 
-    const void* dev_payload(unsigned id) const { return sh->payload + (size_t)id * sh->stride; }
+    const void* dev_payload(unsigned id) const { return payload + (size_t)id * sh->stride; }
 
     bool needs_host_payload() const { return false; }
     int enc_add(unsigned id, const uint8_t*, unsigned bytes, unsigned* num)
@@ -272,13 +279,27 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
     for (const Request& r : reqs) {
         srcs.push_back(r.dev);
         lens.push_back(r.bytes);
-        total += r.bytes;
+        total += (r.bytes + 15) & ~(size_t)15;
     }
-    // the host side of the packets (kept across rounds: no page faults per round)
-    std::vector<uint8_t>& host = sh.landing;
-    if (host.size() < total + 16)
-        host.resize(total + 16);
-    if (sh.api->gather((unsigned)reqs.size(), srcs.data(), lens.data(), host.data()) != 0) {
+    // the host side of the packets: pinned, kept across rounds, one DMA per
+    // gather straight into it (16-byte aligned ranges); the requests come from
+    // completed submissions, so nothing waits for the flushes in flight
+    if (sh.landingCap < total + 16) {
+        if (sh.landing)
+            sh.api->host_free(sh.landing);
+        sh.landingCap = std::max(total + 16, 2 * sh.landingCap);
+        sh.landing = (uint8_t*)sh.api->host_alloc(sh.landingCap);
+        if (!sh.landing) {
+            sh.landingCap = 0;
+            for (const Request& r : reqs)
+                if (r.ok)
+                    *r.ok = false;
+            reqs.clear();
+            return;
+        }
+    }
+    uint8_t* host = sh.landing;
+    if (sh.api->gather_completed((unsigned)reqs.size(), srcs.data(), lens.data(), host) != 0) {
         for (const Request& r : reqs)
             if (r.ok)
                 *r.ok = false;
@@ -288,8 +309,8 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
     std::vector<uint8_t> expect;
     size_t off = 0;
     for (const Request& r : reqs) {
-        const uint8_t* d = host.data() + off;
-        off += r.bytes;
+        const uint8_t* d = host + off;
+        off += (r.bytes + 15) & ~(size_t)15;
         if (r.isPacket && (sh.verify || sh.hashData)) {
             expect.resize(r.bytes + 8);
             scen::fill_payload(r.id, expect.data(), r.bytes);
@@ -484,8 +505,16 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             J.end = (unsigned)((uint64_t)n * (g + 1) / G);
             curJob = (int)next;
             ++next;
-            // the originals arrive in (pinned) host memory with each step
-            if (sh.e2e && g == 0 && api.h2d(sh.devBase, sh.hostPayload, sh.payloadBytes) != 0) {
+            // e2e: the originals arrive in pinned host memory with each step,
+            // into one of two device copies that alternate by step.  The copy
+            // of step s overwrites the one step s-2 read; the pipeline holds
+            // at most G+1 jobs, so every job of step s-2 has retired (its
+            // device work is complete) when step s's first job starts.  The
+            // copy runs on the library's staging stream beside the device
+            // work in flight; the submissions after it wait for it.
+            const bool second = sh.e2e && (J.step & 1u);
+            if (sh.e2e && g == 0 &&
+                api.h2d_async(second ? sh.devBase2 : sh.devBase, sh.hostPayload, sh.payloadBytes) != 0) {
                 rc = -3;
                 break;
             }
@@ -495,6 +524,7 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             for_streams(sh, cnt, [&](size_t i) {
                 BatchCodec& c = J.codecs[i];
                 c.sh = &sh;
+                c.payload = second ? sh.payload2 : sh.payload;
                 c.enc = api.encoder_create();
                 c.dec = api.decoder_create();
                 c.log = &J.streams[i].log;
@@ -611,12 +641,15 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
     sh.checked = sh.mismatches = 0;
     sh.e2e = opt->e2e != 0;
     if (sh.e2e && !sh.hostPayload) {
-        // a pinned host image of the device payload area (untimed)
+        // a pinned host image of the device payload area, and a second
+        // device copy for alternate steps (untimed)
         sh.payloadBytes = ss->payloadBytes;
         sh.devBase = ss->dev;
+        sh.devBase2 = (uint8_t*)api.device_alloc(sh.payloadBytes);
         sh.hostPayload = (uint8_t*)api.host_alloc(sh.payloadBytes);
-        if (!sh.hostPayload)
+        if (!sh.hostPayload || !sh.devBase2)
             return -2;
+        sh.payload2 = sh.devBase2 + (sh.payload - ss->dev);
         const ScenarioConfig* c = &ss->cfg;
         for (size_t k = 0; k < (size_t)c->streams * c->originals; ++k) {
             const unsigned id = (unsigned)((size_t)c->first_stream * c->originals + k);
@@ -680,8 +713,12 @@ void scenario_batch_close(void* session)
     if (!ss)
         return;
     ss->api->device_free(ss->dev);
+    if (ss->sh.devBase2)
+        ss->api->device_free(ss->sh.devBase2);
     if (ss->sh.hostPayload)
         ss->api->host_free(ss->sh.hostPayload);
+    if (ss->sh.landing)
+        ss->api->host_free(ss->sh.landing);
     delete ss;
 }
 

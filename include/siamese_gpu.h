@@ -23,7 +23,8 @@
     also touches the encoder that produced it).  Per-instance calls take no
     global lock.  sgpu_init, sgpu_flush, sgpu_submit, sgpu_enqueue,
     sgpu_gather, sgpu_h2d, and sgpu_decoder_get on a packet whose length is
-    still pending (it flushes) must not run concurrently with any other call.
+    still pending (it flushes) must not run concurrently with any other call;
+    sgpu_h2d_async and sgpu_gather_completed may run beside instance calls.
 
     Pipelined submission: sgpu_enqueue() hands all queued work to the
     library's launcher thread and returns a ticket at once; sgpu_wait(ticket)
@@ -114,6 +115,19 @@ SIAMESE_EXPORT int sgpu_h2d(void* deviceDst, const void* hostSrc, size_t bytes);
 /// Runs immediately; queued-but-unflushed codec work is left untouched.
 SIAMESE_EXPORT int sgpu_gather(unsigned count, const void* const* deviceSrcs, const unsigned* bytes,
                                void* hostOut);
+
+/// Asynchronous host -> device copy for packets arriving in pinned host
+/// memory: issued at once on the library's staging stream; every submission
+/// enqueued after this call waits for it on the device (the host never
+/// blocks), so the copy overlaps the device work already in flight.  The
+/// caller guarantees that no unfinished submission reads or writes deviceDst.
+SIAMESE_EXPORT int sgpu_h2d_async(void* deviceDst, const void* hostSrc, size_t bytes);
+/// Gather `count` device ranges produced by COMPLETED submissions into pinned
+/// host memory (sgpu_host_alloc) on the library's gather stream, without
+/// waiting for submissions still in flight.  Range i lands at offset
+/// sum over k < i of align16(bytes[k]) (16-byte aligned, one DMA for all).
+SIAMESE_EXPORT int sgpu_gather_completed(unsigned count, const void* const* deviceSrcs, const unsigned* bytes,
+                                         void* pinnedOut);
 
 /// Device timing of flushed work since the last reset (milliseconds).
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs);

@@ -55,7 +55,8 @@ bool be_sync();
 /// fault, and releases it.  The launcher thread creates fences, the
 /// completer thread waits for them.
 void* be_fence();
-bool be_fence_wait(void* fence);
+/// spinUs: poll this long before sleeping (latency-bound small flushes).
+bool be_fence_wait(void* fence, unsigned spinUs);
 
 /// Transfer streams beside the codec stream (end-to-end packet flows).
 /// be_stage_h2d copies host -> device on the staging stream right away (the

@@ -2361,7 +2361,7 @@ void* be_fence()
     return e;
 }
 
-bool be_fence_wait(void* fence)
+bool be_fence_wait(void* fence, unsigned spinUs)
 {
     bind_device();
     if (!fence)
@@ -2369,11 +2369,12 @@ bool be_fence_wait(void* fence)
     hipEvent_t e = static_cast<hipEvent_t>(fence);
     // Poll first: a blocking-sync wait sleeps until an interrupt wakes the
     // thread, tens of microseconds a flush on the latency-bound single-stream
-    // path (C3); the completer is a dedicated thread, so it spins up to
-    // kFenceSpinUs before it sleeps.
-    constexpr int64_t kFenceSpinUs = 2000;
+    // path (C3); the completer is a dedicated thread, so for small flushes it
+    // spins up to spinUs before it sleeps (large ones leave the core to the
+    // application's threads).
+    const int64_t kFenceSpinUs = spinUs;
     hipError_t r = hipEventQuery(e);
-    if (r == hipErrorNotReady) {
+    if (r == hipErrorNotReady && kFenceSpinUs > 0) {
         const auto t0 = std::chrono::steady_clock::now();
         do {
             __builtin_ia32_pause();

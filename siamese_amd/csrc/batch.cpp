@@ -273,6 +273,21 @@ SIAMESE_EXPORT int sgpu_gather(unsigned count, const void* const* deviceSrcs, co
     return eng->gather(count, deviceSrcs, bytes, hostOut) ? 0 : -1;
 }
 
+SIAMESE_EXPORT int sgpu_h2d_async(void* deviceDst, const void* hostSrc, size_t bytes)
+{
+    if (!g_batchReady)
+        return -1;
+    return Engine::global()->stage_in(deviceDst, hostSrc, bytes) ? 0 : -1;
+}
+
+SIAMESE_EXPORT int sgpu_gather_completed(unsigned count, const void* const* deviceSrcs, const unsigned* bytes,
+                                         void* pinnedOut)
+{
+    if (!g_batchReady)
+        return -1;
+    return Engine::global()->gather_completed(count, deviceSrcs, bytes, pinnedOut) ? 0 : -1;
+}
+
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs)
 {
     be_timing_enable(enable != 0);

@@ -71,3 +71,15 @@ def test_hostsim_batch_length_only_digest():
     assert rep.mismatches == 0 and rep.checked > 0
     if ref is not None:
         assert S.digests(res) == S.digests(ref)
+
+
+@pytest.mark.parametrize("name", ["C2x64", "smoke_C4x8"])
+def test_hostsim_batch_end_to_end_pipelined(name):
+    """End-to-end mode: the originals arrive by asynchronous copies into two
+    device copies that alternate by step (sgpu_h2d_async), results come back
+    through the gather stream into pinned memory (sgpu_gather_completed);
+    several pipelined steps verify every recovered byte."""
+    cfg = golden.config(name)
+    res, rep = S.run_batch(S.SIM_LIB, cfg, steps=3, verify=True, threads=4, groups=2, e2e=True)
+    _check(name, res)
+    assert rep.mismatches == 0 and rep.checked > 0
