@@ -45,7 +45,8 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct);
 /// recovered bytes it outputs.  maxRows: largest m among the solves (sizes
 /// the LDS staging).
 void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
-                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct);
+                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
+                     uint32_t solveBegin, uint32_t solveCount);
 
 /// Block until all queued work has finished.  Returns false on a device fault.
 bool be_sync();

@@ -1416,92 +1416,86 @@ __device__ __forceinline__ int parse_prefix(uint32_t w, uint32_t avail, uint32_t
     return 4;
 }
 
-// The solve's bytes 0..3 (the recovered length prefixes), by the first wave
-// of a k_solve_main workgroup while the others wait at the same barriers:
-// MultiplyLowerTriangle and BackSubstitution on one dword per row (reference
-// SiameseDecoder.cpp:1065-1238) give each row's header length and length, or
-// stop at the first corrupt prefix.  rw[0] = rows recovered from the right,
-// rw[1 + i] = (header << 29) | length.  Every tile of a solve computes the
-// same words (two dozen cycles per row pair against the tile's own sweeps)
-// from the rows' first 16 bytes as copied before the solve (SolveDesc.head),
-// so the solve needs no separate launch; the tile-0 workgroup publishes them
-// (`out`) with the byte counts: the diagonal scaling of max(32 clipped,
-// recovered) bytes and one muladd of min(recovered, row) bytes per earlier
-// row each completed step eliminates (:1131-1212).
-__device__ void solve_prefix_block(uint32_t m, const SolveRow* __restrict__ R, uint64_t head,
-                                   const uint8_t* __restrict__ C,
-                                   uint32_t* __restrict__ rw, uint32_t* __restrict__ P, uint32_t* __restrict__ sh,
-                                   uint32_t* __restrict__ out, unsigned long long* __restrict__ acct)
+// The solve's bytes 0..3 (the recovered length prefixes): MultiplyLowerTriangle
+// and BackSubstitution on one dword per row (reference SiameseDecoder.cpp:
+// 1065-1238) give each row's header length and length, or stop at the first
+// corrupt prefix.  rw[0] = rows recovered from the right, rw[1 + i] =
+// (header << 29) | length.  One wave does it with no barrier: lane l holds
+// rows l, l+64, l+128, l+192 in registers (p4), row i's word reaches every
+// lane by readlane, the coefficients and lengths come from the tile's LDS
+// copies and per-lane multipliers from the LDS multiply tables.  Every tile
+// of a solve computes the same words from the rows' first 16 bytes as copied
+// before the solve (SolveDesc.head: tile 0 may already have stored solved
+// rows), so the solve needs no separate launch; the tile-0 workgroup
+// publishes them (`out`) with the byte counts: the diagonal scaling of
+// max(32 clipped, recovered) bytes and one muladd of min(recovered, row)
+// bytes per earlier row each completed step eliminates (:1131-1212).
+__device__ __forceinline__ uint32_t p4_get(const uint32_t (&p4)[4], uint32_t i)
 {
-    // sh[0] = X, sh[1] = bb, sh[2] = stop
-    const uint32_t tid = threadIdx.x;
-    const bool w0 = tid < 64;
-    const uint32_t lane = tid & 63u;
-    if (w0) {
-        for (uint32_t j = lane; j < m; j += 64)
-            P[j] = ld4_masked(head + (uint64_t)j * 16u, R[j].initBytes);   // (not R[j].buf: tile 0 may
-                                                                           // have stored the solved row)
-        if (lane == 0)
-            sh[2] = 0;
-    }
-    __syncthreads();
+    // row i's word (i uniform): its lane's register k = i / 64
+    const uint32_t k = i >> 6;
+    const uint32_t v = k == 0 ? p4[0] : k == 1 ? p4[1] : k == 2 ? p4[2] : p4[3];
+    return rl(v, i & 63u);
+}
+
+__device__ void solve_prefix_wave(uint32_t m, uint32_t lane, uint32_t (&p4)[4], const uint8_t* Ct,
+                                  const uint32_t* lowL, const uint32_t* finB, const uint4* permL,
+                                  const uint32_t* permC, uint32_t* rw, uint32_t* __restrict__ out,
+                                  unsigned long long* __restrict__ acct)
+{
     for (uint32_t i = 0; i + 1 < m; ++i) {
-        if (w0) {
-            const uint32_t src = P[i] & byte_mask((int)R[i].lowerLen);
-            for (uint32_t j = i + 1 + lane; j < m; j += 64) {
-                const uint32_t y = C[(size_t)j * m + i];
+        const uint32_t src = p4_get(p4, i) & byte_mask((int)uni(lowL[i]));
+        const uint8_t* col = Ct + i * m;
+#pragma unroll
+        for (unsigned k = 0; k < 4; ++k) {
+            const uint32_t j = lane + 64u * k;
+            if (j > i && j < m) {
+                const uint32_t y = col[j];
                 if (y)
-                    P[j] ^= gf_mul_dword(src, y);
+                    p4[k] ^= gf_mul_tab(src, gf_tab_l(permL, permC, y));
             }
         }
-        __syncthreads();
     }
     uint32_t ok = 0;
     unsigned long long opAcc = 0, outAcc = 0;
     for (int i = (int)m - 1; i >= 0; --i) {
-        if (tid == 0) {
-            const uint32_t fb = R[i].finalBytes;
-            const uint32_t lc = fb < 32 ? fb : 32;
-            const uint32_t y = C[(size_t)i * m + i];
-            const uint32_t x = gf_mul_dword(P[i], c_inv[y]) & byte_mask((int)lc);
-            uint32_t len = 0;
-            const int h = parse_prefix(x, lc, &len);
-            if (h < 1 || len == 0 || (uint32_t)h + len > fb) {
-                sh[2] = 1;
-            } else {
-                rw[1 + i] = ((uint32_t)h << 29) | len;
-                sh[1] = (uint32_t)h + len;
-                sh[0] = x & byte_mask((int)((uint32_t)h + len));
-                opAcc += lc > sh[1] ? lc : sh[1];
-                outAcc += sh[1];
-            }
-        }
-        __syncthreads();
-        if (sh[2])
+        const uint8_t* col = Ct + (uint32_t)i * m;
+        const uint32_t fb = uni(finB[i]);
+        const uint32_t lc = fb < 32 ? fb : 32;
+        const uint32_t x = gf_mul_dword(p4_get(p4, (uint32_t)i), c_inv[uni(col[i])]) & byte_mask((int)lc);
+        uint32_t len = 0;
+        const int h = parse_prefix(x, lc, &len);
+        if (h < 1 || len == 0 || (uint32_t)h + len > fb)
             break;
+        const uint32_t b = (uint32_t)h + len;
+        if (lane == 0) {
+            rw[1 + i] = ((uint32_t)h << 29) | len;
+            opAcc += lc > b ? lc : b;
+            outAcc += b;
+        }
         ++ok;
-        if (w0) {
-            const uint32_t xi = sh[0], b = sh[1];
-            for (uint32_t j = lane; j < (uint32_t)i; j += 64) {
-                const uint32_t c = C[(size_t)j * m + i];
+        const uint32_t xi = x & byte_mask((int)b);
+#pragma unroll
+        for (unsigned k = 0; k < 4; ++k) {
+            const uint32_t j = lane + 64u * k;
+            if (j < (uint32_t)i) {
+                const uint32_t c = col[j];
                 if (c) {
-                    const uint32_t ab = b < R[j].finalBytes ? b : R[j].finalBytes;
-                    P[j] ^= gf_mul_dword(xi & byte_mask((int)ab), c);
+                    const uint32_t fj = finB[j];
+                    const uint32_t ab = b < fj ? b : fj;
+                    p4[k] ^= gf_mul_tab(xi & byte_mask((int)ab), gf_tab_l(permL, permC, c));
                     opAcc += ab;
                 }
             }
         }
-        __syncthreads();
     }
-    if (tid == 0)
+    if (lane == 0)
         rw[0] = ok;
-    if (w0) {
-        // rows not reached keep word 0 (as the host reads them)
-        for (uint32_t j = lane; j + ok < m; j += 64)
-            rw[1 + j] = 0;
-    }
-    __syncthreads();
-    if (out && w0) {
+    for (uint32_t j = lane; j + ok < m; j += 64)
+        rw[1 + j] = 0;   // rows not reached (the host does not read them)
+    if (out) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         for (uint32_t k = lane; k <= m; k += 64)
             out[k] = rw[k];
         // one atomic per wave (per-lane global atomics serialise at one address)
@@ -1517,21 +1511,32 @@ __device__ void solve_prefix_block(uint32_t m, const SolveRow* __restrict__ R, u
     }
 }
 
-// k_solve_main: one workgroup of kSolveWaves waves per (solve, 1 KiB tile).
+// rows' first words for the prefix pass (wave 0), loaded before the staging
+// so their latency overlaps it
+__device__ __forceinline__ void prefix_load(uint32_t (&p4)[4], uint32_t m, uint32_t lane, uint64_t head,
+                                            const SolveRow* __restrict__ R)
+{
+#pragma unroll
+    for (unsigned k = 0; k < 4; ++k) {
+        const uint32_t j = lane + 64u * k;
+        p4[k] = j < m ? ld4_masked(head + (uint64_t)j * 16u, R[j].initBytes) : 0u;
+    }
+}
+
+// k_solve_main: one workgroup of kSolveWaves waves per (solve, tile).  Wave 0
+// first solves the length prefixes (solve_prefix_wave) while the others wait.
 //
-// LDS path (m * 1 KiB fits the launch's dynamic LDS): the tile of all m rows
-// is staged in LDS once (bytes past each row's initial length read as zero:
+// 1 KiB tiles (m <= kSolveWideMaxRows): the tile of all m rows is staged in
+// LDS once (bytes past each row's initial length read as zero:
 // the reference's zero-padded growth), wave w owns rows j = w (mod W), and
 // both triangular sweeps run in LDS with one barrier per pivot step.  Each
 // recovered row is stored once, right after its back-substitution step;
 // rows left unsolved (a corrupt length prefix) are stored at the end.  HBM
 // traffic is one read and one write of each row instead of ~m of each.
 //
-// Narrow LDS path (m > kSolveWideMaxRows): the same sweeps on 256-byte tiles
-// (solve_tile_narrow below), up to the 255-column limit.
-//
-// Global path (only when the device refuses the large dynamic-LDS grant):
-// wave 0 alone, rows updated in place in HBM.
+// 256-byte tiles (m > kSolveWideMaxRows): the same sweeps (solve_tile_narrow
+// below), up to the 255-column limit.  Both need ~140 KiB of dynamic LDS at
+// their largest m, which gfx950 grants (be_init fails otherwise).
 //
 // The staged rows take m KiB of LDS, so only one or two workgroups fit on a
 // CU.  Eight waves per workgroup measured best (A/B of 4/8/16: 16 waves put
@@ -1541,16 +1546,21 @@ __device__ void solve_prefix_block(uint32_t m, const SolveRow* __restrict__ R, u
 #endif
 constexpr unsigned kSolveWaves = SGPU_SOLVE_WAVES;
 constexpr unsigned kSolveLdsMaxRows = 255;   // kMaximumLossRecoveryCount (SiameseCommon.h:80)
+constexpr unsigned kSolvePrefixSplit = 16;   // solves per launch from which the prefix pass is its own launch
 
 // LDS bytes of the staged solve: row tiles, the transposed coefficient
 // matrix, per-row lengths and the result words.
-__host__ __device__ constexpr uint32_t solve_lds_bytes(uint32_t m)
+// (the multiply tables at the end only when the tiles run the prefix pass:
+// 5 KiB more can halve the workgroups that fit a CU)
+__host__ __device__ constexpr uint32_t solve_lds_bytes(uint32_t m, bool prefix = true)
 {
-    return m * 1024u + ((m * m + 15u) & ~15u) + m * 12u + (m + 1u) * 4u;
+    return m * 1024u + ((m * m + 15u) & ~15u) + ((m * 12u + (m + 1u) * 4u + 15u) & ~15u) +
+           (prefix ? 256u * 20u : 0u);
 }
 
 __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow* __restrict__ R,
-                               const uint8_t* __restrict__ C, const uint32_t* __restrict__ res,
+                               const uint8_t* __restrict__ C, uint64_t head, const uint32_t* __restrict__ resIn,
+                               uint32_t* __restrict__ out, unsigned long long* __restrict__ acct,
                                uint32_t tileBase)
 {
     const uint32_t tid = threadIdx.x;
@@ -1564,7 +1574,22 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
     uint32_t* lowL = initB + m;
     uint32_t* finB = lowL + m;
     uint32_t* rw = finB + m;                                     // result words
+    uint4* permL = reinterpret_cast<uint4*>(initB + ((m * 12u + (m + 1u) * 4u + 15u) & ~15u) / 4u);
+    uint32_t* permC = reinterpret_cast<uint32_t*>(permL + 256);  // (prefix pass only)
 
+    uint32_t p4[4];
+    if (resIn) {
+        for (uint32_t k = tid; k <= m; k += 64 * kSolveWaves)
+            rw[k] = resIn[k];   // (solved by k_solve_prefix)
+    } else {
+        if (wave == 0)
+            prefix_load(p4, m, lane, head, R);
+        for (uint32_t y = tid; y < 256; y += 64 * kSolveWaves) {
+            const uint32_t* t = c_perm[y];
+            permL[y] = make_uint4(t[0], t[1], t[2], t[3]);
+            permC[y] = t[4];
+        }
+    }
     for (uint32_t k = tid; k < m * m; k += 64 * kSolveWaves) {
         const uint32_t j = k / m, i = k - j * m;
         Ct[i * m + j] = C[k];
@@ -1574,8 +1599,6 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
         lowL[j] = R[j].lowerLen;
         finB[j] = R[j].finalBytes;
     }
-    for (uint32_t k = tid; k <= m; k += 64 * kSolveWaves)
-        rw[k] = res[k];
     // row tiles: wave w stages rows w, w+W, ... four loads in flight per lane
     for (uint32_t j0 = wave; j0 < m; j0 += 4 * kSolveWaves) {
         uint4 v[4];
@@ -1600,6 +1623,11 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
         }
     }
     __syncthreads();
+    if (!resIn) {
+        if (wave == 0)
+            solve_prefix_wave(m, lane, p4, Ct, lowL, finB, permL, permC, rw, out, acct);
+        __syncthreads();
+    }
 
     // MultiplyLowerTriangle in pivot order (reference SiameseDecoder.cpp:1065-1104)
     // LDS values read by every lane alike are moved to scalar registers
@@ -1689,7 +1717,8 @@ __host__ __device__ constexpr uint32_t solve_narrow_lds_bytes(uint32_t m)
 }
 
 __device__ void solve_tile_narrow(uint4* __restrict__ X, uint32_t m, const SolveRow* __restrict__ R,
-                                  const uint8_t* __restrict__ C, const uint32_t* __restrict__ res,
+                                  const uint8_t* __restrict__ C, uint64_t head, const uint32_t* __restrict__ resIn,
+                                  uint32_t* __restrict__ out, unsigned long long* __restrict__ acct,
                                   uint32_t tileBase)
 {
     constexpr uint32_t kChunks = kSolveNarrowTileBytes / 16;   // 16 lanes per row
@@ -1706,6 +1735,13 @@ __device__ void solve_tile_narrow(uint4* __restrict__ X, uint32_t m, const Solve
     uint32_t* finB = lowL + m;
     uint32_t* rw = finB + m;
 
+    uint32_t p4[4];
+    if (resIn) {
+        for (uint32_t k = tid; k <= m; k += 64 * kSolveWaves)
+            rw[k] = resIn[k];   // (solved by k_solve_prefix)
+    } else if (tid < 64) {
+        prefix_load(p4, m, tid, head, R);
+    }
     for (uint32_t y = tid; y < 256; y += 64 * kSolveWaves) {
         const uint32_t* t = c_perm[y];
         permL[y] = make_uint4(t[0], t[1], t[2], t[3]);
@@ -1720,8 +1756,6 @@ __device__ void solve_tile_narrow(uint4* __restrict__ X, uint32_t m, const Solve
         lowL[j] = R[j].lowerLen;
         finB[j] = R[j].finalBytes;
     }
-    for (uint32_t k = tid; k <= m; k += 64 * kSolveWaves)
-        rw[k] = res[k];
     // row tiles, bytes past each row's initial length as zero; four loads
     // in flight per lane
     for (uint32_t j0 = slot; j0 < m; j0 += 4 * kSlots) {
@@ -1747,6 +1781,11 @@ __device__ void solve_tile_narrow(uint4* __restrict__ X, uint32_t m, const Solve
         }
     }
     __syncthreads();
+    if (!resIn) {
+        if (tid < 64)
+            solve_prefix_wave(m, tid, p4, Ct, lowL, finB, permL, permC, rw, out, acct);
+        __syncthreads();
+    }
 
     // MultiplyLowerTriangle in pivot order (reference SiameseDecoder.cpp:1065-1104)
     for (uint32_t i = 0; i + 1 < m; ++i) {
@@ -1819,24 +1858,21 @@ __device__ void solve_tile_narrow(uint4* __restrict__ X, uint32_t m, const Solve
 }
 
 // bytes of dynamic LDS a solve launch needs for its largest m
-__host__ __device__ constexpr uint32_t solve_launch_lds_bytes(uint32_t maxRows)
+__host__ __device__ constexpr uint32_t solve_launch_lds_bytes(uint32_t maxRows, bool prefix = true)
 {
     return maxRows > kSolveWideMaxRows
-               ? (solve_narrow_lds_bytes(maxRows) > solve_lds_bytes(kSolveWideMaxRows)
+               ? (solve_narrow_lds_bytes(maxRows) > solve_lds_bytes(kSolveWideMaxRows, prefix)
                       ? solve_narrow_lds_bytes(maxRows)
-                      : solve_lds_bytes(kSolveWideMaxRows))
-               : solve_lds_bytes(maxRows);
+                      : solve_lds_bytes(kSolveWideMaxRows, prefix))
+               : solve_lds_bytes(maxRows, prefix);
 }
 
 __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const SolveDesc* __restrict__ solves, const SolveRow* __restrict__ rows,
     const uint8_t* __restrict__ coef, uint32_t* __restrict__ results,
-    const SolveItem* __restrict__ items, uint32_t ldsRows, unsigned long long* __restrict__ acct)
+    const SolveItem* __restrict__ items, unsigned long long* __restrict__ acct, uint32_t prefixDone)
 {
     extern __shared__ uint4 X[];
-    __shared__ uint32_t rwS[kSolveLdsMaxRows + 1];   // the solve's result words (prefix pass)
-    __shared__ uint32_t prefP[kSolveLdsMaxRows + 1];
-    __shared__ uint32_t prefSh[4];
     const SolveItem it = items[blockIdx.x];
     const SolveDesc sd = solves[it.solve];
     const uint32_t m = sd.m;
@@ -1844,82 +1880,60 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const uint8_t* C = coef + sd.coefOffset;
     if (m > kSolveLdsMaxRows)
         return;   // (the host never queues m > 255: kMaximumLossRecoveryCount)
-    solve_prefix_block(m, R, sd.head, C, rwS, prefP, prefSh, it.tileBase == 0 ? results + sd.result : nullptr,
-                       acct);
-    const uint32_t* res = rwS;
-    if (m <= ldsRows && m <= kSolveWideMaxRows) {
-        solve_tile_lds(X, m, R, C, res, it.tileBase);
-        return;
-    }
-    if (m <= ldsRows) {
-        solve_tile_narrow(X, m, R, C, res, it.tileBase);
-        return;
-    }
-    if (threadIdx.x >= 64)
-        return;
-    // (the item's tile: 1 KiB, or 256 B for m > kSolveWideMaxRows)
-    const uint32_t tileEnd = it.tileBase + (m > kSolveWideMaxRows ? kSolveNarrowTileBytes : kTileBytes);
-    const uint32_t p = it.tileBase + threadIdx.x * 16;
-    if (p >= sd.maxBytes || p >= tileEnd)
-        return;
+    // prefixDone: k_solve_prefix already solved the length prefixes
+    const uint32_t* resIn = prefixDone ? results + sd.result : nullptr;
+    uint32_t* out = (!prefixDone && it.tileBase == 0) ? results + sd.result : nullptr;
+    if (m <= kSolveWideMaxRows)
+        solve_tile_lds(X, m, R, C, sd.head, resIn, out, acct, it.tileBase);
+    else
+        solve_tile_narrow(X, m, R, C, sd.head, resIn, out, acct, it.tileBase);
+}
 
-    // Zero the region each row grows into (GrowZeroPadded) up front.
-    for (uint32_t j = 0; j < m; ++j) {
-        const uint32_t a = R[j].initBytes, b = R[j].finalBytes;
-        if (b <= a || p >= b || p + 16 <= a)
-            continue;
-        uint4 v = ld16(R[j].buf + p);
-        const uint4 keep = mask16(make_uint4(~0u, ~0u, ~0u, ~0u), (int)a - (int)p);
-        v.x &= keep.x;
-        v.y &= keep.y;
-        v.z &= keep.z;
-        v.w &= keep.w;
-        st16(R[j].buf + p, v);
-    }
+// k_solve_prefix: the length-prefix pass alone, one wave per solve, ahead of
+// k_solve_main when a launch holds many solves (the fused pass would run on
+// every tile of every solve, serially before its sweeps).
+__host__ __device__ constexpr uint32_t solve_prefix_lds_bytes(uint32_t m)
+{
+    return 256u * 20u + ((m * m + 15u) & ~15u) + m * 8u + (m + 1u) * 4u;
+}
 
-    // Lower triangle in pivot order
-    for (uint32_t i = 0; i + 1 < m; ++i) {
-        const uint32_t L = R[i].lowerLen;
-        if (p >= L)
-            continue;
-        uint4 src = ld16(R[i].buf + p);
-        if (p + 16 > L)
-            src = mask16(src, (int)L - (int)p);
-        for (uint32_t j = i + 1; j < m; ++j) {
-            const uint32_t y = C[(size_t)j * m + i];
-            if (!y)
-                continue;
-            st16(R[j].buf + p, xor16(ld16(R[j].buf + p), gf_mul16(src, y)));
-        }
+__global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict__ solves,
+                                                     const SolveRow* __restrict__ rows,
+                                                     const uint8_t* __restrict__ coef,
+                                                     uint32_t* __restrict__ results,
+                                                     unsigned long long* __restrict__ acct)
+{
+    extern __shared__ uint4 X[];
+    const SolveDesc sd = solves[blockIdx.x];
+    const uint32_t m = sd.m;
+    if (m > kSolveLdsMaxRows)
+        return;
+    const SolveRow* R = rows + sd.rowBegin;
+    const uint8_t* C = coef + sd.coefOffset;
+    const uint32_t lane = threadIdx.x;
+    uint4* permL = X;
+    uint32_t* permC = reinterpret_cast<uint32_t*>(permL + 256);
+    uint8_t* Ct = reinterpret_cast<uint8_t*>(permC + 256);
+    uint32_t* lowL = reinterpret_cast<uint32_t*>(Ct + ((m * m + 15u) & ~15u));
+    uint32_t* finB = lowL + m;
+    uint32_t* rw = finB + m;
+    uint32_t p4[4];
+    prefix_load(p4, m, lane, sd.head, R);
+    for (uint32_t y = lane; y < 256; y += 64) {
+        const uint32_t* t = c_perm[y];
+        permL[y] = make_uint4(t[0], t[1], t[2], t[3]);
+        permC[y] = t[4];
     }
-
-    // Back-substitution from the right-most column
-    const uint32_t ok = res[0];
-    for (int i = (int)m - 1; i >= 0; --i) {
-        if ((uint32_t)(m - 1 - i) >= ok)
-            break;
-        const uint32_t w = res[1 + i];
-        const uint32_t bb = (w >> 29) + (w & kSolveLengthMask);
-        const uint32_t fb = R[i].finalBytes;
-        if (p >= fb)
-            continue;
-        const uint32_t y = C[(size_t)i * m + i];
-        uint4 x = gf_mul16(ld16(R[i].buf + p), c_inv[y]);
-        x = mask16(x, (int)bb - (int)p); // zero beyond the recovered length
-        st16(R[i].buf + p, x);
-        if (p >= bb)
-            continue;
-        for (uint32_t j = 0; j < (uint32_t)i; ++j) {
-            const uint32_t c = C[(size_t)j * m + i];
-            if (!c)
-                continue;
-            const uint32_t ab = bb < R[j].finalBytes ? bb : R[j].finalBytes;
-            if (p >= ab)
-                continue;
-            const uint4 xs = mask16(x, (int)ab - (int)p);
-            st16(R[j].buf + p, xor16(ld16(R[j].buf + p), gf_mul16(xs, c)));
-        }
+    for (uint32_t k = lane; k < m * m; k += 64) {
+        const uint32_t j = k / m, i = k - j * m;
+        Ct[i * m + j] = C[k];
     }
+    for (uint32_t j = lane; j < m; j += 64) {
+        lowL[j] = R[j].lowerLen;
+        finB[j] = R[j].finalBytes;
+    }
+    __syncthreads();
+    solve_prefix_wave(m, lane, p4, Ct, lowL, finB, permL, permC, rw, results + sd.result, acct);
 }
 
 // ---------------------------------------------------------------------------
@@ -1946,10 +1960,6 @@ inline void bind_device()
     }
 }
 bool g_timing = false;
-// largest m staged in LDS: 56 keeps solve_lds_bytes under the default 64 KiB
-// dynamic-LDS limit; raised at init to 255 (1 KiB tiles up to m = 120,
-// 256-byte tiles above) when the device grants ~140 KiB
-uint32_t g_solveLdsRows = 56;
 // window elements an OP_ROWS batch stages in LDS per tile (256 B each, beside
 // the 24 sums); sized at init to the LDS the kernel's static arrays leave
 // free; SGPU_STAGE overrides (0 = read every element from memory)
@@ -2159,8 +2169,16 @@ bool be_init(int device, const char** err)
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_pcgG), pg, sizeof(pg)), "hipMemcpyToSymbol(pcgG)");
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_main),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)solve_launch_lds_bytes(kSolveLdsMaxRows)) == hipSuccess)
-        g_solveLdsRows = kSolveLdsMaxRows;
+                            (int)solve_launch_lds_bytes(kSolveLdsMaxRows)) != hipSuccess) {
+        *err = "the device refused the triangular solve's LDS (gfx950 grants 160 KiB per workgroup)";
+        return false;
+    }
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_prefix),
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)solve_prefix_lds_bytes(kSolveLdsMaxRows)) != hipSuccess) {
+        *err = "the device refused the solve prefix pass's LDS";
+        return false;
+    }
     if (hipDeviceSynchronize() != hipSuccess) {
         *err = "device synchronisation failed during init";
         return false;
@@ -2265,15 +2283,24 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
 }
 
 void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
-                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct)
+                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
+                     uint32_t solveBegin, uint32_t solveCount)
 {
     if (count == 0)
         return;
     Timed t(false);
-    const uint32_t ldsRows = maxRows < g_solveLdsRows ? maxRows : g_solveLdsRows;
+    const uint32_t rowsCap = maxRows < kSolveLdsMaxRows ? maxRows : kSolveLdsMaxRows;
+    // Many solves: their prefixes in one wave each first (once per solve, all
+    // in parallel); few (single-stream flushes): fused into the tiles, one
+    // launch fewer on the flush's critical path.
+    const bool separate = solveCount >= kSolvePrefixSplit;
+    if (separate)
+        hipLaunchKernelGGL(k_solve_prefix, dim3(solveCount), dim3(64), (size_t)solve_prefix_lds_bytes(rowsCap),
+                           g_stream, solves + solveBegin, rows, coef, results,
+                           reinterpret_cast<unsigned long long*>(acct));
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
-                       (size_t)solve_launch_lds_bytes(ldsRows), g_stream, solves, rows, coef, results, items,
-                       ldsRows, reinterpret_cast<unsigned long long*>(acct));
+                       (size_t)solve_launch_lds_bytes(rowsCap, !separate), g_stream, solves, rows, coef, results,
+                       items, reinterpret_cast<unsigned long long*>(acct), separate ? 1u : 0u);
 }
 
 void* be_stage_h2d(void* dst, const void* src, size_t bytes)

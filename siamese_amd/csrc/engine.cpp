@@ -1403,7 +1403,8 @@ void Engine::launch_batch(Batch& bt)
             // solve items index solves globally; pass the global desc base
             be_launch_solve((const SolveDesc*)(xs.upDev + bt.oSD), (const SolveRow*)(xs.upDev + bt.oSR),
                             xs.upDev + bt.oCoef, resultsDev, (const SolveItem*)(xs.upDev + bt.oSI) + ph.itemBegin,
-                            (uint32_t)ph.itemCount, ph.maxRows, acctDev + 1);
+                            (uint32_t)ph.itemCount, ph.maxRows, acctDev + 1, (uint32_t)ph.solveBegin,
+                            (uint32_t)ph.solveCount);
         }
     }
     be_d2h(xs.downHost, xs.downDev, kAcctBytes + (size_t)bt.resultWords * 4);

@@ -115,7 +115,8 @@ double be_timing_exec_ms() { return 0; }
 double be_timing_total_ms() { return 0; }
 
 void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
-                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct)
+                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
+                     uint32_t, uint32_t)
 {
     // the device fuses both passes; here the prefix of each solve (its tile-0
     // item), then every tile
