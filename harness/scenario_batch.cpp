@@ -359,6 +359,7 @@ void for_streams(Shared& sh, size_t count, const F& fn)
 struct Job
 {
     unsigned step = 0, begin = 0, end = 0;
+    unsigned index = 0;             // step * groups + group
     std::vector<BatchCodec> codecs;
     std::unique_ptr<BatchStream[]> streams;
     std::vector<unsigned> live;     // indices into codecs/streams
@@ -495,7 +496,18 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             active.erase(active.begin() + (long)k);
             lap(4);
         }
-        if (rc == 0 && next < jobs && active.size() < depth) {
+        // e2e: a job's device copy of its originals is overwritten by the job
+        // two steps later (the copies alternate by step); that job starts
+        // only once the earlier one has retired
+        auto copy_busy = [&](unsigned idx) {
+            if (!sh.e2e || idx < 2 * G)
+                return false;
+            for (const auto& a : active)
+                if (a->index == idx - 2 * G)
+                    return true;
+            return false;
+        };
+        if (rc == 0 && next < jobs && active.size() < depth && !copy_busy(next)) {
             did = true;
             std::unique_ptr<Job> jp(new Job);
             Job& J = *jp;
@@ -503,20 +515,23 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             const unsigned g = next % G;
             J.begin = (unsigned)((uint64_t)n * g / G);
             J.end = (unsigned)((uint64_t)n * (g + 1) / G);
+            J.index = next;
             curJob = (int)next;
             ++next;
-            // e2e: the originals arrive in pinned host memory with each step,
-            // into one of two device copies that alternate by step.  The copy
-            // of step s overwrites the one step s-2 read; the pipeline holds
-            // at most G+1 jobs, so every job of step s-2 has retired (its
-            // device work is complete) when step s's first job starts.  The
+            // e2e: the originals arrive in pinned host memory with each job,
+            // into one of two device copies that alternate by step: only the
+            // job's own streams' originals, so its device work waits for its
+            // slice alone while the next slices are still on the bus.  The
             // copy runs on the library's staging stream beside the device
             // work in flight; the submissions after it wait for it.
             const bool second = sh.e2e && (J.step & 1u);
-            if (sh.e2e && g == 0 &&
-                api.h2d_async(second ? sh.devBase2 : sh.devBase, sh.hostPayload, sh.payloadBytes) != 0) {
-                rc = -3;
-                break;
+            if (sh.e2e) {
+                const size_t per = (size_t)cfg->originals * sh.stride;
+                const size_t off = (size_t)J.begin * per, len = (size_t)(J.end - J.begin) * per;
+                if (api.h2d_async((second ? sh.devBase2 : sh.devBase) + off, sh.hostPayload + off, len) != 0) {
+                    rc = -3;
+                    break;
+                }
             }
             const unsigned cnt = J.end - J.begin;
             J.codecs.resize(cnt);

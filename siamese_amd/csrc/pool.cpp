@@ -11,6 +11,18 @@ namespace sgpu {
 
 namespace {
 // SIAMESE_AMD_WORKER_NICE overrides (0 = same priority as the engine threads)
+// pause iterations a worker (or a joining caller) spins before blocking;
+// SIAMESE_AMD_POOL_SPIN overrides (0 = block at once)
+const unsigned kSpin = [] {
+    const char* v = std::getenv("SIAMESE_AMD_POOL_SPIN");
+    return v ? (unsigned)std::atoi(v) : 4096u;
+}();
+inline void cpu_relax()
+{
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+}
 const int kWorkerNice = [] {
     const char* v = std::getenv("SIAMESE_AMD_WORKER_NICE");
     return v ? std::atoi(v) : 10;
@@ -44,7 +56,7 @@ WorkerPool::~WorkerPool()
 {
     {
         std::lock_guard<std::mutex> g(mu_);
-        stop_ = true;
+        stop_.store(true, std::memory_order_relaxed);
     }
     cv_.notify_all();
     for (std::thread& t : workers_)
@@ -65,19 +77,32 @@ void WorkerPool::loop()
 {
     uint64_t seen = 0;
     for (;;) {
+        // Fork-joins come in quick succession (one per job round and per
+        // assembly pass): spin a short while for the next one before
+        // sleeping, so a worker joins it without a futex wake-up.
+        for (unsigned k = 0; k < kSpin && gen_.load(std::memory_order_acquire) == seen &&
+                             !stop_.load(std::memory_order_relaxed);
+             ++k)
+            cpu_relax();
         {
             std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-            if (stop_)
+            if (gen_.load(std::memory_order_relaxed) == seen && !stop_.load(std::memory_order_relaxed)) {
+                ++sleepers_;
+                cv_.wait(lk, [&] {
+                    return stop_.load(std::memory_order_relaxed) ||
+                           gen_.load(std::memory_order_relaxed) != seen;
+                });
+                --sleepers_;
+            }
+            if (stop_.load(std::memory_order_relaxed))
                 return;
-            seen = gen_;
-            ++busy_;
+            seen = gen_.load(std::memory_order_relaxed);
+            busy_.fetch_add(1, std::memory_order_acq_rel);
         }
         drain();
-        {
+        if (busy_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
             std::lock_guard<std::mutex> g(mu_);
-            if (--busy_ == 0)
-                doneCv_.notify_all();
+            doneCv_.notify_all();
         }
     }
 }
@@ -91,18 +116,23 @@ void WorkerPool::run(size_t count, const std::function<void(size_t)>& fn)
             fn(i);
         return;
     }
+    bool wake;
     {
         std::lock_guard<std::mutex> g(mu_);
         fn_ = &fn;
         count_ = count;
         next_.store(0, std::memory_order_release);
-        ++gen_;
+        gen_.fetch_add(1, std::memory_order_acq_rel);
+        wake = sleepers_ > 0;
     }
-    cv_.notify_all();
+    if (wake)
+        cv_.notify_all();
     drain();
-    std::unique_lock<std::mutex> lk(mu_);
     // every index has been claimed; wait for the workers still finishing one
-    doneCv_.wait(lk, [&] { return busy_ == 0; });
+    for (unsigned k = 0; k < kSpin && busy_.load(std::memory_order_acquire) != 0; ++k)
+        cpu_relax();
+    std::unique_lock<std::mutex> lk(mu_);
+    doneCv_.wait(lk, [&] { return busy_.load(std::memory_order_acquire) == 0; });
     fn_ = nullptr;
 }
 

@@ -38,9 +38,10 @@ private:
     const std::function<void(size_t)>* fn_ = nullptr;
     size_t count_ = 0;
     std::atomic<size_t> next_{0};
-    unsigned busy_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::atomic<unsigned> busy_{0};
+    std::atomic<uint64_t> gen_{0};
+    unsigned sleepers_ = 0;   // workers blocked on cv_ (mu_)
+    std::atomic<bool> stop_{false};
 };
 
 } // namespace sgpu
