@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <malloc.h>
 #include <memory>
 
@@ -95,6 +96,8 @@ struct Api
     int (*gather)(unsigned, const void* const*, const unsigned*, void*);
     int (*h2d_async)(void*, const void*, size_t);
     int (*gather_completed)(unsigned, const void* const*, const unsigned*, void*);
+    long long (*gather_async)(unsigned, const void* const*, const unsigned*, void*);
+    int (*gather_wait)(long long);
     void (*timing)(int, int, double*, double*);
     void (*engine_stats)(uint64_t*);
     uint64_t (*arena_bytes)(void);
@@ -133,6 +136,7 @@ bool load_api(const char* path, Api& a)
            bind(h, a.host_alloc, "sgpu_host_alloc") && bind(h, a.host_free, "sgpu_host_free") &&
            bind(h, a.h2d, "sgpu_h2d") && bind(h, a.gather, "sgpu_gather") &&
            bind(h, a.h2d_async, "sgpu_h2d_async") && bind(h, a.gather_completed, "sgpu_gather_completed") &&
+           bind(h, a.gather_async, "sgpu_gather_async") && bind(h, a.gather_wait, "sgpu_gather_wait") &&
            bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats") &&
            bind(h, a.arena_bytes, "sgpu_arena_bytes") && bind(h, a.arena_reserve, "sgpu_arena_reserve");
 }
@@ -177,8 +181,20 @@ struct Shared
     uint8_t* devBase = nullptr;       // its device-resident counterparts
     uint8_t* devBase2 = nullptr;
     size_t payloadBytes = 0;
-    uint8_t* landing = nullptr;       // pinned host buffer the packets are gathered into
-    size_t landingCap = 0;
+    // gathers in flight (oldest first) and their pinned landing buffers
+    struct Landing
+    {
+        uint8_t* buf = nullptr;
+        size_t cap = 0;
+    };
+    struct Gather
+    {
+        long long ticket;
+        Landing land;
+        std::vector<Request> reqs;   // kept only when the bytes are checked or hashed
+    };
+    std::deque<Gather> gathers;
+    std::vector<Landing> landings;    // free ones
     uint64_t checked = 0, mismatches = 0;
     std::unique_ptr<sgpu::WorkerPool> pool;
     unsigned groups = 1;
@@ -268,7 +284,51 @@ struct BatchCodec
 
 using BatchStream = scen::Stream<BatchCodec, Rec, Pkt>;
 
-// Resolve tokens whose data was produced by an already completed flush.
+// Wait for the oldest gather in flight, then check / hash its bytes.
+void land_gather(Shared& sh)
+{
+    Shared::Gather g = std::move(sh.gathers.front());
+    sh.gathers.pop_front();
+    if (sh.api->gather_wait(g.ticket) != 0) {
+        for (const Request& r : g.reqs)
+            if (r.ok)
+                *r.ok = false;
+        ++sh.mismatches;
+    } else {
+        std::vector<uint8_t> expect;
+        size_t off = 0;
+        for (const Request& r : g.reqs) {
+            const uint8_t* d = g.land.buf + off;
+            off += (r.bytes + 15) & ~(size_t)15;
+            if (r.isPacket && (sh.verify || sh.hashData)) {
+                expect.resize(r.bytes + 8);
+                scen::fill_payload(r.id, expect.data(), r.bytes);
+                ++sh.checked;
+                if (std::memcmp(expect.data(), d, r.bytes) != 0) {
+                    ++sh.mismatches;
+                    *r.ok = false;
+                }
+            }
+            if (sh.hashData)
+                (*r.log)[r.pos] = scen::data_token(true, d, r.bytes);
+        }
+    }
+    sh.landings.push_back(g.land);
+}
+
+void land_gathers(Shared& sh)
+{
+    while (!sh.gathers.empty())
+        land_gather(sh);
+}
+
+// Resolve tokens whose data was produced by an already completed flush: one
+// gather of all their device ranges into a pinned landing buffer (16-byte
+// aligned ranges, one DMA), issued without waiting.  The requests come from
+// completed submissions, so nothing waits for the flushes in flight, and the
+// codecs owning the ranges may be driven on at once (later device work waits
+// for the gather's reads).  Bytes that are checked or hashed are examined
+// when the gather lands (land_gather).
 void resolve_requests(Shared& sh, std::vector<Request>& reqs)
 {
     if (reqs.empty())
@@ -281,48 +341,43 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
         lens.push_back(r.bytes);
         total += (r.bytes + 15) & ~(size_t)15;
     }
-    // the host side of the packets: pinned, kept across rounds, one DMA per
-    // gather straight into it (16-byte aligned ranges); the requests come from
-    // completed submissions, so nothing waits for the flushes in flight
-    if (sh.landingCap < total + 16) {
-        if (sh.landing)
-            sh.api->host_free(sh.landing);
-        sh.landingCap = std::max(total + 16, 2 * sh.landingCap);
-        sh.landing = (uint8_t*)sh.api->host_alloc(sh.landingCap);
-        if (!sh.landing) {
-            sh.landingCap = 0;
-            for (const Request& r : reqs)
-                if (r.ok)
-                    *r.ok = false;
-            reqs.clear();
-            return;
+    constexpr size_t kInFlight = 4;
+    if (sh.gathers.size() >= kInFlight)
+        land_gather(sh);
+    // a free landing buffer that fits (the largest one otherwise, regrown)
+    Shared::Landing land;
+    size_t pick = sh.landings.size();
+    for (size_t k = 0; k < sh.landings.size(); ++k)
+        if (sh.landings[k].cap >= total + 16 && (pick == sh.landings.size() || sh.landings[k].cap < sh.landings[pick].cap))
+            pick = k;
+    if (pick < sh.landings.size()) {
+        land = sh.landings[pick];
+        sh.landings.erase(sh.landings.begin() + (long)pick);
+    } else {
+        if (!sh.landings.empty()) {
+            sh.api->host_free(sh.landings.back().buf);
+            sh.landings.pop_back();
         }
+        land.cap = ((total + 16) + (8u << 20) - 1) & ~(size_t)((8u << 20) - 1);
+        land.buf = (uint8_t*)sh.api->host_alloc(land.cap);
     }
-    uint8_t* host = sh.landing;
-    if (sh.api->gather_completed((unsigned)reqs.size(), srcs.data(), lens.data(), host) != 0) {
+    const long long t = land.buf ? sh.api->gather_async((unsigned)reqs.size(), srcs.data(), lens.data(), land.buf) : -1;
+    if (t <= 0) {
+        if (land.buf)
+            sh.landings.push_back(land);
         for (const Request& r : reqs)
             if (r.ok)
                 *r.ok = false;
+        ++sh.mismatches;
         reqs.clear();
         return;
     }
-    std::vector<uint8_t> expect;
-    size_t off = 0;
-    for (const Request& r : reqs) {
-        const uint8_t* d = host + off;
-        off += (r.bytes + 15) & ~(size_t)15;
-        if (r.isPacket && (sh.verify || sh.hashData)) {
-            expect.resize(r.bytes + 8);
-            scen::fill_payload(r.id, expect.data(), r.bytes);
-            ++sh.checked;
-            if (std::memcmp(expect.data(), d, r.bytes) != 0) {
-                ++sh.mismatches;
-                *r.ok = false;
-            }
-        }
-        if (sh.hashData)
-            (*r.log)[r.pos] = scen::data_token(true, d, r.bytes);
-    }
+    Shared::Gather g;
+    g.ticket = t;
+    g.land = land;
+    if (sh.verify || sh.hashData)
+        g.reqs.swap(reqs);
+    sh.gathers.push_back(std::move(g));
     reqs.clear();
 }
 
@@ -485,6 +540,8 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             }
             reqs = take(J, false);
             resolve_requests(sh, reqs);
+            if (sh.verify || sh.hashData)
+                land_gathers(sh);   // (their requests point into the job's streams)
             for_streams(sh, J.end - J.begin, [&](size_t i) {
                 J.streams[i].finish();
                 api.encoder_free(J.codecs[i].enc);   // (null if freed already)
@@ -569,6 +626,8 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
     if (api.flush() != 0)
         rc = -3;
     lap(2);
+    land_gathers(sh);   // every output is in host memory before the run ends
+    lap(3);
     return rc;
 }
 
@@ -732,8 +791,9 @@ void scenario_batch_close(void* session)
         ss->api->device_free(ss->sh.devBase2);
     if (ss->sh.hostPayload)
         ss->api->host_free(ss->sh.hostPayload);
-    if (ss->sh.landing)
-        ss->api->host_free(ss->sh.landing);
+    land_gathers(ss->sh);
+    for (const Shared::Landing& l : ss->sh.landings)
+        ss->api->host_free(l.buf);
     delete ss;
 }
 

@@ -128,6 +128,17 @@ SIAMESE_EXPORT int sgpu_h2d_async(void* deviceDst, const void* hostSrc, size_t b
 /// sum over k < i of align16(bytes[k]) (16-byte aligned, one DMA for all).
 SIAMESE_EXPORT int sgpu_gather_completed(unsigned count, const void* const* deviceSrcs, const unsigned* bytes,
                                          void* pinnedOut);
+/// sgpu_gather_completed without waiting for the copy: returns a gather
+/// ticket (> 0; -1 on failure) at once.  The sources are read before the
+/// device work of any later submission runs (that work waits for them on the
+/// device), so the instances owning them may be driven on right away;
+/// pinnedOut holds the bytes once sgpu_gather_wait(ticket) returns 0.  May
+/// run beside instance calls, like sgpu_gather_completed.
+SIAMESE_EXPORT long long sgpu_gather_async(unsigned count, const void* const* deviceSrcs, const unsigned* bytes,
+                                           void* pinnedOut);
+/// Wait until gather `ticket` and every earlier one have landed in host
+/// memory.  0 on success, -1 after a device fault.
+SIAMESE_EXPORT int sgpu_gather_wait(long long ticket);
 
 /// Device timing of flushed work since the last reset (milliseconds).
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs);

@@ -69,11 +69,16 @@ void* be_stage_h2d(void* dst, const void* src, size_t bytes);
 void be_wait_mark(void* mark);
 void be_mark_release(void* mark);
 /// Gather on the gather stream: upload `count` ingest descriptors (from
-/// pinned descsHost to descsDev), pack their sources into devStage, copy
-/// `bytes` of it to hostOut, and wait for the gather stream only (not for
-/// in-flight codec work).  False on a device fault.
+/// pinned descsHost to descsDev), pack their sources into devStage and copy
+/// `bytes` of it to hostOut, without waiting (not even for the gather
+/// stream).  Returns two marks: *packed is passed once the sources have been
+/// read (be_wait_mark / be_mark_release, like a staging mark), *landed once
+/// hostOut holds the bytes (be_mark_sync).  False if it could not be queued.
 bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, const void* devStage,
-               void* hostOut, size_t bytes);
+               void* hostOut, size_t bytes, void** packed, void** landed);
+/// Block until the device has passed `mark`, then recycle it; false on a
+/// device fault.
+bool be_mark_sync(void* mark);
 
 /// Device-time accounting: every executor/solve launch is bracketed with
 /// events; these return the accumulated milliseconds since the last reset.

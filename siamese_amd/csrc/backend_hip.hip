@@ -2337,22 +2337,58 @@ void be_mark_release(void* mark)
     g_fenceFree.push_back(static_cast<hipEvent_t>(mark));
 }
 
+hipEvent_t take_mark()
+{
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_evMu);
+        if (!g_fenceFree.empty()) {
+            e = g_fenceFree.back();
+            g_fenceFree.pop_back();
+        }
+    }
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    return e;
+}
+
 bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, const void* devStage,
-               void* hostOut, size_t bytes)
+               void* hostOut, size_t bytes, void** packed, void** landed)
 {
     bind_device();
-    if (count == 0)
-        return true;
+    *packed = *landed = nullptr;
+    hipEvent_t p = take_mark(), l = take_mark();
+    if (!p || !l) {
+        be_mark_release(p);
+        be_mark_release(l);
+        return false;
+    }
     if (hipMemcpyAsync(descsDev, descsHost, (size_t)count * sizeof(IngestDesc), hipMemcpyHostToDevice,
                        g_gatherStream) != hipSuccess)
         return false;
     hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves), dim3(64 * kIngestWaves),
                        0, g_gatherStream, static_cast<const IngestDesc*>(descsDev), count);
-    if (hipMemcpyAsync(hostOut, devStage, bytes, hipMemcpyDeviceToHost, g_gatherStream) != hipSuccess)
+    if (hipEventRecord(p, g_gatherStream) != hipSuccess)
         return false;
-    const hipError_t e = hipStreamSynchronize(g_gatherStream);
+    *packed = p;
+    if (hipMemcpyAsync(hostOut, devStage, bytes, hipMemcpyDeviceToHost, g_gatherStream) != hipSuccess ||
+        hipEventRecord(l, g_gatherStream) != hipSuccess) {
+        be_mark_release(l);
+        return false;
+    }
+    *landed = l;
+    return true;
+}
+
+bool be_mark_sync(void* mark)
+{
+    bind_device();
+    if (!mark)
+        return false;
+    const hipError_t e = hipEventSynchronize(static_cast<hipEvent_t>(mark));
+    be_mark_release(mark);
     if (e != hipSuccess) {
-        check(e, "hipStreamSynchronize(gather)");
+        check(e, "hipEventSynchronize(mark)");
         return false;
     }
     return true;

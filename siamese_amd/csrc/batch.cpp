@@ -288,6 +288,21 @@ SIAMESE_EXPORT int sgpu_gather_completed(unsigned count, const void* const* devi
     return Engine::global()->gather_completed(count, deviceSrcs, bytes, pinnedOut) ? 0 : -1;
 }
 
+SIAMESE_EXPORT long long sgpu_gather_async(unsigned count, const void* const* deviceSrcs, const unsigned* bytes,
+                                           void* pinnedOut)
+{
+    if (!g_batchReady)
+        return -1;
+    return (long long)Engine::global()->gather_async(count, deviceSrcs, bytes, pinnedOut);
+}
+
+SIAMESE_EXPORT int sgpu_gather_wait(long long ticket)
+{
+    if (!g_batchReady)
+        return -1;
+    return Engine::global()->gather_wait((int64_t)ticket) ? 0 : -1;
+}
+
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs)
 {
     be_timing_enable(enable != 0);

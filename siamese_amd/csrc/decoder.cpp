@@ -30,6 +30,101 @@ inline unsigned first_clear(uint64_t bits, unsigned from)
 DecoderCore::DecoderCore(Engine* eng, bool hostMirror)
     : eng_(eng), prog_(eng, 1), mirror_(hostMirror)
 {
+    adopt_spare();
+}
+
+// Every recycled vector is empty in a fresh decoder; a spare holds them
+// cleared (capacity kept), so swapping one in leaves the decoder in exactly
+// its freshly constructed state.  pend_ keeps its slots, all idle (a slot is
+// claimed by the first search for a non-live one and fully rewritten).
+struct DecoderCore::Spare
+{
+    std::vector<DecSubwindowPtr> subwindows;
+    std::vector<SiameseOriginalPacket> recovered;
+    std::vector<unsigned> recoveredColumns;
+    std::vector<RowInfo> rows;
+    std::vector<ColInfo> cols;
+    std::vector<uint8_t> colLane, colCx, colCx2;
+    std::vector<uint32_t> pickCol;
+    std::vector<uint8_t> mat;
+    std::vector<unsigned> pivots;
+    std::vector<PendingDecode> pend;
+    std::vector<Fix> lastDecoded;
+    std::vector<RecPacket*> scratchRec;
+    std::vector<unsigned> scratchLen;
+    std::vector<SolveRow> scratchRows;
+    std::vector<uint8_t> scratchCoef;
+};
+
+void DecoderCore::adopt_spare()
+{
+    Spare* s = CapStash<Spare>::take();
+    if (!s)
+        return;
+    subwindows_.swap(s->subwindows);
+    recovered_.swap(s->recovered);
+    recoveredColumns_.swap(s->recoveredColumns);
+    rows_.swap(s->rows);
+    cols_.swap(s->cols);
+    colLane_.swap(s->colLane);
+    colCx_.swap(s->colCx);
+    colCx2_.swap(s->colCx2);
+    pickCol_.swap(s->pickCol);
+    mat_.swap(s->mat);
+    pivots_.swap(s->pivots);
+    pend_.swap(s->pend);
+    lastDecoded_.swap(s->lastDecoded);
+    scratchRec_.swap(s->scratchRec);
+    scratchLen_.swap(s->scratchLen);
+    scratchRows_.swap(s->scratchRows);
+    scratchCoef_.swap(s->scratchCoef);
+    CapStash<Spare>::put_shell(s);   // (now holding this decoder's empty vectors)
+}
+
+void DecoderCore::donate_spare()
+{
+    Spare* s = CapStash<Spare>::shell();
+    subwindows_.clear();   // (subwindows go back to their own pool)
+    recovered_.clear();
+    recoveredColumns_.clear();
+    rows_.clear();
+    cols_.clear();
+    colLane_.clear();
+    colCx_.clear();
+    colCx2_.clear();
+    pickCol_.clear();
+    mat_.clear();
+    pivots_.clear();
+    for (PendingDecode& pd : pend_) {
+        pd.fixes.clear();
+        pd.base = 0;
+        pd.m = 0;
+        pd.serial = 0;
+        pd.live = false;
+    }
+    lastDecoded_.clear();
+    scratchRec_.clear();
+    scratchLen_.clear();
+    scratchRows_.clear();
+    scratchCoef_.clear();
+    subwindows_.swap(s->subwindows);
+    recovered_.swap(s->recovered);
+    recoveredColumns_.swap(s->recoveredColumns);
+    rows_.swap(s->rows);
+    cols_.swap(s->cols);
+    colLane_.swap(s->colLane);
+    colCx_.swap(s->colCx);
+    colCx2_.swap(s->colCx2);
+    pickCol_.swap(s->pickCol);
+    mat_.swap(s->mat);
+    pivots_.swap(s->pivots);
+    pend_.swap(s->pend);
+    lastDecoded_.swap(s->lastDecoded);
+    scratchRec_.swap(s->scratchRec);
+    scratchLen_.swap(s->scratchLen);
+    scratchRows_.swap(s->scratchRows);
+    scratchCoef_.swap(s->scratchCoef);
+    CapStash<Spare>::give(s);
 }
 
 DecoderCore::~DecoderCore()
@@ -53,6 +148,7 @@ DecoderCore::~DecoderCore()
     for (auto& lane : lanes_)
         for (Sum& s : lane)
             eng_->release(s.d.buf);
+    donate_spare();
 }
 
 // ---------------------------------------------------------------------------

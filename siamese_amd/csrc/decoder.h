@@ -273,6 +273,14 @@ private:
     std::vector<SolveRow> scratchRows_;
     std::vector<uint8_t> scratchCoef_;
     uint64_t decodeSerial_ = 0;
+
+    // Heap capacity of the vectors above, handed from a freed decoder to the
+    // next one created on the same thread: a bench step creates and frees
+    // thousands of decoders, and growing these from empty each time costs
+    // ~40 mallocs per decoder on contended heap arenas.
+    struct Spare;
+    void adopt_spare();
+    void donate_spare();
     unsigned pendingSolves_ = 0;
 
     uint64_t stats_[SiameseDecoderStats_Count] = {};

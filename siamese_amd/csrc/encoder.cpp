@@ -13,6 +13,12 @@ EncoderCore::EncoderCore(Engine* eng, bool hostMirror) : eng_(eng), prog_(eng, 0
     for (unsigned l = 0; l < kLanes; ++l)
         for (unsigned s = 0; s < kSums; ++s)
             lanes_[l].next[s] = l;
+    // the subwindow table's capacity comes from an encoder freed on this
+    // thread (see DecoderCore::Spare)
+    if (SubwindowTable* t = CapStash<SubwindowTable>::take()) {
+        subwindows_.swap(t->v);
+        CapStash<SubwindowTable>::put_shell(t);
+    }
 }
 
 EncoderCore::~EncoderCore()
@@ -24,6 +30,10 @@ EncoderCore::~EncoderCore()
         for (DevSum& s : l.sum)
             eng_->release(s.buf);
     eng_->release(recovery_);
+    subwindows_.clear();   // (subwindows go back to their own pool)
+    SubwindowTable* t = CapStash<SubwindowTable>::shell();
+    subwindows_.swap(t->v);
+    CapStash<SubwindowTable>::give(t);
 }
 
 // ---------------------------------------------------------------------------

@@ -133,6 +133,10 @@ private:
     bool disabled_ = false;
 
     std::vector<EncSubwindowPtr> subwindows_;
+    struct SubwindowTable
+    {
+        std::vector<EncSubwindowPtr> v;
+    };
     unsigned nextColumn_ = 0;
     unsigned count_ = 0;
     unsigned columnStart_ = 0;

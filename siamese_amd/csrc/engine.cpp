@@ -1537,14 +1537,31 @@ bool Engine::stage_in(void* dst, const void* src, size_t bytes)
     return true;
 }
 
-bool Engine::gather_completed(unsigned count, const void* const* srcs, const unsigned* bytes,
-                              void* pinnedOut)
+bool Engine::gather_land(GatherSlot& g)
+{
+    if (!g.landed)
+        return true;
+    void* m = g.landed;
+    g.landed = nullptr;
+    if (!be_mark_sync(m)) {
+        failed_.store(true, std::memory_order_relaxed);
+        return false;
+    }
+    return true;
+}
+
+int64_t Engine::gather_async(unsigned count, const void* const* srcs, const unsigned* bytes,
+                             void* pinnedOut)
 {
     if (failed())
-        return false;
+        return -1;
+    std::lock_guard<std::mutex> lk(gatherMu_);
+    const int64_t ticket = ++gNext_;
     if (count == 0)
-        return true;
-    std::lock_guard<std::mutex> g(gatherMu_);
+        return ticket;
+    GatherSlot& g = gslots_[ticket % kGatherSlots];
+    if (!gather_land(g))   // (the slot's previous gather, kGatherSlots back)
+        return -1;
     const size_t upBytes = count * sizeof(IngestDesc);
     size_t total = 0;
     for (unsigned i = 0; i < count; ++i)
@@ -1564,24 +1581,47 @@ bool Engine::gather_completed(unsigned count, const void* const* srcs, const uns
         cap = c;
     };
     uint8_t* noHost = nullptr;
-    grow(cUpHost_, cUpDev_, cUpCap_, upBytes, true);
-    grow(noHost, cDev_, cCap_, total, false);
-    if (!cUpHost_ || !cUpDev_ || !cDev_)
-        return false;
-    IngestDesc* descs = reinterpret_cast<IngestDesc*>(cUpHost_);
+    grow(g.upHost, g.upDev, g.upCap, upBytes, true);
+    grow(noHost, g.stage, g.stageCap, total, false);
+    if (!g.upHost || !g.upDev || !g.stage)
+        return -1;
+    IngestDesc* descs = reinterpret_cast<IngestDesc*>(g.upHost);
     size_t off = 0;
     for (unsigned i = 0; i < count; ++i) {
         std::memset(&descs[i], 0, sizeof(IngestDesc));
         descs[i].src = (uint64_t)(uintptr_t)srcs[i];
         descs[i].bytes = bytes[i];
-        descs[i].dst = (uint64_t)(uintptr_t)cDev_ + off;
+        descs[i].dst = (uint64_t)(uintptr_t)g.stage + off;
         off = align16(off + bytes[i]);
     }
-    if (!be_gather(descs, cUpDev_, count, cDev_, pinnedOut, total)) {
+    void* packed = nullptr;
+    if (!be_gather(descs, g.upDev, count, g.stage, pinnedOut, total, &packed, &g.landed)) {
         failed_.store(true, std::memory_order_relaxed);
-        return false;
+        return -1;
     }
-    return true;
+    g.ticket = ticket;
+    // later submissions may overwrite the sources (recycled buffers, the
+    // next encode's packet): their device work waits for the packing
+    std::lock_guard<std::mutex> q(qMu_);
+    pendingMarks_.push_back(packed);
+    return ticket;
+}
+
+bool Engine::gather_wait(int64_t ticket)
+{
+    std::lock_guard<std::mutex> lk(gatherMu_);
+    bool ok = true;
+    for (GatherSlot& g : gslots_)
+        if (g.landed && g.ticket <= ticket)
+            ok = gather_land(g) && ok;
+    return ok && !failed();
+}
+
+bool Engine::gather_completed(unsigned count, const void* const* srcs, const unsigned* bytes,
+                              void* pinnedOut)
+{
+    const int64_t t = gather_async(count, srcs, bytes, pinnedOut);
+    return t > 0 && gather_wait(t);
 }
 
 bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* bytes, void* hostOut)

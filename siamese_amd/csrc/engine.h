@@ -317,6 +317,14 @@ public:
     /// Range i lands at the 16-byte aligned running offset (see
     /// sgpu_gather_completed).
     bool gather_completed(unsigned count, const void* const* srcs, const unsigned* bytes, void* pinnedOut);
+    /// The same without waiting for the copy: returns a gather ticket (> 0,
+    /// or -1 on failure).  The sources are read before any later submission's
+    /// device work runs (it waits for them on the device), so the caller may
+    /// go on driving the instances that own them; pinnedOut is filled once
+    /// gather_wait(ticket) returns true.
+    int64_t gather_async(unsigned count, const void* const* srcs, const unsigned* bytes, void* pinnedOut);
+    /// Wait until gather `ticket` and every earlier one have landed.
+    bool gather_wait(int64_t ticket);
     /// Host -> device copy on the staging stream, issued now; every later
     /// submission's device work waits for it (the host does not).  The caller
     /// guarantees that no unfinished submission touches dst.
@@ -425,12 +433,21 @@ private:
     uint8_t* gHost_ = nullptr;
     uint8_t* gDev_ = nullptr;
     size_t gCap_ = 0;
-    // gather_completed buffers (gatherMu_)
-    uint8_t* cUpHost_ = nullptr;
-    uint8_t* cUpDev_ = nullptr;
-    size_t cUpCap_ = 0;
-    uint8_t* cDev_ = nullptr;
-    size_t cCap_ = 0;
+    // gather_async slots, one per gather in flight (gatherMu_): descriptor
+    // upload and packing area, reused once the slot's previous gather landed
+    static constexpr unsigned kGatherSlots = 4;
+    struct GatherSlot
+    {
+        uint8_t* upHost = nullptr;
+        uint8_t* upDev = nullptr;
+        size_t upCap = 0;
+        uint8_t* stage = nullptr;
+        size_t stageCap = 0;
+        void* landed = nullptr;   // mark passed once the host bytes are in place
+        int64_t ticket = 0;
+    } gslots_[kGatherSlots];
+    int64_t gNext_ = 0;
+    bool gather_land(GatherSlot& g);
 };
 
 /// Per-host-thread engine state.  Only its owning thread touches it between

@@ -52,4 +52,68 @@ private:
     }
 };
 
+/// Per-thread stash of objects that hold reusable heap capacity (cleared
+/// vectors) for the next instance of a codec created on the same thread, and
+/// of the empty shells such an object leaves once its capacity is taken.
+template <class T>
+class CapStash
+{
+public:
+    /// An object holding capacity, or null.
+    static T* take()
+    {
+        Lists& l = lists();
+        if (l.full.empty())
+            return nullptr;
+        T* p = l.full.back();
+        l.full.pop_back();
+        return p;
+    }
+    static void give(T* p)
+    {
+        Lists& l = lists();
+        if (l.full.size() < kMax)
+            l.full.push_back(p);
+        else
+            delete p;
+    }
+    /// An object whose members are all empty (to fill and give back).
+    static T* shell()
+    {
+        Lists& l = lists();
+        if (l.shells.empty())
+            return new T;
+        T* p = l.shells.back();
+        l.shells.pop_back();
+        return p;
+    }
+    static void put_shell(T* p)
+    {
+        Lists& l = lists();
+        if (l.shells.size() < kMax)
+            l.shells.push_back(p);
+        else
+            delete p;
+    }
+
+private:
+    static constexpr size_t kMax = 1u << 12;
+    struct Lists
+    {
+        std::vector<T*> full, shells;
+        ~Lists()
+        {
+            for (T* p : full)
+                delete p;
+            for (T* p : shells)
+                delete p;
+        }
+    };
+    static Lists& lists()
+    {
+        thread_local Lists l;
+        return l;
+    }
+};
+
 } // namespace sgpu

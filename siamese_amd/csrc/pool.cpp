@@ -11,11 +11,13 @@ namespace sgpu {
 
 namespace {
 // SIAMESE_AMD_WORKER_NICE overrides (0 = same priority as the engine threads)
-// pause iterations a worker (or a joining caller) spins before blocking;
-// SIAMESE_AMD_POOL_SPIN overrides (0 = block at once)
+// pause iterations a worker (or a joining caller) spins before blocking
+// (SIAMESE_AMD_POOL_SPIN).  Off by default: on the MI355X box's host share,
+// spinning workers slowed the codec stepping they share the cores with
+// (A/B); it helps on hosts with idle cores.
 const unsigned kSpin = [] {
     const char* v = std::getenv("SIAMESE_AMD_POOL_SPIN");
-    return v ? (unsigned)std::atoi(v) : 4096u;
+    return v ? (unsigned)std::atoi(v) : 0u;
 }();
 inline void cpu_relax()
 {
@@ -78,8 +80,8 @@ void WorkerPool::loop()
     uint64_t seen = 0;
     for (;;) {
         // Fork-joins come in quick succession (one per job round and per
-        // assembly pass): spin a short while for the next one before
-        // sleeping, so a worker joins it without a futex wake-up.
+        // assembly pass): optionally spin a short while for the next one
+        // before sleeping, so a worker joins it without a futex wake-up.
         for (unsigned k = 0; k < kSpin && gen_.load(std::memory_order_acquire) == seen &&
                              !stop_.load(std::memory_order_relaxed);
              ++k)

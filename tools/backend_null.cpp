@@ -97,9 +97,12 @@ void* be_stage_h2d(void* dst, const void* src, size_t bytes)
 }
 void be_wait_mark(void*) {}
 void be_mark_release(void*) {}
+bool be_mark_sync(void*) { return true; }
+// (synchronous here: both marks are passed on return)
 bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, const void* devStage,
-               void* hostOut, size_t bytes)
+               void* hostOut, size_t bytes, void** packed, void** landed)
 {
+    *packed = *landed = reinterpret_cast<void*>(1);
     std::memcpy(descsDev, descsHost, (size_t)count * sizeof(IngestDesc));
     (void)count;
     std::memcpy(hostOut, devStage, bytes);

@@ -13,7 +13,28 @@ import scenario_lib as S  # noqa: E402
 import bench  # noqa: E402
 
 
+def pcie_rates(nbytes):
+    """H2D / D2H GB/s of one pinned copy of `nbytes` (torch, the current GPU)."""
+    import time
+    import torch
+    if not torch.cuda.is_available():
+        return None
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    out = []
+    for src, dst in ((h, d), (d, h)):
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(3):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        out.append(round(3 * nbytes / (time.perf_counter() - t) / 1e9, 1))
+    return out
+
+
 def main():
+    print("pinned H2D/D2H GB/s (367 MB):", pcie_rates(367 << 20), flush=True)
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     lib = os.environ.get("SGPU_LIB", os.path.join(ROOT, "siamese_amd", "libsiamese_amd.so"))
     cfg = bench.workload(0, 1024)
