@@ -123,13 +123,16 @@ def engine_bytes(rep):
 
 def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu_sample):
     """One extra BASELINE config on one GPU: a verified warm-up, then `runs`
-    timed runs; the reference on the host beside it."""
+    timed runs; the reference on the host beside it.  Multi-stream configs
+    run in 4 stream groups pipelined like the headline workload (one group's
+    host work beside another's device work); a single stream is one group."""
+    groups = 4 if cfg.streams >= 64 else 1
     sess = S.BatchSession(library, cfg, device=device)
     try:
-        res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=1)
+        res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=groups)
         if rep.mismatches or any(r.status for r in res):
             raise RuntimeError("bench leg %s: verification failed" % name)
-        res, rep = sess.run(steps=runs, warmup=0, verify=False, threads=threads, groups=1,
+        res, rep = sess.run(steps=runs, warmup=0, verify=False, threads=threads, groups=groups,
                             digest=False)
     finally:
         sess.close()
@@ -143,6 +146,7 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
             cfg.streams, "s" if cfg.streams > 1 else "", cfg.originals, cfg.payload_bytes,
             cfg.loss_pct),
         "runs": runs,
+        "stream_groups": groups,
         "ms_per_run": round(sec / runs * 1e3, 3),
         "value": round(alg / sec / 1e9, 3),
         "unit": "GB/s",

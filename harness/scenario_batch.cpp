@@ -379,6 +379,10 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
         g.reqs.swap(reqs);
     sh.gathers.push_back(std::move(g));
     reqs.clear();
+    // SCENARIO_SYNC_GATHER=1: land every gather at once (debugging aid)
+    static const bool syncGather = std::getenv("SCENARIO_SYNC_GATHER") != nullptr;
+    if (syncGather)
+        land_gathers(sh);
 }
 
 // fn(i) for i in [0, count), blocks of a few streams per pool task: on the
@@ -419,6 +423,7 @@ struct Job
     std::unique_ptr<BatchStream[]> streams;
     std::vector<unsigned> live;     // indices into codecs/streams
     long long ticket = 0;           // its latest submission
+    bool collected = false;         // that submission's tokens already gathered
 };
 
 int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* rounds,
@@ -479,8 +484,27 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
         for (BatchCodec& c : J.codecs)
             std::swap(c.prev, c.cur);
     };
+    std::vector<std::unique_ptr<Job>> active;
+    // Gather the tokens of every job whose latest submission has completed.
+    // Runs before each submission: buffers a completed submission released
+    // (a decoder's delivered slots, a freed codec's symbols) are free for any
+    // job's next allocation, so the bytes a token names must be read before
+    // any later submission, whose device work waits for the gather's reads,
+    // can rewrite them.
+    auto collect_all = [&]() {
+        for (auto& a : active) {
+            Job& J = *a;
+            if (J.collected || api.query(J.ticket) != 1)
+                continue;
+            std::vector<Request> reqs = take(J, true);
+            resolve_requests(sh, reqs);
+            J.collected = true;
+        }
+    };
     auto submit = [&](Job& J) {
+        collect_all();
         J.ticket = api.enqueue();
+        J.collected = false;
         if (timeline)
             std::fprintf(stderr, "tl submit j%d t%lld live %zu\n", curJob, J.ticket, J.live.size());
         ++*rounds;
@@ -504,7 +528,6 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
 
     const unsigned jobs = nsteps * G;
     const size_t depth = G + 1;   // jobs in flight
-    std::vector<std::unique_ptr<Job>> active;
     unsigned next = 0;
     int rc = 0;
     // Host work is done whenever some is available: a job whose submission
@@ -526,8 +549,12 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 continue;
             }
             did = true;
-            std::vector<Request> reqs = take(J, true);
-            resolve_requests(sh, reqs);
+            std::vector<Request> reqs;
+            if (!J.collected) {
+                reqs = take(J, true);
+                resolve_requests(sh, reqs);
+                J.collected = true;
+            }
             lap(3);
             if (!J.live.empty()) {
                 advance(J);

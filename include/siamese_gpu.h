@@ -18,6 +18,15 @@
     sgpu_decode carry device pointers whose DataBytes are exact after the
     next sgpu_flush() (they read 0 until then).
 
+    Device pointer lifetime: a symbol an instance drops (a decoder sliding its
+    window past delivered packets, a freed instance) is recycled once the
+    submission holding that call has completed, and any later submission may
+    then rewrite it.  Read (sgpu_gather_async / sgpu_gather_completed) the
+    bytes behind a pointer from sgpu_decode, sgpu_decoder_get or sgpu_encode
+    after the submission that produced them completes and before the next
+    submission is enqueued; the gather's reads are ordered before that
+    submission's device work.
+
     Threading: instances may be driven from many host threads at once, each
     instance by one thread at a time (handing a recovery packet to a decoder
     also touches the encoder that produced it).  Per-instance calls take no
