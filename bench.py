@@ -49,7 +49,7 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 STREAMS_PER_GPU = 1024
 METRIC = "device-resident GB/s encode+decode, 1400B pkts @20% loss; % HBM peak"
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2g_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2j_traffic.json")
 
 
 def pmc_traffic(kernel):
@@ -123,10 +123,10 @@ def engine_bytes(rep):
 
 def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu_sample):
     """One extra BASELINE config on one GPU: a verified warm-up, then `runs`
-    timed runs; the reference on the host beside it.  Multi-stream configs
-    run in 4 stream groups pipelined like the headline workload (one group's
-    host work beside another's device work); a single stream is one group."""
-    groups = 4 if cfg.streams >= 64 else 1
+    timed runs; the reference on the host beside it.  Every leg runs as one
+    stream group: for C2, 2 or 4 pipelined groups were not faster (more,
+    smaller launches doubled its device time; tools/c2_groups.sh)."""
+    groups = 1
     sess = S.BatchSession(library, cfg, device=device)
     try:
         res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=groups)
