@@ -714,7 +714,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         const uint32_t n = uni(h0.z), valid = uni(h0.w);
         const uint32_t kind = uni(h1.x);
         uint32_t itemWords = kOpWords;
-        if (kind == OP_LINCOMB || kind == OP_ROWS || kind == OP_COPIES)
+        if (kind == OP_LINCOMB || kind == OP_ROWS || kind == OP_COPIES || kind == OP_LINCOMBS)
             itemWords += uni(h1.w);
         const uint32_t next = pos + itemWords;
         // prefetch the next op's block while this one runs
@@ -1329,6 +1329,42 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 atomicAdd(&g_phaseClk[11], (unsigned long long)E);
                 atomicAdd(&g_phaseClk[12], (unsigned long long)staged);
 #endif
+            }
+        } else if (kind == OP_LINCOMBS) {
+            // independent combinations, whole items per wave: each wave
+            // streams its item's terms (kExecDepth loads in flight) and
+            // stores it, no barrier until the batch ends
+            for (uint32_t k = wave; k < n; k += kExecWaves) {
+                const uint32_t iw = kOpWords + k * kLcWords;
+                const uint4 w0 = op_word(rb, seg, pos, iw);
+                const uint4 w1 = op_word(rb, seg, pos, iw + 1);
+                const uint64_t idst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                const uint32_t in = uni(w0.z), ivalid = uni(w0.w);
+                const uint32_t ts = uni(w1.x), tc = uni(w1.y), mixLit = uni(w1.z);
+                const uint32_t imix = mixLit & 0xffu, litLen = (mixLit >> 8) & 0xffu;
+                if (tileBase < align16u(in)) {   // uniform: the item reaches this tile
+                    const uint32_t c0 = load_cur(p, idst, in, ivalid);
+                    uint32_t acc0 = 0, acc1 = 0;
+                    uint4 dv = make_uint4(0, 0, 0, 0);
+                    gather(0, tc, tileBase, p, acc0, acc1,
+                           [&](uint32_t t, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                               const uint32_t j = t & 63u;
+                               if (j == 0) {
+                                   const uint32_t idx = t + lane;
+                                   dv = idx < tc ? op_word(rb, seg, pos, kOpWords + ts + idx)
+                                                 : make_uint4(0, 0, 0, 0);
+                               }
+                               lane_term(dv, j, src, len);
+                               ca = rl(dv.w, j);
+                               return true;
+                           });
+                    store_item(acc0 ^ (imix > 1 ? gf_mul_dword(acc1, imix) : acc1), p, idst, in, ivalid, c0);
+                }
+                if (litLen) {
+                    // the footer after its combination (same lanes, in order)
+                    const uint4 w2 = op_word(rb, seg, pos, iw + 2);
+                    store_literal(p, idst, uni(w1.w), litLen, uni(w2.x), uni(w2.y));
+                }
             }
         } else if (kind == OP_COPIES) {
             // kCopyBatch copies per wave at a time, all their loads in flight

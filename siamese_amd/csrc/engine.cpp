@@ -95,6 +95,7 @@ void ProgramBody::clear()
     rb.updates.clear();
     rb.rows.clear();
     copies.clear();
+    lcb.clear();
 }
 
 void ProgramBody::new_segment()
@@ -124,8 +125,127 @@ void ProgramBody::rows_open(uint32_t base, bool keepWindow)
     rb.maxExtent = 0;
 }
 
+namespace {
+// [a, a + an) and [b, b + bn) share a byte
+inline bool overlaps(uint64_t a, uint64_t an, uint64_t b, uint64_t bn) { return a < b + bn && b < a + an; }
+inline uint64_t lane_span(uint32_t n) { return ((uint64_t)n + 15) & ~(uint64_t)15; }
+} // namespace
+
+void ProgramBody::lc_seal()
+{
+    if (lcb.items.empty())
+        return;
+    Segment& s = segs[nsegs - 1];
+    if (lcb.items.size() == 1) {
+        // one combination: the plain op (all waves share its terms)
+        const LcItem& it = lcb.items[0];
+        GfOp op;
+        std::memset(&op, 0, sizeof(op));
+        op.dst = it.dst;
+        op.n = it.n;
+        op.valid = it.valid;
+        op.kind = OP_LINCOMB;
+        op.mix = it.mixLit & 0xff;
+        op.termBegin = (uint32_t)s.terms.size();
+        op.termCount = it.termCount;
+        s.ops.push_back(op);
+        s.terms.insert(s.terms.end(), lcb.terms.begin(), lcb.terms.end());
+        const uint32_t litLen = (it.mixLit >> 8) & 0xff;
+        if (litLen) {
+            GfOp lo;
+            std::memset(&lo, 0, sizeof(lo));
+            lo.dst = it.dst;
+            lo.n = it.litOffset;
+            lo.valid = litLen;
+            lo.kind = OP_LITERAL;
+            std::memcpy(lo.lit, it.lit, litLen);
+            s.ops.push_back(lo);
+        }
+        lcb.clear();
+        return;
+    }
+    const uint32_t itemWords = (uint32_t)lcb.items.size() * kLcWords;
+    for (LcItem& it : lcb.items)
+        it.termStart += itemWords;   // (block-relative word of its first term)
+    GfOp op;
+    std::memset(&op, 0, sizeof(op));
+    op.kind = OP_LINCOMBS;
+    op.n = (uint32_t)lcb.items.size();
+    op.termBegin = (uint32_t)(s.rowsData.size() / 16);
+    op.termCount = itemWords + (uint32_t)lcb.terms.size();
+    s.ops.push_back(op);
+    const size_t at = s.rowsData.size();
+    s.rowsData.resize(at + (size_t)op.termCount * 16);
+    std::memcpy(s.rowsData.data() + at, lcb.items.data(), lcb.items.size() * sizeof(LcItem));
+    std::memcpy(s.rowsData.data() + at + lcb.items.size() * sizeof(LcItem), lcb.terms.data(),
+                lcb.terms.size() * sizeof(GfTerm));
+    s.rowsWords += op.termCount;
+    lcb.clear();
+}
+
+void ProgramBody::lc_absorb()
+{
+    // SIAMESE_AMD_LC_BATCH=0: every combination stays a plain op (A/B aid)
+    static const bool enabled = [] {
+        const char* v = std::getenv("SIAMESE_AMD_LC_BATCH");
+        return !v || std::atoi(v) != 0;
+    }();
+    if (!enabled)
+        return;
+    Segment& s = segs[nsegs - 1];
+    const GfOp op = s.ops.back();
+    const GfTerm* t = s.terms.data() + op.termBegin;
+    if (op.termCount > kLcMaxTerms) {
+        // stays a plain op; the batch before it is sealed ahead of it
+        s.ops.pop_back();
+        lc_seal();
+        s.ops.push_back(op);
+        return;
+    }
+    // independent of every item of the open batch?  (writes: [dst,
+    // align16(n)) and the literal; reads: the terms and dst's kept bytes)
+    bool indep = lcb.items.size() < kLcMaxItems;
+    const uint64_t w = lane_span(op.n);
+    for (size_t i = 0; indep && i < lcb.items.size(); ++i) {
+        const LcItem& it = lcb.items[i];
+        const uint32_t litEnd = it.litOffset + ((it.mixLit >> 8) & 0xff);
+        const uint64_t iw = std::max<uint64_t>(lane_span(it.n), litEnd);
+        if (overlaps(op.dst, w, it.dst, iw)) {
+            indep = false;
+            break;
+        }
+        for (uint32_t k = 0; k < op.termCount; ++k)
+            if (overlaps(t[k].src, lane_span(t[k].len), it.dst, iw)) {
+                indep = false;
+                break;
+            }
+        const GfTerm* u = lcb.terms.data() + it.termStart;
+        for (uint32_t k = 0; indep && k < it.termCount; ++k)
+            if (overlaps(u[k].src, lane_span(u[k].len), op.dst, w))
+                indep = false;
+    }
+    // (its terms are the segment's last: move them out before a seal of a
+    // single-item batch appends that item's terms to the segment)
+    lcScratch.assign(t, t + op.termCount);
+    s.terms.resize(op.termBegin);
+    s.ops.pop_back();
+    if (!indep)
+        lc_seal();
+    LcItem it;
+    std::memset(&it, 0, sizeof(it));
+    it.dst = op.dst;
+    it.n = op.n;
+    it.valid = op.valid;
+    it.termStart = (uint32_t)lcb.terms.size();
+    it.termCount = op.termCount;
+    it.mixLit = op.mix & 0xff;
+    lcb.items.push_back(it);
+    lcb.terms.insert(lcb.terms.end(), lcScratch.begin(), lcScratch.end());
+}
+
 void ProgramBody::rows_close()
 {
+    lc_seal();
     if (!copies.empty()) {
         // seal the open copy batch
         Segment& g = segs[nsegs - 1];
@@ -251,7 +371,11 @@ void Program::attach()
 void Program::lc_begin(uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix)
 {
     touch();
-    b_->rows_close();
+    if (b_->rb.open || !b_->copies.empty()) {
+        // (an open OP_LINCOMBS batch stays open: lc_end decides)
+        b_->lc_seal();
+        b_->rows_close();
+    }
     if (b_->nsegs == 0)
         b_->new_segment();
     ProgramBody::Segment& s = b_->segs[b_->nsegs - 1];
@@ -277,6 +401,7 @@ void Program::lc_end()
     }
     if (op.n > s.maxExtent)
         s.maxExtent = op.n;
+    b_->lc_absorb();
 }
 
 void Program::add_mem(uint64_t dst, uint64_t src, uint32_t n)
@@ -319,6 +444,19 @@ void Program::literal(uint64_t dst, uint32_t offset, const uint8_t* bytes, uint3
     if (len == 0)
         return;
     touch();
+    if (!b_->lcb.items.empty()) {
+        // a footer right after its combination joins that batch item
+        LcItem& it = b_->lcb.items.back();
+        if (it.dst == dst && (it.mixLit >> 8) == 0 && len <= 8) {
+            it.mixLit |= len << 8;
+            it.litOffset = offset;
+            std::memcpy(it.lit, bytes, len);
+            ProgramBody::Segment& s = b_->segs[b_->nsegs - 1];
+            if (offset + len > s.maxExtent)
+                s.maxExtent = offset + len;
+            return;
+        }
+    }
     b_->rows_close();
     if (b_->nsegs == 0)
         b_->new_segment();
@@ -1269,7 +1407,7 @@ void Engine::assemble_batch(Batch& bt)
                     const GfOp& op = s.ops[oi];
                     std::memcpy(w, &op, sizeof(GfOp));
                     w += sizeof(GfOp);
-                    if (op.kind == OP_ROWS || op.kind == OP_COPIES) {
+                    if (op.kind == OP_ROWS || op.kind == OP_COPIES || op.kind == OP_LINCOMBS) {
                         const size_t bytes = (size_t)op.termCount * 16;   // block (rows_close)
                         std::memcpy(w, s.rowsData.data() + (size_t)op.termBegin * 16, bytes);
                         // wide rows of this batch: their scratch pair as the

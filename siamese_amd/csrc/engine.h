@@ -116,8 +116,29 @@ struct ProgramBody
     std::vector<Completion> callbacks;
     RowsBuild rb;
     std::vector<CopyItem> copies;       // the open OP_COPIES batch (segment's last op)
+    /// The open OP_LINCOMBS batch (ops.h): independent combinations waiting
+    /// to be sealed as one op after the segment's last op.
+    struct LcBuild
+    {
+        std::vector<LcItem> items;
+        std::vector<GfTerm> terms;   // termStart: index into this, made block-relative on seal
+        void clear()
+        {
+            items.clear();
+            terms.clear();
+        }
+    } lcb;
+    std::vector<GfTerm> lcScratch;
+    void lc_seal();                     // seals the open OP_LINCOMBS batch
+    /// Move the segment's last op (an OP_LINCOMB) into the open batch, or
+    /// seal the batch first when they are not independent.
+    void lc_absorb();
 
-    bool empty() const { return nsegs == 0 || (nsegs == 1 && segs[0].ops.empty() && copies.empty() && !rb.open); }
+    bool empty() const
+    {
+        return nsegs == 0 ||
+               (nsegs == 1 && segs[0].ops.empty() && copies.empty() && lcb.items.empty() && !rb.open);
+    }
     void new_segment();
     void rows_open(uint32_t base, bool keepWindow);
     void rows_close();   // closes the open OP_ROWS or OP_COPIES batch

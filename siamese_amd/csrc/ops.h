@@ -33,6 +33,7 @@ enum GfOpKind : uint32_t
     OP_LITERAL = 2,   // dst[n, n+valid) = literal bytes (<= 8)
     OP_ROWS = 3,      // a batch of Siamese rows of one codec (sum updates, rows)
     OP_COPIES = 4,    // independent copies dst[0,len) = src[0,len)
+    OP_LINCOMBS = 5,  // independent OP_LINCOMBs (+ footer literals), one per wave
 };
 
 /// One op.  For OP_LINCOMB:
@@ -181,6 +182,31 @@ struct CopyItem
 static_assert(sizeof(CopyItem) == 32, "CopyItem layout");
 constexpr unsigned kCopyWords = sizeof(CopyItem) / 16;
 
+/// OP_LINCOMBS: n mutually independent linear combinations (no item reads or
+/// writes bytes another item of the batch writes), each optionally followed
+/// by a literal (a recovery packet's footer) on its own dst.  After the GfOp
+/// header (termCount = the block's words): n LcItem (3 words each), then the
+/// items' GfTerm words; termStart is an item's first term word within the
+/// block.  The executor gives each wave whole items, so a run of small
+/// combinations (Cauchy / parity rows of a short window, reference
+/// SiameseEncoder.cpp:1334-1441, and the decoder's elimination of received
+/// originals from each recovery packet, SiameseDecoder.cpp:812-1063) costs
+/// one memory round trip and one barrier instead of one per combination.
+struct LcItem
+{
+    uint64_t dst;
+    uint32_t n, valid;           // as OP_LINCOMB
+    uint32_t termStart, termCount;
+    uint32_t mixLit;             // mix | litLen << 8
+    uint32_t litOffset;          // literal at dst + litOffset (litLen <= 8)
+    uint8_t lit[8];
+    uint32_t pad[2];
+};
+static_assert(sizeof(LcItem) == 48, "LcItem layout");
+constexpr unsigned kLcWords = sizeof(LcItem) / 16;
+constexpr unsigned kLcMaxTerms = 64;    // larger combinations keep all waves on one op
+constexpr unsigned kLcMaxItems = 256;
+
 /// PCG-XSH-RR as the reference seeds it (SiameseTools.h:80-102).
 constexpr uint64_t kPcgMul = 6364136223846793005ULL;
 
@@ -188,7 +214,9 @@ inline uint32_t op_words(const GfOp& op)
 {
     // (an OP_ROWS header's termCount is its whole block in words)
     return kOpWords +
-           ((op.kind == OP_LINCOMB || op.kind == OP_ROWS || op.kind == OP_COPIES) ? op.termCount : 0);
+           ((op.kind == OP_LINCOMB || op.kind == OP_ROWS || op.kind == OP_COPIES || op.kind == OP_LINCOMBS)
+                ? op.termCount
+                : 0);
 }
 
 /// Executor work item: one (instance segment, byte tile).

@@ -173,6 +173,27 @@ void exec_tile(const uint8_t* stream, const ExecItem& it, uint64_t* acct)
             lincomb_tile(op.dst, op.n, op.valid, op.mix, terms, t0);
             continue;
         }
+        if (op.kind == OP_LINCOMBS) {
+            const LcItem* items = reinterpret_cast<const LcItem*>(body);
+            const GfTerm* words = reinterpret_cast<const GfTerm*>(body);
+            if (body + (size_t)op.termCount * 16 != w)
+                std::abort(); // malformed block
+            for (uint32_t i = 0; i < op.n; ++i) {
+                const LcItem& it = items[i];
+                if (it.termStart + it.termCount > op.termCount)
+                    std::abort();
+                terms.clear();
+                for (uint32_t k = 0; k < it.termCount; ++k) {
+                    const GfTerm& g = words[it.termStart + k];
+                    terms.push_back(TileTerm{g.src, g.len, g.coeff, g.acc});
+                }
+                lincomb_tile(it.dst, it.n, it.valid, (uint8_t)(it.mixLit & 0xff), terms, t0);
+                const uint32_t litLen = (it.mixLit >> 8) & 0xff;
+                if (litLen)
+                    literal_tile(it.dst, it.litOffset, it.lit, litLen, t0);
+            }
+            continue;
+        }
         if (op.kind == OP_COPIES) {
             const CopyItem* cs = reinterpret_cast<const CopyItem*>(body);
             if (reinterpret_cast<const uint8_t*>(cs + op.n) != w)
