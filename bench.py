@@ -49,7 +49,7 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 STREAMS_PER_GPU = 1024
 METRIC = "device-resident GB/s encode+decode, 1400B pkts @20% loss; % HBM peak"
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2j_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2k_traffic.json")
 
 
 def pmc_traffic(kernel):
@@ -171,6 +171,42 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
     return out
 
 
+def dropin_leg(library, use_cpu, runs=5):
+    """C1 through the drop-in siamese.h ABI: one stream, every call
+    synchronous with its own flush, as a caller of the reference API sees it
+    (latency per call, not throughput).  The reference on one core beside it."""
+    cfg = S.replace(S.CONFIGS["C1"], hash_data=0)
+
+    def measure(lib):
+        S.run_capi(lib, cfg)   # warm
+        wall = codec = 0.0
+        calls = 0
+        for _ in range(runs):
+            res, sec, w = S.run_capi(lib, cfg)
+            if any(r.status for r in res):
+                raise RuntimeError("drop-in leg: stream failed (%s)" % lib)
+            wall += w
+            codec += sec
+            for r in res:
+                # encoder adds + decoder adds, encodes + recovery adds,
+                # decodes, in-order deliveries (get)
+                calls += (2 * cfg.originals - r.originals_lost + 2 * r.encodes - r.recovery_lost +
+                          r.decode_calls + r.delivered)
+        return {"ms_per_run": round(wall / runs * 1e3, 3),
+                "codec_ms_per_run": round(codec / runs * 1e3, 3),
+                "calls_per_run": calls // runs,
+                "us_per_call": round(codec / max(1, calls) * 1e6, 3)}
+
+    out = {"workload": "C1 through siamese.h (1 stream x 200 x 1400 B, 10% loss, acks)", "runs": runs}
+    out.update(measure(library))
+    out["cpu_baseline"] = None
+    if use_cpu and os.path.exists(S.REF_LIB):
+        ref = measure(S.REF_LIB)
+        ref.update({"cores": 1, "kind": "reference"})
+        out["cpu_baseline"] = ref
+    return out
+
+
 def legs(library, device, threads, use_cpu):
     cpu_threads = min(16, os.cpu_count() or 1)
     specs = [
@@ -191,6 +227,7 @@ def legs(library, device, threads, use_cpu):
     for name, cfg, runs, cpu_cfg, cpu_thr, sample in specs:
         out[name] = run_leg(name, library, cfg, device, threads, runs,
                             cpu_cfg if use_cpu else None, cpu_thr, sample)
+    out["dropin_C1"] = dropin_leg(library, use_cpu)
     return out
 
 
