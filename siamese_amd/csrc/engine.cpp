@@ -1027,6 +1027,7 @@ struct Batch
     };
     std::vector<Download> downloads;
     std::vector<void*> marks;              // staged copies its device work waits for
+    bool assembled = false;                // laid out (by enqueue, or by the launcher)
 };
 
 namespace {
@@ -1127,14 +1128,21 @@ uint64_t Engine::enqueue()
         std::lock_guard<std::mutex> g(qMu_);
         b->marks.swap(pendingMarks_);
     }
-    {
-        // this ticket's transfer set must be free (its previous user done)
-        std::unique_lock<std::mutex> lk(qMu_);
-        setCv_.wait(lk, [&] { return stop_ || sets_[b->set].busyTicket == 0; });
-        sets_[b->set].busyTicket = ticket;
+    // The batch is laid out here, on the caller's thread and the shared
+    // pool.  SIAMESE_AMD_ASYNC_ASSEMBLY=1 hands it to the launcher thread and
+    // its own pool instead, so the caller goes back to driving instances at
+    // once; on the MI355X box's 16-core host share that only moved the same
+    // CPU work beside the stepping threads (same-box A/B), so
+    // it is off by default.
+    static const bool asyncAssembly = [] {
+        const char* v = std::getenv("SIAMESE_AMD_ASYNC_ASSEMBLY");
+        return v && std::atoi(v) != 0;
+    }();
+    if (!asyncAssembly) {
+        claim_set(*b);
+        assemble_batch(*b, pool());
+        tl("assembled", ticket);
     }
-    assemble_batch(*b);
-    tl("assembled", ticket);
     {
         std::lock_guard<std::mutex> g(qMu_);
         toLaunch_.push_back(b);   // (b belongs to the pipeline from here on)
@@ -1170,6 +1178,11 @@ void Engine::launcher_loop()
             b = toLaunch_.front();
             toLaunch_.pop_front();
         }
+        if (!b->assembled && !failed()) {
+            claim_set(*b);
+            assemble_batch(*b, asm_pool());
+            tl("assembled", b->ticket);
+        }
         tl("launch begin", b->ticket);
         if (!failed())
             launch_batch(*b);
@@ -1188,8 +1201,29 @@ void Engine::launcher_loop()
 //   2. a sequential pass fixes every segment's place in the upload and its
 //      work items, and every solve's place in the result array;
 //   3. segments, solve data and ingest descriptors are copied (parallel).
-void Engine::assemble_batch(Batch& bt)
+void Engine::claim_set(Batch& b)
 {
+    // this ticket's transfer set must be free (its previous user done)
+    std::unique_lock<std::mutex> lk(qMu_);
+    setCv_.wait(lk, [&] { return stop_ || sets_[b.set].busyTicket == 0; });
+    sets_[b.set].busyTicket = b.ticket;
+}
+
+WorkerPool& Engine::asm_pool()
+{
+    // the launcher's own pool: the application may be running a fork-join
+    // on pool() while a batch is laid out (SIAMESE_AMD_ASM_THREADS, default 8)
+    if (!asmPool_) {
+        const char* v = std::getenv("SIAMESE_AMD_ASM_THREADS");
+        const int n = v ? std::atoi(v) : 8;
+        asmPool_.reset(new WorkerPool((unsigned)std::max(1, std::min(64, n))));
+    }
+    return *asmPool_;
+}
+
+void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
+{
+    bt.assembled = true;
     const uint64_t t0 = now_ns();
     XferSet& xs = sets_[bt.set];
     EngineStats& st = bt.st;
@@ -1205,7 +1239,7 @@ void Engine::assemble_batch(Batch& bt)
     const bool parallel = approxWords >= kParallelWords;
     auto run = [&](size_t n, const std::function<void(size_t)>& fn) {
         if (parallel)
-            pool().run(n, fn);
+            wp.run(n, fn);
         else
             for (size_t i = 0; i < n; ++i)
                 fn(i);
@@ -1572,7 +1606,8 @@ void Engine::completer_loop()
         tl("complete end", b->ticket);
         {
             std::lock_guard<std::mutex> g(qMu_);
-            sets_[b->set].busyTicket = 0;
+            if (sets_[b->set].busyTicket == b->ticket)   // (a failed batch may never have claimed it)
+                sets_[b->set].busyTicket = 0;
             doneTicket_ = b->ticket;
         }
         setCv_.notify_all();

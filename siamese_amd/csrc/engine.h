@@ -378,7 +378,9 @@ private:
     // ---- flush pipeline
     void launcher_loop();
     void completer_loop();
-    void assemble_batch(Batch& b);
+    void assemble_batch(Batch& b, WorkerPool& wp);
+    void claim_set(Batch& b);
+    WorkerPool& asm_pool();   // launcher thread only
     void launch_batch(Batch& b);
     void complete_batch(Batch& b);
     void start_threads();
@@ -423,6 +425,7 @@ private:
     bool stop_ = false;
     std::thread launcher_, completer_;
     std::unique_ptr<WorkerPool> pool_;
+    std::unique_ptr<WorkerPool> asmPool_;
 
     // transfer buffer sets: one per submission in flight (ticket % kSets)
     static constexpr unsigned kSets = 4;
