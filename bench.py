@@ -261,7 +261,9 @@ def run_rank(rank, world, local, args, library, use_cuda):
 
     # End-to-end (PCIe-inclusive) leg, timed separately: the originals start
     # in pinned host memory and every recovery packet and recovered original
-    # is copied back to the host.  Reported beside, never as, `value`.
+    # is copied back to the host (originals delivered intact are not: the
+    # application holds them in host memory already).  Reported beside, never
+    # as, `value`.
     e2e_elapsed = None
     if args.e2e:
         # (pipelined warm-up over both alternating device copies, every
@@ -382,7 +384,8 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "payload_GBps": round(payload_total / e2e_max / 1e9, 3),
             "ms_per_step": round(e2e_max / steps * 1e3, 3),
             "note": "originals H2D from pinned host memory each step; every recovery packet "
-                    "and recovered original D2H (PCIe-inclusive; not `value`)",
+                    "and recovered original D2H, originals delivered intact stay on the host "
+                    "(PCIe-inclusive; not `value`)",
         }
     if not args.no_cpu and world == 1:
         # the reference on the host cores, rank 0 at N=1 only, on a bounded

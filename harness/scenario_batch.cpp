@@ -274,7 +274,11 @@ struct BatchCodec
                 std::fprintf(stderr, "pkt_token: id %u entry %d bytes %u want %u data %p\n", id,
                              p.entry != nullptr, bytes, want, data);
             *ok = false;
-        } else if (sh->hashData || sh->verify || sh->e2e)
+        } else if (sh->hashData || sh->verify || (sh->e2e && p.entry))
+            // end-to-end mode copies back what exists only on the device: a
+            // recovered original (a decode output); a delivered original that
+            // arrived intact came from host memory, where the application
+            // still has it
             cur.push_back(Request{log, log->size(), data, bytes, id, true, ok});
         return bytes;
     }
