@@ -123,10 +123,12 @@ def engine_bytes(rep):
 
 def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu_sample):
     """One extra BASELINE config on one GPU: a verified warm-up, then `runs`
-    timed runs; the reference on the host beside it.  Every leg runs as one
-    stream group: for C2, 2 or 4 pipelined groups were not faster (more,
-    smaller launches doubled its device time; tools/c2_groups.sh)."""
-    groups = 1
+    timed runs; the reference on the host beside it.  C2's 1024 streams run
+    in two pipelined stream groups (one group's host work beside the other's
+    device work: 22.5-24.4 vs 25.0-26.6 ms per run with one group, same box,
+    profiles/r2l_c2_groups_ab.txt; four groups' smaller launches doubled the
+    device time); a single stream is one group."""
+    groups = 2 if cfg.streams >= 64 else 1
     sess = S.BatchSession(library, cfg, device=device)
     try:
         res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=groups)
