@@ -1394,6 +1394,12 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     bt.oWide = off;
     off = align16(off + nWide * sizeof(LdpcItem));
     bt.upBytes = off;
+    // SGPU_UPLOAD_STATS=1: one stderr line per flush, upload bytes by part (profiling aid)
+    static const bool upStats = std::getenv("SGPU_UPLOAD_STATS") != nullptr;
+    if (upStats)
+        std::fprintf(stderr, "upload %zu: stage %zu ingest %zu stream %zu items %zu solves %zu wide %zu\n",
+                     bt.upBytes, bt.oIngD - oStage, bt.oStream - bt.oIngD, bt.oItems - bt.oStream,
+                     bt.oSD - bt.oItems, bt.oWide - bt.oSD, bt.upBytes - bt.oWide);
     if (bt.upBytes)
         ensure_up(xs, bt.upBytes);
     if (wideBytes) {
