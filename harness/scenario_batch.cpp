@@ -395,7 +395,14 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
 template <class F>
 void for_streams(Shared& sh, size_t count, const F& fn)
 {
-    constexpr size_t kBlock = 4;
+    // streams per pool task (SCENARIO_BLOCK, default 2): small tasks keep a
+    // fork-join's tail short (same-box A/B, profiles/r2m_block_ab.txt:
+    // 7.04-7.36 ms/step with 2, 7.17-7.85 with 1, 7.84-8.82 with 4)
+    static const size_t kBlock = [] {
+        const char* v = std::getenv("SCENARIO_BLOCK");
+        const long b = v ? std::atol(v) : 2;
+        return (size_t)(b > 0 ? b : 2);
+    }();
     const size_t blocks = (count + kBlock - 1) / kBlock;
     auto body = [&](size_t b) {
         const size_t end = std::min(count, (b + 1) * kBlock);
