@@ -1048,6 +1048,20 @@ constexpr size_t kAcctBytes = 32;
 // below this many stream words a submission is assembled on the calling
 // thread alone (the drop-in API's per-call flushes)
 constexpr size_t kParallelWords = 1u << 16;
+// flush assembly task sizes (bodies sealed, segments, ingest records and
+// solves per pool task)
+#ifndef SGPU_SEAL_CHUNK
+#define SGPU_SEAL_CHUNK 32
+#endif
+#ifndef SGPU_SEG_CHUNK
+#define SGPU_SEG_CHUNK 16
+#endif
+#ifndef SGPU_INGEST_CHUNK
+#define SGPU_INGEST_CHUNK 8192
+#endif
+#ifndef SGPU_SOLVE_CHUNK
+#define SGPU_SOLVE_CHUNK 64
+#endif
 
 } // namespace
 
@@ -1246,8 +1260,10 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     };
 
     // ---- 1. seal -------------------------------------------------------------
-    run((totalBodies + 31) / 32, [&](size_t c) {
-        for (size_t i = c * 32; i < std::min(totalBodies, c * 32 + 32); ++i) {
+    // (task sizes: small enough that a fork-join's tail stays short)
+    constexpr size_t kSealChunk = SGPU_SEAL_CHUNK;
+    run((totalBodies + kSealChunk - 1) / kSealChunk, [&](size_t c) {
+        for (size_t i = c * kSealChunk; i < std::min(totalBodies, c * kSealChunk + kSealChunk); ++i) {
             const size_t n0 = bt.bodies[0].size();
             (i < n0 ? bt.bodies[0][i] : bt.bodies[1][i - n0])->rows_close();
         }
@@ -1417,9 +1433,9 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     // ---- 3. copy into the pinned upload buffer -------------------------------
     uint8_t* up = xs.upHost;
     const uint64_t stageDev = (uint64_t)(uintptr_t)(xs.upDev + oStage);
-    constexpr size_t kSegChunk = 16;
-    constexpr size_t kIngestChunk = 8192;
-    constexpr size_t kSolveChunk = 64;
+    constexpr size_t kSegChunk = SGPU_SEG_CHUNK;
+    constexpr size_t kIngestChunk = SGPU_INGEST_CHUNK;
+    constexpr size_t kSolveChunk = SGPU_SOLVE_CHUNK;
     struct Task
     {
         int kind;   // 0 = segments, 1 = ingest chunk, 2 = solves
