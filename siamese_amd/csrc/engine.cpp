@@ -243,6 +243,22 @@ void ProgramBody::lc_absorb()
     lcb.terms.insert(lcb.terms.end(), lcScratch.begin(), lcScratch.end());
 }
 
+bool ProgramBody::lc_literal_fits(uint64_t at, uint32_t len) const
+{
+    // the literal's bytes must not be read or written by another item
+    for (size_t i = 0; i + 1 < lcb.items.size(); ++i) {
+        const LcItem& it = lcb.items[i];
+        const uint32_t litEnd = it.litOffset + ((it.mixLit >> 8) & 0xff);
+        if (overlaps(at, len, it.dst, std::max<uint64_t>(lane_span(it.n), litEnd)))
+            return false;
+        const GfTerm* u = lcb.terms.data() + it.termStart;
+        for (uint32_t k = 0; k < it.termCount; ++k)
+            if (overlaps(u[k].src, lane_span(u[k].len), at, len))
+                return false;
+    }
+    return true;
+}
+
 void ProgramBody::rows_close()
 {
     lc_seal();
@@ -447,7 +463,7 @@ void Program::literal(uint64_t dst, uint32_t offset, const uint8_t* bytes, uint3
     if (!b_->lcb.items.empty()) {
         // a footer right after its combination joins that batch item
         LcItem& it = b_->lcb.items.back();
-        if (it.dst == dst && (it.mixLit >> 8) == 0 && len <= 8) {
+        if (it.dst == dst && (it.mixLit >> 8) == 0 && len <= 8 && b_->lc_literal_fits(dst + offset, len)) {
             it.mixLit |= len << 8;
             it.litOffset = offset;
             std::memcpy(it.lit, bytes, len);

@@ -133,6 +133,8 @@ struct ProgramBody
     /// Move the segment's last op (an OP_LINCOMB) into the open batch, or
     /// seal the batch first when they are not independent.
     void lc_absorb();
+    /// May a literal at [at, at + len) join the batch's last item?
+    bool lc_literal_fits(uint64_t at, uint32_t len) const;
 
     bool empty() const
     {
