@@ -1176,13 +1176,29 @@ uint64_t Engine::enqueue()
     {
         std::lock_guard<std::mutex> g(qMu_);
         toLaunch_.push_back(b);   // (b belongs to the pipeline from here on)
+        queuedSeen_.fetch_add(1, std::memory_order_release);
     }
     launchCv_.notify_one();
     return ticket;
 }
 
+namespace {
+// SIAMESE_AMD_HANDOFF_SPIN_US: how long the launcher spins for the next batch,
+// and a waiting caller for its ticket, before blocking.  Off by default: a
+// same-box A/B of 100 us showed no gain on C3 or the headline.
+const uint64_t kHandoffSpinNs = [] {
+    const char* v = std::getenv("SIAMESE_AMD_HANDOFF_SPIN_US");
+    return (uint64_t)(v ? std::atol(v) : 0) * 1000u;
+}();
+} // namespace
+
 bool Engine::wait(uint64_t ticket)
 {
+    if (kHandoffSpinNs && doneSeen_.load(std::memory_order_acquire) < ticket) {
+        const uint64_t until = now_ns() + kHandoffSpinNs;
+        while (doneSeen_.load(std::memory_order_acquire) < ticket && !failed() && now_ns() < until)
+            __builtin_ia32_pause();
+    }
     std::unique_lock<std::mutex> lk(qMu_);
     doneCv_.wait(lk, [&] { return stop_ || doneTicket_ >= ticket; });
     return !failed();
@@ -1198,8 +1214,14 @@ bool Engine::flush()
 
 void Engine::launcher_loop()
 {
+    uint64_t taken = 0;   // batches taken from toLaunch_
     for (;;) {
         Batch* b = nullptr;
+        if (kHandoffSpinNs && queuedSeen_.load(std::memory_order_acquire) == taken) {
+            const uint64_t until = now_ns() + kHandoffSpinNs;
+            while (queuedSeen_.load(std::memory_order_acquire) == taken && now_ns() < until)
+                __builtin_ia32_pause();
+        }
         {
             std::unique_lock<std::mutex> lk(qMu_);
             launchCv_.wait(lk, [&] { return stop_ || !toLaunch_.empty(); });
@@ -1207,6 +1229,7 @@ void Engine::launcher_loop()
                 return;
             b = toLaunch_.front();
             toLaunch_.pop_front();
+            ++taken;
         }
         if (!b->assembled && !failed()) {
             claim_set(*b);
@@ -1647,6 +1670,7 @@ void Engine::completer_loop()
             if (sets_[b->set].busyTicket == b->ticket)   // (a failed batch may never have claimed it)
                 sets_[b->set].busyTicket = 0;
             doneTicket_ = b->ticket;
+            doneSeen_.store(b->ticket, std::memory_order_release);
         }
         setCv_.notify_all();
         doneCv_.notify_all();

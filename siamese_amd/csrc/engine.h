@@ -424,6 +424,11 @@ private:
     std::vector<void*> pendingMarks_;               // staged copies the next submission waits for (qMu_)
     std::mutex gatherMu_;
     uint64_t doneTicket_ = 0;                       // every ticket <= this has completed
+    // lock-free mirrors for the short spins before blocking (single-stream
+    // latency: a flush is a few tens of microseconds of device work, less
+    // than a futex wake-up of the launcher plus one of the waiting caller)
+    std::atomic<uint64_t> doneSeen_{0};             // doneTicket_
+    std::atomic<uint64_t> queuedSeen_{0};           // batches pushed to toLaunch_
     bool stop_ = false;
     std::thread launcher_, completer_;
     std::unique_ptr<WorkerPool> pool_;
