@@ -33,6 +33,7 @@ max/sum reductions use gloo on the host: no RCCL anywhere (there is no
 data-path exchange between stream shards).
 """
 import argparse
+import ctypes
 import json
 import os
 import socket
@@ -68,21 +69,70 @@ def workload(rank, streams):
                      hash_data=0)
 
 
-def cpu_baseline(cfg, threads, alg_bytes, sample):
-    """The reference codec on the host cores over `cfg` (a bounded sample of
-    the workload whose algorithmic bytes are `alg_bytes`)."""
+def symbol_bytes(payload):
+    """Length prefix + payload (reference SiameseSerializers.h:566-593)."""
+    return payload + (1 if payload <= 0x7f else 2 if payload <= 0x3fff else 3 if payload <= 0x1fffff else 4)
+
+
+def ref_algorithmic_bytes(cfg, threads):
+    """Algorithmic bytes of `cfg` as the reference itself runs
+    it: the source bytes of every bulk GF(256) op, counted by the op-counting
+    build of the unmodified reference (oracle/_ref/libsiamese_ref_counted.so),
+    plus the recovery packets and recovered originals it writes."""
+    if not os.path.exists(S.REF_COUNTED_LIB):
+        return None
+    lib = ctypes.CDLL(S.REF_COUNTED_LIB)
+    lib.ref_op_bytes.restype = ctypes.c_uint64
+    lib.ref_op_bytes.argtypes = [ctypes.c_int]
+    lib.ref_op_bytes(1)
+    res, _, _ = S.run_capi(S.REF_COUNTED_LIB, cfg, threads=threads)
+    ops = lib.ref_op_bytes(1)
+    if any(r.status for r in res) or cfg.payload_bytes == 0:
+        return None
+    out = sum(r.recovery_bytes for r in res) + sum(r.recovered for r in res) * symbol_bytes(cfg.payload_bytes)
+    return ops + out
+
+
+def host_info():
+    """The host cores the CPU baselines run on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return {"nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": model}
+
+
+def cpu_baseline(cfg, threads, sample):
+    """The reference codec on `threads` host cores over `cfg` (a bounded
+    sample of the workload).  value = the reference's own algorithmic bytes
+    for exactly this sample (op-counting build, one untimed run) over the
+    time spent inside codec calls (the longest thread's, when several drive
+    their own streams at once); payload generation is not timed."""
     if not os.path.exists(S.REF_LIB):
         return None
-    res, _, wall = S.run_capi(S.REF_LIB, cfg, threads=threads)
+    alg = ref_algorithmic_bytes(cfg, threads)
+    res, sec, wall = S.run_capi(S.REF_LIB, cfg, threads=threads)
+    if alg is None or sec <= 0 or any(r.status for r in res):
+        return None
     payload = sum(r.payload_bytes for r in res)
     return {
-        "value": round(alg_bytes / wall / 1e9, 3),
+        "value": round(alg / sec / 1e9, 3),
         "unit": "GB/s",
-        "payload_GBps": round(payload / wall / 1e9, 3),
+        "payload_GBps": round(payload / sec / 1e9, 3),
         "cores": threads,
         "kind": "reference",
-        "sample": "%s on %d thread%s, %.2f s" % (sample, threads, "s" if threads > 1 else "",
-                                                 wall),
+        "sample": "%s on %d thread%s: %.4f s in codec calls (%.4f s wall), %d algorithmic bytes"
+                  % (sample, threads, "s" if threads > 1 else "", sec, wall, alg),
+        "host": host_info(),
     }
 
 
@@ -123,23 +173,29 @@ def engine_bytes(rep):
 
 def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu_sample):
     """One extra BASELINE config on one GPU: a verified warm-up, then `runs`
-    timed runs; the reference on the host beside it.  C2's 1024 streams run
-    in two pipelined stream groups (one group's host work beside the other's
-    device work: 22.5-24.4 vs 25.0-26.6 ms per run with one group, same box,
-    profiles/r2l_c2_groups_ab.txt; four groups' smaller launches doubled the
-    device time); a single stream is one group."""
+    timed runs ONE AT A TIME (no run overlaps another run of the same
+    streams), the median reported; the reference on the host beside it.
+    C2's 1024 streams run in two pipelined stream groups (one group's host
+    work beside the other's device work: 22.5-24.4 vs 25.0-26.6 ms per run
+    with one group, same box, profiles/r2l_c2_groups_ab.txt); a single
+    stream is one group."""
     groups = 2 if cfg.streams >= 64 else 1
     sess = S.BatchSession(library, cfg, device=device)
+    per = []
     try:
         res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=groups)
         if rep.mismatches or any(r.status for r in res):
             raise RuntimeError("bench leg %s: verification failed" % name)
-        res, rep = sess.run(steps=runs, warmup=0, verify=False, threads=threads, groups=groups,
-                            digest=False)
+        for _ in range(runs):
+            res, rep = sess.run(steps=1, warmup=0, verify=False, threads=threads, groups=groups,
+                                digest=False)
+            per.append(rep)
     finally:
         sess.close()
+    per.sort(key=lambda r: r.seconds)
+    rep = per[len(per) // 2]   # the median run
     eng, alg = engine_bytes(rep)
-    payload = sum(r.payload_bytes for r in res) * runs
+    payload = rep.payload_bytes   # (one run)
     sec = rep.seconds
     exec_s = rep.exec_ms / 1e3
     exec_bytes = alg - eng["solve_bytes"]
@@ -149,13 +205,15 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
             cfg.loss_pct),
         "runs": runs,
         "stream_groups": groups,
-        "ms_per_run": round(sec / runs * 1e3, 3),
+        "ms_per_run": round(sec * 1e3, 3),
+        "ms_per_run_all": [round(r.seconds * 1e3, 3) for r in per],
         "value": round(alg / sec / 1e9, 3),
         "unit": "GB/s",
         "payload_GBps": round(payload / sec / 1e9, 3),
-        "device_ms_per_run": round(rep.device_ms / runs, 3),
-        "rounds_per_run": rep.rounds / runs,
-        "algorithmic_bytes_per_run": alg // runs,
+        "device_ms_per_run": round(rep.device_ms, 3),
+        "rounds_per_run": rep.rounds,
+        "algorithmic_bytes_per_run": alg,
+        "payload_bytes_per_run": payload,
         "roofline": {
             "bound": "hbm", "kernel": "k_exec",
             "achieved": round(exec_bytes / exec_s / 1e9, 2) if exec_s > 0 else None,
@@ -165,11 +223,7 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
         "cpu_baseline": None,
     }
     if cpu_cfg is not None:
-        # algorithmic bytes of the sample: the library's count scaled by payload
-        per_payload = alg / max(1, payload)
-        sample_payload = cpu_cfg.streams * cpu_cfg.originals * cpu_cfg.payload_bytes
-        out["cpu_baseline"] = cpu_baseline(cpu_cfg, cpu_threads, per_payload * sample_payload,
-                                           cpu_sample)
+        out["cpu_baseline"] = cpu_baseline(cpu_cfg, cpu_threads, cpu_sample)
     return out
 
 
@@ -210,14 +264,14 @@ def dropin_leg(library, use_cpu, runs=5):
 
 
 def legs(library, device, threads, use_cpu):
-    cpu_threads = min(16, os.cpu_count() or 1)
+    cpu_threads = min(16, host_info()["usable_cpus"] or 1)
     specs = [
         # C2: 1024 streams, Cauchy/parity path; reference on all host cores
         ("C2", S.replace(S.CONFIGS["C2"], hash_data=0), 3,
          S.replace(S.CONFIGS["C2"], hash_data=0), cpu_threads,
          "the full C2 (1024 streams x 256 x 1400 B)"),
         # C3: one stream; reference on one core (an instance is single-threaded)
-        ("C3", S.replace(S.CONFIGS["C3"], hash_data=0), 2,
+        ("C3", S.replace(S.CONFIGS["C3"], hash_data=0), 3,
          S.replace(S.CONFIGS["C3"], hash_data=0), 1, "the full C3 (1 stream x 8192 x 1400 B)"),
         # C5: one stream of 64 KiB symbols; reference on one core over the
         # first 2000 originals (the whole stream takes it ~15 s)
@@ -284,7 +338,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
     sess.close()
 
     eng, alg_bytes = engine_bytes(rep)
-    payload = sum(r.payload_bytes for r in res) * args.steps
+    payload = rep.payload_bytes   # (all timed steps)
     digest = 0
     for d in verified_digests:
         digest = (digest * 1099511628211 + d) % (1 << 61)
@@ -392,13 +446,11 @@ def run_rank(rank, world, local, args, library, use_cuda):
     if not args.no_cpu and world == 1:
         # the reference on the host cores, rank 0 at N=1 only, on a bounded
         # sample of C4 streams
-        threads = min(16, os.cpu_count() or 1)
-        per_stream = alg_bytes / steps / args.streams
+        threads = min(16, host_info()["usable_cpus"] or 1)
         sample_cfg = S.replace(S.CONFIGS["C4"], streams=args.cpu_streams, first_stream=0,
                                hash_data=0)
         line["cpu_baseline"] = cpu_baseline(
-            sample_cfg, threads, per_stream * args.cpu_streams,
-            "%d C4 streams (256 x 1400 B, 20%% loss, block mode)" % args.cpu_streams)
+            sample_cfg, threads, "%d C4 streams (256 x 1400 B, 20%% loss, block mode)" % args.cpu_streams)
     return line
 
 

@@ -58,6 +58,7 @@ struct BatchReport
     /// stepping (host control plane), sgpu_flush (assembly + upload + device
     /// + completion), token resolution, finish + free
     double phase_seconds[5];
+    uint64_t payload_bytes;   ///< payload bytes of the originals added in the timed steps (all steps)
 };
 
 } // extern "C"
@@ -432,13 +433,17 @@ struct Job
     unsigned index = 0;             // step * groups + group
     std::vector<BatchCodec> codecs;
     std::unique_ptr<BatchStream[]> streams;
+    // the job's own per-stream results: jobs of different steps run the
+    // same streams and may be in flight together, so each keeps its own and
+    // the last step's are copied out when it retires
+    std::vector<StreamResult> res;
     std::vector<unsigned> live;     // indices into codecs/streams
     long long ticket = 0;           // its latest submission
     bool collected = false;         // that submission's tokens already gathered
 };
 
 int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* rounds,
-                 double* phase)
+                 double* phase, uint64_t* payloadBytes)
 {
     const Api& api = *sh.api;
     const ScenarioConfig* cfg = sh.cfg;
@@ -447,7 +452,6 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
     auto t = Clock::now();
     // SCENARIO_TIMELINE=1: one stderr line per phase (debugging aid)
     static const bool timeline = std::getenv("SCENARIO_TIMELINE") != nullptr;
-    const auto t00 = t;
     int curJob = -1;
     auto lap = [&](int k) {
         const auto now = Clock::now();
@@ -587,6 +591,10 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 J.codecs[i].enc = nullptr;
                 J.codecs[i].dec = nullptr;
             });
+            for (const StreamResult& r : J.res)
+                *payloadBytes += r.payload_bytes;
+            if (J.step + 1 == nsteps)
+                std::copy(J.res.begin(), J.res.end(), results + J.begin);
             dump(J);
             active.erase(active.begin() + (long)k);
             lap(4);
@@ -631,6 +639,7 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             const unsigned cnt = J.end - J.begin;
             J.codecs.resize(cnt);
             J.streams.reset(new BatchStream[cnt]);
+            J.res.resize(cnt);
             for_streams(sh, cnt, [&](size_t i) {
                 BatchCodec& c = J.codecs[i];
                 c.sh = &sh;
@@ -640,7 +649,7 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 c.log = &J.streams[i].log;
                 // the event log only feeds digests: timed bench steps run without it
                 J.streams[i].logOn = sh.verify || sh.hashData || sh.digest;
-                J.streams[i].init(cfg, &c, &results[J.begin + i], cfg->first_stream + J.begin + (unsigned)i);
+                J.streams[i].init(cfg, &c, &J.res[i], cfg->first_stream + J.begin + (unsigned)i);
                 if (!c.enc || !c.dec)
                     J.streams[i].fail(2);
             });
@@ -784,7 +793,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         else if (!sh.pool || sh.pool->size() != opt->threads)
             sh.pool.reset(new sgpu::WorkerPool(opt->threads));
         sh.groups = opt->groups ? opt->groups : 1;
-        uint64_t rounds = 0;
+        uint64_t rounds = 0, payload = 0;
         double phase[5] = {0, 0, 0, 0, 0};
         // headroom over the warm-up's high-water mark, so the working set's
         // run-to-run variation in a pipelined loop takes reserved chunks
@@ -796,7 +805,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         e0[kEngineStats] = api.arena_bytes();
         api.timing(timed ? 1 : 0, 1, nullptr, nullptr);
         const auto t1 = Clock::now();
-        rc = run_pipeline(sh, results, timed ? opt->steps : 1, &rounds, phase);
+        rc = run_pipeline(sh, results, timed ? opt->steps : 1, &rounds, phase, &payload);
         const double dt = std::chrono::duration<double>(Clock::now() - t1).count();
         double execMs = 0, totalMs = 0;
         api.timing(0, 1, &execMs, &totalMs);
@@ -807,6 +816,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
             report->device_ms += totalMs;
             report->exec_ms += execMs;
             report->rounds += rounds;
+            report->payload_bytes += payload;
             for (int k = 0; k < 5; ++k)
                 report->phase_seconds[k] += phase[k];
             for (int k = 0; k <= kEngineStats; ++k)

@@ -718,7 +718,7 @@ WorkerPool& Engine::pool()
     static std::mutex m;
     std::lock_guard<std::mutex> g(m);
     if (!pool_)
-        pool_.reset(new WorkerPool(WorkerPool::default_threads()));
+        pool_.reset(new WorkerPool(WorkerPool::default_threads(), WorkerPool::shared_nice()));
     return *pool_;
 }
 
@@ -833,12 +833,21 @@ bool Engine::refill(Shard& s, size_t cls, uint32_t cap)
 {
     std::vector<uint8_t*>& list = s.freeLists[cls];
     {
+        // the newest magazine whose submission reads as done (the completer
+        // files a submission's magazines just before it publishes the ticket)
+        const uint64_t done = doneSeen_.load(std::memory_order_acquire);
         std::lock_guard<std::mutex> g(depotMu_);
-        if (cls < depot_.size() && !depot_[cls].empty()) {
-            list.swap(depot_[cls].back());
-            depot_[cls].pop_back();
-            if (!list.empty())
-                return true;
+        if (cls < depot_.size()) {
+            auto& mags = depot_[cls];
+            for (size_t k = mags.size(); k-- > 0;) {
+                if (mags[k].ticket > done)
+                    continue;
+                list.swap(mags[k].bufs);
+                mags.erase(mags.begin() + (long)k);
+                if (!list.empty())
+                    return true;
+                break;
+            }
         }
     }
     if (cap > kRegionBytes / 4) {
@@ -1451,10 +1460,35 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     bt.upBytes = off;
     // SGPU_UPLOAD_STATS=1: one stderr line per flush, upload bytes by part (profiling aid)
     static const bool upStats = std::getenv("SGPU_UPLOAD_STATS") != nullptr;
-    if (upStats)
+    if (upStats) {
         std::fprintf(stderr, "upload %zu: stage %zu ingest %zu stream %zu items %zu solves %zu wide %zu\n",
                      bt.upBytes, bt.oIngD - oStage, bt.oStream - bt.oIngD, bt.oItems - bt.oStream,
                      bt.oSD - bt.oItems, bt.oWide - bt.oSD, bt.upBytes - bt.oWide);
+        // per phase: kind, work items, ops by kind (exec) or solve sizes
+        for (const Phase& ph : phases) {
+            if (ph.kind == Phase::EXEC) {
+                size_t k[6] = {0, 0, 0, 0, 0, 0}, rows = 0, upd = 0, win = 0;
+                for (const SegRef& r : segs) {
+                    if (r.itemBase < ph.itemBegin || r.itemBase >= ph.itemBegin + ph.itemCount)
+                        continue;
+                    for (const GfOp& op : r.seg->ops) {
+                        k[op.kind < 6 ? op.kind : 0]++;
+                        if (op.kind == OP_ROWS) {
+                            rows += op.n;
+                            upd += op.mix;
+                            win += op.valid;
+                        }
+                    }
+                }
+                std::fprintf(stderr, "  exec items %zu wide %zu: lincomb %zu literal %zu rows %zu(r%zu u%zu w%zu) "
+                             "copies %zu lcs %zu\n", ph.itemCount, ph.wideCount, k[OP_LINCOMB], k[OP_LITERAL],
+                             k[OP_ROWS], rows, upd, win, k[OP_COPIES], k[OP_LINCOMBS]);
+            } else {
+                std::fprintf(stderr, "  solve items %zu solves %zu maxm %u\n", ph.itemCount, ph.solveCount,
+                             ph.maxRows);
+            }
+        }
+    }
     if (bt.upBytes)
         ensure_up(xs, bt.upBytes);
     if (wideBytes) {
@@ -1663,8 +1697,22 @@ void Engine::completer_loop()
             toComplete_.pop_front();
         }
         tl("complete begin", b->ticket);
-        complete_batch(*b);
+        // (released buffers go back to the depot tagged with the ticket:
+        // refill() takes them only once the ticket reads as done below, so a
+        // caller that gathers a completed submission's outputs before its
+        // next submission -- the siamese_gpu.h lifetime rule -- always sees
+        // that submission done before anyone can reuse its buffers)
+        if (complete_batch(*b))
+            reclaim_batch(*b);
         tl("complete end", b->ticket);
+        // SGPU_TEST_PUBLISH_DELAY_US: widen the window between filing the
+        // released buffers and publishing the ticket (CPU test of the rule above)
+        static const long kPublishDelayUs = [] {
+            const char* v = std::getenv("SGPU_TEST_PUBLISH_DELAY_US");
+            return v ? std::atol(v) : 0L;
+        }();
+        if (kPublishDelayUs > 0)
+            std::this_thread::sleep_for(std::chrono::microseconds(kPublishDelayUs));
         {
             std::lock_guard<std::mutex> g(qMu_);
             if (sets_[b->set].busyTicket == b->ticket)   // (a failed batch may never have claimed it)
@@ -1678,7 +1726,7 @@ void Engine::completer_loop()
     }
 }
 
-void Engine::complete_batch(Batch& bt)
+bool Engine::complete_batch(Batch& bt)
 {
     const uint64_t t0 = now_ns();
     EngineStats st;
@@ -1700,7 +1748,7 @@ void Engine::complete_batch(Batch& bt)
             }
         std::lock_guard<std::mutex> g(statsMu_);
         flushStats_.add(st);
-        return;
+        return false;
     }
     XferSet& xs = sets_[bt.set];
     for (const Batch::Download& d : bt.downloads)
@@ -1725,8 +1773,16 @@ void Engine::complete_batch(Batch& bt)
                 fn(results + bt.resultBase[g][i]);
             ProgramBody::put(p);
         }
+    st.completeNs = now_ns() - t1;
+    std::lock_guard<std::mutex> g(statsMu_);
+    flushStats_.add(st);
+    return true;
+}
+
+void Engine::reclaim_batch(Batch& bt)
+{
     const uint64_t t2 = now_ns();
-    st.completeNs = t2 - t1;
+    EngineStats st;
     // Released buffers are free once this submission (and so every earlier
     // one) has run: they go back to the depot as magazines, and the emptied
     // queues back to their shard.
@@ -1741,11 +1797,15 @@ void Engine::complete_batch(Batch& bt)
                 depot_.resize(cls + 1);
             if (r.size() <= kMaxMagazine) {
                 depot_[cls].emplace_back();
-                depot_[cls].back().swap(r);
+                depot_[cls].back().ticket = bt.ticket;
+                depot_[cls].back().bufs.swap(r);
             } else {
-                for (size_t k = 0; k < r.size(); k += kMaxMagazine)
-                    depot_[cls].emplace_back(r.begin() + (long)k,
-                                             r.begin() + (long)std::min(r.size(), k + kMaxMagazine));
+                for (size_t k = 0; k < r.size(); k += kMaxMagazine) {
+                    depot_[cls].emplace_back();
+                    depot_[cls].back().ticket = bt.ticket;
+                    depot_[cls].back().bufs.assign(r.begin() + (long)k,
+                                                   r.begin() + (long)std::min(r.size(), k + kMaxMagazine));
+                }
                 r.clear();
             }
         }

@@ -384,7 +384,8 @@ private:
     void claim_set(Batch& b);
     WorkerPool& asm_pool();   // launcher thread only
     void launch_batch(Batch& b);
-    void complete_batch(Batch& b);
+    bool complete_batch(Batch& b);   // false: the submission failed
+    void reclaim_batch(Batch& b);    // released buffers to the depot (before the ticket is published)
     void start_threads();
     void stop_threads();
 
@@ -408,7 +409,12 @@ private:
     std::vector<Chunk> spare_;   // reserved ahead, not yet carved
     std::atomic<uint64_t> arenaBytes_{0};
     std::mutex depotMu_;
-    std::vector<std::vector<std::vector<uint8_t*>>> depot_;   // [class] -> magazines
+    struct Magazine
+    {
+        uint64_t ticket = 0;          // the submission that released these buffers
+        std::vector<uint8_t*> bufs;
+    };
+    std::vector<std::vector<Magazine>> depot_;   // [class] -> magazines
 
     // ---- shards (one per host thread that touched the engine)
     mutable std::mutex shardsMu_;

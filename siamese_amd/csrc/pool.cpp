@@ -10,7 +10,6 @@
 namespace sgpu {
 
 namespace {
-// SIAMESE_AMD_WORKER_NICE overrides (0 = same priority as the engine threads)
 // pause iterations a worker (or a joining caller) spins before blocking
 // (SIAMESE_AMD_POOL_SPIN).  Off by default: on the MI355X box's host share,
 // spinning workers slowed the codec stepping they share the cores with
@@ -25,11 +24,16 @@ inline void cpu_relax()
     __builtin_ia32_pause();
 #endif
 }
-const int kWorkerNice = [] {
-    const char* v = std::getenv("SIAMESE_AMD_WORKER_NICE");
-    return v ? std::atoi(v) : 10;
-}();
 } // namespace
+
+int WorkerPool::shared_nice()
+{
+    static const int n = [] {
+        const char* v = std::getenv("SIAMESE_AMD_WORKER_NICE");
+        return v ? std::atoi(v) : 10;
+    }();
+    return n;
+}
 
 unsigned WorkerPool::default_threads()
 {
@@ -42,14 +46,12 @@ unsigned WorkerPool::default_threads()
     return std::max(1u, std::min(16u, hw));
 }
 
-WorkerPool::WorkerPool(unsigned threads)
+WorkerPool::WorkerPool(unsigned threads, int nice)
 {
     for (unsigned i = 1; i < threads; ++i)
-        workers_.emplace_back([this] {
-            // Workers yield the CPU to the engine's launcher and completer
-            // threads (nice 0), which sit on the device's critical path:
-            // a nice-10 worker is preempted as soon as either wakes up.
-            (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), kWorkerNice);
+        workers_.emplace_back([this, nice] {
+            if (nice != 0)
+                (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice);
             loop();
         });
 }

@@ -16,7 +16,8 @@ namespace sgpu {
 class WorkerPool
 {
 public:
-    explicit WorkerPool(unsigned threads);
+    /// `nice`: scheduling priority of the worker threads (0 = the caller's).
+    explicit WorkerPool(unsigned threads, int nice = 0);
     ~WorkerPool();
     WorkerPool(const WorkerPool&) = delete;
     WorkerPool& operator=(const WorkerPool&) = delete;
@@ -27,6 +28,12 @@ public:
     /// Threads to use by default: SIAMESE_AMD_THREADS, else OMP_NUM_THREADS,
     /// else min(16, hardware threads).
     static unsigned default_threads();
+    /// Priority of the engine's shared stepping pool (Engine::pool):
+    /// SIAMESE_AMD_WORKER_NICE, default 10, so its workers yield to the
+    /// engine's launcher and completer threads, which sit on the device's
+    /// critical path.  Other pools (the launcher's assembly pool, pools an
+    /// application creates) keep the caller's priority.
+    static int shared_nice();
 
 private:
     void loop();

@@ -13,6 +13,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCENARIO_LIB = os.path.join(ROOT, "harness", "libscenario.so")
 REF_LIB = os.path.join(ROOT, "oracle", "_ref", "libsiamese_ref.so")
+REF_COUNTED_LIB = os.path.join(ROOT, "oracle", "_ref", "libsiamese_ref_counted.so")
 AMD_LIB = os.path.join(ROOT, "siamese_amd", "libsiamese_amd.so")
 SIM_LIB = os.path.join(ROOT, "tests", "hostsim", "libsiamese_hostsim.so")
 
@@ -85,7 +86,7 @@ class BatchReport(ctypes.Structure):
                 ("exec_ms", ctypes.c_double), ("setup_seconds", ctypes.c_double),
                 ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 16),
                 ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64),
-                ("phase_seconds", ctypes.c_double * 5)]
+                ("phase_seconds", ctypes.c_double * 5), ("payload_bytes", ctypes.c_uint64)]
 
 PHASES = ("create", "step", "flush", "resolve", "finish")
 
@@ -112,7 +113,10 @@ def lib():
 def run_capi(library, cfg, threads=1, event_log=None):
     """Run `cfg` through the siamese.h API of `library`.
 
-    Returns (results array, codec seconds, wall seconds)."""
+    Returns (results array, codec seconds, wall seconds).  Codec seconds: the
+    time spent inside codec calls (one thread), or the longest any thread
+    spent inside them (several threads, each driving its own streams
+    concurrently); payload generation and checking are outside it."""
     res = (StreamResult * cfg.streams)()
     sec = ctypes.c_double()
     t0 = time.time()

@@ -44,3 +44,48 @@ def test_oplincombs_batches_match_plain_ops():
         assert r.returncode == 0, r.stderr[-2000:]
         out[v] = r.stdout.strip().splitlines()[-1]
     assert out["0"] == out["1"]
+
+
+def test_pipelined_steps_keep_their_own_results():
+    """Steps of one session may be in flight together (the next step's first
+    job starts while the last one runs), and they run the same streams: each
+    job keeps its own per-stream results, so the results describe exactly one
+    run and the report counts every step's payload once."""
+    cfg = S.replace(S.CONFIGS["C3"], hash_data=0, originals=600)
+    sess = S.BatchSession(S.SIM_LIB, cfg)
+    try:
+        res1, rep1 = sess.run(steps=1, warmup=0, verify=False, groups=1, digest=False)
+        one = sum(r.payload_bytes for r in res1)
+        assert one == 600 * 1400
+        assert rep1.payload_bytes == one
+        res, rep = sess.run(steps=2, warmup=0, verify=False, groups=1, digest=False)
+        assert sum(r.payload_bytes for r in res) == one
+        assert rep.payload_bytes == 2 * one
+        assert [r.encodes for r in res] == [r.encodes for r in res1]
+    finally:
+        sess.close()
+
+
+def test_released_buffers_wait_for_the_published_ticket():
+    """A completed submission's released buffers are filed in the depot just
+    before its ticket is published; with that window widened (the completer
+    sleeps between the two), no stream may hand such a buffer to a new
+    submission before the harness has gathered the completed job's outputs:
+    every recovered byte of 1024 C2 streams in 4 pipelined groups verifies."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import scenario_lib as S\n"
+        "cfg = S.replace(S.CONFIGS['C2'], hash_data=0, streams=1024)\n"
+        "sess = S.BatchSession(S.SIM_LIB, cfg)\n"
+        "res, rep = sess.run(steps=0, warmup=1, verify=True, threads=8, groups=4)\n"
+        "sess.close()\n"
+        "assert rep.checked > 0 and rep.mismatches == 0, rep.mismatches\n"
+        "assert not any(r.status for r in res)\n"
+        "print('ok', rep.checked)\n" % os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SGPU_TEST_PUBLISH_DELAY_US="300")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().startswith("ok")
