@@ -41,6 +41,12 @@ struct BatchOptions
     uint32_t e2e;      ///< originals start in pinned host memory (H2D each step) and every
                        ///< recovery packet and recovered original is copied back (D2H)
     uint32_t digest;   ///< keep event logs and digests on unverified runs too
+    uint32_t defer;    ///< 0: a stream yields after each decode and waits for its
+                       ///< submission (sgpu_decode / sgpu_decoder_get);
+                       ///< k > 0: deferred outputs (sgpu_decode_deferred /
+                       ///< sgpu_decoder_get_deferred), a stream yields after
+                       ///< every k-th decode and a job is driven on with up to
+                       ///< two of its submissions in flight
 };
 
 struct BatchReport
@@ -83,6 +89,8 @@ struct Api
     SiameseResult (*decoder_is_ready)(SgpuDecoder);
     SiameseResult (*decode)(SgpuDecoder, SiameseOriginalPacket**, unsigned*);
     SiameseResult (*decoder_get)(SgpuDecoder, SiameseOriginalPacket*);
+    SiameseResult (*decode_deferred)(SgpuDecoder, SiameseOriginalPacket*, unsigned, unsigned*);
+    SiameseResult (*decoder_get_deferred)(SgpuDecoder, SiameseOriginalPacket*);
     int (*flush)(void);
     int (*submit)(void);
     long long (*enqueue)(void);
@@ -129,7 +137,9 @@ bool load_api(const char* path, Api& a)
            bind(h, a.decoder_add_original, "sgpu_decoder_add_original") &&
            bind(h, a.decoder_add_recovery, "sgpu_decoder_add_recovery") &&
            bind(h, a.decoder_is_ready, "sgpu_decoder_is_ready") && bind(h, a.decode, "sgpu_decode") &&
-           bind(h, a.decoder_get, "sgpu_decoder_get") && bind(h, a.flush, "sgpu_flush") && bind(h, a.submit, "sgpu_submit") &&
+           bind(h, a.decoder_get, "sgpu_decoder_get") && bind(h, a.decode_deferred, "sgpu_decode_deferred") &&
+           bind(h, a.decoder_get_deferred, "sgpu_decoder_get_deferred") &&
+           bind(h, a.flush, "sgpu_flush") && bind(h, a.submit, "sgpu_submit") &&
            bind(h, a.enqueue, "sgpu_enqueue") && bind(h, a.wait, "sgpu_wait") &&
            bind(h, a.query, "sgpu_query") &&
            bind(h, a.parallel_for, "sgpu_parallel_for") &&
@@ -155,8 +165,8 @@ struct Pkt
     const SiameseOriginalPacket* entry = nullptr; // decode output entry (resolved at flush)
 };
 
-// A token whose value needs device bytes, resolved once the flush that
-// produced them has completed.
+// A token whose value needs device results, resolved once the submission
+// that closed the round it was made in has completed.
 struct Request
 {
     std::vector<uint64_t>* log;
@@ -166,6 +176,8 @@ struct Request
     unsigned id;     // payload id to verify against (packets only)
     bool isPacket;
     bool* ok;
+    const SiameseOriginalPacket* entry = nullptr;   // deferred output: dev/bytes read at resolution
+    unsigned* inFlight = nullptr;                   // its codec's count of unresolved requests
 };
 
 struct Shared
@@ -200,6 +212,7 @@ struct Shared
     std::unique_ptr<sgpu::WorkerPool> pool;
     unsigned groups = 1;
     bool digest = true;   // per-stream digests (event logs) also on unverified runs
+    unsigned defer = 0;   // BatchOptions::defer
 };
 
 struct BatchCodec
@@ -209,7 +222,24 @@ struct BatchCodec
     SgpuEncoder enc = nullptr;
     SgpuDecoder dec = nullptr;
     std::vector<uint64_t>* log = nullptr;
-    std::vector<Request> cur, prev;   // tokens waiting for device bytes
+    std::vector<Request> cur;           // tokens made in the current round
+    unsigned inFlight = 0;              // tokens made in rounds not yet resolved
+    unsigned decodes = 0;               // decodes since the last yield (deferred mode)
+    // deferred outputs: caller-owned entries the library fills at completion
+    // (stable addresses, kept until the job retires)
+    std::vector<std::unique_ptr<SiameseOriginalPacket[]>> slabs;
+    unsigned slabUsed = kSlab;
+    static constexpr unsigned kSlab = 1024;
+    SiameseOriginalPacket* entries(unsigned n)
+    {
+        if (slabUsed + n > kSlab) {
+            slabs.emplace_back(new SiameseOriginalPacket[kSlab]);
+            slabUsed = 0;
+        }
+        SiameseOriginalPacket* e = slabs.back().get() + slabUsed;
+        slabUsed += n;
+        return e;
+    }
 
     const void* dev_payload(unsigned id) const { return payload + (size_t)id * sh->stride; }
 
@@ -234,7 +264,17 @@ struct BatchCodec
     {
         SiameseOriginalPacket* p = nullptr;
         unsigned n = 0;
-        const int r = sh->api->decode(dec, &p, &n);
+        int r;
+        if (sh->defer) {
+            // (capacity: a solve's 255 packets or what single recoveries hold;
+            // unused entries are handed back)
+            constexpr unsigned kCap = 255;
+            p = entries(kCap);
+            r = sh->api->decode_deferred(dec, p, kCap, &n);
+            slabUsed -= kCap - (r == 0 ? n : 0);
+        } else {
+            r = sh->api->decode(dec, &p, &n);
+        }
         if (r == 0)
             for (unsigned i = 0; i < n; ++i) {
                 Pkt k;
@@ -246,6 +286,18 @@ struct BatchCodec
     }
     int dec_get(unsigned num, Pkt* out)
     {
+        if (sh->defer) {
+            SiameseOriginalPacket* e = entries(1);
+            e->PacketNum = num;
+            e->Data = nullptr;
+            e->DataBytes = 0;
+            const int r = sh->api->decoder_get_deferred(dec, e);
+            if (r != 0)
+                --slabUsed;
+            out->num = num;
+            out->entry = r == 0 ? e : nullptr;
+            return r;
+        }
         SiameseOriginalPacket p;
         p.PacketNum = num;
         p.Data = nullptr;
@@ -262,11 +314,17 @@ struct BatchCodec
     {
         // end-to-end mode: every recovery packet goes back to host memory
         if (sh->hashData || sh->e2e)
-            cur.push_back(Request{log, log->size(), r.pkt.DeviceData, r.bytes, 0, false, nullptr});
+            push(Request{log, log->size(), r.pkt.DeviceData, r.bytes, 0, false, nullptr});
         return r.bytes;
     }
     uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok)
     {
+        if (sh->defer && p.entry) {
+            // length and bytes arrive with the round's completion: the token
+            // is written into the log then (resolve_requests)
+            push(Request{log, log->size(), nullptr, 0, id, true, ok, p.entry});
+            return 0;
+        }
         const unsigned bytes = p.entry ? p.entry->DataBytes : p.bytes;
         const void* data = p.entry ? p.entry->Data : p.data;
         const unsigned want = sh->cfg->payload_bytes ? sh->cfg->payload_bytes : scen::variable_bytes(id);
@@ -280,10 +338,24 @@ struct BatchCodec
             // recovered original (a decode output); a delivered original that
             // arrived intact came from host memory, where the application
             // still has it
-            cur.push_back(Request{log, log->size(), data, bytes, id, true, ok});
+            push(Request{log, log->size(), data, bytes, id, true, ok});
         return bytes;
     }
-    bool wants_yield_after_decode() const { return true; }
+    void push(Request r)
+    {
+        r.inFlight = &inFlight;
+        ++inFlight;
+        cur.push_back(r);
+    }
+    bool wants_yield_after_decode()
+    {
+        if (!sh->defer)
+            return true;
+        if (++decodes < sh->defer)
+            return false;
+        decodes = 0;
+        return true;
+    }
     bool wants_yield_after_encode() const { return sh->hashData; }
 };
 
@@ -312,6 +384,13 @@ void land_gather(Shared& sh)
                 if (std::memcmp(expect.data(), d, r.bytes) != 0) {
                     ++sh.mismatches;
                     *r.ok = false;
+                    if (std::getenv("SCENARIO_DEBUG")) {
+                        size_t at = 0;
+                        while (at < r.bytes && expect[at] == d[at])
+                            ++at;
+                        std::fprintf(stderr, "mismatch: id %u bytes %u first differing byte %zu (deferred %d) dev %p\n",
+                                     r.id, r.bytes, at, r.entry != nullptr, r.dev);
+                    }
                 }
             }
             if (sh.hashData)
@@ -336,6 +415,35 @@ void land_gathers(Shared& sh)
 // when the gather lands (land_gather).
 void resolve_requests(Shared& sh, std::vector<Request>& reqs)
 {
+    if (reqs.empty())
+        return;
+    // deferred outputs: their length and pointer are final now; a token
+    // that needs no bytes is written here, the rest join the gather
+    size_t keep = 0;
+    for (size_t i = 0; i < reqs.size(); ++i) {
+        Request r = reqs[i];
+        --*r.inFlight;
+        if (r.entry) {
+            r.dev = r.entry->Data;
+            r.bytes = r.entry->DataBytes;
+            const unsigned want = sh.cfg->payload_bytes ? sh.cfg->payload_bytes : scen::variable_bytes(r.id);
+            if (r.bytes != want || !r.dev) {
+                if (std::getenv("SCENARIO_DEBUG"))
+                    std::fprintf(stderr, "deferred token: id %u bytes %u want %u data %p\n", r.id, r.bytes,
+                                 want, r.dev);
+                *r.ok = false;
+                if (!r.log->empty())
+                    (*r.log)[r.pos] = r.bytes;
+                continue;
+            }
+            if (!r.log->empty())
+                (*r.log)[r.pos] = r.bytes;   // (the token without hash_data; land_gather hashes)
+            if (!(sh.hashData || sh.verify || sh.e2e))
+                continue;
+        }
+        reqs[keep++] = r;
+    }
+    reqs.resize(keep);
     if (reqs.empty())
         return;
     std::vector<const void*> srcs;
@@ -423,10 +531,19 @@ void for_streams(Shared& sh, size_t count, const F& fn)
 // One job = one contiguous group of a step's streams.  Jobs flow through a
 // pipeline so that the host work of one job overlaps the device work (and
 // the library's launch and completion work) of the others: every iteration
-// takes each active job in turn, waits for its last submission, advances its
-// streams (round two and later: deliveries after a decode) and submits
-// again without waiting (sgpu_enqueue); a new job (round one: adds, encodes,
-// decodes) starts while the pipeline is shallow.
+// takes each active job in turn, resolves the tokens of its completed
+// submissions, advances its streams to their next yield and submits again
+// without waiting (sgpu_enqueue); a new job starts while the pipeline is
+// shallow.  A job advances only once its last submission has completed
+// (classic mode), or with up to two of its submissions in flight (deferred
+// outputs, BatchOptions::defer: a single stream then keeps the GPU busy with
+// one round while the host prepares the next).
+struct Round
+{
+    long long ticket;
+    std::vector<Request> reqs;   // tokens made in the round this submission closed
+};
+
 struct Job
 {
     unsigned step = 0, begin = 0, end = 0;
@@ -438,8 +555,7 @@ struct Job
     // the last step's are copied out when it retires
     std::vector<StreamResult> res;
     std::vector<unsigned> live;     // indices into codecs/streams
-    long long ticket = 0;           // its latest submission
-    bool collected = false;         // that submission's tokens already gathered
+    std::deque<Round> rounds;       // submitted, tokens not yet resolved (oldest first)
 };
 
 int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* rounds,
@@ -449,6 +565,12 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
     const ScenarioConfig* cfg = sh.cfg;
     const unsigned n = cfg->streams;
     const unsigned G = std::max(1u, std::min(sh.groups, n));
+    // (SCENARIO_INFLIGHT overrides the deferred mode's depth: debugging aid)
+    static const size_t kDeferDepth = [] {
+        const char* v = std::getenv("SCENARIO_INFLIGHT");
+        return (size_t)(v && std::atoi(v) > 0 ? std::atoi(v) : 2);
+    }();
+    const size_t inFlightPerJob = sh.defer ? kDeferDepth : 1;
     auto t = Clock::now();
     // SCENARIO_TIMELINE=1: one stderr line per phase (debugging aid)
     static const bool timeline = std::getenv("SCENARIO_TIMELINE") != nullptr;
@@ -464,18 +586,18 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                          curJob);
         t = now;
     };
-    auto take = [](Job& J, bool prev) {
+    auto take_cur = [](Job& J) {
         std::vector<Request> reqs;
         for (BatchCodec& c : J.codecs) {
-            std::vector<Request>& q = prev ? c.prev : c.cur;
-            reqs.insert(reqs.end(), q.begin(), q.end());
-            q.clear();
+            reqs.insert(reqs.end(), c.cur.begin(), c.cur.end());
+            c.cur.clear();
         }
         return reqs;
     };
     // advance every live stream of J until it yields; finished streams free
-    // their codecs right away (their state is still hot); digests wait for
-    // the job's last device bytes (retirement)
+    // their codecs right away (their state is still hot) unless tokens of
+    // theirs still wait for device results; digests wait for the job's last
+    // device bytes (retirement)
     auto advance = [&](Job& J) {
         for_streams(sh, J.live.size(), [&](size_t k) {
             const unsigned i = J.live[k];
@@ -483,10 +605,8 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             while (!st.done())
                 if (st.step())
                     break;
-            // (a stream with device bytes still to read keeps its codecs, and
-            // so its buffers, until the job retires)
             BatchCodec& c = J.codecs[i];
-            if (st.done() && c.cur.empty() && c.prev.empty()) {
+            if (st.done() && c.inFlight == 0) {
                 api.encoder_free(c.enc);
                 api.decoder_free(c.dec);
                 c.enc = nullptr;
@@ -496,34 +616,49 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
         J.live.erase(std::remove_if(J.live.begin(), J.live.end(),
                                     [&](unsigned i) { return J.streams[i].done(); }),
                      J.live.end());
-        for (BatchCodec& c : J.codecs)
-            std::swap(c.prev, c.cur);
     };
     std::vector<std::unique_ptr<Job>> active;
-    // Gather the tokens of every job whose latest submission has completed.
-    // Runs before each submission: buffers a completed submission released
-    // (a decoder's delivered slots, a freed codec's symbols) are free for any
-    // job's next allocation, so the bytes a token names must be read before
-    // any later submission, whose device work waits for the gather's reads,
-    // can rewrite them.
-    auto collect_all = [&]() {
-        for (auto& a : active) {
-            Job& J = *a;
-            if (J.collected || api.query(J.ticket) != 1)
-                continue;
-            std::vector<Request> reqs = take(J, true);
-            resolve_requests(sh, reqs);
-            J.collected = true;
+    // Resolve the tokens of J's completed rounds (oldest first).  -1 on a
+    // device failure, else the number resolved.
+    auto collect = [&](Job& J) {
+        int got = 0;
+        while (!J.rounds.empty()) {
+            const int q = api.query(J.rounds.front().ticket);
+            if (q < 0)
+                return -1;
+            if (q == 0)
+                break;
+            resolve_requests(sh, J.rounds.front().reqs);
+            J.rounds.pop_front();
+            ++got;
         }
+        return got;
+    };
+    // Gather the tokens of every job's completed rounds.  Runs before each
+    // submission: buffers a completed submission released (a decoder's
+    // delivered slots, a freed codec's symbols) are free for any job's next
+    // allocation, so the bytes a token names must be read before any later
+    // submission, whose device work waits for the gather's reads, can
+    // rewrite them.
+    auto collect_all = [&]() {
+        for (auto& a : active)
+            if (collect(*a) < 0)
+                return false;
+        return true;
     };
     auto submit = [&](Job& J) {
-        collect_all();
-        J.ticket = api.enqueue();
-        J.collected = false;
+        if (!collect_all())
+            return false;
+        Round r;
+        r.reqs = take_cur(J);
+        r.ticket = api.enqueue();
         if (timeline)
-            std::fprintf(stderr, "tl submit j%d t%lld live %zu\n", curJob, J.ticket, J.live.size());
+            std::fprintf(stderr, "tl submit j%d t%lld live %zu\n", curJob, r.ticket, J.live.size());
         ++*rounds;
-        return J.ticket >= 0;
+        if (r.ticket < 0)
+            return false;
+        J.rounds.push_back(std::move(r));
+        return true;
     };
     auto dump = [&](Job& J) {
         // debugging aid: SCENARIO_DUMP="<stream index>:<path>" writes that
@@ -545,42 +680,42 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
     const size_t depth = G + 1;   // jobs in flight
     unsigned next = 0;
     int rc = 0;
-    // Host work is done whenever some is available: a job whose submission
-    // has completed is advanced (or retired), a new job starts (round one,
-    // the bulk of a step's host work) while the pipeline is shallow; the
-    // thread blocks only when neither is possible.
+    // Host work is done whenever some is available: a job's completed rounds
+    // are resolved, a job with room in flight is advanced (or retired), a new
+    // job starts (round one, the bulk of a step's host work) while the
+    // pipeline is shallow; the thread blocks only when none is possible.
     while (rc == 0 && (next < jobs || !active.empty())) {
         bool did = false;
         for (size_t k = 0; k < active.size() && rc == 0;) {
             Job& J = *active[k];
             curJob = (int)(J.step * G + J.begin);
-            const int q = api.query(J.ticket);
-            if (q < 0) {
+            const int got = collect(J);
+            if (got < 0) {
                 rc = -3;
                 break;
             }
-            if (q == 0) {
+            if (got > 0) {
+                did = true;
+                lap(3);
+            }
+            if (!J.live.empty()) {
+                if (J.rounds.size() < inFlightPerJob) {
+                    did = true;
+                    advance(J);
+                    lap(1);
+                    if (!submit(J))
+                        rc = -3;
+                    lap(2);
+                }
+                ++k;
+                continue;
+            }
+            if (!J.rounds.empty()) {
                 ++k;
                 continue;
             }
             did = true;
-            std::vector<Request> reqs;
-            if (!J.collected) {
-                reqs = take(J, true);
-                resolve_requests(sh, reqs);
-                J.collected = true;
-            }
-            lap(3);
-            if (!J.live.empty()) {
-                advance(J);
-                lap(1);
-                if (!submit(J))
-                    rc = -3;
-                lap(2);
-                ++k;
-                continue;
-            }
-            reqs = take(J, false);
+            std::vector<Request> reqs = take_cur(J);   // (none: every round ends with a submission)
             resolve_requests(sh, reqs);
             if (sh.verify || sh.hashData)
                 land_gathers(sh);   // (their requests point into the job's streams)
@@ -664,9 +799,13 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             active.push_back(std::move(jp));
         }
         if (rc == 0 && !did && !active.empty()) {
-            // nothing to do until the oldest submission completes
-            if (api.wait(active.front()->ticket) != 0)
-                rc = -3;
+            // nothing to do until the oldest round in flight completes
+            for (auto& a : active)
+                if (!a->rounds.empty()) {
+                    if (api.wait(a->rounds.front().ticket) != 0)
+                        rc = -3;
+                    break;
+                }
             lap(2);
         }
     }
@@ -793,6 +932,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         else if (!sh.pool || sh.pool->size() != opt->threads)
             sh.pool.reset(new sgpu::WorkerPool(opt->threads));
         sh.groups = opt->groups ? opt->groups : 1;
+        sh.defer = opt->defer;
         uint64_t rounds = 0, payload = 0;
         double phase[5] = {0, 0, 0, 0, 0};
         // headroom over the warm-up's high-water mark, so the working set's

@@ -39,8 +39,18 @@
     library's launcher thread and returns a ticket at once; sgpu_wait(ticket)
     returns when that submission (and every earlier one) has run on the GPU
     and its results are delivered.  sgpu_wait may run while other threads
-    drive instances; an instance with work in a submission must not be called
-    again until that submission has been waited for.
+    drive instances.  An instance may be driven on while its earlier
+    submissions are still in flight (a single stream keeps the GPU busy with
+    one submission while the host prepares the next): completions never
+    touch an instance's state behind its back, each call first applies the
+    completions that have arrived.
+
+    Deferred outputs: sgpu_decode_deferred and sgpu_decoder_get_deferred
+    never wait for the GPU.  They write into entries the caller owns; an
+    entry whose packet is still being solved gets its Data and DataBytes
+    when the submission carrying the solve completes, before sgpu_query /
+    sgpu_wait report that submission (or a later one) done.  The caller keeps
+    such entries alive until then (freeing the decoder does not cancel them).
 */
 #ifndef SIAMESE_GPU_H
 #define SIAMESE_GPU_H
@@ -89,6 +99,18 @@ SIAMESE_EXPORT SiameseResult sgpu_decode(SgpuDecoder decoder, SiameseOriginalPac
 /// Returns a device pointer; waits for outstanding work if the packet's
 /// exact length is still being computed.
 SIAMESE_EXPORT SiameseResult sgpu_decoder_get(SgpuDecoder decoder, SiameseOriginalPacket* packet);
+/// sgpu_decode without waiting (see "Deferred outputs" above): the recovered
+/// packets are written to out[0, *countOut), PacketNum at once, Data and
+/// DataBytes at once or when the solve's submission completes.  capacity must
+/// be at least 255 (the most one solve recovers) and at least the packets
+/// held by single-packet recoveries since the last decode; Siamese_InvalidInput
+/// otherwise, with nothing consumed.
+SIAMESE_EXPORT SiameseResult sgpu_decode_deferred(SgpuDecoder decoder, SiameseOriginalPacket* out,
+                                                  unsigned capacity, unsigned* countOut);
+/// sgpu_decoder_get without waiting: Success / NeedMoreData as
+/// sgpu_decoder_get returns them; for a packet still being solved, *packet's
+/// Data and DataBytes are written when the solve's submission completes.
+SIAMESE_EXPORT SiameseResult sgpu_decoder_get_deferred(SgpuDecoder decoder, SiameseOriginalPacket* packet);
 /// Non-blocking lookup: Success if the packet is present (length may still
 /// be pending), NeedMoreData if not.
 SIAMESE_EXPORT SiameseResult sgpu_decoder_has(SgpuDecoder decoder, unsigned packetNum);

@@ -237,7 +237,7 @@ SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder, SiameseOrigi
         core.download_recovered();
         if (!eng->flush_and_sync())
             return Siamese_Disabled;
-        if (core.disabled())
+        if (core.disabled())   // (applies the completed solve first)
             return Siamese_Disabled;
     }
     return r;

@@ -381,6 +381,7 @@ unsigned DecoderCore::find_next_got(unsigned start)
 
 SiameseResult DecoderCore::acknowledgement(uint8_t* buffer, unsigned byteLimit, unsigned& usedBytes)
 {
+    settle();
     if (dead())
         return Siamese_Disabled;
     const unsigned count = count_;

@@ -175,6 +175,21 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_get(SgpuDecoder decoder, SiameseOrigin
     return BD(decoder)->core.get(*packet);
 }
 
+SIAMESE_EXPORT SiameseResult sgpu_decode_deferred(SgpuDecoder decoder, SiameseOriginalPacket* out,
+                                                  unsigned capacity, unsigned* countOut)
+{
+    if (!decoder || !out || !countOut)
+        return Siamese_InvalidInput;
+    return BD(decoder)->core.decode_deferred(out, capacity, countOut);
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_decoder_get_deferred(SgpuDecoder decoder, SiameseOriginalPacket* packet)
+{
+    if (!decoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    return BD(decoder)->core.get_deferred(*packet);
+}
+
 SIAMESE_EXPORT SiameseResult sgpu_decoder_has(SgpuDecoder decoder, unsigned packetNum)
 {
     if (!decoder || packetNum > SIAMESE_PACKET_NUM_MAX)

@@ -31,12 +31,16 @@ DecoderCore::DecoderCore(Engine* eng, bool hostMirror)
     : eng_(eng), prog_(eng, 1), mirror_(hostMirror)
 {
     adopt_spare();
+    if (!res_)
+        res_ = std::make_shared<Resolver>();
+    res_->mirror = mirror_;
 }
 
 // Every recycled vector is empty in a fresh decoder; a spare holds them
 // cleared (capacity kept), so swapping one in leaves the decoder in exactly
-// its freshly constructed state.  pend_ keeps its slots, all idle (a slot is
-// claimed by the first search for a non-live one and fully rewritten).
+// its freshly constructed state.  The resolver is recycled only when no
+// completion holds it any more (its slots all idle; a slot is claimed by the
+// first search for a non-live one and fully rewritten).
 struct DecoderCore::Spare
 {
     std::vector<DecSubwindowPtr> subwindows;
@@ -48,7 +52,7 @@ struct DecoderCore::Spare
     std::vector<uint32_t> pickCol;
     std::vector<uint8_t> mat;
     std::vector<unsigned> pivots;
-    std::vector<PendingDecode> pend;
+    std::shared_ptr<Resolver> res;
     std::vector<Fix> lastDecoded;
     std::vector<RecPacket*> scratchRec;
     std::vector<unsigned> scratchLen;
@@ -72,7 +76,7 @@ void DecoderCore::adopt_spare()
     pickCol_.swap(s->pickCol);
     mat_.swap(s->mat);
     pivots_.swap(s->pivots);
-    pend_.swap(s->pend);
+    res_.swap(s->res);
     lastDecoded_.swap(s->lastDecoded);
     scratchRec_.swap(s->scratchRec);
     scratchLen_.swap(s->scratchLen);
@@ -95,12 +99,31 @@ void DecoderCore::donate_spare()
     pickCol_.clear();
     mat_.clear();
     pivots_.clear();
-    for (PendingDecode& pd : pend_) {
-        pd.fixes.clear();
-        pd.base = 0;
-        pd.m = 0;
-        pd.serial = 0;
-        pd.live = false;
+    if (res_ && res_.use_count() == 1) {
+        // no completion holds it: back to its freshly constructed state
+        for (PendingDecode& pd : res_->pend) {
+            pd.fixes.clear();
+            pd.words.clear();
+            pd.targets.clear();
+            pd.base = 0;
+            pd.m = 0;
+            pd.serial = 0;
+            pd.live = false;
+            pd.done = false;
+        }
+        res_->doneCount.store(0, std::memory_order_relaxed);
+        res_->orphan = false;
+        res_->out = nullptr;
+        res_->outCount = 0;
+        res_->outSerial = 0;
+    } else if (res_) {
+        // completions still queued or in flight: they fill the caller-owned
+        // entries they carry and leave this decoder's memory alone
+        std::lock_guard<std::mutex> g(res_->mu);
+        res_->orphan = true;
+        res_->out = nullptr;
+        res_->outCount = 0;
+        res_.reset();
     }
     lastDecoded_.clear();
     scratchRec_.clear();
@@ -118,7 +141,7 @@ void DecoderCore::donate_spare()
     pickCol_.swap(s->pickCol);
     mat_.swap(s->mat);
     pivots_.swap(s->pivots);
-    pend_.swap(s->pend);
+    res_.swap(s->res);
     lastDecoded_.swap(s->lastDecoded);
     scratchRec_.swap(s->scratchRec);
     scratchLen_.swap(s->scratchLen);
@@ -129,14 +152,8 @@ void DecoderCore::donate_spare()
 
 DecoderCore::~DecoderCore()
 {
-    if (pendingSolves_ > 0) {
-        // Completions must not reach a freed decoder: drop the ones still
-        // queued in our program, and let submitted ones finish first (the
-        // siamese_gpu.h contract has the caller wait before freeing; this
-        // covers callers that do not).
-        prog_.drop_callbacks();
-        eng_->wait(eng_->last_ticket());
-    }
+    // (completions still queued or in flight hold the shared resolver, not
+    // this decoder: nothing to wait for, see donate_spare)
     for (RecPacket* r = head_; r;) {
         RecPacket* n = r->next;
         free_packet(r);
@@ -233,6 +250,7 @@ bool DecoderCore::grow_window(unsigned end)
 
 SiameseResult DecoderCore::add_original(const SiameseOriginalPacket& packet, uint64_t deviceSrc)
 {
+    settle();
     // :1467-1536
     if (dead())
         return Siamese_Disabled;
@@ -652,6 +670,7 @@ void DecoderCore::list_delete_before(unsigned element)
 
 SiameseResult DecoderCore::add_recovery(const SiameseRecoveryPacket& packet)
 {
+    settle();
     if (dead())
         return Siamese_Disabled;
     RowMeta m;
@@ -665,6 +684,7 @@ SiameseResult DecoderCore::add_recovery(const SiameseRecoveryPacket& packet)
 
 SiameseResult DecoderCore::add_recovery_device(const DeviceRecovery& rec)
 {
+    settle();
     if (dead())
         return Siamese_Disabled;
     RowMeta m;
@@ -807,15 +827,21 @@ bool DecoderCore::add_single(const RowMeta& m, const uint8_t* headBytes, unsigne
     s.column = m.columnStart;
     s.pending = false;
 
-    if (!hasRecovered_) {
-        hasRecovered_ = true;
-        recovered_.clear();
+    {
+        // (a completion may be patching the previous decode's outputs)
+        std::lock_guard<std::mutex> g(res_->mu);
+        if (!hasRecovered_) {
+            hasRecovered_ = true;
+            recovered_.clear();
+            ++decodeSerial_;
+        }
+        SiameseOriginalPacket out;
+        out.PacketNum = m.columnStart;
+        out.DataBytes = length;
+        out.Data = (mirror_ ? s.host.data() : s.buf.ptr) + h;
+        recovered_.push_back(out);
+        publish_outputs();
     }
-    SiameseOriginalPacket out;
-    out.PacketNum = m.columnStart;
-    out.DataBytes = length;
-    out.Data = (mirror_ ? s.host.data() : s.buf.ptr) + h;
-    recovered_.push_back(out);
     recoveredColumns_.push_back(m.columnStart);
 
     if (element >= region_.elementStart && element < region_.nextCheckStart)
@@ -902,6 +928,7 @@ bool DecoderCore::check_recovery_possible()
 
 SiameseResult DecoderCore::is_ready()
 {
+    settle();
     if (hasRecovered_ || check_recovery_possible())
         return Siamese_Success;
     return Siamese_NeedMoreData;
@@ -909,6 +936,7 @@ SiameseResult DecoderCore::is_ready()
 
 SiameseResult DecoderCore::decode(SiameseOriginalPacket** packetsOut, unsigned* countOut)
 {
+    settle();
     if (dead())
         return Siamese_Disabled;
     if (hasRecovered_) {
@@ -1428,49 +1456,59 @@ SiameseResult DecoderCore::solve_and_substitute()
     const uint32_t base = prog_.solve(desc, coef.data(), maxBytes);
 
     // Host side of BackSubstitution: swap buffers into the window, record
-    // the outputs (lengths patched in resolve()).
-    recovered_.resize(m);
-    ++decodeSerial_;
-    // a free slot for this solve's completion state
-    unsigned slot = 0;
-    while (slot < pend_.size() && pend_[slot].live)
-        ++slot;
-    if (slot == pend_.size())
-        pend_.emplace_back();
-    PendingDecode& pd = pend_[slot];
-    pd.live = true;
-    pd.base = base;
-    pd.m = m;
-    pd.serial = decodeSerial_;
-    std::vector<Fix>& fixes = pd.fixes;
-    fixes.clear();
+    // the outputs (exact lengths arrive with the completion, complete_solve).
     bool advanced = false;
-    for (int ci = (int)m - 1; ci >= 0; --ci) {
-        RecPacket* r = pr[ci];
-        ColInfo& col = cols_[ci];
-        DecSlot* o = col.original;
-        DevBuf old = o->buf;
-        o->buf = r->buf;
-        o->bytes = len[ci];
-        o->column = col.column;
-        o->header = 0;
-        o->pending = true;
-        r->buf = old;
-        r->bytes = 0;
-        SiameseOriginalPacket& out = recovered_[ci];
-        out.PacketNum = col.column;
-        out.DataBytes = 0;
-        out.Data = nullptr;
-        recoveredColumns_.push_back(col.column);
-        advanced |= mark_got(col.column);
-        fixes.push_back(Fix{o, o->buf.ptr, (uint32_t)ci, (unsigned)ci, len[ci]});
+    unsigned slot = 0;
+    {
+        std::lock_guard<std::mutex> g(res_->mu);
+        recovered_.resize(m);
+        ++decodeSerial_;
+        // a free slot for this solve's completion state
+        std::vector<PendingDecode>& pend = res_->pend;
+        while (slot < pend.size() && pend[slot].live)
+            ++slot;
+        if (slot == pend.size())
+            pend.emplace_back();
+        PendingDecode& pd = pend[slot];
+        pd.live = true;
+        pd.done = false;
+        pd.base = base;
+        pd.m = m;
+        pd.serial = decodeSerial_;
+        pd.words.clear();
+        pd.targets.clear();
+        std::vector<Fix>& fixes = pd.fixes;
+        fixes.clear();
+        for (int ci = (int)m - 1; ci >= 0; --ci) {
+            RecPacket* r = pr[ci];
+            ColInfo& col = cols_[ci];
+            DecSlot* o = col.original;
+            DevBuf old = o->buf;
+            o->buf = r->buf;
+            o->bytes = len[ci];
+            o->column = col.column;
+            o->header = 0;
+            o->pending = true;
+            o->pendSlot = slot;
+            o->pendCi = (uint32_t)ci;
+            r->buf = old;
+            r->bytes = 0;
+            SiameseOriginalPacket& out = recovered_[ci];
+            out.PacketNum = col.column;
+            out.DataBytes = 0;
+            out.Data = nullptr;
+            recoveredColumns_.push_back(col.column);
+            advanced |= mark_got(col.column);
+            fixes.push_back(Fix{o, o->buf.ptr, (uint32_t)ci, (unsigned)ci, len[ci]});
+        }
+        lastDecoded_ = fixes;
+        publish_outputs();
     }
-    lastDecoded_ = fixes;
+    lastPendSlot_ = slot;
     pendingSolves_++;
     // (the back-substitution's reference source bytes need the recovered
-    // lengths: the solve kernel counts them, SiameseDecoder.cpp:1131-1212).
-    // The callback holds two words, so std::function keeps it inline.
-    prog_.on_complete([this, slot](const uint32_t* results) { resolve_solve(results, slot); });
+    // lengths: the solve kernel counts them, SiameseDecoder.cpp:1131-1212)
+    prog_.on_complete([r = res_, slot](const uint32_t* results) { complete_solve(*r, slot, results); });
 
     if (!advanced) {
         disabled_ = true;
@@ -1484,37 +1522,82 @@ SiameseResult DecoderCore::solve_and_substitute()
     return Siamese_Success;
 }
 
-void DecoderCore::resolve_solve(const uint32_t* results, unsigned slot)
+void DecoderCore::publish_outputs()
 {
-    PendingDecode& pd = pend_[slot];
-    const uint32_t base = pd.base;
-    const unsigned m = pd.m;
-    const unsigned okCount = results[base];
-    if (okCount < m)
-        disabled_ = true; // corrupt length prefix (reference :1142-1154)
-    for (const Fix& f : pd.fixes) {
-        const unsigned ci = f.outIndex;
-        if (ci + okCount < m)
-            continue; // not reached before the failure
-        const uint32_t w = results[base + 1 + ci];
-        const unsigned hdr = w >> 29;
-        const unsigned len = w & kSolveLengthMask;
-        DecSlot* s = f.slot;
-        if (s->pending && s->buf.ptr == f.buf) {
-            s->bytes = hdr + len;
-            s->header = hdr;
-            s->pending = false;
-            if (mirror_ && s->host.size() < s->bytes)
-                s->host.resize(s->bytes);
-        }
-        if (pd.serial == decodeSerial_ && ci < recovered_.size()) {
-            SiameseOriginalPacket& out = recovered_[ci];
-            out.DataBytes = len;
-            out.Data = (mirror_ ? s->host.data() : f.buf) + hdr;
-        }
+    res_->out = recovered_.data();
+    res_->outCount = recovered_.size();
+    res_->outSerial = decodeSerial_;
+}
+
+void DecoderCore::fill_entry(const PendingDecode& pd, unsigned ci, SiameseOriginalPacket& out)
+{
+    const unsigned okCount = pd.words[0];
+    if (ci >= pd.m || ci + okCount < pd.m) {
+        // not reached before a corrupt length prefix (reference :1142-1154)
+        out.DataBytes = 0;
+        out.Data = nullptr;
+        return;
     }
-    pd.live = false;
-    pendingSolves_--;
+    const uint32_t w = pd.words[1 + ci];
+    out.DataBytes = w & kSolveLengthMask;
+    out.Data = pd.fixes[pd.m - 1 - ci].buf + (w >> 29);
+}
+
+// Engine completer thread: the submission carrying the solve has completed.
+void DecoderCore::complete_solve(Resolver& r, unsigned slot, const uint32_t* results)
+{
+    std::lock_guard<std::mutex> g(r.mu);
+    PendingDecode& pd = r.pend[slot];
+    pd.words.assign(results + pd.base, results + pd.base + pd.m + 1);
+    for (const auto& t : pd.targets)
+        fill_entry(pd, t.first, *t.second);
+    pd.targets.clear();
+    if (!r.orphan && !r.mirror && pd.serial == r.outSerial)
+        for (unsigned ci = 0; ci < pd.m && ci < r.outCount; ++ci)
+            fill_entry(pd, ci, r.out[ci]);
+    pd.done = true;
+    r.doneCount.fetch_add(1, std::memory_order_release);
+}
+
+// Owner thread: apply arrived completions to the decoder's own state.
+void DecoderCore::apply_resolved()
+{
+    std::lock_guard<std::mutex> g(res_->mu);
+    std::vector<PendingDecode>& pend = res_->pend;
+    for (unsigned k = 0; k < pend.size(); ++k) {
+        PendingDecode& pd = pend[k];
+        if (!pd.live || !pd.done)
+            continue;
+        const unsigned m = pd.m;
+        const unsigned okCount = pd.words[0];
+        if (okCount < m)
+            disabled_ = true; // corrupt length prefix (reference :1142-1154)
+        for (const Fix& f : pd.fixes) {
+            const unsigned ci = f.outIndex;
+            if (ci + okCount < m)
+                continue; // not reached before the failure
+            const uint32_t w = pd.words[1 + ci];
+            const unsigned hdr = w >> 29;
+            const unsigned len = w & kSolveLengthMask;
+            DecSlot* s = f.slot;
+            if (s->pending && s->buf.ptr == f.buf && s->pendSlot == k && s->pendCi == ci) {
+                s->bytes = hdr + len;
+                s->header = hdr;
+                s->pending = false;
+                if (mirror_ && s->host.size() < s->bytes)
+                    s->host.resize(s->bytes);
+            }
+            if (mirror_ && pd.serial == decodeSerial_ && ci < recovered_.size()) {
+                SiameseOriginalPacket& out = recovered_[ci];
+                out.DataBytes = len;
+                out.Data = s->host.data() + hdr;
+            }
+        }
+        pd.live = false;
+        pd.done = false;
+        pendingSolves_--;
+        ++appliedCount_;
+    }
 }
 
 void DecoderCore::download_recovered()
@@ -1531,6 +1614,7 @@ void DecoderCore::download_recovered()
 
 SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
 {
+    settle();
     if (dead())
         return Siamese_Disabled;
     const unsigned element = column_to_element(packet.PacketNum);
@@ -1541,7 +1625,10 @@ SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
     }
     if (slot(element).pending) {
         // Exact length still on the device: finish the outstanding work.
-        if (!eng_->flush_and_sync() || dead())
+        if (!eng_->flush_and_sync())
+            return Siamese_Disabled;
+        settle();
+        if (dead())
             return Siamese_Disabled;
     }
     DecSlot& s = slot(element);
@@ -1550,8 +1637,68 @@ SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
     return Siamese_Success;
 }
 
+SiameseResult DecoderCore::decode_deferred(SiameseOriginalPacket* out, unsigned capacity, unsigned* countOut)
+{
+    settle();
+    *countOut = 0;
+    // room for any decode's outputs: a solve returns at most 255 packets
+    // (kMaximumLossRecoveryCount), the single-recovery path what it holds
+    if (capacity < kMaxLossRecovery || (hasRecovered_ && recovered_.size() > capacity))
+        return Siamese_InvalidInput;
+    SiameseOriginalPacket* p = nullptr;
+    unsigned n = 0;
+    const uint64_t serial = decodeSerial_;
+    const SiameseResult r = decode(&p, &n);
+    if (r != Siamese_Success)
+        return r;
+    std::copy(p, p + n, out);
+    *countOut = n;
+    if (decodeSerial_ != serial) {
+        // a solve queued by this call: its lengths arrive with its completion
+        std::lock_guard<std::mutex> g(res_->mu);
+        PendingDecode& pd = res_->pend[lastPendSlot_];
+        for (unsigned i = 0; i < n; ++i) {
+            if (pd.done)
+                fill_entry(pd, i, out[i]);
+            else
+                pd.targets.emplace_back(i, &out[i]);
+        }
+    }
+    return Siamese_Success;
+}
+
+SiameseResult DecoderCore::get_deferred(SiameseOriginalPacket& packet)
+{
+    settle();
+    if (dead())
+        return Siamese_Disabled;
+    const unsigned element = column_to_element(packet.PacketNum);
+    if (element >= count_ || slot(element).bytes == 0) {
+        packet.Data = nullptr;
+        packet.DataBytes = 0;
+        return Siamese_NeedMoreData;
+    }
+    DecSlot& s = slot(element);
+    if (!s.pending) {
+        packet.Data = (mirror_ ? s.host.data() : s.buf.ptr) + s.header;
+        packet.DataBytes = s.bytes - s.header;
+        return Siamese_Success;
+    }
+    std::lock_guard<std::mutex> g(res_->mu);
+    PendingDecode& pd = res_->pend[s.pendSlot];
+    if (pd.done) {
+        fill_entry(pd, s.pendCi, packet);
+    } else {
+        packet.Data = nullptr;
+        packet.DataBytes = 0;
+        pd.targets.emplace_back(s.pendCi, &packet);
+    }
+    return Siamese_Success;
+}
+
 SiameseResult DecoderCore::stats(uint64_t* out, unsigned count)
 {
+    settle();
     if (count > SiameseDecoderStats_Count)
         count = SiameseDecoderStats_Count;
     uint64_t mem = 0;

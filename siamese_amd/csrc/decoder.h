@@ -20,7 +20,9 @@
 #include "objpool.h"
 #include "../../include/siamese.h"
 
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 namespace sgpu {
@@ -32,6 +34,8 @@ struct DecSlot
     unsigned column = 0;        // packet number, or matrix column while lost
     unsigned header = 0;
     bool pending = false;       // recovered, exact length not yet known
+    uint32_t pendSlot = 0;      // while pending: the solve that recovers it (Resolver::pend index)
+    uint32_t pendCi = 0;        //   and its column within that solve
     std::vector<uint8_t> host;  // host mirror (drop-in mode)
 };
 
@@ -100,16 +104,35 @@ public:
     /// Queues the solve; packets' lengths become exact after resolve().
     SiameseResult decode(SiameseOriginalPacket** packetsOut, unsigned* countOut);
     SiameseResult get(SiameseOriginalPacket& packet);
+    /// Deferred forms (siamese_gpu.h sgpu_decode_deferred /
+    /// sgpu_decoder_get_deferred): never wait for the device.  Outputs go to
+    /// caller-owned entries; an entry whose length is still being solved gets
+    /// Data/DataBytes written when the submission carrying the solve
+    /// completes (before that submission reads as done).
+    SiameseResult decode_deferred(SiameseOriginalPacket* out, unsigned capacity, unsigned* countOut);
+    SiameseResult get_deferred(SiameseOriginalPacket& packet);
+    /// Apply completed solves to the decoder's own state (recovered slots'
+    /// exact lengths, a corrupt prefix's Disabled): every call does this first.
+    void settle()
+    {
+        if (res_->doneCount.load(std::memory_order_acquire) != appliedCount_)
+            apply_resolved();
+    }
     SiameseResult stats(uint64_t* out, unsigned count);
     /// ARQ: siamese_decoder_ack (arq.cpp)
     SiameseResult acknowledgement(uint8_t* buffer, unsigned byteLimit, unsigned& usedBytes);
 
     /// Disabled: this instance failed (sticky), or the device did (Engine::failed).
-    bool disabled() const { return dead(); }
+    bool disabled()
+    {
+        settle();
+        return dead();
+    }
     bool dead() const { return disabled_ || eng_->failed(); }
     /// Packet present in the window (received or recovered, length may be pending)
     bool has(unsigned packetNum)
     {
+        settle();
         const unsigned e = column_to_element(packetNum);
         return !dead() && e < count_ && slot(e).bytes > 0;
     }
@@ -255,17 +278,47 @@ private:
         unsigned outIndex;     // index into recovered_
         unsigned bound;        // upper bound on the length (row length)
     };
-    /// A queued solve whose completion has not run yet (slots are reused).
+    /// A queued solve whose completion has not been applied yet (slots are
+    /// reused).  Written by the owner thread when the decode queues the solve
+    /// and by the engine's completer thread when its submission completes,
+    /// both under Resolver::mu.
     struct PendingDecode
     {
-        std::vector<Fix> fixes;
+        std::vector<Fix> fixes;       // by descending column: fixes[m - 1 - ci] is column ci
         uint32_t base = 0;
         unsigned m = 0;
         uint64_t serial = 0;
-        bool live = false;
+        bool live = false;            // queued, not yet applied to the decoder's slots
+        bool done = false;            // the completion arrived: `words` holds the results
+        std::vector<uint32_t> words;  // [0] rows recovered, [1 + ci] header << 29 | length
+        /// caller-owned outputs to fill at completion (deferred API): (ci, entry)
+        std::vector<std::pair<unsigned, SiameseOriginalPacket*>> targets;
     };
-    void resolve_solve(const uint32_t* results, unsigned slot);
-    std::vector<PendingDecode> pend_;
+    /// Shared between the decoder and the completions it queued, so a freed
+    /// decoder never waits for them: a completion that finds the decoder
+    /// gone (orphan) still fills the caller-owned entries, nothing else.
+    struct Resolver
+    {
+        std::mutex mu;
+        std::vector<PendingDecode> pend;
+        std::atomic<uint64_t> doneCount{0};   // completions arrived (monotonic)
+        bool orphan = false;
+        // the legacy output array (sgpu_decode / siamese_decode, valid until
+        // the next decode): patched by the completer when it still belongs to
+        // the decode that queued the solve (batch API; the drop-in mirror
+        // patches on the owner's thread in apply_resolved)
+        SiameseOriginalPacket* out = nullptr;
+        size_t outCount = 0;
+        uint64_t outSerial = 0;
+        bool mirror = false;
+    };
+    static void complete_solve(Resolver& r, unsigned slot, const uint32_t* results);
+    static void fill_entry(const PendingDecode& pd, unsigned ci, SiameseOriginalPacket& out);
+    void apply_resolved();
+    void publish_outputs();   // Resolver::out* = recovered_ (caller holds res_->mu)
+    std::shared_ptr<Resolver> res_;
+    uint64_t appliedCount_ = 0;
+    unsigned lastPendSlot_ = 0;   // Resolver::pend slot of the latest queued solve
     std::vector<Fix> lastDecoded_;
     // scratch of solve_and_substitute (reused across decodes)
     std::vector<RecPacket*> scratchRec_;

@@ -469,8 +469,13 @@ static void solve_main(const SolveDesc* solves, const SolveRow* rows, const uint
             const uint8_t inv = g_inv[C[(size_t)i * m + i]];
             for (uint32_t b = t0; b < fb; ++b)
                 P(R[i].buf)[b] = b < bb ? gf_mul(P(R[i].buf)[b], inv) : 0;
-            for (uint32_t b = fb > t0 ? fb : t0; b < clip((bb + 15) & ~15u); ++b)
-                P(R[i].buf)[b] = 0;   // the kernel stores whole 16-byte lanes
+            // the kernel stores whole 16-byte lanes for every byte below the
+            // row's final length, zero past the recovered length: bytes up to
+            // align16(finalBytes) read as zero afterwards (a pending slot's
+            // length bound is finalBytes, siamese_amd/csrc/decoder.h)
+            const uint32_t fbEnd = (R[i].finalBytes > bb ? R[i].finalBytes : bb);
+            for (uint32_t b = fb > t0 ? fb : t0; b < clip((fbEnd + 15) & ~15u); ++b)
+                P(R[i].buf)[b] = 0;
             for (uint32_t j = 0; j < (uint32_t)i; ++j) {
                 const uint8_t c = C[(size_t)j * m + i];
                 if (!c)

@@ -83,3 +83,33 @@ def test_hostsim_batch_end_to_end_pipelined(name):
     res, rep = S.run_batch(S.SIM_LIB, cfg, steps=3, verify=True, threads=4, groups=2, e2e=True)
     _check(name, res)
     assert rep.mismatches == 0 and rep.checked > 0
+
+
+@pytest.mark.parametrize("name", SMALL)
+@pytest.mark.parametrize("defer", [1, 3])
+def test_hostsim_deferred_outputs_match_golden(name, defer):
+    """Deferred outputs (sgpu_decode_deferred / sgpu_decoder_get_deferred): a
+    stream yields only after every `defer`-th decode and each group keeps two
+    submissions in flight, so instances are driven while their solves are
+    still pending (recovered lengths are bounds until the completion is
+    applied).  Every byte is verified and the digests are the reference's."""
+    cfg = golden.config(name)
+    res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True, defer=defer, threads=4,
+                           groups=2 if cfg.streams >= 8 else 1)
+    _check(name, res)
+    assert rep.mismatches == 0
+
+
+@pytest.mark.parametrize("name", ["edge_lag", "C1var", "edge_var_block"])
+def test_hostsim_deferred_length_only(name):
+    """Length-only digests (hash_data=0: no yield after each encode) with
+    variable packet sizes: the rounds hold several decodes with recovered
+    lengths still pending, and every recovered byte must still verify."""
+    cfg = S.replace(golden.config(name), hash_data=0)
+    ref, _, _ = S.run_capi(S.REF_LIB, cfg) if os.path.exists(S.REF_LIB) else (None, 0, 0)
+    for defer in (1, 4):
+        res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True, defer=defer, threads=4)
+        assert rep.mismatches == 0 and rep.checked > 0
+        assert not any(r.status for r in res)
+        if ref is not None:
+            assert S.digests(res) == S.digests(ref)
