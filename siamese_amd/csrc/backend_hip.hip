@@ -351,9 +351,12 @@ __device__ __forceinline__ uint4 op_word(const uint4* ring, const uint4* __restr
 // false for an absent term.  The loads of up to kExecDepth terms go out back
 // to back before the first is used; a term that ends before the tile is not
 // loaded.
-template <class Fetch>
+template <bool Exact = false, class Fetch>
 __device__ __forceinline__ void gather(uint32_t k0, uint32_t k1, uint32_t tileBase, uint32_t p,
                                        uint32_t& acc0, uint32_t& acc1, Fetch&& fetch)
+// (Exact: bytes at or past a term's length read as zero even inside its last
+// dword -- the lane sums of a row batch, which an update in the same batch may
+// have grown past the length the row reads)
 {
     for (uint32_t k = k0; k < k1; k += kExecDepth) {
         uint32_t v[kExecDepth], ca[kExecDepth];
@@ -365,6 +368,8 @@ __device__ __forceinline__ void gather(uint32_t k0, uint32_t k1, uint32_t tileBa
             uint32_t len = 0;
             act[u] = idx < k1 && fetch(idx, src, len, ca[u]) && tileBase < len;
             v[u] = act[u] ? term_load(src, len, p) : 0u;
+            if (Exact && p < len)
+                v[u] &= byte_mask((int)len - (int)p);
         }
 #pragma unroll
         for (unsigned u = 0; u < kExecDepth; ++u) {
@@ -651,6 +656,99 @@ __global__ __launch_bounds__(64 * kLdpcWaves) void k_ldpc(const LdpcItem* __rest
     }
 }
 
+// Versioned sum reads (RowItem.cutoff, ops.h): a row's selected sums as it
+// read them = the batch's final sums with the contributions of each update's
+// elements at or past the row's cutoff taken back out.  Quad layout (planned
+// rows): the lane holds bytes [p16, p16 + 16) of its quad's row; m0 / m1 /
+// cut are the quad's row's masks and cutoff (per lane), `live` whether the
+// row reaches this tile.
+__device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_t cut, bool live, uint32_t p16,
+                                               uint32_t b4, const uint32_t* updOfL, const uint32_t* updFromL,
+                                               const uint32_t* updToL, const uint32_t* cxL, const uint4* permL,
+                                               const uint32_t* permC, const uint32_t* stage, uint32_t stageLo,
+                                               uint32_t staged, const uint4* tableL, const uint4* __restrict__ seg,
+                                               uint32_t blk, uint4& a0, uint4& a1)
+{
+    for (uint32_t k = 0; k < kRowSums; ++k) {
+        if (updOfL[k] == 0xffu)
+            continue;   // (uniform) sum k has no update in this batch
+        const uint32_t from = updFromL[k], to = updToL[k];
+        const bool in0 = (m0 >> k) & 1u, in1 = (m1 >> k) & 1u;
+        // the update's first element at or past the cutoff (its lane's grid)
+        uint32_t e = cut <= from ? from : from + ((cut - from + kLanes - 1) / kLanes) * kLanes;
+        if (!live || !(in0 || in1))
+            e = to;
+        const uint32_t sidx = k % kSums;
+        const uint32_t slen = tableL[k].z;   // the sum's length as the rows read it (clips the terms)
+        if (p16 >= slen)
+            e = to;
+        for (; e < to; e += kLanes) {
+            uint4 v;
+            if (e - stageLo < staged) {
+                v = lds16(stage, (kRowSums + e - stageLo) * 64 + b4);
+            } else {
+                const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
+                const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+                v = p16 < d.z ? ld16(src + p16) : make_uint4(0, 0, 0, 0);
+            }
+            if (sidx != 0) {
+                const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e).w;
+                const uint32_t cx = cxL[col % kColumnValuePeriod];
+                v = gf_mul16_tab(v, gf_tab_l(permL, permC, sidx == 1 ? (cx & 0xffu) : (cx >> 8)));
+            }
+            if (p16 + 16 > slen)
+                v = mask16(v, (int)slen - (int)p16);
+            if (in0)
+                a0 = xor16(a0, v);
+            if (in1)
+                a1 = xor16(a1, v);
+        }
+    }
+}
+
+// The same for a row in the dword layout (general path: one wave, the lane
+// holds bytes [p, p + 4)); m0 / m1 / cut are wave-uniform.
+__device__ __forceinline__ void row_versions4(uint32_t m0, uint32_t m1, uint32_t cut, uint32_t tileBase, uint32_t p,
+                                              uint32_t lane, const uint32_t* updOfL, const uint32_t* updFromL,
+                                              const uint32_t* updToL, const uint32_t* cxL, const uint32_t* stage,
+                                              uint32_t stageLo, uint32_t staged, const uint4* tableL,
+                                              const uint4* __restrict__ seg, uint32_t blk, uint32_t& acc0,
+                                              uint32_t& acc1)
+{
+    for (uint32_t k = 0; k < kRowSums; ++k) {
+        const bool in0 = (m0 >> k) & 1u, in1 = (m1 >> k) & 1u;
+        if ((!in0 && !in1) || uni(updOfL[k]) == 0xffu)
+            continue;
+        const uint32_t from = uni(updFromL[k]), to = uni(updToL[k]);
+        const uint32_t sidx = k % kSums;
+        const uint32_t slen = uni(tableL[k].z);   // the sum's length as the row reads it (clips the terms)
+        if (tileBase >= slen)
+            continue;
+        const uint32_t clip = byte_mask((int)slen - (int)p);
+        for (uint32_t e = cut <= from ? from : from + ((cut - from + kLanes - 1) / kLanes) * kLanes; e < to;
+             e += kLanes) {
+            uint32_t v;
+            const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
+            if (e - stageLo < staged) {
+                v = stage[(kRowSums + e - stageLo) * 64 + lane];
+            } else {
+                const uint64_t src = ((uint64_t)uni(d.y) << 32) | uni(d.x);
+                const uint32_t len = uni(d.z);
+                v = tileBase < len ? term_load(src, len, p) : 0u;
+            }
+            if (sidx != 0) {
+                const uint32_t cx = cxL[uni(d.w) % kColumnValuePeriod];
+                v = gf_mul_dword(v, sidx == 1 ? (cx & 0xffu) : (cx >> 8));
+            }
+            v &= clip;
+            if (in0)
+                acc0 ^= v;
+            if (in1)
+                acc1 ^= v;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
                                                        const ExecItem* __restrict__ items,
                                                        unsigned long long* __restrict__ acct,
@@ -665,6 +763,10 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ unsigned long long acctL;          // reference source bytes counted by this workgroup
     __shared__ uint32_t generalRows;               // a row of this OP_ROWS batch has no plan
     __shared__ uint32_t sumsDirty;                 // a staged lane sum must be re-read after the updates
+    // versioned sum reads (RowItem.cutoff): per sum k, the batch's update of
+    // it (index, or 0xff) and that update's element range [from, to)
+    __shared__ uint32_t updOfL[kRowSums];
+    __shared__ uint32_t updFromL[kRowSums], updToL[kRowSums];
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
@@ -793,6 +895,21 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             // (the host points the stage at the elements the batch reads:
             // GfOp.dst low word = stageLo, ops.h)
             const uint32_t stageLo = uni(h0.x) < E ? uni(h0.x) : E;
+            if (tid < kRowSums) {
+                // (at most one update per sum in a batch: Program::rows_update)
+                uint32_t found = 0xffu, from = 0, to = 0;
+                for (uint32_t u = 0; u < U; ++u) {
+                    const uint4 w1 = table_entry(tableL, seg, blk, kRowSums + E + u * kUpdateWords + 1);
+                    if (w1.z == tid && w1.y > w1.x) {
+                        found = u;
+                        from = w1.x;
+                        to = w1.y;
+                    }
+                }
+                updOfL[tid] = found;
+                updFromL[tid] = from;
+                updToL[tid] = to;
+            }
             const uint32_t staged = E - stageLo < stageCap ? E - stageLo : stageCap;
             const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
             const bool sumsStaged = stageSlots >= kRowSums;
@@ -1099,8 +1216,10 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     const uint64_t src = ((uint64_t)uni(d.y) << 32) | uni(d.x);
                     const uint32_t len = uni(d.z);
                     if (src == udst) {
+                        // (exactly the sum's first `len` bytes, as the rows read
+                        // it: with versioned reads the update may have grown it)
                         if (align16u(len) <= align16u(un))
-                            stage[k * 64 + lane] = p < align16u(len) ? out : 0u;
+                            stage[k * 64 + lane] = p < len ? out & byte_mask((int)len - (int)p) : 0u;
                         else
                             stale = true;
                     }
@@ -1120,7 +1239,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     const uint64_t src = ((uint64_t)d.y << 32) | d.x;
                     uint4 v = make_uint4(0, 0, 0, 0);
                     if (tileBase + q16 < d.z)
-                        v = ld16(src + tileBase + q16);
+                        v = mask16(ld16(src + tileBase + q16), (int)d.z - (int)(tileBase + q16));
                     *reinterpret_cast<uint4*>(&stage[k * 64 + q16 / 4]) = v;
                 }
                 __syncthreads();
@@ -1196,6 +1315,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             SGPU_QUAD_GROUP(12)
 #undef SGPU_QUAD_GROUP
                     }
+                    // (rows read the sums as of their cutoff, ops.h RowItem)
+                    row_versions16(w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, live, p16, b4, updOfL, updFromL,
+                                   updToL, cxL, permL, permC, stage, stageLo, staged, tableL, seg, blk, a0, a1);
                     PHASE_MARK(14, qclk);
                     if (live)
                         store_item16(xor16(a0, gf_mul16_tab(a1, tab)), p16, rdst, rn, rvalid, cur);
@@ -1243,7 +1365,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     // lane*3+s; mask1 feeds the product)
                     if (q == 0) {
                         uint64_t bits = (uint64_t)(m0 & 0xffffffu) | ((uint64_t)(m1 & 0xffffffu) << 24);
-                        gather(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
+                        gather<true>(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
                                [&](uint32_t, uint64_t& src, uint32_t& len, uint32_t& ca) {
                                    const uint32_t b = (uint32_t)__builtin_ctzll(bits);
                                    bits &= bits - 1;
@@ -1252,6 +1374,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                    ca = 1u | ((b >= kRowSums ? 1u : 0u) << 8);
                                    return len != 0;
                                });
+                        // (the sums as of the row's cutoff, ops.h RowItem)
+                        row_versions4(m0 & 0xffffffu, m1 & 0xffffffu, uni(w2.y), tileBase, p, lane, updOfL, updFromL,
+                                      updToL, cxL, stage, stageLo, staged, tableL, seg, blk, acc0, acc1);
                     }
                     // sparse part: this unit's share of the 2*ceil(N/16) draws
                     // (pairs stay whole: even draw -> row, odd -> product)

@@ -1384,7 +1384,7 @@ bool DecoderCore::eliminate_original_data()
         // rows of one decode share the sums: one row of the program's batch
         cover(windowLo_, ee);
         prog_.rows_row(sums, rec->buf.addr(), rb, rb, row_value(m.row), mask[0], mask[1], m.row,
-                       m.ldpcCount, es);
+                       m.ldpcCount, es, ee);
         eng_->account(opBytes);
     }
     // the window snapshot must not see this decode's recoveries

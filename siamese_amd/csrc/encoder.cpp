@@ -470,7 +470,7 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     // of the program's Siamese row batch (consecutive rows share the sums)
     cover(std::min(start, sumStart_), sumEnd_);
     prog_.rows_row(sumTable_, recovery_.addr(), recoveryBytes, 0, row_value(row), mask[0], mask[1], row,
-                   n, start, footer, footerBytes);
+                   n, start, count_, footer, footerBytes);
     eng_->account(opBytes);
 
     finish_row(out, m, recoveryBytes, true);

@@ -114,6 +114,7 @@ void ProgramBody::rows_open(uint32_t base, bool keepWindow)
     rb.open = true;
     rb.haveSums = false;
     rb.readMask = 0;
+    rb.cutMax = 0;
     if (!keepWindow) {
         rb.base = base;
         rb.win.clear();
@@ -567,10 +568,20 @@ void Program::rows_update(unsigned k, uint64_t dst, uint32_t n, uint32_t valid, 
                           uint32_t fromElement, uint32_t toElement)
 {
     ProgramBody::RowsBuild& b = b_->rb;
-    // a row of this batch already read sum k: the update belongs to a new
-    // batch over the same window (its rows run after this batch's rows)
-    if (b.readMask >> k & 1)
-        rows_open(b.base, true);
+    // A row of this batch already read sum k: the update may join the batch
+    // only if it extends the sum those rows read (same buffer, keeping every
+    // byte they saw), so each row can take back what was folded in after it
+    // (RowItem.cutoff).  A restarted or moved sum starts a new batch, whose
+    // rows run after this batch's rows.
+    static const bool versioned = [] {
+        const char* v = std::getenv("SIAMESE_AMD_ROW_VERSIONS");   // 0: a batch per sum re-read (A/B aid)
+        return !v || std::atoi(v) != 0;
+    }();
+    if (b.readMask >> k & 1) {
+        const WinEntry& seen = b.sums[k];
+        if (!versioned || seen.src != dst || valid < seen.len)
+            rows_open(b.base, true);
+    }
     const uint32_t from = fromElement - b.base, to = toElement - b.base;
     int& ui = b.updateOf[k];
     if (ui >= 0) {
@@ -608,11 +619,14 @@ void Program::rows_update(unsigned k, uint64_t dst, uint32_t n, uint32_t valid, 
 
 void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix,
                        uint32_t mask0, uint32_t mask1, unsigned row, uint32_t ldpcN,
-                       uint32_t ldpcFirst, const uint8_t* lit, uint32_t litLen)
+                       uint32_t ldpcFirst, uint32_t cutoff, const uint8_t* lit, uint32_t litLen)
 {
     ProgramBody::RowsBuild& b = b_->rb;
-    if (b.haveSums && std::memcmp(b.sums, sums, sizeof(b.sums)) != 0)
+    // (a row whose cutoff is below an earlier row's reads sums folded past
+    // its own cutoff: it starts a batch after every update so far)
+    if ((b.haveSums && std::memcmp(b.sums, sums, sizeof(b.sums)) != 0) || cutoff < b.cutMax)
         rows_open(b.base, true);
+    b.cutMax = std::max(b.cutMax, cutoff);
     if (!b.haveSums) {
         std::memcpy(b.sums, sums, sizeof(b.sums));
         b.haveSums = true;
@@ -627,6 +641,7 @@ void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t 
     r.row = row;
     r.ldpcN = ldpcN;
     r.ldpcOff = ldpcFirst - b.base;
+    r.cutoff = cutoff - b.base;
     if (litLen)
         std::memcpy(r.lit, lit, litLen);
     b.rows.push_back(r);

@@ -93,6 +93,7 @@ struct ProgramBody
         bool haveSums = false;
         WinEntry sums[kRowSums];
         uint32_t readMask = 0;          // sums read by the batch's rows
+        uint32_t cutMax = 0;            // largest row cutoff so far (absolute element)
         uint32_t base = 0;              // window element of entry 0
         std::vector<WinEntry> win;
         std::vector<SumUpdate> updates;
@@ -226,9 +227,11 @@ public:
     WinEntry* rows_window(uint32_t lo, uint32_t hi, uint32_t* from);
     void rows_update(unsigned sumIndex, uint64_t dst, uint32_t n, uint32_t valid, unsigned s,
                      uint32_t fromElement, uint32_t toElement);
+    /// `cutoff`: the row reads each sum as folded over window elements below
+    /// it (every sum the row reads was brought up to it; RowItem.cutoff).
     void rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix,
                   uint32_t mask0, uint32_t mask1, unsigned row, uint32_t ldpcN,
-                  uint32_t ldpcFirst, const uint8_t* lit = nullptr, uint32_t litLen = 0);
+                  uint32_t ldpcFirst, uint32_t cutoff, const uint8_t* lit = nullptr, uint32_t litLen = 0);
     /// Close the open batch (its window may change after this).
     void rows_seal()
     {

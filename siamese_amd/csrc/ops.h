@@ -114,6 +114,15 @@ struct SumUpdate
 ///   acc1 = sums selected by mask1              ^ window[ldpcOff + PCG_2i+1 % ldpcN]
 /// over i < ceil(ldpcN/16) pairs of PCG.Seed(row, ldpcN) draws, then litLen
 /// footer bytes at dst + n.
+///
+/// A row reads each sum as it stood when the row was made: the batch's sum
+/// updates are incremental (each extends its sum over later window elements,
+/// SumUpdate), so sum k as row r reads it is the sum after every update of
+/// the batch with the contributions of the update's elements at or past the
+/// row's `cutoff` (batch-relative element index) taken back out.  Rows made
+/// one after another in a streaming encoder (each folding the originals
+/// added since the previous one into the sums it reads) then share one batch
+/// instead of a batch each.
 struct RowItem
 {
     uint64_t dst;
@@ -124,7 +133,7 @@ struct RowItem
     uint32_t row;
     uint32_t ldpcN;
     uint32_t ldpcOff;
-    uint32_t pad;
+    uint32_t cutoff;     // sums as of window elements < cutoff (batch-relative)
     uint8_t lit[8];
 };
 /// RowItem.mask0 bit 31: a wide row whose LDPC sums k_ldpc computed

@@ -97,6 +97,7 @@ struct TileTerm
     uint64_t src;
     uint32_t len;
     uint8_t coeff, acc;
+    bool exact = false;   // read exactly len bytes (a clipped term), not through its last lane
 };
 
 void lincomb_tile(uint64_t dstAddr, uint32_t n, uint32_t valid, uint32_t mix,
@@ -116,7 +117,7 @@ void lincomb_tile(uint64_t dstAddr, uint32_t n, uint32_t valid, uint32_t mix,
         // read through the end of the term's last 16-byte lane, as the kernel
         // does: those bytes must be zero in memory (ops.h), and garbage there
         // shows up as a parity failure here
-        const uint32_t lenA = (tm.len + 15) & ~15u;
+        const uint32_t lenA = tm.exact ? tm.len : (tm.len + 15) & ~15u;
         const unsigned k = (lenA < end ? lenA : end) - t0;
         std::memcpy(tmp, P(tm.src) + t0, k);
         if (tm.coeff != 1)
@@ -240,10 +241,37 @@ void exec_tile(const uint8_t* stream, const ExecItem& it, uint64_t* acct)
             const RowItem& h = rows[r];
             terms.clear();
             for (unsigned k = 0; k < kRowSums; ++k) {
+                // (exactly the sum's first len bytes: an update of this batch
+                // may have grown it past what the row reads, ops.h RowItem)
                 if ((h.mask0 >> k & 1) && sums[k].len)
-                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 0});
+                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 0, true});
                 if ((h.mask1 >> k & 1) && sums[k].len)
-                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 1});
+                    terms.push_back(TileTerm{sums[k].src, sums[k].len, 1, 1, true});
+            }
+            // versioned sum reads (ops.h RowItem.cutoff): take back out the
+            // update elements at or past the row's cutoff
+            for (uint32_t u = 0; u < U; ++u) {
+                const SumUpdate& up = ups[u];
+                const uint32_t k = up.sum;
+                const bool in[2] = {(h.mask0 >> k & 1) != 0 && k < kRowSums, (h.mask1 >> k & 1) != 0 && k < kRowSums};
+                if (!in[0] && !in[1])
+                    continue;
+                // (clipped to the sum's length as the row reads it)
+                const uint32_t slen = sums[k].len;
+                for (uint32_t e = up.from; e < up.to; e += kLanes) {
+                    if (e < h.cutoff || win[e].len == 0)
+                        continue;
+                    uint8_t c = 1;
+                    if (up.s > 0) {
+                        c = column_value(win[e].column);
+                        if (up.s == 2)
+                            c = gf_sqr(c);
+                    }
+                    const uint32_t len = win[e].len < slen ? win[e].len : slen;
+                    for (uint8_t a = 0; a < 2; ++a)
+                        if (in[a] && len)
+                            terms.push_back(TileTerm{win[e].src, len, c, a, len < win[e].len});
+                }
             }
             if (h.mask0 & kRowWide) {
                 // L0 / L1 of a wide row (k_ldpc), as two draws
