@@ -171,24 +171,27 @@ def engine_bytes(rep):
     return eng, eng["ref_op_bytes"] + eng["out_bytes"]
 
 
-def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu_sample):
+def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu_sample, defer):
     """One extra BASELINE config on one GPU: a verified warm-up, then `runs`
     timed runs ONE AT A TIME (no run overlaps another run of the same
     streams), the median reported; the reference on the host beside it.
     C2's 1024 streams run in two pipelined stream groups (one group's host
     work beside the other's device work: 22.5-24.4 vs 25.0-26.6 ms per run
     with one group, same box, profiles/r2l_c2_groups_ab.txt); a single
-    stream is one group."""
+    stream is one group.  `defer`: the deferred-output API (siamese_gpu.h),
+    a stream submits after every `defer`-th decode and is driven on while
+    up to two of its submissions run (profiles/r3c_defer_sweep.txt)."""
     groups = 2 if cfg.streams >= 64 else 1
     sess = S.BatchSession(library, cfg, device=device)
     per = []
     try:
-        res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=groups)
+        res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=groups,
+                            defer=defer)
         if rep.mismatches or any(r.status for r in res):
             raise RuntimeError("bench leg %s: verification failed" % name)
         for _ in range(runs):
             res, rep = sess.run(steps=1, warmup=0, verify=False, threads=threads, groups=groups,
-                                digest=False)
+                                digest=False, defer=defer)
             per.append(rep)
     finally:
         sess.close()
@@ -205,6 +208,7 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
             cfg.loss_pct),
         "runs": runs,
         "stream_groups": groups,
+        "defer": defer,
         "ms_per_run": round(sec * 1e3, 3),
         "ms_per_run_all": [round(r.seconds * 1e3, 3) for r in per],
         "value": round(alg / sec / 1e9, 3),
@@ -269,20 +273,20 @@ def legs(library, device, threads, use_cpu):
         # C2: 1024 streams, Cauchy/parity path; reference on all host cores
         ("C2", S.replace(S.CONFIGS["C2"], hash_data=0), 3,
          S.replace(S.CONFIGS["C2"], hash_data=0), cpu_threads,
-         "the full C2 (1024 streams x 256 x 1400 B)"),
+         "the full C2 (1024 streams x 256 x 1400 B)", 4),
         # C3: one stream; reference on one core (an instance is single-threaded)
         ("C3", S.replace(S.CONFIGS["C3"], hash_data=0), 3,
-         S.replace(S.CONFIGS["C3"], hash_data=0), 1, "the full C3 (1 stream x 8192 x 1400 B)"),
+         S.replace(S.CONFIGS["C3"], hash_data=0), 1, "the full C3 (1 stream x 8192 x 1400 B)", 8),
         # C5: one stream of 64 KiB symbols; reference on one core over the
         # first 2000 originals (the whole stream takes it ~15 s)
         ("C5", S.replace(S.CONFIGS["C5"], hash_data=0), 1,
          S.replace(S.CONFIGS["C5"], hash_data=0, originals=2000), 1,
-         "C5's first 2000 originals (1 stream x 2000 x 64 KiB)"),
+         "C5's first 2000 originals (1 stream x 2000 x 64 KiB)", 8),
     ]
     out = {}
-    for name, cfg, runs, cpu_cfg, cpu_thr, sample in specs:
+    for name, cfg, runs, cpu_cfg, cpu_thr, sample, defer in specs:
         out[name] = run_leg(name, library, cfg, device, threads, runs,
-                            cpu_cfg if use_cpu else None, cpu_thr, sample)
+                            cpu_cfg if use_cpu else None, cpu_thr, sample, defer)
     out["dropin_C1"] = dropin_leg(library, use_cpu)
     return out
 

@@ -25,8 +25,9 @@ void be_h2d(void* dst, const void* src, size_t bytes);
 void be_d2h(void* dst, const void* src, size_t bytes);
 void be_memset(void* dst, int value, size_t bytes);
 
-/// One wave per descriptor (count descriptors), looping over its tiles.
-void be_launch_ingest(const IngestDesc* descs, uint32_t count);
+/// One wave per (descriptor, kIngestChunkBytes chunk): maxBytes is the
+/// largest hdrLen + bytes among the descriptors (sizes the grid).
+void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes);
 /// `stream`: the instruction words of every segment (see ExecItem).
 /// `acct`: device counter the executor adds the reference's source bytes of
 /// the terms it expands itself (sum updates, LDPC picks) to (ops.h).

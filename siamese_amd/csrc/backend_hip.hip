@@ -20,6 +20,7 @@
 #include "pool.h"
 #include "gf.h"
 
+#include <algorithm>
 #include <cctype>
 #include <chrono>
 #include <cstdlib>
@@ -132,8 +133,9 @@ __device__ __forceinline__ void st16(uint64_t addr, uint4 v)
 // ---------------------------------------------------------------------------
 // Ingest
 
-// One wave per symbol; lane L of each 1 KiB tile writes dst bytes
-// [16L, 16L+16).  The source is shifted by the 1-4 byte length prefix, so a
+// One wave per (symbol, 8 KiB chunk) -- blockIdx.y is the chunk, so a
+// 64 KiB symbol is copied by nine waves across the chip instead of one wave
+// looping over it; lane L of each 1 KiB tile writes dst bytes [16L, 16L+16).  The source is shifted by the 1-4 byte length prefix, so a
 // lane's 16 bytes straddle two aligned 16-byte source words: both are loaded
 // (coalesced) and recombined with v_alignbyte_b32.  The word offset and byte
 // shift are uniform per symbol, so the selection is a uniform branch, not a
@@ -165,8 +167,10 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
     const uint64_t srcEnd = d.src + d.bytes;
     const uint32_t h0 = d.hdr[0] | (d.hdr[1] << 8) | (d.hdr[2] << 16) | ((uint32_t)d.hdr[3] << 24);
     const uint32_t h1 = d.hdr[4] | (d.hdr[5] << 8) | (d.hdr[6] << 16) | ((uint32_t)d.hdr[7] << 24);
+    const uint32_t c0 = blockIdx.y * kIngestChunkBytes;
+    const uint32_t c1 = c0 + kIngestChunkBytes < total ? c0 + kIngestChunkBytes : total;
 
-    for (uint32_t t = 0; t < total; t += 2 * kTileBytes) {
+    for (uint32_t t = c0; t < c1; t += 2 * kTileBytes) {
         uint4 out[2];
 #pragma unroll
         for (unsigned u = 0; u < 2; ++u) {
@@ -2409,12 +2413,13 @@ void be_memset(void* dst, int value, size_t bytes)
     check(hipMemsetAsync(dst, value, bytes, g_stream), "memset");
 }
 
-void be_launch_ingest(const IngestDesc* descs, uint32_t count)
+void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes)
 {
     if (count == 0)
         return;
     Timed t(false);
-    hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves),
+    const uint32_t chunks = maxBytes ? (maxBytes + kIngestChunkBytes - 1) / kIngestChunkBytes : 1;
+    hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves, chunks),
                        dim3(64 * kIngestWaves), 0, g_stream, descs, count);
 }
 
@@ -2524,11 +2529,15 @@ bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, cons
         be_mark_release(l);
         return false;
     }
+    uint32_t maxBytes = 0;
+    for (uint32_t i = 0; i < count; ++i)
+        maxBytes = std::max(maxBytes, descsHost[i].bytes + descsHost[i].hdrLen);
+    const uint32_t gatherChunks = maxBytes ? (maxBytes + kIngestChunkBytes - 1) / kIngestChunkBytes : 1;
     if (hipMemcpyAsync(descsDev, descsHost, (size_t)count * sizeof(IngestDesc), hipMemcpyHostToDevice,
                        g_gatherStream) != hipSuccess)
         return false;
-    hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves), dim3(64 * kIngestWaves),
-                       0, g_gatherStream, static_cast<const IngestDesc*>(descsDev), count);
+    hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves, gatherChunks),
+                       dim3(64 * kIngestWaves), 0, g_gatherStream, static_cast<const IngestDesc*>(descsDev), count);
     if (hipEventRecord(p, g_gatherStream) != hipSuccess)
         return false;
     *packed = p;

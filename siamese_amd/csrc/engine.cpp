@@ -689,6 +689,7 @@ void Shard::Queues::clear()
     ingest.clear();
     hostStage.clear();
     downloads.clear();
+    maxIngest = 0;
     for (auto& r : released)
         r.clear();
 }
@@ -942,11 +943,14 @@ void Engine::stage_host_ingest(const DevBuf& dst, const void* data, uint32_t byt
     d.bytes = hdrLen + bytes;
     d.hdrLen = 0;
     s.q.ingest.push_back(Shard::IngestRec{d, (int64_t)off});
+    s.q.maxIngest = std::max(s.q.maxIngest, d.bytes);
 }
 
 void Engine::add_ingest(const IngestDesc& d, int64_t hostStageOffset)
 {
-    shard().q.ingest.push_back(Shard::IngestRec{d, hostStageOffset});
+    Shard::Queues& q = shard().q;
+    q.ingest.push_back(Shard::IngestRec{d, hostStageOffset});
+    q.maxIngest = std::max(q.maxIngest, d.bytes + d.hdrLen);
 }
 
 bool Engine::pending() const
@@ -1049,6 +1053,7 @@ struct Batch
     // layout (enqueue -> launcher)
     std::vector<Phase> phases;
     size_t upBytes = 0, nIngest = 0;
+    uint32_t maxIngest = 0;
     size_t oIngD = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
     uint64_t wideBase = 0;                 // this submission's k_ldpc scratch: bytes into the ring
     bool wideZero = false;                 // the ring wrapped: zero it before the first exec launch
@@ -1449,6 +1454,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         descBase.push_back(nIngest);
         stageBase.push_back(stageBytes);
         nIngest += q.ingest.size();
+        bt.maxIngest = std::max(bt.maxIngest, q.maxIngest);
         stageBytes = align16(stageBytes + q.hostStage.size());
     }
     bt.nIngest = nIngest;
@@ -1656,7 +1662,7 @@ void Engine::launch_batch(Batch& bt)
     if (bt.upBytes)
         be_h2d(xs.upDev, xs.upHost, bt.upBytes);
     if (bt.nIngest)
-        be_launch_ingest((const IngestDesc*)(xs.upDev + bt.oIngD), (uint32_t)bt.nIngest);
+        be_launch_ingest((const IngestDesc*)(xs.upDev + bt.oIngD), (uint32_t)bt.nIngest, bt.maxIngest);
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
     if (xs.acctZero) {
@@ -1970,7 +1976,10 @@ bool Engine::gather(unsigned count, const void* const* srcs, const unsigned* byt
         d.dst += (uint64_t)(uintptr_t)gDev_;
     std::memcpy(gUpHost_, descs.data(), upBytes);
     be_h2d(gUpDev_, gUpHost_, upBytes);
-    be_launch_ingest((const IngestDesc*)gUpDev_, count);
+    uint32_t maxBytes = 0;
+    for (unsigned i = 0; i < count; ++i)
+        maxBytes = std::max(maxBytes, bytes[i]);
+    be_launch_ingest((const IngestDesc*)gUpDev_, count, maxBytes);
     be_d2h(gHost_, gDev_, total);
     const bool ok = be_sync();
     if (!ok) {

@@ -513,6 +513,7 @@ struct Shard
         std::vector<uint8_t> hostStage;
         std::vector<Download> downloads;
         std::vector<std::vector<uint8_t*>> released;   // by capacity class
+        uint32_t maxIngest = 0;                         // largest hdrLen + bytes among `ingest`
         bool empty() const;
         void clear();
     };

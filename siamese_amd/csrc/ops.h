@@ -290,6 +290,7 @@ struct IngestDesc
 };
 
 constexpr unsigned kTileBytes = 1024;       // solve tiles: 64 lanes x 16 bytes
+constexpr unsigned kIngestChunkBytes = 8192;   // k_ingest: bytes per wave (8 x 1 KiB tiles)
 /// Solves with more rows than this stage 256-byte tiles (16 lanes x 16 bytes
 /// per row, four rows per wave) so all m <= 255 rows and the m x m
 /// coefficients still fit one workgroup's LDS.

@@ -344,7 +344,7 @@ void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, byt
 
 static bool noexec();
 
-void be_launch_ingest(const IngestDesc* descs, uint32_t count)
+void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t)
 {
     if (noexec())
         return;
@@ -530,7 +530,7 @@ bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, cons
 {
     *packed = *landed = reinterpret_cast<void*>(1);
     std::memcpy(descsDev, descsHost, (size_t)count * sizeof(IngestDesc));
-    be_launch_ingest(static_cast<const IngestDesc*>(descsDev), count);
+    be_launch_ingest(static_cast<const IngestDesc*>(descsDev), count, 0);
     std::memcpy(hostOut, devStage, bytes);
     return true;
 }

@@ -69,7 +69,7 @@ void be_h2d(void* dst, const void* src, size_t bytes)
 void be_d2h(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
-void be_launch_ingest(const IngestDesc*, uint32_t) {}
+void be_launch_ingest(const IngestDesc*, uint32_t, uint32_t) {}
 void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*, uint32_t) {}
 void be_launch_ldpc(const LdpcItem*, uint32_t, uint64_t*) {}
 
