@@ -329,14 +329,15 @@ def run_rank(rank, world, local, args, library, use_cuda):
         # (pipelined warm-up over both alternating device copies, every
         # recovered byte checked against the payloads)
         res_e, rep_e = sess.run(steps=max(2, args.warmup), warmup=0, verify=args.verify,
-                                threads=args.threads, groups=args.groups, e2e=True, digest=False)
+                                threads=args.threads, groups=args.groups, e2e=True, digest=False,
+                                frames=args.frames)
         if args.verify and (rep_e.mismatches or any(r.status for r in res_e)):
             raise RuntimeError("bench: end-to-end verification failed: %d byte mismatches"
                                % rep_e.mismatches)
         coll.barrier()
         t1 = time.perf_counter()
         sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
-                 groups=args.groups, e2e=True, digest=False)
+                 groups=args.groups, e2e=True, digest=False, frames=args.frames)
         coll.barrier()
         e2e_elapsed = time.perf_counter() - t1
     sess.close()
@@ -443,9 +444,13 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "unit": "GB/s",
             "payload_GBps": round(payload_total / e2e_max / 1e9, 3),
             "ms_per_step": round(e2e_max / steps * 1e3, 3),
-            "note": "originals H2D from pinned host memory each step; every recovery packet "
-                    "and recovered original D2H, originals delivered intact stay on the host "
-                    "(PCIe-inclusive; not `value`)",
+            "framed": bool(args.frames),
+            "note": "originals H2D from pinned host memory each step%s; every recovery packet "
+                    "%sand recovered original D2H, originals delivered intact stay on the host "
+                    "(PCIe-inclusive; not `value`)" % (
+                        " as framed datagrams handed to the decoders by sgpu_frames_recv"
+                        if args.frames else "",
+                        "(framed by sgpu_frames_send) " if args.frames else ""),
         }
     if not args.no_cpu and world == 1:
         # the reference on the host cores, rank 0 at N=1 only, on a bounded
@@ -507,6 +512,8 @@ def main(argv=None):
                     help="stream groups alternating host and device work (1 = no overlap)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip the PCIe-inclusive end-to-end leg")
+    ap.add_argument("--no-frames", dest="frames", action="store_false",
+                    help="end-to-end leg with raw payloads instead of framed datagrams")
     ap.add_argument("--no-legs", dest="legs", action="store_false",
                     help="skip the C2/C3/C5 legs (N=1)")
     ap.add_argument("--library", default=S.AMD_LIB, help=argparse.SUPPRESS)

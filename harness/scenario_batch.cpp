@@ -47,6 +47,10 @@ struct BatchOptions
                        ///< sgpu_decoder_get_deferred), a stream yields after
                        ///< every k-th decode and a job is driven on with up to
                        ///< two of its submissions in flight
+    uint32_t frames;   ///< with e2e: packets travel as framed datagrams (siamese_gpu.h):
+                       ///< originals staged as frames and handed to the decoders by
+                       ///< sgpu_frames_recv, recovery packets copied back framed by
+                       ///< sgpu_frames_send and parsed on landing
 };
 
 struct BatchReport
@@ -106,6 +110,12 @@ struct Api
     int (*h2d_async)(void*, const void*, size_t);
     int (*gather_completed)(unsigned, const void* const*, const unsigned*, void*);
     long long (*gather_async)(unsigned, const void* const*, const unsigned*, void*);
+    unsigned (*frame_header_bytes)(unsigned, unsigned);
+    unsigned (*frame_write_header)(unsigned, unsigned, unsigned, unsigned, void*);
+    SiameseResult (*frames_parse)(const void*, size_t, SgpuFrame*, unsigned, unsigned*);
+    SiameseResult (*frames_recv)(const SgpuDecoder*, unsigned, const void*, const void*, size_t, SiameseResult*,
+                                 unsigned, unsigned*);
+    long long (*frames_send)(unsigned, const SgpuRecoveryPacket*, const unsigned*, void*, size_t, size_t*);
     int (*gather_wait)(long long);
     void (*timing)(int, int, double*, double*);
     void (*engine_stats)(uint64_t*);
@@ -148,6 +158,9 @@ bool load_api(const char* path, Api& a)
            bind(h, a.h2d, "sgpu_h2d") && bind(h, a.gather, "sgpu_gather") &&
            bind(h, a.h2d_async, "sgpu_h2d_async") && bind(h, a.gather_completed, "sgpu_gather_completed") &&
            bind(h, a.gather_async, "sgpu_gather_async") && bind(h, a.gather_wait, "sgpu_gather_wait") &&
+           bind(h, a.frame_header_bytes, "sgpu_frame_header_bytes") &&
+           bind(h, a.frame_write_header, "sgpu_frame_write_header") && bind(h, a.frames_parse, "sgpu_frames_parse") &&
+           bind(h, a.frames_recv, "sgpu_frames_recv") && bind(h, a.frames_send, "sgpu_frames_send") &&
            bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats") &&
            bind(h, a.arena_bytes, "sgpu_arena_bytes") && bind(h, a.arena_reserve, "sgpu_arena_reserve");
 }
@@ -194,6 +207,14 @@ struct Shared
     uint8_t* devBase = nullptr;       // its device-resident counterparts
     uint8_t* devBase2 = nullptr;
     size_t payloadBytes = 0;
+    // framed datagrams (BatchOptions::frames, with e2e): every original as a
+    // frame in a pinned ring at a fixed stride, and its two device copies
+    bool frames = false;
+    uint8_t* frameHost = nullptr;
+    uint8_t* frameDev = nullptr;
+    uint8_t* frameDev2 = nullptr;
+    size_t fstride = 0, frameBytes = 0;
+    uint64_t idBase = 0;       // global payload id of the session's first original
     // gathers in flight (oldest first) and their pinned landing buffers
     struct Landing
     {
@@ -205,6 +226,8 @@ struct Shared
         long long ticket;
         Landing land;
         std::vector<Request> reqs;   // kept only when the bytes are checked or hashed
+        bool framed = false;         // landed as frames (sgpu_frames_send)
+        size_t bytes = 0;            // framed: the frame stream's length
     };
     std::deque<Gather> gathers;
     std::vector<Landing> landings;    // free ones
@@ -219,6 +242,8 @@ struct BatchCodec
 {
     Shared* sh;
     const uint8_t* payload = nullptr;   // the step's device copy of the originals
+    const SgpuDecoder* decTable = nullptr;   // frames: the job's decoders by flow (stream index)
+    unsigned flow = 0;                       // frames: this stream's flow id
     SgpuEncoder enc = nullptr;
     SgpuDecoder dec = nullptr;
     std::vector<uint64_t>* log = nullptr;
@@ -241,7 +266,17 @@ struct BatchCodec
         return e;
     }
 
-    const void* dev_payload(unsigned id) const { return payload + (size_t)id * sh->stride; }
+    unsigned payload_bytes(unsigned id) const
+    {
+        return sh->cfg->payload_bytes ? sh->cfg->payload_bytes : scen::variable_bytes(id);
+    }
+    const void* dev_payload(unsigned id) const
+    {
+        if (sh->frames)   // (the payload after the frame's header)
+            return payload + (id - sh->idBase) * sh->fstride +
+                   sh->api->frame_header_bytes(SGPU_FRAME_ORIGINAL, payload_bytes(id));
+        return payload + (size_t)id * sh->stride;
+    }
 
     bool needs_host_payload() const { return false; }
     int enc_add(unsigned id, const uint8_t*, unsigned bytes, unsigned* num)
@@ -256,6 +291,21 @@ struct BatchCodec
     }
     int dec_add_original(unsigned id, unsigned num, const uint8_t*, unsigned bytes)
     {
+        if (sh->frames) {
+            // the datagram as it arrives: its frame in the pinned ring (the
+            // header rewritten with the packet number the encoder gave it),
+            // whose device copy the job staged; parsed and routed by the library
+            const size_t slot = (id - sh->idBase) * sh->fstride;
+            uint8_t* f = sh->frameHost + slot;
+            const unsigned h = sh->api->frame_write_header(SGPU_FRAME_ORIGINAL, flow, num, bytes, f);
+            SiameseResult r = Siamese_InvalidInput;
+            unsigned n = 0;
+            if (h == 0)
+                return Siamese_InvalidInput;
+            // (the call's status is the frame's result; n says whether it was taken)
+            (void)sh->api->frames_recv(decTable, sh->cfg->streams, f, payload + slot, h + bytes, &r, 1, &n);
+            return n == 1 ? r : Siamese_InvalidInput;
+        }
         return sh->api->decoder_add_original(dec, num, dev_payload(id), bytes);
     }
     int dec_add_recovery(const Rec& r) { return sh->api->decoder_add_recovery(dec, &r.pkt); }
@@ -314,7 +364,7 @@ struct BatchCodec
     {
         // end-to-end mode: every recovery packet goes back to host memory
         if (sh->hashData || sh->e2e)
-            push(Request{log, log->size(), r.pkt.DeviceData, r.bytes, 0, false, nullptr});
+            push(Request{log, log->size(), r.pkt.DeviceData, r.bytes, flow, false, nullptr});
         return r.bytes;
     }
     uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok)
@@ -374,9 +424,31 @@ void land_gather(Shared& sh)
     } else {
         std::vector<uint8_t> expect;
         size_t off = 0;
-        for (const Request& r : g.reqs) {
+        std::vector<SgpuFrame> frames;
+        if (g.framed) {
+            // the landed frame stream: one recovery frame per request, in order
+            frames.resize(g.reqs.size());
+            unsigned n = 0;
+            if (sh.api->frames_parse(g.land.buf, g.bytes, frames.data(), (unsigned)frames.size(), &n) !=
+                    Siamese_Success || n != g.reqs.size()) {
+                for (const Request& r : g.reqs)
+                    if (r.ok)
+                        *r.ok = false;
+                ++sh.mismatches;
+                sh.landings.push_back(g.land);
+                return;
+            }
+        }
+        for (size_t i = 0; i < g.reqs.size(); ++i) {
+            const Request& r = g.reqs[i];
             const uint8_t* d = g.land.buf + off;
             off += (r.bytes + 15) & ~(size_t)15;
+            if (g.framed) {
+                const SgpuFrame& f = frames[i];
+                d = g.land.buf + f.Offset;
+                if (f.Type != SGPU_FRAME_RECOVERY || f.Flow != r.id || f.Bytes != r.bytes)
+                    ++sh.mismatches;
+            }
             if (r.isPacket && (sh.verify || sh.hashData)) {
                 expect.resize(r.bytes + 8);
                 scen::fill_payload(r.id, expect.data(), r.bytes);
@@ -413,6 +485,8 @@ void land_gathers(Shared& sh)
 // codecs owning the ranges may be driven on at once (later device work waits
 // for the gather's reads).  Bytes that are checked or hashed are examined
 // when the gather lands (land_gather).
+void gather_requests(Shared& sh, std::vector<Request>& reqs, bool framed);
+
 void resolve_requests(Shared& sh, std::vector<Request>& reqs)
 {
     if (reqs.empty())
@@ -446,6 +520,24 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
     reqs.resize(keep);
     if (reqs.empty())
         return;
+    if (sh.frames) {
+        // recovery packets leave as framed datagrams (sgpu_frames_send); the
+        // recovered originals' bytes by a plain gather
+        std::vector<Request> rec, pkt;
+        for (const Request& r : reqs)
+            (r.isPacket ? pkt : rec).push_back(r);
+        reqs.clear();
+        if (!rec.empty())
+            gather_requests(sh, rec, true);
+        if (!pkt.empty())
+            gather_requests(sh, pkt, false);
+        return;
+    }
+    gather_requests(sh, reqs, false);
+}
+
+void gather_requests(Shared& sh, std::vector<Request>& reqs, bool framed)
+{
     std::vector<const void*> srcs;
     std::vector<unsigned> lens;
     size_t total = 0;
@@ -453,6 +545,8 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
         srcs.push_back(r.dev);
         lens.push_back(r.bytes);
         total += (r.bytes + 15) & ~(size_t)15;
+        if (framed)
+            total += 16;   // (a frame header, at most 8 bytes, can add one lane)
     }
     constexpr size_t kInFlight = 4;
     if (sh.gathers.size() >= kInFlight)
@@ -474,7 +568,21 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
         land.cap = ((total + 16) + (8u << 20) - 1) & ~(size_t)((8u << 20) - 1);
         land.buf = (uint8_t*)sh.api->host_alloc(land.cap);
     }
-    const long long t = land.buf ? sh.api->gather_async((unsigned)reqs.size(), srcs.data(), lens.data(), land.buf) : -1;
+    long long t = -1;
+    size_t frameBytes = 0;
+    if (land.buf && framed) {
+        std::vector<SgpuRecoveryPacket> pk(reqs.size());
+        std::vector<unsigned> flows(reqs.size());
+        for (size_t i = 0; i < reqs.size(); ++i) {
+            std::memset(&pk[i], 0, sizeof(pk[i]));
+            pk[i].DeviceData = static_cast<const unsigned char*>(reqs[i].dev);
+            pk[i].DataBytes = reqs[i].bytes;
+            flows[i] = reqs[i].id;
+        }
+        t = sh.api->frames_send((unsigned)reqs.size(), pk.data(), flows.data(), land.buf, land.cap, &frameBytes);
+    } else if (land.buf) {
+        t = sh.api->gather_async((unsigned)reqs.size(), srcs.data(), lens.data(), land.buf);
+    }
     if (t <= 0) {
         if (land.buf)
             sh.landings.push_back(land);
@@ -488,7 +596,9 @@ void resolve_requests(Shared& sh, std::vector<Request>& reqs)
     Shared::Gather g;
     g.ticket = t;
     g.land = land;
-    if (sh.verify || sh.hashData)
+    g.framed = framed;
+    g.bytes = frameBytes;
+    if (sh.verify || sh.hashData || framed)
         g.reqs.swap(reqs);
     sh.gathers.push_back(std::move(g));
     reqs.clear();
@@ -556,6 +666,7 @@ struct Job
     std::vector<StreamResult> res;
     std::vector<unsigned> live;     // indices into codecs/streams
     std::deque<Round> rounds;       // submitted, tokens not yet resolved (oldest first)
+    std::vector<SgpuDecoder> decTable;   // frames: decoders by flow (the session's stream index)
 };
 
 int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* rounds,
@@ -764,9 +875,13 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             // work in flight; the submissions after it wait for it.
             const bool second = sh.e2e && (J.step & 1u);
             if (sh.e2e) {
-                const size_t per = (size_t)cfg->originals * sh.stride;
+                // (frames: the job's slice of the framed ring instead)
+                const size_t stride = sh.frames ? sh.fstride : sh.stride;
+                uint8_t* dev = sh.frames ? (second ? sh.frameDev2 : sh.frameDev) : (second ? sh.devBase2 : sh.devBase);
+                const uint8_t* host = sh.frames ? sh.frameHost : sh.hostPayload;
+                const size_t per = (size_t)cfg->originals * stride;
                 const size_t off = (size_t)J.begin * per, len = (size_t)(J.end - J.begin) * per;
-                if (api.h2d_async((second ? sh.devBase2 : sh.devBase) + off, sh.hostPayload + off, len) != 0) {
+                if (api.h2d_async(dev + off, host + off, len) != 0) {
                     rc = -3;
                     break;
                 }
@@ -775,12 +890,19 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             J.codecs.resize(cnt);
             J.streams.reset(new BatchStream[cnt]);
             J.res.resize(cnt);
+            if (sh.frames)
+                J.decTable.assign(n, nullptr);
             for_streams(sh, cnt, [&](size_t i) {
                 BatchCodec& c = J.codecs[i];
                 c.sh = &sh;
-                c.payload = second ? sh.payload2 : sh.payload;
+                c.payload = sh.frames ? (second ? sh.frameDev2 : sh.frameDev) : (second ? sh.payload2 : sh.payload);
                 c.enc = api.encoder_create();
                 c.dec = api.decoder_create();
+                c.flow = J.begin + (unsigned)i;
+                if (sh.frames) {
+                    J.decTable[c.flow] = c.dec;
+                    c.decTable = J.decTable.data();
+                }
                 c.log = &J.streams[i].log;
                 // the event log only feeds digests: timed bench steps run without it
                 J.streams[i].logOn = sh.verify || sh.hashData || sh.digest;
@@ -917,6 +1039,32 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
             scen::fill_payload(id, sh.hostPayload + k * sh.stride, b);
         }
     }
+    sh.frames = sh.e2e && opt->frames != 0;
+    if (sh.frames && !sh.frameHost) {
+        // every original of the session as a framed datagram (siamese_gpu.h)
+        // at a fixed stride in a pinned ring, and two device copies (untimed)
+        const ScenarioConfig* c = &ss->cfg;
+        const unsigned maxBytes = c->payload_bytes ? c->payload_bytes : 1200;
+        sh.fstride = (api.frame_header_bytes(SGPU_FRAME_ORIGINAL, maxBytes) + maxBytes + 15) & ~(size_t)15;
+        const size_t total = (size_t)c->streams * c->originals;
+        sh.frameBytes = total * sh.fstride;
+        sh.idBase = (uint64_t)c->first_stream * c->originals;
+        sh.frameHost = (uint8_t*)api.host_alloc(sh.frameBytes);
+        sh.frameDev = (uint8_t*)api.device_alloc(sh.frameBytes);
+        sh.frameDev2 = (uint8_t*)api.device_alloc(sh.frameBytes);
+        if (!sh.frameHost || !sh.frameDev || !sh.frameDev2)
+            return -2;
+        std::memset(sh.frameHost, 0, sh.frameBytes);
+        for (size_t k = 0; k < total; ++k) {
+            const unsigned id = (unsigned)(sh.idBase + k);
+            const unsigned b = c->payload_bytes ? c->payload_bytes : scen::variable_bytes(id);
+            uint8_t* f = sh.frameHost + k * sh.fstride;
+            // (PacketNum: the stream's k-th original; rewritten when it is sent)
+            const unsigned h = api.frame_write_header(SGPU_FRAME_ORIGINAL, (unsigned)(k / c->originals),
+                                                      (unsigned)(k % c->originals), b, f);
+            scen::fill_payload(id, f + h, b);
+        }
+    }
     int rc = 0;
     // warm-up runs one at a time (the first may verify every byte); then all
     // timed steps as one pipeline, so one step's device tail overlaps the
@@ -979,6 +1127,12 @@ void scenario_batch_close(void* session)
         ss->api->device_free(ss->sh.devBase2);
     if (ss->sh.hostPayload)
         ss->api->host_free(ss->sh.hostPayload);
+    if (ss->sh.frameHost)
+        ss->api->host_free(ss->sh.frameHost);
+    if (ss->sh.frameDev)
+        ss->api->device_free(ss->sh.frameDev);
+    if (ss->sh.frameDev2)
+        ss->api->device_free(ss->sh.frameDev2);
     land_gathers(ss->sh);
     for (const Shared::Landing& l : ss->sh.landings)
         ss->api->host_free(l.buf);

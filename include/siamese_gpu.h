@@ -171,6 +171,64 @@ SIAMESE_EXPORT long long sgpu_gather_async(unsigned count, const void* const* de
 /// memory.  0 on success, -1 after a device fault.
 SIAMESE_EXPORT int sgpu_gather_wait(long long ticket);
 
+/*
+    Framed datagrams: packet ingest and egress in bulk (the UDP side of an
+    application; replaces nothing in siamese.h).  A frame carries one
+    datagram:
+      [L: byte length of the rest, in the symbol length-prefix format of
+          the reference (SiameseSerializers.h:566-593), 1-4 bytes]
+      [type: 1 byte, SGPU_FRAME_ORIGINAL or SGPU_FRAME_RECOVERY]
+      [flow: 3 bytes little-endian, the application's stream id]
+      original:  [PacketNum: 3 bytes LE] [payload]
+      recovery:  [the recovery packet, its metadata footer included
+                  (SiameseSerializers.h:736-800)]
+    Frames follow each other directly; a zero byte where a frame would start
+    is an empty frame and is skipped (senders pad frames with zeros).
+*/
+#define SGPU_FRAME_ORIGINAL 0
+#define SGPU_FRAME_RECOVERY 1
+
+typedef struct SgpuFrame
+{
+    unsigned Type;        ///< SGPU_FRAME_ORIGINAL / SGPU_FRAME_RECOVERY
+    unsigned Flow;
+    unsigned PacketNum;   ///< originals
+    unsigned Offset;      ///< byte offset of the data (payload / recovery packet) in the buffer
+    unsigned Bytes;       ///< data bytes
+} SgpuFrame;
+
+/// Header bytes a frame of `type` carrying `dataBytes` puts before its data.
+SIAMESE_EXPORT unsigned sgpu_frame_header_bytes(unsigned type, unsigned dataBytes);
+/// Write a frame header to `out` (sgpu_frame_header_bytes bytes); the data
+/// follows it.  Returns the header size, 0 on invalid input.
+SIAMESE_EXPORT unsigned sgpu_frame_write_header(unsigned type, unsigned flow, unsigned packetNum,
+                                                unsigned dataBytes, void* out);
+/// Parse up to maxFrames frames of frames[0, bytes) (host memory).
+/// InvalidInput on a malformed frame or when more frames remain.
+SIAMESE_EXPORT SiameseResult sgpu_frames_parse(const void* frames, size_t bytes, SgpuFrame* out,
+                                               unsigned maxFrames, unsigned* countOut);
+/// Packet ingest: the frames in hostFrames[0, bytes) (pinned host memory)
+/// whose identical copy the caller staged at deviceFrames with
+/// sgpu_h2d_async.  Parses them in bulk and hands each datagram to
+/// decoders[flow]: originals to sgpu_decoder_add_original, recovery packets
+/// to sgpu_decoder_add_recovery (footer and head read from the host copy,
+/// the bytes copied from the device copy by the next submission, which
+/// waits for the staging copy on the device).  results[i] (optional) is the
+/// call's result for frame i (InvalidInput for a flow without a decoder).
+/// The decoders must not be driven concurrently with this call; deviceFrames
+/// stays untouched until the next submission has completed.
+SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsigned decoderCount,
+                                              const void* hostFrames, const void* deviceFrames, size_t bytes,
+                                              SiameseResult* results, unsigned maxFrames, unsigned* countOut);
+/// Packet egress: frame `count` recovery packets (flows[i] their stream ids)
+/// into pinned host memory without waiting (a gather, as
+/// sgpu_gather_async: same lifetime rule for the packets).  Frame i starts
+/// at a 16-byte boundary, zero padding between frames.  *bytesOut = the
+/// frame stream's length (<= capacity).  Returns a gather ticket for
+/// sgpu_gather_wait, -1 on failure (capacity too small, device fault).
+SIAMESE_EXPORT long long sgpu_frames_send(unsigned count, const SgpuRecoveryPacket* packets, const unsigned* flows,
+                                          void* pinnedOut, size_t capacity, size_t* bytesOut);
+
 /// Device timing of flushed work since the last reset (milliseconds).
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs);
 /// Engine counters (15 values): flushes, launches, ops, terms, solves,

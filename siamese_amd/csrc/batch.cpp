@@ -6,14 +6,17 @@
 
 #include "backend.h"
 #include "decoder.h"
+#include "frames.h"
 #include "encoder.h"
 #include "engine.h"
 #include "pool.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <vector>
 
 using namespace sgpu;
 
@@ -316,6 +319,126 @@ SIAMESE_EXPORT int sgpu_gather_wait(long long ticket)
     if (!g_batchReady)
         return -1;
     return Engine::global()->gather_wait((int64_t)ticket) ? 0 : -1;
+}
+
+SIAMESE_EXPORT unsigned sgpu_frame_header_bytes(unsigned type, unsigned dataBytes)
+{
+    if (type > SGPU_FRAME_RECOVERY)
+        return 0;
+    return frame_header_bytes(type, dataBytes);
+}
+
+SIAMESE_EXPORT unsigned sgpu_frame_write_header(unsigned type, unsigned flow, unsigned packetNum,
+                                                unsigned dataBytes, void* out)
+{
+    if (!out || type > SGPU_FRAME_RECOVERY || flow > kFrameMaxFlow || packetNum > SIAMESE_PACKET_NUM_MAX ||
+        dataBytes == 0 || dataBytes > SIAMESE_MAX_PACKET_BYTES)
+        return 0;
+    return frame_write_header(type, flow, packetNum, dataBytes, static_cast<uint8_t*>(out));
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_frames_parse(const void* frames, size_t bytes, SgpuFrame* out,
+                                               unsigned maxFrames, unsigned* countOut)
+{
+    if (!frames || !out || !countOut)
+        return Siamese_InvalidInput;
+    static_assert(sizeof(SgpuFrame) == sizeof(FrameInfo), "SgpuFrame layout");
+    size_t consumed = 0, bad = 0;
+    const long n = frames_parse(static_cast<const uint8_t*>(frames), bytes, reinterpret_cast<FrameInfo*>(out),
+                                maxFrames, &consumed, &bad);
+    if (n < 0) {
+        *countOut = 0;
+        return Siamese_InvalidInput;
+    }
+    *countOut = (unsigned)n;
+    return consumed == bytes ? Siamese_Success : Siamese_InvalidInput;
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsigned decoderCount,
+                                              const void* hostFrames, const void* deviceFrames, size_t bytes,
+                                              SiameseResult* results, unsigned maxFrames, unsigned* countOut)
+{
+    if (!decoders || !hostFrames || !deviceFrames || !countOut)
+        return Siamese_InvalidInput;
+    *countOut = 0;
+    const uint8_t* host = static_cast<const uint8_t*>(hostFrames);
+    const uint64_t dev = (uint64_t)(uintptr_t)deviceFrames;
+    // parse in blocks: the headers of a whole ring in one pass, then the calls
+    FrameInfo fi[256];
+    size_t at = 0;
+    unsigned done = 0;
+    SiameseResult status = Siamese_Success;
+    while (at < bytes && done < maxFrames) {
+        size_t consumed = 0, bad = 0;
+        const size_t want = std::min<size_t>(256, maxFrames - done);
+        const long n = frames_parse(host + at, bytes - at, fi, want, &consumed, &bad);
+        if (n < 0)
+            return Siamese_InvalidInput;
+        for (long k = 0; k < n; ++k) {
+            const FrameInfo& f = fi[k];
+            const size_t off = at + f.offset;
+            SiameseResult r = Siamese_InvalidInput;
+            SgpuDecoder d = f.flow < decoderCount ? decoders[f.flow] : nullptr;
+            if (d && f.type == kFrameOriginal) {
+                if (f.bytes <= SIAMESE_MAX_PACKET_BYTES && f.packetNum <= SIAMESE_PACKET_NUM_MAX) {
+                    SiameseOriginalPacket p;
+                    p.PacketNum = f.packetNum;
+                    p.Data = reinterpret_cast<const unsigned char*>((uintptr_t)(dev + off));
+                    p.DataBytes = f.bytes;
+                    r = BD(d)->core.add_original(p, dev + off);
+                }
+            } else if (d && f.type == kFrameRecovery) {
+                RowMeta m;
+                const int footer = read_footer(host + off, f.bytes, &m);
+                if (footer > 0 && (unsigned)footer < f.bytes) {
+                    DeviceRecovery rec;
+                    rec.data = dev + off;
+                    rec.bytes = f.bytes;
+                    rec.footer = host + off + f.bytes - footer;
+                    rec.footerBytes = (unsigned)footer;
+                    rec.head = host + off;
+                    rec.producer = nullptr;   // staged: ingested from the device copy
+                    r = BD(d)->core.add_recovery_device(rec);
+                }
+            }
+            if (results)
+                results[done] = r;
+            if (r != Siamese_Success && status == Siamese_Success)
+                status = r;
+            ++done;
+        }
+        at += consumed;
+        if (n == 0)
+            break;
+    }
+    *countOut = done;
+    return at >= bytes ? status : Siamese_InvalidInput;
+}
+
+SIAMESE_EXPORT long long sgpu_frames_send(unsigned count, const SgpuRecoveryPacket* packets, const unsigned* flows,
+                                          void* pinnedOut, size_t capacity, size_t* bytesOut)
+{
+    if (!g_batchReady || !packets || !flows || !pinnedOut || !bytesOut)
+        return -1;
+    std::vector<const void*> srcs(count);
+    std::vector<unsigned> lens(count), hlen(count);
+    std::vector<uint8_t> hdr((size_t)count * 8);
+    size_t total = 0;
+    for (unsigned i = 0; i < count; ++i) {
+        if (!packets[i].DeviceData || flows[i] > kFrameMaxFlow)
+            return -1;
+        srcs[i] = packets[i].DeviceData;
+        lens[i] = packets[i].DataBytes;
+        hlen[i] = frame_write_header(kFrameRecovery, flows[i], 0, lens[i], hdr.data() + 8 * (size_t)i);
+        if (hlen[i] > 8)
+            return -1;
+        total = (total + hlen[i] + lens[i] + 15) & ~(size_t)15;
+    }
+    *bytesOut = total;
+    if (total > capacity)
+        return -1;
+    return (long long)Engine::global()->gather_async_framed(count, srcs.data(), lens.data(), hdr.data(), hlen.data(),
+                                                            pinnedOut);
 }
 
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs)

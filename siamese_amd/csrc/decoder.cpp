@@ -769,6 +769,10 @@ SiameseResult DecoderCore::add_recovery_common(const RowMeta& m, int footer, uns
     static const uint8_t none[1] = {0};
     if (hostData)
         prog_.ingest_host(r->buf, hostData, payload, none, 0);
+    else if (!producer)
+        // staged from host memory (framed datagrams, sgpu_frames_recv): in
+        // place before the submission starts, at any byte alignment
+        prog_.ingest_device(r->buf, devData, payload, none, 0);
     else {
         // A device-resident packet may have been encoded in this very flush:
         // copy it with an op of this (group-1) program, which runs after
@@ -811,9 +815,8 @@ bool DecoderCore::add_single(const RowMeta& m, const uint8_t* headBytes, unsigne
         return false;
     if (hostData)
         prog_.ingest_host(s.buf, (const uint8_t*)hostData + headerBytes, length, hdr, h);
-    else if ((unsigned)headerBytes == h) {
+    else if ((unsigned)headerBytes == h && producer) {
         // Same byte alignment: a copy op of this program (see add_recovery_common)
-        (void)producer;
         prog_.copy(s.buf.addr(), devData, h + length);
     } else
         prog_.ingest_device(s.buf, devData + headerBytes, length, hdr, h);

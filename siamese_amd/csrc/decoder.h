@@ -84,7 +84,9 @@ struct DeviceRecovery
     const uint8_t* footer = nullptr;  // host copy of the footer bytes
     unsigned footerBytes = 0;
     const uint8_t* head = nullptr;    // host copy of the first bytes (single rows)
-    Program* producer = nullptr;      // program that must perform the copy
+    Program* producer = nullptr;      // program that must perform the copy; null:
+                                      // a staged packet (a host -> device copy the
+                                      // submission waits for, any alignment)
 };
 
 class DecoderCore

@@ -1869,6 +1869,12 @@ bool Engine::gather_land(GatherSlot& g)
 int64_t Engine::gather_async(unsigned count, const void* const* srcs, const unsigned* bytes,
                              void* pinnedOut)
 {
+    return gather_async_framed(count, srcs, bytes, nullptr, nullptr, pinnedOut);
+}
+
+int64_t Engine::gather_async_framed(unsigned count, const void* const* srcs, const unsigned* bytes,
+                                    const uint8_t* hdrs, const unsigned* hdrLens, void* pinnedOut)
+{
     if (failed())
         return -1;
     std::lock_guard<std::mutex> lk(gatherMu_);
@@ -1881,7 +1887,7 @@ int64_t Engine::gather_async(unsigned count, const void* const* srcs, const unsi
     const size_t upBytes = count * sizeof(IngestDesc);
     size_t total = 0;
     for (unsigned i = 0; i < count; ++i)
-        total = align16(total + bytes[i]);
+        total = align16(total + bytes[i] + (hdrLens ? hdrLens[i] : 0));
     auto grow = [](uint8_t*& h, uint8_t*& d, size_t& cap, size_t need, bool host) {
         if (need <= cap)
             return;
@@ -1908,7 +1914,11 @@ int64_t Engine::gather_async(unsigned count, const void* const* srcs, const unsi
         descs[i].src = (uint64_t)(uintptr_t)srcs[i];
         descs[i].bytes = bytes[i];
         descs[i].dst = (uint64_t)(uintptr_t)g.stage + off;
-        off = align16(off + bytes[i]);
+        if (hdrLens) {
+            descs[i].hdrLen = hdrLens[i] < 8 ? hdrLens[i] : 8;
+            std::memcpy(descs[i].hdr, hdrs + 8 * (size_t)i, descs[i].hdrLen);
+        }
+        off = align16(off + bytes[i] + descs[i].hdrLen);
     }
     void* packed = nullptr;
     if (!be_gather(descs, g.upDev, count, g.stage, pinnedOut, total, &packed, &g.landed)) {

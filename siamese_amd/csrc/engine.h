@@ -349,6 +349,11 @@ public:
     /// go on driving the instances that own them; pinnedOut is filled once
     /// gather_wait(ticket) returns true.
     int64_t gather_async(unsigned count, const void* const* srcs, const unsigned* bytes, void* pinnedOut);
+    /// The same with a header of hdrLens[i] <= 8 bytes (hdrs + 8 i) written
+    /// before range i: range i lands at the running offset of
+    /// align16(hdrLens[k] + bytes[k]) over k < i, zero-padded (framed egress).
+    int64_t gather_async_framed(unsigned count, const void* const* srcs, const unsigned* bytes,
+                                const uint8_t* hdrs, const unsigned* hdrLens, void* pinnedOut);
     /// Wait until gather `ticket` and every earlier one have landed.
     bool gather_wait(int64_t ticket);
     /// Host -> device copy on the staging stream, issued now; every later

@@ -78,7 +78,8 @@ class BatchOptions(ctypes.Structure):
     _fields_ = [("steps", ctypes.c_uint32), ("warmup", ctypes.c_uint32),
                 ("verify", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("threads", ctypes.c_uint32), ("groups", ctypes.c_uint32),
-                ("e2e", ctypes.c_uint32), ("digest", ctypes.c_uint32), ("defer", ctypes.c_uint32)]
+                ("e2e", ctypes.c_uint32), ("digest", ctypes.c_uint32), ("defer", ctypes.c_uint32),
+                ("frames", ctypes.c_uint32)]
 
 
 class BatchReport(ctypes.Structure):
@@ -129,18 +130,20 @@ def run_capi(library, cfg, threads=1, event_log=None):
 
 
 def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0, groups=1,
-              e2e=False, defer=0):
+              e2e=False, defer=0, frames=False):
     """Run `cfg` through the device-resident batch API (lock-step rounds),
     streams driven by `threads` host threads (0 = library default), split
     into `groups` groups whose host work and device work alternate.  With
     e2e the originals are copied from pinned host memory every step and every
     recovery packet and recovered original is copied back.  defer=k > 0: the
     deferred-output API, a stream yields after every k-th decode and a group
-    keeps up to two submissions in flight.
+    keeps up to two submissions in flight.  frames (with e2e): packets travel
+    as framed datagrams (sgpu_frames_recv / sgpu_frames_send).
 
     Returns (results of the last run, BatchReport)."""
     res = (StreamResult * cfg.streams)()
-    opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads, groups, 1 if e2e else 0, 1, defer)
+    opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads, groups, 1 if e2e else 0, 1, defer,
+                       1 if frames else 0)
     rep = BatchReport()
     rc = lib().scenario_run_batch(library.encode(), ctypes.byref(cfg), res, ctypes.byref(opt),
                                   ctypes.byref(rep))
@@ -175,12 +178,13 @@ class BatchSession:
         if not self.handle:
             raise RuntimeError("scenario_batch_open(%s) failed" % library)
 
-    def run(self, steps=1, warmup=0, verify=False, threads=0, groups=1, e2e=False, digest=True, defer=0):
+    def run(self, steps=1, warmup=0, verify=False, threads=0, groups=1, e2e=False, digest=True, defer=0,
+            frames=False):
         """digest=False: timed runs skip the per-stream event logs (results
         then carry no digest; take it from a verified run)."""
         res = (StreamResult * self.cfg.streams)()
         opt = BatchOptions(steps, warmup, 1 if verify else 0, -1, threads, groups,
-                           1 if e2e else 0, 1 if digest else 0, defer)
+                           1 if e2e else 0, 1 if digest else 0, defer, 1 if frames else 0)
         rep = BatchReport()
         rc = lib().scenario_batch_run(self.handle, res, ctypes.byref(opt), ctypes.byref(rep))
         if rc != 0:
