@@ -189,19 +189,25 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
                             defer=defer)
         if rep.mismatches or any(r.status for r in res):
             raise RuntimeError("bench leg %s: verification failed" % name)
+        # the timed runs without per-launch timing events (each orders its
+        # launch behind a timestamp: +30 % on C3, profiles/r3f_timing_ab.txt),
+        # then one more run with them for the device and executor times
         for _ in range(runs):
             res, rep = sess.run(steps=1, warmup=0, verify=False, threads=threads, groups=groups,
-                                digest=False, defer=defer)
+                                digest=False, defer=defer, timing=False)
             per.append(rep)
+        _, trep = sess.run(steps=1, warmup=0, verify=False, threads=threads, groups=groups,
+                           digest=False, defer=defer, timing=True)
     finally:
         sess.close()
     per.sort(key=lambda r: r.seconds)
     rep = per[len(per) // 2]   # the median run
     eng, alg = engine_bytes(rep)
+    teng, talg = engine_bytes(trep)
     payload = rep.payload_bytes   # (one run)
     sec = rep.seconds
-    exec_s = rep.exec_ms / 1e3
-    exec_bytes = alg - eng["solve_bytes"]
+    exec_s = trep.exec_ms / 1e3
+    exec_bytes = talg - teng["solve_bytes"]
     out = {
         "workload": "%d stream%s x %d originals x %d B, %d%% loss" % (
             cfg.streams, "s" if cfg.streams > 1 else "", cfg.originals, cfg.payload_bytes,
@@ -214,7 +220,8 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
         "value": round(alg / sec / 1e9, 3),
         "unit": "GB/s",
         "payload_GBps": round(payload / sec / 1e9, 3),
-        "device_ms_per_run": round(rep.device_ms, 3),
+        "device_ms_per_run": round(trep.device_ms, 3),
+        "device_ms_note": "one extra run with per-launch HIP events (the timed runs have none)",
         "rounds_per_run": rep.rounds,
         "algorithmic_bytes_per_run": alg,
         "payload_bytes_per_run": payload,

@@ -51,6 +51,10 @@ struct BatchOptions
                        ///< originals staged as frames and handed to the decoders by
                        ///< sgpu_frames_recv, recovery packets copied back framed by
                        ///< sgpu_frames_send and parsed on landing
+    uint32_t no_timing; ///< timed steps without the per-launch device timing events
+                        ///< (device_ms / exec_ms read 0): the events order every launch
+                        ///< behind a timestamp, tens of microseconds a flush on the
+                        ///< latency-bound single-stream legs
 };
 
 struct BatchReport
@@ -1091,7 +1095,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         uint64_t e0[kEngineStats + 1], e1[kEngineStats + 1];
         api.engine_stats(e0);
         e0[kEngineStats] = api.arena_bytes();
-        api.timing(timed ? 1 : 0, 1, nullptr, nullptr);
+        api.timing(timed && !opt->no_timing ? 1 : 0, 1, nullptr, nullptr);
         const auto t1 = Clock::now();
         rc = run_pipeline(sh, results, timed ? opt->steps : 1, &rounds, phase, &payload);
         const double dt = std::chrono::duration<double>(Clock::now() - t1).count();

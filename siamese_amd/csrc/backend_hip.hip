@@ -666,6 +666,17 @@ __global__ __launch_bounds__(64 * kLdpcWaves) void k_ldpc(const LdpcItem* __rest
 // rows): the lane holds bytes [p16, p16 + 16) of its quad's row; m0 / m1 /
 // cut are the quad's row's masks and cutoff (per lane), `live` whether the
 // row reaches this tile.
+__device__ __forceinline__ uint4 version_elem16(uint32_t e, uint32_t p16, uint32_t b4, const uint32_t* stage,
+                                                uint32_t stageLo, uint32_t staged, const uint4* tableL,
+                                                const uint4* __restrict__ seg, uint32_t blk)
+{
+    if (e - stageLo < staged)
+        return lds16(stage, (kRowSums + e - stageLo) * 64 + b4);
+    const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
+    const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+    return p16 < d.z ? ld16(src + p16) : make_uint4(0, 0, 0, 0);
+}
+
 __device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_t cut, bool live, uint32_t p16,
                                                uint32_t b4, const uint32_t* updOfL, const uint32_t* updFromL,
                                                const uint32_t* updToL, const uint32_t* cxL, const uint4* permL,
@@ -673,39 +684,88 @@ __device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_
                                                uint32_t staged, const uint4* tableL, const uint4* __restrict__ seg,
                                                uint32_t blk, uint4& a0, uint4& a1)
 {
-    for (uint32_t k = 0; k < kRowSums; ++k) {
-        if (updOfL[k] == 0xffu)
-            continue;   // (uniform) sum k has no update in this batch
-        const uint32_t from = updFromL[k], to = updToL[k];
-        const bool in0 = (m0 >> k) & 1u, in1 = (m1 >> k) & 1u;
-        // the update's first element at or past the cutoff (its lane's grid)
-        uint32_t e = cut <= from ? from : from + ((cut - from + kLanes - 1) / kLanes) * kLanes;
-        if (!live || !(in0 || in1))
-            e = to;
-        const uint32_t sidx = k % kSums;
-        const uint32_t slen = tableL[k].z;   // the sum's length as the rows read it (clips the terms)
-        if (p16 >= slen)
-            e = to;
-        for (; e < to; e += kLanes) {
-            uint4 v;
-            if (e - stageLo < staged) {
-                v = lds16(stage, (kRowSums + e - stageLo) * 64 + b4);
-            } else {
-                const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
-                const uint64_t src = ((uint64_t)d.y << 32) | d.x;
-                v = p16 < d.z ? ld16(src + p16) : make_uint4(0, 0, 0, 0);
+    // Lane by lane: the three sums of lane l fold the same elements (one
+    // residue class mod 8), so an element's corrections for the sums the row
+    // selects combine into one coefficient per accumulator (1 ^ CX ^ CX^2 as
+    // the masks pick them): one load and at most two multiplies per element.
+    // A sum whose length ends inside this 16-byte lane is taken per sum, with
+    // its exact clip.
+    for (uint32_t l = 0; l < kLanes; ++l) {
+        uint32_t lo = 0xffffffffu, hi = 0, full = 0, part = 0;
+        uint32_t f[kSums], t[kSums];
+#pragma unroll
+        for (uint32_t s = 0; s < kSums; ++s) {
+            const uint32_t k = l * kSums + s;
+            f[s] = t[s] = 0;
+            if (updOfL[k] == 0xffu)
+                continue;
+            const bool sel = ((m0 | m1) >> k) & 1u;
+            const uint32_t slen = tableL[k].z;
+            if (!live || !sel || p16 >= slen)
+                continue;
+            f[s] = updFromL[k];
+            t[s] = updToL[k];
+            const uint32_t first = cut <= f[s] ? f[s] : f[s] + ((cut - f[s] + kLanes - 1) / kLanes) * kLanes;
+            if (first >= t[s])
+                continue;
+            if (p16 + 16 > slen) {
+                part |= 1u << s;
+                continue;
             }
-            if (sidx != 0) {
+            full |= 1u << s;
+            lo = min(lo, first);
+            hi = max(hi, t[s]);
+        }
+        // (lo: a lane element, every range of the lane shares its residue)
+        for (uint32_t e = lo; e < hi; e += kLanes) {
+            uint32_t y0 = 0, y1 = 0, cx = 0;
+            bool need = false;
+#pragma unroll
+            for (uint32_t s = 0; s < kSums; ++s)
+                need |= (full >> s & 1u) && s != 0 && e >= f[s] && e < t[s];
+            if (need) {
                 const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e).w;
-                const uint32_t cx = cxL[col % kColumnValuePeriod];
-                v = gf_mul16_tab(v, gf_tab_l(permL, permC, sidx == 1 ? (cx & 0xffu) : (cx >> 8)));
+                cx = cxL[col % kColumnValuePeriod];
             }
-            if (p16 + 16 > slen)
+#pragma unroll
+            for (uint32_t s = 0; s < kSums; ++s) {
+                if (!(full >> s & 1u) || e < f[s] || e >= t[s])
+                    continue;
+                const uint32_t k = l * kSums + s;
+                const uint32_t c = s == 0 ? 1u : s == 1 ? (cx & 0xffu) : (cx >> 8);
+                if ((m0 >> k) & 1u)
+                    y0 ^= c;
+                if ((m1 >> k) & 1u)
+                    y1 ^= c;
+            }
+            if (!(y0 | y1))
+                continue;
+            const uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
+            if (y0)
+                a0 = xor16(a0, y0 == 1 ? v : gf_mul16_tab(v, gf_tab_l(permL, permC, y0)));
+            if (y1)
+                a1 = xor16(a1, y1 == 1 ? v : gf_mul16_tab(v, gf_tab_l(permL, permC, y1)));
+        }
+        // sums ending inside this lane: per sum, clipped to their length
+        for (; part; part &= part - 1) {
+            const uint32_t s = (uint32_t)__builtin_ctz(part);
+            const uint32_t k = l * kSums + s;
+            const uint32_t slen = tableL[k].z;
+            const bool in0 = (m0 >> k) & 1u, in1 = (m1 >> k) & 1u;
+            for (uint32_t e = cut <= f[s] ? f[s] : f[s] + ((cut - f[s] + kLanes - 1) / kLanes) * kLanes; e < t[s];
+                 e += kLanes) {
+                uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
+                if (s != 0) {
+                    const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e).w;
+                    const uint32_t cx = cxL[col % kColumnValuePeriod];
+                    v = gf_mul16_tab(v, gf_tab_l(permL, permC, s == 1 ? (cx & 0xffu) : (cx >> 8)));
+                }
                 v = mask16(v, (int)slen - (int)p16);
-            if (in0)
-                a0 = xor16(a0, v);
-            if (in1)
-                a1 = xor16(a1, v);
+                if (in0)
+                    a0 = xor16(a0, v);
+                if (in1)
+                    a1 = xor16(a1, v);
+            }
         }
     }
 }
@@ -771,6 +831,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     // it (index, or 0xff) and that update's element range [from, to)
     __shared__ uint32_t updOfL[kRowSums];
     __shared__ uint32_t updFromL[kRowSums], updToL[kRowSums];
+    __shared__ uint32_t updMaxLast1;   // 1 + the last element any update of the batch folds in (0: none)
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
@@ -1019,6 +1080,17 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 }
             }
             const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
+            if (tid == 0) {
+                // rows whose cutoff is past every update's last element read
+                // the final sums as they are (no version corrections)
+                uint32_t m = 0;
+                for (uint32_t k = 0; k < kRowSums; ++k)
+                    if (updOfL[k] != 0xffu) {
+                        const uint32_t f = updFromL[k], t = updToL[k];
+                        m = max(m, f + ((t - f - 1) / kLanes) * kLanes + 1);
+                    }
+                updMaxLast1 = m;
+            }
             for (uint32_t unit = wave; unit < uUnits + nPairs; unit += kExecWaves) {
                 if (unit < uUnits) {
                     [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
@@ -1320,7 +1392,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
 #undef SGPU_QUAD_GROUP
                     }
                     // (rows read the sums as of their cutoff, ops.h RowItem)
-                    row_versions16(w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, live, p16, b4, updOfL, updFromL,
+                    if (__any(act && w2.y < updMaxLast1 ? 1 : 0))
+                        row_versions16(w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, live, p16, b4, updOfL, updFromL,
                                    updToL, cxL, permL, permC, stage, stageLo, staged, tableL, seg, blk, a0, a1);
                     PHASE_MARK(14, qclk);
                     if (live)
@@ -1379,7 +1452,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                    return len != 0;
                                });
                         // (the sums as of the row's cutoff, ops.h RowItem)
-                        row_versions4(m0 & 0xffffffu, m1 & 0xffffffu, uni(w2.y), tileBase, p, lane, updOfL, updFromL,
+                        if (uni(w2.y) < updMaxLast1)
+                            row_versions4(m0 & 0xffffffu, m1 & 0xffffffu, uni(w2.y), tileBase, p, lane, updOfL, updFromL,
                                       updToL, cxL, stage, stageLo, staged, tableL, seg, blk, acc0, acc1);
                     }
                     // sparse part: this unit's share of the 2*ceil(N/16) draws
@@ -2628,7 +2702,15 @@ bool be_fence_wait(void* fence, unsigned spinUs)
     return true;
 }
 
-void be_timing_enable(bool on) { g_timing = on; }
+void be_timing_enable(bool on)
+{
+    // SGPU_TIMING=0: no per-launch events at all (A/B of their cost)
+    static const bool allowed = [] {
+        const char* v = std::getenv("SGPU_TIMING");
+        return !v || std::atoi(v) != 0;
+    }();
+    g_timing = on && allowed;
+}
 void be_timing_reset()
 {
     g_execMs = 0;

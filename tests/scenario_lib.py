@@ -79,7 +79,7 @@ class BatchOptions(ctypes.Structure):
                 ("verify", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("threads", ctypes.c_uint32), ("groups", ctypes.c_uint32),
                 ("e2e", ctypes.c_uint32), ("digest", ctypes.c_uint32), ("defer", ctypes.c_uint32),
-                ("frames", ctypes.c_uint32)]
+                ("frames", ctypes.c_uint32), ("no_timing", ctypes.c_uint32)]
 
 
 class BatchReport(ctypes.Structure):
@@ -179,12 +179,13 @@ class BatchSession:
             raise RuntimeError("scenario_batch_open(%s) failed" % library)
 
     def run(self, steps=1, warmup=0, verify=False, threads=0, groups=1, e2e=False, digest=True, defer=0,
-            frames=False):
+            frames=False, timing=True):
         """digest=False: timed runs skip the per-stream event logs (results
         then carry no digest; take it from a verified run)."""
         res = (StreamResult * self.cfg.streams)()
         opt = BatchOptions(steps, warmup, 1 if verify else 0, -1, threads, groups,
-                           1 if e2e else 0, 1 if digest else 0, defer, 1 if frames else 0)
+                           1 if e2e else 0, 1 if digest else 0, defer, 1 if frames else 0,
+                           0 if timing else 1)
         rep = BatchReport()
         rc = lib().scenario_batch_run(self.handle, res, ctypes.byref(opt), ctypes.byref(rep))
         if rc != 0:

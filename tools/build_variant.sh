@@ -9,7 +9,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 cd $ROOT/siamese_amd
 OUT=build/var_$NAME
 mkdir -p $OUT
-HOST="gf codedef pool placement engine encoder decoder arq api batch"
+HOST="gf codedef pool placement engine encoder decoder arq api batch frames"
 for f in $HOST; do
     g++ -std=c++17 -O2 -g -mavx2 -fPIC -ftls-model=initial-exec -fvisibility=hidden "$@" -c csrc/$f.cpp -o $OUT/$f.o &
 done

@@ -27,7 +27,7 @@ def main():
         secs = []
         for _ in range(runs):
             res, rep = sess.run(steps=1, warmup=0, verify=False, threads=0, groups=groups, digest=False,
-                                defer=defer)
+                                defer=defer, timing=os.environ.get("LEG_TIMING", "0") == "1")
             secs.append(rep.seconds * 1e3)
     finally:
         sess.close()
