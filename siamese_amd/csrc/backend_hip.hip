@@ -510,10 +510,13 @@ __device__ __forceinline__ uint64_t pcg_jump(uint64_t s, uint64_t inc, uint32_t 
 }
 
 // Sum or window descriptor i of the current OP_ROWS batch (per lane)
+// (LDS slot j holds block word j < kRowSums, else word j + skip: window
+// entries below the batch's stageLo, which only k_ldpc reads, stay in memory)
 __device__ __forceinline__ uint4 table_entry(const uint4* tableL, const uint4* __restrict__ seg,
-                                             uint32_t blockWord, uint32_t i)
+                                             uint32_t blockWord, uint32_t i, uint32_t skip)
 {
-    return i < kRowsTableLds ? tableL[i] : ld16((uint64_t)(seg + blockWord + i));
+    const uint32_t j = i < kRowSums ? i : i - kRowSums >= skip ? i - skip : kRowsTableLds;
+    return j < kRowsTableLds ? tableL[j] : ld16((uint64_t)(seg + blockWord + i));
 }
 
 // One Siamese row's LDPC picks [d0, d1) of PCG.Seed(row, N) (pair index
@@ -536,7 +539,7 @@ __device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t
         // lane j: draw c + j -> window element e and its descriptor
         const uint64_t st = pcgA * sc + inc * pcgG;
         const uint32_t e = off + pcg_output(st) % N;
-        const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
+        const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
         sc = c_pcgA[64] * sc + inc * c_pcgG[64];
         const uint32_t cnt = d1 - c < 64 ? d1 - c : 64;
         for (uint32_t j0 = 0; j0 < cnt; j0 += kExecDepth) {
@@ -672,25 +675,27 @@ __device__ __forceinline__ uint4 version_elem16(uint32_t e, uint32_t p16, uint32
 {
     if (e - stageLo < staged)
         return lds16(stage, (kRowSums + e - stageLo) * 64 + b4);
-    const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
+    const uint4 d = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
     const uint64_t src = ((uint64_t)d.y << 32) | d.x;
     return p16 < d.z ? ld16(src + p16) : make_uint4(0, 0, 0, 0);
 }
 
-__device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_t cut, bool live, uint32_t p16,
-                                               uint32_t b4, const uint32_t* updOfL, const uint32_t* updFromL,
-                                               const uint32_t* updToL, const uint32_t* cxL, const uint4* permL,
-                                               const uint32_t* permC, const uint32_t* stage, uint32_t stageLo,
-                                               uint32_t staged, const uint4* tableL, const uint4* __restrict__ seg,
-                                               uint32_t blk, uint4& a0, uint4& a1)
+//
+// One Siamese lane l at a time: its three sums fold the same elements (one
+// residue class mod 8), so an element's corrections for the sums the row
+// selects combine into one coefficient per accumulator (1 ^ CX ^ CX^2 as the
+// masks pick them): one load and at most two multiplies per element.  A sum
+// whose length ends inside this 16-byte lane is taken per sum, with its
+// exact clip.
+__device__ __forceinline__ void version_lane16(uint32_t l, uint32_t m0, uint32_t m1, uint32_t cut, bool live,
+                                               uint32_t p16, uint32_t b4, const uint32_t* updOfL,
+                                               const uint32_t* updFromL, const uint32_t* updToL,
+                                               const uint32_t* cxL, const uint4* permL, const uint32_t* permC,
+                                               const uint32_t* stage, uint32_t stageLo, uint32_t staged,
+                                               const uint4* tableL, const uint4* __restrict__ seg, uint32_t blk,
+                                               uint4& a0, uint4& a1)
 {
-    // Lane by lane: the three sums of lane l fold the same elements (one
-    // residue class mod 8), so an element's corrections for the sums the row
-    // selects combine into one coefficient per accumulator (1 ^ CX ^ CX^2 as
-    // the masks pick them): one load and at most two multiplies per element.
-    // A sum whose length ends inside this 16-byte lane is taken per sum, with
-    // its exact clip.
-    for (uint32_t l = 0; l < kLanes; ++l) {
+    {
         uint32_t lo = 0xffffffffu, hi = 0, full = 0, part = 0;
         uint32_t f[kSums], t[kSums];
 #pragma unroll
@@ -718,13 +723,14 @@ __device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_
         }
         // (lo: a lane element, every range of the lane shares its residue)
         for (uint32_t e = lo; e < hi; e += kLanes) {
+            PHASE_ADD(24, 1);
             uint32_t y0 = 0, y1 = 0, cx = 0;
             bool need = false;
 #pragma unroll
             for (uint32_t s = 0; s < kSums; ++s)
                 need |= (full >> s & 1u) && s != 0 && e >= f[s] && e < t[s];
             if (need) {
-                const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e).w;
+                const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e, stageLo).w;
                 cx = cxL[col % kColumnValuePeriod];
             }
 #pragma unroll
@@ -754,9 +760,10 @@ __device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_
             const bool in0 = (m0 >> k) & 1u, in1 = (m1 >> k) & 1u;
             for (uint32_t e = cut <= f[s] ? f[s] : f[s] + ((cut - f[s] + kLanes - 1) / kLanes) * kLanes; e < t[s];
                  e += kLanes) {
+                PHASE_ADD(25, 1);
                 uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
                 if (s != 0) {
-                    const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e).w;
+                    const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e, stageLo).w;
                     const uint32_t cx = cxL[col % kColumnValuePeriod];
                     v = gf_mul16_tab(v, gf_tab_l(permL, permC, s == 1 ? (cx & 0xffu) : (cx >> 8)));
                 }
@@ -768,6 +775,18 @@ __device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_
             }
         }
     }
+}
+
+__device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_t cut, bool live, uint32_t p16,
+                                               uint32_t b4, const uint32_t* updOfL, const uint32_t* updFromL,
+                                               const uint32_t* updToL, const uint32_t* cxL, const uint4* permL,
+                                               const uint32_t* permC, const uint32_t* stage, uint32_t stageLo,
+                                               uint32_t staged, const uint4* tableL, const uint4* __restrict__ seg,
+                                               uint32_t blk, uint4& a0, uint4& a1)
+{
+    for (uint32_t l = 0; l < kLanes; ++l)
+        version_lane16(l, m0, m1, cut, live, p16, b4, updOfL, updFromL, updToL, cxL, permL, permC, stage, stageLo,
+                       staged, tableL, seg, blk, a0, a1);
 }
 
 // The same for a row in the dword layout (general path: one wave, the lane
@@ -792,7 +811,7 @@ __device__ __forceinline__ void row_versions4(uint32_t m0, uint32_t m1, uint32_t
         for (uint32_t e = cut <= from ? from : from + ((cut - from + kLanes - 1) / kLanes) * kLanes; e < to;
              e += kLanes) {
             uint32_t v;
-            const uint4 d = table_entry(tableL, seg, blk, kRowSums + e);
+            const uint4 d = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
             if (e - stageLo < staged) {
                 v = stage[(kRowSums + e - stageLo) * 64 + lane];
             } else {
@@ -832,6 +851,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint32_t updOfL[kRowSums];
     __shared__ uint32_t updFromL[kRowSums], updToL[kRowSums];
     __shared__ uint32_t updMaxLast1;   // 1 + the last element any update of the batch folds in (0: none)
+    // the version corrections of the batch's first kVersionRows rows (this
+    // tile, dword layout), computed lane by lane in phase A
+    __shared__ uint32_t corrL[kVersionRows][2][64];
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
@@ -939,8 +961,15 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             // the whole block (descriptors, updates, rows) to LDS: every
             // later header read is an LDS read, not a memory round trip
             const uint32_t blockWords = uni(h1.w);
-            for (uint32_t i = tid; i < blockWords && i < kRowsTableLds; i += kExecThreads)
-                tableL[i] = op_word(rb, seg, pos, kOpWords + i);
+            // (the host points the stage at the elements the batch reads:
+            // GfOp.dst low word = stageLo, ops.h; the LDS table skips the
+            // window entries below it: table_entry)
+            const uint32_t stageLo = uni(h0.x) < E ? uni(h0.x) : E;
+            for (uint32_t i = tid; i < kRowsTableLds; i += kExecThreads) {
+                const uint32_t word = i < kRowSums ? i : i + stageLo;
+                if (word < blockWords)
+                    tableL[i] = op_word(rb, seg, pos, kOpWords + word);
+            }
             if (tid == 0)
                 generalRows = 0;
             // the next op's prefetched block goes to the ring now (the ring's
@@ -957,14 +986,11 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             // t loads 16 bytes of entry t/16 per pass, four passes in flight;
             // bytes past an entry's length (absent elements: all of them)
             // read zero.
-            // (the host points the stage at the elements the batch reads:
-            // GfOp.dst low word = stageLo, ops.h)
-            const uint32_t stageLo = uni(h0.x) < E ? uni(h0.x) : E;
             if (tid < kRowSums) {
                 // (at most one update per sum in a batch: Program::rows_update)
                 uint32_t found = 0xffu, from = 0, to = 0;
                 for (uint32_t u = 0; u < U; ++u) {
-                    const uint4 w1 = table_entry(tableL, seg, blk, kRowSums + E + u * kUpdateWords + 1);
+                    const uint4 w1 = table_entry(tableL, seg, blk, kRowSums + E + u * kUpdateWords + 1, stageLo);
                     if (w1.z == tid && w1.y > w1.x) {
                         found = u;
                         from = w1.x;
@@ -986,6 +1012,11 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             static_assert(kExecWaves * 2 >= kRowSums, "update accumulators fit part[]");
             for (uint32_t i = tid; i < U * 64; i += kExecThreads)
                 updAcc[i] = 0;
+            // rows [0, Rv) of a versioned batch (GfOp.dst high word, ops.h)
+            // take their corrections from corrL
+            const uint32_t Rv = min(min(uni(h0.y), R), (uint32_t)kVersionRows);
+            for (uint32_t i = tid; i < Rv * 128; i += kExecThreads)
+                (&corrL[0][0][0])[i] = 0;
             if (tid == 0)
                 sumsDirty = 0;
             {
@@ -997,7 +1028,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         const uint32_t x = x0 + u * kPass;
                         v[u] = make_uint4(0, 0, 0, 0);
                         if (x < entries) {
-                            const uint4 d = table_entry(tableL, seg, blk, x < kRowSums ? x : x + stageLo);
+                            const uint4 d = table_entry(tableL, seg, blk, x < kRowSums ? x : x + stageLo, stageLo);
                             const uint64_t src = ((uint64_t)d.y << 32) | d.x;
                             if (tileBase + q16 < d.z)
                                 v[u] = ld16(src + tileBase + q16);
@@ -1041,7 +1072,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             uint64_t sdst = 0;
             uint32_t sn = 0, svalid = 0, scur = 0;
             if (wave < U) {
-                const uint4 w0 = table_entry(tableL, seg, blk, updWord + wave * kUpdateWords - kOpWords);
+                const uint4 w0 = table_entry(tableL, seg, blk, updWord + wave * kUpdateWords - kOpWords, stageLo);
                 sdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
                 sn = uni(w0.z);
                 svalid = uni(w0.w) & 0x3fffffffu;
@@ -1054,7 +1085,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     const uint32_t r = r0 + lane;
                     uint32_t size = 0, n01 = 0;
                     if (r < planned) {
-                        const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
+                        const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
                         // (a wide row reads its two k_ldpc sums as one pair)
                         const uint32_t pairs = (w1.x & kRowWide) ? 1u : (w1.w + kPairRate - 1) / kPairRate;
                         const uint32_t n0 = __builtin_popcount(w1.x & 0xffffffu) + pairs;
@@ -1091,13 +1122,41 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     }
                 updMaxLast1 = m;
             }
-            for (uint32_t unit = wave; unit < uUnits + nPairs; unit += kExecWaves) {
-                if (unit < uUnits) {
+            const uint32_t vTasks = Rv * kLanes / 4;   // (row, lane) units, four per wave task
+            for (uint32_t unit = wave; unit < uUnits + nPairs + vTasks; unit += kExecWaves) {
+                if (unit >= uUnits + nPairs) {
+                    // version corrections: quad g takes (row, lane) unit
+                    // 4*task + g; the lanes of a row meet in corrL
+                    const uint32_t v = 4 * (unit - uUnits - nPairs) + g;
+                    const uint32_t r = v / kLanes, l = v % kLanes;
+                    const uint32_t p16 = tileBase + (lane & 15u) * 16u;
+                    const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
+                    const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
+                    const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo);
+                    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+                    version_lane16(l, w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, tileBase < align16u(w0.z), p16, b4,
+                                   updOfL, updFromL, updToL, cxL, permL, permC, stage, stageLo, staged, tableL, seg,
+                                   blk, a0, a1);
+                    uint32_t* c0 = &corrL[r][0][b4];
+                    uint32_t* c1 = &corrL[r][1][b4];
+                    if (a0.x | a0.y | a0.z | a0.w) {
+                        atomicXor(c0 + 0, a0.x);
+                        atomicXor(c0 + 1, a0.y);
+                        atomicXor(c0 + 2, a0.z);
+                        atomicXor(c0 + 3, a0.w);
+                    }
+                    if (a1.x | a1.y | a1.z | a1.w) {
+                        atomicXor(c1 + 0, a1.x);
+                        atomicXor(c1 + 1, a1.y);
+                        atomicXor(c1 + 2, a1.z);
+                        atomicXor(c1 + 3, a1.w);
+                    }
+                } else if (unit < uUnits) {
                     [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
                     const uint32_t u = unit / Q;
                     const uint32_t uq = unit % Q;
-                    const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
-                    const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords);
+                    const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords, stageLo);
+                    const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords, stageLo);
                     const uint32_t un = uni(w0.z), us = uni(w0.w) >> 30;
                     const uint32_t from = uni(w1.x), to = uni(w1.y);
                     const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
@@ -1115,7 +1174,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                     const uint32_t k = kk + 4 * j + g;
                                     const bool act = k < k1;
                                     const uint32_t e = from + (act ? k : k0) * kLanes;
-                                    const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
+                                    const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
                                     if (act && (lane & 15u) == 0)
                                         refBytes += ev.z;
                                     slot[j] = act ? kRowSums + e - stageLo : zeroSlot;
@@ -1141,7 +1200,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             uint32_t acc = 0;
                             for (uint32_t c = k0; c < k1; c += 64) {
                                 const uint32_t e = from + (c + lane) * kLanes;
-                                const uint4 ev = c + lane < k1 ? table_entry(tableL, seg, blk, kRowSums + e)
+                                const uint4 ev = c + lane < k1 ? table_entry(tableL, seg, blk, kRowSums + e, stageLo)
                                                                : make_uint4(0, 0, 0, 0);
                                 const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
                                 const GfTab tab = gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8));
@@ -1197,9 +1256,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     if (!__any(act ? 1 : 0))
                         continue;
                     const uint4 z4 = make_uint4(0, 0, 0, 0);
-                    const uint4 w0 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords) : z4;
-                    const uint4 w1 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords) : z4;
-                    const uint4 w2 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords) : z4;
+                    const uint4 w0 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo) : z4;
+                    const uint4 w1 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo) : z4;
+                    const uint4 w2 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo) : z4;
                     const uint32_t rn = w0.z;
                     const uint32_t m0 = w1.x & 0xffffffu, m1 = w1.y & 0xffffffu;
                     const uint32_t row = w1.z, N = act ? w1.w : 0u, woff = w2.x;
@@ -1244,7 +1303,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                 rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
                                 e = woff + (uint32_t)rr;
                             }
-                            const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e).z;
+                            const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e, stageLo).z;
                             if (!wide)
                                 refBytes += len < rn ? len : rn;
                             general |= e - stageLo >= staged;
@@ -1272,8 +1331,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             // ones; anything else marks the stage stale and the sums are
             // re-read from memory after a barrier.
             for (uint32_t u = wave; u < U; u += kExecWaves) {
-                const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords);
-                const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords);
+                const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords, stageLo);
+                const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords, stageLo);
                 const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
                 const uint32_t un = uni(w0.z), uvalid = uni(w0.w) & 0x3fffffffu;
                 if (tileBase >= align16u(un))
@@ -1342,9 +1401,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     if (!__any(act ? 1 : 0))
                         continue;
                     const uint4 z4 = make_uint4(0, 0, 0, 0);
-                    const uint4 w0 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords) : z4;
-                    const uint4 w1 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords) : z4;
-                    const uint4 w2 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords) : z4;
+                    const uint4 w0 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo) : z4;
+                    const uint4 w1 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo) : z4;
+                    const uint4 w2 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo) : z4;
                     const uint64_t rdst = ((uint64_t)w0.y << 32) | w0.x;
                     const uint32_t rn = w0.z, rvalid = w0.w;
                     const uint32_t mix = w1.y >> 24;
@@ -1391,11 +1450,19 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             SGPU_QUAD_GROUP(12)
 #undef SGPU_QUAD_GROUP
                     }
-                    // (rows read the sums as of their cutoff, ops.h RowItem)
-                    if (__any(act && w2.y < updMaxLast1 ? 1 : 0))
-                        row_versions16(w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, live, p16, b4, updOfL, updFromL,
-                                   updToL, cxL, permL, permC, stage, stageLo, staged, tableL, seg, blk, a0, a1);
                     PHASE_MARK(14, qclk);
+                    // (rows read the sums as of their cutoff, ops.h RowItem)
+                    if (r < Rv) {
+                        a0 = xor16(a0, lds16(&corrL[r][0][0], b4));
+                        a1 = xor16(a1, lds16(&corrL[r][1][0], b4));
+                    }
+                    if (__any(act && r >= Rv && w2.y < updMaxLast1 ? 1 : 0)) {
+                        row_versions16(w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, live && r >= Rv, p16, b4, updOfL, updFromL,
+                                       updToL, cxL, permL, permC, stage, stageLo, staged, tableL, seg, blk, a0, a1);
+                        PHASE_MARK(16, qclk);
+                        if (lane == 0)
+                            PHASE_ADD(17, 1);
+                    }
                     if (live)
                         store_item16(xor16(a0, gf_mul16_tab(a1, tab)), p16, rdst, rn, rvalid, cur);
                     if (act) {
@@ -1417,9 +1484,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             for (uint32_t unit = wave; unit < units; unit += kExecWaves) {
                 const uint32_t r = P == 1 ? unit : unit / P;
                 const uint32_t q = P == 1 ? 0 : unit % P;
-                const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
-                const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
-                const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords);
+                const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
+                const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
+                const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo);
                 const uint64_t rdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
                 const uint32_t rn = uni(w0.z), rvalid = uni(w0.w);
                 const uint32_t m0 = uni(w1.x), m1 = uni(w1.y), row = uni(w1.z), N = uni(w1.w);
@@ -1452,7 +1519,10 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                    return len != 0;
                                });
                         // (the sums as of the row's cutoff, ops.h RowItem)
-                        if (uni(w2.y) < updMaxLast1)
+                        if (r < Rv) {
+                            acc0 ^= corrL[r][0][lane];
+                            acc1 ^= corrL[r][1][lane];
+                        } else if (uni(w2.y) < updMaxLast1)
                             row_versions4(m0 & 0xffffffu, m1 & 0xffffffu, uni(w2.y), tileBase, p, lane, updOfL, updFromL,
                                       updToL, cxL, stage, stageLo, staged, tableL, seg, blk, acc0, acc1);
                     }
@@ -1467,7 +1537,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             if (e - stageLo < staged) {
                                 v = stage[(kRowSums + e - stageLo) * 64 + lane];
                             } else {
-                                const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e);
+                                const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
                                 const uint64_t src = ((uint64_t)uni(ev.y) << 32) | uni(ev.x);
                                 const uint32_t len = uni(ev.z);
                                 if (tileBase < len)
@@ -1495,9 +1565,10 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 } else {
                     if (tileBase < align16u(rn))
                         store_item(acc0 ^ (mix > 1 ? gf_mul_tab(acc1, mixTab) : acc1), p, rdst, rn, rvalid, c0);
-                    PHASE_MARK(14, rclk);
+                    PHASE_MARK(18, rclk);
+                    PHASE_ADD(23, 1);
                     store_literal(p, rdst, rn, row_lit_len(m0), uni(w2.z), uni(w2.w));
-                    PHASE_MARK(15, rclk);
+                    PHASE_MARK(22, rclk);
                 }
             }
             if (P > 1 && units) {
@@ -1505,9 +1576,9 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 if (wave < units && wave % P == 0 &&
                     !(wave / P < planned && uni(rowInfo[wave / P].x) < kPlanGeneral)) {
                     const uint32_t r = wave / P;
-                    const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords);
-                    const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords);
-                    const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords);
+                    const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
+                    const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
+                    const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo);
                     const uint64_t rdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
                     const uint32_t rn = uni(w0.z), rvalid = uni(w0.w);
                     const uint32_t m0 = uni(w1.x), mix = uni(w1.y) >> 24;

@@ -115,6 +115,7 @@ void ProgramBody::rows_open(uint32_t base, bool keepWindow)
     rb.haveSums = false;
     rb.readMask = 0;
     rb.cutMax = 0;
+    rb.versioned = false;
     if (!keepWindow) {
         rb.base = base;
         rb.win.clear();
@@ -324,7 +325,8 @@ void ProgramBody::rows_close()
             stageLo = std::min(stageLo, r.ldpcOff);
     GfOp op;
     std::memset(&op, 0, sizeof(op));
-    op.dst = stageLo;   // (OP_ROWS has no dst of its own)
+    // (OP_ROWS has no dst of its own)
+    op.dst = stageLo | (uint64_t)(b.versioned ? std::min<uint32_t>(R, kVersionRows) : 0u) << 32;
     op.kind = OP_ROWS;
     op.n = R;
     op.valid = E;
@@ -577,10 +579,17 @@ void Program::rows_update(unsigned k, uint64_t dst, uint32_t n, uint32_t valid, 
         const char* v = std::getenv("SIAMESE_AMD_ROW_VERSIONS");   // 0: a batch per sum re-read (A/B aid)
         return !v || std::atoi(v) != 0;
     }();
+    // Rows that read the sum before the update take its elements back out
+    // (ops.h RowItem), so only short extensions join (a streaming encoder's
+    // few new originals per row; not a decoder row whose range ends far past
+    // the previous row's), into a batch of fewer than kVersionRows rows.
     if (b.readMask >> k & 1) {
         const WinEntry& seen = b.sums[k];
-        if (!versioned || seen.src != dst || valid < seen.len)
+        if (!versioned || seen.src != dst || valid < seen.len || toElement - fromElement > kVersionMaxSpan ||
+            b.rows.size() >= kVersionRows)
             rows_open(b.base, true);
+        else
+            b.versioned = true;
     }
     const uint32_t from = fromElement - b.base, to = toElement - b.base;
     int& ui = b.updateOf[k];
@@ -623,8 +632,10 @@ void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t 
 {
     ProgramBody::RowsBuild& b = b_->rb;
     // (a row whose cutoff is below an earlier row's reads sums folded past
-    // its own cutoff: it starts a batch after every update so far)
-    if ((b.haveSums && std::memcmp(b.sums, sums, sizeof(b.sums)) != 0) || cutoff < b.cutMax)
+    // its own cutoff: it starts a batch after every update so far; a
+    // versioned batch takes at most kVersionRows rows)
+    if ((b.haveSums && std::memcmp(b.sums, sums, sizeof(b.sums)) != 0) || cutoff < b.cutMax ||
+        (b.versioned && b.rows.size() >= kVersionRows))
         rows_open(b.base, true);
     b.cutMax = std::max(b.cutMax, cutoff);
     if (!b.haveSums) {

@@ -94,6 +94,7 @@ struct ProgramBody
         WinEntry sums[kRowSums];
         uint32_t readMask = 0;          // sums read by the batch's rows
         uint32_t cutMax = 0;            // largest row cutoff so far (absolute element)
+        bool versioned = false;         // an update joined after a row read its sum
         uint32_t base = 0;              // window element of entry 0
         std::vector<WinEntry> win;
         std::vector<SumUpdate> updates;

@@ -79,8 +79,10 @@ constexpr unsigned kOpWords = sizeof(GfOp) / 16;
 ///
 /// Stream layout after the GfOp header (kind = OP_ROWS, n = rows R,
 /// valid = window entries E, mix = sum updates U, termCount = block words,
-/// dst = stageLo: the first window element the batch reads, where the
-/// executor's LDS stage of the window starts):
+/// dst low word = stageLo: the first window element the batch reads, where
+/// the executor's LDS stage of the window starts; dst high word = Rv: the
+/// rows [0, Rv) that may read versioned sums, kVersionRows at most, 0 when no
+/// update of the batch joined after a row read its sum):
 ///   24 words   WinEntry of the lane sums as the rows read them (lane*3 + s)
 ///   E words    WinEntry of window elements [base, base+E): an absent
 ///              (lost) element has len 0 and contributes nothing
@@ -122,7 +124,11 @@ struct SumUpdate
 /// row's `cutoff` (batch-relative element index) taken back out.  Rows made
 /// one after another in a streaming encoder (each folding the originals
 /// added since the previous one into the sums it reads) then share one batch
-/// instead of a batch each.
+/// instead of a batch each.  A batch with such joins (Program::rows_update)
+/// holds at most kVersionRows rows, and only short joins: the executor
+/// computes the corrections of each (row, lane) pair in parallel.
+constexpr unsigned kVersionRows = 16;
+constexpr unsigned kVersionMaxSpan = 32;   // window elements one joining update may add
 struct RowItem
 {
     uint64_t dst;

@@ -28,4 +28,7 @@ for k, nm in enumerate(names):
     print("  %-14s %10.0f clocks per op" % (nm, out[k] / ops))
 print("  rows detail (wave 0 quad tasks): descriptors %.0f, terms %.0f, stores %.0f clocks per op"
       % (out[13] / ops, out[14] / ops, out[15] / ops))
+print("  versions: %.0f clocks per op, %d quad tasks with corrections" % (out[16] / ops, out[17]))
+print("  version element iterations (lane 0 of each wave): %d combined, %d part-lane" % (out[24], out[25]))
+print("  general rows: terms %.0f, stores %.0f clocks per op, %d row units" % (out[18] / ops, out[22] / ops, out[23]))
 print("kernel: %d workgroups, %.0f clocks each" % (out[7], out[6] / max(1, out[7])))
