@@ -852,7 +852,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint32_t updFromL[kRowSums], updToL[kRowSums];
     __shared__ uint32_t updMaxLast1;   // 1 + the last element any update of the batch folds in (0: none)
     // the version corrections of the batch's first kVersionRows rows (this
-    // tile, dword layout), computed lane by lane in phase A
+    // tile, dword layout), computed per lane sum in phase A
     __shared__ uint32_t corrL[kVersionRows][2][64];
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
@@ -1065,9 +1065,21 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             // parallel, two rows per wave (lanes 32h.. take row 2i+h), and
             // their reference source bytes counted; a row with a draw outside
             // the staged window keeps reading memory (phase B1b).
-            const uint32_t Q = U == 0 ? 1u : (U >= kExecWaves ? 1u : kExecWaves / U);
+            //
+            // Version corrections (rows [0, Rv)): quad g of version task t
+            // takes lane sum 4t + g for every row; the sums of a row meet in
+            // corrL.
+            // Units x < vTasks are version tasks, then the update parts, then
+            // the row pairs.  Fewer than 16 version tasks own a wave each (the
+            // longest units, started first); the other waves share the rest.
+            const uint32_t vTasks = Rv ? kRowSums / 4 : 0u;
+            const uint32_t vWaves = vTasks < kExecWaves ? vTasks : 0u;
+            const uint32_t W2 = kExecWaves - vWaves;
+            const uint32_t Q = U == 0 ? 1u : (U >= W2 ? 1u : W2 / U);
             const uint32_t uUnits = U * Q;
             const uint32_t nPairs = sumsStaged ? (planned + 1) / 2 : 0u;
+            const uint32_t nUnits = vTasks + uUnits + nPairs;
+            auto unit_wave = [&](uint32_t x) { return vWaves ? (x < vWaves ? x : vWaves + (x - vWaves) % W2) : x % kExecWaves; };
             // the update this wave stores: its dst as kept, fetched now
             uint64_t sdst = 0;
             uint32_t sn = 0, svalid = 0, scur = 0;
@@ -1101,7 +1113,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             incl += t;
                     }
                     const uint32_t offs = carry + incl - size;
-                    if (r < planned && (uUnits + (r >> 1)) % kExecWaves == wave) {
+                    if (r < planned && unit_wave(vTasks + uUnits + (r >> 1)) == wave) {
                         const bool fits = offs + size <= kPlanCap;
                         rowInfo[r] = make_uint2(fits ? offs : kNoPlan, n01);
                         if (!fits)
@@ -1111,46 +1123,77 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 }
             }
             const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
-            if (tid == 0) {
+            if (wave == kExecWaves - 1) {
                 // rows whose cutoff is past every update's last element read
                 // the final sums as they are (no version corrections)
                 uint32_t m = 0;
-                for (uint32_t k = 0; k < kRowSums; ++k)
-                    if (updOfL[k] != 0xffu) {
-                        const uint32_t f = updFromL[k], t = updToL[k];
-                        m = max(m, f + ((t - f - 1) / kLanes) * kLanes + 1);
-                    }
-                updMaxLast1 = m;
+                if (lane < kRowSums && updOfL[lane] != 0xffu) {
+                    const uint32_t f = updFromL[lane], t = updToL[lane];
+                    m = f + ((t - f - 1) / kLanes) * kLanes + 1;
+                }
+#pragma unroll
+                for (unsigned d = 16; d >= 1; d >>= 1)
+                    m = max(m, (uint32_t)__shfl_xor(m, d, 64));
+                if (lane == 0)
+                    updMaxLast1 = m;
             }
-            const uint32_t vTasks = Rv * kLanes / 4;   // (row, lane) units, four per wave task
-            for (uint32_t unit = wave; unit < uUnits + nPairs + vTasks; unit += kExecWaves) {
-                if (unit >= uUnits + nPairs) {
-                    // version corrections: quad g takes (row, lane) unit
-                    // 4*task + g; the lanes of a row meet in corrL
-                    const uint32_t v = 4 * (unit - uUnits - nPairs) + g;
-                    const uint32_t r = v / kLanes, l = v % kLanes;
+            PHASE_MARK(30, tclk);
+            const uint32_t xStep = vWaves ? (wave < vWaves ? nUnits : W2) : kExecWaves;
+            for (uint32_t x = vWaves && wave >= vWaves ? vTasks + wave - vWaves : wave; x < nUnits; x += xStep) {
+                const uint32_t unit = x - vTasks;   // (update parts, then row pairs)
+                if (x < vTasks) {
+                    [[maybe_unused]] const unsigned long long vclk0 = PHASE_CLK();
+                    // sum k's update elements as suffix sums: rows from the
+                    // last (largest cutoff) down, each adding the elements
+                    // in [its cutoff, the previous row's) and handing the
+                    // suffix to the row if its masks select sum k (the rows'
+                    // cutoffs never decrease: Program::rows_row)
+                    const uint32_t k = 4 * x + g;
+                    const uint32_t sidx = k % kSums;
                     const uint32_t p16 = tileBase + (lane & 15u) * 16u;
-                    const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
-                    const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
-                    const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo);
-                    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
-                    version_lane16(l, w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, tileBase < align16u(w0.z), p16, b4,
-                                   updOfL, updFromL, updToL, cxL, permL, permC, stage, stageLo, staged, tableL, seg,
-                                   blk, a0, a1);
-                    uint32_t* c0 = &corrL[r][0][b4];
-                    uint32_t* c1 = &corrL[r][1][b4];
-                    if (a0.x | a0.y | a0.z | a0.w) {
-                        atomicXor(c0 + 0, a0.x);
-                        atomicXor(c0 + 1, a0.y);
-                        atomicXor(c0 + 2, a0.z);
-                        atomicXor(c0 + 3, a0.w);
+                    const uint32_t f = updFromL[k], t = updToL[k], slen = tableL[k].z;
+                    const bool any = updOfL[k] != 0xffu && t > f && p16 < slen;
+                    uint4 S = make_uint4(0, 0, 0, 0);
+                    uint32_t hiE = t;
+                    for (uint32_t r1 = Rv; r1 > 0; --r1) {
+                        const uint32_t r = r1 - 1;
+                        const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
+                        const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
+                        const uint32_t cut = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo).y;
+                        if (any) {
+                            const uint32_t first = cut <= f ? f : f + ((cut - f + kLanes - 1) / kLanes) * kLanes;
+                            for (uint32_t e = first; e < hiE; e += kLanes) {
+                                uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
+                                if (sidx != 0) {
+                                    const uint32_t cx = cxL[table_entry(tableL, seg, blk, kRowSums + e, stageLo).w %
+                                                            kColumnValuePeriod];
+                                    v = gf_mul16_tab(v, gf_tab_l(permL, permC, sidx == 1 ? (cx & 0xffu) : (cx >> 8)));
+                                }
+                                S = xor16(S, v);
+                            }
+                            hiE = min(hiE, first);
+                        }
+                        const bool in0 = (w1.x >> k) & 1u, in1 = (w1.y >> k) & 1u;
+                        if (any && (in0 || in1) && tileBase < align16u(w0.z) && (S.x | S.y | S.z | S.w)) {
+                            const uint4 V = p16 + 16 > slen ? mask16(S, (int)slen - (int)p16) : S;
+                            if (in0) {
+                                uint32_t* c0 = &corrL[r][0][b4];
+                                atomicXor(c0 + 0, V.x);
+                                atomicXor(c0 + 1, V.y);
+                                atomicXor(c0 + 2, V.z);
+                                atomicXor(c0 + 3, V.w);
+                            }
+                            if (in1) {
+                                uint32_t* c1 = &corrL[r][1][b4];
+                                atomicXor(c1 + 0, V.x);
+                                atomicXor(c1 + 1, V.y);
+                                atomicXor(c1 + 2, V.z);
+                                atomicXor(c1 + 3, V.w);
+                            }
+                        }
                     }
-                    if (a1.x | a1.y | a1.z | a1.w) {
-                        atomicXor(c1 + 0, a1.x);
-                        atomicXor(c1 + 1, a1.y);
-                        atomicXor(c1 + 2, a1.z);
-                        atomicXor(c1 + 3, a1.w);
-                    }
+                    PHASE_ADD(26, PHASE_CLK() - vclk0);
+                    PHASE_ADD(29, 1);
                 } else if (unit < uUnits) {
                     [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
                     const uint32_t u = unit / Q;
@@ -1245,8 +1288,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         if (tileBase == 0)
                             acct_wave(&acctL, refBytes);
                     }
-                    if (wave == 0)
-                        PHASE_ADD(19, PHASE_CLK() - uclk0);
+                    PHASE_ADD(19, PHASE_CLK() - uclk0);
+                    PHASE_ADD(27, 1);
                 } else {
                     [[maybe_unused]] const unsigned long long pclk0 = PHASE_CLK();
                     const uint32_t h = lane >> 5, hl = lane & 31u;
@@ -1318,10 +1361,11 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         rowInfo[r].x = kPlanGeneral;
                         generalRows = 1;
                     }
-                    if (wave == 0)
-                        PHASE_ADD(20, PHASE_CLK() - pclk0);
+                    PHASE_ADD(20, PHASE_CLK() - pclk0);
+                    PHASE_ADD(28, 1);
                 }
             }
+            PHASE_MARK(31, tclk);
             __syncthreads();
             PHASE_MARK(2, tclk);
 

@@ -30,5 +30,8 @@ print("  rows detail (wave 0 quad tasks): descriptors %.0f, terms %.0f, stores %
       % (out[13] / ops, out[14] / ops, out[15] / ops))
 print("  versions: %.0f clocks per op, %d quad tasks with corrections" % (out[16] / ops, out[17]))
 print("  version element iterations (lane 0 of each wave): %d combined, %d part-lane" % (out[24], out[25]))
+print("  phase A on wave 0: before units %.0f, units %.0f, barrier %.0f clocks per op" % (out[30] / ops, out[31] / ops, out[2] / ops))
+print("  phase A units (all waves): updates %d x %.0f clocks, plans %d x %.0f, versions %d x %.0f"
+      % (out[27], out[19] / max(1, out[27]), out[28], out[20] / max(1, out[28]), out[29], out[26] / max(1, out[29])))
 print("  general rows: terms %.0f, stores %.0f clocks per op, %d row units" % (out[18] / ops, out[22] / ops, out[23]))
 print("kernel: %d workgroups, %.0f clocks each" % (out[7], out[6] / max(1, out[7])))
