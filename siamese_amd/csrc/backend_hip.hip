@@ -512,11 +512,26 @@ __device__ __forceinline__ uint64_t pcg_jump(uint64_t s, uint64_t inc, uint32_t 
 // Sum or window descriptor i of the current OP_ROWS batch (per lane)
 // (LDS slot j holds block word j < kRowSums, else word j + skip: window
 // entries below the batch's stageLo, which only k_ldpc reads, stay in memory)
+// (LDS slot j holds block word j < kRowSums, else word j + skip: window
+// entries below the batch's stageLo, which only k_ldpc reads, stay in memory.
+// table_entry: a word past the window (updates, rows); win_entry: window
+// element e; table_word: any word)
 __device__ __forceinline__ uint4 table_entry(const uint4* tableL, const uint4* __restrict__ seg,
                                              uint32_t blockWord, uint32_t i, uint32_t skip)
 {
-    const uint32_t j = i < kRowSums ? i : i - kRowSums >= skip ? i - skip : kRowsTableLds;
+    const uint32_t j = i - skip;
     return j < kRowsTableLds ? tableL[j] : ld16((uint64_t)(seg + blockWord + i));
+}
+__device__ __forceinline__ uint4 win_entry(const uint4* tableL, const uint4* __restrict__ seg, uint32_t blockWord,
+                                           uint32_t e, uint32_t skip)
+{
+    const uint32_t j = e - skip;   // (wraps for e < skip)
+    return j < kRowsTableLds - kRowSums ? tableL[kRowSums + j] : ld16((uint64_t)(seg + blockWord + kRowSums + e));
+}
+__device__ __forceinline__ uint4 table_word(const uint4* tableL, const uint4* __restrict__ seg, uint32_t blockWord,
+                                            uint32_t i, uint32_t skip)
+{
+    return i < kRowSums ? tableL[i] : win_entry(tableL, seg, blockWord, i - kRowSums, skip);
 }
 
 // One Siamese row's LDPC picks [d0, d1) of PCG.Seed(row, N) (pair index
@@ -539,7 +554,7 @@ __device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t
         // lane j: draw c + j -> window element e and its descriptor
         const uint64_t st = pcgA * sc + inc * pcgG;
         const uint32_t e = off + pcg_output(st) % N;
-        const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
+        const uint4 ev = win_entry(tableL, seg, blk, e, stageLo);
         sc = c_pcgA[64] * sc + inc * c_pcgG[64];
         const uint32_t cnt = d1 - c < 64 ? d1 - c : 64;
         for (uint32_t j0 = 0; j0 < cnt; j0 += kExecDepth) {
@@ -675,7 +690,7 @@ __device__ __forceinline__ uint4 version_elem16(uint32_t e, uint32_t p16, uint32
 {
     if (e - stageLo < staged)
         return lds16(stage, (kRowSums + e - stageLo) * 64 + b4);
-    const uint4 d = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
+    const uint4 d = win_entry(tableL, seg, blk, e, stageLo);
     const uint64_t src = ((uint64_t)d.y << 32) | d.x;
     return p16 < d.z ? ld16(src + p16) : make_uint4(0, 0, 0, 0);
 }
@@ -730,7 +745,7 @@ __device__ __forceinline__ void version_lane16(uint32_t l, uint32_t m0, uint32_t
             for (uint32_t s = 0; s < kSums; ++s)
                 need |= (full >> s & 1u) && s != 0 && e >= f[s] && e < t[s];
             if (need) {
-                const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e, stageLo).w;
+                const uint32_t col = win_entry(tableL, seg, blk, e, stageLo).w;
                 cx = cxL[col % kColumnValuePeriod];
             }
 #pragma unroll
@@ -763,7 +778,7 @@ __device__ __forceinline__ void version_lane16(uint32_t l, uint32_t m0, uint32_t
                 PHASE_ADD(25, 1);
                 uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
                 if (s != 0) {
-                    const uint32_t col = table_entry(tableL, seg, blk, kRowSums + e, stageLo).w;
+                    const uint32_t col = win_entry(tableL, seg, blk, e, stageLo).w;
                     const uint32_t cx = cxL[col % kColumnValuePeriod];
                     v = gf_mul16_tab(v, gf_tab_l(permL, permC, s == 1 ? (cx & 0xffu) : (cx >> 8)));
                 }
@@ -811,7 +826,7 @@ __device__ __forceinline__ void row_versions4(uint32_t m0, uint32_t m1, uint32_t
         for (uint32_t e = cut <= from ? from : from + ((cut - from + kLanes - 1) / kLanes) * kLanes; e < to;
              e += kLanes) {
             uint32_t v;
-            const uint4 d = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
+            const uint4 d = win_entry(tableL, seg, blk, e, stageLo);
             if (e - stageLo < staged) {
                 v = stage[(kRowSums + e - stageLo) * 64 + lane];
             } else {
@@ -853,7 +868,11 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint32_t updMaxLast1;   // 1 + the last element any update of the batch folds in (0: none)
     // the version corrections of the batch's first kVersionRows rows (this
     // tile, dword layout), computed per lane sum in phase A
+#ifdef SGPU_NO_CORR
+    __shared__ uint32_t corrL[1][2][64];
+#else
     __shared__ uint32_t corrL[kVersionRows][2][64];
+#endif
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
@@ -1014,7 +1033,11 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 updAcc[i] = 0;
             // rows [0, Rv) of a versioned batch (GfOp.dst high word, ops.h)
             // take their corrections from corrL
+#ifdef SGPU_NO_CORR
+            const uint32_t Rv = 0;
+#else
             const uint32_t Rv = min(min(uni(h0.y), R), (uint32_t)kVersionRows);
+#endif
             for (uint32_t i = tid; i < Rv * 128; i += kExecThreads)
                 (&corrL[0][0][0])[i] = 0;
             if (tid == 0)
@@ -1028,7 +1051,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         const uint32_t x = x0 + u * kPass;
                         v[u] = make_uint4(0, 0, 0, 0);
                         if (x < entries) {
-                            const uint4 d = table_entry(tableL, seg, blk, x < kRowSums ? x : x + stageLo, stageLo);
+                            const uint4 d = table_word(tableL, seg, blk, x < kRowSums ? x : x + stageLo, stageLo);
                             const uint64_t src = ((uint64_t)d.y << 32) | d.x;
                             if (tileBase + q16 < d.z)
                                 v[u] = ld16(src + tileBase + q16);
@@ -1165,7 +1188,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             for (uint32_t e = first; e < hiE; e += kLanes) {
                                 uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
                                 if (sidx != 0) {
-                                    const uint32_t cx = cxL[table_entry(tableL, seg, blk, kRowSums + e, stageLo).w %
+                                    const uint32_t cx = cxL[win_entry(tableL, seg, blk, e, stageLo).w %
                                                             kColumnValuePeriod];
                                     v = gf_mul16_tab(v, gf_tab_l(permL, permC, sidx == 1 ? (cx & 0xffu) : (cx >> 8)));
                                 }
@@ -1217,7 +1240,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                     const uint32_t k = kk + 4 * j + g;
                                     const bool act = k < k1;
                                     const uint32_t e = from + (act ? k : k0) * kLanes;
-                                    const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
+                                    const uint4 ev = win_entry(tableL, seg, blk, e, stageLo);
                                     if (act && (lane & 15u) == 0)
                                         refBytes += ev.z;
                                     slot[j] = act ? kRowSums + e - stageLo : zeroSlot;
@@ -1243,7 +1266,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             uint32_t acc = 0;
                             for (uint32_t c = k0; c < k1; c += 64) {
                                 const uint32_t e = from + (c + lane) * kLanes;
-                                const uint4 ev = c + lane < k1 ? table_entry(tableL, seg, blk, kRowSums + e, stageLo)
+                                const uint4 ev = c + lane < k1 ? win_entry(tableL, seg, blk, e, stageLo)
                                                                : make_uint4(0, 0, 0, 0);
                                 const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
                                 const GfTab tab = gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8));
@@ -1346,7 +1369,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                 rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
                                 e = woff + (uint32_t)rr;
                             }
-                            const uint32_t len = table_entry(tableL, seg, blk, kRowSums + e, stageLo).z;
+                            const uint32_t len = win_entry(tableL, seg, blk, e, stageLo).z;
                             if (!wide)
                                 refBytes += len < rn ? len : rn;
                             general |= e - stageLo >= staged;
@@ -1581,7 +1604,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             if (e - stageLo < staged) {
                                 v = stage[(kRowSums + e - stageLo) * 64 + lane];
                             } else {
-                                const uint4 ev = table_entry(tableL, seg, blk, kRowSums + e, stageLo);
+                                const uint4 ev = win_entry(tableL, seg, blk, e, stageLo);
                                 const uint64_t src = ((uint64_t)uni(ev.y) << 32) | uni(ev.x);
                                 const uint32_t len = uni(ev.z);
                                 if (tileBase < len)
