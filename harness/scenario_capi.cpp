@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <thread>
 
 namespace {
@@ -80,12 +81,27 @@ struct Pkt
 
 using Clock = std::chrono::steady_clock;
 
+// per call kind: count and seconds (SCENARIO_CAPI_CALLS=1 prints them per
+// stream range on stderr; profiling aid)
+enum CallKind { kCreate, kEncAdd, kEncode, kDecAddOrig, kDecAddRec, kIsReady, kDecode, kDecGet, kRemove, kFree, kKinds };
+const char* const kCallNames[kKinds] = {"create", "enc_add", "encode", "dec_add_orig", "dec_add_rec",
+                                        "is_ready", "decode", "dec_get", "remove_before", "free"};
+
 struct Timer
 {
     double& acc;
+    double* kind;
     Clock::time_point t0;
-    explicit Timer(double& a) : acc(a), t0(Clock::now()) {}
-    ~Timer() { acc += std::chrono::duration<double>(Clock::now() - t0).count(); }
+    explicit Timer(double& a, double* k = nullptr) : acc(a), kind(k), t0(Clock::now()) {}
+    ~Timer()
+    {
+        const double d = std::chrono::duration<double>(Clock::now() - t0).count();
+        acc += d;
+        if (kind) {
+            kind[0] += 1;
+            kind[1] += d;
+        }
+    }
 };
 
 struct CapiCodec
@@ -96,6 +112,7 @@ struct CapiCodec
     SiameseDecoder dec = nullptr;
     std::vector<uint8_t> expect;
     double seconds = 0;
+    double calls[kKinds][2] = {};
 
     bool needs_host_payload() const { return true; }
 
@@ -107,7 +124,7 @@ struct CapiCodec
         p.DataBytes = bytes;
         int r;
         {
-            Timer t(seconds);
+            Timer t(seconds, calls[kEncAdd]);
             r = api->encoder_add(enc, &p);
         }
         *num = p.PacketNum;
@@ -118,7 +135,7 @@ struct CapiCodec
         SiameseRecoveryPacket r{};
         int res;
         {
-            Timer t(seconds);
+            Timer t(seconds, calls[kEncode]);
             res = api->encode(enc, &r);
         }
         rec->bytes = r.DataBytes;
@@ -131,7 +148,7 @@ struct CapiCodec
         p.PacketNum = num;
         p.Data = data;
         p.DataBytes = bytes;
-        Timer t(seconds);
+        Timer t(seconds, calls[kDecAddOrig]);
         return api->decoder_add_original(dec, &p);
     }
     int dec_add_recovery(const Rec& rec)
@@ -139,12 +156,12 @@ struct CapiCodec
         SiameseRecoveryPacket r;
         r.Data = rec.data;
         r.DataBytes = rec.bytes;
-        Timer t(seconds);
+        Timer t(seconds, calls[kDecAddRec]);
         return api->decoder_add_recovery(dec, &r);
     }
     int is_ready()
     {
-        Timer t(seconds);
+        Timer t(seconds, calls[kIsReady]);
         return api->decoder_is_ready(dec);
     }
     int decode(std::vector<Pkt>* out)
@@ -153,7 +170,7 @@ struct CapiCodec
         unsigned count = 0;
         int r;
         {
-            Timer t(seconds);
+            Timer t(seconds, calls[kDecode]);
             r = api->decode(dec, &pkts, &count);
         }
         if (r == 0)
@@ -169,7 +186,7 @@ struct CapiCodec
         p.DataBytes = 0;
         int r;
         {
-            Timer t(seconds);
+            Timer t(seconds, calls[kDecGet]);
             r = api->decoder_get(dec, &p);
         }
         out->num = num;
@@ -179,7 +196,7 @@ struct CapiCodec
     }
     int enc_remove_before(unsigned num)
     {
-        Timer t(seconds);
+        Timer t(seconds, calls[kRemove]);
         return api->encoder_remove_before(enc, num);
     }
     uint64_t rec_token(const Rec& rec) { return scen::data_token(cfg->hash_data, rec.data, rec.bytes); }
@@ -206,7 +223,7 @@ void run_range(const CApi* api, const ScenarioConfig* cfg, StreamResult* results
         codec.api = api;
         codec.cfg = cfg;
         {
-            Timer t(codec.seconds);
+            Timer t(codec.seconds, codec.calls[kCreate]);
             codec.enc = api->encoder_create();
             codec.dec = api->decoder_create();
         }
@@ -218,7 +235,7 @@ void run_range(const CApi* api, const ScenarioConfig* cfg, StreamResult* results
             st.step();
         st.finish();
         {
-            Timer t(codec.seconds);
+            Timer t(codec.seconds, codec.calls[kFree]);
             api->encoder_free(codec.enc);
             api->decoder_free(codec.dec);
         }
@@ -227,6 +244,12 @@ void run_range(const CApi* api, const ScenarioConfig* cfg, StreamResult* results
                 std::fprintf(log, "%016llx\n", (unsigned long long)e);
         }
         *seconds += codec.seconds;
+        static const bool printCalls = std::getenv("SCENARIO_CAPI_CALLS") != nullptr;
+        if (printCalls)
+            for (unsigned k = 0; k < kKinds; ++k)
+                if (codec.calls[k][0] > 0)
+                    std::fprintf(stderr, "capi %-14s %6.0f calls %9.1f us  %7.2f us/call\n", kCallNames[k],
+                                 codec.calls[k][0], codec.calls[k][1] * 1e6, codec.calls[k][1] * 1e6 / codec.calls[k][0]);
     }
 }
 

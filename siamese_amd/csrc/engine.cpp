@@ -1144,10 +1144,8 @@ void Engine::stop_threads()
         completer_.join();
 }
 
-uint64_t Engine::enqueue()
+Batch* Engine::take_batch()
 {
-    if (failed())
-        return 0;
     std::vector<Shard*> shards;
     {
         std::lock_guard<std::mutex> g(shardsMu_);
@@ -1189,7 +1187,7 @@ uint64_t Engine::enqueue()
         }
     }
     if (!b)
-        return nextTicket_;   // nothing queued: the latest submission covers everything
+        return nullptr;
     const uint64_t ticket = ++nextTicket_;
     tl("enqueue", ticket);
     b->ticket = ticket;
@@ -1198,17 +1196,35 @@ uint64_t Engine::enqueue()
         std::lock_guard<std::mutex> g(qMu_);
         b->marks.swap(pendingMarks_);
     }
+    return b;
+}
+
+namespace {
+bool async_assembly()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("SIAMESE_AMD_ASYNC_ASSEMBLY");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
+} // namespace
+
+uint64_t Engine::enqueue()
+{
+    if (failed())
+        return 0;
+    Batch* b = take_batch();
+    if (!b)
+        return nextTicket_;   // nothing queued: the latest submission covers everything
+    const uint64_t ticket = b->ticket;
     // The batch is laid out here, on the caller's thread and the shared
     // pool.  SIAMESE_AMD_ASYNC_ASSEMBLY=1 hands it to the launcher thread and
     // its own pool instead, so the caller goes back to driving instances at
     // once; on the MI355X box's 16-core host share that only moved the same
     // CPU work beside the stepping threads (same-box A/B), so
     // it is off by default.
-    static const bool asyncAssembly = [] {
-        const char* v = std::getenv("SIAMESE_AMD_ASYNC_ASSEMBLY");
-        return v && std::atoi(v) != 0;
-    }();
-    if (!asyncAssembly) {
+    if (!async_assembly()) {
         claim_set(*b);
         assemble_batch(*b, pool());
         tl("assembled", ticket);
@@ -1244,6 +1260,63 @@ bool Engine::wait(uint64_t ticket)
     return !failed();
 }
 
+bool Engine::flush_and_sync()
+{
+    if (failed())
+        return false;
+    Batch* b = take_batch();
+    if (!b)
+        return wait(nextTicket_) && nextTicket_ != 0;
+    const uint64_t ticket = b->ticket;
+    // SIAMESE_AMD_INLINE_SYNC=0 always hands the submission to the threads
+    static const bool kInline = [] {
+        const char* v = std::getenv("SIAMESE_AMD_INLINE_SYNC");
+        return !v || std::atoi(v) != 0;
+    }();
+    bool inl = false;
+    if (kInline && !async_assembly()) {
+        std::lock_guard<std::mutex> g(qMu_);
+        if (toLaunch_.empty() && toComplete_.empty() && !launching_ && !completing_ && !inlineBusy_ &&
+            doneTicket_ + 1 == ticket) {
+            inlineBusy_ = true;   // (the launcher waits: its stream order stays ticket order)
+            inl = true;
+        }
+    }
+    if (!inl) {
+        if (!async_assembly()) {
+            claim_set(*b);
+            assemble_batch(*b, pool());
+        }
+        {
+            std::lock_guard<std::mutex> g(qMu_);
+            toLaunch_.push_back(b);
+            queuedSeen_.fetch_add(1, std::memory_order_release);
+        }
+        launchCv_.notify_one();
+        return wait(ticket) && !failed();
+    }
+    tl("inline", ticket);
+    claim_set(*b);
+    assemble_batch(*b, pool());
+    if (!failed())
+        launch_batch(*b);
+    if (complete_batch(*b))
+        reclaim_batch(*b);
+    {
+        std::lock_guard<std::mutex> g(qMu_);
+        if (sets_[b->set].busyTicket == b->ticket)
+            sets_[b->set].busyTicket = 0;
+        doneTicket_ = b->ticket;
+        doneSeen_.store(b->ticket, std::memory_order_release);
+        inlineBusy_ = false;
+    }
+    setCv_.notify_all();
+    doneCv_.notify_all();
+    launchCv_.notify_one();
+    delete b;
+    return !failed();
+}
+
 bool Engine::flush()
 {
     const uint64_t prev = nextTicket_;
@@ -1264,12 +1337,13 @@ void Engine::launcher_loop()
         }
         {
             std::unique_lock<std::mutex> lk(qMu_);
-            launchCv_.wait(lk, [&] { return stop_ || !toLaunch_.empty(); });
+            launchCv_.wait(lk, [&] { return stop_ || (!toLaunch_.empty() && !inlineBusy_); });
             if (stop_)
                 return;
             b = toLaunch_.front();
             toLaunch_.pop_front();
             ++taken;
+            launching_ = true;
         }
         if (!b->assembled && !failed()) {
             claim_set(*b);
@@ -1283,6 +1357,7 @@ void Engine::launcher_loop()
         {
             std::lock_guard<std::mutex> g(qMu_);
             toComplete_.push_back(b);
+            launching_ = false;
         }
         completeCv_.notify_one();
     }
@@ -1727,6 +1802,7 @@ void Engine::completer_loop()
                 return;
             b = toComplete_.front();
             toComplete_.pop_front();
+            completing_ = true;
         }
         tl("complete begin", b->ticket);
         // (released buffers go back to the depot tagged with the ticket:
@@ -1751,6 +1827,7 @@ void Engine::completer_loop()
                 sets_[b->set].busyTicket = 0;
             doneTicket_ = b->ticket;
             doneSeen_.store(b->ticket, std::memory_order_release);
+            completing_ = false;
         }
         setCv_.notify_all();
         doneCv_.notify_all();

@@ -327,11 +327,11 @@ public:
     bool flush();
     /// Complete every submission.
     bool sync() { return wait(nextTicket_); }
-    bool flush_and_sync()
-    {
-        const uint64_t t = enqueue();
-        return wait(t) && t != 0;
-    }
+    /// Submit everything queued and wait for it.  With nothing in flight
+    /// the caller's thread runs the submission itself (assembly, launches,
+    /// fence poll, completion): no hand-off to the launcher and completer
+    /// threads, the drop-in siamese.h path's per-call latency.
+    bool flush_and_sync();
     /// A device operation failed; the engine accepts no further work.
     bool failed() const { return failed_.load(std::memory_order_relaxed); }
     bool pending() const;
@@ -390,6 +390,7 @@ private:
     void launcher_loop();
     void completer_loop();
     void assemble_batch(Batch& b, WorkerPool& wp);
+    Batch* take_batch();   // queued programs and queues as a batch with its ticket (nullptr: none)
     void claim_set(Batch& b);
     WorkerPool& asm_pool();   // launcher thread only
     void launch_batch(Batch& b);
@@ -445,6 +446,9 @@ private:
     std::atomic<uint64_t> doneSeen_{0};             // doneTicket_
     std::atomic<uint64_t> queuedSeen_{0};           // batches pushed to toLaunch_
     bool stop_ = false;
+    bool launching_ = false;                        // the launcher holds a batch (qMu_)
+    bool completing_ = false;                       // the completer holds a batch (qMu_)
+    bool inlineBusy_ = false;                       // a caller runs a submission itself (qMu_)
     std::thread launcher_, completer_;
     std::unique_ptr<WorkerPool> pool_;
     std::unique_ptr<WorkerPool> asmPool_;
