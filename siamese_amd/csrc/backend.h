@@ -18,12 +18,26 @@ const char* be_name();
 void* be_dev_alloc(size_t bytes);
 void be_dev_free(void* p);
 void* be_host_alloc(size_t bytes);   // page-locked
+/// The device's address of page-locked host memory (kernels read it over
+/// the bus: zero-copy).
+void* be_host_device_ptr(void* host);
 void be_host_free(void* p);
 
 // All transfers and launches are asynchronous on the engine's stream.
 void be_h2d(void* dst, const void* src, size_t bytes);
 void be_d2h(void* dst, const void* src, size_t bytes);
 void be_memset(void* dst, int value, size_t bytes);
+/// Copies between device memory and page-locked host memory (be_host_alloc):
+/// small totals run as one kernel on the engine's stream (no copy-engine
+/// hand-off, whose cross-queue wait costs more than the bytes on the
+/// latency-bound single-stream path), large ones as DMA.
+struct BeCopy
+{
+    uint64_t dst, src;
+    uint64_t bytes;
+};
+constexpr unsigned kBeCopyMax = 8;   // ranges per be_copy_pinned call
+void be_copy_pinned(const BeCopy* ranges, unsigned count, bool toDevice);
 
 /// One wave per (descriptor, kIngestChunkBytes chunk): maxBytes is the
 /// largest hdrLen + bytes among the descriptors (sizes the grid).

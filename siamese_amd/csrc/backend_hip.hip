@@ -2600,6 +2600,13 @@ void* be_host_alloc(size_t bytes)
     return p;
 }
 
+void* be_host_device_ptr(void* host)
+{
+    bind_device();
+    void* d = nullptr;
+    return hipHostGetDevicePointer(&d, host, 0) == hipSuccess ? d : nullptr;
+}
+
 void be_host_free(void* p)
 {
     bind_device();
@@ -2617,6 +2624,64 @@ void be_d2h(void* dst, const void* src, size_t bytes)
 {
     bind_device();
     check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, g_stream), "D2H");
+}
+
+namespace {
+constexpr uint64_t kKernelCopyMax = 256u << 10;   // total bytes a be_copy_pinned kernel moves at most
+constexpr unsigned kHostCopyThreads = 256;
+struct HostCopyArgs
+{
+    BeCopy r[kBeCopyMax];
+    uint32_t count;
+};
+} // namespace
+
+// Pinned host <-> device copies as a kernel (be_copy_pinned): blockIdx.y is
+// the range, each thread moves 16-byte words (bytes at the unaligned ends);
+// host memory is page-locked and mapped, written with ordinary stores.
+__global__ __launch_bounds__(kHostCopyThreads) void k_hostcopy(HostCopyArgs a)
+{
+    const BeCopy& c = a.r[blockIdx.y];
+    uint8_t* dst = reinterpret_cast<uint8_t*>(c.dst);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(c.src);
+    const uint64_t n = c.bytes;
+    const bool aligned = ((c.dst | c.src) & 15u) == 0;
+    const uint64_t words = aligned ? n / 16 : 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kHostCopyThreads + threadIdx.x; i < words;
+         i += (uint64_t)gridDim.x * kHostCopyThreads)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (uint64_t i = words * 16 + (uint64_t)blockIdx.x * kHostCopyThreads + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kHostCopyThreads)
+        dst[i] = src[i];
+}
+
+void be_copy_pinned(const BeCopy* ranges, unsigned count, bool toDevice)
+{
+    bind_device();
+    uint64_t total = 0, most = 0;
+    for (unsigned i = 0; i < count; ++i) {
+        total += ranges[i].bytes;
+        most = std::max<uint64_t>(most, ranges[i].bytes);
+    }
+    if (count == 0 || total == 0)
+        return;
+    if (count > kBeCopyMax || total > kKernelCopyMax) {
+        for (unsigned i = 0; i < count; ++i)
+            if (ranges[i].bytes)
+                check(hipMemcpyAsync((void*)(uintptr_t)ranges[i].dst, (const void*)(uintptr_t)ranges[i].src,
+                                     ranges[i].bytes, toDevice ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost,
+                                     g_stream),
+                      toDevice ? "H2D" : "D2H");
+        return;
+    }
+    HostCopyArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (unsigned i = 0; i < count; ++i)
+        a.r[i] = ranges[i];
+    a.count = count;
+    const uint64_t perBlock = (uint64_t)kHostCopyThreads * 16u * 4u;   // four words per thread
+    const unsigned blocks = (unsigned)std::min<uint64_t>(64, (most + perBlock - 1) / perBlock);
+    hipLaunchKernelGGL(k_hostcopy, dim3(std::max(1u, blocks), count), dim3(kHostCopyThreads), 0, g_stream, a);
 }
 
 void be_memset(void* dst, int value, size_t bytes)

@@ -986,6 +986,7 @@ void Engine::ensure_up(XferSet& x, size_t bytes)
         be_dev_free(x.upDev);
     x.upHost = (uint8_t*)be_host_alloc(cap);
     x.upDev = (uint8_t*)be_dev_alloc(cap);
+    x.upHostDev = x.upHost ? (uint8_t*)be_host_device_ptr(x.upHost) : nullptr;
     x.upCap = cap;
 }
 
@@ -1070,6 +1071,8 @@ struct Batch
     bool wideZero = false;                 // the ring wrapped: zero it before the first exec launch
     uint32_t resultWords = 0;
     std::vector<const Shard::Download*> dls;
+    std::vector<BeCopy> copies;         // D2H ranges of launch_batch (scratch)
+    uint8_t* upBase = nullptr;          // where the kernels read the upload: the set's device copy, or zero-copy
     EngineStats st;
     // launcher -> completer
     void* fence = nullptr;
@@ -1598,6 +1601,15 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     }
     if (bt.upBytes)
         ensure_up(xs, bt.upBytes);
+    // A small upload is not copied: the kernels read it from the pinned
+    // buffer over the bus (zero-copy), which skips a copy and its hand-off
+    // on the latency-bound paths (SIAMESE_AMD_ZEROCOPY_UP bytes at most,
+    // default 32 KiB; 0 disables).
+    static const size_t kZeroCopyUp = [] {
+        const char* v = std::getenv("SIAMESE_AMD_ZEROCOPY_UP");
+        return v ? (size_t)std::atol(v) : (size_t)32768;
+    }();
+    bt.upBase = (xs.upHostDev && bt.upBytes <= kZeroCopyUp) ? xs.upHostDev : xs.upDev;
     if (wideBytes) {
         // k_ldpc scratch comes from the set's ring, which is zeroed as a whole
         // when it wraps (not per submission: most flushes then need no memset)
@@ -1612,7 +1624,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
 
     // ---- 3. copy into the pinned upload buffer -------------------------------
     uint8_t* up = xs.upHost;
-    const uint64_t stageDev = (uint64_t)(uintptr_t)(xs.upDev + oStage);
+    const uint64_t stageDev = (uint64_t)(uintptr_t)(bt.upBase + oStage);
     constexpr size_t kSegChunk = SGPU_SEG_CHUNK;
     constexpr size_t kIngestChunk = SGPU_INGEST_CHUNK;
     constexpr size_t kSolveChunk = SGPU_SOLVE_CHUNK;
@@ -1648,7 +1660,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                         std::memcpy(w, s.rowsData.data() + (size_t)op.termBegin * 16, bytes);
                         // wide rows of this batch: their scratch pair as the
                         // appended window entries, and their k_ldpc items
-                        const uint64_t winDev = (uint64_t)(uintptr_t)(xs.upDev + (w - up)) + kRowSums * 16;
+                        const uint64_t winDev = (uint64_t)(uintptr_t)(bt.upBase + (w - up)) + kRowSums * 16;
                         for (; wi < s.wide.size() && s.wide[wi].op == oi; ++wi) {
                             const ProgramBody::Segment::Wide& x = s.wide[wi];
                             const uint32_t span = (x.n + kLdpcTileBytes - 1) / kLdpcTileBytes * kLdpcTileBytes;
@@ -1745,10 +1757,12 @@ void Engine::launch_batch(Batch& bt)
         be_mark_release(m);
     }
     bt.marks.clear();
-    if (bt.upBytes)
-        be_h2d(xs.upDev, xs.upHost, bt.upBytes);
+    if (bt.upBytes && bt.upBase == xs.upDev) {
+        const BeCopy up{(uint64_t)(uintptr_t)xs.upDev, (uint64_t)(uintptr_t)xs.upHost, bt.upBytes};
+        be_copy_pinned(&up, 1, true);
+    }
     if (bt.nIngest)
-        be_launch_ingest((const IngestDesc*)(xs.upDev + bt.oIngD), (uint32_t)bt.nIngest, bt.maxIngest);
+        be_launch_ingest((const IngestDesc*)(bt.upBase + bt.oIngD), (uint32_t)bt.nIngest, bt.maxIngest);
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
     if (xs.acctZero) {
@@ -1764,27 +1778,35 @@ void Engine::launch_batch(Batch& bt)
     for (size_t k = 0; k < bt.phases.size() && bt.phases[k].kind == Phase::EXEC; ++k)
         wideDone = bt.phases[k].wideBegin + bt.phases[k].wideCount;
     if (wideDone)
-        be_launch_ldpc((const LdpcItem*)(xs.upDev + bt.oWide), (uint32_t)wideDone, acctDev);
+        be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide), (uint32_t)wideDone, acctDev);
     for (const Phase& ph : bt.phases) {
         if (ph.kind == Phase::EXEC) {
             if (ph.wideCount && ph.wideBegin >= wideDone)
-                be_launch_ldpc((const LdpcItem*)(xs.upDev + bt.oWide) + ph.wideBegin, (uint32_t)ph.wideCount,
+                be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide) + ph.wideBegin, (uint32_t)ph.wideCount,
                                acctDev);
-            be_launch_exec(xs.upDev + bt.oStream, (const ExecItem*)(xs.upDev + bt.oItems) + ph.itemBegin,
+            be_launch_exec(bt.upBase + bt.oStream, (const ExecItem*)(bt.upBase + bt.oItems) + ph.itemBegin,
                            (uint32_t)ph.itemCount, acctDev, ph.maxRows);
             st.execLaunches++;
         } else {
             // solve items index solves globally; pass the global desc base
-            be_launch_solve((const SolveDesc*)(xs.upDev + bt.oSD), (const SolveRow*)(xs.upDev + bt.oSR),
-                            xs.upDev + bt.oCoef, resultsDev, (const SolveItem*)(xs.upDev + bt.oSI) + ph.itemBegin,
+            be_launch_solve((const SolveDesc*)(bt.upBase + bt.oSD), (const SolveRow*)(bt.upBase + bt.oSR),
+                            bt.upBase + bt.oCoef, resultsDev, (const SolveItem*)(bt.upBase + bt.oSI) + ph.itemBegin,
                             (uint32_t)ph.itemCount, ph.maxRows, acctDev + 1, (uint32_t)ph.solveBegin,
                             (uint32_t)ph.solveCount);
         }
     }
-    be_d2h(xs.downHost, xs.downDev, kAcctBytes + (size_t)bt.resultWords * 4);
-    for (size_t i = 0; i < bt.dls.size(); ++i)
-        be_d2h(xs.downHost + bt.downloads[i].off, (const void*)(uintptr_t)bt.dls[i]->dev,
-               bt.dls[i]->bytes);
+    {
+        // the counters and solve results, then the downloads, in one call
+        // (one kernel when small: be_copy_pinned)
+        std::vector<BeCopy>& cp = bt.copies;
+        cp.clear();
+        cp.push_back(BeCopy{(uint64_t)(uintptr_t)xs.downHost, (uint64_t)(uintptr_t)xs.downDev,
+                            kAcctBytes + (uint64_t)bt.resultWords * 4});
+        for (size_t i = 0; i < bt.dls.size(); ++i)
+            cp.push_back(BeCopy{(uint64_t)(uintptr_t)(xs.downHost + bt.downloads[i].off), bt.dls[i]->dev,
+                                bt.dls[i]->bytes});
+        be_copy_pinned(cp.data(), (unsigned)cp.size(), false);
+    }
     bt.fence = be_fence();
     bt.launched = true;
     std::lock_guard<std::mutex> g(statsMu_);

@@ -459,6 +459,7 @@ private:
     {
         uint8_t* upHost = nullptr;
         uint8_t* upDev = nullptr;
+        uint8_t* upHostDev = nullptr;   // upHost as the device addresses it (zero-copy), or null
         size_t upCap = 0;
         uint8_t* downHost = nullptr;
         uint8_t* downDev = nullptr;   // device-side gather area for downloads + results

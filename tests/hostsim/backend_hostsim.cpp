@@ -339,7 +339,13 @@ void be_dev_free(void* p) { std::free(p); }
 void* be_host_alloc(size_t bytes) { return be_dev_alloc(bytes); }
 void be_host_free(void* p) { std::free(p); }
 void be_h2d(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
+void* be_host_device_ptr(void* host) { return host; }
 void be_d2h(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
+void be_copy_pinned(const BeCopy* r, unsigned n, bool)
+{
+    for (unsigned i = 0; i < n; ++i)
+        std::memcpy((void*)(uintptr_t)r[i].dst, (const void*)(uintptr_t)r[i].src, r[i].bytes);
+}
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
 static bool noexec();

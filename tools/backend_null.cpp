@@ -59,6 +59,7 @@ void* be_dev_alloc(size_t bytes)
 void be_dev_free(void* p) { std::free(p); }
 void* be_host_alloc(size_t bytes) { return be_dev_alloc(bytes); }
 void be_host_free(void* p) { std::free(p); }
+void* be_host_device_ptr(void*) { return nullptr; }   // (no zero-copy: uploads stay DMA-shaped)
 void be_h2d(void* dst, const void* src, size_t bytes)
 {
     // a DMA on the GPU: remember the mapping instead of copying
@@ -67,6 +68,15 @@ void be_h2d(void* dst, const void* src, size_t bytes)
     g_upBytes = bytes;
 }
 void be_d2h(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
+void be_copy_pinned(const BeCopy* r, unsigned n, bool toDevice)
+{
+    for (unsigned i = 0; i < n; ++i) {
+        if (toDevice)
+            be_h2d((void*)(uintptr_t)r[i].dst, (const void*)(uintptr_t)r[i].src, r[i].bytes);
+        else
+            be_d2h((void*)(uintptr_t)r[i].dst, (const void*)(uintptr_t)r[i].src, r[i].bytes);
+    }
+}
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
 void be_launch_ingest(const IngestDesc*, uint32_t, uint32_t) {}
