@@ -1,10 +1,14 @@
 // backend_hip.hip -- gfx950 kernels and the HIP side of backend.h.
 //
 // Kernels (all byte-column local, see ops.h):
-//   k_ingest       copy symbols (with their length prefix) into fresh buffers
-//   k_exec         run one segment of every instance's op list on one 1 KiB
-//                  tile: LINCOMB = XOR / GF(256) multiply-accumulate of up to
-//                  thousands of source symbols into one destination
+//   k_ingest       copy symbols (with their length prefix) into fresh buffers,
+//                  8 KiB chunks of a symbol dealt to separate waves
+//   k_exec         run one segment of every instance's op list on one
+//                  256-byte tile (64 lanes x 4 bytes; 16 waves share the
+//                  tile's terms): LINCOMB = XOR / GF(256) multiply-accumulate
+//                  of up to thousands of source symbols into one destination,
+//                  OP_ROWS Siamese row batches staged in LDS
+//   k_ldpc         the LDPC picks of wide rows (windows of >= 512 elements)
 //   k_solve_prefix solve bytes 0..3 of every row of each triangular system
 //                  (one wave per solve) to learn the recovered lengths
 //   k_solve_main   lower-triangle multiply + back-substitution per tile
