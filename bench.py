@@ -306,7 +306,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
     sess = S.BatchSession(library, cfg, device=device)
     # untimed warm-up; its first run checks every recovered byte against the payload
     res, rep = sess.run(steps=0, warmup=1, verify=args.verify, threads=args.threads,
-                        groups=args.groups)
+                        groups=args.groups, defer=args.defer)
     if args.verify and (rep.mismatches or any(r.status for r in res)):
         raise RuntimeError("bench: verification failed: %d byte mismatches, status %s"
                            % (rep.mismatches, S.summary(res)["status"]))
@@ -317,12 +317,12 @@ def run_rank(rank, world, local, args, library, use_cuda):
     # buffer arena reaches the timed loop's high-water mark before timing
     if args.warmup > 0:
         sess.run(steps=args.warmup, warmup=0, verify=False, threads=args.threads,
-                 groups=args.groups, digest=False)
+                 groups=args.groups, digest=False, defer=args.defer)
 
     coll.barrier()
     t0 = time.perf_counter()
     res, rep = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
-                        groups=args.groups, digest=False)
+                        groups=args.groups, digest=False, defer=args.defer)
     coll.barrier()
     elapsed = time.perf_counter() - t0
 
@@ -336,7 +336,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
         # (pipelined warm-up over both alternating device copies, every
         # recovered byte checked against the payloads)
         res_e, rep_e = sess.run(steps=max(2, args.warmup), warmup=0, verify=args.verify,
-                                threads=args.threads, groups=args.groups, e2e=True, digest=False,
+                                threads=args.threads, groups=args.groups, e2e=True, digest=False, defer=args.defer,
                                 frames=args.frames)
         if args.verify and (rep_e.mismatches or any(r.status for r in res_e)):
             raise RuntimeError("bench: end-to-end verification failed: %d byte mismatches"
@@ -344,7 +344,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
         coll.barrier()
         t1 = time.perf_counter()
         sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
-                 groups=args.groups, e2e=True, digest=False, frames=args.frames)
+                 groups=args.groups, e2e=True, digest=False, defer=args.defer, frames=args.frames)
         coll.barrier()
         e2e_elapsed = time.perf_counter() - t1
     sess.close()
@@ -517,6 +517,9 @@ def main(argv=None):
                     help="host threads driving streams (0 = library default)")
     ap.add_argument("--groups", type=int, default=4,
                     help="stream groups alternating host and device work (1 = no overlap)")
+    ap.add_argument("--defer", type=int, default=0,
+                    help="deferred decode outputs: a stream submits after every DEFER-th decode "
+                         "(0: it yields after each decode until its lengths are known)")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip the PCIe-inclusive end-to-end leg")
     ap.add_argument("--no-frames", dest="frames", action="store_false",

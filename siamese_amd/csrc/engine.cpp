@@ -185,6 +185,48 @@ void ProgramBody::lc_seal()
     lcb.clear();
 }
 
+namespace {
+
+using Span = ProgramBody::LcBuild::Span;
+
+// does [lo, hi) meet a span of the disjoint sorted set v?
+bool span_hits(const std::vector<Span>& v, uint64_t lo, uint64_t hi)
+{
+    const auto it = std::upper_bound(v.begin(), v.end(), lo,
+                                     [](uint64_t x, const Span& sp) { return x < sp.hi; });
+    return it != v.end() && it->lo < hi;
+}
+
+// v |= [lo, hi), keeping v disjoint and sorted
+void span_add(std::vector<Span>& v, uint64_t lo, uint64_t hi)
+{
+    if (lo >= hi)
+        return;
+    auto first = std::lower_bound(v.begin(), v.end(), lo,
+                                  [](const Span& sp, uint64_t x) { return sp.hi < x; });
+    auto last = first;
+    while (last != v.end() && last->lo <= hi) {
+        lo = std::min(lo, last->lo);
+        hi = std::max(hi, last->hi);
+        ++last;
+    }
+    if (first == last) {
+        v.insert(first, Span{lo, hi});
+    } else {
+        *first = Span{lo, hi};
+        v.erase(first + 1, last);
+    }
+}
+
+// bytes an item writes: its lanes and its footer literal
+uint64_t lc_write_span(const LcItem& it)
+{
+    const uint32_t litEnd = it.litOffset + ((it.mixLit >> 8) & 0xff);
+    return std::max<uint64_t>(lane_span(it.n), litEnd);
+}
+
+} // namespace
+
 void ProgramBody::lc_absorb()
 {
     // SIAMESE_AMD_LC_BATCH=0: every combination stays a plain op (A/B aid)
@@ -208,19 +250,21 @@ void ProgramBody::lc_absorb()
     // align16(n)) and the literal; reads: the terms and dst's kept bytes)
     bool indep = lcb.items.size() < kLcMaxItems;
     const uint64_t w = lane_span(op.n);
-    for (size_t i = 0; indep && i < lcb.items.size(); ++i) {
-        const LcItem& it = lcb.items[i];
-        const uint32_t litEnd = it.litOffset + ((it.mixLit >> 8) & 0xff);
-        const uint64_t iw = std::max<uint64_t>(lane_span(it.n), litEnd);
-        if (overlaps(op.dst, w, it.dst, iw)) {
+    if (indep && !lcb.items.empty()) {
+        // the items before the last: the span sets
+        if (span_hits(lcb.writes, op.dst, op.dst + w) || span_hits(lcb.reads, op.dst, op.dst + w))
             indep = false;
-            break;
-        }
-        for (uint32_t k = 0; k < op.termCount; ++k)
-            if (overlaps(t[k].src, lane_span(t[k].len), it.dst, iw)) {
+        for (uint32_t k = 0; indep && k < op.termCount; ++k)
+            if (span_hits(lcb.writes, t[k].src, t[k].src + lane_span(t[k].len)))
                 indep = false;
-                break;
-            }
+        // the last item
+        const LcItem& it = lcb.items.back();
+        const uint64_t iw = lc_write_span(it);
+        if (indep && overlaps(op.dst, w, it.dst, iw))
+            indep = false;
+        for (uint32_t k = 0; indep && k < op.termCount; ++k)
+            if (overlaps(t[k].src, lane_span(t[k].len), it.dst, iw))
+                indep = false;
         const GfTerm* u = lcb.terms.data() + it.termStart;
         for (uint32_t k = 0; indep && k < it.termCount; ++k)
             if (overlaps(u[k].src, lane_span(u[k].len), op.dst, w))
@@ -231,8 +275,16 @@ void ProgramBody::lc_absorb()
     lcScratch.assign(t, t + op.termCount);
     s.terms.resize(op.termBegin);
     s.ops.pop_back();
-    if (!indep)
+    if (!indep) {
         lc_seal();
+    } else if (!lcb.items.empty()) {
+        // the last item joins the span sets (its literal can no longer grow)
+        const LcItem& it = lcb.items.back();
+        span_add(lcb.writes, it.dst, it.dst + lc_write_span(it));
+        const GfTerm* u = lcb.terms.data() + it.termStart;
+        for (uint32_t k = 0; k < it.termCount; ++k)
+            span_add(lcb.reads, u[k].src, u[k].src + lane_span(u[k].len));
+    }
     LcItem it;
     std::memset(&it, 0, sizeof(it));
     it.dst = op.dst;
@@ -247,18 +299,9 @@ void ProgramBody::lc_absorb()
 
 bool ProgramBody::lc_literal_fits(uint64_t at, uint32_t len) const
 {
-    // the literal's bytes must not be read or written by another item
-    for (size_t i = 0; i + 1 < lcb.items.size(); ++i) {
-        const LcItem& it = lcb.items[i];
-        const uint32_t litEnd = it.litOffset + ((it.mixLit >> 8) & 0xff);
-        if (overlaps(at, len, it.dst, std::max<uint64_t>(lane_span(it.n), litEnd)))
-            return false;
-        const GfTerm* u = lcb.terms.data() + it.termStart;
-        for (uint32_t k = 0; k < it.termCount; ++k)
-            if (overlaps(u[k].src, lane_span(u[k].len), at, len))
-                return false;
-    }
-    return true;
+    // the literal's bytes must not be read or written by another item (the
+    // items before the last: exactly the span sets)
+    return !span_hits(lcb.writes, at, at + len) && !span_hits(lcb.reads, at, at + len);
 }
 
 void ProgramBody::rows_close()

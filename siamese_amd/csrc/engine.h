@@ -124,10 +124,21 @@ struct ProgramBody
     {
         std::vector<LcItem> items;
         std::vector<GfTerm> terms;   // termStart: index into this, made block-relative on seal
+        /// Byte spans written / read by every item but the last, each set
+        /// disjoint and sorted (the independence tests are binary searches;
+        /// the last item stays out until the next one joins, because a footer
+        /// literal may still grow its write span).
+        struct Span
+        {
+            uint64_t lo, hi;
+        };
+        std::vector<Span> writes, reads;
         void clear()
         {
             items.clear();
             terms.clear();
+            writes.clear();
+            reads.clear();
         }
     } lcb;
     std::vector<GfTerm> lcScratch;
