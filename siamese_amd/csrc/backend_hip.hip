@@ -603,7 +603,10 @@ __device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t
 // over the whole chip instead of running inside the codec's one workgroup
 // per tile.
 constexpr unsigned kLdpcWaves = 4;
-constexpr unsigned kLdpcDepth = 8;
+#ifndef SGPU_LDPC_DEPTH
+#define SGPU_LDPC_DEPTH 8
+#endif
+constexpr unsigned kLdpcDepth = SGPU_LDPC_DEPTH;   // loads in flight per lane
 
 __global__ __launch_bounds__(64 * kLdpcWaves) void k_ldpc(const LdpcItem* __restrict__ items,
                                                           unsigned long long* __restrict__ acct)

@@ -179,7 +179,12 @@ struct LdpcItem
 };
 static_assert(sizeof(LdpcItem) == 48, "LdpcItem layout");
 constexpr uint32_t kLdpcSplitMin = 512;      // ldpcN from which a row's picks go to k_ldpc
-constexpr uint32_t kLdpcPairsPerItem = 32;   // pairs per k_ldpc item
+#ifndef SGPU_LDPC_PAIRS
+#define SGPU_LDPC_PAIRS 64
+#endif
+// pairs per k_ldpc item (64: C5 66-69 ms/run vs 68-81 with 32, 70 with 128;
+// profiles/r3g_ldpc_item_ab.txt)
+constexpr uint32_t kLdpcPairsPerItem = SGPU_LDPC_PAIRS;
 constexpr uint32_t kLdpcTileBytes = 1024;    // k_ldpc tile: 64 lanes x 16 bytes
 
 /// OP_COPIES: n independent copies (the decoder taking in recovery packets,
