@@ -373,9 +373,12 @@ struct BatchCodec
     }
     uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok)
     {
-        if (sh->defer && p.entry) {
+        if (sh->defer && p.entry && p.entry->DataBytes == 0) {
             // length and bytes arrive with the round's completion: the token
-            // is written into the log then (resolve_requests)
+            // is written into the log then (resolve_requests).  (An entry the
+            // call filled at once -- a packet not being solved -- is checked
+            // right here like a plain one: no request to carry through the
+            // main thread's collection.)
             push(Request{log, log->size(), nullptr, 0, id, true, ok, p.entry});
             return 0;
         }

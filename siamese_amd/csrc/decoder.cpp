@@ -1201,7 +1201,14 @@ bool DecoderCore::eliminate_row(const uint8_t* geRow, uint8_t* remRow, unsigned 
     const uint8_t y = gf_div(valJ, valI);
     remRow[pivot] = y;
     if (end > pivot + 1) {
-        gf_muladd_row(remRow + pivot + 1, geRow + pivot + 1, y, end - pivot - 1);
+        // the pivot row's bytes after the pivot, split into nibbles once for
+        // every row it eliminates (geSrcFor_ names the split in geSrc_)
+        if (geSrcRow_ != geRow || geSrcPivot_ != pivot || geSrc_.n != end - pivot - 1) {
+            gf_row_prepare(geSrc_, geRow + pivot + 1, end - pivot - 1);
+            geSrcRow_ = geRow;
+            geSrcPivot_ = pivot;
+        }
+        gf_muladd_prepared(remRow + pivot + 1, geSrc_, y);
         geBytes_ += end - pivot - 1;   // the reference's MulAddRows muladd (:504-520)
     }
     return true;
@@ -1211,6 +1218,7 @@ void DecoderCore::resume_ge(unsigned oldRows, unsigned rows)
 {
     if (oldRows >= rows)
         return;
+    geSrcRow_ = nullptr;
     for (unsigned p = 0; p < geResume_; ++p) {
         const unsigned ri = pivots_[p];
         const uint8_t* ge = mrow(ri);
@@ -1224,6 +1232,7 @@ void DecoderCore::resume_ge(unsigned oldRows, unsigned rows)
 
 bool DecoderCore::gaussian_elimination()
 {
+    geSrcRow_ = nullptr;   // (the matrix may have moved since the last elimination)
     if (geResume_ > 0)
         return pivoted_ge(geResume_);
     const unsigned columns = matCols_;

@@ -17,6 +17,7 @@
 #include "codedef.h"
 #include "encoder.h"
 #include "engine.h"
+#include "gf.h"
 #include "objpool.h"
 #include "../../include/siamese.h"
 
@@ -268,6 +269,10 @@ private:
     std::vector<unsigned> pivots_;
     unsigned geResume_ = 0;
     uint64_t geBytes_ = 0;   // coefficient bytes the elimination multiplied (accounting)
+    // the current pivot row's bytes after the pivot, split for gf_muladd_prepared
+    GfRowSrc geSrc_;
+    const uint8_t* geSrcRow_ = nullptr;
+    unsigned geSrcPivot_ = 0;
 
     unsigned latestColumn_ = 0;
 

@@ -1260,10 +1260,12 @@ uint64_t Engine::enqueue()
 {
     if (failed())
         return 0;
+    const uint64_t tq0 = now_ns();
     Batch* b = take_batch();
     if (!b)
         return nextTicket_;   // nothing queued: the latest submission covers everything
     const uint64_t ticket = b->ticket;
+    const uint64_t tq1 = now_ns();
     // The batch is laid out here, on the caller's thread and the shared
     // pool.  SIAMESE_AMD_ASYNC_ASSEMBLY=1 hands it to the launcher thread and
     // its own pool instead, so the caller goes back to driving instances at
@@ -1272,8 +1274,13 @@ uint64_t Engine::enqueue()
     // it is off by default.
     if (!async_assembly()) {
         claim_set(*b);
+        const uint64_t tq2 = now_ns();
         assemble_batch(*b, pool());
         tl("assembled", ticket);
+        static const bool asmStats = std::getenv("SGPU_ASM_STATS") != nullptr;
+        if (asmStats)
+            std::fprintf(stderr, "enq %zu: take %.3f claim %.3f assemble %.3f ms\n", (size_t)ticket,
+                         (tq1 - tq0) / 1e6, (tq2 - tq1) / 1e6, (now_ns() - tq2) / 1e6);
     }
     {
         std::lock_guard<std::mutex> g(qMu_);
@@ -1469,6 +1476,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         }
     });
 
+    const uint64_t tSeal = now_ns();
     // ---- 2. layout -----------------------------------------------------------
     uint32_t resultWords = 0;
     for (int g = 0; g < 2; ++g)
@@ -1665,6 +1673,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         xs.wideUsed += wideBytes;
     }
 
+    const uint64_t tLayout = now_ns();
     // ---- 3. copy into the pinned upload buffer -------------------------------
     uint8_t* up = xs.upHost;
     const uint64_t stageDev = (uint64_t)(uintptr_t)(bt.upBase + oStage);
@@ -1788,6 +1797,12 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     st.ingests = nIngest;
     st.uploadBytes = bt.upBytes;
     st.assembleNs = now_ns() - t0;
+    // SGPU_ASM_STATS=1: one stderr line per flush, assembly time by stage (profiling aid)
+    static const bool asmStats = std::getenv("SGPU_ASM_STATS") != nullptr;
+    if (asmStats)
+        std::fprintf(stderr, "asm %zu bodies %zu up %zu: seal %.3f layout %.3f copy %.3f ms (%s)\n", (size_t)bt.ticket,
+                     totalBodies, bt.upBytes, (tSeal - t0) / 1e6, (tLayout - tSeal) / 1e6,
+                     (now_ns() - tLayout) / 1e6, parallel ? "parallel" : "serial");
 }
 
 void Engine::launch_batch(Batch& bt)

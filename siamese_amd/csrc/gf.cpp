@@ -101,6 +101,36 @@ void gf_muladd_row(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n)
     }
 }
 
+void gf_row_prepare(GfRowSrc& out, const uint8_t* src, unsigned n)
+{
+    const __m256i m0f = _mm256_set1_epi8(0x0f);
+    out.n = n;
+    for (unsigned i = 0; i < n; i += 32) {
+        const __m256i x = _mm256_loadu_si256((const __m256i*)(src + i));
+        _mm256_store_si256((__m256i*)(out.lo + i), _mm256_and_si256(x, m0f));
+        _mm256_store_si256((__m256i*)(out.hi + i), _mm256_and_si256(_mm256_srli_epi64(x, 4), m0f));
+    }
+}
+
+void gf_muladd_prepared(uint8_t* dst, const GfRowSrc& src, uint8_t y)
+{
+    const unsigned n = src.n;
+    if (y == 0 || n == 0)
+        return;
+    const __m256i tlo = _mm256_broadcastsi128_si256(_mm_load_si128((const __m128i*)g_gf.nib_lo[y]));
+    const __m256i thi = _mm256_broadcastsi128_si256(_mm_load_si128((const __m128i*)g_gf.nib_hi[y]));
+    for (unsigned i = 0; i < n; i += 32) {
+        const __m256i p = _mm256_xor_si256(
+            _mm256_shuffle_epi8(tlo, _mm256_load_si256((const __m256i*)(src.lo + i))),
+            _mm256_shuffle_epi8(thi, _mm256_load_si256((const __m256i*)(src.hi + i))));
+        const __m256i d = _mm256_loadu_si256((const __m256i*)(dst + i));
+        __m256i r = _mm256_xor_si256(d, p);
+        if (n - i < 32)
+            r = _mm256_blendv_epi8(d, r, head_mask(n - i));
+        _mm256_storeu_si256((__m256i*)(dst + i), r);
+    }
+}
+
 void gf_dense_row(uint8_t* out, const uint8_t* lane, const uint8_t* cx, const uint8_t* cx2,
                   const uint8_t opLo[8], const uint8_t opHi[8], uint8_t rx, unsigned n)
 {

@@ -39,6 +39,22 @@ inline uint8_t gf_div(uint8_t x, uint8_t y) { return y ? g_gf.mul[g_gf.inv[y]][x
 /// rewritten unchanged).
 void gf_muladd_row(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n);
 
+/// A coefficient row segment split into nibbles once, for many
+/// dst ^= y * src updates with the same src (one Gaussian-elimination pivot
+/// row against every row below it): up to kGfRowMax bytes.
+struct GfRowSrc
+{
+    static constexpr unsigned kGfRowMax = 288;   // align32(255 + 4) + slack
+    alignas(32) uint8_t lo[kGfRowMax];
+    alignas(32) uint8_t hi[kGfRowMax];
+    unsigned n = 0;
+};
+/// Split src[0, n) (readable 31 bytes past n) into `out`; n <= kGfRowMax - 32.
+void gf_row_prepare(GfRowSrc& out, const uint8_t* src, unsigned n);
+/// dst[i] ^= y * src[i] for i < src.n with the prepared src (dst writable
+/// 31 bytes past n, rewritten unchanged).
+void gf_muladd_prepared(uint8_t* dst, const GfRowSrc& src, uint8_t y);
+
 /// Dense Siamese coefficients of one recovery row for `n` lost columns
 /// (reference SiameseDecoder.cpp:2278-2300): out[j] = comb(opLo[lane[j]]) ^
 /// RX * comb(opHi[lane[j]]) with comb(k) = (k&1) ^ (k&2 ? cx[j] : 0) ^
