@@ -343,7 +343,7 @@ void ProgramBody::rows_close()
         const uint32_t pairs = (r.ldpcN + kPairRate - 1) / kPairRate;
         s.wide.push_back(Segment::Wide{(uint32_t)s.ops.size(), entry, r.n, r.row, r.ldpcN, r.ldpcOff});
         s.wideItems += ((r.n + kLdpcTileBytes - 1) / kLdpcTileBytes) *
-                       ((pairs + kLdpcPairsPerItem - 1) / kLdpcPairsPerItem);
+                       ((pairs + ldpc_pairs_per_item(r.n) - 1) / ldpc_pairs_per_item(r.n));
         s.wideBytes += 2 * (uint64_t)((r.n + kLdpcTileBytes - 1) / kLdpcTileBytes * kLdpcTileBytes);
         WinEntry z;
         std::memset(&z, 0, sizeof(z));
@@ -1724,8 +1724,9 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                             e[1].src = dst + span;
                             e[1].len = x.n;
                             const uint32_t pairs = (x.N + kPairRate - 1) / kPairRate;
+                            const uint32_t ppi = ldpc_pairs_per_item(x.n);
                             for (uint32_t t = 0; t < x.n; t += kLdpcTileBytes)
-                                for (uint32_t p0 = 0; p0 < pairs; p0 += kLdpcPairsPerItem) {
+                                for (uint32_t p0 = 0; p0 < pairs; p0 += ppi) {
                                     LdpcItem& it = *wItem++;
                                     it.win = winDev;
                                     it.dst = dst;
@@ -1736,7 +1737,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                                     it.off = x.off;
                                     it.tileBase = t;
                                     it.pair0 = p0;
-                                    it.pair1 = std::min(pairs, p0 + kLdpcPairsPerItem);
+                                    it.pair1 = std::min(pairs, p0 + ppi);
                                 }
                         }
                         w += bytes;

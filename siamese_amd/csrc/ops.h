@@ -182,10 +182,16 @@ constexpr uint32_t kLdpcSplitMin = 512;      // ldpcN from which a row's picks g
 #ifndef SGPU_LDPC_PAIRS
 #define SGPU_LDPC_PAIRS 64
 #endif
-// pairs per k_ldpc item (64: C5 66-69 ms/run vs 68-81 with 32, 70 with 128;
-// profiles/r3g_ldpc_item_ab.txt)
-constexpr uint32_t kLdpcPairsPerItem = SGPU_LDPC_PAIRS;
 constexpr uint32_t kLdpcTileBytes = 1024;    // k_ldpc tile: 64 lanes x 16 bytes
+/// Pairs per k_ldpc item for a row of `bytes`: rows of large symbols (C5:
+/// 64 tiles each) take SGPU_LDPC_PAIRS, which halves their atomics and item
+/// count (C5 66-69 ms/run vs 68-81 with 32); rows of small symbols keep 32,
+/// so their few tiles still spread over enough workgroups (C3: k_ldpc 10.3
+/// vs 13.1 us per launch with 64).  profiles/r3g_ldpc_item_ab.txt, r3h traces.
+constexpr uint32_t ldpc_pairs_per_item(uint32_t bytes)
+{
+    return bytes >= 16 * kLdpcTileBytes ? SGPU_LDPC_PAIRS : 32u;
+}
 
 /// OP_COPIES: n independent copies (the decoder taking in recovery packets,
 /// reference SiameseDecoder.cpp:437), one CopyItem word pair each after the
