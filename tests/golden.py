@@ -29,6 +29,12 @@ FIXTURES = {
     "C4": ("C4", dict(hash_data=0)),
     "C5x2000": ("C5", dict(originals=2000)),
     "C5": ("C5", dict(hash_data=0)),
+    # full-size configs with every byte of every recovery packet and
+    # recovered original hashed (the bench legs' and the headline shard's
+    # exact workloads)
+    "C2h": ("C2", dict(hash_data=1)),
+    "C4x1024h": ("C4", dict(streams=1024, hash_data=1)),
+    "C5h": ("C5", dict(hash_data=1)),
     # edge cases: tiny packets, variable sizes in block mode, heavy loss with
     # decode failures / stalls, losses close to the 255-column solver limit,
     # lag-based acknowledgements over a long variable-size stream

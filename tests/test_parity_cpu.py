@@ -27,7 +27,7 @@ def _check(name, results):
     assert [int(r.status) for r in results] == want["status"]
 
 
-@pytest.mark.parametrize("name", SMALL + ["C3", "C4x256", "C2"])
+@pytest.mark.parametrize("name", SMALL + ["C3", "C4x256", "C2", "C2h", "C4x1024h"])
 def test_reference_matches_golden(name, ref_available):
     if not ref_available:
         pytest.skip("oracle/_ref not built")
