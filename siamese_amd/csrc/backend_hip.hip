@@ -297,7 +297,7 @@ __device__ __forceinline__ void acct_wave(unsigned long long* acctL, uint32_t v)
 #ifdef SGPU_PHASE_CLOCKS
 // profiling build only: shader clocks per OP_ROWS phase, summed over
 // workgroups as seen by thread 0 (tools/phase_clocks.py reads them)
-__device__ unsigned long long g_phaseClk[32];
+__device__ unsigned long long g_phaseClk[48];
 #define PHASE_MARK(k, t)                                                             \
     do {                                                                             \
         if (tid == 0) {                                                              \
@@ -915,8 +915,15 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         }
     }
     __syncthreads();
+#ifdef SGPU_PHASE_CLOCKS
+    if (threadIdx.x == 0)
+        atomicAdd(&g_phaseClk[32], clock64() - kclk);
+#endif
     uint32_t cur = 0, pos = 0;
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
+#ifdef SGPU_PHASE_CLOCKS
+        const unsigned long long oclk = clock64();
+#endif
         // the thread index, opaque per op: lane-derived addresses are then
         // computed where they are used instead of hoisted out of the op loop,
         // where dozens of them would hold VGPRs through every phase
@@ -1746,6 +1753,12 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         if (kind != OP_ROWS && tid < kRingWords)
             ring[cur ^ 1][tid] = pf;
         __syncthreads();
+#ifdef SGPU_PHASE_CLOCKS
+        if (threadIdx.x == 0 && kind >= 1 && kind <= 5) {
+            atomicAdd(&g_phaseClk[32 + kind], clock64() - oclk);   // 33..37: op time by kind
+            atomicAdd(&g_phaseClk[37 + kind], 1ull);               // 38..42: ops by kind
+        }
+#endif
         cur ^= 1;
         pos = next;
     }
@@ -2614,7 +2627,7 @@ extern "C" __attribute__((visibility("default"))) void sgpu_debug_phase_clocks(u
 {
     bind_device();
     (void)hipDeviceSynchronize();
-    (void)hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_phaseClk), 32 * sizeof(unsigned long long));
+    (void)hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_phaseClk), 48 * sizeof(unsigned long long));
 }
 #endif
 

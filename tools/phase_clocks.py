@@ -14,7 +14,7 @@ import bench  # noqa: E402
 lib = sys.argv[1]
 bench.main(["--library", lib, "--steps", "3", "--warmup", "1", "--no-cpu", "--no-e2e", "--no-legs"])
 L = ctypes.CDLL(os.path.abspath(lib))
-out = (ctypes.c_ulonglong * 32)()
+out = (ctypes.c_ulonglong * 48)()
 L.sgpu_debug_phase_clocks(out)
 ops = max(1, out[8])
 names = ["block load", "stage+plan", "sum updates", "stage sums", "sums barrier", "rows"]
@@ -27,3 +27,9 @@ print("  rows detail (wave 0 quad tasks): descriptors %.0f, terms %.0f, stores %
 print("  detail (wave 0): update units %.0f, plan pairs %.0f clocks per op; stage re-read in %.1f%% of ops"
       % (out[19] / ops, out[20] / ops, 100.0 * out[21] / ops))
 print("kernel: %d workgroups, %.0f clocks each" % (out[7], out[6] / max(1, out[7])))
+wgs = max(1, out[7])
+print("setup %.0f clocks per workgroup" % (out[32] / wgs))
+for k, nm in enumerate(["LINCOMB", "LITERAL", "ROWS", "COPIES", "LINCOMBS"]):
+    c = out[38 + k]
+    print("  %-9s %8d ops, %10.0f clocks per op, %10.0f clocks per workgroup" % (
+        nm, c, out[33 + k] / max(1, c), out[33 + k] / wgs))
