@@ -923,6 +923,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
 #ifdef SGPU_PHASE_CLOCKS
         const unsigned long long oclk = clock64();
+        unsigned long long t5 = 0;   // thread 0 past an OP_ROWS op's last phase
 #endif
         // the thread index, opaque per op: lane-derived addresses are then
         // computed where they are used instead of hoisted out of the op loop,
@@ -1678,6 +1679,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             PHASE_MARK(5, tclk);
             if (tid == 0) {
 #ifdef SGPU_PHASE_CLOCKS
+                t5 = clock64();
                 atomicAdd(&g_phaseClk[8], 1ull);
                 atomicAdd(&g_phaseClk[9], (unsigned long long)R);
                 atomicAdd(&g_phaseClk[10], (unsigned long long)U);
@@ -1757,6 +1759,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         if (threadIdx.x == 0 && kind >= 1 && kind <= 5) {
             atomicAdd(&g_phaseClk[32 + kind], clock64() - oclk);   // 33..37: op time by kind
             atomicAdd(&g_phaseClk[37 + kind], 1ull);               // 38..42: ops by kind
+            if (kind == OP_ROWS)
+                atomicAdd(&g_phaseClk[43], clock64() - t5);        // waiting for the other waves
         }
 #endif
         cur ^= 1;

@@ -33,3 +33,5 @@ for k, nm in enumerate(["LINCOMB", "LITERAL", "ROWS", "COPIES", "LINCOMBS"]):
     c = out[38 + k]
     print("  %-9s %8d ops, %10.0f clocks per op, %10.0f clocks per workgroup" % (
         nm, c, out[33 + k] / max(1, c), out[33 + k] / wgs))
+print("OP_ROWS: thread 0 waits %.0f clocks per op at the op's closing barrier (other waves still in the rows phase)"
+      % (out[43] / max(1, out[40])))
