@@ -1831,6 +1831,31 @@ __device__ __forceinline__ int parse_prefix(uint32_t w, uint32_t avail, uint32_t
 // publishes them (`out`) with the byte counts: the diagonal scaling of
 // max(32 clipped, recovered) bytes and one muladd of min(recovered, row)
 // bytes per earlier row each completed step eliminates (:1131-1212).
+// Ct[i*m + j] = C[j*m + i] for an m x m byte matrix, by `threads` threads
+// (thread t of them), U loads in flight per thread before their stores
+template <unsigned threads, unsigned U>
+__device__ __forceinline__ void stage_transposed(uint8_t* __restrict__ Ct, const uint8_t* __restrict__ C,
+                                                 uint32_t m, uint32_t t)
+{
+    const uint32_t mm = m * m;
+    for (uint32_t k0 = t; k0 < mm; k0 += threads * U) {
+        uint32_t v[U];
+#pragma unroll
+        for (unsigned u = 0; u < U; ++u) {
+            const uint32_t k = k0 + u * threads;
+            v[u] = k < mm ? C[k] : 0u;
+        }
+#pragma unroll
+        for (unsigned u = 0; u < U; ++u) {
+            const uint32_t k = k0 + u * threads;
+            if (k < mm) {
+                const uint32_t j = k / m, i = k - j * m;
+                Ct[i * m + j] = (uint8_t)v[u];
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t p4_get(const uint32_t (&p4)[4], uint32_t i)
 {
     // row i's word (i uniform): its lane's register k = i / 64
@@ -2022,10 +2047,7 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
             permC[y] = t[4];
         }
     }
-    for (uint32_t k = tid; k < m * m; k += 64 * kSolveWaves) {
-        const uint32_t j = k / m, i = k - j * m;
-        Ct[i * m + j] = C[k];
-    }
+    stage_transposed<64 * kSolveWaves, 4>(Ct, C, m, tid);
     for (uint32_t j = tid; j < m; j += 64 * kSolveWaves) {
         initB[j] = R[j].initBytes;
         lowL[j] = R[j].lowerLen;
@@ -2184,10 +2206,7 @@ __device__ void solve_tile_narrow(uint4* __restrict__ X, uint32_t m, const Solve
         permL[y] = make_uint4(t[0], t[1], t[2], t[3]);
         permC[y] = t[4];
     }
-    for (uint32_t k = tid; k < m * m; k += 64 * kSolveWaves) {
-        const uint32_t j = k / m, i = k - j * m;
-        Ct[i * m + j] = C[k];
-    }
+    stage_transposed<64 * kSolveWaves, 4>(Ct, C, m, tid);
     for (uint32_t j = tid; j < m; j += 64 * kSolveWaves) {
         initB[j] = R[j].initBytes;
         lowL[j] = R[j].lowerLen;
@@ -2361,10 +2380,10 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
         permL[y] = make_uint4(t[0], t[1], t[2], t[3]);
         permC[y] = t[4];
     }
-    for (uint32_t k = lane; k < m * m; k += 64) {
-        const uint32_t j = k / m, i = k - j * m;
-        Ct[i * m + j] = C[k];
-    }
+    // the coefficients, transposed: eight loads in flight per lane (one wave
+    // stages up to 255^2 bytes; a load-then-store loop would pay a memory
+    // round trip per 64 bytes)
+    stage_transposed<64, 8>(Ct, C, m, lane);
     for (uint32_t j = lane; j < m; j += 64) {
         lowL[j] = R[j].lowerLen;
         finB[j] = R[j].finalBytes;
