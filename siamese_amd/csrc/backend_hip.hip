@@ -216,6 +216,8 @@ __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* 
             if (p + 16 > total)
                 v = mask16(v, (int)total - (int)p);
             st16(d.dst + p, v);
+            if (d.dst2)   // (uniform)
+                st16(d.dst2 + p, v);
         }
     }
 }

@@ -549,6 +549,7 @@ void Program::ingest_device(const DevBuf& dst, uint64_t src, uint32_t bytes, con
     d.src = src;
     d.bytes = bytes;
     d.hdrLen = hdrLen;
+    d.dst2 = 0;
     uint64_t h = 0;
     std::memcpy(&h, hdr, hdrLen < 8 ? hdrLen : 8);
     std::memcpy(d.hdr, &h, 8);
@@ -1003,6 +1004,21 @@ void Engine::stage_host_ingest(const DevBuf& dst, const void* data, uint32_t byt
 void Engine::add_ingest(const IngestDesc& d, int64_t hostStageOffset)
 {
     Shard::Queues& q = shard().q;
+    // the same device symbol right after itself (an encoder and then its
+    // decoder taking in one original, SIAMESE_AMD_INGEST_PAIRS=0 to keep
+    // them apart): one descriptor with two destinations, the source read once
+    static const bool pairs = [] {
+        const char* v = std::getenv("SIAMESE_AMD_INGEST_PAIRS");
+        return !v || std::atoi(v) != 0;
+    }();
+    if (pairs && hostStageOffset < 0 && !q.ingest.empty()) {
+        Shard::IngestRec& last = q.ingest.back();
+        if (last.hostOffset < 0 && last.d.dst2 == 0 && last.d.src == d.src && last.d.bytes == d.bytes &&
+            last.d.hdrLen == d.hdrLen && std::memcmp(last.d.hdr, d.hdr, sizeof(d.hdr)) == 0) {
+            last.d.dst2 = d.dst;
+            return;
+        }
+    }
     q.ingest.push_back(Shard::IngestRec{d, hostStageOffset});
     q.maxIngest = std::max(q.maxIngest, d.bytes + d.hdrLen);
 }

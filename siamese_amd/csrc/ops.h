@@ -296,7 +296,9 @@ struct SolveItem
 /// op of the same flush before this point), so ingest can run as the first
 /// launch of a flush:  dst[0,hdrLen) = hdr,  dst[hdrLen, hdrLen+bytes) = src,
 /// and dst[total, align16(total)) = 0 (whole 16-byte lanes are stored; dst is
-/// 16-byte aligned with capacity >= align16(total)).
+/// 16-byte aligned with capacity >= align16(total)).  dst2 != 0: the same
+/// symbol written to a second fresh buffer too (an encoder and a decoder
+/// ingesting one original: the source is read once).
 struct IngestDesc
 {
     uint64_t dst;
@@ -304,6 +306,7 @@ struct IngestDesc
     uint32_t bytes;
     uint32_t hdrLen;
     uint8_t hdr[8];
+    uint64_t dst2;
 };
 
 constexpr unsigned kTileBytes = 1024;       // solve tiles: 64 lanes x 16 bytes

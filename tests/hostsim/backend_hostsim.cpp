@@ -361,6 +361,8 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t)
         const uint32_t end = (total + 15) & ~15u;
         for (uint32_t k = 0; k < end; ++k)
             P(d.dst)[k] = k < d.hdrLen ? d.hdr[k] : (k < total ? P(d.src)[k - d.hdrLen] : 0);
+        if (d.dst2)
+            std::memcpy(P(d.dst2), P(d.dst), end);
     }
 }
 
