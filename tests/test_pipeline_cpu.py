@@ -46,6 +46,30 @@ def test_oplincombs_batches_match_plain_ops():
     assert out["0"] == out["1"]
 
 
+def test_paired_ingest_matches_separate_ingest():
+    """Two-destination ingest descriptors (an encoder and then its decoder
+    taking in one device original) give the digests of separate ingests, and
+    the reference's (golden C4x256), with every recovered byte verified."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import scenario_lib as S, golden\n"
+        "res, rep = S.run_batch(S.SIM_LIB, golden.config('C4x256'), verify=True, threads=4, groups=2)\n"
+        "assert rep.mismatches == 0 and not any(r.status for r in res)\n"
+        "assert S.digests(res) == golden.load('C4x256')['digests']\n"
+        "print(S.engine_dict(rep)['ingests'])\n" % os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for v in ("0", "1"):
+        env = dict(os.environ, SIAMESE_AMD_INGEST_PAIRS=v)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[v] = int(r.stdout.strip().splitlines()[-1])
+    assert out["1"] < out["0"]   # the pairs did form (fewer descriptors)
+
+
 def test_pipelined_steps_keep_their_own_results():
     """Steps of one session may be in flight together (the next step's first
     job starts while the last one runs), and they run the same streams: each
