@@ -1866,31 +1866,11 @@ __device__ __forceinline__ uint32_t p4_get(const uint32_t (&p4)[4], uint32_t i)
     return rl(v, i & 63u);
 }
 
-#ifndef SGPU_PREFIX_PIPE
-#define SGPU_PREFIX_PIPE 0
-#endif
 __device__ void solve_prefix_wave(uint32_t m, uint32_t lane, uint32_t (&p4)[4], const uint8_t* Ct,
                                   const uint32_t* lowL, const uint32_t* finB, const uint4* permL,
                                   const uint32_t* permC, uint32_t* rw, uint32_t* __restrict__ out,
                                   unsigned long long* __restrict__ acct)
 {
-#if SGPU_PREFIX_PIPE
-    if (m <= 64) {
-        // one row per lane (register 0): the next step's multiplier table is
-        // fetched while this step multiplies (the coefficients are known up
-        // front), a lane with nothing to update multiplies by the zero table
-        const uint32_t j = lane;
-        GfTab tc = gf_tab_l(permL, permC, (j > 0 && j < m) ? (uint32_t)Ct[j] : 0u);
-        for (uint32_t i = 0; i + 1 < m; ++i) {
-            GfTab tn = tc;
-            if (i + 2 < m)
-                tn = gf_tab_l(permL, permC, (j > i + 1 && j < m) ? (uint32_t)Ct[(i + 1) * m + j] : 0u);
-            const uint32_t src = rl(p4[0], i) & byte_mask((int)uni(lowL[i]));
-            p4[0] ^= gf_mul_tab(src, tc);
-            tc = tn;
-        }
-    } else
-#endif
     for (uint32_t i = 0; i + 1 < m; ++i) {
         const uint32_t src = p4_get(p4, i) & byte_mask((int)uni(lowL[i]));
         const uint8_t* col = Ct + i * m;
