@@ -299,7 +299,7 @@ __device__ __forceinline__ void acct_wave(unsigned long long* acctL, uint32_t v)
 #ifdef SGPU_PHASE_CLOCKS
 // profiling build only: shader clocks per OP_ROWS phase, summed over
 // workgroups as seen by thread 0 (tools/phase_clocks.py reads them)
-__device__ unsigned long long g_phaseClk[48];
+__device__ unsigned long long g_phaseClk[64];
 #define PHASE_MARK(k, t)                                                             \
     do {                                                                             \
         if (tid == 0) {                                                              \
@@ -1866,11 +1866,61 @@ __device__ __forceinline__ uint32_t p4_get(const uint32_t (&p4)[4], uint32_t i)
     return rl(v, i & 63u);
 }
 
+#ifndef SGPU_PREFIX_PIPE
+#define SGPU_PREFIX_PIPE 1
+#endif
 __device__ void solve_prefix_wave(uint32_t m, uint32_t lane, uint32_t (&p4)[4], const uint8_t* Ct,
                                   const uint32_t* lowL, const uint32_t* finB, const uint4* permL,
                                   const uint32_t* permC, uint32_t* rw, uint32_t* __restrict__ out,
                                   unsigned long long* __restrict__ acct)
 {
+#if SGPU_PREFIX_PIPE
+    if (m <= 128) {
+        // rows in registers 0 and 1 (lanes j = lane, lane + 64), their lower
+        // lengths in registers too.  Software pipeline of depth two: during
+        // step i the tables of step i+1 (from coefficients fetched during step
+        // i-1) and the coefficients of step i+2 are in flight, so a step waits
+        // on no LDS round trip it has not overlapped with a step's arithmetic.
+        // A row with nothing to update multiplies by the zero table.
+        const bool two = m > 64;
+        const uint32_t j0 = lane, j1 = lane + 64, jm = m - 1;
+        const uint32_t w0 = lowL[j0 < jm ? j0 : jm], w1 = lowL[j1 < jm ? j1 : jm];
+        // (outside the rows a step updates, the load reads a zero byte: the
+        // product table of 0, so every lane's load is unconditional)
+        const uint8_t* zero = reinterpret_cast<const uint8_t*>(permL);
+        auto cb = [&](uint32_t i, uint32_t j) -> uint32_t {
+            return *((j > i && j < m) ? Ct + i * m + j : zero);
+        };
+        GfTab c0 = gf_tab_l(permL, permC, cb(0, j0)), c1 = c0;
+        if (two)
+            c1 = gf_tab_l(permL, permC, cb(0, j1));
+        uint32_t a0 = 0, a1 = 0;
+        if (m > 2) {
+            a0 = cb(1, j0);
+            if (two)
+                a1 = cb(1, j1);
+        }
+        for (uint32_t i = 0; i + 1 < m; ++i) {
+            const GfTab n0 = gf_tab_l(permL, permC, a0);
+            GfTab n1 = c1;
+            if (two)
+                n1 = gf_tab_l(permL, permC, a1);
+            if (i + 2 < m) {
+                a0 = cb(i + 2, j0);
+                if (two)
+                    a1 = cb(i + 2, j1);
+            }
+            const uint32_t q = i & 63u;
+            const bool lo = i < 64;
+            const uint32_t src = rl(lo ? p4[0] : p4[1], q) & byte_mask((int)rl(lo ? w0 : w1, q));
+            p4[0] ^= gf_mul_tab(src, c0);
+            if (two)
+                p4[1] ^= gf_mul_tab(src, c1);
+            c0 = n0;
+            c1 = n1;
+        }
+    } else
+#endif
     for (uint32_t i = 0; i + 1 < m; ++i) {
         const uint32_t src = p4_get(p4, i) & byte_mask((int)uni(lowL[i]));
         const uint8_t* col = Ct + i * m;
@@ -1884,8 +1934,86 @@ __device__ void solve_prefix_wave(uint32_t m, uint32_t lane, uint32_t (&p4)[4], 
             }
         }
     }
+#ifdef SGPU_PHASE_CLOCKS
+    if (lane == 0)
+        atomicAdd(&g_phaseClk[48], clock64());   // the lower sweep's end (slot 45 pairs it)
+#endif
     uint32_t ok = 0;
     unsigned long long opAcc = 0, outAcc = 0;
+#if SGPU_PREFIX_PIPE
+    if (m <= 128) {
+        // back-substitution with each row's final length and diagonal-inverse
+        // table in registers (lane j holds row j's) and the same two-deep
+        // pipeline of update tables and coefficients as the lower sweep
+        const bool two = m > 64;
+        const uint32_t j0 = lane, j1 = lane + 64, jm = m - 1;
+        const uint32_t r0 = j0 < jm ? j0 : jm, r1 = j1 < jm ? j1 : jm;
+        const uint32_t f0 = finB[r0], f1 = finB[r1];
+        const GfTab v0 = gf_tab_l(permL, permC, c_inv[Ct[r0 * m + r0]]);
+        GfTab v1 = v0;
+        if (two)
+            v1 = gf_tab_l(permL, permC, c_inv[Ct[r1 * m + r1]]);
+        const uint8_t* zero = reinterpret_cast<const uint8_t*>(permL);
+        auto ub = [&](uint32_t i, uint32_t j) -> uint32_t { return *(j < i ? Ct + i * m + j : zero); };
+        uint32_t y0 = ub(jm, j0), y1 = 0;
+        GfTab u0 = gf_tab_l(permL, permC, y0), u1 = u0;
+        if (two) {
+            y1 = ub(jm, j1);
+            u1 = gf_tab_l(permL, permC, y1);
+        }
+        uint32_t b0 = 0, b1 = 0;
+        if (m >= 2) {
+            b0 = ub(m - 2, j0);
+            if (two)
+                b1 = ub(m - 2, j1);
+        }
+        for (int i = (int)m - 1; i >= 0; --i) {
+            const GfTab n0 = gf_tab_l(permL, permC, b0);
+            GfTab n1 = u1;
+            if (two)
+                n1 = gf_tab_l(permL, permC, b1);
+            const uint32_t z0 = b0, z1 = b1;
+            if (i >= 2) {
+                b0 = ub((uint32_t)i - 2, j0);
+                if (two)
+                    b1 = ub((uint32_t)i - 2, j1);
+            }
+            const uint32_t q = (uint32_t)i & 63u;
+            const bool lo = i < 64;
+            const uint32_t fb = rl(lo ? f0 : f1, q);
+            const GfTab d{rl(lo ? v0.a0 : v1.a0, q), rl(lo ? v0.a1 : v1.a1, q), rl(lo ? v0.b0 : v1.b0, q),
+                          rl(lo ? v0.b1 : v1.b1, q), rl(lo ? v0.c : v1.c, q)};
+            const uint32_t lc = fb < 32 ? fb : 32;
+            const uint32_t x = uni(gf_mul_tab(rl(lo ? p4[0] : p4[1], q), d)) & byte_mask((int)lc);
+            uint32_t len = 0;
+            const int h = parse_prefix(x, lc, &len);
+            if (h < 1 || len == 0 || (uint32_t)h + len > fb)
+                break;
+            const uint32_t b = (uint32_t)h + len;
+            if (lane == 0) {
+                rw[1 + i] = ((uint32_t)h << 29) | len;
+                opAcc += lc > b ? lc : b;
+                outAcc += b;
+            }
+            ++ok;
+            const uint32_t xi = x & byte_mask((int)b);
+            if (y0) {
+                const uint32_t ab = b < f0 ? b : f0;
+                p4[0] ^= gf_mul_tab(xi & byte_mask((int)ab), u0);
+                opAcc += ab;
+            }
+            if (two && y1) {
+                const uint32_t ab = b < f1 ? b : f1;
+                p4[1] ^= gf_mul_tab(xi & byte_mask((int)ab), u1);
+                opAcc += ab;
+            }
+            u0 = n0;
+            u1 = n1;
+            y0 = z0;
+            y1 = z1;
+        }
+    } else
+#endif
     for (int i = (int)m - 1; i >= 0; --i) {
         const uint8_t* col = Ct + (uint32_t)i * m;
         const uint32_t fb = uni(finB[i]);
@@ -2376,6 +2504,9 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
     uint32_t* finB = lowL + m;
     uint32_t* rw = finB + m;
     uint32_t p4[4];
+#ifdef SGPU_PHASE_CLOCKS
+    const unsigned long long pclk = clock64();
+#endif
     prefix_load(p4, m, lane, sd.head, R);
     for (uint32_t y = lane; y < 256; y += 64) {
         const uint32_t* t = c_perm[y];
@@ -2391,7 +2522,23 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
         finB[j] = R[j].finalBytes;
     }
     __syncthreads();
+#ifdef SGPU_PHASE_CLOCKS
+    // slots 44-47: setup clocks, solve clocks, sum of m, the largest solve's clocks
+    const unsigned long long sclk = clock64();
+    if (lane == 0) {
+        atomicAdd(&g_phaseClk[44], sclk - pclk);
+        atomicAdd(&g_phaseClk[46], (unsigned long long)m);
+        atomicAdd(&g_phaseClk[49], sclk);
+    }
+#endif
     solve_prefix_wave(m, lane, p4, Ct, lowL, finB, permL, permC, rw, results + sd.result, acct);
+#ifdef SGPU_PHASE_CLOCKS
+    if (lane == 0) {
+        const unsigned long long e = clock64();
+        atomicAdd(&g_phaseClk[45], e - sclk);
+        atomicMax(&g_phaseClk[47], (e - pclk) << 8 | (m & 0xffu));
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2652,7 +2799,7 @@ extern "C" __attribute__((visibility("default"))) void sgpu_debug_phase_clocks(u
 {
     bind_device();
     (void)hipDeviceSynchronize();
-    (void)hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_phaseClk), 48 * sizeof(unsigned long long));
+    (void)hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_phaseClk), 64 * sizeof(unsigned long long));
 }
 #endif
 

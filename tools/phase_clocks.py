@@ -2,7 +2,7 @@
 """Per-phase shader clocks of k_exec's OP_ROWS path (profiling build:
 tools/build_variant.sh phase -DSGPU_PHASE_CLOCKS).  Runs a short C4 bench
 through the variant library, then prints the clocks per workgroup-op.
-usage: python tools/phase_clocks.py siamese_amd/libsiamese_amd_phase.so"""
+usage: python tools/phase_clocks.py siamese_amd/libsiamese_amd_phase.so [bench options]"""
 import ctypes
 import sys
 import os
@@ -12,9 +12,9 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 lib = sys.argv[1]
-bench.main(["--library", lib, "--steps", "3", "--warmup", "1", "--no-cpu", "--no-e2e", "--no-legs"])
+bench.main(["--library", lib, "--steps", "3", "--warmup", "1", "--no-cpu", "--no-e2e", "--no-legs"] + sys.argv[2:])
 L = ctypes.CDLL(os.path.abspath(lib))
-out = (ctypes.c_ulonglong * 48)()
+out = (ctypes.c_ulonglong * 64)()
 L.sgpu_debug_phase_clocks(out)
 ops = max(1, out[8])
 names = ["block load", "stage+plan", "sum updates", "stage sums", "sums barrier", "rows"]
@@ -35,3 +35,9 @@ for k, nm in enumerate(["LINCOMB", "LITERAL", "ROWS", "COPIES", "LINCOMBS"]):
         nm, c, out[33 + k] / max(1, c), out[33 + k] / wgs))
 print("OP_ROWS: thread 0 waits %.0f clocks per op at the op's closing barrier (other waves still in the rows phase)"
       % (out[43] / max(1, out[40])))
+if out[46]:
+    big = out[47]
+    print("k_solve_prefix: setup %.0f, solve %.0f clocks per row (summed over solves); slowest wave %d clocks (m=%d)"
+          % (out[44] / out[46], out[45] / out[46], big >> 8, big & 0xff))
+    low = out[48] - out[49]
+    print("  lower sweep %.0f, back-substitution %.0f clocks per row" % (low / out[46], (out[45] - low) / out[46]))

@@ -18,7 +18,7 @@ sess = S.BatchSession(lib, cfg, device=0)
 res, rep = sess.run(steps=1, warmup=0, verify=False, groups=groups, digest=False, defer=defer)
 sess.close()
 L = ctypes.CDLL(os.path.abspath(lib))
-out = (ctypes.c_ulonglong * 32)()
+out = (ctypes.c_ulonglong * 64)()
 L.sgpu_debug_phase_clocks(out)
 ops = max(1, out[8])
 names = ["block load", "stage+plan", "sum updates", "stage sums", "sums barrier", "rows"]

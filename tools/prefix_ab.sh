@@ -13,8 +13,9 @@ for v in base pipe; do
   D=gpurun_out/pab_${TAG}_$v
   timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o t -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-legs --library $lib > $D.log 2>&1
   echo "== $v $(grep -o '"rank0_digest": [0-9]*' $D.log)" >> $OUT
-  grep -h "k_solve" $D/*kernel_stats.csv | cut -d, -f1-4 | sed 's/(.*)"/"/' >> $OUT
+  python3 tools/kstats.py $D >> $OUT
 done
 cat $OUT
+[ -n "$2" ] || exit 0
 bash tools/pmc_exec.sh > gpurun_out/pmc_$TAG.txt 2>&1
 tail -n 30 gpurun_out/pmc_$TAG.txt
