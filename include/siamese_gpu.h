@@ -203,8 +203,9 @@ SIAMESE_EXPORT unsigned sgpu_frame_header_bytes(unsigned type, unsigned dataByte
 /// follows it.  Returns the header size, 0 on invalid input.
 SIAMESE_EXPORT unsigned sgpu_frame_write_header(unsigned type, unsigned flow, unsigned packetNum,
                                                 unsigned dataBytes, void* out);
-/// Parse up to maxFrames frames of frames[0, bytes) (host memory).
-/// InvalidInput on a malformed frame or when more frames remain.
+/// Parse up to maxFrames frames of frames[0, bytes) (host memory, bytes <
+/// 4 GiB).  InvalidInput on a malformed frame or when more frames remain;
+/// the frames before a malformed one are still returned (*countOut).
 SIAMESE_EXPORT SiameseResult sgpu_frames_parse(const void* frames, size_t bytes, SgpuFrame* out,
                                                unsigned maxFrames, unsigned* countOut);
 /// Packet ingest: the frames in hostFrames[0, bytes) (pinned host memory)
@@ -215,6 +216,8 @@ SIAMESE_EXPORT SiameseResult sgpu_frames_parse(const void* frames, size_t bytes,
 /// the bytes copied from the device copy by the next submission, which
 /// waits for the staging copy on the device).  results[i] (optional) is the
 /// call's result for frame i (InvalidInput for a flow without a decoder).
+/// A malformed frame ends the call: every frame before it is delivered and
+/// counted in *countOut, and the call returns InvalidInput.  bytes < 4 GiB.
 /// The decoders must not be driven concurrently with this call; deviceFrames
 /// stays untouched until the next submission has completed.
 SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsigned decoderCount,
@@ -225,7 +228,8 @@ SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsig
 /// sgpu_gather_async: same lifetime rule for the packets).  Frame i starts
 /// at a 16-byte boundary, zero padding between frames.  *bytesOut = the
 /// frame stream's length (<= capacity).  Returns a gather ticket for
-/// sgpu_gather_wait, -1 on failure (capacity too small, device fault).
+/// sgpu_gather_wait, -1 on failure (capacity too small, a packet of 0 or more
+/// than SIAMESE_MAX_PACKET_BYTES bytes, device fault).
 SIAMESE_EXPORT long long sgpu_frames_send(unsigned count, const SgpuRecoveryPacket* packets, const unsigned* flows,
                                           void* pinnedOut, size_t capacity, size_t* bytesOut);
 

@@ -18,6 +18,10 @@ const char* be_name();
 void* be_dev_alloc(size_t bytes);
 void be_dev_free(void* p);
 void* be_host_alloc(size_t bytes);   // page-locked
+/// Page-locked, mapped and coherent host memory: kernels read and write it
+/// directly (zero-copy uploads, k_hostcopy downloads), and a buffer rewritten
+/// between submissions is never seen stale through a device cache.
+void* be_host_alloc_mapped(size_t bytes);
 /// The device's address of page-locked host memory (kernels read it over
 /// the bus: zero-copy).
 void* be_host_device_ptr(void* host);

@@ -2828,6 +2828,15 @@ void* be_host_alloc(size_t bytes)
     return p;
 }
 
+void* be_host_alloc_mapped(size_t bytes)
+{
+    bind_device();
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return nullptr;
+    return p;
+}
+
 void* be_host_device_ptr(void* host)
 {
     bind_device();
@@ -2904,8 +2913,14 @@ void be_copy_pinned(const BeCopy* ranges, unsigned count, bool toDevice)
     }
     HostCopyArgs a;
     std::memset(&a, 0, sizeof(a));
-    for (unsigned i = 0; i < count; ++i)
+    for (unsigned i = 0; i < count; ++i) {
         a.r[i] = ranges[i];
+        // the host side as the device addresses it (mapped pinned memory)
+        uint64_t& h = toDevice ? a.r[i].src : a.r[i].dst;
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, (void*)(uintptr_t)h, 0) == hipSuccess && d)
+            h = (uint64_t)(uintptr_t)d;
+    }
     a.count = count;
     const uint64_t perBlock = (uint64_t)kHostCopyThreads * 16u * 4u;   // four words per thread
     const unsigned blocks = (unsigned)std::min<uint64_t>(64, (most + perBlock - 1) / perBlock);

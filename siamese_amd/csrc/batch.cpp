@@ -342,16 +342,16 @@ SIAMESE_EXPORT SiameseResult sgpu_frames_parse(const void* frames, size_t bytes,
 {
     if (!frames || !out || !countOut)
         return Siamese_InvalidInput;
+    *countOut = 0;
+    if (bytes > UINT32_MAX)   // (frame offsets are 32-bit)
+        return Siamese_InvalidInput;
     static_assert(sizeof(SgpuFrame) == sizeof(FrameInfo), "SgpuFrame layout");
     size_t consumed = 0, bad = 0;
     const long n = frames_parse(static_cast<const uint8_t*>(frames), bytes, reinterpret_cast<FrameInfo*>(out),
                                 maxFrames, &consumed, &bad);
-    if (n < 0) {
-        *countOut = 0;
-        return Siamese_InvalidInput;
-    }
+    // (the frames before a malformed one are returned with InvalidInput)
     *countOut = (unsigned)n;
-    return consumed == bytes ? Siamese_Success : Siamese_InvalidInput;
+    return consumed == bytes && bad == kNoBadFrame ? Siamese_Success : Siamese_InvalidInput;
 }
 
 SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsigned decoderCount,
@@ -361,6 +361,8 @@ SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsig
     if (!decoders || !hostFrames || !deviceFrames || !countOut)
         return Siamese_InvalidInput;
     *countOut = 0;
+    if (bytes > UINT32_MAX)   // (frame offsets are 32-bit)
+        return Siamese_InvalidInput;
     const uint8_t* host = static_cast<const uint8_t*>(hostFrames);
     const uint64_t dev = (uint64_t)(uintptr_t)deviceFrames;
     // parse in blocks: the headers of a whole ring in one pass, then the calls
@@ -368,12 +370,15 @@ SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsig
     size_t at = 0;
     unsigned done = 0;
     SiameseResult status = Siamese_Success;
-    while (at < bytes && done < maxFrames) {
+    bool malformed = false;
+    while (at < bytes && done < maxFrames && !malformed) {
         size_t consumed = 0, bad = 0;
         const size_t want = std::min<size_t>(256, maxFrames - done);
         const long n = frames_parse(host + at, bytes - at, fi, want, &consumed, &bad);
-        if (n < 0)
-            return Siamese_InvalidInput;
+        // every well-formed frame before a malformed one is still delivered;
+        // the ring is not read past the malformed frame (its length cannot be
+        // trusted to find the next one)
+        malformed = bad != kNoBadFrame;
         for (long k = 0; k < n; ++k) {
             const FrameInfo& f = fi[k];
             const size_t off = at + f.offset;
@@ -412,7 +417,7 @@ SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsig
             break;
     }
     *countOut = done;
-    return at >= bytes ? status : Siamese_InvalidInput;
+    return at >= bytes && !malformed ? status : Siamese_InvalidInput;
 }
 
 SIAMESE_EXPORT long long sgpu_frames_send(unsigned count, const SgpuRecoveryPacket* packets, const unsigned* flows,
@@ -425,7 +430,9 @@ SIAMESE_EXPORT long long sgpu_frames_send(unsigned count, const SgpuRecoveryPack
     std::vector<uint8_t> hdr((size_t)count * 8);
     size_t total = 0;
     for (unsigned i = 0; i < count; ++i) {
-        if (!packets[i].DeviceData || flows[i] > kFrameMaxFlow)
+        // (as sgpu_frame_write_header: an empty or oversized packet is no frame)
+        if (!packets[i].DeviceData || flows[i] > kFrameMaxFlow || packets[i].DataBytes == 0 ||
+            packets[i].DataBytes > SIAMESE_MAX_PACKET_BYTES)
             return -1;
         srcs[i] = packets[i].DeviceData;
         lens[i] = packets[i].DataBytes;

@@ -1043,7 +1043,7 @@ void Engine::ensure_up(XferSet& x, size_t bytes)
         be_host_free(x.upHost);
     if (x.upDev)
         be_dev_free(x.upDev);
-    x.upHost = (uint8_t*)be_host_alloc(cap);
+    x.upHost = (uint8_t*)be_host_alloc_mapped(cap);
     x.upDev = (uint8_t*)be_dev_alloc(cap);
     x.upHostDev = x.upHost ? (uint8_t*)be_host_device_ptr(x.upHost) : nullptr;
     x.upCap = cap;
@@ -1073,7 +1073,7 @@ void Engine::ensure_down(XferSet& x, size_t bytes)
         be_host_free(x.downHost);
     if (x.downDev)
         be_dev_free(x.downDev);
-    x.downHost = (uint8_t*)be_host_alloc(cap);
+    x.downHost = (uint8_t*)be_host_alloc_mapped(cap);
     x.downDev = (uint8_t*)be_dev_alloc(cap);
     x.downCap = cap;
     x.acctZero = true;
@@ -1345,8 +1345,13 @@ bool Engine::flush_and_sync()
     bool inl = false;
     if (kInline && !async_assembly()) {
         std::lock_guard<std::mutex> g(qMu_);
+        // Inline only when the ticket's transfer set is free right now, and
+        // claimed in this same critical section: a later ticket of the same
+        // set (T + kSets) could otherwise claim it first and then wait in
+        // toLaunch_ behind inlineBusy_ while this caller waits for the set.
         if (toLaunch_.empty() && toComplete_.empty() && !launching_ && !completing_ && !inlineBusy_ &&
-            doneTicket_ + 1 == ticket) {
+            doneTicket_ + 1 == ticket && sets_[b->set].busyTicket == 0) {
+            sets_[b->set].busyTicket = ticket;
             inlineBusy_ = true;   // (the launcher waits: its stream order stays ticket order)
             inl = true;
         }
@@ -1365,8 +1370,7 @@ bool Engine::flush_and_sync()
         return wait(ticket) && !failed();
     }
     tl("inline", ticket);
-    claim_set(*b);
-    assemble_batch(*b, pool());
+    assemble_batch(*b, pool());   // (the set was claimed above)
     if (!failed())
         launch_batch(*b);
     if (complete_batch(*b))

@@ -40,6 +40,7 @@ long frames_parse(const uint8_t* buf, size_t bytes, FrameInfo* out, size_t maxFr
                   size_t* badOffset)
 {
     size_t at = 0, n = 0;
+    *badOffset = kNoBadFrame;
     while (at < bytes && n < maxFrames) {
         if (buf[at] == 0) {   // empty frame: padding
             ++at;
@@ -50,7 +51,7 @@ long frames_parse(const uint8_t* buf, size_t bytes, FrameInfo* out, size_t maxFr
         const int h = read_length_prefix(buf + at, left < 4 ? (unsigned)left : 4u, &length);
         if (h < 1 || (size_t)h + length > left || length < 1) {
             *badOffset = at;
-            return -1;
+            break;
         }
         const uint8_t* f = buf + at + h;
         FrameInfo& fi = out[n];
@@ -58,7 +59,7 @@ long frames_parse(const uint8_t* buf, size_t bytes, FrameInfo* out, size_t maxFr
         if (fi.type == kFrameOriginal) {
             if (length <= kOriginalHeader) {
                 *badOffset = at;
-                return -1;
+                break;
             }
             fi.flow = f[1] | ((uint32_t)f[2] << 8) | ((uint32_t)f[3] << 16);
             fi.packetNum = f[4] | ((uint32_t)f[5] << 8) | ((uint32_t)f[6] << 16);
@@ -67,7 +68,7 @@ long frames_parse(const uint8_t* buf, size_t bytes, FrameInfo* out, size_t maxFr
         } else if (fi.type == kFrameRecovery) {
             if (length <= kRecoveryHeader) {
                 *badOffset = at;
-                return -1;
+                break;
             }
             fi.flow = f[1] | ((uint32_t)f[2] << 8) | ((uint32_t)f[3] << 16);
             fi.packetNum = 0;
@@ -75,7 +76,7 @@ long frames_parse(const uint8_t* buf, size_t bytes, FrameInfo* out, size_t maxFr
             fi.bytes = length - kRecoveryHeader;
         } else {
             *badOffset = at;
-            return -1;
+            break;
         }
         ++n;
         at += (size_t)h + length;

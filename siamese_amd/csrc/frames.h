@@ -39,8 +39,12 @@ struct FrameInfo
 unsigned frame_header_bytes(unsigned type, unsigned dataBytes);
 /// Writes the header; returns its size (frame_header_bytes).
 unsigned frame_write_header(unsigned type, unsigned flow, unsigned packetNum, unsigned dataBytes, uint8_t* out);
-/// Parses frames from buf[0, bytes).  Returns the number of frames written to
-/// out (at most maxFrames), or -1 on a malformed frame (*badOffset = where).
+/// No malformed frame was met (frames_parse's *badOffset).
+constexpr size_t kNoBadFrame = ~(size_t)0;
+/// Parses frames from buf[0, bytes) (bytes < 4 GiB: offsets are 32-bit).
+/// Returns the number of frames written to out (at most maxFrames).  Stops
+/// at a malformed frame with *badOffset = where it starts (kNoBadFrame
+/// otherwise): the frames before it are in out and *consumed = *badOffset.
 /// Stops early (returning maxFrames) when out is full: *consumed says how far.
 long frames_parse(const uint8_t* buf, size_t bytes, FrameInfo* out, size_t maxFrames, size_t* consumed,
                   size_t* badOffset);

@@ -337,6 +337,7 @@ void* be_dev_alloc(size_t bytes)
 }
 void be_dev_free(void* p) { std::free(p); }
 void* be_host_alloc(size_t bytes) { return be_dev_alloc(bytes); }
+void* be_host_alloc_mapped(size_t bytes) { return be_dev_alloc(bytes); }
 void be_host_free(void* p) { std::free(p); }
 void be_h2d(void* dst, const void* src, size_t bytes) { std::memcpy(dst, src, bytes); }
 void* be_host_device_ptr(void* host) { return host; }

@@ -131,6 +131,86 @@ def test_bulk_recv_routes_interleaved_frames():
     L.sgpu_device_free(dev)
 
 
+def test_frames_parse_returns_frames_before_malformed():
+    """A malformed frame in the middle of a ring: the frames before it are
+    returned (with InvalidInput), nothing after it."""
+    L = _lib(S.SIM_LIB)
+    good = [_frame(L, 0, 1, k, bytes([k]) * 40) for k in range(3)]
+    ring = good[0] + good[1] + bytes([4, 7]) + b"abcd" + good[2]
+    out = (Frame * 8)()
+    n = ctypes.c_uint()
+    assert L.sgpu_frames_parse(ring, len(ring), out, 8, ctypes.byref(n)) != 0
+    assert n.value == 2 and [f.PacketNum for f in out[:2]] == [0, 1]
+
+
+def test_bulk_recv_delivers_frames_before_malformed():
+    """sgpu_frames_recv over a ring with one corrupt datagram in the middle
+    of a 256-frame parse block: every frame before it reaches its decoder and
+    is counted; the call reports InvalidInput and reads no further."""
+    L = _lib(S.SIM_LIB)
+    assert L.sgpu_init(-1) == 0
+    L.sgpu_decoder_create.restype = ctypes.c_void_p
+    L.sgpu_decoder_free.argtypes = [ctypes.c_void_p]
+    L.sgpu_decoder_has.argtypes = [ctypes.c_void_p, ctypes.c_uint]
+    L.sgpu_device_alloc.restype = ctypes.c_void_p
+    L.sgpu_device_alloc.argtypes = [ctypes.c_size_t]
+    L.sgpu_device_free.argtypes = [ctypes.c_void_p]
+    L.sgpu_h2d.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    L.sgpu_flush.restype = ctypes.c_int
+    L.sgpu_frames_recv.restype = ctypes.c_int
+    L.sgpu_frames_recv.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_size_t, ctypes.POINTER(ctypes.c_int), ctypes.c_uint,
+                                   ctypes.POINTER(ctypes.c_uint)]
+    decs = (ctypes.c_void_p * 1)(L.sgpu_decoder_create())
+    # 300 good frames (past the first 256-frame block), a corrupt one, 5 more
+    ring = b"".join(_frame(L, 0, 0, k, bytes([k & 255]) * 20) for k in range(300))
+    ring += bytes([0x85])                                    # cut-off length prefix...
+    ring += bytes([9, 9, 9])                                 # ...with garbage after it
+    ring += b"".join(_frame(L, 0, 0, k, b"late" * 5) for k in range(300, 305))
+    dev = L.sgpu_device_alloc(len(ring))
+    host = ctypes.create_string_buffer(ring, len(ring))
+    assert L.sgpu_h2d(dev, host, len(ring)) == 0
+    res = (ctypes.c_int * 400)()
+    n = ctypes.c_uint()
+    assert L.sgpu_frames_recv(decs, 1, host, dev, len(ring), res, 400, ctypes.byref(n)) == 1   # InvalidInput
+    assert n.value == 300 and list(res[:300]) == [0] * 300
+    assert L.sgpu_flush() == 0
+    assert all(L.sgpu_decoder_has(decs[0], k) == 0 for k in (0, 255, 256, 299))
+    assert L.sgpu_decoder_has(decs[0], 300) == 2
+    L.sgpu_decoder_free(decs[0])
+    L.sgpu_device_free(dev)
+
+
+def test_frames_send_rejects_empty_and_oversized():
+    """sgpu_frames_send frames no packet sgpu_frame_write_header would refuse
+    (a 0-byte packet would be a bare header the receiver rejects)."""
+    L = _lib(S.SIM_LIB)
+    assert L.sgpu_init(-1) == 0
+
+    class Rec(ctypes.Structure):
+        _fields_ = [("DeviceData", ctypes.c_void_p), ("DataBytes", ctypes.c_uint), ("FooterBytes", ctypes.c_uint),
+                    ("Footer", ctypes.c_ubyte * 8), ("Head", ctypes.c_ubyte * 4), ("Producer", ctypes.c_void_p)]
+
+    L.sgpu_frames_send.restype = ctypes.c_longlong
+    L.sgpu_frames_send.argtypes = [ctypes.c_uint, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint), ctypes.c_void_p,
+                                   ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+    L.sgpu_device_alloc.restype = ctypes.c_void_p
+    L.sgpu_device_alloc.argtypes = [ctypes.c_size_t]
+    L.sgpu_device_free.argtypes = [ctypes.c_void_p]
+    L.sgpu_host_alloc.restype = ctypes.c_void_p
+    L.sgpu_host_alloc.argtypes = [ctypes.c_size_t]
+    L.sgpu_host_free.argtypes = [ctypes.c_void_p]
+    dev = L.sgpu_device_alloc(4096)
+    pinned = L.sgpu_host_alloc(1 << 20)
+    flows = (ctypes.c_uint * 1)(3)
+    used = ctypes.c_size_t()
+    for bad in (0, 536870912):   # (SIAMESE_MAX_PACKET_BYTES + 1)
+        pk = Rec(dev, bad)
+        assert L.sgpu_frames_send(1, ctypes.byref(pk), flows, pinned, 1 << 20, ctypes.byref(used)) == -1
+    L.sgpu_host_free(pinned)
+    L.sgpu_device_free(dev)
+
+
 @pytest.mark.parametrize("name", ["C1", "C1var", "C2x64", "smoke_C4x8", "edge_var_block", "edge_lag"])
 def test_hostsim_frames_match_golden(name):
     """Originals arrive as frames in a pinned ring (staged per job) and go

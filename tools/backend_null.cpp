@@ -58,6 +58,7 @@ void* be_dev_alloc(size_t bytes)
 }
 void be_dev_free(void* p) { std::free(p); }
 void* be_host_alloc(size_t bytes) { return be_dev_alloc(bytes); }
+void* be_host_alloc_mapped(size_t bytes) { return be_dev_alloc(bytes); }
 void be_host_free(void* p) { std::free(p); }
 void* be_host_device_ptr(void*) { return nullptr; }   // (no zero-copy: uploads stay DMA-shaped)
 void be_h2d(void* dst, const void* src, size_t bytes)
