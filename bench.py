@@ -64,9 +64,13 @@ def pmc_traffic(kernel):
         return None, None
 
 
-def workload(rank, streams):
+def workload(rank, streams, ranges=True):
+    """The C4 shard of `rank`.  ranges: each stream's originals go to its
+    encoder and decoder in range calls (sgpu_encoder_add_range,
+    sgpu_decoder_add_original_range, sgpu_decoder_get_range), the same
+    data-plane work as the per-packet calls (harness Stream::add_ranges)."""
     return S.replace(S.CONFIGS["C4"], streams=streams, first_stream=rank * streams,
-                     hash_data=0)
+                     hash_data=0, add_ranges=1 if ranges else 0)
 
 
 def symbol_bytes(payload):
@@ -301,7 +305,7 @@ def legs(library, device, threads, use_cpu):
 def run_rank(rank, world, local, args, library, use_cuda):
     """One rank's share: returns the JSON line on rank 0, None elsewhere."""
     coll = Collective(world)
-    cfg = workload(rank, args.streams)
+    cfg = workload(rank, args.streams, args.ranges)
     device = local if use_cuda else -1
     sess = S.BatchSession(library, cfg, device=device)
     # untimed warm-up; its first run checks every recovered byte against the payload
@@ -395,6 +399,8 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "originals": 256,
             "payload_bytes": 1400,
             "loss_pct": 20,
+            "add_calls": "range (sgpu_encoder_add_range / sgpu_decoder_add_original_range)"
+                         if args.ranges else "per packet",
             "parallelism": "independent streams sharded by index (weak scaling), "
                            "one process per GPU, gloo host barrier",
         },
@@ -524,6 +530,8 @@ def main(argv=None):
                     help="skip the PCIe-inclusive end-to-end leg")
     ap.add_argument("--no-frames", dest="frames", action="store_false",
                     help="end-to-end leg with raw payloads instead of framed datagrams")
+    ap.add_argument("--no-ranges", dest="ranges", action="store_false",
+                    help="headline originals through per-packet add/get calls instead of range calls")
     ap.add_argument("--no-legs", dest="legs", action="store_false",
                     help="skip the C2/C3/C5 legs (N=1)")
     ap.add_argument("--library", default=S.AMD_LIB, help=argparse.SUPPRESS)

@@ -118,6 +118,7 @@ struct ScenarioConfig
     uint32_t tail_limit;        ///< extra encodes after the last original / block limit
     uint32_t seed;              ///< loss channel seed (1013 = reference kSeed)
     uint32_t hash_data;         ///< 1: digests cover packet bytes; 0: lengths only
+    uint32_t add_ranges;        ///< block mode: originals added by range calls (see Stream::add_ranges)
 };
 
 /// Per-stream outcome (ctypes-visible).
@@ -168,6 +169,13 @@ inline uint64_t ev(uint64_t type, uint64_t result, uint64_t a = 0, uint64_t b = 
       uint64_t rec_token(const Rec& rec);
       uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok);
       bool wants_yield_after_decode();        // batch: lengths known after a flush
+
+    Range calls (cfg->add_ranges, block mode; every codec supports them, a
+    per-call API as loops of its single calls):
+
+      int  enc_add_range(unsigned firstId, unsigned count, unsigned* firstNum, unsigned* added);
+      int  dec_add_range(unsigned firstId, unsigned firstNum, unsigned count, int* results, unsigned* calls);
+      int  dec_get_range(unsigned firstNum, unsigned count, Pkt* out, unsigned* got);
 */
 
 inline uint64_t data_token(bool hashData, const uint8_t* p, unsigned bytes)
@@ -254,6 +262,84 @@ struct Stream
         return true;
     }
 
+    // Range form of deliver(): one get_range from nextExpected.
+    bool deliver_range()
+    {
+        if (nextExpected >= cfg->originals)
+            return true;
+        std::vector<Pkt>& got = decoded;   // (empty outside the DECODED phase)
+        got.resize(cfg->originals - nextExpected);
+        unsigned n = 0;
+        const int r = codec->dec_get_range(nextExpected, (unsigned)got.size(), got.data(), &n);
+        for (unsigned k = 0; k < n; ++k) {
+            note(ev(EV_GET, 0, nextExpected));
+            note(codec->pkt_token(got[k], packet_id(nextExpected), &dataOk));
+            ++nextExpected;
+            ++res->delivered;
+        }
+        got.clear();
+        if (r != 0)
+            note(ev(EV_GET, r, nextExpected));
+        return r == 0 || r == 2;
+    }
+
+    // Block mode, cfg->add_ranges: every original in range calls.  The
+    // encoder takes them all in one call; the loss channel draws as the
+    // per-call sequence does (one draw per original added, in order); each
+    // run of consecutive received originals goes to the decoder in one call,
+    // after which the in-order packets are delivered by one get_range.  The
+    // event log records every call's observed results: the same events as
+    // the per-call sequence, without its NeedMoreData probes of packets not
+    // yet added (a run's deliveries are fetched once the run is in).
+    void add_ranges()
+    {
+        const unsigned n = cfg->originals - i;
+        unsigned first = 0, added = 0;
+        const int r = codec->enc_add_range(packet_id(i), n, &first, &added);
+        const unsigned i0 = i;
+        std::vector<uint8_t> lost(added);
+        for (unsigned k = 0; k < added; ++k) {
+            const unsigned num = (first + k) & 0x3fffff;
+            note(ev(EV_ENC_ADD, 0, num));
+            res->payload_bytes += packet_bytes(packet_id(i0 + k));
+            lost[k] = (loss.next() % 100) < cfg->loss_pct;
+            if (lost[k])
+                ++res->originals_lost;
+        }
+        lastNum = added ? ((first + added - 1) & 0x3fffff) : lastNum;
+        if (r != 0) {
+            note(ev(EV_ENC_ADD, r, 0));
+            fail(2);
+            return;
+        }
+        std::vector<int> results;
+        for (unsigned k = 0; k < added;) {
+            if (lost[k]) {
+                ++k;
+                continue;
+            }
+            unsigned e = k;
+            while (e < added && !lost[e])
+                ++e;
+            const unsigned num0 = (first + k) & 0x3fffff;
+            results.assign(e - k, 0);
+            unsigned calls = 0;
+            const int a = codec->dec_add_range(packet_id(i0 + k), num0, e - k, results.data(), &calls);
+            for (unsigned j = 0; j < calls; ++j)
+                note(ev(EV_DEC_ADD_ORIG, results[j], (num0 + j) & 0x3fffff));
+            if ((a != 0 && a != 4) || calls != e - k) {
+                fail(2);
+                return;
+            }
+            if (nextExpected >= i0 + k && nextExpected < i0 + e && !deliver_range()) {
+                fail(2);
+                return;
+            }
+            k = e;
+        }
+        i += added;
+    }
+
     // One encode + channel + add_recovery.
     void encode_once()
     {
@@ -292,6 +378,10 @@ struct Stream
             if (i >= cfg->originals) {
                 tailMode = true;
                 phase = TAIL;
+                return false;
+            }
+            if (cfg->add_ranges && cfg->block_mode) {
+                add_ranges();
                 return false;
             }
             const unsigned id = packet_id(i);

@@ -99,6 +99,11 @@ struct Api
     SiameseResult (*decoder_get)(SgpuDecoder, SiameseOriginalPacket*);
     SiameseResult (*decode_deferred)(SgpuDecoder, SiameseOriginalPacket*, unsigned, unsigned*);
     SiameseResult (*decoder_get_deferred)(SgpuDecoder, SiameseOriginalPacket*);
+    SiameseResult (*encoder_add_range)(SgpuEncoder, const void*, size_t, const unsigned*, unsigned, unsigned,
+                                       unsigned*, unsigned*);
+    SiameseResult (*decoder_add_original_range)(SgpuDecoder, unsigned, const void*, size_t, const unsigned*,
+                                                unsigned, unsigned, SiameseResult*, unsigned*);
+    SiameseResult (*decoder_get_range)(SgpuDecoder, unsigned, unsigned, SiameseOriginalPacket*, unsigned*);
     int (*flush)(void);
     int (*submit)(void);
     long long (*enqueue)(void);
@@ -166,7 +171,10 @@ bool load_api(const char* path, Api& a)
            bind(h, a.frame_write_header, "sgpu_frame_write_header") && bind(h, a.frames_parse, "sgpu_frames_parse") &&
            bind(h, a.frames_recv, "sgpu_frames_recv") && bind(h, a.frames_send, "sgpu_frames_send") &&
            bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats") &&
-           bind(h, a.arena_bytes, "sgpu_arena_bytes") && bind(h, a.arena_reserve, "sgpu_arena_reserve");
+           bind(h, a.arena_bytes, "sgpu_arena_bytes") && bind(h, a.arena_reserve, "sgpu_arena_reserve") &&
+           bind(h, a.encoder_add_range, "sgpu_encoder_add_range") &&
+           bind(h, a.decoder_add_original_range, "sgpu_decoder_add_original_range") &&
+           bind(h, a.decoder_get_range, "sgpu_decoder_get_range");
 }
 
 struct Rec
@@ -363,6 +371,85 @@ struct BatchCodec
         return r;
     }
     int enc_remove_before(unsigned num) { return sh->api->encoder_remove_before(enc, num); }
+
+    // range calls (Stream::add_ranges): the originals of consecutive ids lie
+    // at one stride in the device payload area
+    std::vector<unsigned> lens;
+    const unsigned* range_lens(unsigned firstId, unsigned count)
+    {
+        if (sh->cfg->payload_bytes)
+            return nullptr;
+        lens.resize(count);
+        for (unsigned k = 0; k < count; ++k)
+            lens[k] = scen::variable_bytes(firstId + k);
+        return lens.data();
+    }
+    unsigned payload_bytes_of(unsigned id) const
+    {
+        return sh->cfg->payload_bytes ? sh->cfg->payload_bytes : scen::variable_bytes(id);
+    }
+    int enc_add_range(unsigned firstId, unsigned count, unsigned* firstNum, unsigned* added)
+    {
+        if (sh->frames) {   // (frames: datagrams one at a time)
+            *added = 0;
+            for (unsigned k = 0; k < count; ++k) {
+                unsigned num = 0;
+                const int r = enc_add(firstId + k, nullptr, payload_bytes_of(firstId + k), &num);
+                if (r != 0)
+                    return r;
+                if (k == 0)
+                    *firstNum = num;
+                ++*added;
+            }
+            return 0;
+        }
+        const unsigned* l = range_lens(firstId, count);
+        return sh->api->encoder_add_range(enc, dev_payload(firstId), sh->stride, l, sh->cfg->payload_bytes, count,
+                                          firstNum, added);
+    }
+    int dec_add_range(unsigned firstId, unsigned firstNum, unsigned count, int* results, unsigned* calls)
+    {
+        if (sh->frames) {
+            *calls = 0;
+            for (unsigned k = 0; k < count; ++k) {
+                const int r = dec_add_original(firstId + k, (firstNum + k) & 0x3fffff, nullptr,
+                                               payload_bytes_of(firstId + k));
+                results[k] = r;
+                ++*calls;
+                if (r != 0 && r != 4)
+                    return r;
+            }
+            return 0;
+        }
+        const unsigned* l = range_lens(firstId, count);
+        static_assert(sizeof(SiameseResult) == sizeof(int), "result array");
+        return sh->api->decoder_add_original_range(dec, firstNum, dev_payload(firstId), sh->stride, l,
+                                                   sh->cfg->payload_bytes, count,
+                                                   reinterpret_cast<SiameseResult*>(results), calls);
+    }
+    std::vector<SiameseOriginalPacket> gets;
+    int dec_get_range(unsigned firstNum, unsigned count, Pkt* out, unsigned* got)
+    {
+        if (sh->defer) {   // (deferred entries: one call each)
+            *got = 0;
+            for (unsigned k = 0; k < count; ++k) {
+                const int r = dec_get((firstNum + k) & 0x3fffff, &out[k]);
+                if (r != 0)
+                    return r;
+                ++*got;
+            }
+            return 0;
+        }
+        gets.resize(count);
+        const int r = sh->api->decoder_get_range(dec, firstNum, count, gets.data(), got);
+        for (unsigned k = 0; k < *got; ++k) {
+            out[k].num = gets[k].PacketNum;
+            out[k].bytes = gets[k].DataBytes;
+            out[k].data = gets[k].Data;
+            out[k].entry = nullptr;
+        }
+        return r;
+    }
 
     uint64_t rec_token(const Rec& r)
     {

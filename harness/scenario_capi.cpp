@@ -199,6 +199,57 @@ struct CapiCodec
         Timer t(seconds, calls[kRemove]);
         return api->encoder_remove_before(enc, num);
     }
+    // range calls as loops of the single calls (Stream::add_ranges)
+    std::vector<uint8_t> pbuf;
+    const uint8_t* payload(unsigned id, unsigned* bytes)
+    {
+        *bytes = cfg->payload_bytes ? cfg->payload_bytes : scen::variable_bytes(id);
+        pbuf.resize(*bytes + 8);
+        scen::fill_payload(id, pbuf.data(), *bytes);
+        return pbuf.data();
+    }
+    int enc_add_range(unsigned firstId, unsigned count, unsigned* firstNum, unsigned* added)
+    {
+        *added = 0;
+        *firstNum = 0;
+        for (unsigned k = 0; k < count; ++k) {
+            unsigned bytes = 0, num = 0;
+            const uint8_t* d = payload(firstId + k, &bytes);
+            const int r = enc_add(firstId + k, d, bytes, &num);
+            if (r != 0)
+                return r;
+            if (k == 0)
+                *firstNum = num;
+            ++*added;
+        }
+        return 0;
+    }
+    int dec_add_range(unsigned firstId, unsigned firstNum, unsigned count, int* results, unsigned* calls)
+    {
+        *calls = 0;
+        for (unsigned k = 0; k < count; ++k) {
+            unsigned bytes = 0;
+            const uint8_t* d = payload(firstId + k, &bytes);
+            const int r = dec_add_original(firstId + k, (firstNum + k) & 0x3fffff, d, bytes);
+            results[k] = r;
+            ++*calls;
+            if (r != 0 && r != 4)
+                return r;
+        }
+        return 0;
+    }
+    int dec_get_range(unsigned firstNum, unsigned count, Pkt* out, unsigned* got)
+    {
+        *got = 0;
+        for (unsigned k = 0; k < count; ++k) {
+            const int r = dec_get((firstNum + k) & 0x3fffff, &out[k]);
+            if (r != 0)
+                return r;
+            ++*got;
+        }
+        return 0;
+    }
+
     uint64_t rec_token(const Rec& rec) { return scen::data_token(cfg->hash_data, rec.data, rec.bytes); }
     uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok)
     {

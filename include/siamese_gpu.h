@@ -84,6 +84,17 @@ SIAMESE_EXPORT SgpuEncoder sgpu_encoder_create(void);
 SIAMESE_EXPORT void sgpu_encoder_free(SgpuEncoder encoder);
 SIAMESE_EXPORT SiameseResult sgpu_encoder_add(SgpuEncoder encoder, const void* deviceData,
                                               unsigned bytes, unsigned* packetNumOut);
+/// `count` sgpu_encoder_add calls in one: original k's payload at
+/// deviceData + k * stride, bytes[k] bytes (fixedBytes for all when bytes is
+/// NULL).  Identical to the calls made in order until one fails, whose
+/// result is returned (Success if none did); *addedOut = originals added,
+/// the first as packet *firstPacketNumOut and the others after it.  The
+/// originals of one subwindow fill one slab: a run of adds costs one
+/// allocation and one ingest descriptor (the reference's per-packet
+/// siamese_encoder_add, siamese.cpp:96-108).
+SIAMESE_EXPORT SiameseResult sgpu_encoder_add_range(SgpuEncoder encoder, const void* deviceData, size_t stride,
+                                                    const unsigned* bytes, unsigned fixedBytes, unsigned count,
+                                                    unsigned* firstPacketNumOut, unsigned* addedOut);
 SIAMESE_EXPORT SiameseResult sgpu_encoder_remove_before(SgpuEncoder encoder, unsigned firstKept);
 SIAMESE_EXPORT SiameseResult sgpu_encode(SgpuEncoder encoder, SgpuRecoveryPacket* out);
 
@@ -91,6 +102,17 @@ SIAMESE_EXPORT SgpuDecoder sgpu_decoder_create(void);
 SIAMESE_EXPORT void sgpu_decoder_free(SgpuDecoder decoder);
 SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original(SgpuDecoder decoder, unsigned packetNum,
                                                        const void* deviceData, unsigned bytes);
+/// `count` sgpu_decoder_add_original calls in one: packet firstPacketNum + k
+/// with its payload at deviceData + k * stride, bytes[k] bytes (fixedBytes
+/// when bytes is NULL).  results[k] (optional) = call k's result; like the
+/// calls, DuplicateData goes on and any other failure stops the run, its
+/// result returned (Success if none stopped it); *callsOut = calls made.
+/// (siamese_decoder_add_original, siamese.cpp:207-220, per packet.)
+SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original_range(SgpuDecoder decoder, unsigned firstPacketNum,
+                                                             const void* deviceData, size_t stride,
+                                                             const unsigned* bytes, unsigned fixedBytes,
+                                                             unsigned count, SiameseResult* results,
+                                                             unsigned* callsOut);
 SIAMESE_EXPORT SiameseResult sgpu_decoder_add_recovery(SgpuDecoder decoder,
                                                        const SgpuRecoveryPacket* packet);
 SIAMESE_EXPORT SiameseResult sgpu_decoder_is_ready(SgpuDecoder decoder);
@@ -99,6 +121,11 @@ SIAMESE_EXPORT SiameseResult sgpu_decode(SgpuDecoder decoder, SiameseOriginalPac
 /// Returns a device pointer; waits for outstanding work if the packet's
 /// exact length is still being computed.
 SIAMESE_EXPORT SiameseResult sgpu_decoder_get(SgpuDecoder decoder, SiameseOriginalPacket* packet);
+/// sgpu_decoder_get for packets firstPacketNum, firstPacketNum + 1, ... into
+/// packets[0, count) until one does not return Success; *gotOut = packets
+/// returned.  Returns the result of the get that stopped (Success if none).
+SIAMESE_EXPORT SiameseResult sgpu_decoder_get_range(SgpuDecoder decoder, unsigned firstPacketNum, unsigned count,
+                                                    SiameseOriginalPacket* packets, unsigned* gotOut);
 /// sgpu_decode without waiting (see "Deferred outputs" above): the recovered
 /// packets are written to out[0, *countOut), PacketNum at once, Data and
 /// DataBytes at once or when the solve's submission completes.  capacity must

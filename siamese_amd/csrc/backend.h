@@ -45,7 +45,10 @@ void be_copy_pinned(const BeCopy* ranges, unsigned count, bool toDevice);
 
 /// One wave per (descriptor, kIngestChunkBytes chunk): maxBytes is the
 /// largest hdrLen + bytes among the descriptors (sizes the grid).
-void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes);
+/// blocks: the k_ingest block table (nblocks entries, descriptor << 4 |
+/// 4-symbol group of its run), or null for runs of one (one per wave).
+void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes, const uint32_t* blocks = nullptr,
+                      uint32_t nblocks = 0);
 /// `stream`: the instruction words of every segment (see ExecItem).
 /// `acct`: device counter the executor adds the reference's source bytes of
 /// the terms it expands itself (sum updates, LDPC picks) to (ops.h).

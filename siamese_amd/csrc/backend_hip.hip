@@ -15,7 +15,10 @@
 //
 // GF(256) multiply by a wave-uniform constant uses three v_perm_b32 byte
 // lookups per dword (bits 0-2, 3-5, 6-7 of each byte); the 32-byte table per
-// constant lives in constant memory.  HBM traffic, not VALU, is the roofline.
+// constant lives in constant memory.  The algorithmic roofline is HBM
+// bandwidth, but the measured bounds are on-chip: k_exec waits on LDS
+// staging and its per-op barriers (SQ_WAIT_ANY ~60 %, real HBM traffic about
+// a tenth of peak), and k_solve_main is VALU-issue-bound.
 #include <hip/hip_runtime.h>
 
 #include "backend.h"
@@ -148,7 +151,11 @@ __device__ __forceinline__ void st16(uint64_t addr, uint4 v)
 // never crosses a page), the prefix bytes are merged into lane 0 and bytes
 // past the symbol are masked to zero.  Two tiles' loads are in flight before
 // their stores.
-constexpr unsigned kIngestWaves = 4;
+//
+// Runs (IngestDesc.count > 1): with a block table, workgroup b takes table
+// entry blocks[b] = descriptor << 4 | group, and wave w copies symbol
+// 4 * group + w of that run; without one (the gather path), wave w of
+// workgroup b copies descriptor 4 b + w, a run of one.
 
 __device__ __forceinline__ uint32_t pick(const uint32_t* w, unsigned q, unsigned r, unsigned k)
 {
@@ -156,13 +163,29 @@ __device__ __forceinline__ uint32_t pick(const uint32_t* w, unsigned q, unsigned
 }
 
 __global__ __launch_bounds__(64 * kIngestWaves) void k_ingest(const IngestDesc* __restrict__ descs,
-                                                              uint32_t count)
+                                                              uint32_t count, const uint32_t* __restrict__ blocks)
 {
-    const uint32_t di = blockIdx.x * kIngestWaves + (threadIdx.x >> 6);
+    const uint32_t wave = threadIdx.x >> 6;
+    uint32_t di, k;
+    if (blocks) {
+        const uint32_t e = blocks[blockIdx.x];
+        di = e >> 4;
+        k = (e & 15u) * kIngestWaves + wave;
+    } else {
+        di = blockIdx.x * kIngestWaves + wave;
+        k = 0;
+    }
     if (di >= count)
         return;
     const uint32_t lane = threadIdx.x & 63;
-    const IngestDesc d = descs[di];
+    IngestDesc d = descs[di];
+    if (k >= (d.count ? d.count : 1u))
+        return;
+    d.dst2 = (d.dst2Mask >> k & 1u) ? d.dst2 + (uint64_t)k * d.dstStride : 0;
+    if (k) {
+        d.src += (uint64_t)k * d.srcStride;
+        d.dst += (uint64_t)k * d.dstStride;
+    }
     const uint32_t total = d.hdrLen + d.bytes;
     // source address that lines up with dst byte 0
     const uint64_t base = d.src - d.hdrLen;
@@ -2933,14 +2956,17 @@ void be_memset(void* dst, int value, size_t bytes)
     check(hipMemsetAsync(dst, value, bytes, g_stream), "memset");
 }
 
-void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes)
+void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes, const uint32_t* blocks,
+                      uint32_t nblocks)
 {
     if (count == 0)
         return;
     Timed t(false);
     const uint32_t chunks = maxBytes ? (maxBytes + kIngestChunkBytes - 1) / kIngestChunkBytes : 1;
-    hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves, chunks),
-                       dim3(64 * kIngestWaves), 0, g_stream, descs, count);
+    const uint32_t grid = blocks ? nblocks : (count + kIngestWaves - 1) / kIngestWaves;
+    if (grid == 0)
+        return;
+    hipLaunchKernelGGL(k_ingest, dim3(grid, chunks), dim3(64 * kIngestWaves), 0, g_stream, descs, count, blocks);
 }
 
 void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct,
@@ -3057,7 +3083,8 @@ bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, cons
                        g_gatherStream) != hipSuccess)
         return false;
     hipLaunchKernelGGL(k_ingest, dim3((count + kIngestWaves - 1) / kIngestWaves, gatherChunks),
-                       dim3(64 * kIngestWaves), 0, g_gatherStream, static_cast<const IngestDesc*>(descsDev), count);
+                       dim3(64 * kIngestWaves), 0, g_gatherStream, static_cast<const IngestDesc*>(descsDev), count,
+                       (const uint32_t*)nullptr);
     if (hipEventRecord(p, g_gatherStream) != hipSuccess)
         return false;
     *packed = p;

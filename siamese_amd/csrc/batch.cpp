@@ -86,6 +86,24 @@ SIAMESE_EXPORT SiameseResult sgpu_encoder_add(SgpuEncoder encoder, const void* d
     return r;
 }
 
+SIAMESE_EXPORT SiameseResult sgpu_encoder_add_range(SgpuEncoder encoder, const void* deviceData, size_t stride,
+                                                    const unsigned* bytes, unsigned fixedBytes, unsigned count,
+                                                    unsigned* firstPacketNumOut, unsigned* addedOut)
+{
+    if (addedOut)
+        *addedOut = 0;
+    if (!encoder || (!deviceData && count) || stride > 0xffffffffu || (count > 1 && stride == 0))
+        return Siamese_InvalidInput;
+    unsigned first = 0, added = 0;
+    const SiameseResult r = BE(encoder)->core.add_range((uint64_t)(uintptr_t)deviceData, (uint32_t)stride, bytes,
+                                                        fixedBytes, count, &first, &added);
+    if (firstPacketNumOut)
+        *firstPacketNumOut = first;
+    if (addedOut)
+        *addedOut = added;
+    return r;
+}
+
 SIAMESE_EXPORT SiameseResult sgpu_encoder_remove_before(SgpuEncoder encoder, unsigned firstKept)
 {
     if (!encoder || firstKept > SIAMESE_PACKET_NUM_MAX)
@@ -141,6 +159,26 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original(SgpuDecoder decoder, unsi
     return BD(decoder)->core.add_original(p, (uint64_t)(uintptr_t)deviceData);
 }
 
+SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original_range(SgpuDecoder decoder, unsigned firstPacketNum,
+                                                             const void* deviceData, size_t stride,
+                                                             const unsigned* bytes, unsigned fixedBytes,
+                                                             unsigned count, SiameseResult* results,
+                                                             unsigned* callsOut)
+{
+    if (callsOut)
+        *callsOut = 0;
+    if (!decoder || (!deviceData && count) || firstPacketNum > SIAMESE_PACKET_NUM_MAX || stride > 0xffffffffu ||
+        (count > 1 && stride == 0))
+        return Siamese_InvalidInput;
+    unsigned calls = 0;
+    const SiameseResult r = BD(decoder)->core.add_original_range(firstPacketNum, (uint64_t)(uintptr_t)deviceData,
+                                                                 (uint32_t)stride, bytes, fixedBytes, count, results,
+                                                                 &calls);
+    if (callsOut)
+        *callsOut = calls;
+    return r;
+}
+
 SIAMESE_EXPORT SiameseResult sgpu_decoder_add_recovery(SgpuDecoder decoder, const SgpuRecoveryPacket* packet)
 {
     if (!decoder || !packet || !packet->DeviceData || packet->DataBytes == 0 ||
@@ -176,6 +214,16 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_get(SgpuDecoder decoder, SiameseOrigin
     if (!decoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     return BD(decoder)->core.get(*packet);
+}
+
+SIAMESE_EXPORT SiameseResult sgpu_decoder_get_range(SgpuDecoder decoder, unsigned firstPacketNum, unsigned count,
+                                                    SiameseOriginalPacket* packets, unsigned* gotOut)
+{
+    if (gotOut)
+        *gotOut = 0;
+    if (!decoder || (!packets && count) || !gotOut || firstPacketNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    return BD(decoder)->core.get_range(firstPacketNum, count, packets, gotOut);
 }
 
 SIAMESE_EXPORT SiameseResult sgpu_decode_deferred(SgpuDecoder decoder, SiameseOriginalPacket* out,

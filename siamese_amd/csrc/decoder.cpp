@@ -159,9 +159,11 @@ DecoderCore::~DecoderCore()
         free_packet(r);
         r = n;
     }
-    for (auto& sw : subwindows_)
+    for (auto& sw : subwindows_) {
         for (DecSlot& s : sw->slot)
-            eng_->release(s.buf);
+            release_slot(s);
+        eng_->slab_release(sw->slab);
+    }
     for (auto& lane : lanes_)
         for (Sum& s : lane)
             eng_->release(s.d.buf);
@@ -248,46 +250,31 @@ bool DecoderCore::grow_window(unsigned end)
     return true;
 }
 
-SiameseResult DecoderCore::add_original(const SiameseOriginalPacket& packet, uint64_t deviceSrc)
+bool DecoderCore::place(unsigned element, unsigned need)
 {
-    settle();
-    // :1467-1536
-    if (dead())
-        return Siamese_Disabled;
-    const unsigned element = column_to_element(packet.PacketNum);
-    if (column_delta_negative(element)) {
-        stats_[SiameseDecoderStats_DupedOriginalCount]++;
-        return Siamese_DuplicateData;
-    }
-    grow_window(element + 1);
     DecSubwindow* sw = subwindows_[element / kSubwindow].get();
-    const unsigned bit = element % kSubwindow;
-    DecSlot& s = sw->slot[bit];
-    if (s.bytes > 0) {
-        stats_[SiameseDecoderStats_DupedOriginalCount]++;
-        return Siamese_DuplicateData;
-    }
+    DecSlot& s = sw->slot[element % kSubwindow];
+    release_slot(s);
+    bool failed = false;
+    s.buf = eng_->slab_slot(sw->slab, element % kSubwindow, need, &failed);
+    s.inSlab = (bool)s.buf;
+    if (!s.buf && !failed)
+        s.buf = eng_->alloc(need);
+    return (bool)s.buf;
+}
 
-    uint8_t hdr[kMaxLengthPrefix];
-    const unsigned h = write_length_prefix(packet.DataBytes, hdr);
-    eng_->release(s.buf);
-    s.buf = eng_->alloc(h + packet.DataBytes);
-    if (!s.buf) {
+SiameseResult DecoderCore::accept_original(unsigned element, unsigned column, unsigned header, unsigned dataBytes)
+{
+    if (!place(element, header + dataBytes)) {
         disabled_ = true;
         return Siamese_Disabled;
     }
-    if (deviceSrc)
-        prog_.ingest_device(s.buf, deviceSrc, packet.DataBytes, hdr, h);
-    else
-        prog_.ingest_host(s.buf, packet.Data, packet.DataBytes, hdr, h);
-    if (mirror_) {
-        s.host.resize(h + packet.DataBytes);
-        std::memcpy(s.host.data(), hdr, h);
-        std::memcpy(s.host.data() + h, packet.Data, packet.DataBytes);
-    }
-    s.header = h;
-    s.bytes = h + packet.DataBytes;
-    s.column = packet.PacketNum;
+    DecSubwindow* sw = subwindows_[element / kSubwindow].get();
+    const unsigned bit = element % kSubwindow;
+    DecSlot& s = sw->slot[bit];
+    s.header = header;
+    s.bytes = header + dataBytes;
+    s.column = column;
     s.pending = false;
 
     sw->gotCount++;
@@ -301,8 +288,116 @@ SiameseResult DecoderCore::add_original(const SiameseOriginalPacket& packet, uin
         region_reset();
 
     stats_[SiameseDecoderStats_OriginalCount]++;
-    stats_[SiameseDecoderStats_OriginalBytes] += packet.DataBytes;
+    stats_[SiameseDecoderStats_OriginalBytes] += dataBytes;
     return Siamese_Success;
+}
+
+SiameseResult DecoderCore::add_original(const SiameseOriginalPacket& packet, uint64_t deviceSrc)
+{
+    settle();
+    // :1467-1536
+    if (dead())
+        return Siamese_Disabled;
+    const unsigned element = column_to_element(packet.PacketNum);
+    if (column_delta_negative(element)) {
+        stats_[SiameseDecoderStats_DupedOriginalCount]++;
+        return Siamese_DuplicateData;
+    }
+    grow_window(element + 1);
+    DecSlot& s = slot(element);
+    if (s.bytes > 0) {
+        stats_[SiameseDecoderStats_DupedOriginalCount]++;
+        return Siamese_DuplicateData;
+    }
+
+    uint8_t hdr[kMaxLengthPrefix];
+    const unsigned h = write_length_prefix(packet.DataBytes, hdr);
+    // (the slot keeps its place across the bookkeeping: subwindows_ only grows above)
+    const SiameseResult r = accept_original(element, packet.PacketNum, h, packet.DataBytes);
+    if (r != Siamese_Success)
+        return r;
+    if (deviceSrc)
+        prog_.ingest_device(s.buf, deviceSrc, packet.DataBytes, hdr, h);
+    else
+        prog_.ingest_host(s.buf, packet.Data, packet.DataBytes, hdr, h);
+    if (mirror_) {
+        s.host.resize(h + packet.DataBytes);
+        std::memcpy(s.host.data(), hdr, h);
+        std::memcpy(s.host.data() + h, packet.Data, packet.DataBytes);
+    }
+    return Siamese_Success;
+}
+
+SiameseResult DecoderCore::add_original_range(unsigned firstNum, uint64_t src, uint32_t srcStride,
+                                              const unsigned* lens, unsigned fixedBytes, unsigned count,
+                                              SiameseResult* results, unsigned* added)
+{
+    *added = 0;
+    settle();
+    // the open ingest run: symbols of one length into consecutive slots
+    struct
+    {
+        uint64_t dst = 0, src = 0;
+        uint32_t stride = 0, n = 0, bytes = 0, h = 0;
+        uint8_t hdr[kMaxLengthPrefix] = {};
+    } run;
+    auto close_run = [&] {
+        if (run.n)
+            prog_.ingest_run(run.dst, run.stride, run.src, srcStride, run.n, run.bytes, run.hdr, run.h);
+        run.n = 0;
+    };
+    SiameseResult res = Siamese_Success;
+    for (unsigned k = 0; k < count; ++k) {
+        const unsigned num = (firstNum + k) & SIAMESE_PACKET_NUM_MAX;
+        const unsigned bytes = lens ? lens[k] : fixedBytes;
+        SiameseResult r = Siamese_Success;
+        const unsigned element = column_to_element(num);
+        if (bytes == 0 || bytes > SIAMESE_MAX_PACKET_BYTES)
+            r = Siamese_InvalidInput;
+        else if (dead())
+            r = Siamese_Disabled;
+        else if (column_delta_negative(element))
+            r = Siamese_DuplicateData;
+        else {
+            grow_window(element + 1);
+            if (slot(element).bytes > 0)
+                r = Siamese_DuplicateData;
+        }
+        if (r == Siamese_DuplicateData)
+            stats_[SiameseDecoderStats_DupedOriginalCount]++;
+        if (r == Siamese_Success) {
+            uint8_t hdr[kMaxLengthPrefix];
+            const unsigned h = write_length_prefix(bytes, hdr);
+            r = accept_original(element, num, h, bytes);
+            if (r == Siamese_Success) {
+                const DecSlot& s = slot(element);
+                const uint64_t from = src + (uint64_t)k * srcStride;
+                if (run.n && run.bytes == bytes && run.n < kIngestRunMax && s.buf.cap == run.stride &&
+                    s.buf.addr() == run.dst + (uint64_t)run.n * run.stride &&
+                    from == run.src + (uint64_t)run.n * srcStride)
+                    ++run.n;
+                else {
+                    close_run();
+                    run.dst = s.buf.addr();
+                    run.src = from;
+                    run.stride = s.buf.cap;
+                    run.n = 1;
+                    run.bytes = bytes;
+                    run.h = h;
+                    std::memcpy(run.hdr, hdr, sizeof(hdr));
+                }
+            }
+        }
+        if (results)
+            results[k] = r;
+        ++*added;
+        if (r != Siamese_Success && r != Siamese_DuplicateData) {
+            res = r;
+            break;
+        }
+    }
+    close_run();
+    return res;
 }
 
 // ---------------------------------------------------------------------------
@@ -560,8 +655,18 @@ void DecoderCore::remove_elements()
 
     // window indices shift below: close the open row batch first
     prog_.rows_seal();
-    for (unsigned i = 0; i < keptSub; ++i)
-        subwindows_[i]->reset();
+    for (unsigned i = 0; i < keptSub; ++i) {
+        // (slab slots go with the slab, back to the arena after the flushes
+        // that read them; owned buffers stay until their slot is reused)
+        DecSubwindow* sw = subwindows_[i].get();
+        for (DecSlot& d : sw->slot)
+            if (d.inSlab) {
+                d.buf = DevBuf();
+                d.inSlab = false;
+            }
+        eng_->slab_release(sw->slab);
+        sw->reset();
+    }
     std::rotate(subwindows_.begin(), subwindows_.begin() + keptSub, subwindows_.end());
 
     count_ -= removed;
@@ -587,8 +692,10 @@ void DecoderCore::remove_elements()
 void DecSubwindowRecycle::operator()(DecSubwindow* w) const
 {
     w->reset();
+    w->slab = Slab();
     for (DecSlot& s : w->slot) {
         s.buf = DevBuf();
+        s.inSlab = false;
         s.header = 0;
         s.host.clear();
     }
@@ -809,9 +916,7 @@ bool DecoderCore::add_single(const RowMeta& m, const uint8_t* headBytes, unsigne
 
     uint8_t hdr[kMaxLengthPrefix];
     const unsigned h = write_length_prefix(length, hdr);
-    eng_->release(s.buf);
-    s.buf = eng_->alloc(h + length);
-    if (!s.buf)
+    if (!place(element, h + length))
         return false;
     if (hostData)
         prog_.ingest_host(s.buf, (const uint8_t*)hostData + headerBytes, length, hdr, h);
@@ -1495,7 +1600,10 @@ SiameseResult DecoderCore::solve_and_substitute()
             RecPacket* r = pr[ci];
             ColInfo& col = cols_[ci];
             DecSlot* o = col.original;
-            DevBuf old = o->buf;
+            // (a slab slot is not the slot's to give: the recovery packet
+            // gets it only when owned)
+            DevBuf old = o->inSlab ? DevBuf() : o->buf;
+            o->inSlab = false;
             o->buf = r->buf;
             o->bytes = len[ci];
             o->column = col.column;
@@ -1649,6 +1757,19 @@ SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
     return Siamese_Success;
 }
 
+SiameseResult DecoderCore::get_range(unsigned firstNum, unsigned count, SiameseOriginalPacket* out, unsigned* got)
+{
+    *got = 0;
+    for (unsigned k = 0; k < count; ++k) {
+        out[k].PacketNum = (firstNum + k) & SIAMESE_PACKET_NUM_MAX;
+        const SiameseResult r = get(out[k]);
+        if (r != Siamese_Success)
+            return r;
+        ++*got;
+    }
+    return Siamese_Success;
+}
+
 SiameseResult DecoderCore::decode_deferred(SiameseOriginalPacket* out, unsigned capacity, unsigned* countOut)
 {
     settle();
@@ -1714,9 +1835,12 @@ SiameseResult DecoderCore::stats(uint64_t* out, unsigned count)
     if (count > SiameseDecoderStats_Count)
         count = SiameseDecoderStats_Count;
     uint64_t mem = 0;
-    for (auto& sw : subwindows_)
+    for (auto& sw : subwindows_) {
+        mem += sw->slab.buf.cap;
         for (DecSlot& s : sw->slot)
-            mem += s.buf.cap;
+            if (!s.inSlab)
+                mem += s.buf.cap;
+    }
     for (auto& lane : lanes_)
         for (Sum& s : lane)
             mem += s.d.buf.cap;

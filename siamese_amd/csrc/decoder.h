@@ -31,6 +31,7 @@ namespace sgpu {
 struct DecSlot
 {
     DevBuf buf;
+    bool inSlab = false;        // buf is a slot of the subwindow's slab (not owned)
     unsigned bytes = 0;         // prefix + payload (upper bound while pending)
     unsigned column = 0;        // packet number, or matrix column while lost
     unsigned header = 0;
@@ -45,6 +46,7 @@ struct DecSubwindow
     DecSlot slot[kSubwindow];
     uint64_t got = 0;           // CustomBitSet<64> (PacketAllocator.h:189-437)
     unsigned gotCount = 0;
+    Slab slab;                  // the received originals' shared buffer (engine.h)
     void reset()
     {
         got = 0;
@@ -99,6 +101,19 @@ public:
     Program& program() { return prog_; }
 
     SiameseResult add_original(const SiameseOriginalPacket& packet, uint64_t deviceSrc = 0);
+    /// `count` add_original calls in one (sgpu_decoder_add_original_range):
+    /// packet firstNum + k from src + k * srcStride, lens[k] bytes (fixedBytes
+    /// when lens is null).  results[k] (optional) gets each call's result;
+    /// like the calls, a DuplicateData goes on and any other failure stops
+    /// (its result returned, *added = calls made including it).  Consecutive
+    /// slab slots become one ingest run.
+    SiameseResult add_original_range(unsigned firstNum, uint64_t src, uint32_t srcStride, const unsigned* lens,
+                                     unsigned fixedBytes, unsigned count, SiameseResult* results,
+                                     unsigned* added);
+    /// sgpu_decoder_get_range: get() for packets firstNum, firstNum + 1, ...
+    /// into out[0..count) until one is not Success; *got = packets returned.
+    /// Returns the result of the get that stopped (Success if none did).
+    SiameseResult get_range(unsigned firstNum, unsigned count, SiameseOriginalPacket* out, unsigned* got);
     /// Host-memory recovery packet (drop-in API).
     SiameseResult add_recovery(const SiameseRecoveryPacket& packet);
     /// Device-resident recovery packet (batch API).
@@ -155,6 +170,19 @@ private:
         return e < element ? e + kLanes : e;
     }
     bool mark_got(unsigned column);
+    /// A destination for a symbol of `need` bytes in element's slot: its slab
+    /// slot or a buffer of its own (false: arena failure).
+    bool place(unsigned element, unsigned need);
+    void release_slot(DecSlot& s)
+    {
+        if (!s.inSlab)
+            eng_->release(s.buf);
+        s.buf = DevBuf();
+        s.inSlab = false;
+    }
+    /// add_original after validation and the duplicate checks: the element's
+    /// slot takes its destination (the caller queues the ingest).
+    SiameseResult accept_original(unsigned element, unsigned column, unsigned header, unsigned dataBytes);
     unsigned range_lost(unsigned start, unsigned end);
     unsigned find_next_lost(unsigned start);
     unsigned find_next_got(unsigned start);

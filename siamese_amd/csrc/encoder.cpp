@@ -23,9 +23,11 @@ EncoderCore::EncoderCore(Engine* eng, bool hostMirror) : eng_(eng), prog_(eng, 0
 
 EncoderCore::~EncoderCore()
 {
-    for (auto& sw : subwindows_)
+    for (auto& sw : subwindows_) {
         for (EncSlot& s : sw->slot)
-            eng_->release(s.buf);
+            release_slot(s);
+        eng_->slab_release(sw->slab);
+    }
     for (Lane& l : lanes_)
         for (DevSum& s : l.sum)
             eng_->release(s.buf);
@@ -39,17 +41,11 @@ EncoderCore::~EncoderCore()
 // ---------------------------------------------------------------------------
 // Window bookkeeping
 
-SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc)
+unsigned EncoderCore::take_element()
 {
     // :85-161
-    if (dead())
-        return Siamese_Disabled;
-    if (remaining_slots() == 0)
-        return Siamese_MaxPacketsReached;
-
     const unsigned column = nextColumn_;
     unsigned element = count_;
-    packet.PacketNum = column;
 
     // Keep one lane-width of spare slots ahead of the last subwindow (:108-118)
     if (element + kLanes >= subwindows_.size() * kSubwindow)
@@ -61,29 +57,32 @@ SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc
         element = column % kLanes;
         start_window(column);
     }
+    return element;
+}
 
-    EncSlot& s = slot(element);
-    uint8_t hdr[kMaxLengthPrefix];
-    const unsigned h = write_length_prefix(packet.DataBytes, hdr);
-    eng_->release(s.buf);
-    s.buf = eng_->alloc(h + packet.DataBytes);
+bool EncoderCore::place(unsigned element, unsigned need)
+{
+    EncSubwindow* sw = subwindows_[element / kSubwindow].get();
+    EncSlot& s = sw->slot[element % kSubwindow];
+    release_slot(s);
+    bool failed = false;
+    s.buf = eng_->slab_slot(sw->slab, element % kSubwindow, need, &failed);
+    s.inSlab = (bool)s.buf;
+    if (!s.buf && !failed)
+        s.buf = eng_->alloc(need);
     if (!s.buf) {
         disabled_ = true;
-        return Siamese_Disabled;
+        return false;
     }
-    if (deviceSrc)
-        prog_.ingest_device(s.buf, deviceSrc, packet.DataBytes, hdr, h);
-    else
-        prog_.ingest_host(s.buf, packet.Data, packet.DataBytes, hdr, h);
-    if (mirror_) {
-        s.host.resize(h + packet.DataBytes);
-        std::memcpy(s.host.data(), hdr, h);
-        std::memcpy(s.host.data() + h, packet.Data, packet.DataBytes);
-    }
-    s.header = h;
-    s.bytes = h + packet.DataBytes;
+    return true;
+}
+
+void EncoderCore::fill_slot(EncSlot& s, unsigned column, unsigned header, unsigned dataBytes, uint32_t stamp)
+{
+    s.header = header;
+    s.bytes = header + dataBytes;
     s.column = column;
-    s.lastSend = (uint32_t)now_msec();
+    s.lastSend = stamp;
 
     nextColumn_ = column_add(nextColumn_, 1);
 
@@ -95,14 +94,115 @@ SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc
         longest_ = s.bytes;
 
     stats_[SiameseEncoderStats_OriginalCount]++;
-    stats_[SiameseEncoderStats_OriginalBytes] += packet.DataBytes;
+    stats_[SiameseEncoderStats_OriginalBytes] += dataBytes;
+}
+
+SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc)
+{
+    // :85-161
+    if (dead())
+        return Siamese_Disabled;
+    if (remaining_slots() == 0)
+        return Siamese_MaxPacketsReached;
+
+    const unsigned column = nextColumn_;
+    packet.PacketNum = column;
+    const unsigned element = take_element();
+
+    uint8_t hdr[kMaxLengthPrefix];
+    const unsigned h = write_length_prefix(packet.DataBytes, hdr);
+    if (!place(element, h + packet.DataBytes))
+        return Siamese_Disabled;
+    EncSlot& s = slot(element);
+    if (deviceSrc)
+        prog_.ingest_device(s.buf, deviceSrc, packet.DataBytes, hdr, h);
+    else
+        prog_.ingest_host(s.buf, packet.Data, packet.DataBytes, hdr, h);
+    if (mirror_) {
+        s.host.resize(h + packet.DataBytes);
+        std::memcpy(s.host.data(), hdr, h);
+        std::memcpy(s.host.data() + h, packet.Data, packet.DataBytes);
+    }
+    fill_slot(s, column, h, packet.DataBytes, (uint32_t)now_msec());
     return Siamese_Success;
+}
+
+SiameseResult EncoderCore::add_range(uint64_t src, uint32_t srcStride, const unsigned* lens, unsigned fixedBytes,
+                                     unsigned count, unsigned* firstNum, unsigned* added)
+{
+    *added = 0;
+    *firstNum = nextColumn_;
+    if (dead())
+        return Siamese_Disabled;
+    // one timestamp for the call (ARQ's RTO is milliseconds)
+    const uint32_t stamp = count ? (uint32_t)now_msec() : 0;
+    // the open ingest run: symbols of one length into consecutive slots
+    struct
+    {
+        uint64_t dst = 0, src = 0;
+        uint32_t stride = 0, n = 0, bytes = 0, h = 0;
+        uint8_t hdr[kMaxLengthPrefix] = {};
+    } run;
+    auto close_run = [&] {
+        if (run.n)
+            prog_.ingest_run(run.dst, run.stride, run.src, srcStride, run.n, run.bytes, run.hdr, run.h);
+        run.n = 0;
+    };
+    SiameseResult res = Siamese_Success;
+    for (unsigned k = 0; k < count; ++k) {
+        const unsigned bytes = lens ? lens[k] : fixedBytes;
+        if (bytes == 0 || bytes > SIAMESE_MAX_PACKET_BYTES) {
+            res = Siamese_InvalidInput;
+            break;
+        }
+        if (remaining_slots() == 0) {
+            res = Siamese_MaxPacketsReached;
+            break;
+        }
+        const unsigned column = nextColumn_;
+        const unsigned element = take_element();
+        uint8_t hdr[kMaxLengthPrefix];
+        const unsigned h = write_length_prefix(bytes, hdr);
+        if (!place(element, h + bytes)) {
+            res = Siamese_Disabled;
+            break;
+        }
+        EncSlot& s = slot(element);
+        const uint64_t from = src + (uint64_t)k * srcStride;
+        if (run.n && run.bytes == bytes && run.n < kIngestRunMax && s.buf.cap == run.stride &&
+            s.buf.addr() == run.dst + (uint64_t)run.n * run.stride &&
+            from == run.src + (uint64_t)run.n * srcStride)
+            ++run.n;
+        else {
+            close_run();
+            run.dst = s.buf.addr();
+            run.src = from;
+            run.stride = s.buf.cap;
+            run.n = 1;
+            run.bytes = bytes;
+            run.h = h;
+            std::memcpy(run.hdr, hdr, sizeof(hdr));
+        }
+        fill_slot(s, column, h, bytes, stamp);
+        ++*added;
+    }
+    close_run();
+    return res;
 }
 
 void EncoderCore::start_window(unsigned column)
 {
     // :163-181 -- element % 8 == column % 8 is an invariant of the window
     const unsigned element = column % kLanes;
+    // every element of the old window was acknowledged: slabs start afresh
+    for (auto& sw : subwindows_) {
+        for (EncSlot& s : sw->slot)
+            if (s.inSlab) {
+                s.buf = DevBuf();
+                s.inSlab = false;
+            }
+        eng_->slab_release(sw->slab);
+    }
     columnStart_ = column - element;
     sumStart_ = element;
     sumEnd_ = element;
@@ -171,7 +271,17 @@ void EncoderCore::remove_elements()
 
     // window indices shift below: close the open row batch first
     prog_.rows_seal();
-    // Removed subwindows rotate to the back for reuse
+    // Removed subwindows rotate to the back for reuse; their slabs go back
+    // to the arena (after the flushes that read them)
+    for (unsigned i = 0; i < keptSub; ++i) {
+        EncSubwindow* sw = subwindows_[i].get();
+        for (EncSlot& s : sw->slot)
+            if (s.inSlab) {
+                s.buf = DevBuf();
+                s.inSlab = false;
+            }
+        eng_->slab_release(sw->slab);
+    }
     std::rotate(subwindows_.begin(), subwindows_.begin() + keptSub, subwindows_.end());
 
     count_ -= removed;
@@ -482,9 +592,12 @@ SiameseResult EncoderCore::stats(uint64_t* out, unsigned count)
     if (count > SiameseEncoderStats_Count)
         count = SiameseEncoderStats_Count;
     uint64_t mem = recovery_.cap;
-    for (auto& sw : subwindows_)
+    for (auto& sw : subwindows_) {
+        mem += sw->slab.buf.cap;
         for (EncSlot& s : sw->slot)
-            mem += s.buf.cap;
+            if (!s.inSlab)
+                mem += s.buf.cap;
+    }
     for (Lane& l : lanes_)
         for (DevSum& s : l.sum)
             mem += s.buf.cap;

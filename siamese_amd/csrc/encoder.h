@@ -21,6 +21,7 @@ namespace sgpu {
 struct EncSlot
 {
     DevBuf buf;                 // [length prefix || payload] in HBM
+    bool inSlab = false;        // buf is a slot of the subwindow's slab (not owned)
     unsigned bytes = 0;         // prefix + payload
     unsigned column = 0;
     unsigned header = 0;        // length-prefix bytes
@@ -31,6 +32,7 @@ struct EncSlot
 struct EncSubwindow
 {
     EncSlot slot[kSubwindow];
+    Slab slab;                  // the slots' shared buffer (engine.h)
 };
 
 /// unique_ptr deleter: subwindows go back to the thread's pool, emptied
@@ -39,8 +41,10 @@ struct EncSubwindowRecycle
 {
     void operator()(EncSubwindow* w) const
     {
+        w->slab = Slab();
         for (EncSlot& s : w->slot) {
             s.buf = DevBuf();
+            s.inSlab = false;
             s.bytes = s.column = s.header = 0;
             s.lastSend = 0;
             s.host.clear();
@@ -81,6 +85,14 @@ public:
 
     /// siamese_encoder_add.  Source is host memory or (device != 0) HBM.
     SiameseResult add(SiameseOriginalPacket& packet, uint64_t deviceSrc = 0);
+    /// `count` adds of device originals in one call (sgpu_encoder_add_range):
+    /// original k at src + k * srcStride, lens[k] bytes (fixedBytes when lens
+    /// is null).  Identical to `count` add() calls that stop at the first
+    /// failure, whose result is returned; *added originals were taken, the
+    /// first as packet *firstNum (the rest follow it).  Consecutive slab slots
+    /// become one ingest run.
+    SiameseResult add_range(uint64_t src, uint32_t srcStride, const unsigned* lens, unsigned fixedBytes,
+                            unsigned count, unsigned* firstNum, unsigned* added);
     void remove_before(unsigned firstKeptColumn);
     SiameseResult get(SiameseOriginalPacket& packet);
     /// Generate the next recovery packet (device ops queued, not flushed).
@@ -109,6 +121,22 @@ private:
         return e < element ? e + kLanes : e;
     }
     unsigned unacked() const { return count_ - firstUnremoved_; }
+    /// The window bookkeeping of one add (reference :85-161) up to its slot:
+    /// the element the packet takes (its column is nextColumn_ before).
+    unsigned take_element();
+    /// Give element's slot a destination for `need` bytes: its slab slot, or
+    /// a buffer of its own.  False on an arena failure (the encoder is then
+    /// disabled).
+    bool place(unsigned element, unsigned need);
+    /// The slot's fields and the window's lengths after its symbol is queued.
+    void fill_slot(EncSlot& s, unsigned column, unsigned header, unsigned dataBytes, uint32_t stamp);
+    void release_slot(EncSlot& s)
+    {
+        if (!s.inSlab)
+            eng_->release(s.buf);
+        s.buf = DevBuf();
+        s.inSlab = false;
+    }
     void start_window(unsigned column);
     void reset_sums(unsigned elementStart);
     void remove_elements();

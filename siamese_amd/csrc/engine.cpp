@@ -544,15 +544,22 @@ void Program::ingest_host(const DevBuf& dst, const void* data, uint32_t bytes, c
 void Program::ingest_device(const DevBuf& dst, uint64_t src, uint32_t bytes, const uint8_t* hdr,
                             uint32_t hdrLen)
 {
+    ingest_run(dst.addr(), 0, src, 0, 1, bytes, hdr, hdrLen);
+}
+
+void Program::ingest_run(uint64_t dst, uint32_t dstStride, uint64_t src, uint32_t srcStride, uint32_t count,
+                         uint32_t bytes, const uint8_t* hdr, uint32_t hdrLen)
+{
     IngestDesc d;
-    d.dst = dst.addr();
+    std::memset(&d, 0, sizeof(d));
+    d.dst = dst;
     d.src = src;
     d.bytes = bytes;
     d.hdrLen = hdrLen;
-    d.dst2 = 0;
-    uint64_t h = 0;
-    std::memcpy(&h, hdr, hdrLen < 8 ? hdrLen : 8);
-    std::memcpy(d.hdr, &h, 8);
+    d.count = count;
+    d.srcStride = count > 1 ? srcStride : 0;
+    d.dstStride = count > 1 ? dstStride : 0;
+    std::memcpy(d.hdr, hdr, hdrLen < 8 ? hdrLen : 8);
     eng_->add_ingest(d, -1);
 }
 
@@ -745,6 +752,7 @@ void Shard::Queues::clear()
     hostStage.clear();
     downloads.clear();
     maxIngest = 0;
+    pairCursor = 0;
     for (auto& r : released)
         r.clear();
 }
@@ -824,8 +832,6 @@ uint64_t Engine::bytes_in_use() const
     return (uint64_t)t;
 }
 
-namespace {
-
 uint32_t round_cap(uint32_t bytes)
 {
     if (bytes < 64)
@@ -836,6 +842,8 @@ uint32_t round_cap(uint32_t bytes)
         return (bytes + 1023) & ~1023u;
     return (bytes + 65535) & ~65535u;
 }
+
+namespace {
 
 size_t cap_class(uint32_t cap)
 {
@@ -963,6 +971,44 @@ DevBuf Engine::alloc(uint32_t bytes)
     return b;
 }
 
+bool slabs_enabled()
+{
+    static const bool v = [] {
+        const char* e = std::getenv("SIAMESE_AMD_SLABS");
+        return !e || std::atoi(e) != 0;
+    }();
+    return v;
+}
+
+DevBuf Engine::slab_slot(Slab& sl, unsigned bit, uint32_t need, bool* failed)
+{
+    *failed = false;
+    if (!slabs_enabled())
+        return DevBuf();
+    if (!sl.buf) {
+        // slots of one MTU-sized class at least: a subwindow of small and
+        // mixed-size datagrams still shares one slab
+        constexpr uint32_t kMinSlot = 1408;
+        const uint32_t stride = round_cap(std::max(need, kMinSlot));
+        if ((uint64_t)stride * kSubwindow > 0xffffffffu)
+            return DevBuf();
+        sl.buf = alloc(stride * kSubwindow);
+        if (!sl.buf) {
+            *failed = true;
+            return DevBuf();
+        }
+        sl.stride = stride;
+        sl.used = 0;
+    }
+    if (need > sl.stride || (sl.used >> bit & 1u))
+        return DevBuf();
+    sl.used |= 1ull << bit;
+    DevBuf b;
+    b.ptr = sl.buf.ptr + (size_t)bit * sl.stride;
+    b.cap = sl.stride;
+    return b;
+}
+
 void Engine::release(DevBuf& b)
 {
     if (b.ptr) {
@@ -1001,23 +1047,116 @@ void Engine::stage_host_ingest(const DevBuf& dst, const void* data, uint32_t byt
     s.q.maxIngest = std::max(s.q.maxIngest, d.bytes);
 }
 
+namespace {
+
+inline bool same_symbols(const IngestDesc& a, const IngestDesc& b)
+{
+    return a.bytes == b.bytes && a.hdrLen == b.hdrLen && std::memcmp(a.hdr, b.hdr, sizeof(a.hdr)) == 0;
+}
+
+inline uint32_t run_count(const IngestDesc& d)
+{
+    return d.count ? d.count : 1u;
+}
+
+/// Stride that takes `from` to `to` in one step (0: none fits 32 bits)
+inline uint32_t step_of(uint64_t from, uint64_t to)
+{
+    return to > from && to - from <= 0xffffffffu ? (uint32_t)(to - from) : 0u;
+}
+
+/// Append run b to run a when b's symbols continue a's (same shape, same
+/// strides, second destinations on one base); true if merged.
+bool extend_run(IngestDesc& a, const IngestDesc& b)
+{
+    const uint32_t na = run_count(a), nb = run_count(b);
+    if (!same_symbols(a, b) || na + nb > kIngestRunMax)
+        return false;
+    uint32_t ss = a.srcStride, ds = a.dstStride;
+    if (na == 1) {   // a's strides are fixed by b's first symbol
+        ss = step_of(a.src, b.src);
+        ds = step_of(a.dst, b.dst);
+        if (!ss || !ds)
+            return false;
+    }
+    if (nb > 1 && (b.srcStride != ss || b.dstStride != ds))
+        return false;
+    if (b.src != a.src + (uint64_t)na * ss || b.dst != a.dst + (uint64_t)na * ds)
+        return false;
+    uint64_t base2 = a.dst2;
+    if (b.dst2Mask) {
+        const uint64_t want = b.dst2 - (uint64_t)na * ds;   // b's second base seen from a's symbol 0
+        if (a.dst2Mask && want != a.dst2)
+            return false;
+        base2 = want;
+    }
+    a.srcStride = ss;
+    a.dstStride = ds;
+    a.dst2 = base2;
+    a.dst2Mask |= b.dst2Mask << na;
+    a.count = na + nb;
+    return true;
+}
+
+} // namespace
+
 void Engine::add_ingest(const IngestDesc& d, int64_t hostStageOffset)
 {
     Shard::Queues& q = shard().q;
-    // the same device symbol right after itself (an encoder and then its
-    // decoder taking in one original, SIAMESE_AMD_INGEST_PAIRS=0 to keep
-    // them apart): one descriptor with two destinations, the source read once
+    // SIAMESE_AMD_INGEST_PAIRS=0 keeps an encoder's and a decoder's ingest of
+    // one original apart (A/B aid)
     static const bool pairs = [] {
         const char* v = std::getenv("SIAMESE_AMD_INGEST_PAIRS");
         return !v || std::atoi(v) != 0;
     }();
-    if (pairs && hostStageOffset < 0 && !q.ingest.empty()) {
-        Shard::IngestRec& last = q.ingest.back();
-        if (last.hostOffset < 0 && last.d.dst2 == 0 && last.d.src == d.src && last.d.bytes == d.bytes &&
-            last.d.hdrLen == d.hdrLen && std::memcmp(last.d.hdr, d.hdr, sizeof(d.hdr)) == 0) {
-            last.d.dst2 = d.dst;
-            return;
+    if (hostStageOffset < 0 && !q.ingest.empty()) {
+        // The same device symbols as a recent run's (an encoder and then its
+        // decoder taking in the same originals): the decoder's destinations
+        // become that run's second destinations, the source read once.  The
+        // run keeps one base for them; its mask says which symbols have one.
+        // (The search looks at the last few runs and at the one matched last:
+        // a decoder's runs follow its encoder's run by run.)
+        if (pairs && d.dst2Mask == 0) {
+            auto try_pair = [&](Shard::IngestRec& e) {
+                if (e.hostOffset >= 0 || !same_symbols(e.d, d))
+                    return false;
+                const uint32_t n = run_count(e.d), c = run_count(d);
+                const uint32_t ss = n > 1 ? e.d.srcStride : 0;
+                uint32_t k;
+                if (d.src == e.d.src)
+                    k = 0;
+                else if (ss && d.src > e.d.src && (d.src - e.d.src) % ss == 0 && (d.src - e.d.src) / ss < n)
+                    k = (uint32_t)((d.src - e.d.src) / ss);
+                else
+                    return false;
+                if (k + c > n || (c > 1 && (d.srcStride != ss || d.dstStride != e.d.dstStride)))
+                    return false;   // (a run both sides must step through alike)
+                const uint64_t base = d.dst - (uint64_t)k * e.d.dstStride;
+                const uint64_t bits = (c >= 64 ? ~0ull : ((1ull << c) - 1)) << k;
+                if (e.d.dst2Mask && (e.d.dst2 != base || (e.d.dst2Mask & bits)))
+                    return false;
+                e.d.dst2 = base;
+                e.d.dst2Mask |= bits;
+                return true;
+            };
+            const size_t sz = q.ingest.size();
+            for (size_t i = q.pairCursor; i < sz && i < q.pairCursor + 8; ++i)
+                if (try_pair(q.ingest[i])) {
+                    q.pairCursor = i;
+                    return;
+                }
+            const size_t lo = sz > 8 ? sz - 8 : 0;
+            for (size_t i = sz; i-- > lo;)
+                if (i >= q.pairCursor + 8 && try_pair(q.ingest[i])) {
+                    q.pairCursor = i;
+                    return;
+                }
         }
+        // the next symbols of the last run (consecutive slab slots from
+        // consecutive device originals): one descriptor grows
+        Shard::IngestRec& last = q.ingest.back();
+        if (last.hostOffset < 0 && extend_run(last.d, d))
+            return;
     }
     q.ingest.push_back(Shard::IngestRec{d, hostStageOffset});
     q.maxIngest = std::max(q.maxIngest, d.bytes + d.hdrLen);
@@ -1123,9 +1262,9 @@ struct Batch
     unsigned set = 0;                      // transfer set (ticket % kSets)
     // layout (enqueue -> launcher)
     std::vector<Phase> phases;
-    size_t upBytes = 0, nIngest = 0;
+    size_t upBytes = 0, nIngest = 0, nIngBlocks = 0;
     uint32_t maxIngest = 0;
-    size_t oIngD = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
+    size_t oIngD = 0, oIngB = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
     uint64_t wideBase = 0;                 // this submission's k_ldpc scratch: bytes into the ring
     bool wideZero = false;                 // the ring wrapped: zero it before the first exec launch
     uint32_t resultWords = 0;
@@ -1608,22 +1747,36 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         }
     }
 
-    size_t nIngest = 0, stageBytes = 0;
+    constexpr size_t kIngestChunk = SGPU_INGEST_CHUNK;
+    size_t nIngest = 0, stageBytes = 0, nIngBlocks = 0;
     std::vector<size_t> descBase, stageBase;
-    for (const Shard::Queues& q : bt.queues) {
+    // the k_ingest block table's first entry of every ingest chunk (a run of
+    // n symbols takes ceil(n / kIngestWaves) entries)
+    std::vector<std::vector<size_t>> blockBase(bt.queues.size());
+    for (size_t qi = 0; qi < bt.queues.size(); ++qi) {
+        const Shard::Queues& q = bt.queues[qi];
         descBase.push_back(nIngest);
         stageBase.push_back(stageBytes);
         nIngest += q.ingest.size();
         bt.maxIngest = std::max(bt.maxIngest, q.maxIngest);
         stageBytes = align16(stageBytes + q.hostStage.size());
+        for (size_t i = 0; i < q.ingest.size(); ++i) {
+            if (i % kIngestChunk == 0)
+                blockBase[qi].push_back(nIngBlocks);
+            const uint32_t n = q.ingest[i].d.count ? q.ingest[i].d.count : 1u;
+            nIngBlocks += (n + kIngestWaves - 1) / kIngestWaves;
+        }
     }
     bt.nIngest = nIngest;
+    bt.nIngBlocks = nIngBlocks;
 
     size_t off = 0;
     const size_t oStage = off;
     off = align16(off + stageBytes);
     bt.oIngD = off;
     off = align16(off + nIngest * sizeof(IngestDesc));
+    bt.oIngB = off;
+    off = align16(off + nIngBlocks * sizeof(uint32_t));
     bt.oStream = off;
     off = align16(off + nWords * 16);
     bt.oItems = off;
@@ -1698,7 +1851,6 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     uint8_t* up = xs.upHost;
     const uint64_t stageDev = (uint64_t)(uintptr_t)(bt.upBase + oStage);
     constexpr size_t kSegChunk = SGPU_SEG_CHUNK;
-    constexpr size_t kIngestChunk = SGPU_INGEST_CHUNK;
     constexpr size_t kSolveChunk = SGPU_SOLVE_CHUNK;
     struct Task
     {
@@ -1784,11 +1936,17 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
             const Shard::Queues& q = bt.queues[t.a];
             IngestDesc* descs = (IngestDesc*)(up + bt.oIngD) + descBase[t.a];
             const size_t end = std::min(q.ingest.size(), t.b + kIngestChunk);
+            uint32_t* blk = t.b < q.ingest.size() ? (uint32_t*)(up + bt.oIngB) + blockBase[t.a][t.b / kIngestChunk]
+                                                  : nullptr;
             for (size_t i = t.b; i < end; ++i) {
                 IngestDesc d = q.ingest[i].d;
                 if (q.ingest[i].hostOffset >= 0)
                     d.src = stageDev + stageBase[t.a] + (uint64_t)q.ingest[i].hostOffset;
                 descs[i] = d;
+                const uint32_t di = (uint32_t)(descBase[t.a] + i);
+                const uint32_t n = d.count ? d.count : 1u;
+                for (uint32_t g = 0; g * kIngestWaves < n; ++g)
+                    *blk++ = di << 4 | g;
             }
             if (t.b == 0 && !q.hostStage.empty())
                 std::memcpy(up + oStage + stageBase[t.a], q.hostStage.data(), q.hostStage.size());
@@ -1841,7 +1999,8 @@ void Engine::launch_batch(Batch& bt)
         be_copy_pinned(&up, 1, true);
     }
     if (bt.nIngest)
-        be_launch_ingest((const IngestDesc*)(bt.upBase + bt.oIngD), (uint32_t)bt.nIngest, bt.maxIngest);
+        be_launch_ingest((const IngestDesc*)(bt.upBase + bt.oIngD), (uint32_t)bt.nIngest, bt.maxIngest,
+                         (const uint32_t*)(bt.upBase + bt.oIngB), (uint32_t)bt.nIngBlocks);
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
     if (xs.acctZero) {

@@ -43,6 +43,28 @@ struct DevBuf
     uint64_t addr() const { return (uint64_t)(uintptr_t)ptr; }
 };
 
+/// Buffer capacity for `bytes` (64 B classes up to 4 KiB, 1 KiB classes up
+/// to 128 KiB, 64 KiB classes above).
+uint32_t round_cap(uint32_t bytes);
+
+/// The originals of one subwindow (64 consecutive window elements) live in
+/// one slab: 64 slots of one capacity, taken whole from the arena when the
+/// subwindow's first original arrives and released whole when the
+/// subwindow leaves the window (the reference recycles whole subwindows,
+/// SiameseEncoder.cpp:284-315).  Consecutive originals then fill
+/// consecutive slots, so a run of adds is one ingest descriptor and one
+/// allocation.  A slot is written at most once per slab: a later symbol for
+/// it (or one too large for the stride) gets a buffer of its own, since
+/// ops of the same flush may still read the slot's first contents.
+struct Slab
+{
+    DevBuf buf;
+    uint32_t stride = 0;
+    uint64_t used = 0;   // slots written since the slab was taken
+};
+/// SIAMESE_AMD_SLABS=0 gives every symbol its own buffer (A/B aid).
+bool slabs_enabled();
+
 class Engine;
 struct Shard;
 struct Batch;
@@ -213,6 +235,10 @@ public:
                      uint32_t hdrLen);
     void ingest_device(const DevBuf& dst, uint64_t src, uint32_t bytes, const uint8_t* hdr,
                        uint32_t hdrLen);
+    /// `count` symbols of one shape: symbol k from src + k * srcStride into
+    /// the fresh slot dst + k * dstStride (IngestDesc runs).
+    void ingest_run(uint64_t dst, uint32_t dstStride, uint64_t src, uint32_t srcStride, uint32_t count,
+                    uint32_t bytes, const uint8_t* hdr, uint32_t hdrLen);
 
     /// Queue a triangular solve; returns the result-word index it will fill
     /// (valid in this program's completion callbacks of the flush that runs it).
@@ -305,6 +331,16 @@ public:
 
     DevBuf alloc(uint32_t bytes);
     void release(DevBuf& b);               // recycled after the next flush completes
+    /// Slot `bit` of the slab for a symbol of `need` bytes (the slab is
+    /// taken on first use), or a null buffer when it cannot hold it (taken
+    /// slot, too large, slabs off); *failed on an arena failure.
+    DevBuf slab_slot(Slab& sl, unsigned bit, uint32_t need, bool* failed);
+    void slab_release(Slab& sl)
+    {
+        release(sl.buf);
+        sl.stride = 0;
+        sl.used = 0;
+    }
     uint64_t bytes_in_use() const;
     uint64_t arena_bytes() const { return arenaBytes_.load(std::memory_order_relaxed); }
     /// Keep at least `bytes` of untouched arena chunks in reserve, so later
@@ -536,6 +572,7 @@ struct Shard
         std::vector<Download> downloads;
         std::vector<std::vector<uint8_t*>> released;   // by capacity class
         uint32_t maxIngest = 0;                         // largest hdrLen + bytes among `ingest`
+        size_t pairCursor = 0;                          // ingest run a decoder's symbols paired with last
         bool empty() const;
         void clear();
     };

@@ -292,22 +292,38 @@ struct SolveItem
     uint32_t tileBase;
 };
 
-/// Ingest of one symbol into a FRESH device buffer (never referenced by any
-/// op of the same flush before this point), so ingest can run as the first
-/// launch of a flush:  dst[0,hdrLen) = hdr,  dst[hdrLen, hdrLen+bytes) = src,
-/// and dst[total, align16(total)) = 0 (whole 16-byte lanes are stored; dst is
-/// 16-byte aligned with capacity >= align16(total)).  dst2 != 0: the same
-/// symbol written to a second fresh buffer too (an encoder and a decoder
-/// ingesting one original: the source is read once).
+/// Ingest of a run of `count` symbols into FRESH device buffers (never
+/// referenced by any op of the same flush before this point), so ingest can
+/// run as the first launch of a flush.  Symbol k of the run (k < count; a
+/// count of 0 reads as 1) has its source at src + k * srcStride and its
+/// destination at dst + k * dstStride:  dst[0,hdrLen) = hdr,
+/// dst[hdrLen, hdrLen+bytes) = src, and dst[total, align16(total)) = 0 (whole
+/// 16-byte lanes are stored; dst is 16-byte aligned with capacity >=
+/// align16(total)).  Bit k of dst2Mask set: symbol k is also written to the
+/// fresh buffer dst2 + k * dstStride (an encoder and a decoder ingesting the
+/// same originals: the source is read once; the decoder's lost originals
+/// are the clear bits).  A run is a slab's consecutive slots filled from
+/// consecutive device originals: one descriptor instead of one per symbol.
 struct IngestDesc
 {
     uint64_t dst;
     uint64_t src;
+    uint64_t dst2;
+    uint64_t dst2Mask;
     uint32_t bytes;
     uint32_t hdrLen;
     uint8_t hdr[8];
-    uint64_t dst2;
+    uint32_t count;
+    uint32_t srcStride;
+    uint32_t dstStride;
+    uint32_t pad;
 };
+
+/// Symbols of one ingest run at most (k_ingest block table: 4 bits of
+/// 4-symbol groups per entry).
+constexpr uint32_t kIngestRunMax = 64;
+/// k_ingest work per workgroup: one symbol per wave.
+constexpr uint32_t kIngestWaves = 4;
 
 constexpr unsigned kTileBytes = 1024;       // solve tiles: 64 lanes x 16 bytes
 constexpr unsigned kIngestChunkBytes = 8192;   // k_ingest: bytes per wave (8 x 1 KiB tiles)

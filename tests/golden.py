@@ -46,6 +46,15 @@ FIXTURES = {
     "edge_maxloss": ("C4", dict(streams=4, originals=1000, loss_pct=24, recovery_loss_pct=0,
                                 tail_limit=400)),
     "edge_lag": ("C1", dict(originals=2000, payload_bytes=0, streams=2)),
+    # block mode with the originals added by range calls (harness
+    # Stream::add_ranges; the reference runs the same sequence as loops of
+    # its single calls): the headline shard as bench.py runs it, every byte
+    # hashed, and variable sizes
+    "smoke_C4x8r": ("C4", dict(streams=8, add_ranges=1)),
+    "C4x1024hr": ("C4", dict(streams=1024, hash_data=1, add_ranges=1)),
+    "C4r": ("C4", dict(hash_data=0, add_ranges=1)),
+    "edge_var_block_r": ("C4", dict(streams=32, originals=300, payload_bytes=0, loss_pct=30,
+                                    recovery_loss_pct=10, add_ranges=1)),
 }
 
 

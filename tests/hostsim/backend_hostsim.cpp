@@ -351,19 +351,43 @@ void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, byt
 
 static bool noexec();
 
-void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t)
+static void ingest_one(const IngestDesc& run, uint32_t k)
+{
+    IngestDesc d = run;
+    d.dst2 = (d.dst2Mask >> k & 1u) ? d.dst2 + (uint64_t)k * d.dstStride : 0;
+    d.src += (uint64_t)k * d.srcStride;
+    d.dst += (uint64_t)k * d.dstStride;
+    const uint32_t total = d.hdrLen + d.bytes;
+    // the kernel stores whole 16-byte lanes, zero past the symbol
+    const uint32_t end = (total + 15) & ~15u;
+    for (uint32_t b = 0; b < end; ++b)
+        P(d.dst)[b] = b < d.hdrLen ? d.hdr[b] : (b < total ? P(d.src)[b - d.hdrLen] : 0);
+    if (d.dst2)
+        std::memcpy(P(d.dst2), P(d.dst), end);
+}
+
+// The kernel's work assignment, block by block (a symbol the host's block
+// table misses is not copied here either)
+void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t, const uint32_t* blocks, uint32_t nblocks)
 {
     if (noexec())
         return;
-    for (uint32_t i = 0; i < count; ++i) {
-        const IngestDesc& d = descs[i];
-        const uint32_t total = d.hdrLen + d.bytes;
-        // the kernel stores whole 16-byte lanes, zero past the symbol
-        const uint32_t end = (total + 15) & ~15u;
-        for (uint32_t k = 0; k < end; ++k)
-            P(d.dst)[k] = k < d.hdrLen ? d.hdr[k] : (k < total ? P(d.src)[k - d.hdrLen] : 0);
-        if (d.dst2)
-            std::memcpy(P(d.dst2), P(d.dst), end);
+    if (!blocks) {
+        for (uint32_t i = 0; i < count; ++i)
+            ingest_one(descs[i], 0);
+        return;
+    }
+    for (uint32_t b = 0; b < nblocks; ++b) {
+        const uint32_t di = blocks[b] >> 4;
+        if (di >= count)
+            continue;
+        const IngestDesc& d = descs[di];
+        const uint32_t n = d.count ? d.count : 1u;
+        for (uint32_t w = 0; w < kIngestWaves; ++w) {
+            const uint32_t k = (blocks[b] & 15u) * kIngestWaves + w;
+            if (k < n)
+                ingest_one(d, k);
+        }
     }
 }
 

@@ -19,7 +19,7 @@ SIM_LIB = os.path.join(ROOT, "tests", "hostsim", "libsiamese_hostsim.so")
 
 _FIELDS = ("block_mode streams first_stream originals payload_bytes loss_pct "
            "recovery_loss_pct recovery_interval recovery_phase ack_policy ack_lag "
-           "tail_limit seed hash_data").split()
+           "tail_limit seed hash_data add_ranges").split()
 
 
 class Config(ctypes.Structure):
@@ -40,7 +40,7 @@ class StreamResult(ctypes.Structure):
 def make_config(**kw):
     base = dict(block_mode=0, streams=1, first_stream=0, originals=200, payload_bytes=1400,
                 loss_pct=10, recovery_loss_pct=5, recovery_interval=8, recovery_phase=0,
-                ack_policy=0, ack_lag=40, tail_limit=600, seed=1013, hash_data=1)
+                ack_policy=0, ack_lag=40, tail_limit=600, seed=1013, hash_data=1, add_ranges=0)
     base.update(kw)
     return Config(**base)
 

@@ -16,7 +16,7 @@ import golden
 import scenario_lib as S
 
 SMALL = ["smoke_C4x8", "C1", "C1var", "C2x64", "edge_tiny", "edge_var_block", "edge_heavy",
-         "edge_maxloss", "edge_lag"]
+         "edge_maxloss", "edge_lag", "smoke_C4x8r", "edge_var_block_r"]
 
 
 def _check(name, results):
@@ -27,7 +27,7 @@ def _check(name, results):
     assert [int(r.status) for r in results] == want["status"]
 
 
-@pytest.mark.parametrize("name", SMALL + ["C3", "C4x256", "C2", "C2h", "C4x1024h"])
+@pytest.mark.parametrize("name", SMALL + ["C3", "C4x256", "C2", "C2h", "C4x1024h", "C4x1024hr"])
 def test_reference_matches_golden(name, ref_available):
     if not ref_available:
         pytest.skip("oracle/_ref not built")
@@ -51,7 +51,7 @@ def test_hostsim_batch_matches_golden(name):
     assert rep.mismatches == 0
 
 
-@pytest.mark.parametrize("name", ["C2x64", "C1var", "edge_lag", "smoke_C4x8"])
+@pytest.mark.parametrize("name", ["C2x64", "C1var", "edge_lag", "smoke_C4x8", "edge_var_block_r"])
 @pytest.mark.parametrize("threads,groups", [(1, 2), (4, 2), (8, 3)])
 def test_hostsim_batch_threads_and_pipelining(name, threads, groups):
     """Streams driven from several host threads (per-thread engine shards)

@@ -80,7 +80,7 @@ void be_copy_pinned(const BeCopy* r, unsigned n, bool toDevice)
 }
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
-void be_launch_ingest(const IngestDesc*, uint32_t, uint32_t) {}
+void be_launch_ingest(const IngestDesc*, uint32_t, uint32_t, const uint32_t*, uint32_t) {}
 void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*, uint32_t) {}
 void be_launch_ldpc(const LdpcItem*, uint32_t, uint64_t*) {}
 
