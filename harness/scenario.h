@@ -214,6 +214,7 @@ struct Stream
     bool tailMode = false;        // all originals added; only encodes remain
     std::vector<uint8_t> buf;
     std::vector<Pkt> decoded;     // output of the last successful decode
+    std::vector<Pkt> getBuf;      // deliver_range's packets
     bool dataOk = true;           // every returned packet matched its payload
 
     void init(const ScenarioConfig* c, Codec* k, StreamResult* r, unsigned globalIndex)
@@ -247,6 +248,8 @@ struct Stream
     // Pull every in-order packet already present at the decoder.
     bool deliver()
     {
+        if (cfg->add_ranges)   // (one get_range: the same calls' results, the same log)
+            return deliver_range();
         while (nextExpected < cfg->originals) {
             Pkt p;
             const int r = codec->dec_get(nextExpected, &p);
@@ -267,7 +270,7 @@ struct Stream
     {
         if (nextExpected >= cfg->originals)
             return true;
-        std::vector<Pkt>& got = decoded;   // (empty outside the DECODED phase)
+        std::vector<Pkt>& got = getBuf;
         got.resize(cfg->originals - nextExpected);
         unsigned n = 0;
         const int r = codec->dec_get_range(nextExpected, (unsigned)got.size(), got.data(), &n);

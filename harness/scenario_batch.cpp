@@ -20,6 +20,7 @@
 
 #include <dlfcn.h>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -177,6 +178,48 @@ bool load_api(const char* path, Api& a)
            bind(h, a.decoder_get_range, "sgpu_decoder_get_range");
 }
 
+// SCENARIO_BATCH_CALLS=1: time every codec call by kind and print the
+// totals after each run (diagnostic: the clock reads add ~40 ns per call)
+enum CallKind { kEncAdd, kEncode, kDecAddOrig, kDecAddRec, kIsReady, kDecode, kDecGet, kRemove, kCreate, kFree,
+                kCallKinds };
+const char* const kCallNames[kCallKinds] = {"enc_add", "encode", "dec_add_orig", "dec_add_rec", "is_ready",
+                                            "decode", "dec_get", "remove", "create", "free"};
+std::atomic<uint64_t> g_calls[kCallKinds][3];   // calls, ns, items
+const bool kCallTiming = std::getenv("SCENARIO_BATCH_CALLS") != nullptr;
+
+struct CallTimer
+{
+    CallKind k;
+    uint64_t items;
+    Clock::time_point t0;
+    explicit CallTimer(CallKind kind, uint64_t n = 1) : k(kind), items(n)
+    {
+        if (kCallTiming)
+            t0 = Clock::now();
+    }
+    ~CallTimer()
+    {
+        if (!kCallTiming)
+            return;
+        g_calls[k][0].fetch_add(1, std::memory_order_relaxed);
+        g_calls[k][1].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count(),
+                                std::memory_order_relaxed);
+        g_calls[k][2].fetch_add(items, std::memory_order_relaxed);
+    }
+};
+
+void print_calls()
+{
+    if (!kCallTiming)
+        return;
+    for (unsigned k = 0; k < kCallKinds; ++k) {
+        const uint64_t c = g_calls[k][0].exchange(0), ns = g_calls[k][1].exchange(0), it = g_calls[k][2].exchange(0);
+        if (c)
+            std::fprintf(stderr, "batch %-13s %9llu calls %9llu items %10.1f us  %8.3f us/item\n", kCallNames[k],
+                         (unsigned long long)c, (unsigned long long)it, ns / 1e3, ns / 1e3 / (double)it);
+    }
+}
+
 struct Rec
 {
     unsigned bytes = 0;
@@ -293,10 +336,12 @@ struct BatchCodec
     bool needs_host_payload() const { return false; }
     int enc_add(unsigned id, const uint8_t*, unsigned bytes, unsigned* num)
     {
+        CallTimer ct(kEncAdd);
         return sh->api->encoder_add(enc, dev_payload(id), bytes, num);
     }
     int encode(Rec* r)
     {
+        CallTimer ct(kEncode);
         const int res = sh->api->encode(enc, &r->pkt);
         r->bytes = r->pkt.DataBytes;
         return res;
@@ -318,15 +363,25 @@ struct BatchCodec
             (void)sh->api->frames_recv(decTable, sh->cfg->streams, f, payload + slot, h + bytes, &r, 1, &n);
             return n == 1 ? r : Siamese_InvalidInput;
         }
+        CallTimer ct(kDecAddOrig);
         return sh->api->decoder_add_original(dec, num, dev_payload(id), bytes);
     }
-    int dec_add_recovery(const Rec& r) { return sh->api->decoder_add_recovery(dec, &r.pkt); }
-    int is_ready() { return sh->api->decoder_is_ready(dec); }
+    int dec_add_recovery(const Rec& r)
+    {
+        CallTimer ct(kDecAddRec);
+        return sh->api->decoder_add_recovery(dec, &r.pkt);
+    }
+    int is_ready()
+    {
+        CallTimer ct(kIsReady);
+        return sh->api->decoder_is_ready(dec);
+    }
     int decode(std::vector<Pkt>* out)
     {
         SiameseOriginalPacket* p = nullptr;
         unsigned n = 0;
         int r;
+        CallTimer ct(kDecode);
         if (sh->defer) {
             // (capacity: a solve's 255 packets or what single recoveries hold;
             // unused entries are handed back)
@@ -364,6 +419,7 @@ struct BatchCodec
         p.PacketNum = num;
         p.Data = nullptr;
         p.DataBytes = 0;
+        CallTimer ct(kDecGet);
         const int r = sh->api->decoder_get(dec, &p);
         out->num = num;
         out->bytes = p.DataBytes;
@@ -404,6 +460,7 @@ struct BatchCodec
             return 0;
         }
         const unsigned* l = range_lens(firstId, count);
+        CallTimer ct(kEncAdd, count);
         return sh->api->encoder_add_range(enc, dev_payload(firstId), sh->stride, l, sh->cfg->payload_bytes, count,
                                           firstNum, added);
     }
@@ -423,6 +480,7 @@ struct BatchCodec
         }
         const unsigned* l = range_lens(firstId, count);
         static_assert(sizeof(SiameseResult) == sizeof(int), "result array");
+        CallTimer ct(kDecAddOrig, count);
         return sh->api->decoder_add_original_range(dec, firstNum, dev_payload(firstId), sh->stride, l,
                                                    sh->cfg->payload_bytes, count,
                                                    reinterpret_cast<SiameseResult*>(results), calls);
@@ -441,6 +499,7 @@ struct BatchCodec
             return 0;
         }
         gets.resize(count);
+        CallTimer ct(kDecGet, count);
         const int r = sh->api->decoder_get_range(dec, firstNum, count, gets.data(), got);
         for (unsigned k = 0; k < *got; ++k) {
             out[k].num = gets[k].PacketNum;
@@ -1207,6 +1266,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
     }
     report->checked = sh.checked;
     report->mismatches = sh.mismatches;
+    print_calls();
     return rc;
 }
 

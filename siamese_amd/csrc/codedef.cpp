@@ -16,6 +16,14 @@ struct LdpcCache
     std::unordered_map<uint64_t, std::unique_ptr<std::vector<uint32_t>>> map;
     size_t bytes = 0;
     std::vector<uint32_t> scratch;
+    // direct-mapped by row in front of the map: the rows of one decode or
+    // encode share n, so a lookup is one load instead of a hash-bucket walk
+    // (cold in cache after the thread has driven other streams)
+    struct Front
+    {
+        uint32_t row = ~0u, n = 0;
+        const std::vector<uint32_t>* v = nullptr;
+    } front[256];
 };
 
 void compute(unsigned row, unsigned n, std::vector<uint32_t>& out)
@@ -57,7 +65,16 @@ const RowSelect& row_select(unsigned row) { return g_rowSelect.t[row & 255]; }
 
 const uint32_t* ldpc_offsets(unsigned row, unsigned n, unsigned* count)
 {
-    thread_local LdpcCache cache;
+    // (on the heap: the library's TLS is initial-exec and must stay small)
+    thread_local std::unique_ptr<LdpcCache> cachePtr;
+    if (!cachePtr)
+        cachePtr.reset(new LdpcCache);
+    LdpcCache& cache = *cachePtr;
+    LdpcCache::Front& f = cache.front[row & 255];
+    if (f.row == row && f.n == n) {
+        *count = (unsigned)f.v->size();
+        return f.v->data();
+    }
     const uint64_t key = ((uint64_t)row << 32) | n;
     auto it = cache.map.find(key);
     if (it == cache.map.end()) {
@@ -71,12 +88,17 @@ const uint32_t* ldpc_offsets(unsigned row, unsigned n, unsigned* count)
         if (cache.bytes + need > kMaxBytes) {
             cache.map.clear();
             cache.bytes = 0;
+            for (LdpcCache::Front& e : cache.front)
+                e = LdpcCache::Front();
         }
         std::unique_ptr<std::vector<uint32_t>> v(new std::vector<uint32_t>);
         compute(row, n, *v);
         cache.bytes += need + 64;
         it = cache.map.emplace(key, std::move(v)).first;
     }
+    f.row = row;
+    f.n = n;
+    f.v = it->second.get();
     *count = (unsigned)it->second->size();
     return it->second->data();
 }

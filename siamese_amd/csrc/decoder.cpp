@@ -3,7 +3,11 @@
 #include "decoder.h"
 
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <x86intrin.h>
 
 namespace sgpu {
 
@@ -1098,15 +1102,46 @@ SiameseResult DecoderCore::decode(SiameseOriginalPacket** packetsOut, unsigned* 
     return Siamese_NeedMoreData;
 }
 
+namespace {
+// SIAMESE_AMD_DECODE_CLOCKS=1: TSC ticks of decode_region's phases, summed
+// over all decoders and printed at exit (profiling aid)
+const bool kDecodeClocks = std::getenv("SIAMESE_AMD_DECODE_CLOCKS") != nullptr;
+struct DecodeClocks
+{
+    std::atomic<uint64_t> n{0}, rows{0}, cols{0}, fails{0}, fresh{0}, t[4];
+    ~DecodeClocks()
+    {
+        if (!kDecodeClocks || !n)
+            return;
+        std::fprintf(stderr, "decode_region %llu solved, %llu failed, %llu fresh matrices, rows %.1f cols %.1f; "
+                     "ticks/solved call: generate %.0f ge %.0f eliminate %.0f solve %.0f\n",
+                     (unsigned long long)n.load(), (unsigned long long)fails.load(), (unsigned long long)fresh.load(),
+                     (double)rows / (n + fails), (double)cols / (n + fails), (double)t[0] / n, (double)t[1] / n,
+                     (double)t[2] / n, (double)t[3] / n);
+    }
+} g_decodeClocks;
+} // namespace
+
 SiameseResult DecoderCore::decode_region()
 {
+    uint64_t c0 = kDecodeClocks ? __rdtsc() : 0, c1 = 0, c2 = 0, c3 = 0;
+    const size_t oldRowsAtEntry = rows_.size();
     geBytes_ = 0;   // (generate_matrix may resume an elimination)
     if (!generate_matrix()) {
         disabled_ = true;
         return Siamese_Disabled;
     }
+    if (kDecodeClocks)
+        c1 = __rdtsc();
     const bool solved = gaussian_elimination();
     eng_->account(geBytes_);
+    if (kDecodeClocks) {
+        c2 = __rdtsc();
+        g_decodeClocks.rows += matRows_;
+        g_decodeClocks.cols += matCols_;
+        g_decodeClocks.fails += solved ? 0 : 1;
+        g_decodeClocks.fresh += oldRowsAtEntry == 0 ? 1 : 0;
+    }
     if (!solved) {
         region_.solveFailed = true;
         stats_[SiameseDecoderStats_SolveFailCount]++;
@@ -1116,7 +1151,17 @@ SiameseResult DecoderCore::decode_region()
         disabled_ = true;
         return Siamese_Disabled;
     }
+    if (kDecodeClocks)
+        c3 = __rdtsc();
     const SiameseResult res = solve_and_substitute();
+    if (kDecodeClocks) {
+        const uint64_t c4 = __rdtsc();
+        g_decodeClocks.n++;
+        g_decodeClocks.t[0] += c1 - c0;
+        g_decodeClocks.t[1] += c2 - c1;
+        g_decodeClocks.t[2] += c3 - c2;
+        g_decodeClocks.t[3] += c4 - c3;
+    }
     region_reset();
     return res;
 }
@@ -1126,13 +1171,17 @@ SiameseResult DecoderCore::decode_region()
 
 bool DecoderCore::matrix_resize(unsigned rows, unsigned columns, bool initialize)
 {
-    // GrowingAlignedByteMatrix semantics (reference SiameseCommon.cpp:51-117)
-    const unsigned stride = align_up(columns + 4);
+    // GrowingAlignedByteMatrix semantics (reference SiameseCommon.cpp:51-117).
+    // 64 bytes more than the reference's stride: the elimination's 64-byte
+    // masked row stores then never cover the next row's pivot byte, which a
+    // store-to-load forward cannot serve (a 3-4x stall per row update), and
+    // generate_matrix has spare bytes past the columns
+    const unsigned stride = align_up(columns + 4) + 64;
     if (initialize) {
         matAllocRows_ = rows + 4;
         matStride_ = stride;
         mat_.resize((size_t)matAllocRows_ * matStride_ + kRowSlack);
-    } else if (!(rows <= matAllocRows_ && columns <= matStride_)) {
+    } else if (!(rows <= matAllocRows_ && columns + 4 <= matStride_)) {   // (a spare byte per row, generate_matrix)
         std::vector<uint8_t> nm((size_t)(rows + 4) * stride + kRowSlack);
         const unsigned copy = std::min(matCols_, columns);
         if (matCols_ > 0)
@@ -1221,7 +1270,6 @@ bool DecoderCore::generate_matrix()
     populate_rows(oldRows, rows);
 
     const unsigned startRow = (columns <= oldColumns) ? oldRows : 0;
-    const size_t matBytes = mat_.size();
 
     // The sparse picks only land on lost slots: one pass over the elements
     // the new rows span gives each its matrix column (kNoColumn: received),
@@ -1242,6 +1290,9 @@ bool DecoderCore::generate_matrix()
             pickCol_[e - pickLo] = a.bytes == 0 ? a.column : kNoColumn;
         }
     }
+    // rows of one decode share their column range: the end of the dense
+    // part for the last (columnStart, sumCount, startCol) is remembered
+    unsigned endKeyStart = ~0u, endKeyCount = 0, endKeyFrom = 0, endVal = 0;
     for (unsigned i = startRow; i < rows; ++i) {
         uint8_t* row = mrow(i);
         const RecPacket* rec = rows_[i].rec;
@@ -1268,23 +1319,36 @@ bool DecoderCore::generate_matrix()
         const uint8_t* opLo = sel.opLo;
         const uint8_t* opHi = sel.opHi;
         unsigned jEnd = startCol;
-        while (jEnd < columns && column_sub(cols_[jEnd].column, m.columnStart) < m.sumCount)
-            ++jEnd;
+        if (endKeyStart == m.columnStart && endKeyCount == m.sumCount && endKeyFrom == startCol)
+            jEnd = endVal;
+        else {
+            while (jEnd < columns && column_sub(cols_[jEnd].column, m.columnStart) < m.sumCount)
+                ++jEnd;
+            endKeyStart = m.columnStart;
+            endKeyCount = m.sumCount;
+            endKeyFrom = startCol;
+            endVal = jEnd;
+        }
         if (jEnd > startCol)
             gf_dense_row(row + startCol, colLane_.data() + startCol, colCx_.data() + startCol,
                          colCx2_.data() + startCol, opLo, opHi, rx, jEnd - startCol);
         if (jEnd < columns)
             std::memset(row + jEnd, 0, columns - jEnd);
 
-        // Sparse columns that landed on lost data
+        // Sparse columns that landed on lost data.  A pick on a received
+        // original (or on a column this row already has) lands on one of
+        // the row's spare bytes past `columns` instead of branching: they are
+        // outside the matrix, and rewritten if the matrix ever grows over them.
         unsigned picks = 0;
         const uint32_t* off = ldpc_offsets(m.row, m.ldpcCount, &picks);
-        const size_t rowOff = (size_t)i * matStride_;
         const uint32_t* pc = pickCol_.data() + (rec->elementStart - pickLo);
+        // (eight spare bytes, so picks on received originals do not chain
+        // through one byte's load-xor-store)
+        const uint8_t val[2] = {1, rx};
         for (unsigned k = 0; k < picks; ++k) {
             const uint32_t c = pc[off[k]];
-            if (c != kNoColumn && c >= startCol && rowOff + c < matBytes)
-                mat_[rowOff + c] ^= (k & 1) ? rx : 1;
+            const uint32_t at = (c < columns && c >= startCol) ? c : columns + (k & 7);
+            row[at] ^= val[k & 1];
         }
     }
 
@@ -1296,6 +1360,10 @@ bool DecoderCore::generate_matrix()
     return true;
 }
 
+namespace {
+const bool kGfni = (gf_init(), gf_gfni());
+} // namespace
+
 bool DecoderCore::eliminate_row(const uint8_t* geRow, uint8_t* remRow, unsigned pivot, unsigned end,
                                 uint8_t valI)
 {
@@ -1306,6 +1374,11 @@ bool DecoderCore::eliminate_row(const uint8_t* geRow, uint8_t* remRow, unsigned 
     const uint8_t y = gf_div(valJ, valI);
     remRow[pivot] = y;
     if (end > pivot + 1) {
+        if (kGfni) {   // one affine multiply per 64 bytes (gf.h)
+            gf_muladd_fast(remRow + pivot + 1, geRow + pivot + 1, y, end - pivot - 1);
+            geBytes_ += end - pivot - 1;
+            return true;
+        }
         // the pivot row's bytes after the pivot, split into nibbles once for
         // every row it eliminates (geSrcFor_ names the split in geSrc_)
         if (geSrcRow_ != geRow || geSrcPivot_ != pivot || geSrc_.n != end - pivot - 1) {

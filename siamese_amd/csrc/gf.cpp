@@ -2,6 +2,7 @@
 #include "gf.h"
 
 #include <immintrin.h>
+#include <cstdlib>
 #include <cstring>
 
 namespace sgpu {
@@ -9,6 +10,8 @@ namespace sgpu {
 GfTables g_gf;
 
 static bool g_ready = false;
+
+void gf_muladd_gfni(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n);
 
 bool gf_init()
 {
@@ -51,6 +54,32 @@ bool gf_init()
         }
     }
 
+    for (unsigned y = 0; y < 256; ++y) {
+        uint64_t m = 0;
+        for (unsigned i = 0; i < 8; ++i) {
+            unsigned row = 0;
+            for (unsigned j = 0; j < 8; ++j)
+                row |= ((g_gf.mul[y][1u << j] >> i) & 1u) << j;
+            m |= (uint64_t)row << (8 * (7 - i));
+        }
+        g_gf.affine[y] = m;
+    }
+    if (__builtin_cpu_supports("gfni") && __builtin_cpu_supports("avx512bw") &&
+        __builtin_cpu_supports("avx512vl") && !std::getenv("SIAMESE_AMD_NO_GFNI")) {
+        gf_muladd_fast = gf_muladd_gfni;
+        // the instruction against the tables, every y on every x
+        alignas(64) uint8_t x[256], d[256];
+        for (unsigned i = 0; i < 256; ++i)
+            x[i] = (uint8_t)i;
+        for (unsigned y = 0; y < 256; ++y) {
+            std::memset(d, 0, sizeof(d));
+            gf_muladd_gfni(d, x, (uint8_t)y, 256);
+            for (unsigned i = 0; i < 256; ++i)
+                if (d[i] != g_gf.mul[y][i])
+                    return false;
+        }
+    }
+
     // Self-check: every non-zero element times its inverse is one, and the
     // known answers the reference pins.
     for (unsigned x = 1; x < 256; ++x)
@@ -62,6 +91,33 @@ bool gf_init()
 
     g_ready = true;
     return true;
+}
+
+__attribute__((target("avx512f,avx512bw,avx512vl,gfni"))) void gf_muladd_gfni(uint8_t* dst, const uint8_t* src,
+                                                                              uint8_t y, unsigned n)
+{
+    if (y == 0 || n == 0)
+        return;
+    const __m512i a = _mm512_set1_epi64((long long)g_gf.affine[y]);
+    unsigned i = 0;
+    for (; i + 64 <= n; i += 64) {
+        const __m512i x = _mm512_loadu_si512((const void*)(src + i));
+        const __m512i d = _mm512_loadu_si512((const void*)(dst + i));
+        _mm512_storeu_si512((void*)(dst + i), _mm512_xor_si512(d, _mm512_gf2p8affine_epi64_epi8(x, a, 0)));
+    }
+    if (i < n) {
+        const __mmask64 k = (1ull << (n - i)) - 1;   // (n - i < 64)
+        const __m512i x = _mm512_maskz_loadu_epi8(k, src + i);
+        const __m512i d = _mm512_maskz_loadu_epi8(k, dst + i);
+        _mm512_mask_storeu_epi8(dst + i, k, _mm512_xor_si512(d, _mm512_gf2p8affine_epi64_epi8(x, a, 0)));
+    }
+}
+
+void (*gf_muladd_fast)(uint8_t*, const uint8_t*, uint8_t, unsigned) = gf_muladd_row;
+
+bool gf_gfni()
+{
+    return gf_muladd_fast == gf_muladd_gfni;
 }
 
 namespace {

@@ -21,6 +21,9 @@ struct GfTables
     // Nibble tables for the AVX2 row kernel: lo[y][n] = y*n, hi[y][n] = y*(n<<4)
     alignas(32) uint8_t nib_lo[256][16];
     alignas(32) uint8_t nib_hi[256][16];
+    // Multiply-by-y as the 8x8 bit matrix GF2P8AFFINEQB applies to every
+    // byte: byte 7-i of affine[y] holds, in bit j, bit i of y * 2^j
+    uint64_t affine[256];
 };
 
 extern GfTables g_gf;
@@ -54,6 +57,13 @@ void gf_row_prepare(GfRowSrc& out, const uint8_t* src, unsigned n);
 /// dst[i] ^= y * src[i] for i < src.n with the prepared src (dst writable
 /// 31 bytes past n, rewritten unchanged).
 void gf_muladd_prepared(uint8_t* dst, const GfRowSrc& src, uint8_t y);
+
+/// dst[i] ^= y * src[i] for i < n: GF2P8AFFINEQB over 64-byte masked
+/// vectors where the host has GFNI and AVX-512BW (no slack past n needed;
+/// one instruction multiplies 64 bytes by y), else gf_muladd_row.
+extern void (*gf_muladd_fast)(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n);
+/// True when gf_muladd_fast runs on GFNI.
+bool gf_gfni();
 
 /// Dense Siamese coefficients of one recovery row for `n` lost columns
 /// (reference SiameseDecoder.cpp:2278-2300): out[j] = comb(opLo[lane[j]]) ^
