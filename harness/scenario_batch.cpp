@@ -142,6 +142,15 @@ bool bind(void* h, F& fn, const char* name)
     return fn != nullptr;
 }
 
+// (range calls are optional: a library without them -- an older build in
+// an A/B -- gets loops of the single calls, the same call results)
+template <class F>
+bool bind_optional(void* h, F& fn, const char* name)
+{
+    fn = reinterpret_cast<F>(dlsym(h, name));
+    return true;
+}
+
 bool load_api(const char* path, Api& a)
 {
     void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
@@ -173,9 +182,9 @@ bool load_api(const char* path, Api& a)
            bind(h, a.frames_recv, "sgpu_frames_recv") && bind(h, a.frames_send, "sgpu_frames_send") &&
            bind(h, a.timing, "sgpu_timing") && bind(h, a.engine_stats, "sgpu_engine_stats") &&
            bind(h, a.arena_bytes, "sgpu_arena_bytes") && bind(h, a.arena_reserve, "sgpu_arena_reserve") &&
-           bind(h, a.encoder_add_range, "sgpu_encoder_add_range") &&
-           bind(h, a.decoder_add_original_range, "sgpu_decoder_add_original_range") &&
-           bind(h, a.decoder_get_range, "sgpu_decoder_get_range");
+           bind_optional(h, a.encoder_add_range, "sgpu_encoder_add_range") &&
+           bind_optional(h, a.decoder_add_original_range, "sgpu_decoder_add_original_range") &&
+           bind_optional(h, a.decoder_get_range, "sgpu_decoder_get_range");
 }
 
 // SCENARIO_BATCH_CALLS=1: time every codec call by kind and print the
@@ -446,7 +455,7 @@ struct BatchCodec
     }
     int enc_add_range(unsigned firstId, unsigned count, unsigned* firstNum, unsigned* added)
     {
-        if (sh->frames) {   // (frames: datagrams one at a time)
+        if (sh->frames || !sh->api->encoder_add_range) {   // (frames: datagrams one at a time)
             *added = 0;
             for (unsigned k = 0; k < count; ++k) {
                 unsigned num = 0;
@@ -466,7 +475,7 @@ struct BatchCodec
     }
     int dec_add_range(unsigned firstId, unsigned firstNum, unsigned count, int* results, unsigned* calls)
     {
-        if (sh->frames) {
+        if (sh->frames || !sh->api->decoder_add_original_range) {
             *calls = 0;
             for (unsigned k = 0; k < count; ++k) {
                 const int r = dec_add_original(firstId + k, (firstNum + k) & 0x3fffff, nullptr,
@@ -488,7 +497,7 @@ struct BatchCodec
     std::vector<SiameseOriginalPacket> gets;
     int dec_get_range(unsigned firstNum, unsigned count, Pkt* out, unsigned* got)
     {
-        if (sh->defer) {   // (deferred entries: one call each)
+        if (sh->defer || !sh->api->decoder_get_range) {   // (deferred entries: one call each)
             *got = 0;
             for (unsigned k = 0; k < count; ++k) {
                 const int r = dec_get((firstNum + k) & 0x3fffff, &out[k]);

@@ -270,7 +270,7 @@ SiameseResult EncoderCore::acknowledge(const uint8_t* data, unsigned bytes, unsi
 SiameseResult EncoderCore::retransmit_slot(EncSlot& s, SiameseOriginalPacket& out)
 {
     out.PacketNum = s.column;
-    out.Data = mirror_ ? s.host.data() + s.header : s.buf.ptr + s.header;
+    out.Data = mirror_ ? s.host().data() + s.header : s.buf.ptr + s.header;
     out.DataBytes = s.bytes - s.header;
     if (out.DataBytes == 0) {
         disabled_ = true;

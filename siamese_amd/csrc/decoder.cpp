@@ -325,9 +325,9 @@ SiameseResult DecoderCore::add_original(const SiameseOriginalPacket& packet, uin
     else
         prog_.ingest_host(s.buf, packet.Data, packet.DataBytes, hdr, h);
     if (mirror_) {
-        s.host.resize(h + packet.DataBytes);
-        std::memcpy(s.host.data(), hdr, h);
-        std::memcpy(s.host.data() + h, packet.Data, packet.DataBytes);
+        s.host().resize(h + packet.DataBytes);
+        std::memcpy(s.host().data(), hdr, h);
+        std::memcpy(s.host().data() + h, packet.Data, packet.DataBytes);
     }
     return Siamese_Success;
 }
@@ -701,7 +701,8 @@ void DecSubwindowRecycle::operator()(DecSubwindow* w) const
         s.buf = DevBuf();
         s.inSlab = false;
         s.header = 0;
-        s.host.clear();
+        if (s.hostp)
+            s.hostp->clear();
     }
     ObjPool<DecSubwindow>::put(w);
 }
@@ -930,9 +931,9 @@ bool DecoderCore::add_single(const RowMeta& m, const uint8_t* headBytes, unsigne
     } else
         prog_.ingest_device(s.buf, devData + headerBytes, length, hdr, h);
     if (mirror_) {
-        s.host.resize(h + length);
-        std::memcpy(s.host.data(), hdr, h);
-        std::memcpy(s.host.data() + h, (const uint8_t*)hostData + headerBytes, length);
+        s.host().resize(h + length);
+        std::memcpy(s.host().data(), hdr, h);
+        std::memcpy(s.host().data() + h, (const uint8_t*)hostData + headerBytes, length);
     }
     s.header = h;
     s.bytes = h + length;
@@ -950,7 +951,7 @@ bool DecoderCore::add_single(const RowMeta& m, const uint8_t* headBytes, unsigne
         SiameseOriginalPacket out;
         out.PacketNum = m.columnStart;
         out.DataBytes = length;
-        out.Data = (mirror_ ? s.host.data() : s.buf.ptr) + h;
+        out.Data = (mirror_ ? s.host().data() : s.buf.ptr) + h;
         recovered_.push_back(out);
         publish_outputs();
     }
@@ -1777,13 +1778,13 @@ void DecoderCore::apply_resolved()
                 s->bytes = hdr + len;
                 s->header = hdr;
                 s->pending = false;
-                if (mirror_ && s->host.size() < s->bytes)
-                    s->host.resize(s->bytes);
+                if (mirror_ && s->host().size() < s->bytes)
+                    s->host().resize(s->bytes);
             }
             if (mirror_ && pd.serial == decodeSerial_ && ci < recovered_.size()) {
                 SiameseOriginalPacket& out = recovered_[ci];
                 out.DataBytes = len;
-                out.Data = s->host.data() + hdr;
+                out.Data = s->host().data() + hdr;
             }
         }
         pd.live = false;
@@ -1799,8 +1800,8 @@ void DecoderCore::download_recovered()
         return;
     for (const Fix& f : lastDecoded_) {
         DecSlot* s = f.slot;
-        s->host.resize(f.bound);
-        eng_->download(s->host.data(), (uint64_t)(uintptr_t)f.buf, f.bound);
+        s->host().resize(f.bound);
+        eng_->download(s->host().data(), (uint64_t)(uintptr_t)f.buf, f.bound);
     }
     lastDecoded_.clear();
 }
@@ -1825,7 +1826,7 @@ SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
             return Siamese_Disabled;
     }
     DecSlot& s = slot(element);
-    packet.Data = (mirror_ ? s.host.data() : s.buf.ptr) + s.header;
+    packet.Data = (mirror_ ? s.host().data() : s.buf.ptr) + s.header;
     packet.DataBytes = s.bytes - s.header;
     return Siamese_Success;
 }
@@ -1886,7 +1887,7 @@ SiameseResult DecoderCore::get_deferred(SiameseOriginalPacket& packet)
     }
     DecSlot& s = slot(element);
     if (!s.pending) {
-        packet.Data = (mirror_ ? s.host.data() : s.buf.ptr) + s.header;
+        packet.Data = (mirror_ ? s.host().data() : s.buf.ptr) + s.header;
         packet.DataBytes = s.bytes - s.header;
         return Siamese_Success;
     }

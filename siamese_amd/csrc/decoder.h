@@ -38,7 +38,15 @@ struct DecSlot
     bool pending = false;       // recovered, exact length not yet known
     uint32_t pendSlot = 0;      // while pending: the solve that recovers it (Resolver::pend index)
     uint32_t pendCi = 0;        //   and its column within that solve
-    std::vector<uint8_t> host;  // host mirror (drop-in mode)
+    // host mirror (drop-in mode only): out of line, so the batch path's
+    // window scans touch a 48-byte slot
+    std::unique_ptr<std::vector<uint8_t>> hostp;
+    std::vector<uint8_t>& host()
+    {
+        if (!hostp)
+            hostp.reset(new std::vector<uint8_t>);
+        return *hostp;
+    }
 };
 
 struct DecSubwindow

@@ -119,9 +119,9 @@ SiameseResult EncoderCore::add(SiameseOriginalPacket& packet, uint64_t deviceSrc
     else
         prog_.ingest_host(s.buf, packet.Data, packet.DataBytes, hdr, h);
     if (mirror_) {
-        s.host.resize(h + packet.DataBytes);
-        std::memcpy(s.host.data(), hdr, h);
-        std::memcpy(s.host.data() + h, packet.Data, packet.DataBytes);
+        s.host().resize(h + packet.DataBytes);
+        std::memcpy(s.host().data(), hdr, h);
+        std::memcpy(s.host().data() + h, packet.Data, packet.DataBytes);
     }
     fill_slot(s, column, h, packet.DataBytes, (uint32_t)now_msec());
     return Siamese_Success;
@@ -381,7 +381,7 @@ SiameseResult EncoderCore::get(SiameseOriginalPacket& packet)
     }
     EncSlot& s = slot(element);
     packet.PacketNum = s.column;
-    packet.Data = mirror_ ? s.host.data() + s.header : s.buf.ptr + s.header;
+    packet.Data = mirror_ ? s.host().data() + s.header : s.buf.ptr + s.header;
     packet.DataBytes = s.bytes - s.header;
     return Siamese_Success;
 }

@@ -26,7 +26,15 @@ struct EncSlot
     unsigned column = 0;
     unsigned header = 0;        // length-prefix bytes
     uint32_t lastSend = 0;      // msec timestamp of the last (re)send (ARQ)
-    std::vector<uint8_t> host;  // host mirror (drop-in mode only)
+    // host mirror (drop-in mode only): out of line, so the batch path's
+    // window scans touch a 48-byte slot
+    std::unique_ptr<std::vector<uint8_t>> hostp;
+    std::vector<uint8_t>& host()
+    {
+        if (!hostp)
+            hostp.reset(new std::vector<uint8_t>);
+        return *hostp;
+    }
 };
 
 struct EncSubwindow
@@ -47,7 +55,8 @@ struct EncSubwindowRecycle
             s.inSlab = false;
             s.bytes = s.column = s.header = 0;
             s.lastSend = 0;
-            s.host.clear();
+            if (s.hostp)
+                s.hostp->clear();
         }
         ObjPool<EncSubwindow>::put(w);
     }
