@@ -115,29 +115,65 @@ def host_info():
     return {"nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": model}
 
 
-def cpu_baseline(cfg, threads, sample):
+class CpuBaseline:
     """The reference codec on `threads` host cores over `cfg` (a bounded
-    sample of the workload).  value = the reference's own algorithmic bytes
-    for exactly this sample (op-counting build, one untimed run) over the
-    time spent inside codec calls (the longest thread's, when several drive
-    their own streams at once); payload generation is not timed."""
-    if not os.path.exists(S.REF_LIB):
-        return None
-    alg = ref_algorithmic_bytes(cfg, threads)
-    res, sec, wall = S.run_capi(S.REF_LIB, cfg, threads=threads)
-    if alg is None or sec <= 0 or any(r.status for r in res):
-        return None
-    payload = sum(r.payload_bytes for r in res)
-    return {
-        "value": round(alg / sec / 1e9, 3),
-        "unit": "GB/s",
-        "payload_GBps": round(payload / sec / 1e9, 3),
-        "cores": threads,
-        "kind": "reference",
-        "sample": "%s on %d thread%s: %.4f s in codec calls (%.4f s wall), %d algorithmic bytes"
-                  % (sample, threads, "s" if threads > 1 else "", sec, wall, alg),
-        "host": host_info(),
-    }
+    sample of the workload), measured once per measure() call so the runs can
+    be interleaved with the GPU runs they are compared to.  A run's value =
+    the reference's own algorithmic bytes for exactly this sample
+    (op-counting build, one untimed run) over the time spent inside codec
+    calls (the longest thread's, when several drive their own streams at
+    once); payload generation is not timed.  The reported value is the
+    median run."""
+
+    def __init__(self, cfg, threads, sample):
+        self.cfg, self.threads, self.sample = cfg, threads, sample
+        self.alg = ref_algorithmic_bytes(cfg, threads) if os.path.exists(S.REF_LIB) else None
+        self.runs = []   # (GB/s, codec seconds, wall seconds, payload bytes)
+
+    def measure(self):
+        if self.alg is None:
+            return None
+        res, sec, wall = S.run_capi(S.REF_LIB, self.cfg, threads=self.threads)
+        if sec <= 0 or any(r.status for r in res):
+            return None
+        v = self.alg / sec / 1e9
+        self.runs.append((v, sec, wall, sum(r.payload_bytes for r in res)))
+        return v
+
+    def result(self, gpu_values=None):
+        """gpu_values: the GPU run beside each CPU run (same order), for
+        per-run ratios."""
+        if not self.runs:
+            return None
+        order = sorted(range(len(self.runs)), key=lambda i: self.runs[i][0])
+        v, sec, wall, payload = self.runs[order[len(order) // 2]]
+        out = {
+            "value": round(v, 3),
+            "unit": "GB/s",
+            "payload_GBps": round(payload / sec / 1e9, 3),
+            "cores": self.threads,
+            "kind": "reference",
+            "runs_all": [round(r[0], 3) for r in self.runs],
+            "sample": "%s on %d thread%s: median of %d runs, %.4f s in codec calls (%.4f s wall), "
+                      "%d algorithmic bytes" % (self.sample, self.threads, "s" if self.threads > 1 else "",
+                                                len(self.runs), sec, wall, self.alg),
+            "host": host_info(),
+        }
+        if gpu_values:
+            ratios = [g / r[0] for g, r in zip(gpu_values, self.runs) if g and r[0]]
+            if ratios:
+                out["ratio"] = [round(x, 2) for x in ratios]
+                out["ratio_median"] = round(sorted(ratios)[len(ratios) // 2], 2)
+                out["ratio_note"] = "GPU value / reference value of the runs taken side by side"
+        return out
+
+
+def cpu_baseline(cfg, threads, sample, runs=3):
+    """CpuBaseline over `runs` back-to-back runs (no GPU runs beside it)."""
+    cb = CpuBaseline(cfg, threads, sample)
+    for _ in range(runs):
+        cb.measure()
+    return cb.result()
 
 
 class Collective:
@@ -186,8 +222,10 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
     a stream submits after every `defer`-th decode and is driven on while
     up to two of its submissions run (profiles/r3c_defer_sweep.txt)."""
     groups = 2 if cfg.streams >= 64 else 1
+    cb = CpuBaseline(cpu_cfg, cpu_threads, cpu_sample) if cpu_cfg is not None else None
     sess = S.BatchSession(library, cfg, device=device)
     per = []
+    gpu_vals = []
     try:
         res, rep = sess.run(steps=0, warmup=1, verify=True, threads=threads, groups=groups,
                             defer=defer)
@@ -195,23 +233,32 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
             raise RuntimeError("bench leg %s: verification failed" % name)
         # the timed runs without per-launch timing events (each orders its
         # launch behind a timestamp: +30 % on C3, profiles/r3f_timing_ab.txt),
-        # then one more run with them for the device and executor times
+        # each followed by a run of the reference on the host (interleaved,
+        # so both see the same box), then one more GPU run with the events
+        # for the device and per-kernel times
         for _ in range(runs):
             res, rep = sess.run(steps=1, warmup=0, verify=False, threads=threads, groups=groups,
                                 digest=False, defer=defer, timing=False)
             per.append(rep)
+            if cb is not None:
+                _, a = engine_bytes(rep)
+                gpu_vals.append(a / rep.seconds / 1e9)
+                cb.measure()
         _, trep = sess.run(steps=1, warmup=0, verify=False, threads=threads, groups=groups,
                            digest=False, defer=defer, timing=True)
     finally:
         sess.close()
-    per.sort(key=lambda r: r.seconds)
-    rep = per[len(per) // 2]   # the median run
+    order = sorted(range(len(per)), key=lambda i: per[i].seconds)
+    rep = per[order[len(order) // 2]]   # the median run
     eng, alg = engine_bytes(rep)
     teng, talg = engine_bytes(trep)
     payload = rep.payload_bytes   # (one run)
     sec = rep.seconds
-    exec_s = trep.exec_ms / 1e3
-    exec_bytes = talg - teng["solve_bytes"]
+    kms = dict(zip(S.KERNELS, trep.kernel_ms))
+    exec_s = kms["k_exec"] / 1e3
+    ldpc_s = kms["k_ldpc"] / 1e3
+    exec_bytes = talg - teng["solve_bytes"] - teng["ldpc_bytes"]
+    ldpc_bytes = teng["ldpc_bytes"]
     out = {
         "workload": "%d stream%s x %d originals x %d B, %d%% loss" % (
             cfg.streams, "s" if cfg.streams > 1 else "", cfg.originals, cfg.payload_bytes,
@@ -225,6 +272,7 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
         "unit": "GB/s",
         "payload_GBps": round(payload / sec / 1e9, 3),
         "device_ms_per_run": round(trep.device_ms, 3),
+        "kernel_ms_per_run": {k: round(v, 3) for k, v in kms.items()},
         "device_ms_note": "one extra run with per-launch HIP events (the timed runs have none)",
         "rounds_per_run": rep.rounds,
         "algorithmic_bytes_per_run": alg,
@@ -234,11 +282,19 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
             "achieved": round(exec_bytes / exec_s / 1e9, 2) if exec_s > 0 else None,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(exec_bytes / exec_s / 1e9 / HBM_PEAK_GBPS, 4) if exec_s > 0 else None,
+            "bytes_per_run": exec_bytes,
         },
+        "roofline_ldpc": {
+            "bound": "hbm", "kernel": "k_ldpc",
+            "achieved": round(ldpc_bytes / ldpc_s / 1e9, 2) if ldpc_s > 0 else None,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(ldpc_bytes / ldpc_s / 1e9 / HBM_PEAK_GBPS, 4) if ldpc_s > 0 else None,
+            "bytes_per_run": ldpc_bytes,
+        } if ldpc_bytes else None,
         "cpu_baseline": None,
     }
-    if cpu_cfg is not None:
-        out["cpu_baseline"] = cpu_baseline(cpu_cfg, cpu_threads, cpu_sample)
+    if cb is not None:
+        out["cpu_baseline"] = cb.result(gpu_vals)
     return out
 
 
@@ -323,12 +379,26 @@ def run_rank(rank, world, local, args, library, use_cuda):
         sess.run(steps=args.warmup, warmup=0, verify=False, threads=args.threads,
                  groups=args.groups, digest=False, defer=args.defer)
 
+    # the reference on the host cores (rank 0 at N=1 only) over a bounded
+    # sample of C4 streams, one run before the timed steps, one after them
+    # and one after the end-to-end leg (interleaved with the GPU's runs)
+    cb = None
+    if not args.no_cpu and world == 1:
+        threads = min(16, host_info()["usable_cpus"] or 1)
+        sample_cfg = S.replace(S.CONFIGS["C4"], streams=args.cpu_streams, first_stream=0,
+                               hash_data=0, add_ranges=1 if args.ranges else 0)
+        cb = CpuBaseline(sample_cfg, threads, "%d C4 streams (256 x 1400 B, 20%% loss, block mode)"
+                         % args.cpu_streams)
+        cb.measure()
+
     coll.barrier()
     t0 = time.perf_counter()
     res, rep = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
                         groups=args.groups, digest=False, defer=args.defer)
     coll.barrier()
     elapsed = time.perf_counter() - t0
+    if cb is not None:
+        cb.measure()
 
     # End-to-end (PCIe-inclusive) leg, timed separately: the originals start
     # in pinned host memory and every recovery packet and recovered original
@@ -352,6 +422,8 @@ def run_rank(rank, world, local, args, library, use_cuda):
         coll.barrier()
         e2e_elapsed = time.perf_counter() - t1
     sess.close()
+    if cb is not None:
+        cb.measure()
 
     eng, alg_bytes = engine_bytes(rep)
     payload = rep.payload_bytes   # (all timed steps)
@@ -408,6 +480,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
         "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
         "device": {
             "exec_ms_per_step": round(rep.exec_ms / steps, 3),
+            "kernel_ms_per_step": {k: round(v / steps, 3) for k, v in zip(S.KERNELS, rep.kernel_ms)},
             "device_ms_per_step": round(rep.device_ms / steps, 3),
             "rounds_per_step": rep.rounds / steps,
             "launches_per_step": eng["launches"] / steps,
@@ -465,14 +538,8 @@ def run_rank(rank, world, local, args, library, use_cuda):
                         if args.frames else "",
                         "(framed by sgpu_frames_send) " if args.frames else ""),
         }
-    if not args.no_cpu and world == 1:
-        # the reference on the host cores, rank 0 at N=1 only, on a bounded
-        # sample of C4 streams
-        threads = min(16, host_info()["usable_cpus"] or 1)
-        sample_cfg = S.replace(S.CONFIGS["C4"], streams=args.cpu_streams, first_stream=0,
-                               hash_data=0)
-        line["cpu_baseline"] = cpu_baseline(
-            sample_cfg, threads, "%d C4 streams (256 x 1400 B, 20%% loss, block mode)" % args.cpu_streams)
+    if cb is not None:
+        line["cpu_baseline"] = cb.result([value] * len(cb.runs))
     return line
 
 

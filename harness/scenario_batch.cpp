@@ -65,7 +65,7 @@ struct BatchReport
     double exec_ms;        ///< device time of the executor launches only
     double setup_seconds;  ///< payload generation + staging (untimed)
     uint64_t rounds;       ///< rounds (flushes) in the timed steps
-    uint64_t engine[16];   ///< engine counters over the timed steps (see sgpu_engine_stats),
+    uint64_t engine[17];   ///< engine counters over the timed steps (see sgpu_engine_stats_ex),
                            ///< then the arena growth (sgpu_arena_bytes)
     uint64_t checked;      ///< packets whose bytes were verified
     uint64_t mismatches;   ///< verification failures
@@ -74,13 +74,14 @@ struct BatchReport
     /// + completion), token resolution, finish + free
     double phase_seconds[5];
     uint64_t payload_bytes;   ///< payload bytes of the originals added in the timed steps (all steps)
+    double kernel_ms[4];      ///< device time by kernel class (sgpu_timing_kernels)
 };
 
 } // extern "C"
 
 namespace {
 
-constexpr int kEngineStats = 15;
+constexpr int kEngineStats = 16;
 using Clock = std::chrono::steady_clock;
 
 struct Api
@@ -129,6 +130,8 @@ struct Api
     int (*gather_wait)(long long);
     void (*timing)(int, int, double*, double*);
     void (*engine_stats)(uint64_t*);
+    void (*engine_stats_ex)(uint64_t*, unsigned);
+    void (*timing_kernels)(double*, unsigned);
     uint64_t (*arena_bytes)(void);
     int (*arena_reserve)(size_t);
 };
@@ -184,7 +187,9 @@ bool load_api(const char* path, Api& a)
            bind(h, a.arena_bytes, "sgpu_arena_bytes") && bind(h, a.arena_reserve, "sgpu_arena_reserve") &&
            bind_optional(h, a.encoder_add_range, "sgpu_encoder_add_range") &&
            bind_optional(h, a.decoder_add_original_range, "sgpu_decoder_add_original_range") &&
-           bind_optional(h, a.decoder_get_range, "sgpu_decoder_get_range");
+           bind_optional(h, a.decoder_get_range, "sgpu_decoder_get_range") &&
+           bind_optional(h, a.engine_stats_ex, "sgpu_engine_stats_ex") &&
+           bind_optional(h, a.timing_kernels, "sgpu_timing_kernels");
 }
 
 // SCENARIO_BATCH_CALLS=1: time every codec call by kind and print the
@@ -1251,20 +1256,30 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         if (timed && api.arena_reserve(api.arena_bytes() / 4) != 0)
             return -2;
         uint64_t e0[kEngineStats + 1], e1[kEngineStats + 1];
-        api.engine_stats(e0);
-        e0[kEngineStats] = api.arena_bytes();
+        auto stats = [&](uint64_t* e) {
+            e[kEngineStats - 1] = 0;
+            if (api.engine_stats_ex)
+                api.engine_stats_ex(e, kEngineStats);
+            else
+                api.engine_stats(e);   // (an older build: no k_ldpc bytes)
+            e[kEngineStats] = api.arena_bytes();
+        };
+        stats(e0);
         api.timing(timed && !opt->no_timing ? 1 : 0, 1, nullptr, nullptr);
         const auto t1 = Clock::now();
         rc = run_pipeline(sh, results, timed ? opt->steps : 1, &rounds, phase, &payload);
         const double dt = std::chrono::duration<double>(Clock::now() - t1).count();
-        double execMs = 0, totalMs = 0;
+        double execMs = 0, totalMs = 0, kernelMs[4] = {0, 0, 0, 0};
+        if (api.timing_kernels)
+            api.timing_kernels(kernelMs, 4);
         api.timing(0, 1, &execMs, &totalMs);
-        api.engine_stats(e1);
-        e1[kEngineStats] = api.arena_bytes();
+        stats(e1);
         if (timed) {
             report->seconds += dt;
             report->device_ms += totalMs;
             report->exec_ms += execMs;
+            for (int k = 0; k < 4; ++k)
+                report->kernel_ms[k] += kernelMs[k];
             report->rounds += rounds;
             report->payload_bytes += payload;
             for (int k = 0; k < 5; ++k)

@@ -262,6 +262,10 @@ SIAMESE_EXPORT long long sgpu_frames_send(unsigned count, const SgpuRecoveryPack
 
 /// Device timing of flushed work since the last reset (milliseconds).
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs);
+/// Device milliseconds per kernel class since the last sgpu_timing reset,
+/// while timing is enabled: [0] k_ingest, [1] k_exec, [2] k_ldpc, [3] the
+/// solve kernels (k_solve_prefix + k_solve_main); count entries at most.
+SIAMESE_EXPORT void sgpu_timing_kernels(double* msOut, unsigned count);
 /// Engine counters (15 values): flushes, launches, ops, terms, solves,
 /// ingests, upload bytes, algorithmic op bytes, algorithmic output bytes,
 /// the part of the algorithmic bytes handled by the solve kernels, then host
@@ -269,6 +273,9 @@ SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* t
 /// running completions, and reclaiming released buffers, then the number of
 /// executor launches.
 SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15);
+/// sgpu_engine_stats' 15 values, then the algorithmic bytes of k_ldpc (the
+/// wide rows' picks, part of the algorithmic op bytes); count entries at most.
+SIAMESE_EXPORT void sgpu_engine_stats_ex(uint64_t* out, unsigned count);
 
 /// Device bytes the engine's symbol arena has taken from hipMalloc so far
 /// (grows while warming up, then stays flat: buffers are recycled).

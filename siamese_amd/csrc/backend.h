@@ -104,7 +104,12 @@ bool be_mark_sync(void* mark);
 
 /// Device-time accounting: every executor/solve launch is bracketed with
 /// events; these return the accumulated milliseconds since the last reset.
+/// Kernel classes of the per-launch device timing.
+enum BeKernel { kBeIngest, kBeExec, kBeLdpc, kBeSolve, kBeKernelKinds };
 void be_timing_enable(bool on);
+/// Device milliseconds of one kernel class since the last reset
+/// (be_timing_exec_ms is kBeExec's).
+double be_timing_kernel_ms(BeKernel kind);
 void be_timing_reset();
 double be_timing_exec_ms();
 double be_timing_total_ms();

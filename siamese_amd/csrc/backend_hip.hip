@@ -2593,11 +2593,12 @@ bool g_timing = false;
 // free; SGPU_STAGE overrides (0 = read every element from memory)
 uint32_t g_stageCap = 0;
 double g_execMs = 0, g_totalMs = 0;
+double g_kernelMs[kBeKernelKinds] = {};   // by BeKernel
 
 struct EvPair
 {
     hipEvent_t a, b;
-    bool exec;
+    BeKernel kind;
 };
 // Launches come from the engine's launcher thread, fence waits from its
 // completer thread: the event lists are shared under g_evMu.
@@ -2606,7 +2607,7 @@ std::vector<EvPair> g_evFree;
 std::deque<EvPair> g_evUsed;
 std::vector<hipEvent_t> g_fenceFree;
 
-EvPair take_events(bool exec)
+EvPair take_events(BeKernel kind)
 {
     EvPair e;
     {
@@ -2614,13 +2615,13 @@ EvPair take_events(bool exec)
         if (!g_evFree.empty()) {
             e = g_evFree.back();
             g_evFree.pop_back();
-            e.exec = exec;
+            e.kind = kind;
             return e;
         }
     }
     (void)hipEventCreate(&e.a);
     (void)hipEventCreate(&e.b);
-    e.exec = exec;
+    e.kind = kind;
     return e;
 }
 
@@ -2628,11 +2629,11 @@ struct Timed
 {
     EvPair ev;
     bool on;
-    explicit Timed(bool exec) : on(g_timing)
+    explicit Timed(BeKernel kind) : on(g_timing)
     {
         bind_device();
         if (on) {
-            ev = take_events(exec);
+            ev = take_events(kind);
             (void)hipEventRecord(ev.a, g_stream);
         }
     }
@@ -2658,7 +2659,8 @@ void harvest_timing(bool all)
         float ms = 0;
         (void)hipEventElapsedTime(&ms, ev.a, ev.b);
         g_totalMs += ms;
-        if (ev.exec)
+        g_kernelMs[ev.kind] += ms;
+        if (ev.kind == kBeExec)
             g_execMs += ms;
         g_evFree.push_back(ev);
         g_evUsed.pop_front();
@@ -2961,7 +2963,7 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes
 {
     if (count == 0)
         return;
-    Timed t(false);
+    Timed t(kBeIngest);
     const uint32_t chunks = maxBytes ? (maxBytes + kIngestChunkBytes - 1) / kIngestChunkBytes : 1;
     const uint32_t grid = blocks ? nblocks : (count + kIngestWaves - 1) / kIngestWaves;
     if (grid == 0)
@@ -2974,7 +2976,7 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
 {
     if (count == 0)
         return;
-    Timed t(true);
+    Timed t(kBeExec);
     // LDS stage: the 24 sums plus the largest OP_ROWS window of the launch,
     // up to the device's budget (none for launches without row batches)
     uint32_t slots = 0;
@@ -2989,7 +2991,7 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
 {
     if (count == 0)
         return;
-    Timed t(true);   // (part of the executor's work: counted as exec time)
+    Timed t(kBeLdpc);
     hipLaunchKernelGGL(k_ldpc, dim3(count), dim3(64 * kLdpcWaves), 0, g_stream, items,
                        reinterpret_cast<unsigned long long*>(acct));
 }
@@ -3000,7 +3002,7 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 {
     if (count == 0)
         return;
-    Timed t(false);
+    Timed t(kBeSolve);
     const uint32_t rowsCap = maxRows < kSolveLdsMaxRows ? maxRows : kSolveLdsMaxRows;
     // Many solves: their prefixes in one wave each first (once per solve, all
     // in parallel); few (single-stream flushes): fused into the tiles, one
@@ -3184,8 +3186,15 @@ void be_timing_enable(bool on)
     }();
     g_timing = on && allowed;
 }
+double be_timing_kernel_ms(BeKernel kind)
+{
+    return kind < kBeKernelKinds ? g_kernelMs[kind] : 0.0;
+}
+
 void be_timing_reset()
 {
+    for (double& v : g_kernelMs)
+        v = 0;
     g_execMs = 0;
     g_totalMs = 0;
 }

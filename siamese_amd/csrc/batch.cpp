@@ -507,6 +507,23 @@ SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* t
         be_timing_reset();
 }
 
+SIAMESE_EXPORT void sgpu_timing_kernels(double* msOut, unsigned count)
+{
+    for (unsigned k = 0; k < count && k < kBeKernelKinds; ++k)
+        msOut[k] = be_timing_kernel_ms((BeKernel)k);
+}
+
+SIAMESE_EXPORT void sgpu_engine_stats_ex(uint64_t* out, unsigned count)
+{
+    const EngineStats s = Engine::global()->stats();
+    const uint64_t v[16] = {s.flushes,    s.launches,    s.ops,        s.terms,    s.solves,
+                            s.ingests,    s.uploadBytes, s.refOpBytes, s.outBytes, s.solveBytes,
+                            s.assembleNs, s.waitNs,      s.completeNs, s.reclaimNs,
+                            s.execLaunches, s.ldpcBytes};
+    for (unsigned k = 0; k < count && k < 16; ++k)
+        out[k] = v[k];
+}
+
 SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15)
 {
     const EngineStats s = Engine::global()->stats();

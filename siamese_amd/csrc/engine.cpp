@@ -31,6 +31,7 @@ void EngineStats::add(const EngineStats& o)
     refOpBytes += o.refOpBytes;
     outBytes += o.outBytes;
     solveBytes += o.solveBytes;
+    ldpcBytes += o.ldpcBytes;
     assembleNs += o.assembleNs;
     waitNs += o.waitNs;
     completeNs += o.completeNs;
@@ -1216,7 +1217,7 @@ void Engine::ensure_down(XferSet& x, size_t bytes)
     x.downDev = (uint8_t*)be_dev_alloc(cap);
     x.downCap = cap;
     x.acctZero = true;
-    x.acctPrev[0] = x.acctPrev[1] = x.acctPrev[2] = 0;
+    x.acctPrev[0] = x.acctPrev[1] = x.acctPrev[2] = x.acctPrev[3] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -2004,7 +2005,7 @@ void Engine::launch_batch(Batch& bt)
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
     if (xs.acctZero) {
-        be_memset(acctDev, 0, 3 * sizeof(uint64_t));
+        be_memset(acctDev, 0, 4 * sizeof(uint64_t));
         xs.acctZero = false;
     }
     if (bt.wideZero)
@@ -2016,12 +2017,12 @@ void Engine::launch_batch(Batch& bt)
     for (size_t k = 0; k < bt.phases.size() && bt.phases[k].kind == Phase::EXEC; ++k)
         wideDone = bt.phases[k].wideBegin + bt.phases[k].wideCount;
     if (wideDone)
-        be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide), (uint32_t)wideDone, acctDev);
+        be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide), (uint32_t)wideDone, acctDev + 3);
     for (const Phase& ph : bt.phases) {
         if (ph.kind == Phase::EXEC) {
             if (ph.wideCount && ph.wideBegin >= wideDone)
                 be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide) + ph.wideBegin, (uint32_t)ph.wideCount,
-                               acctDev);
+                               acctDev + 3);
             be_launch_exec(bt.upBase + bt.oStream, (const ExecItem*)(bt.upBase + bt.oItems) + ph.itemBegin,
                            (uint32_t)ph.itemCount, acctDev, ph.maxRows);
             st.execLaunches++;
@@ -2125,15 +2126,16 @@ bool Engine::complete_batch(Batch& bt)
     // bytes the kernels counted: terms the executor expanded itself, and the
     // solves' back-substitution (source bytes, recovered bytes); the device
     // counters of a transfer set only grow
-    uint64_t acct[3], cur[3];
+    uint64_t acct[4], cur[4];
     std::memcpy(cur, xs.downHost, sizeof(cur));
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 4; ++k) {
         acct[k] = cur[k] - xs.acctPrev[k];
         xs.acctPrev[k] = cur[k];
     }
-    st.refOpBytes += acct[0] + acct[1];
+    st.refOpBytes += acct[0] + acct[1] + acct[3];
     st.outBytes += acct[2];
     st.solveBytes += acct[1] + acct[2];
+    st.ldpcBytes += acct[3];
     const uint32_t* results = (const uint32_t*)(xs.downHost + kAcctBytes);
     for (int g = 0; g < 2; ++g)
         for (size_t i = 0; i < bt.bodies[g].size(); ++i) {

@@ -310,6 +310,7 @@ struct EngineStats
     // originals produced.
     uint64_t refOpBytes = 0, outBytes = 0;
     uint64_t solveBytes = 0;   // the part of both done by the solve kernels
+    uint64_t ldpcBytes = 0;    // the part of refOpBytes done by k_ldpc (wide rows' picks)
     // host time of flush assembly (launcher thread), device waits and
     // completion callbacks (completer thread), and returning released
     // buffers to the arena (nanoseconds)
@@ -517,7 +518,7 @@ private:
         size_t wideUsed = 0;          // bytes of the ring dirtied since it was zeroed
         // the device byte counters at the head of downDev only grow (no
         // memset per submission): each completion takes the difference
-        uint64_t acctPrev[3] = {0, 0, 0};
+        uint64_t acctPrev[4] = {0, 0, 0, 0};
         bool acctZero = false;        // fresh downDev: zero the counters first
     } sets_[kSets];
     void ensure_up(XferSet& x, size_t bytes);

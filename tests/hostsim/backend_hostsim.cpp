@@ -586,6 +586,7 @@ void* be_fence() { return reinterpret_cast<void*>(1); }
 bool be_fence_wait(void*, unsigned) { return be_sync(); }
 void be_timing_enable(bool) {}
 void be_timing_reset() {}
+double be_timing_kernel_ms(BeKernel) { return 0; }
 double be_timing_exec_ms() { return 0; }
 double be_timing_total_ms() { return 0; }
 

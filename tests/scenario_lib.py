@@ -85,9 +85,12 @@ class BatchOptions(ctypes.Structure):
 class BatchReport(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("device_ms", ctypes.c_double),
                 ("exec_ms", ctypes.c_double), ("setup_seconds", ctypes.c_double),
-                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 16),
+                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 17),
                 ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64),
-                ("phase_seconds", ctypes.c_double * 5), ("payload_bytes", ctypes.c_uint64)]
+                ("phase_seconds", ctypes.c_double * 5), ("payload_bytes", ctypes.c_uint64),
+                ("kernel_ms", ctypes.c_double * 4)]
+
+KERNELS = ("k_ingest", "k_exec", "k_ldpc", "k_solve")
 
 PHASES = ("create", "step", "flush", "resolve", "finish")
 
@@ -154,7 +157,7 @@ def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0
 
 ENGINE_KEYS = ("flushes launches ops terms solves ingests upload_bytes ref_op_bytes "
                "out_bytes solve_bytes assemble_ns wait_ns complete_ns reclaim_ns "
-               "exec_launches arena_growth").split()
+               "exec_launches ldpc_bytes arena_growth").split()
 
 
 def engine_dict(report):
