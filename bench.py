@@ -334,6 +334,47 @@ def dropin_leg(library, use_cpu, runs=5):
     return out
 
 
+def dropin_threads_leg(library, use_cpu, threads=16, runs=3):
+    """C2 through the drop-in siamese.h ABI from `threads` application
+    threads at once, each driving its own 1024/threads streams (per-instance
+    calls concurrent, flushes group-committed), every stream's digest
+    checked against the reference's own run of the same streams; the
+    reference on the same number of threads beside it (interleaved runs)."""
+    cfg = S.replace(S.CONFIGS["C2"], hash_data=0)
+    alg = ref_algorithmic_bytes(cfg, threads) if use_cpu else None
+    gpu, ref = [], []
+    ref_digests = None
+    for _ in range(runs):
+        res, sec, wall = S.run_capi(library, cfg, threads=threads)
+        if any(r.status for r in res):
+            raise RuntimeError("drop-in C2 leg: a stream failed")
+        gpu.append((sec, wall, S.digests(res)))
+        if use_cpu and os.path.exists(S.REF_LIB):
+            rres, rsec, rwall = S.run_capi(S.REF_LIB, cfg, threads=threads)
+            ref.append((rsec, rwall))
+            ref_digests = S.digests(rres)
+    if ref_digests is not None and any(g[2] != ref_digests for g in gpu):
+        raise RuntimeError("drop-in C2 leg: digests differ from the reference's")
+    walls = sorted(g[1] for g in gpu)
+    out = {"workload": "C2 through siamese.h from %d threads (%d streams each)" % (threads, cfg.streams // threads),
+           "runs": runs, "threads": threads,
+           "wall_ms_all": [round(g[1] * 1e3, 3) for g in gpu],
+           "wall_ms": round(walls[len(walls) // 2] * 1e3, 3),
+           "digests_match_reference": ref_digests is not None,
+           "cpu_baseline": None}
+    if alg:
+        out["value"] = round(alg / walls[len(walls) // 2] / 1e9, 3)
+        out["unit"] = "GB/s (reference algorithmic bytes / wall time)"
+    if ref:
+        rw = sorted(r[1] for r in ref)
+        out["cpu_baseline"] = {"wall_ms_all": [round(r[1] * 1e3, 3) for r in ref],
+                               "wall_ms": round(rw[len(rw) // 2] * 1e3, 3), "cores": threads,
+                               "kind": "reference",
+                               "value": round(alg / rw[len(rw) // 2] / 1e9, 3) if alg else None,
+                               "ratio_median": round(rw[len(rw) // 2] / walls[len(walls) // 2], 2)}
+    return out
+
+
 def legs(library, device, threads, use_cpu):
     cpu_threads = min(16, host_info()["usable_cpus"] or 1)
     specs = [
@@ -355,6 +396,7 @@ def legs(library, device, threads, use_cpu):
         out[name] = run_leg(name, library, cfg, device, threads, runs,
                             cpu_cfg if use_cpu else None, cpu_thr, sample, defer)
     out["dropin_C1"] = dropin_leg(library, use_cpu)
+    out["dropin_C2_threads"] = dropin_threads_leg(library, use_cpu, threads=min(16, cpu_threads))
     return out
 
 

@@ -1,11 +1,16 @@
 // api.cpp -- the drop-in siamese.h entry points (reference siamese.cpp:35-302).
 //
 // Argument validation and result codes follow the reference entry points
-// one-for-one.  Each call takes the process-wide engine lock; calls that must
-// hand host memory back to the caller (siamese_encode, siamese_decode, and
-// siamese_decoder_get on a freshly recovered packet) flush the queued device
-// work and wait for it, copying the bytes into host buffers whose lifetime
-// matches the reference contract (siamese.h:335-336, :410-414).
+// one-for-one.  Instances are independent: as in the reference, each is used
+// by one thread at a time (siamese.h:57-58), and calls on different instances
+// run concurrently, holding the engine's instance lock shared.  Calls that
+// must hand host memory back to the caller (siamese_encode, siamese_decode,
+// and siamese_decoder_get on a freshly recovered packet) queue their device
+// work, drop the lock and flush: concurrent flushes commit as a group (the
+// first carries everything queued before it, Engine::flush_and_sync), and no
+// thread holds a lock across a device round trip.  The bytes land in host
+// buffers whose lifetime matches the reference contract (siamese.h:335-336,
+// :410-414).
 #define SIAMESE_BUILDING
 #include "../../include/siamese.h"
 
@@ -18,6 +23,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <new>
+#include <shared_mutex>
 
 using namespace sgpu;
 
@@ -40,6 +46,12 @@ inline ApiEncoder* E(SiameseEncoder e) { return reinterpret_cast<ApiEncoder*>(e)
 inline ApiDecoder* D(SiameseDecoder d) { return reinterpret_cast<ApiDecoder*>(d); }
 
 using Lock = std::lock_guard<std::mutex>;
+// an instance call (shared: other instances' calls run beside it)
+struct Shared
+{
+    std::shared_lock<std::shared_mutex> l;
+    Shared() : l(Engine::global()->instance_lock()) {}
+};
 
 } // namespace
 
@@ -71,7 +83,7 @@ SIAMESE_EXPORT SiameseEncoder siamese_encoder_create()
 {
     if (!g_initialized)
         return nullptr;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return reinterpret_cast<SiameseEncoder>(new (std::nothrow) ApiEncoder);
 }
 
@@ -79,7 +91,7 @@ SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder)
 {
     if (!encoder)
         return;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     delete E(encoder);
 }
 
@@ -87,7 +99,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_is_ready(SiameseEncoder encoder)
 {
     if (!encoder)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     // keep two slots of slack for the application (siamese.cpp:86-91)
     if (E(encoder)->core.remaining_slots() <= 2)
         return Siamese_MaxPacketsReached;
@@ -99,7 +111,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder, Siamese
     if (!encoder || !packet || !packet->Data || packet->DataBytes <= 0 ||
         packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return E(encoder)->core.add(*packet);
 }
 
@@ -107,7 +119,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder, Siamese
 {
     if (!encoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return E(encoder)->core.get(*packet);
 }
 
@@ -115,7 +127,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_remove_before(SiameseEncoder encode
 {
     if (!encoder || packetNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     E(encoder)->core.remove_before(packetNum);
     return Siamese_Success;
 }
@@ -125,7 +137,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder, const v
 {
     if (!encoder || !buffer || bytes < 1 || !nextExpectedPacketNum)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return E(encoder)->core.acknowledge((const uint8_t*)buffer, bytes, *nextExpectedPacketNum);
 }
 
@@ -134,7 +146,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder,
 {
     if (!encoder || !original)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return E(encoder)->core.retransmit(*original);
 }
 
@@ -143,18 +155,20 @@ SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder, SiameseRecov
     if (!encoder || !recovery)
         return Siamese_InvalidInput;
     Engine* eng = Engine::global();
-    Lock lock(eng->mutex());
     ApiEncoder* enc = E(encoder);
     EncodeOut o;
-    const SiameseResult r = enc->core.encode(o);
-    if (r != Siamese_Success) {
-        if (r == Siamese_NeedMoreData)
-            recovery->DataBytes = 0;
-        return r;
+    {
+        Shared lock;
+        const SiameseResult r = enc->core.encode(o);
+        if (r != Siamese_Success) {
+            if (r == Siamese_NeedMoreData)
+                recovery->DataBytes = 0;
+            return r;
+        }
+        enc->out.resize(o.bytes);
+        eng->download(enc->out.data(), o.buf.addr(), o.bytes);
     }
-    enc->out.resize(o.bytes);
-    eng->download(enc->out.data(), o.buf.addr(), o.bytes);
-    if (!eng->flush_and_sync())
+    if (!eng->flush_and_sync(&eng->instance_lock()))
         return Siamese_Disabled;
     recovery->Data = enc->out.data();
     recovery->DataBytes = o.bytes;
@@ -166,7 +180,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder, uint6
 {
     if (!encoder || !statsOut || statsCount <= 0)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return E(encoder)->core.stats(statsOut, statsCount);
 }
 
@@ -176,7 +190,7 @@ SIAMESE_EXPORT SiameseDecoder siamese_decoder_create()
 {
     if (!g_initialized)
         return nullptr;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return reinterpret_cast<SiameseDecoder>(new (std::nothrow) ApiDecoder);
 }
 
@@ -184,7 +198,7 @@ SIAMESE_EXPORT void siamese_decoder_free(SiameseDecoder decoder)
 {
     if (!decoder)
         return;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     delete D(decoder);
 }
 
@@ -194,7 +208,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_original(SiameseDecoder decoder
     if (!decoder || !packet || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES ||
         packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return D(decoder)->core.add_original(*packet);
 }
 
@@ -204,7 +218,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_recovery(SiameseDecoder decoder
     if (!decoder || !packet || !packet->Data || packet->DataBytes <= 0 ||
         packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return D(decoder)->core.add_recovery(*packet);
 }
 
@@ -212,15 +226,25 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder, Siamese
 {
     if (!decoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
-    return D(decoder)->core.get(*packet);
+    Engine* eng = Engine::global();
+    DecoderCore& core = D(decoder)->core;
+    {
+        Shared lock;
+        if (!core.pending(packet->PacketNum))
+            return core.get(*packet);
+    }
+    // a freshly recovered packet whose exact length is still on the device
+    if (!eng->flush_and_sync(&eng->instance_lock()))
+        return Siamese_Disabled;
+    Shared lock;
+    return core.get(*packet);
 }
 
 SIAMESE_EXPORT SiameseResult siamese_decoder_is_ready(SiameseDecoder decoder)
 {
     if (!decoder)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return D(decoder)->core.is_ready();
 }
 
@@ -230,16 +254,20 @@ SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder, SiameseOrigi
     if (!decoder || (!packetsPtrOut != !countOut))
         return Siamese_InvalidInput;
     Engine* eng = Engine::global();
-    Lock lock(eng->mutex());
     DecoderCore& core = D(decoder)->core;
-    const SiameseResult r = core.decode(packetsPtrOut, countOut);
-    if (core.has_pending()) {
+    SiameseResult r;
+    {
+        Shared lock;
+        r = core.decode(packetsPtrOut, countOut);
+        if (!core.has_pending())
+            return r;
         core.download_recovered();
-        if (!eng->flush_and_sync())
-            return Siamese_Disabled;
-        if (core.disabled())   // (applies the completed solve first)
-            return Siamese_Disabled;
     }
+    if (!eng->flush_and_sync(&eng->instance_lock()))
+        return Siamese_Disabled;
+    Shared lock;
+    if (core.disabled())   // (applies the completed solve first)
+        return Siamese_Disabled;
     return r;
 }
 
@@ -248,7 +276,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder, void* b
 {
     if (!decoder || !buffer || !usedBytes || byteLimit < SIAMESE_ACK_MIN_BYTES)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return D(decoder)->core.acknowledgement((uint8_t*)buffer, byteLimit, *usedBytes);
 }
 
@@ -257,7 +285,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_stats(SiameseDecoder decoder, uint6
 {
     if (!decoder || !statsOut || statsCount <= 0)
         return Siamese_InvalidInput;
-    Lock lock(Engine::global()->mutex());
+    Shared lock;
     return D(decoder)->core.stats(statsOut, statsCount);
 }
 

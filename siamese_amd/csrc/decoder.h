@@ -162,6 +162,14 @@ public:
         const unsigned e = column_to_element(packetNum);
         return !dead() && e < count_ && slot(e).bytes > 0;
     }
+    /// Present, but its exact length still being solved on the device (a
+    /// get() would flush and wait).
+    bool pending(unsigned packetNum)
+    {
+        settle();
+        const unsigned e = column_to_element(packetNum);
+        return !dead() && e < count_ && slot(e).bytes > 0 && slot(e).pending;
+    }
     /// True while a queued solve has not been resolved by a completed flush.
     bool has_pending() const { return pendingSolves_ > 0; }
     /// Drop-in mode: queue D2H copies of the packets just recovered.

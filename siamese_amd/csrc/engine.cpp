@@ -1416,6 +1416,7 @@ uint64_t Engine::enqueue()
 {
     if (failed())
         return 0;
+    std::lock_guard<std::mutex> sub(submitMu_);
     const uint64_t tq0 = now_ns();
     Batch* b = take_batch();
     if (!b)
@@ -1469,13 +1470,25 @@ bool Engine::wait(uint64_t ticket)
     return !failed();
 }
 
-bool Engine::flush_and_sync()
+bool Engine::flush_and_sync(std::shared_mutex* detach)
 {
     if (failed())
         return false;
-    Batch* b = take_batch();
-    if (!b)
-        return wait(nextTicket_) && nextTicket_ != 0;
+    std::unique_lock<std::mutex> sub(submitMu_);
+    Batch* b;
+    uint64_t last;
+    {
+        std::unique_lock<std::shared_mutex> w;
+        if (detach)
+            w = std::unique_lock<std::shared_mutex>(*detach);
+        b = take_batch();
+        last = nextTicket_;
+    }
+    if (!b) {
+        // (an earlier submission took this caller's work: wait for it)
+        sub.unlock();
+        return wait(last) && last != 0;
+    }
     const uint64_t ticket = b->ticket;
     // SIAMESE_AMD_INLINE_SYNC=0 always hands the submission to the threads
     static const bool kInline = [] {
@@ -1506,6 +1519,7 @@ bool Engine::flush_and_sync()
             toLaunch_.push_back(b);
             queuedSeen_.fetch_add(1, std::memory_order_release);
         }
+        sub.unlock();
         launchCv_.notify_one();
         return wait(ticket) && !failed();
     }
@@ -1513,6 +1527,7 @@ bool Engine::flush_and_sync()
     assemble_batch(*b, pool());   // (the set was claimed above)
     if (!failed())
         launch_batch(*b);
+    sub.unlock();   // (the next submission may be laid out while this one runs)
     if (complete_batch(*b))
         reclaim_batch(*b);
     {
@@ -1532,7 +1547,11 @@ bool Engine::flush_and_sync()
 
 bool Engine::flush()
 {
-    const uint64_t prev = nextTicket_;
+    uint64_t prev;
+    {
+        std::lock_guard<std::mutex> sub(submitMu_);
+        prev = nextTicket_;
+    }
     enqueue();
     // complete what was in flight before this submission (one flush in flight)
     return wait(prev) && !failed();

@@ -27,6 +27,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -370,16 +371,20 @@ public:
         return doneTicket_ >= ticket;
     }
     /// Ticket of the latest submission.
-    uint64_t last_ticket() const { return nextTicket_; }
+    uint64_t last_ticket() const { return nextTicket_.load(std::memory_order_acquire); }
     /// Submit, then complete the previous submission (one flush in flight).
     bool flush();
     /// Complete every submission.
-    bool sync() { return wait(nextTicket_); }
+    bool sync() { return wait(nextTicket_.load(std::memory_order_acquire)); }
     /// Submit everything queued and wait for it.  With nothing in flight
     /// the caller's thread runs the submission itself (assembly, launches,
     /// fence poll, completion): no hand-off to the launcher and completer
-    /// threads, the drop-in siamese.h path's per-call latency.
-    bool flush_and_sync();
+    /// threads, the drop-in siamese.h path's per-call latency.  detach: a
+    /// lock that instance calls hold shared (the drop-in API's), held
+    /// exclusively while the queued work is detached; concurrent callers
+    /// commit as a group (the first one's submission carries everything
+    /// queued before it, the others find their work taken and only wait).
+    bool flush_and_sync(std::shared_mutex* detach = nullptr);
     /// A device operation failed; the engine accepts no further work.
     bool failed() const { return failed_.load(std::memory_order_relaxed); }
     bool pending() const;
@@ -410,9 +415,12 @@ public:
     /// guarantees that no unfinished submission touches dst.
     bool stage_in(void* dst, const void* src, size_t bytes);
 
-    /// Serialises the drop-in siamese.h entry points and the exclusive
-    /// siamese_gpu.h calls.
+    /// Serialises the exclusive siamese_gpu.h calls.
     std::mutex& mutex() { return mu_; }
+    /// Shared by the drop-in siamese.h instance calls (each instance used by
+    /// one thread at a time, siamese.h:57-58), exclusive only while a flush
+    /// detaches the queued work (flush_and_sync(&instance_lock())).
+    std::shared_mutex& instance_lock() { return instMu_; }
 
     /// Counts toward the calling thread's statistics.
     void account(uint64_t opBytes, uint64_t outBytes = 0, bool inSolve = false);
@@ -450,6 +458,11 @@ private:
     bool ready_ = false;
     std::atomic<bool> failed_{false};
     std::mutex mu_;
+    std::shared_mutex instMu_;
+    // one submission detached and assembled at a time (take_batch hands out
+    // tickets, and toLaunch_ keeps ticket order); held by enqueue() and
+    // flush_and_sync() until the batch is queued or launched
+    std::mutex submitMu_;
 
     // ---- arena: 64 MiB hipMalloc chunks are cut into 4 MiB regions under
     // arenaMu_; a shard bump-allocates buffers from its own region.  Free
@@ -481,7 +494,7 @@ private:
     // ---- flush pipeline state
     std::mutex statsMu_;
     EngineStats flushStats_;
-    uint64_t nextTicket_ = 0;                       // last ticket handed out (enqueue only)
+    std::atomic<uint64_t> nextTicket_{0};           // last ticket handed out (take_batch, under submitMu_)
     std::mutex qMu_;
     std::condition_variable launchCv_, completeCv_, doneCv_, setCv_;
     std::deque<Batch*> toLaunch_, toComplete_;

@@ -43,6 +43,16 @@ def test_hostsim_dropin_matches_golden(name):
     _check(name, res)
 
 
+@pytest.mark.parametrize("name", ["C2x64", "smoke_C4x8", "C1var"])
+def test_hostsim_dropin_threads_match_golden(name):
+    """siamese.h from several threads at once, each driving its own streams:
+    instance calls run concurrently under the shared instance lock and their
+    flushes commit as groups; every stream's digest is the reference's."""
+    cfg = golden.config(name)
+    res, _, _ = S.run_capi(S.SIM_LIB, cfg, threads=min(8, cfg.streams))
+    _check(name, res)
+
+
 @pytest.mark.parametrize("name", SMALL)
 def test_hostsim_batch_matches_golden(name):
     cfg = golden.config(name)
