@@ -2124,6 +2124,7 @@ __device__ __forceinline__ void prefix_load(uint32_t (&p4)[4], uint32_t m, uint3
 #define SGPU_SOLVE_WAVES 8
 #endif
 constexpr unsigned kSolveWaves = SGPU_SOLVE_WAVES;
+constexpr unsigned kMfmaMaxRows = 120;       // k_solve_mfma takes solves of up to this many rows
 constexpr unsigned kSolveLdsMaxRows = 255;   // kMaximumLossRecoveryCount (SiameseCommon.h:80)
 constexpr unsigned kSolvePrefixSplit = 16;   // solves per launch from which the prefix pass is its own launch
 
@@ -2479,7 +2480,7 @@ __host__ __device__ constexpr uint32_t solve_launch_lds_bytes(uint32_t maxRows, 
 __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const SolveDesc* __restrict__ solves, const SolveRow* __restrict__ rows,
     const uint8_t* __restrict__ coef, uint32_t* __restrict__ results,
-    const SolveItem* __restrict__ items, unsigned long long* __restrict__ acct, uint32_t prefixDone)
+    const SolveItem* __restrict__ items, unsigned long long* __restrict__ acct, uint32_t flags)
 {
     extern __shared__ uint4 X[];
     const SolveItem it = items[blockIdx.x];
@@ -2489,7 +2490,11 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const uint8_t* C = coef + sd.coefOffset;
     if (m > kSolveLdsMaxRows)
         return;   // (the host never queues m > 255: kMaximumLossRecoveryCount)
-    // prefixDone: k_solve_prefix already solved the length prefixes
+    // flags bit 0: k_solve_prefix already solved the length prefixes; bit 1:
+    // k_solve_mfma ran before this launch and took every solve it could
+    const bool prefixDone = (flags & 1u) != 0;
+    if ((flags & 2u) && m <= kMfmaMaxRows && results[sd.result] == m)
+        return;
     const uint32_t* resIn = prefixDone ? results + sd.result : nullptr;
     uint32_t* out = (!prefixDone && it.tileBase == 0) ? results + sd.result : nullptr;
     if (m <= kSolveWideMaxRows)
@@ -2562,6 +2567,231 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
         atomicMax(&g_phaseClk[47], (e - pclk) << 8 | (m & 0xffu));
     }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// Bulk solve on the matrix cores (k_solve_mfma)
+//
+// The solve's result rows are X = T R, with T = U^-1 L^-1 the m x m inverse
+// of the eliminated coefficient matrix (MultiplyLowerTriangle applies L^-1,
+// BackSubstitution U^-1; reference SiameseDecoder.cpp:1065-1238).  Over
+// GF(2) a GF(256) product c*x is the 8x8 bit matrix of c applied to x's bits,
+// so X's bits are one binary matrix product,
+//     bit b of X[i][n] = parity( sum_{j,k} bit b of (T[i][j] * 2^k) * bit k of R[j][n] ),
+// an integer dot product of 0/1 bytes whose low bit is the GF(2) sum: the
+// int8 MFMA v_mfma_i32_32x32x32_i8 computes 32 output bits x 32 columns over
+// 32 input bits (four input rows) per instruction, exactly.
+//
+// One workgroup per (solve, column half):
+//   1. T in LDS: the reference's two sweeps applied to the identity (rows of
+//      m bytes, one half-wave per row update);
+//   2. per 64-column chunk: the rows' bytes expanded to 0/1 bytes in LDS
+//      (the B operand, laid out so a lane's 16-byte fragment is one
+//      ds_read_b128), then each wave takes 32 output bits (four rows) and
+//      runs the K loop, its A fragments built from T and the multiply-by-y
+//      bit matrices (c_aff), and packs the parities back to bytes.
+// It runs only when k_solve_prefix found every recovered length valid
+// (results[0] == m): the exact sweeps and the prefixes then agree byte for
+// byte, since bytes past a row's length are zero in the true originals (the
+// clips of the sequential sweeps change nothing).  A solve with a corrupt
+// prefix, or m > kMfmaMaxRows, is left to k_solve_main, which reproduces the
+// reference's partial back-substitution exactly.
+constexpr unsigned kMfmaWaves = 8;
+constexpr unsigned kMfmaThreads = 64 * kMfmaWaves;
+constexpr unsigned kMfmaYStride = 128;                 // bytes per row of T in LDS
+constexpr unsigned kMfmaTiles = 2;                     // 32-column MFMA tiles per chunk
+constexpr unsigned kMfmaChunk = 32 * kMfmaTiles;       // columns per chunk
+constexpr unsigned kMfmaSplit = 2;                     // workgroups per solve (column ranges)
+
+__constant__ uint8_t c_aff[256][8];   // [y][7 - b]: bit k = bit b of y * 2^k (GF2P8AFFINEQB rows)
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+__host__ __device__ constexpr uint32_t mfma_rows(uint32_t m) { return (m + 3u) & ~3u; }
+__host__ __device__ constexpr uint32_t solve_mfma_lds_bytes(uint32_t m)
+{
+    return ((m * m + 15u) & ~15u) + mfma_rows(m) * kMfmaYStride + 256u * 16u + 256u * 4u + 256u * 8u +
+           ((3u * m * 4u + 15u) & ~15u) + mfma_rows(m) * 8u * kMfmaChunk + mfma_rows(m) * kMfmaChunk;
+}
+
+// the four low bits of v as four 0/1 bytes (byte q = bit q)
+__device__ __forceinline__ uint32_t bits4(uint32_t v) { return ((v & 15u) * 0x00204081u) & 0x01010101u; }
+
+__global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __restrict__ solves,
+                                                           const SolveRow* __restrict__ rows,
+                                                           const uint8_t* __restrict__ coef,
+                                                           const uint32_t* __restrict__ results)
+{
+    extern __shared__ uint4 Ls[];
+    const uint32_t part = blockIdx.x % kMfmaSplit;
+    const SolveDesc sd = solves[blockIdx.x / kMfmaSplit];
+    const uint32_t m = sd.m;
+    if (m == 0 || m > kMfmaMaxRows || results[sd.result] != m)
+        return;   // (uniform: k_solve_main solves it)
+    const SolveRow* R = rows + sd.rowBegin;
+    const uint8_t* C = coef + sd.coefOffset;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t mp = mfma_rows(m);
+
+    uint8_t* base = reinterpret_cast<uint8_t*>(Ls);
+    uint8_t* Ct = base;                                          // Ct[i*m + j] = C[j][i]
+    uint8_t* Y = Ct + ((m * m + 15u) & ~15u);                    // T, rows of kMfmaYStride bytes
+    uint4* permL = reinterpret_cast<uint4*>(Y + mp * kMfmaYStride);
+    uint32_t* permC = reinterpret_cast<uint32_t*>(permL + 256);
+    uint8_t* aff = reinterpret_cast<uint8_t*>(permC + 256);
+    uint32_t* initB = reinterpret_cast<uint32_t*>(aff + 2048);
+    uint32_t* finB = initB + m;
+    uint32_t* bbB = finB + m;                                    // recovered header + length
+    uint8_t* bits = reinterpret_cast<uint8_t*>(initB) + ((3u * m * 4u + 15u) & ~15u);
+    uint8_t* outT = bits + mp * 8u * kMfmaChunk;
+
+    stage_transposed<kMfmaThreads, 2>(Ct, C, m, tid);
+    if (tid < 256) {
+        const uint32_t* t = c_perm[tid];
+        permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
+        permC[tid] = t[4];
+    }
+    for (uint32_t k = tid; k < 512; k += kMfmaThreads)
+        reinterpret_cast<uint32_t*>(aff)[k] = reinterpret_cast<const uint32_t*>(c_aff)[k];
+    for (uint32_t j = tid; j < m; j += kMfmaThreads) {
+        initB[j] = R[j].initBytes;
+        finB[j] = R[j].finalBytes;
+        const uint32_t w = results[sd.result + 1 + j];
+        bbB[j] = (w >> 29) + (w & kSolveLengthMask);
+    }
+    // T starts as the identity (rows past m stay zero)
+    uint32_t* Yw = reinterpret_cast<uint32_t*>(Y);
+    for (uint32_t k = tid; k < mp * (kMfmaYStride / 4); k += kMfmaThreads) {
+        const uint32_t i = k / (kMfmaYStride / 4), c4 = (k % (kMfmaYStride / 4)) * 4;
+        Yw[k] = (i < m && i >= c4 && i < c4 + 4) ? 1u << (8 * (i - c4)) : 0u;
+    }
+    __syncthreads();
+
+    // 1. T: MultiplyLowerTriangle, then BackSubstitution, on the identity's
+    // rows (a row of T is m <= 120 bytes: one half-wave, four bytes a lane)
+    constexpr uint32_t kHalves = kMfmaThreads / 32;
+    const uint32_t hw = tid >> 5, l32 = tid & 31;
+    for (uint32_t i = 0; i + 1 < m; ++i) {
+        const uint32_t src = Yw[i * 32 + l32];
+        for (uint32_t j = i + 1 + hw; j < m; j += kHalves) {
+            const uint32_t y = Ct[i * m + j];   // C[j][i]
+            if (y)
+                Yw[j * 32 + l32] ^= gf_mul_tab(src, gf_tab_l(permL, permC, y));
+        }
+        __syncthreads();
+    }
+    for (int i = (int)m - 1; i > 0; --i) {
+        const uint32_t xi = gf_mul_tab(Yw[i * 32 + l32], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]]));
+        for (uint32_t j = hw; j < (uint32_t)i; j += kHalves) {
+            const uint32_t y = Ct[(uint32_t)i * m + j];   // C[j][i]
+            if (y)
+                Yw[j * 32 + l32] ^= gf_mul_tab(xi, gf_tab_l(permL, permC, y));
+        }
+        __syncthreads();
+    }
+    for (uint32_t k = tid; k < m * 32u; k += kMfmaThreads) {
+        const uint32_t i = k >> 5;
+        Yw[k] = gf_mul_tab(Yw[k], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]]));
+    }
+    __syncthreads();
+
+    // 2. X = T R, 64 columns at a time
+    const uint32_t S = mp / 4;   // K steps (four input rows = 32 input bits each)
+    uint32_t maxB = 0;
+    for (uint32_t j = 0; j < m; ++j)
+        maxB = finB[j] > maxB ? finB[j] : maxB;
+    for (uint32_t ch = part; ch * kMfmaChunk < maxB; ch += kMfmaSplit) {
+        const uint32_t c0 = ch * kMfmaChunk;
+        // the B operand: byte (j, col) as eight 0/1 bytes at
+        // bits[((t * S + j / 4) * 32 + col % 32) * 32 + (j % 4) * 8], t = col / 32
+        for (uint32_t it = tid; it < mp * (kMfmaChunk / 4); it += kMfmaThreads) {
+            const uint32_t j = it / (kMfmaChunk / 4), q = it % (kMfmaChunk / 4);
+            uint32_t x = 0;
+            if (j < m) {
+                const uint32_t p = c0 + 4 * q, ib = initB[j];
+                if (p < ib) {
+                    x = ld4(R[j].buf + p);
+                    if (p + 4 > ib)
+                        x &= byte_mask((int)(ib - p));
+                }
+            }
+#pragma unroll
+            for (uint32_t cc = 0; cc < 4; ++cc) {
+                const uint32_t col = 4 * q + cc, v = (x >> (8 * cc)) & 0xffu;
+                *reinterpret_cast<uint2*>(bits + (((col / 32) * S + j / 4) * 32 + col % 32) * 32 + (j % 4) * 8) =
+                    make_uint2(bits4(v), bits4(v >> 4));
+            }
+        }
+        __syncthreads();
+        const uint32_t r = lane & 31, h = lane >> 5;
+        for (uint32_t mt = wave; mt < mp / 4; mt += kMfmaWaves) {
+            // rows 4 mt .. 4 mt + 3 of X: lane's A row is output bit b of row i
+            const uint32_t i = 4 * mt + (r >> 3), b = 7 - (r & 7);
+            const uint8_t* ty = Y + i * kMfmaYStride + 2 * h;
+            i32x16 acc[kMfmaTiles];
+#pragma unroll
+            for (uint32_t t = 0; t < kMfmaTiles; ++t)
+                acc[t] = i32x16{};
+            for (uint32_t s = 0; s < S; ++s) {
+                // A[r][16 h + jj]: bit b of T[i][4 s + 2 h + jj / 8] * 2^(jj % 8)
+                const uint32_t a1 = aff[ty[4 * s] * 8u + b], a2 = aff[ty[4 * s + 1] * 8u + b];
+                const i32x4 A = {(int)bits4(a1), (int)bits4(a1 >> 4), (int)bits4(a2), (int)bits4(a2 >> 4)};
+#pragma unroll
+                for (uint32_t t = 0; t < kMfmaTiles; ++t) {
+                    const i32x4 B = *reinterpret_cast<const i32x4*>(bits + ((t * S + s) * 32 + r) * 32 + h * 16);
+                    acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc[t], 0, 0, 0);
+                }
+            }
+            // D[row][col]: row = (reg & 3) + 8 (reg >> 2) + 4 h, col = r; row
+            // 8 g + 4 h + q is bit 4 h + q of X row 4 mt + g
+#pragma unroll
+            for (uint32_t t = 0; t < kMfmaTiles; ++t)
+#pragma unroll
+                for (uint32_t g = 0; g < 4; ++g) {
+                    const uint32_t nib = (acc[t][4 * g] & 1) | (acc[t][4 * g + 1] & 1) << 1 |
+                                         (acc[t][4 * g + 2] & 1) << 2 | (acc[t][4 * g + 3] & 1) << 3;
+                    const uint32_t v = nib << (4 * h);
+                    const uint32_t byte = v | (uint32_t)__shfl_xor((int)v, 32);
+                    if (h == 0)
+                        outT[(4 * mt + g) * kMfmaChunk + t * 32 + r] = (uint8_t)byte;
+                }
+        }
+        __syncthreads();
+        // x masked past the recovered length, stored below the row's final
+        // bytes (the stores of the exact back-substitution)
+        for (uint32_t it = tid; it < m * (kMfmaChunk / 16); it += kMfmaThreads) {
+            const uint32_t i = it / (kMfmaChunk / 16), u = it % (kMfmaChunk / 16);
+            const uint32_t p = c0 + 16 * u;
+            if (p < finB[i]) {
+                uint4 v = *reinterpret_cast<const uint4*>(outT + i * kMfmaChunk + 16 * u);
+                v = mask16(v, (int)bbB[i] - (int)p);
+                st16(R[i].buf + p, v);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Layout check of the int8 MFMA (tests): D = A B for 32 x 32 x 32 with
+// asymmetric integer data, fragments as k_solve_mfma reads them.
+__global__ void k_mfma_i8_check(int* __restrict__ out)
+{
+    const uint32_t l = threadIdx.x, r = l & 31, h = l >> 5;
+    i32x4 A, B;
+    int8_t* a = reinterpret_cast<int8_t*>(&A);
+    int8_t* b = reinterpret_cast<int8_t*>(&B);
+    for (uint32_t jj = 0; jj < 16; ++jj) {
+        const uint32_t k = 16 * h + jj;
+        a[jj] = (int8_t)((int)((r * 7 + k * 3) % 5) - 2);
+        b[jj] = (int8_t)((int)((k * 11 + r * 5) % 7) - 3);
+    }
+    i32x16 acc = {};
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc, 0, 0, 0);
+    for (uint32_t reg = 0; reg < 16; ++reg) {
+        const uint32_t row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        out[row * 32 + r] = acc[reg];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2760,6 +2990,12 @@ bool be_init(int device, const char** err)
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_perm), perm, sizeof(perm)), "hipMemcpyToSymbol(perm)");
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_inv), g_gf.inv, 256), "hipMemcpyToSymbol(inv)");
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_sqr), g_gf.sqr, 256), "hipMemcpyToSymbol(sqr)");
+    // the multiply-by-y bit matrices, row b of y at [y][7 - b] (gf.h affine)
+    static uint8_t aff[256][8];
+    for (unsigned y = 0; y < 256; ++y)
+        for (unsigned k = 0; k < 8; ++k)
+            aff[y][k] = (uint8_t)(g_gf.affine[y] >> (8 * k));
+    check(hipMemcpyToSymbol(HIP_SYMBOL(c_aff), aff, sizeof(aff)), "hipMemcpyToSymbol(aff)");
     // PCG jump-ahead: state after j draws = A^j s + inc * (A^0 + ... + A^(j-1))
     uint64_t pa[65], pg[65];
     pa[0] = 1;
@@ -2803,6 +3039,11 @@ bool be_init(int device, const char** err)
         *err = "the device refused the triangular solve's LDS (gfx950 grants 160 KiB per workgroup)";
         return false;
     }
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_mfma), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)solve_mfma_lds_bytes(kMfmaMaxRows)) != hipSuccess) {
+        *err = "the device refused the matrix-core solve's LDS";
+        return false;
+    }
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_prefix),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)solve_prefix_lds_bytes(kSolveLdsMaxRows)) != hipSuccess) {
@@ -2818,6 +3059,33 @@ bool be_init(int device, const char** err)
 }
 
 const char* be_name() { return "hip-gfx950"; }
+
+// Test hook: the int8 MFMA fragment layout k_solve_mfma relies on, against
+// the host's product of the same 32 x 32 x 32 integer matrices.  Returns the
+// number of differing outputs (0: the layout holds), -1 on a device error.
+extern "C" __attribute__((visibility("default"))) int sgpu_selftest_mfma_i8(void)
+{
+    bind_device();
+    int* d = nullptr;
+    if (hipMalloc(&d, 32 * 32 * sizeof(int)) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(k_mfma_i8_check, dim3(1), dim3(64), 0, g_stream, d);
+    int h[32 * 32];
+    const bool ok = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, g_stream) == hipSuccess &&
+                    hipStreamSynchronize(g_stream) == hipSuccess;
+    (void)hipFree(d);
+    if (!ok)
+        return -1;
+    int bad = 0;
+    for (int i = 0; i < 32; ++i)
+        for (int j = 0; j < 32; ++j) {
+            int want = 0;
+            for (int k = 0; k < 32; ++k)
+                want += ((i * 7 + k * 3) % 5 - 2) * ((k * 11 + j * 5) % 7 - 3);
+            bad += h[i * 32 + j] != want;
+        }
+    return bad;
+}
 
 #ifdef SGPU_PHASE_CLOCKS
 extern "C" __attribute__((visibility("default"))) void sgpu_debug_phase_clocks(unsigned long long* out32)
@@ -3012,9 +3280,20 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
         hipLaunchKernelGGL(k_solve_prefix, dim3(solveCount), dim3(64), (size_t)solve_prefix_lds_bytes(rowsCap),
                            g_stream, solves + solveBegin, rows, coef, results,
                            reinterpret_cast<unsigned long long*>(acct));
+    // the solves whose lengths all came out valid on the matrix cores
+    // (SGPU_MFMA_SOLVE=0: every solve by the sweeps, A/B aid)
+    static const bool kMfmaSolve = [] {
+        const char* v = std::getenv("SGPU_MFMA_SOLVE");
+        return !v || std::atoi(v) != 0;
+    }();
+    const bool mfma = separate && kMfmaSolve;
+    if (mfma)
+        hipLaunchKernelGGL(k_solve_mfma, dim3(solveCount * kMfmaSplit), dim3(kMfmaThreads),
+                           (size_t)solve_mfma_lds_bytes(rowsCap < kMfmaMaxRows ? rowsCap : kMfmaMaxRows), g_stream,
+                           solves + solveBegin, rows, coef, results);
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
                        (size_t)solve_launch_lds_bytes(rowsCap, !separate), g_stream, solves, rows, coef, results,
-                       items, reinterpret_cast<unsigned long long*>(acct), separate ? 1u : 0u);
+                       items, reinterpret_cast<unsigned long long*>(acct), (separate ? 1u : 0u) | (mfma ? 2u : 0u));
 }
 
 void* be_stage_h2d(void* dst, const void* src, size_t bytes)
