@@ -101,3 +101,72 @@ def test_ack_roundtrip_removes_window(ref, sim):
         outs.append(o)
     assert outs[0] == outs[1]
     assert outs[0][0][0] == Success
+
+
+def _batch_lib():
+    import ctypes
+    L = ctypes.CDLL(S.SIM_LIB)
+    assert L.sgpu_init(-1) == 0
+    L.sgpu_encoder_create.restype = ctypes.c_void_p
+    L.sgpu_decoder_create.restype = ctypes.c_void_p
+    L.sgpu_encoder_free.argtypes = [ctypes.c_void_p]
+    L.sgpu_decoder_free.argtypes = [ctypes.c_void_p]
+    L.sgpu_device_alloc.restype = ctypes.c_void_p
+    L.sgpu_device_alloc.argtypes = [ctypes.c_size_t]
+    L.sgpu_device_free.argtypes = [ctypes.c_void_p]
+    L.sgpu_h2d.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    U = ctypes.c_uint
+    L.sgpu_encoder_add_range.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(U), U, U,
+                                         ctypes.POINTER(U), ctypes.POINTER(U)]
+    L.sgpu_encoder_add.argtypes = [ctypes.c_void_p, ctypes.c_void_p, U, ctypes.POINTER(U)]
+    L.sgpu_decoder_add_original_range.argtypes = [ctypes.c_void_p, U, ctypes.c_void_p, ctypes.c_size_t,
+                                                  ctypes.POINTER(U), U, U, ctypes.POINTER(ctypes.c_int),
+                                                  ctypes.POINTER(U)]
+    L.sgpu_decoder_has.argtypes = [ctypes.c_void_p, U]
+    return L
+
+
+def test_range_calls_stop_like_the_single_calls():
+    """sgpu_encoder_add_range stops where a loop of sgpu_encoder_add would
+    (an invalid length mid-range: the ones before it are added, packet numbers
+    consecutive); sgpu_decoder_add_original_range goes on past a duplicate and
+    reports each call's result, as the single calls would."""
+    import ctypes
+    L = _batch_lib()
+    U = ctypes.c_uint
+    stride = 64
+    dev = L.sgpu_device_alloc(stride * 16)
+    host = bytes(range(256)) * 4
+    assert L.sgpu_h2d(dev, host, stride * 16) == 0
+    enc = L.sgpu_encoder_create()
+    lens = (U * 6)(10, 20, 30, 0, 40, 50)          # the fourth is invalid
+    first, added = U(), U()
+    r = L.sgpu_encoder_add_range(enc, dev, stride, lens, 0, 6, ctypes.byref(first), ctypes.byref(added))
+    assert r == InvalidInput and added.value == 3 and first.value == 0
+    num = U()
+    assert L.sgpu_encoder_add(enc, dev, 10, ctypes.byref(num)) == Success and num.value == 3
+    dec = L.sgpu_decoder_create()
+    res = (ctypes.c_int * 8)()
+    calls = U()
+    assert L.sgpu_decoder_add_original_range(dec, 2, dev, stride, None, 12, 3, res, ctypes.byref(calls)) == Success
+    assert calls.value == 3 and list(res[:3]) == [Success] * 3
+    # packets 3 and 4 again (duplicates), then 5 and 6 new: every call made
+    assert L.sgpu_decoder_add_original_range(dec, 3, dev, stride, None, 12, 4, res, ctypes.byref(calls)) == Success
+    assert calls.value == 4 and list(res[:4]) == [DuplicateData, DuplicateData, Success, Success]
+    for n in (2, 3, 4, 5, 6):
+        assert L.sgpu_decoder_has(dec, n) == Success
+    assert L.sgpu_decoder_has(dec, 7) == NeedMoreData
+    L.sgpu_encoder_free(enc)
+    L.sgpu_decoder_free(dec)
+    L.sgpu_device_free(dev)
+
+
+def test_range_adds_use_few_ingest_descriptors():
+    """A stream's originals added by range calls become a handful of ingest
+    runs (one per slab of 64 slots), the decoder's received ones riding on
+    the encoder's runs as second destinations."""
+    cfg = S.replace(S.CONFIGS["C4"], streams=16, hash_data=0, add_ranges=1)
+    res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True)
+    assert rep.mismatches == 0 and all(r.status == 0 for r in res)
+    ingests = S.engine_dict(rep)["ingests"]
+    assert ingests <= 16 * 6, ingests   # (4 slabs of originals per stream, a few recovery staging runs)
