@@ -470,16 +470,29 @@ DevSum& DecoderCore::get_sum(unsigned lane, unsigned s, unsigned elementEnd)
     if (element >= elementEnd)
         return S.d;
 
-    unsigned newBytes = S.d.bytes;
-    unsigned got = 0;
+    // (the three sums of a lane usually walk the same elements: the walk's
+    // result is kept per lane for the next of them)
+    LaneScan& ls = laneScan_[lane];
     unsigned end = element;
-    for (; end < elementEnd; end += kLanes) {
-        const unsigned b = slot(end).bytes;
-        if (b > 0) {
-            newBytes = std::max(newBytes, b);
-            ++got;
+    if (!(ls.from == element && ls.to == elementEnd && ls.epoch == scanEpoch_)) {
+        unsigned most = 0, cnt = 0;
+        for (; end < elementEnd; end += kLanes) {
+            const unsigned b = slot(end).bytes;
+            if (b > 0) {
+                most = std::max(most, b);
+                ++cnt;
+            }
         }
+        ls.from = element;
+        ls.to = elementEnd;
+        ls.end = end;
+        ls.most = most;
+        ls.got = cnt;
+        ls.epoch = scanEpoch_;
     }
+    end = ls.end;
+    const unsigned got = ls.got;
+    const unsigned newBytes = std::max(S.d.bytes, ls.most);
     if (got > 0) {
         if (!grow_sum(S.d, newBytes))
             return S.d;
@@ -641,6 +654,7 @@ void DecoderCore::remove_elements()
                 return;
             }
         }
+        ++scanEpoch_;
         for (unsigned lane = 0; lane < kLanes; ++lane) {
             for (unsigned s = 0; s < kSums; ++s) {
                 get_sum(lane, s, removed);
@@ -1110,10 +1124,28 @@ const bool kDecodeClocks = std::getenv("SIAMESE_AMD_DECODE_CLOCKS") != nullptr;
 struct DecodeClocks
 {
     std::atomic<uint64_t> n{0}, rows{0}, cols{0}, fails{0}, fresh{0}, t[4];
+    // per-call samples for medians (a noisy host: averages swing with steal time)
+    std::mutex mu;
+    std::vector<uint32_t> samples[4];
+    void sample(const uint64_t* d)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (int k = 0; k < 4; ++k)
+            if (samples[k].size() < (1u << 16))
+                samples[k].push_back((uint32_t)d[k]);
+    }
     ~DecodeClocks()
     {
         if (!kDecodeClocks || !n)
             return;
+        double med[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 4; ++k)
+            if (!samples[k].empty()) {
+                std::nth_element(samples[k].begin(), samples[k].begin() + samples[k].size() / 2, samples[k].end());
+                med[k] = samples[k][samples[k].size() / 2];
+            }
+        std::fprintf(stderr, "decode_region medians (ticks): generate %.0f ge %.0f eliminate %.0f solve %.0f\n",
+                     med[0], med[1], med[2], med[3]);
         std::fprintf(stderr, "decode_region %llu solved, %llu failed, %llu fresh matrices, rows %.1f cols %.1f; "
                      "ticks/solved call: generate %.0f ge %.0f eliminate %.0f solve %.0f\n",
                      (unsigned long long)n.load(), (unsigned long long)fails.load(), (unsigned long long)fresh.load(),
@@ -1162,6 +1194,8 @@ SiameseResult DecoderCore::decode_region()
         g_decodeClocks.t[1] += c2 - c1;
         g_decodeClocks.t[2] += c3 - c2;
         g_decodeClocks.t[3] += c4 - c3;
+        const uint64_t d[4] = {c1 - c0, c2 - c1, c3 - c2, c4 - c3};
+        g_decodeClocks.sample(d);
     }
     region_reset();
     return res;
@@ -1416,6 +1450,19 @@ bool DecoderCore::gaussian_elimination()
         return pivoted_ge(geResume_);
     const unsigned columns = matCols_;
     const unsigned rows = matRows_;
+    {
+        // the whole loop in one vector routine where the host has GFNI
+        geEnd_.resize(columns);
+        for (unsigned p = 0; p < columns; ++p)
+            geEnd_[p] = rows_[p].columnCount;
+        bool done = false;
+        const unsigned stop = gf_ge_nopivot(mat_.data(), matStride_, rows, columns, 0, geEnd_.data(), &geBytes_, &done);
+        if (done) {
+            for (unsigned p = 0; p < stop; ++p)
+                rows_[p].used = true;
+            return stop < columns ? pivoted_ge(stop) : true;
+        }
+    }
     for (unsigned p = 0; p < columns; ++p) {
         uint8_t* ge = mrow(p);
         const uint8_t val = ge[p];
@@ -1473,6 +1520,7 @@ bool DecoderCore::pivoted_ge(unsigned pivot)
 
 bool DecoderCore::eliminate_original_data()
 {
+    ++scanEpoch_;   // (get_sum's lane walks are reused within this call only)
     const unsigned rows = region_.recoveryCount;
     // the current run of rows with one sum range (see below)
     bool haveRun = false;
@@ -1606,14 +1654,29 @@ SiameseResult DecoderCore::solve_and_substitute()
     }
     // Row growth of MultiplyLowerTriangle (GrowZeroPadded), simulated here
     uint64_t lowerOpBytes = 0;
-    for (unsigned i = 0; i + 1 < m; ++i) {
-        desc[i].lowerLen = len[i];
-        for (unsigned j = i + 1; j < m; ++j) {
-            if (mrow(pivots_[j])[i] == 0)
-                continue;
-            lowerOpBytes += len[i];
-            if (len[j] < len[i])
-                len[j] = len[i];
+    bool equal = true;
+    for (unsigned i = 1; i < m && equal; ++i)
+        equal = len[i] == len[0];
+    if (equal) {
+        // rows of one length (a block of equal packets) never grow: the
+        // lower step's source bytes are that length per non-zero multiplier
+        // below the diagonal, counted a row at a time
+        uint64_t nz = 0;
+        for (unsigned j = 1; j < m; ++j)
+            nz += gf_count_nonzero(mrow(pivots_[j]), j);
+        lowerOpBytes = nz * (m ? len[0] : 0);
+        for (unsigned i = 0; i + 1 < m; ++i)
+            desc[i].lowerLen = len[i];
+    } else {
+        for (unsigned i = 0; i + 1 < m; ++i) {
+            desc[i].lowerLen = len[i];
+            for (unsigned j = i + 1; j < m; ++j) {
+                if (mrow(pivots_[j])[i] == 0)
+                    continue;
+                lowerOpBytes += len[i];
+                if (len[j] < len[i])
+                    len[j] = len[i];
+            }
         }
     }
     eng_->account(lowerOpBytes, 0, true);

@@ -216,6 +216,15 @@ private:
     void cover(unsigned lo, unsigned hi);   // row batch window covers [lo, hi)
     unsigned windowLo_ = 0;                 // lowest element the current row references
     DevSum& get_sum(unsigned lane, unsigned s, unsigned elementEnd);
+    /// get_sum's walk of a lane's elements [from, to): valid while the
+    /// window's slots are unchanged (scanEpoch_ moves on every change)
+    struct LaneScan
+    {
+        unsigned from = ~0u, to = 0, end = 0, most = 0, got = 0;
+        uint64_t epoch = ~0ull;
+    };
+    LaneScan laneScan_[kLanes];
+    uint64_t scanEpoch_ = 0;
     bool start_sums(unsigned elementStart, unsigned bufferBytes);
     void reset_sums(unsigned elementStart);
     bool plug_sum_holes(unsigned elementStart);
@@ -311,6 +320,7 @@ private:
     std::vector<uint8_t> mat_;
     unsigned matRows_ = 0, matCols_ = 0, matAllocRows_ = 0, matStride_ = 0;
     std::vector<unsigned> pivots_;
+    std::vector<unsigned> geEnd_;   // gaussian_elimination: each pivot row's column count
     unsigned geResume_ = 0;
     uint64_t geBytes_ = 0;   // coefficient bytes the elimination multiplied (accounting)
     // the current pivot row's bytes after the pivot, split for gf_muladd_prepared

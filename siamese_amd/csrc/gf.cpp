@@ -12,6 +12,7 @@ GfTables g_gf;
 static bool g_ready = false;
 
 void gf_muladd_gfni(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n);
+static unsigned count_nonzero_avx512(const uint8_t* row, unsigned n);
 
 bool gf_init()
 {
@@ -64,6 +65,8 @@ bool gf_init()
         }
         g_gf.affine[y] = m;
     }
+    if (__builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vl"))
+        gf_count_nonzero = count_nonzero_avx512;
     if (__builtin_cpu_supports("gfni") && __builtin_cpu_supports("avx512bw") &&
         __builtin_cpu_supports("avx512vl") && !std::getenv("SIAMESE_AMD_NO_GFNI")) {
         gf_muladd_fast = gf_muladd_gfni;
@@ -114,6 +117,82 @@ __attribute__((target("avx512f,avx512bw,avx512vl,gfni"))) void gf_muladd_gfni(ui
 }
 
 void (*gf_muladd_fast)(uint8_t*, const uint8_t*, uint8_t, unsigned) = gf_muladd_row;
+
+__attribute__((target("avx512f,avx512bw,avx512vl,gfni"))) static unsigned ge_nopivot_gfni(
+    uint8_t* mat, unsigned stride, unsigned rows, unsigned columns, unsigned from, const unsigned* end,
+    uint64_t* bytes)
+{
+    uint64_t b = 0;
+    unsigned p = from;
+    for (; p < columns; ++p) {
+        uint8_t* ge = mat + (size_t)p * stride;
+        const uint8_t val = ge[p];
+        if (val == 0)
+            break;
+        const unsigned n = end[p] > p + 1 ? end[p] - p - 1 : 0;
+        const uint8_t* invRow = g_gf.mul[g_gf.inv[val]];
+        // the pivot row's bytes after the pivot, in registers for every row below
+        const unsigned chunks = (n + 63) / 64;
+        __m512i src[4];
+        __mmask64 km[4];
+        for (unsigned c = 0; c < 4; ++c) {
+            const unsigned lo = c * 64;
+            km[c] = lo >= n ? 0 : (n - lo >= 64 ? ~0ull : (1ull << (n - lo)) - 1);
+            src[c] = _mm512_maskz_loadu_epi8(km[c], ge + p + 1 + lo);
+        }
+        for (unsigned k = p + 1; k < rows; ++k) {
+            uint8_t* row = mat + (size_t)k * stride;
+            const uint8_t vj = row[p];
+            if (vj == 0)
+                continue;
+            const uint8_t y = invRow[vj];
+            row[p] = y;
+            if (!n)
+                continue;
+            b += n;
+            const __m512i a = _mm512_set1_epi64((long long)g_gf.affine[y]);
+            for (unsigned c = 0; c < chunks; ++c) {
+                uint8_t* d = row + p + 1 + c * 64;
+                const __m512i x = _mm512_maskz_loadu_epi8(km[c], d);
+                _mm512_mask_storeu_epi8(d, km[c], _mm512_xor_si512(x, _mm512_gf2p8affine_epi64_epi8(src[c], a, 0)));
+            }
+        }
+    }
+    *bytes += b;
+    return p;
+}
+
+unsigned gf_ge_nopivot(uint8_t* mat, unsigned stride, unsigned rows, unsigned columns, unsigned from,
+                       const unsigned* end, uint64_t* bytes, bool* done)
+{
+    *done = gf_gfni() && columns <= 256;
+    return *done ? ge_nopivot_gfni(mat, stride, rows, columns, from, end, bytes) : from;
+}
+
+static unsigned count_nonzero_scalar(const uint8_t* row, unsigned n)
+{
+    unsigned c = 0;
+    for (unsigned i = 0; i < n; ++i)
+        c += row[i] != 0;
+    return c;
+}
+
+__attribute__((target("avx512f,avx512bw,avx512vl"))) static unsigned count_nonzero_avx512(const uint8_t* row,
+                                                                                        unsigned n)
+{
+    unsigned c = 0, i = 0;
+    for (; i + 64 <= n; i += 64)
+        c += (unsigned)__builtin_popcountll(
+            _mm512_test_epi8_mask(_mm512_loadu_si512((const void*)(row + i)), _mm512_set1_epi8(-1)));
+    if (i < n) {
+        const __mmask64 k = (1ull << (n - i)) - 1;
+        c += (unsigned)__builtin_popcountll(
+            _mm512_mask_test_epi8_mask(k, _mm512_maskz_loadu_epi8(k, row + i), _mm512_set1_epi8(-1)));
+    }
+    return c;
+}
+
+unsigned (*gf_count_nonzero)(const uint8_t*, unsigned) = count_nonzero_scalar;
 
 bool gf_gfni()
 {

@@ -64,6 +64,20 @@ void gf_muladd_prepared(uint8_t* dst, const GfRowSrc& src, uint8_t y);
 extern void (*gf_muladd_fast)(uint8_t* dst, const uint8_t* src, uint8_t y, unsigned n);
 /// True when gf_muladd_fast runs on GFNI.
 bool gf_gfni();
+/// Gaussian elimination without pivoting over rows [0, rows) of an m-column
+/// matrix (row r at mat + r * stride, stride >= align(columns) + 64), the
+/// reference's GaussianElimination loop (SiameseDecoder.cpp:2423-2466): for
+/// pivot p = from, from + 1, ... while the pivot byte is non-zero, every row
+/// below gets y = row[p] / pivot stored at [p] and y * pivot row (p, end[p])
+/// added after it.  Returns the first pivot whose byte is zero (columns when
+/// none is), with *bytes += the multiplied bytes (the reference's muladds).
+/// GFNI + AVX-512 where the host has them (*done = false otherwise: the
+/// caller runs its own loop).
+unsigned gf_ge_nopivot(uint8_t* mat, unsigned stride, unsigned rows, unsigned columns, unsigned from,
+                       const unsigned* end, uint64_t* bytes, bool* done);
+
+/// Number of non-zero bytes in row[0, n) (AVX-512 where the host has it).
+extern unsigned (*gf_count_nonzero)(const uint8_t* row, unsigned n);
 
 /// Dense Siamese coefficients of one recovery row for `n` lost columns
 /// (reference SiameseDecoder.cpp:2278-2300): out[j] = comb(opLo[lane[j]]) ^
