@@ -1374,15 +1374,17 @@ bool DecoderCore::generate_matrix()
         // original (or on a column this row already has) lands on one of
         // the row's spare bytes past `columns` instead of branching: they are
         // outside the matrix, and rewritten if the matrix ever grows over them.
+        // (eight spare bytes, so picks on received originals do not chain
+        // through one byte's load-xor-store; one unsigned range test, so the
+        // pick's target is a select, not a branch)
         unsigned picks = 0;
         const uint32_t* off = ldpc_offsets(m.row, m.ldpcCount, &picks);
         const uint32_t* pc = pickCol_.data() + (rec->elementStart - pickLo);
-        // (eight spare bytes, so picks on received originals do not chain
-        // through one byte's load-xor-store)
         const uint8_t val[2] = {1, rx};
+        const uint32_t span = columns - startCol;
         for (unsigned k = 0; k < picks; ++k) {
             const uint32_t c = pc[off[k]];
-            const uint32_t at = (c < columns && c >= startCol) ? c : columns + (k & 7);
+            const uint32_t at = (c - startCol < span) ? c : columns + (k & 7);
             row[at] ^= val[k & 1];
         }
     }
