@@ -1258,13 +1258,10 @@ void DecoderCore::populate_columns(unsigned oldColumns, unsigned newColumns)
                 ColInfo& c = cols_[column];
                 c.column = element_to_column(sub * kSubwindow + bit);
                 c.original = &sw->slot[bit];
-                c.cx = column_value(c.column);
-                const uint8_t cx2 = gf_sqr(c.cx);
-                for (unsigned k = 0; k < 8; ++k)
-                    c.comb[k] = (uint8_t)((k & 1) ^ ((k & 2) ? c.cx : 0) ^ ((k & 4) ? cx2 : 0));
+                const uint8_t cx = column_value(c.column);
                 colLane_[column] = (uint8_t)(c.column % kLanes);
-                colCx_[column] = c.cx;
-                colCx2_[column] = cx2;
+                colCx_[column] = cx;
+                colCx2_[column] = gf_sqr(cx);
                 c.original->column = column; // lost slot -> matrix column
                 if (++column >= newColumns)
                     return;
@@ -1371,21 +1368,38 @@ bool DecoderCore::generate_matrix()
             std::memset(row + jEnd, 0, columns - jEnd);
 
         // Sparse columns that landed on lost data.  A pick on a received
-        // original (or on a column this row already has) lands on one of
-        // the row's spare bytes past `columns` instead of branching: they are
-        // outside the matrix, and rewritten if the matrix ever grows over them.
-        // (eight spare bytes, so picks on received originals do not chain
-        // through one byte's load-xor-store; one unsigned range test, so the
-        // pick's target is a select, not a branch)
-        unsigned picks = 0;
-        const uint32_t* off = ldpc_offsets(m.row, m.ldpcCount, &picks);
+        // original (or on a column this row already has) adds nothing.
         const uint32_t* pc = pickCol_.data() + (rec->elementStart - pickLo);
-        const uint8_t val[2] = {1, rx};
         const uint32_t span = columns - startCol;
-        for (unsigned k = 0; k < picks; ++k) {
-            const uint32_t c = pc[off[k]];
-            const uint32_t at = (c - startCol < span) ? c : columns + (k & 7);
-            row[at] ^= val[k & 1];
+        uint64_t hit1 = 0, hitRx = 0;
+        unsigned picks = 0;
+        const uint32_t* off = nullptr;
+        if (columns <= 64 && (ldpc_pick_hits(m.row, m.ldpcCount, pc, startCol, span, &hit1, &hitRx) ||
+                              (off = ldpc_offsets(m.row, m.ldpcCount, &picks)) != nullptr)) {
+            // XOR-ing 1 (even picks) or RX (odd picks) into a byte any number
+            // of times is the parity of its hits: a bit per column each, in
+            // registers (no byte read-modify-write chains through memory)
+            for (unsigned k = 0; k + 1 < picks; k += 2) {
+                const uint32_t c0 = pc[off[k]], c1 = pc[off[k + 1]];
+                hit1 ^= (uint64_t)(c0 - startCol < span) << (c0 & 63);
+                hitRx ^= (uint64_t)(c1 - startCol < span) << (c1 & 63);
+            }
+            for (uint64_t b = hit1 | hitRx; b; b &= b - 1) {
+                const unsigned j = (unsigned)__builtin_ctzll(b);
+                row[j] ^= (uint8_t)(((hit1 >> j) & 1) ^ (((hitRx >> j) & 1) ? rx : 0));
+            }
+        } else {
+            // (eight spare bytes past `columns` take the picks that land
+            // nowhere, so they do not chain through one byte's
+            // load-xor-store; they are outside the matrix, rewritten if it
+            // ever grows over them)
+            off = ldpc_offsets(m.row, m.ldpcCount, &picks);
+            const uint8_t val[2] = {1, rx};
+            for (unsigned k = 0; k < picks; ++k) {
+                const uint32_t c = pc[off[k]];
+                const uint32_t at = (c - startCol < span) ? c : columns + (k & 7);
+                row[at] ^= val[k & 1];
+            }
         }
     }
 

@@ -306,8 +306,6 @@ private:
     {
         DecSlot* original = nullptr;
         unsigned column = 0;
-        uint8_t cx = 0;
-        uint8_t comb[8] = {}; // comb[k] = (k&1) ^ (k&2 ? cx : 0) ^ (k&4 ? cx^2 : 0)
     };
     std::vector<RowInfo> rows_;
     std::vector<ColInfo> cols_;
