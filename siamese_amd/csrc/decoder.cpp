@@ -101,7 +101,8 @@ void DecoderCore::donate_spare()
     colCx_.clear();
     colCx2_.clear();
     pickCol_.clear();
-    mat_.clear();
+    // (mat_ keeps its size: generate_matrix writes every byte of a fresh
+    // matrix it reads, so the next decoder skips a zero fill of the bytes)
     pivots_.clear();
     if (res_ && res_.use_count() == 1) {
         // no completion holds it: back to its freshly constructed state
