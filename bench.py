@@ -407,8 +407,9 @@ def run_rank(rank, world, local, args, library, use_cuda):
     device = local if use_cuda else -1
     sess = S.BatchSession(library, cfg, device=device)
     # untimed warm-up; its first run checks every recovered byte against the payload
+    dge = args.device_ge and args.defer == 0
     res, rep = sess.run(steps=0, warmup=1, verify=args.verify, threads=args.threads,
-                        groups=args.groups, defer=args.defer)
+                        groups=args.groups, defer=args.defer, device_ge=dge)
     if args.verify and (rep.mismatches or any(r.status for r in res)):
         raise RuntimeError("bench: verification failed: %d byte mismatches, status %s"
                            % (rep.mismatches, S.summary(res)["status"]))
@@ -419,7 +420,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
     # buffer arena reaches the timed loop's high-water mark before timing
     if args.warmup > 0:
         sess.run(steps=args.warmup, warmup=0, verify=False, threads=args.threads,
-                 groups=args.groups, digest=False, defer=args.defer)
+                 groups=args.groups, digest=False, defer=args.defer, device_ge=dge)
 
     # the reference on the host cores (rank 0 at N=1 only) over a bounded
     # sample of C4 streams, one run before the timed steps, one after them
@@ -436,7 +437,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
     coll.barrier()
     t0 = time.perf_counter()
     res, rep = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
-                        groups=args.groups, digest=False, defer=args.defer)
+                        groups=args.groups, digest=False, defer=args.defer, device_ge=dge)
     coll.barrier()
     elapsed = time.perf_counter() - t0
     if cb is not None:
@@ -453,14 +454,14 @@ def run_rank(rank, world, local, args, library, use_cuda):
         # recovered byte checked against the payloads)
         res_e, rep_e = sess.run(steps=max(2, args.warmup), warmup=0, verify=args.verify,
                                 threads=args.threads, groups=args.groups, e2e=True, digest=False, defer=args.defer,
-                                frames=args.frames)
+                                frames=args.frames, device_ge=dge)
         if args.verify and (rep_e.mismatches or any(r.status for r in res_e)):
             raise RuntimeError("bench: end-to-end verification failed: %d byte mismatches"
                                % rep_e.mismatches)
         coll.barrier()
         t1 = time.perf_counter()
         sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
-                 groups=args.groups, e2e=True, digest=False, defer=args.defer, frames=args.frames)
+                 groups=args.groups, e2e=True, digest=False, defer=args.defer, frames=args.frames, device_ge=dge)
         coll.barrier()
         e2e_elapsed = time.perf_counter() - t1
     sess.close()
@@ -515,6 +516,8 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "loss_pct": 20,
             "add_calls": "range (sgpu_encoder_add_range / sgpu_decoder_add_original_range)"
                          if args.ranges else "per packet",
+            "decode": "sgpu_decode_device (recovery matrix generated and eliminated on the GPU, k_ge)"
+                      if dge else "sgpu_decode (recovery matrix on the host)",
             "parallelism": "independent streams sharded by index (weak scaling), "
                            "one process per GPU, gloo host barrier",
         },
@@ -639,6 +642,9 @@ def main(argv=None):
                     help="skip the PCIe-inclusive end-to-end leg")
     ap.add_argument("--no-frames", dest="frames", action="store_false",
                     help="end-to-end leg with raw payloads instead of framed datagrams")
+    ap.add_argument("--device-ge", dest="device_ge", action="store_true",
+                    help="decodes by sgpu_decode_device (recovery matrix on the GPU)")
+    ap.add_argument("--no-device-ge", dest="device_ge", action="store_false")
     ap.add_argument("--no-ranges", dest="ranges", action="store_false",
                     help="headline originals through per-packet add/get calls instead of range calls")
     ap.add_argument("--no-legs", dest="legs", action="store_false",

@@ -191,7 +191,9 @@ inline uint64_t data_token(bool hashData, const uint8_t* p, unsigned bytes)
 template <class Codec, class Rec, class Pkt>
 struct Stream
 {
-    enum Phase { ADD, ENCODE, DECODE_LOOP, DECODED, ACK, TAIL, DONE };
+    enum Phase { ADD, ENCODE, DECODE_LOOP, DECODE_PENDING, DECODED, ACK, TAIL, DONE };
+    /// codec decode(): a device matrix job was queued, call again after a flush
+    static constexpr int kDecodePending = 6;
 
     const ScenarioConfig* cfg = nullptr;
     Codec* codec = nullptr;
@@ -372,6 +374,24 @@ struct Stream
         phase = DECODE_LOOP;
     }
 
+    // The decode's outcome (one EV_DECODE per decode, however many calls it
+    // took); the step's return value.
+    bool decoded_result(int r)
+    {
+        note(ev(EV_DECODE, r, (uint64_t)decoded.size()));
+        if (r == 2) {
+            ++res->decode_fail;
+            phase = DECODE_LOOP;
+            return false;
+        }
+        if (r != 0) {
+            fail(2);
+            return false;
+        }
+        phase = DECODED;
+        return codec->wants_yield_after_decode();
+    }
+
     // Advance by one unit of work.  Returns true if the driver should stop
     // stepping this stream until outstanding device work has been flushed.
     bool step()
@@ -440,17 +460,17 @@ struct Stream
             decoded.clear();
             ++res->decode_calls;
             const int r = codec->decode(&decoded);
-            note(ev(EV_DECODE, r, (uint64_t)decoded.size()));
-            if (r == 2) {
-                ++res->decode_fail;
-                return false;
+            if (r == kDecodePending) {
+                phase = DECODE_PENDING;
+                return true;   // (its outcome arrives with the flush)
             }
-            if (r != 0) {
-                fail(2);
-                return false;
-            }
-            phase = DECODED;
-            return codec->wants_yield_after_decode();
+            return decoded_result(r);
+        }
+        case DECODE_PENDING: {
+            const int r = codec->decode(&decoded);
+            if (r == kDecodePending)
+                return true;
+            return decoded_result(r);
         }
         case DECODED: {
             for (const Pkt& p : decoded) {

@@ -53,6 +53,8 @@ struct BatchOptions
                        ///< sgpu_frames_recv, recovery packets copied back framed by
                        ///< sgpu_frames_send and parsed on landing
     uint32_t no_timing; ///< timed steps without the per-launch device timing events
+    uint32_t device_ge; ///< defer 0: decodes by sgpu_decode_device (recovery matrix generated and
+                        ///< eliminated on the device; a decode then takes two submissions)
                         ///< (device_ms / exec_ms read 0): the events order every launch
                         ///< behind a timestamp, tens of microseconds a flush on the
                         ///< latency-bound single-stream legs
@@ -74,7 +76,7 @@ struct BatchReport
     /// + completion), token resolution, finish + free
     double phase_seconds[5];
     uint64_t payload_bytes;   ///< payload bytes of the originals added in the timed steps (all steps)
-    double kernel_ms[4];      ///< device time by kernel class (sgpu_timing_kernels)
+    double kernel_ms[5];      ///< device time by kernel class (sgpu_timing_kernels)
 };
 
 } // extern "C"
@@ -106,6 +108,7 @@ struct Api
     SiameseResult (*decoder_add_original_range)(SgpuDecoder, unsigned, const void*, size_t, const unsigned*,
                                                 unsigned, unsigned, SiameseResult*, unsigned*);
     SiameseResult (*decoder_get_range)(SgpuDecoder, unsigned, unsigned, SiameseOriginalPacket*, unsigned*);
+    SiameseResult (*decode_device)(SgpuDecoder, SiameseOriginalPacket**, unsigned*);
     int (*flush)(void);
     int (*submit)(void);
     long long (*enqueue)(void);
@@ -189,7 +192,8 @@ bool load_api(const char* path, Api& a)
            bind_optional(h, a.decoder_add_original_range, "sgpu_decoder_add_original_range") &&
            bind_optional(h, a.decoder_get_range, "sgpu_decoder_get_range") &&
            bind_optional(h, a.engine_stats_ex, "sgpu_engine_stats_ex") &&
-           bind_optional(h, a.timing_kernels, "sgpu_timing_kernels");
+           bind_optional(h, a.timing_kernels, "sgpu_timing_kernels") &&
+           bind_optional(h, a.decode_device, "sgpu_decode_device");
 }
 
 // SCENARIO_BATCH_CALLS=1: time every codec call by kind and print the
@@ -305,6 +309,7 @@ struct Shared
     unsigned groups = 1;
     bool digest = true;   // per-stream digests (event logs) also on unverified runs
     unsigned defer = 0;   // BatchOptions::defer
+    bool deviceGe = false;   // BatchOptions::device_ge (and the library has it)
 };
 
 struct BatchCodec
@@ -403,6 +408,8 @@ struct BatchCodec
             p = entries(kCap);
             r = sh->api->decode_deferred(dec, p, kCap, &n);
             slabUsed -= kCap - (r == 0 ? n : 0);
+        } else if (sh->deviceGe) {
+            r = sh->api->decode_device(dec, &p, &n);
         } else {
             r = sh->api->decode(dec, &p, &n);
         }
@@ -1248,6 +1255,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
             sh.pool.reset(new sgpu::WorkerPool(opt->threads));
         sh.groups = opt->groups ? opt->groups : 1;
         sh.defer = opt->defer;
+        sh.deviceGe = opt->device_ge && !opt->defer && api.decode_device;
         uint64_t rounds = 0, payload = 0;
         double phase[5] = {0, 0, 0, 0, 0};
         // headroom over the warm-up's high-water mark, so the working set's
@@ -1269,16 +1277,16 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         const auto t1 = Clock::now();
         rc = run_pipeline(sh, results, timed ? opt->steps : 1, &rounds, phase, &payload);
         const double dt = std::chrono::duration<double>(Clock::now() - t1).count();
-        double execMs = 0, totalMs = 0, kernelMs[4] = {0, 0, 0, 0};
+        double execMs = 0, totalMs = 0, kernelMs[5] = {0, 0, 0, 0, 0};
         if (api.timing_kernels)
-            api.timing_kernels(kernelMs, 4);
+            api.timing_kernels(kernelMs, 5);
         api.timing(0, 1, &execMs, &totalMs);
         stats(e1);
         if (timed) {
             report->seconds += dt;
             report->device_ms += totalMs;
             report->exec_ms += execMs;
-            for (int k = 0; k < 4; ++k)
+            for (int k = 0; k < 5; ++k)
                 report->kernel_ms[k] += kernelMs[k];
             report->rounds += rounds;
             report->payload_bytes += payload;

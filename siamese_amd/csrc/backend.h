@@ -70,6 +70,11 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
                      const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
                      uint32_t solveBegin, uint32_t solveCount);
 
+/// Device recovery-matrix generation + elimination (ops.h GeDesc): one job
+/// per desc, its input at in + desc.in, its output in results + desc.result.
+/// Reads nothing any other launch of the flush writes.
+void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results);
+
 /// Block until all queued work has finished.  Returns false on a device fault.
 bool be_sync();
 
@@ -105,7 +110,7 @@ bool be_mark_sync(void* mark);
 /// Device-time accounting: every executor/solve launch is bracketed with
 /// events; these return the accumulated milliseconds since the last reset.
 /// Kernel classes of the per-launch device timing.
-enum BeKernel { kBeIngest, kBeExec, kBeLdpc, kBeSolve, kBeKernelKinds };
+enum BeKernel { kBeIngest, kBeExec, kBeLdpc, kBeSolve, kBeGe, kBeKernelKinds };
 void be_timing_enable(bool on);
 /// Device milliseconds of one kernel class since the last reset
 /// (be_timing_exec_ms is kBeExec's).

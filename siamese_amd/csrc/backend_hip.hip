@@ -2773,6 +2773,240 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
     }
 }
 
+// ---------------------------------------------------------------------------
+// The recovery matrix of a decode on the device (k_ge, ops.h GeDesc)
+//
+// One workgroup per decode, the matrix resident in LDS (kGeStride bytes a
+// row).  Generation (the host's generate_matrix; reference
+// SiameseDecoder.cpp:2157-2383) writes four columns per thread: the dense
+// part from the row's opcodes (Siamese), 1/(X ^ Y) (Cauchy) or 1 (parity);
+// then the LDPC picks, one row per wave and 64 PCG draws per pass (jump-ahead
+// c_pcgA/c_pcgG), land by LDS XOR atomics.  The elimination is the
+// reference's (:2423-2531): no pivoting while each pivot byte is non-zero,
+// then row pivoting from the first zero one; each pivot is one multiplier
+// pass over the rows below (y = row[p] / pivot, kept at [p]) and one
+// row-update pass over their bytes (p, end), a dword per thread.
+constexpr unsigned kGeThreads = 256;
+constexpr unsigned kGeStride = kGeMaxCols + 4;   // 33 dwords: consecutive rows start in different banks
+
+__device__ __forceinline__ uint32_t ge_opcode(uint32_t lane, uint32_t row)
+{
+    // SiameseCommon.h:150-174 (wang_hash32 of lane + (row + 3) * 8, 0 -> 16)
+    uint32_t k = lane + (row + 3u) * kLanes;
+    k += ~(k << 15);
+    k ^= k >> 10;
+    k += k << 3;
+    k ^= k >> 6;
+    k += ~(k << 11);
+    k ^= k >> 16;
+    const uint32_t op = k & 63u;
+    return op ? op : 16u;
+}
+
+__device__ __forceinline__ uint32_t ge_comb(uint32_t k, uint32_t cx, uint32_t cx2)
+{
+    return (k & 1u) ^ ((k & 2u) ? cx : 0u) ^ ((k & 4u) ? cx2 : 0u);
+}
+
+__global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ descs, const uint8_t* __restrict__ in,
+                                                  uint32_t* __restrict__ results)
+{
+    constexpr uint32_t S4 = kGeStride / 4;
+    __shared__ uint32_t M[kGeMaxRows * S4];
+    __shared__ uint4 permL[256];
+    __shared__ uint32_t permC[256];
+    __shared__ uint8_t piv[kGeMaxRows], used[kGeMaxRows], yv[kGeMaxRows];
+    __shared__ uint16_t cnt[kGeMaxRows];
+    __shared__ uint32_t found;
+    __shared__ unsigned long long bytesL;
+    uint8_t* Mb = reinterpret_cast<uint8_t*>(M);
+    const GeDesc d = descs[blockIdx.x];
+    const uint32_t rows = d.rows, cols = d.cols;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const GeRow* R = reinterpret_cast<const GeRow*>(in + d.in);
+    const GeCol* C = reinterpret_cast<const GeCol*>(R + rows);
+    const uint8_t* pick = reinterpret_cast<const uint8_t*>(C + cols);
+    {
+        const uint32_t* t = c_perm[tid];   // (kGeThreads == 256)
+        permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
+        permC[tid] = t[4];
+    }
+    for (uint32_t i = tid; i < rows; i += kGeThreads) {
+        piv[i] = (uint8_t)i;
+        used[i] = 0;
+        cnt[i] = R[i].colCount;
+    }
+    if (tid == 0)
+        bytesL = 0;
+    __syncthreads();
+
+    // 1. dense parts, a dword (four columns) per thread
+    const uint32_t wpr = (cols + 3u) / 4u;
+    for (uint32_t x = tid; x < rows * wpr; x += kGeThreads) {
+        const uint32_t r = x / wpr, w = x - r * wpr;
+        const GeRow g = R[r];
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t j = 4u * w + q;
+            if (j < cols && j < g.jEnd) {
+                const GeCol c = C[j];
+                uint32_t v = 1u, h = 0u;
+                if (g.kind == GE_CAUCHY) {
+                    v = c_inv[(uint8_t)(g.rbase ^ c.ccol)];
+                } else if (g.kind == GE_SIAMESE) {
+                    const uint32_t op = ge_opcode(c.lane, g.row);
+                    v = ge_comb(op & 7u, c.cx, c.cx2);
+                    h = ge_comb(op >> 3, c.cx, c.cx2);
+                }
+                lo |= v << (8u * q);
+                hi |= h << (8u * q);
+            }
+        }
+        if (hi)   // v ^ RX * h
+            lo ^= gf_mul_tab(hi, gf_tab_l(permL, permC, 1u + (g.row + 1u) % kRowValuePeriod));
+        M[r * S4 + w] = lo;
+    }
+    __syncthreads();
+
+    // 2. LDPC picks: one Siamese row per wave, draws c0 + lane per pass
+    for (uint32_t r = wave; r < rows; r += kGeThreads / 64u) {
+        const GeRow g = R[r];
+        if (g.kind != GE_SIAMESE || g.ldpcN == 0)
+            continue;   // (uniform in the wave)
+        const uint32_t N = g.ldpcN, P = 2u * ((N + kPairRate - 1u) / kPairRate);
+        const uint64_t inc = ((uint64_t)g.row << 1) | 1u;
+        uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed(row, N)
+        const uint64_t ja = c_pcgA[lane], jg = c_pcgG[lane];
+        const uint32_t rx = 1u + (g.row + 1u) % kRowValuePeriod;
+        for (uint32_t c0 = 0; c0 < P; c0 += 64u) {
+            const uint32_t k = c0 + lane;
+            const uint64_t st = ja * sc + inc * jg;
+            sc = c_pcgA[64] * sc + inc * c_pcgG[64];
+            if (k < P) {
+                const uint32_t col = pick[g.pickOff + pcg_output(st) % N];
+                if (col < cols)
+                    atomicXor(&M[r * S4 + col / 4u], ((k & 1u) ? rx : 1u) << (8u * (col & 3u)));
+            }
+        }
+    }
+    __syncthreads();
+
+    // 3. elimination.  One pivot step: the rows below `pivot` (through piv[]
+    // when pivoting) take y = row[pivot] / val at [pivot], then y * the
+    // source row's bytes (pivot, end) (SiameseDecoder.h:504-541)
+    unsigned long long myBytes = 0;
+    auto eliminate = [&](uint32_t src, uint32_t pivot, uint32_t end, uint32_t val, bool pivoted) {
+        const GfTab iv = gf_tab_l(permL, permC, c_inv[val]);
+        for (uint32_t k = pivot + 1u + tid; k < rows; k += kGeThreads) {
+            const uint32_t rk = pivoted ? piv[k] : k;
+            const uint32_t v = Mb[rk * kGeStride + pivot];
+            uint32_t y = 0;
+            if (v) {
+                y = gf_mul_tab(v, iv) & 0xffu;
+                Mb[rk * kGeStride + pivot] = (uint8_t)y;
+                if (end > pivot + 1u)
+                    myBytes += end - pivot - 1u;
+                if (pivoted && cnt[rk] < end)
+                    cnt[rk] = (uint16_t)end;
+            }
+            yv[rk] = (uint8_t)y;
+        }
+        __syncthreads();
+        if (end > pivot + 1u) {
+            const uint32_t w0 = (pivot + 1u) / 4u, nw = (end + 3u) / 4u - w0;
+            const uint32_t nr = rows - pivot - 1u;
+            for (uint32_t x = tid; x < nr * nw; x += kGeThreads) {
+                const uint32_t kk = x / nw, w = w0 + (x - kk * nw);
+                const uint32_t rk = pivoted ? piv[pivot + 1u + kk] : pivot + 1u + kk;
+                const uint32_t y = yv[rk];
+                if (!y)
+                    continue;
+                const uint32_t mask = byte_mask((int)end - (int)(4u * w)) & ~byte_mask((int)(pivot + 1u) - (int)(4u * w));
+                M[rk * S4 + w] ^= gf_mul_tab(M[src * S4 + w], gf_tab_l(permL, permC, y)) & mask;
+            }
+        }
+        __syncthreads();
+    };
+    uint32_t p = 0;
+    for (; p < cols; ++p) {
+        const uint32_t val = Mb[p * kGeStride + p];
+        if (val == 0)
+            break;
+        if (tid == 0)
+            used[p] = 1;
+        eliminate(p, p, cnt[p], val, false);
+    }
+    uint32_t stop = cols;
+    if (p < cols) {
+        uint32_t jFrom = p + 1u;   // (the caller found column p zero in row p)
+        for (uint32_t pivot = p; pivot < cols; ++pivot) {
+            if (tid == 0)
+                found = 0xffffffffu;
+            __syncthreads();
+            for (uint32_t j = jFrom + tid; j < rows; j += kGeThreads)
+                if (Mb[piv[j] * kGeStride + pivot])
+                    atomicMin(&found, j);
+            __syncthreads();
+            const uint32_t j = found;
+            if (j == 0xffffffffu) {
+                stop = pivot;
+                break;
+            }
+            const uint32_t rj = piv[j];
+            __syncthreads();   // (every thread has read piv[j])
+            if (tid == 0) {
+                piv[j] = piv[pivot];
+                piv[pivot] = (uint8_t)rj;
+                used[rj] = 1;
+            }
+            __syncthreads();
+            if (pivot >= cols - 1u)
+                break;
+            eliminate(rj, pivot, cnt[rj], Mb[rj * kGeStride + pivot], true);
+            jFrom = pivot + 1u;
+        }
+    }
+
+    // 4. outcome, pivots, used rows, column counts, the matrix
+    if (myBytes)
+        atomicAdd(&bytesL, myBytes);
+    __syncthreads();
+    uint32_t* out = results + d.result;
+    if (tid == 0) {
+        out[0] = stop;
+        out[1] = (uint32_t)bytesL;
+        out[2] = (uint32_t)(bytesL >> 32);
+        out[3] = 0;
+    }
+    for (uint32_t w = tid; w < (rows + 3u) / 4u; w += kGeThreads) {
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            if (4u * w + q < rows) {
+                a |= (uint32_t)piv[4u * w + q] << (8u * q);
+                b |= (uint32_t)used[4u * w + q] << (8u * q);
+            }
+        out[ge_out_pivots(rows) + w] = a;
+        out[ge_out_used(rows) + w] = b;
+    }
+    for (uint32_t w = tid; w < (rows + 1u) / 2u; w += kGeThreads)
+        out[ge_out_counts(rows) + w] = (uint32_t)cnt[2u * w] | (2u * w + 1u < rows ? (uint32_t)cnt[2u * w + 1u] << 16 : 0u);
+    const uint32_t total = rows * cols;
+    for (uint32_t w = tid; w < (total + 3u) / 4u; w += kGeThreads) {
+        uint32_t a = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t b = 4u * w + q;
+            if (b < total) {
+                const uint32_t r = b / cols;
+                a |= (uint32_t)Mb[r * kGeStride + (b - r * cols)] << (8u * q);
+            }
+        }
+        out[ge_out_matrix(rows) + w] = a;
+    }
+}
+
 // Layout check of the int8 MFMA (tests): D = A B for 32 x 32 x 32 with
 // asymmetric integer data, fragments as k_solve_mfma reads them.
 __global__ void k_mfma_i8_check(int* __restrict__ out)
@@ -3262,6 +3496,14 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
     Timed t(kBeLdpc);
     hipLaunchKernelGGL(k_ldpc, dim3(count), dim3(64 * kLdpcWaves), 0, g_stream, items,
                        reinterpret_cast<unsigned long long*>(acct));
+}
+
+void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results)
+{
+    if (count == 0)
+        return;
+    Timed t(kBeGe);
+    hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), 0, g_stream, descs, in, results);
 }
 
 void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,

@@ -149,7 +149,7 @@ SIAMESE_EXPORT void sgpu_decoder_free(SgpuDecoder decoder)
 SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original(SgpuDecoder decoder, unsigned packetNum,
                                                        const void* deviceData, unsigned bytes)
 {
-    if (!decoder || !deviceData || bytes == 0 || bytes > SIAMESE_MAX_PACKET_BYTES ||
+    if (!decoder || BD(decoder)->core.ge_pending() || !deviceData || bytes == 0 || bytes > SIAMESE_MAX_PACKET_BYTES ||
         packetNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     SiameseOriginalPacket p;
@@ -167,7 +167,7 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original_range(SgpuDecoder decoder
 {
     if (callsOut)
         *callsOut = 0;
-    if (!decoder || (!deviceData && count) || firstPacketNum > SIAMESE_PACKET_NUM_MAX || stride > 0xffffffffu ||
+    if (!decoder || BD(decoder)->core.ge_pending() || (!deviceData && count) || firstPacketNum > SIAMESE_PACKET_NUM_MAX || stride > 0xffffffffu ||
         (count > 1 && stride == 0))
         return Siamese_InvalidInput;
     unsigned calls = 0;
@@ -181,7 +181,7 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original_range(SgpuDecoder decoder
 
 SIAMESE_EXPORT SiameseResult sgpu_decoder_add_recovery(SgpuDecoder decoder, const SgpuRecoveryPacket* packet)
 {
-    if (!decoder || !packet || !packet->DeviceData || packet->DataBytes == 0 ||
+    if (!decoder || BD(decoder)->core.ge_pending() || !packet || !packet->DeviceData || packet->DataBytes == 0 ||
         packet->FooterBytes == 0 || packet->FooterBytes > 8 || packet->FooterBytes >= packet->DataBytes)
         return Siamese_InvalidInput;
     DeviceRecovery r;
@@ -196,7 +196,7 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_add_recovery(SgpuDecoder decoder, cons
 
 SIAMESE_EXPORT SiameseResult sgpu_decoder_is_ready(SgpuDecoder decoder)
 {
-    if (!decoder)
+    if (!decoder || BD(decoder)->core.ge_pending())
         return Siamese_InvalidInput;
     return BD(decoder)->core.is_ready();
 }
@@ -204,14 +204,22 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_is_ready(SgpuDecoder decoder)
 SIAMESE_EXPORT SiameseResult sgpu_decode(SgpuDecoder decoder, SiameseOriginalPacket** packetsOut,
                                          unsigned* countOut)
 {
-    if (!decoder || (!packetsOut != !countOut))
+    if (!decoder || BD(decoder)->core.ge_pending() || (!packetsOut != !countOut))
         return Siamese_InvalidInput;
     return BD(decoder)->core.decode(packetsOut, countOut);
 }
 
+SIAMESE_EXPORT SiameseResult sgpu_decode_device(SgpuDecoder decoder, SiameseOriginalPacket** packetsOut,
+                                                unsigned* countOut)
+{
+    if (!decoder || (!packetsOut != !countOut))
+        return Siamese_InvalidInput;
+    return BD(decoder)->core.decode_device(packetsOut, countOut);
+}
+
 SIAMESE_EXPORT SiameseResult sgpu_decoder_get(SgpuDecoder decoder, SiameseOriginalPacket* packet)
 {
-    if (!decoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
+    if (!decoder || BD(decoder)->core.ge_pending() || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     return BD(decoder)->core.get(*packet);
 }
@@ -221,7 +229,7 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_get_range(SgpuDecoder decoder, unsigne
 {
     if (gotOut)
         *gotOut = 0;
-    if (!decoder || (!packets && count) || !gotOut || firstPacketNum > SIAMESE_PACKET_NUM_MAX)
+    if (!decoder || BD(decoder)->core.ge_pending() || (!packets && count) || !gotOut || firstPacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     return BD(decoder)->core.get_range(firstPacketNum, count, packets, gotOut);
 }
@@ -229,21 +237,21 @@ SIAMESE_EXPORT SiameseResult sgpu_decoder_get_range(SgpuDecoder decoder, unsigne
 SIAMESE_EXPORT SiameseResult sgpu_decode_deferred(SgpuDecoder decoder, SiameseOriginalPacket* out,
                                                   unsigned capacity, unsigned* countOut)
 {
-    if (!decoder || !out || !countOut)
+    if (!decoder || BD(decoder)->core.ge_pending() || !out || !countOut)
         return Siamese_InvalidInput;
     return BD(decoder)->core.decode_deferred(out, capacity, countOut);
 }
 
 SIAMESE_EXPORT SiameseResult sgpu_decoder_get_deferred(SgpuDecoder decoder, SiameseOriginalPacket* packet)
 {
-    if (!decoder || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
+    if (!decoder || BD(decoder)->core.ge_pending() || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     return BD(decoder)->core.get_deferred(*packet);
 }
 
 SIAMESE_EXPORT SiameseResult sgpu_decoder_has(SgpuDecoder decoder, unsigned packetNum)
 {
-    if (!decoder || packetNum > SIAMESE_PACKET_NUM_MAX)
+    if (!decoder || BD(decoder)->core.ge_pending() || packetNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     return BD(decoder)->core.has(packetNum) ? Siamese_Success : Siamese_NeedMoreData;
 }

@@ -121,6 +121,8 @@ void DecoderCore::donate_spare()
         res_->out = nullptr;
         res_->outCount = 0;
         res_->outSerial = 0;
+        res_->geOut.clear();
+        res_->geDone = false;
     } else if (res_) {
         // completions still queued or in flight: they fill the caller-owned
         // entries they carry and leave this decoder's memory alone
@@ -1081,7 +1083,11 @@ SiameseResult DecoderCore::decode(SiameseOriginalPacket** packetsOut, unsigned* 
     }
     if (!check_recovery_possible())
         return Siamese_NeedMoreData;
+    return decode_loop(packetsOut, countOut);
+}
 
+SiameseResult DecoderCore::decode_loop(SiameseOriginalPacket** packetsOut, unsigned* countOut)
+{
     RecPacket* r = region_.last;
     unsigned nextCheck = region_.nextCheckStart;
     unsigned recCount = region_.recoveryCount;
@@ -1176,11 +1182,8 @@ SiameseResult DecoderCore::decode_region()
         g_decodeClocks.fails += solved ? 0 : 1;
         g_decodeClocks.fresh += oldRowsAtEntry == 0 ? 1 : 0;
     }
-    if (!solved) {
-        region_.solveFailed = true;
-        stats_[SiameseDecoderStats_SolveFailCount]++;
-        return Siamese_NeedMoreData;
-    }
+    if (!solved)
+        return finish_region(false);
     if (!eliminate_original_data()) {
         disabled_ = true;
         return Siamese_Disabled;
@@ -1199,6 +1202,179 @@ SiameseResult DecoderCore::decode_region()
         g_decodeClocks.sample(d);
     }
     region_reset();
+    return res;
+}
+
+SiameseResult DecoderCore::finish_region(bool solved)
+{
+    if (!solved) {
+        region_.solveFailed = true;
+        stats_[SiameseDecoderStats_SolveFailCount]++;
+        return Siamese_NeedMoreData;
+    }
+    if (!eliminate_original_data()) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    const SiameseResult res = solve_and_substitute();
+    region_reset();
+    return res;
+}
+
+// ---------------------------------------------------------------------------
+// The recovery matrix on the device (decode_device, ops.h GeDesc)
+
+SiameseResult DecoderCore::decode_device(SiameseOriginalPacket** packetsOut, unsigned* countOut)
+{
+    if (geState_)
+        return finish_device_ge(packetsOut, countOut);
+    settle();
+    if (dead())
+        return Siamese_Disabled;
+    if (hasRecovered_) {
+        hasRecovered_ = false;
+        if (packetsOut) {
+            *packetsOut = recovered_.data();
+            *countOut = (unsigned)recovered_.size();
+        }
+        return Siamese_Success;
+    }
+    if (packetsOut) {
+        *packetsOut = nullptr;
+        *countOut = 0;
+    }
+    if (!check_recovery_possible())
+        return Siamese_NeedMoreData;
+    // (the search's first attempt, on a fresh matrix: decode_loop's first
+    // decode_region)
+    if (region_.recoveryCount >= region_.lostCount && rows_.empty() && geResume_ == 0 && submit_device_ge())
+        return kDecodePending;
+    return decode_loop(packetsOut, countOut);
+}
+
+bool DecoderCore::submit_device_ge()
+{
+    const unsigned columns = region_.lostCount;
+    const unsigned rows = region_.recoveryCount;
+    if (columns == 0 || columns > kGeMaxCols || rows > kGeMaxRows)
+        return false;
+    // generate_matrix's bookkeeping on a fresh matrix; the coefficients are
+    // the device's
+    matrix_resize(rows, columns, true);
+    populate_columns(0, columns);
+    populate_rows(0, rows);
+    unsigned pickLo = ~0u, pickHi = 0;
+    for (unsigned i = 0; i < rows; ++i) {
+        const RecPacket* rec = rows_[i].rec;
+        if (rec->meta.sumCount <= kCauchyThreshold)
+            continue;
+        pickLo = std::min(pickLo, rec->elementStart);
+        pickHi = std::max(pickHi, rec->elementStart + rec->meta.ldpcCount);
+    }
+    const unsigned pickLen = pickHi > pickLo ? pickHi - pickLo : 0;
+    if (disabled_ || pickLen > kGeMaxPick) {
+        // (the host path meets the same condition and handles it)
+        disabled_ = false;
+        matrix_reset();
+        return false;
+    }
+    uint32_t base = 0;
+    uint8_t* in = prog_.ge_job(rows, columns, pickLen, &base);
+    GeRow* R = reinterpret_cast<GeRow*>(in);
+    GeCol* C = reinterpret_cast<GeCol*>(R + rows);
+    uint8_t* pick = reinterpret_cast<uint8_t*>(C + columns);
+    for (unsigned j = 0; j < columns; ++j)
+        C[j] = GeCol{colLane_[j], colCx_[j], colCx2_[j], (uint8_t)(cols_[j].column % kCauchyMaxColumns)};
+    for (unsigned e = pickLo; e < pickHi; ++e) {
+        const DecSlot& a = slot(e);
+        pick[e - pickLo] = (a.bytes == 0 && a.column < columns) ? (uint8_t)a.column : kGeNoColumn;
+    }
+    // rows of one decode share their column range: the end of the dense
+    // part for the last (columnStart, sumCount) is remembered
+    unsigned endKeyStart = ~0u, endKeyCount = 0, endVal = 0;
+    for (unsigned i = 0; i < rows; ++i) {
+        const RecPacket* rec = rows_[i].rec;
+        const RowMeta m = rec->meta;
+        unsigned jEnd = 0;
+        if (endKeyStart == m.columnStart && endKeyCount == m.sumCount)
+            jEnd = endVal;
+        else {
+            while (jEnd < columns && column_sub(cols_[jEnd].column, m.columnStart) < m.sumCount)
+                ++jEnd;
+            endKeyStart = m.columnStart;
+            endKeyCount = m.sumCount;
+            endVal = jEnd;
+        }
+        GeRow& g = R[i];
+        std::memset(&g, 0, sizeof(g));
+        g.jEnd = (uint16_t)jEnd;
+        g.colCount = (uint16_t)rows_[i].columnCount;
+        if (m.sumCount <= kCauchyThreshold) {
+            g.kind = m.row == 0 ? GE_PARITY : GE_CAUCHY;
+            g.rbase = (uint8_t)(m.row - 1 + kCauchyMaxColumns);
+        } else {
+            g.kind = GE_SIAMESE;
+            g.row = (uint16_t)m.row;
+            g.ldpcN = m.ldpcCount;
+            g.pickOff = rec->elementStart - pickLo;
+        }
+    }
+    const uint32_t words = ge_result_words(rows, columns);
+    prog_.on_complete([r = res_, base, words](const uint32_t* results) {
+        std::lock_guard<std::mutex> g(r->mu);
+        r->geOut.assign(results + base, results + base + words);
+        r->geDone = true;
+    });
+    geState_ = 1;
+    geRows_ = rows;
+    geCols_ = columns;
+    return true;
+}
+
+SiameseResult DecoderCore::finish_device_ge(SiameseOriginalPacket** packetsOut, unsigned* countOut)
+{
+    {
+        std::lock_guard<std::mutex> g(res_->mu);
+        if (!res_->geDone)
+            return kDecodePending;   // (its flush has not completed yet)
+        geOut_.swap(res_->geOut);
+        res_->geDone = false;
+    }
+    geState_ = 0;
+    settle();
+    if (packetsOut) {
+        *packetsOut = nullptr;
+        *countOut = 0;
+    }
+    if (dead())
+        return Siamese_Disabled;
+    const unsigned rows = geRows_, columns = geCols_;
+    const uint32_t* o = geOut_.data();
+    if (o[0] < columns) {
+        // the elimination stopped short of a pivot: the host repeats it (the
+        // resumable state the reference keeps for the next attempt), and the
+        // search goes on as decode() does
+        matrix_reset();
+        return decode_loop(packetsOut, countOut);
+    }
+    const uint8_t* piv = reinterpret_cast<const uint8_t*>(o + ge_out_pivots(rows));
+    const uint8_t* used = reinterpret_cast<const uint8_t*>(o + ge_out_used(rows));
+    const uint16_t* cnt = reinterpret_cast<const uint16_t*>(o + ge_out_counts(rows));
+    const uint8_t* mat = reinterpret_cast<const uint8_t*>(o + ge_out_matrix(rows));
+    pivots_.resize(rows);
+    for (unsigned i = 0; i < rows; ++i) {
+        pivots_[i] = piv[i];
+        rows_[i].used = used[i] != 0;
+        rows_[i].columnCount = cnt[i];
+        std::memcpy(mrow(i), mat + (size_t)i * columns, columns);
+    }
+    geBytes_ = ((uint64_t)o[2] << 32) | o[1];
+    eng_->account(geBytes_);
+    const SiameseResult res = finish_region(true);
+    if (res == Siamese_Success && packetsOut) {
+        *packetsOut = recovered_.data();
+        *countOut = (unsigned)recovered_.size();
+    }
     return res;
 }
 

@@ -28,6 +28,10 @@
 
 namespace sgpu {
 
+/// decode_device: a matrix job was queued; call again after the flush
+/// (siamese_gpu.h SGPU_DECODE_PENDING)
+constexpr SiameseResult kDecodePending = static_cast<SiameseResult>(6);
+
 struct DecSlot
 {
     DevBuf buf;
@@ -129,6 +133,14 @@ public:
     SiameseResult is_ready();
     /// Queues the solve; packets' lengths become exact after resolve().
     SiameseResult decode(SiameseOriginalPacket** packetsOut, unsigned* countOut);
+    /// decode() with a fresh recovery matrix generated and eliminated on the
+    /// device (sgpu_decode_device): returns kDecodePending after queueing the
+    /// matrix job; the next call after the flush that ran it finishes the
+    /// decode as decode() would have (an elimination that stopped short is
+    /// repeated on the host, which keeps the resumable state).
+    SiameseResult decode_device(SiameseOriginalPacket** packetsOut, unsigned* countOut);
+    /// A device matrix job is queued and not yet finished by decode_device.
+    bool ge_pending() const { return geState_ != 0; }
     SiameseResult get(SiameseOriginalPacket& packet);
     /// Deferred forms (siamese_gpu.h sgpu_decode_deferred /
     /// sgpu_decoder_get_deferred): never wait for the device.  Outputs go to
@@ -240,6 +252,17 @@ private:
     void matrix_reset();
     bool check_recovery_possible();
     SiameseResult decode_region();
+    /// decode()'s search over the checked region (after check_recovery_possible)
+    SiameseResult decode_loop(SiameseOriginalPacket** packetsOut, unsigned* countOut);
+    /// decode_region after the elimination: its outcome, then the
+    /// elimination of received data and the solve
+    SiameseResult finish_region(bool solved);
+    /// decode_device's two halves
+    bool submit_device_ge();
+    SiameseResult finish_device_ge(SiameseOriginalPacket** packetsOut, unsigned* countOut);
+    unsigned geState_ = 0;               // 1: a device matrix job is queued
+    unsigned geRows_ = 0, geCols_ = 0;   // ... of this size
+    std::vector<uint32_t> geOut_;        // its output (ops.h GeDesc)
     bool generate_matrix();
     void populate_columns(unsigned oldColumns, unsigned newColumns);
     void populate_rows(unsigned oldRows, unsigned newRows);
@@ -370,6 +393,9 @@ private:
         size_t outCount = 0;
         uint64_t outSerial = 0;
         bool mirror = false;
+        // the output of the decoder's device matrix job (decode_device)
+        std::vector<uint32_t> geOut;
+        bool geDone = false;
     };
     static void complete_solve(Resolver& r, unsigned slot, const uint32_t* results);
     static void fill_entry(const PendingDecode& pd, unsigned ci, SiameseOriginalPacket& out);

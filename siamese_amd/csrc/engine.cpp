@@ -90,6 +90,7 @@ void ProgramBody::clear()
     nsegs = 0;
     resultWords = 0;
     nsolves = 0;   // (their vectors keep their capacity)
+    nges = 0;
     callbacks.clear();
     rb.open = false;
     rb.win.clear();
@@ -592,6 +593,22 @@ uint32_t Program::solve(const std::vector<SolveRow>& rows, const uint8_t* coef, 
     const uint32_t r = ps.desc.result;
     b_->new_segment(); // ops after the solve go to the next segment
     return r;
+}
+
+uint8_t* Program::ge_job(unsigned rows, unsigned cols, unsigned pickLen, uint32_t* resultWord)
+{
+    touch();
+    if (b_->nges == b_->ges.size())
+        b_->ges.emplace_back();
+    ProgramBody::PendingGe& g = b_->ges[b_->nges++];
+    g.rows = (uint16_t)rows;
+    g.cols = (uint16_t)cols;
+    g.pickLen = pickLen;
+    g.result = b_->resultWords;
+    b_->resultWords += ge_result_words(rows, cols);
+    g.in.resize(ge_input_bytes(rows, cols, pickLen));
+    *resultWord = g.result;
+    return g.in.data();
 }
 
 void Program::on_complete(Completion fn)
@@ -1266,6 +1283,7 @@ struct Batch
     size_t upBytes = 0, nIngest = 0, nIngBlocks = 0;
     uint32_t maxIngest = 0;
     size_t oIngD = 0, oIngB = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
+    size_t oGeD = 0, oGeIn = 0, nGe = 0;   // device matrix jobs: descs, inputs
     uint64_t wideBase = 0;                 // this submission's k_ldpc scratch: bytes into the ring
     bool wideZero = false;                 // the ring wrapped: zero it before the first exec launch
     uint32_t resultWords = 0;
@@ -1767,6 +1785,33 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         }
     }
 
+    // device matrix jobs (any body, either group: they read only their input)
+    struct GeRef
+    {
+        const ProgramBody::PendingGe* g;
+        size_t inOff;
+    };
+    std::vector<GeDesc> gdescs;
+    std::vector<GeRef> grefs;
+    size_t geInBytes = 0;
+    for (int g = 0; g < 2; ++g)
+        for (size_t pi = 0; pi < bt.bodies[g].size(); ++pi) {
+            const ProgramBody* p = bt.bodies[g][pi];
+            for (size_t k = 0; k < p->nges; ++k) {
+                const ProgramBody::PendingGe& ge = p->ges[k];
+                GeDesc d;
+                d.in = (uint32_t)geInBytes;
+                d.result = ge.result + bt.resultBase[g][pi];
+                d.rows = ge.rows;
+                d.cols = ge.cols;
+                d.pickLen = ge.pickLen;
+                gdescs.push_back(d);
+                grefs.push_back(GeRef{&ge, geInBytes});
+                geInBytes = align16(geInBytes + ge.in.size());
+            }
+        }
+    bt.nGe = gdescs.size();
+
     constexpr size_t kIngestChunk = SGPU_INGEST_CHUNK;
     size_t nIngest = 0, stageBytes = 0, nIngBlocks = 0;
     std::vector<size_t> descBase, stageBase;
@@ -1811,6 +1856,10 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     off = align16(off + sitems.size() * sizeof(SolveItem));
     bt.oWide = off;
     off = align16(off + nWide * sizeof(LdpcItem));
+    bt.oGeD = off;
+    off = align16(off + gdescs.size() * sizeof(GeDesc));
+    bt.oGeIn = off;
+    off = align16(off + geInBytes);
     bt.upBytes = off;
     // SGPU_UPLOAD_STATS=1: one stderr line per flush, upload bytes by part (profiling aid)
     static const bool upStats = std::getenv("SGPU_UPLOAD_STATS") != nullptr;
@@ -1874,12 +1923,14 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     constexpr size_t kSolveChunk = SGPU_SOLVE_CHUNK;
     struct Task
     {
-        int kind;   // 0 = segments, 1 = ingest chunk, 2 = solves
+        int kind;   // 0 = segments, 1 = ingest chunk, 2 = solves, 3 = matrix jobs
         size_t a, b;
     };
     std::vector<Task> tasks;
     for (size_t i = 0; i < segs.size(); i += kSegChunk)
         tasks.push_back(Task{0, i, std::min(segs.size(), i + kSegChunk)});
+    for (size_t i = 0; i < grefs.size(); i += kSolveChunk)
+        tasks.push_back(Task{3, i, std::min(grefs.size(), i + kSolveChunk)});
     for (size_t i = 0; i < srefs.size(); i += kSolveChunk)
         tasks.push_back(Task{2, i, std::min(srefs.size(), i + kSolveChunk)});
     for (size_t qi = 0; qi < bt.queues.size(); ++qi)
@@ -1945,6 +1996,9 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 for (uint32_t tb = 0; tb < s.maxExtent; tb += kExecTileBytes)
                     items[n++] = ExecItem{r.wordBase, r.words, nOpsSeg, tb};
             }
+        } else if (t.kind == 3) {
+            for (size_t i = t.a; i < t.b; ++i)
+                std::memcpy(up + bt.oGeIn + grefs[i].inOff, grefs[i].g->in.data(), grefs[i].g->in.size());
         } else if (t.kind == 2) {
             for (size_t i = t.a; i < t.b; ++i) {
                 const SolveRef& r = srefs[i];
@@ -1976,6 +2030,8 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         std::memcpy(up + bt.oSD, sdescs.data(), sdescs.size() * sizeof(SolveDesc));
         std::memcpy(up + bt.oSI, sitems.data(), sitems.size() * sizeof(SolveItem));
     }
+    if (!gdescs.empty())
+        std::memcpy(up + bt.oGeD, gdescs.data(), gdescs.size() * sizeof(GeDesc));
 
     // download area: the byte counters (kAcctBytes), the solve results, then
     // each requested range
@@ -1989,7 +2045,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     ensure_down(xs, dOff);
 
     st.flushes = 1;
-    st.launches = phases.size() + (nIngest ? 1 : 0);
+    st.launches = phases.size() + (nIngest ? 1 : 0) + (gdescs.empty() ? 0 : 1);
     st.ops = nOps;
     st.terms = nTerms;
     st.solves = sdescs.size();
@@ -2029,6 +2085,8 @@ void Engine::launch_batch(Batch& bt)
     }
     if (bt.wideZero)
         be_memset(xs.wideDev, 0, xs.wideCap);
+    if (bt.nGe)
+        be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev);
     // k_ldpc items of every exec phase before the first solve go in one
     // launch (they read only window elements that exist before the flush's
     // first solve); a phase after a solve launches its own

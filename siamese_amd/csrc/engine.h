@@ -131,6 +131,15 @@ struct ProgramBody
         std::vector<SolveRow> rows;
         std::vector<uint8_t> coef;
     };
+    /// A device matrix generation + elimination (ops.h GeDesc): its input
+    /// as k_ge reads it and its first result word.
+    struct PendingGe
+    {
+        uint16_t rows = 0, cols = 0;
+        uint32_t pickLen = 0;
+        uint32_t result = 0;
+        std::vector<uint8_t> in;
+    };
 
     int group = 0;
     uint32_t resultWords = 0;   // result words reserved in this body
@@ -138,6 +147,8 @@ struct ProgramBody
     std::vector<Segment> segs;
     std::vector<PendingSolve> solves;   // solve k follows segment k (nsolves in use)
     size_t nsolves = 0;
+    std::vector<PendingGe> ges;         // independent of the segments (nges in use)
+    size_t nges = 0;
     std::vector<Completion> callbacks;
     RowsBuild rb;
     std::vector<CopyItem> copies;       // the open OP_COPIES batch (segment's last op)
@@ -174,8 +185,9 @@ struct ProgramBody
 
     bool empty() const
     {
-        return nsegs == 0 ||
-               (nsegs == 1 && segs[0].ops.empty() && copies.empty() && lcb.items.empty() && !rb.open);
+        return nges == 0 &&
+               (nsegs == 0 ||
+                (nsegs == 1 && segs[0].ops.empty() && copies.empty() && lcb.items.empty() && !rb.open));
     }
     void new_segment();
     void rows_open(uint32_t base, bool keepWindow);
@@ -244,6 +256,13 @@ public:
     /// Queue a triangular solve; returns the result-word index it will fill
     /// (valid in this program's completion callbacks of the flush that runs it).
     uint32_t solve(const std::vector<SolveRow>& rows, const uint8_t* coef, uint32_t maxBytes);
+
+    /// Queue a device matrix generation + elimination (ops.h GeDesc) of
+    /// rows x cols with a pick table of pickLen bytes: returns the job's
+    /// input buffer (ge_input_bytes, for the caller to fill before the next
+    /// flush) and *resultWord, its first result word (valid in this
+    /// program's completion callbacks).
+    uint8_t* ge_job(unsigned rows, unsigned cols, unsigned pickLen, uint32_t* resultWord);
 
     /// Run `fn(results)` once the flush holding this program's work completes.
     void on_complete(Completion fn);

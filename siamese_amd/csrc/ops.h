@@ -336,6 +336,76 @@ inline unsigned solve_tile_bytes(uint32_t m)
 {
     return m > kSolveWideMaxRows ? kSolveNarrowTileBytes : kTileBytes;
 }
+/// Recovery-matrix generation + Gaussian elimination of one decode on the
+/// device (k_ge; reference SiameseDecoder.cpp:2157-2531, the host's
+/// generate_matrix + gaussian_elimination).  A job is a FRESH matrix of
+/// `rows` recovery rows x `cols` lost columns (rows >= cols):
+///   input (16-byte aligned, at GeDesc.in in the upload):
+///     GeRow[rows], GeCol[cols], then pickLen bytes of pick columns: the
+///     matrix column of window element pickLo + x (0xff: received);
+///   output (GeDesc.result words of the result array, ge_result_words):
+///     [0] the first pivot whose column has no non-zero left (== cols: the
+///         matrix was eliminated), [1..2] the elimination's multiplied bytes
+///         (the reference's muladds, u64), [3] 0;
+///     then per row, bytes padded to words: pivots (u8 row index per pivot
+///     position), used (u8 0/1), column counts (u16); then the matrix, rows
+///     x cols bytes in row order.
+/// Row kinds: Siamese (dense over [0, jEnd) from the row's opcodes, then
+/// 2*ceil(ldpcN/16) PCG picks over [pickOff, pickOff + ldpcN)), Cauchy
+/// (1/((rbase) ^ ccol) over [0, jEnd)) and parity (1 over [0, jEnd)).
+struct GeDesc
+{
+    uint32_t in;        // byte offset of the job's input in the upload
+    uint32_t result;    // first result word
+    uint16_t rows, cols;
+    uint32_t pickLen;
+};
+
+enum : uint8_t
+{
+    GE_SIAMESE = 0,
+    GE_CAUCHY = 1,
+    GE_PARITY = 2
+};
+
+struct GeRow
+{
+    uint16_t row;        // Siamese row number (opcodes, RX) / unused
+    uint8_t kind;        // GE_*
+    uint8_t rbase;       // Cauchy: (uint8)(row - 1 + kCauchyMaxColumns)
+    uint16_t jEnd;       // dense columns [0, jEnd)
+    uint16_t colCount;   // the row's column count (RecoveryPacket lost count)
+    uint32_t ldpcN;      // Siamese: picks draw over ldpcN window elements
+    uint32_t pickOff;    // ... starting at this index of the pick table
+};
+
+struct GeCol
+{
+    uint8_t lane;        // column % kLanes
+    uint8_t cx, cx2;     // CX(column), CX(column)^2
+    uint8_t ccol;        // column % kCauchyMaxColumns
+};
+
+/// Device elimination limits (LDS-resident matrix of one workgroup).
+constexpr unsigned kGeMaxCols = 128;
+constexpr unsigned kGeMaxRows = 192;
+constexpr unsigned kGeMaxPick = 65535;
+constexpr uint8_t kGeNoColumn = 0xff;
+
+constexpr uint32_t ge_input_bytes(uint32_t rows, uint32_t cols, uint32_t pickLen)
+{
+    return (rows * 16u + cols * 4u + pickLen + 15u) & ~15u;
+}
+/// Word offsets of the output parts (ge_result_words: the total).
+constexpr uint32_t ge_out_pivots(uint32_t) { return 4; }
+constexpr uint32_t ge_out_used(uint32_t rows) { return 4 + (rows + 3) / 4; }
+constexpr uint32_t ge_out_counts(uint32_t rows) { return 4 + 2 * ((rows + 3) / 4); }
+constexpr uint32_t ge_out_matrix(uint32_t rows) { return ge_out_counts(rows) + (rows + 1) / 2; }
+constexpr uint32_t ge_result_words(uint32_t rows, uint32_t cols)
+{
+    return ge_out_matrix(rows) + (rows * cols + 3) / 4;
+}
+
 constexpr uint32_t kNoRows = 0xffffffffu;   // be_launch_exec: no OP_ROWS in the launch
 constexpr unsigned kExecTileBytes = 256;    // executor tiles: 64 lanes x 4 bytes
 

@@ -602,4 +602,123 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
     solve_main(solves, rows, coef, results, items, count, maxRows);
 }
 
+// k_ge: a fresh recovery matrix from its job (generation as the host's
+// generate_matrix, reference SiameseDecoder.cpp:2157-2383), then the
+// elimination without pivoting while the pivots allow it and with row
+// pivoting from the first zero pivot (:2423-2531), as the kernel runs it.
+void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results)
+{
+    for (uint32_t jb = 0; jb < count; ++jb) {
+        const GeDesc d = descs[jb];
+        const unsigned rows = d.rows, cols = d.cols;
+        const GeRow* R = reinterpret_cast<const GeRow*>(in + d.in);
+        const GeCol* C = reinterpret_cast<const GeCol*>(R + rows);
+        const uint8_t* pick = reinterpret_cast<const uint8_t*>(C + cols);
+        std::vector<uint8_t> M((size_t)rows * cols, 0);
+        for (unsigned r = 0; r < rows; ++r) {
+            const GeRow& g = R[r];
+            uint8_t* row = &M[(size_t)r * cols];
+            const uint8_t rx = row_value(g.row);
+            for (unsigned j = 0; j < g.jEnd && j < cols; ++j) {
+                if (g.kind == GE_PARITY) {
+                    row[j] = 1;
+                } else if (g.kind == GE_CAUCHY) {
+                    row[j] = gf_inv((uint8_t)(g.rbase ^ C[j].ccol));
+                } else {
+                    const unsigned op = row_opcode(C[j].lane, g.row);
+                    auto comb = [&](unsigned k) {
+                        return (uint8_t)((k & 1) ^ ((k & 2) ? C[j].cx : 0) ^ ((k & 4) ? C[j].cx2 : 0));
+                    };
+                    row[j] = (uint8_t)(comb(op & 7) ^ gf_mul(comb(op >> 3), rx));
+                }
+            }
+            if (g.kind != GE_SIAMESE || g.ldpcN == 0)
+                continue;
+            Pcg32 prng;
+            prng.seed(g.row, g.ldpcN);
+            const unsigned picks = 2 * ((g.ldpcN + kPairRate - 1) / kPairRate);
+            for (unsigned k = 0; k < picks; ++k) {
+                const uint8_t c = pick[g.pickOff + prng.next() % g.ldpcN];
+                if (c < cols)
+                    row[c] ^= (k & 1) ? rx : 1;
+            }
+        }
+        std::vector<uint8_t> piv(rows), used(rows, 0);
+        std::vector<uint16_t> cnt(rows);
+        for (unsigned i = 0; i < rows; ++i) {
+            piv[i] = (uint8_t)i;
+            cnt[i] = R[i].colCount;
+        }
+        uint64_t bytes = 0;
+        auto elim = [&](unsigned src, unsigned dst, unsigned p, unsigned end, uint8_t val) {
+            uint8_t* a = &M[(size_t)dst * cols];
+            const uint8_t* b = &M[(size_t)src * cols];
+            if (a[p] == 0)
+                return false;
+            const uint8_t y = gf_div(a[p], val);
+            a[p] = y;
+            if (end > p + 1) {
+                for (unsigned c = p + 1; c < end; ++c)
+                    a[c] ^= gf_mul(b[c], y);
+                bytes += end - p - 1;
+            }
+            return true;
+        };
+        unsigned p = 0;
+        for (; p < cols; ++p) {
+            const uint8_t val = M[(size_t)p * cols + p];
+            if (val == 0)
+                break;
+            used[p] = 1;
+            for (unsigned k = p + 1; k < rows; ++k)
+                elim(p, k, p, cnt[p], val);
+        }
+        unsigned stop = cols;
+        if (p < cols) {
+            unsigned j = p + 1;
+            for (unsigned pivot = p; pivot < cols; ++pivot) {
+                if (pivot != p)
+                    j = pivot;
+                while (j < rows && M[(size_t)piv[j] * cols + pivot] == 0)
+                    ++j;
+                if (j >= rows) {
+                    stop = pivot;
+                    break;
+                }
+                const unsigned rj = piv[j];
+                std::swap(piv[pivot], piv[j]);
+                used[rj] = 1;
+                const unsigned end = cnt[rj];
+                if (pivot >= cols - 1)
+                    break;
+                const uint8_t val = M[(size_t)rj * cols + pivot];
+                for (unsigned k = pivot + 1; k < rows; ++k) {
+                    const unsigned rk = piv[k];
+                    if (elim(rj, rk, pivot, end, val) && cnt[rk] < end)
+                        cnt[rk] = (uint16_t)end;
+                }
+            }
+        }
+        uint32_t* out = results + d.result;
+        out[0] = stop;
+        out[1] = (uint32_t)bytes;
+        out[2] = (uint32_t)(bytes >> 32);
+        out[3] = 0;
+        uint8_t* po = reinterpret_cast<uint8_t*>(out + ge_out_pivots(rows));
+        uint8_t* uo = reinterpret_cast<uint8_t*>(out + ge_out_used(rows));
+        uint16_t* co = reinterpret_cast<uint16_t*>(out + ge_out_counts(rows));
+        std::memset(po, 0, 4 * ((rows + 3) / 4));
+        std::memset(uo, 0, 4 * ((rows + 3) / 4));
+        std::memset(co, 0, 4 * ((rows + 1) / 2));
+        for (unsigned i = 0; i < rows; ++i) {
+            po[i] = piv[i];
+            uo[i] = used[i];
+            co[i] = cnt[i];
+        }
+        uint8_t* mo = reinterpret_cast<uint8_t*>(out + ge_out_matrix(rows));
+        std::memset(mo, 0, 4 * ((rows * cols + 3) / 4));
+        std::memcpy(mo, M.data(), M.size());
+    }
+}
+
 } // namespace sgpu

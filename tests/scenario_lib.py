@@ -79,7 +79,8 @@ class BatchOptions(ctypes.Structure):
                 ("verify", ctypes.c_uint32), ("device", ctypes.c_int32),
                 ("threads", ctypes.c_uint32), ("groups", ctypes.c_uint32),
                 ("e2e", ctypes.c_uint32), ("digest", ctypes.c_uint32), ("defer", ctypes.c_uint32),
-                ("frames", ctypes.c_uint32), ("no_timing", ctypes.c_uint32)]
+                ("frames", ctypes.c_uint32), ("no_timing", ctypes.c_uint32),
+                ("device_ge", ctypes.c_uint32)]
 
 
 class BatchReport(ctypes.Structure):
@@ -88,9 +89,9 @@ class BatchReport(ctypes.Structure):
                 ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 17),
                 ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64),
                 ("phase_seconds", ctypes.c_double * 5), ("payload_bytes", ctypes.c_uint64),
-                ("kernel_ms", ctypes.c_double * 4)]
+                ("kernel_ms", ctypes.c_double * 5)]
 
-KERNELS = ("k_ingest", "k_exec", "k_ldpc", "k_solve")
+KERNELS = ("k_ingest", "k_exec", "k_ldpc", "k_solve", "k_ge")
 
 PHASES = ("create", "step", "flush", "resolve", "finish")
 
@@ -133,7 +134,7 @@ def run_capi(library, cfg, threads=1, event_log=None):
 
 
 def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0, groups=1,
-              e2e=False, defer=0, frames=False):
+              e2e=False, defer=0, frames=False, device_ge=False):
     """Run `cfg` through the device-resident batch API (lock-step rounds),
     streams driven by `threads` host threads (0 = library default), split
     into `groups` groups whose host work and device work alternate.  With
@@ -141,12 +142,14 @@ def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0
     recovery packet and recovered original is copied back.  defer=k > 0: the
     deferred-output API, a stream yields after every k-th decode and a group
     keeps up to two submissions in flight.  frames (with e2e): packets travel
-    as framed datagrams (sgpu_frames_recv / sgpu_frames_send).
+    as framed datagrams (sgpu_frames_recv / sgpu_frames_send).  device_ge
+    (defer=0): decodes by sgpu_decode_device (the recovery matrix generated
+    and eliminated on the device).
 
     Returns (results of the last run, BatchReport)."""
     res = (StreamResult * cfg.streams)()
     opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads, groups, 1 if e2e else 0, 1, defer,
-                       1 if frames else 0)
+                       1 if frames else 0, 0, 1 if device_ge else 0)
     rep = BatchReport()
     rc = lib().scenario_run_batch(library.encode(), ctypes.byref(cfg), res, ctypes.byref(opt),
                                   ctypes.byref(rep))
@@ -182,13 +185,14 @@ class BatchSession:
             raise RuntimeError("scenario_batch_open(%s) failed" % library)
 
     def run(self, steps=1, warmup=0, verify=False, threads=0, groups=1, e2e=False, digest=True, defer=0,
-            frames=False, timing=True):
+            frames=False, timing=True, device_ge=False):
         """digest=False: timed runs skip the per-stream event logs (results
-        then carry no digest; take it from a verified run)."""
+        then carry no digest; take it from a verified run).  device_ge (with
+        defer=0): decodes by sgpu_decode_device."""
         res = (StreamResult * self.cfg.streams)()
         opt = BatchOptions(steps, warmup, 1 if verify else 0, -1, threads, groups,
                            1 if e2e else 0, 1 if digest else 0, defer, 1 if frames else 0,
-                           0 if timing else 1)
+                           0 if timing else 1, 1 if device_ge else 0)
         rep = BatchReport()
         rc = lib().scenario_batch_run(self.handle, res, ctypes.byref(opt), ctypes.byref(rep))
         if rc != 0:

@@ -1,0 +1,56 @@
+"""Recovery matrix on the device (sgpu_decode_device, kernel k_ge): CPU
+parity through the backend's CPU test double (tests/hostsim, never shipped).
+
+A decode that starts a fresh elimination queues the matrix job and returns
+SGPU_DECODE_PENDING; the call after the flush finishes it.  The harness logs
+one EV_DECODE per decode, so the event digests must be the reference's
+exactly, and the algorithmic bytes (the elimination's multiplies are counted
+by the job) those of the host elimination.  The same checks run on the
+MI355X in test_gpu_parity.py.
+"""
+import pytest
+
+import golden
+import scenario_lib as S
+from test_parity_cpu import SMALL, _check
+
+
+@pytest.mark.parametrize("name", SMALL + ["C2x64"])
+def test_device_ge_matches_golden(name):
+    cfg = golden.config(name)
+    res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True, device_ge=True)
+    _check(name, res)
+    assert rep.mismatches == 0
+
+
+@pytest.mark.parametrize("name", ["C2x64", "C1var", "smoke_C4x8", "edge_maxloss", "edge_heavy"])
+@pytest.mark.parametrize("threads,groups", [(4, 2), (8, 3)])
+def test_device_ge_threads_and_pipelining(name, threads, groups):
+    cfg = golden.config(name)
+    res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True, threads=threads, groups=groups, device_ge=True)
+    _check(name, res)
+    assert rep.mismatches == 0
+
+
+@pytest.mark.parametrize("name,jobs", [("smoke_C4x8", True), ("C2x64", True), ("C1var", True),
+                                       ("edge_lag", True), ("edge_maxloss", False)])
+def test_device_ge_accounting_and_launches(name, jobs):
+    """Same algorithmic bytes as the host elimination; the jobs ran (one more
+    launch per flush that carried any).  edge_maxloss's decodes exceed the
+    kernel's 128 columns: they stay on the host."""
+    cfg = golden.config(name)
+    _, rep0 = S.run_batch(S.SIM_LIB, cfg, verify=True)
+    _, rep1 = S.run_batch(S.SIM_LIB, cfg, verify=True, device_ge=True)
+    e0, e1 = S.engine_dict(rep0), S.engine_dict(rep1)
+    assert e1["ref_op_bytes"] == e0["ref_op_bytes"]
+    assert e1["out_bytes"] == e0["out_bytes"]
+    assert (e1["launches"] > e0["launches"]) == jobs
+
+
+def test_device_ge_headline_shard_slice():
+    """A slice of the bench workload (C4 block mode, hashed) in range mode."""
+    cfg = S.replace(golden.config("C4x1024hr"), streams=96)
+    ref = golden.load("C4x1024hr")
+    res, rep = S.run_batch(S.SIM_LIB, cfg, verify=True, threads=4, groups=2, device_ge=True)
+    assert S.digests(res) == ref["digests"][:96]
+    assert rep.mismatches == 0

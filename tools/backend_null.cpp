@@ -142,4 +142,25 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
     solve_main(solves, rows, coef, results, items, count, maxRows);
 }
 
+// matrix jobs: every one reports an eliminated matrix with identity pivots,
+// its first `cols` rows used and zero coefficients (no elimination on the host)
+void be_launch_ge(const GeDesc* descs, const uint8_t*, uint32_t count, uint32_t* results)
+{
+    const GeDesc* dd = host_view(descs);
+    for (uint32_t j = 0; j < count; ++j) {
+        const GeDesc d = dd[j];
+        uint32_t* out = results + d.result;
+        std::memset(out, 0, (size_t)ge_result_words(d.rows, d.cols) * 4);
+        out[0] = d.cols;
+        uint8_t* po = reinterpret_cast<uint8_t*>(out + ge_out_pivots(d.rows));
+        uint8_t* uo = reinterpret_cast<uint8_t*>(out + ge_out_used(d.rows));
+        uint16_t* co = reinterpret_cast<uint16_t*>(out + ge_out_counts(d.rows));
+        for (unsigned i = 0; i < d.rows; ++i) {
+            po[i] = (uint8_t)i;
+            uo[i] = i < d.cols;
+            co[i] = (uint16_t)d.cols;
+        }
+    }
+}
+
 } // namespace sgpu
