@@ -2672,6 +2672,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
     // rows (a row of T is m <= 120 bytes: one half-wave, four bytes a lane)
     constexpr uint32_t kHalves = kMfmaThreads / 32;
     const uint32_t hw = tid >> 5, l32 = tid & 31;
+#ifndef SGPU_MFMA_SKIP_T
     for (uint32_t i = 0; i + 1 < m; ++i) {
         const uint32_t src = Yw[i * 32 + l32];
         for (uint32_t j = i + 1 + hw; j < m; j += kHalves) {
@@ -2694,6 +2695,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
         const uint32_t i = k >> 5;
         Yw[k] = gf_mul_tab(Yw[k], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]]));
     }
+#endif
     __syncthreads();
 
     // 2. X = T R, 64 columns at a time
@@ -2725,6 +2727,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
         }
         __syncthreads();
         const uint32_t r = lane & 31, h = lane >> 5;
+#ifndef SGPU_MFMA_SKIP_MMA
         for (uint32_t mt = wave; mt < mp / 4; mt += kMfmaWaves) {
             // rows 4 mt .. 4 mt + 3 of X: lane's A row is output bit b of row i
             const uint32_t i = 4 * mt + (r >> 3), b = 7 - (r & 7);
@@ -2757,6 +2760,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
                         outT[(4 * mt + g) * kMfmaChunk + t * 32 + r] = (uint8_t)byte;
                 }
         }
+#endif
         __syncthreads();
         // x masked past the recovered length, stored below the row's final
         // bytes (the stores of the exact back-substitution)

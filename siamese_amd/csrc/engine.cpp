@@ -703,14 +703,25 @@ void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t 
     // (a row whose cutoff is below an earlier row's reads sums folded past
     // its own cutoff: it starts a batch after every update so far; a
     // versioned batch takes at most kVersionRows rows)
-    if ((b.haveSums && std::memcmp(b.sums, sums, sizeof(b.sums)) != 0) || cutoff < b.cutMax ||
-        (b.versioned && b.rows.size() >= kVersionRows))
+    // The batch's sums table: entries an earlier row read must be this row's
+    // too; an entry no row has read yet takes this row's value (a sum brought
+    // up to date for this row: its update joined the batch, and the rows
+    // before do not read it), so consecutive rows over one window share a
+    // batch while the sums fill in.
+    bool same = true;
+    if (b.haveSums)
+        for (uint32_t r = b.readMask; r; r &= r - 1) {
+            const unsigned k = (unsigned)__builtin_ctz(r);
+            if (std::memcmp(&b.sums[k], &sums[k], sizeof(WinEntry)) != 0) {
+                same = false;
+                break;
+            }
+        }
+    if (!same || cutoff < b.cutMax || (b.versioned && b.rows.size() >= kVersionRows))
         rows_open(b.base, true);
     b.cutMax = std::max(b.cutMax, cutoff);
-    if (!b.haveSums) {
-        std::memcpy(b.sums, sums, sizeof(b.sums));
-        b.haveSums = true;
-    }
+    std::memcpy(b.sums, sums, sizeof(b.sums));
+    b.haveSums = true;
     RowItem r;
     std::memset(&r, 0, sizeof(r));
     r.dst = dst;
