@@ -2124,9 +2124,7 @@ __device__ __forceinline__ void prefix_load(uint32_t (&p4)[4], uint32_t m, uint3
 #define SGPU_SOLVE_WAVES 8
 #endif
 constexpr unsigned kSolveWaves = SGPU_SOLVE_WAVES;
-constexpr unsigned kMfmaMaxRows = 120;       // k_solve_mfma takes solves of up to this many rows
 constexpr unsigned kSolveLdsMaxRows = 255;   // kMaximumLossRecoveryCount (SiameseCommon.h:80)
-constexpr unsigned kSolvePrefixSplit = 16;   // solves per launch from which the prefix pass is its own launch
 
 // LDS bytes of the staged solve: row tiles, the transposed coefficient
 // matrix, per-row lengths and the result words.
@@ -2493,7 +2491,7 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     // flags bit 0: k_solve_prefix already solved the length prefixes; bit 1:
     // k_solve_mfma ran before this launch and took every solve it could
     const bool prefixDone = (flags & 1u) != 0;
-    if ((flags & 2u) && m <= kMfmaMaxRows && results[sd.result] == m)
+    if ((flags & 2u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m)
         return;
     const uint32_t* resIn = prefixDone ? results + sd.result : nullptr;
     uint32_t* out = (!prefixDone && it.tileBase == 0) ? results + sd.result : nullptr;
@@ -2570,7 +2568,7 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// Bulk solve on the matrix cores (k_solve_mfma)
+// Bulk solve on the matrix cores (k_solve_pre + k_solve_mfma)
 //
 // The solve's result rows are X = T R, with T = U^-1 L^-1 the m x m inverse
 // of the eliminated coefficient matrix (MultiplyLowerTriangle applies L^-1,
@@ -2582,15 +2580,23 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 // int8 MFMA v_mfma_i32_32x32x32_i8 computes 32 output bits x 32 columns over
 // 32 input bits (four input rows) per instruction, exactly.
 //
-// One workgroup per (solve, column half):
-//   1. T in LDS: the reference's two sweeps applied to the identity (rows of
-//      m bytes, one half-wave per row update);
-//   2. per 64-column chunk: the rows' bytes expanded to 0/1 bytes in LDS
-//      (the B operand, laid out so a lane's 16-byte fragment is one
-//      ds_read_b128), then each wave takes 32 output bits (four rows) and
-//      runs the K loop, its A fragments built from T and the multiply-by-y
-//      bit matrices (c_aff), and packs the parities back to bytes.
-// It runs only when k_solve_prefix found every recovered length valid
+// k_solve_pre (one launch, two kinds of workgroup):
+//   workgroups [0, n): the length-prefix pass of solve b (all waves stage the
+//   coefficients, then wave 0 runs solve_prefix_wave);
+//   workgroups [n, 2n): T of solve b - n, the reference's two sweeps applied
+//   to the identity in LDS (rows of m <= 120 bytes, one half-wave a row),
+//   written to the solve's scratch (SolveDesc.tinv, rows of kTStride bytes).
+// The two kinds run side by side, so T costs no time on the prefix pass's
+// serial critical path.
+//
+// k_solve_mfma: one workgroup per (solve, 32 output rows); wave w computes
+// output rows 4w..4w+3 of its group, its A operands read from the group's
+// bit-matrix table AF (8 bytes per T coefficient: c_aff, the multiply-by-y
+// bit matrix) one 16-bit LDS read per K step.  Per 64-column chunk: the rows'
+// bytes are expanded to 0/1 bytes in LDS (the B operand, laid out so a
+// lane's 16-byte fragment is one ds_read_b128), each wave runs its K loop,
+// the parities are packed back to bytes and stored.
+// It runs only when the prefix pass found every recovered length valid
 // (results[0] == m): the exact sweeps and the prefixes then agree byte for
 // byte, since bytes past a row's length are zero in the true originals (the
 // clips of the sequential sweeps change nothing).  A solve with a corrupt
@@ -2598,67 +2604,53 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 // reference's partial back-substitution exactly.
 constexpr unsigned kMfmaWaves = 8;
 constexpr unsigned kMfmaThreads = 64 * kMfmaWaves;
-constexpr unsigned kMfmaYStride = 128;                 // bytes per row of T in LDS
+constexpr unsigned kMfmaYStride = kTStride;            // bytes per row of T in LDS
 constexpr unsigned kMfmaTiles = 2;                     // 32-column MFMA tiles per chunk
 constexpr unsigned kMfmaChunk = 32 * kMfmaTiles;       // columns per chunk
-constexpr unsigned kMfmaSplit = 2;                     // workgroups per solve (column ranges)
+constexpr unsigned kMfmaGroupRows = 4 * kMfmaWaves;    // output rows per workgroup
+constexpr unsigned kMfmaGroups = (kMfmaMaxRows + kMfmaGroupRows - 1) / kMfmaGroupRows;
 
-__constant__ uint8_t c_aff[256][8];   // [y][7 - b]: bit k = bit b of y * 2^k (GF2P8AFFINEQB rows)
+__constant__ __attribute__((aligned(16))) uint8_t c_aff[256][8];   // [y][7 - b]: bit k = bit b of y * 2^k (GF2P8AFFINEQB rows)
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 __host__ __device__ constexpr uint32_t mfma_rows(uint32_t m) { return (m + 3u) & ~3u; }
+// k_solve_pre: the larger of the prefix pass's staging and the T build's
+__host__ __device__ constexpr uint32_t solve_tbuild_lds_bytes(uint32_t m)
+{
+    return ((m * m + 15u) & ~15u) + mfma_rows(m) * kMfmaYStride + 256u * 20u;
+}
+__host__ __device__ constexpr uint32_t solve_pre_lds_bytes(uint32_t m)
+{
+    return solve_prefix_lds_bytes(m) > solve_tbuild_lds_bytes(m < kMfmaMaxRows ? m : kMfmaMaxRows)
+               ? solve_prefix_lds_bytes(m)
+               : solve_tbuild_lds_bytes(m < kMfmaMaxRows ? m : kMfmaMaxRows);
+}
+// k_solve_mfma: the group's bit-matrix table, the B operand, the packed
+// outputs, the rows' lengths
 __host__ __device__ constexpr uint32_t solve_mfma_lds_bytes(uint32_t m)
 {
-    return ((m * m + 15u) & ~15u) + mfma_rows(m) * kMfmaYStride + 256u * 16u + 256u * 4u + 256u * 8u +
-           ((3u * m * 4u + 15u) & ~15u) + mfma_rows(m) * 8u * kMfmaChunk + mfma_rows(m) * kMfmaChunk;
+    return kMfmaGroupRows * 8u * mfma_rows(m) + mfma_rows(m) * 8u * kMfmaChunk + kMfmaGroupRows * kMfmaChunk +
+           ((3u * m * 4u + 15u) & ~15u);
 }
 
 // the four low bits of v as four 0/1 bytes (byte q = bit q)
 __device__ __forceinline__ uint32_t bits4(uint32_t v) { return ((v & 15u) * 0x00204081u) & 0x01010101u; }
 
-__global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __restrict__ solves,
-                                                           const SolveRow* __restrict__ rows,
-                                                           const uint8_t* __restrict__ coef,
-                                                           const uint32_t* __restrict__ results)
+// T = U^-1 L^-1 of solve sd into sd.tinv (all waves of the workgroup)
+__device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C, uint8_t* base, uint32_t tid)
 {
-    extern __shared__ uint4 Ls[];
-    const uint32_t part = blockIdx.x % kMfmaSplit;
-    const SolveDesc sd = solves[blockIdx.x / kMfmaSplit];
-    const uint32_t m = sd.m;
-    if (m == 0 || m > kMfmaMaxRows || results[sd.result] != m)
-        return;   // (uniform: k_solve_main solves it)
-    const SolveRow* R = rows + sd.rowBegin;
-    const uint8_t* C = coef + sd.coefOffset;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t mp = mfma_rows(m);
-
-    uint8_t* base = reinterpret_cast<uint8_t*>(Ls);
+    const uint32_t m = sd.m, mp = mfma_rows(m);
     uint8_t* Ct = base;                                          // Ct[i*m + j] = C[j][i]
     uint8_t* Y = Ct + ((m * m + 15u) & ~15u);                    // T, rows of kMfmaYStride bytes
     uint4* permL = reinterpret_cast<uint4*>(Y + mp * kMfmaYStride);
     uint32_t* permC = reinterpret_cast<uint32_t*>(permL + 256);
-    uint8_t* aff = reinterpret_cast<uint8_t*>(permC + 256);
-    uint32_t* initB = reinterpret_cast<uint32_t*>(aff + 2048);
-    uint32_t* finB = initB + m;
-    uint32_t* bbB = finB + m;                                    // recovered header + length
-    uint8_t* bits = reinterpret_cast<uint8_t*>(initB) + ((3u * m * 4u + 15u) & ~15u);
-    uint8_t* outT = bits + mp * 8u * kMfmaChunk;
-
     stage_transposed<kMfmaThreads, 2>(Ct, C, m, tid);
     if (tid < 256) {
         const uint32_t* t = c_perm[tid];
         permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
         permC[tid] = t[4];
-    }
-    for (uint32_t k = tid; k < 512; k += kMfmaThreads)
-        reinterpret_cast<uint32_t*>(aff)[k] = reinterpret_cast<const uint32_t*>(c_aff)[k];
-    for (uint32_t j = tid; j < m; j += kMfmaThreads) {
-        initB[j] = R[j].initBytes;
-        finB[j] = R[j].finalBytes;
-        const uint32_t w = results[sd.result + 1 + j];
-        bbB[j] = (w >> 29) + (w & kSolveLengthMask);
     }
     // T starts as the identity (rows past m stay zero)
     uint32_t* Yw = reinterpret_cast<uint32_t*>(Y);
@@ -2667,12 +2659,10 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
         Yw[k] = (i < m && i >= c4 && i < c4 + 4) ? 1u << (8 * (i - c4)) : 0u;
     }
     __syncthreads();
-
-    // 1. T: MultiplyLowerTriangle, then BackSubstitution, on the identity's
-    // rows (a row of T is m <= 120 bytes: one half-wave, four bytes a lane)
+    // MultiplyLowerTriangle, then BackSubstitution, on the identity's rows (a
+    // row of T is m <= 120 bytes: one half-wave, four bytes a lane)
     constexpr uint32_t kHalves = kMfmaThreads / 32;
     const uint32_t hw = tid >> 5, l32 = tid & 31;
-#ifndef SGPU_MFMA_SKIP_T
     for (uint32_t i = 0; i + 1 < m; ++i) {
         const uint32_t src = Yw[i * 32 + l32];
         for (uint32_t j = i + 1 + hw; j < m; j += kHalves) {
@@ -2691,20 +2681,110 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
         }
         __syncthreads();
     }
-    for (uint32_t k = tid; k < m * 32u; k += kMfmaThreads) {
+    GMEM uint32_t* out = reinterpret_cast<GMEM uint32_t*>(sd.tinv);
+    for (uint32_t k = tid; k < mp * 32u; k += kMfmaThreads) {
         const uint32_t i = k >> 5;
-        Yw[k] = gf_mul_tab(Yw[k], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]]));
+        out[k] = i < m ? gf_mul_tab(Yw[k], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]])) : 0u;
     }
-#endif
+}
+
+__global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __restrict__ solves,
+                                                          const SolveRow* __restrict__ rows,
+                                                          const uint8_t* __restrict__ coef,
+                                                          uint32_t* __restrict__ results,
+                                                          unsigned long long* __restrict__ acct,
+                                                          uint32_t count)
+{
+    extern __shared__ uint4 X[];
+    const uint32_t tid = threadIdx.x;
+    if (blockIdx.x >= count) {
+        const SolveDesc sd = solves[blockIdx.x - count];
+        if (sd.m == 0 || sd.m > kMfmaMaxRows || sd.tinv == 0)
+            return;   // (uniform)
+        solve_tbuild(sd, coef + sd.coefOffset, reinterpret_cast<uint8_t*>(X), tid);
+        return;
+    }
+    const SolveDesc sd = solves[blockIdx.x];
+    const uint32_t m = sd.m;
+    if (m > kSolveLdsMaxRows)
+        return;
+    const SolveRow* R = rows + sd.rowBegin;
+    const uint8_t* C = coef + sd.coefOffset;
+    uint4* permL = X;
+    uint32_t* permC = reinterpret_cast<uint32_t*>(permL + 256);
+    uint8_t* Ct = reinterpret_cast<uint8_t*>(permC + 256);
+    uint32_t* lowL = reinterpret_cast<uint32_t*>(Ct + ((m * m + 15u) & ~15u));
+    uint32_t* finB = lowL + m;
+    uint32_t* rw = finB + m;
+    uint32_t p4[4];
+    if (tid < 64)
+        prefix_load(p4, m, tid, sd.head, R);
+    if (tid < 256) {
+        const uint32_t* t = c_perm[tid];
+        permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
+        permC[tid] = t[4];
+    }
+    // (every wave stages; then wave 0 alone runs the serial pass)
+    stage_transposed<kMfmaThreads, 2>(Ct, C, m, tid);
+    for (uint32_t j = tid; j < m; j += kMfmaThreads) {
+        lowL[j] = R[j].lowerLen;
+        finB[j] = R[j].finalBytes;
+    }
+    __syncthreads();
+    if (tid >= 64)
+        return;
+    solve_prefix_wave(m, tid, p4, Ct, lowL, finB, permL, permC, rw, results + sd.result, acct);
+}
+
+__global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __restrict__ solves,
+                                                           const SolveRow* __restrict__ rows,
+                                                           const uint32_t* __restrict__ results)
+{
+    extern __shared__ uint4 Ls[];
+    const uint32_t grp = blockIdx.x % kMfmaGroups;
+    const SolveDesc sd = solves[blockIdx.x / kMfmaGroups];
+    const uint32_t m = sd.m, mp = mfma_rows(m);
+    if (m == 0 || m > kMfmaMaxRows || sd.tinv == 0 || grp * kMfmaGroupRows >= mp || results[sd.result] != m)
+        return;   // (uniform: k_solve_main solves it, or another group has these rows)
+    const SolveRow* R = rows + sd.rowBegin;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t row0 = grp * kMfmaGroupRows;
+
+    uint8_t* AF = reinterpret_cast<uint8_t*>(Ls);                // [il][q][j]: c_aff[T[row0+il][j]][q]
+    uint8_t* bits = AF + kMfmaGroupRows * 8u * mp;
+    uint8_t* outT = bits + mp * 8u * kMfmaChunk;
+    uint32_t* initB = reinterpret_cast<uint32_t*>(outT + kMfmaGroupRows * kMfmaChunk);
+    uint32_t* finB = initB + m;
+    uint32_t* bbB = finB + m;                                    // recovered header + length
+
+    const GMEM uint8_t* T = reinterpret_cast<const GMEM uint8_t*>(sd.tinv);
+    for (uint32_t x = tid; x < kMfmaGroupRows * mp; x += kMfmaThreads) {
+        const uint32_t il = x / mp, j = x - il * mp;
+        const uint32_t i = row0 + il;
+        const uint32_t y = (i < m && j < m) ? T[i * kMfmaYStride + j] : 0u;
+        const uint2 a = *reinterpret_cast<const uint2*>(c_aff[y]);
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q)
+            AF[(il * 8u + q) * mp + j] = (uint8_t)((q < 4 ? a.x : a.y) >> (8 * (q & 3)));
+    }
+    for (uint32_t j = tid; j < m; j += kMfmaThreads) {
+        initB[j] = R[j].initBytes;
+        finB[j] = R[j].finalBytes;
+        const uint32_t w = results[sd.result + 1 + j];
+        bbB[j] = (w >> 29) + (w & kSolveLengthMask);
+    }
     __syncthreads();
 
-    // 2. X = T R, 64 columns at a time
     const uint32_t S = mp / 4;   // K steps (four input rows = 32 input bits each)
     uint32_t maxB = 0;
     for (uint32_t j = 0; j < m; ++j)
         maxB = finB[j] > maxB ? finB[j] : maxB;
-    for (uint32_t ch = part; ch * kMfmaChunk < maxB; ch += kMfmaSplit) {
-        const uint32_t c0 = ch * kMfmaChunk;
+    const uint32_t r = lane & 31, h = lane >> 5;
+    // lane's A row: output bit 7 - (r & 7) of row row0 + 4 wave + r / 8
+    const uint8_t* af = AF + ((4u * wave + (r >> 3)) * 8u + (7u - (r & 7u))) * mp + 2u * h;
+    const bool active = row0 + 4u * wave < mp;
+    const uint32_t rowsHere = (m - row0 < kMfmaGroupRows ? m - row0 : kMfmaGroupRows);
+    for (uint32_t c0 = 0; c0 < maxB; c0 += kMfmaChunk) {
         // the B operand: byte (j, col) as eight 0/1 bytes at
         // bits[((t * S + j / 4) * 32 + col % 32) * 32 + (j % 4) * 8], t = col / 32
         for (uint32_t it = tid; it < mp * (kMfmaChunk / 4); it += kMfmaThreads) {
@@ -2726,20 +2806,15 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
             }
         }
         __syncthreads();
-        const uint32_t r = lane & 31, h = lane >> 5;
-#ifndef SGPU_MFMA_SKIP_MMA
-        for (uint32_t mt = wave; mt < mp / 4; mt += kMfmaWaves) {
-            // rows 4 mt .. 4 mt + 3 of X: lane's A row is output bit b of row i
-            const uint32_t i = 4 * mt + (r >> 3), b = 7 - (r & 7);
-            const uint8_t* ty = Y + i * kMfmaYStride + 2 * h;
+        if (active) {
             i32x16 acc[kMfmaTiles];
 #pragma unroll
             for (uint32_t t = 0; t < kMfmaTiles; ++t)
                 acc[t] = i32x16{};
             for (uint32_t s = 0; s < S; ++s) {
                 // A[r][16 h + jj]: bit b of T[i][4 s + 2 h + jj / 8] * 2^(jj % 8)
-                const uint32_t a1 = aff[ty[4 * s] * 8u + b], a2 = aff[ty[4 * s + 1] * 8u + b];
-                const i32x4 A = {(int)bits4(a1), (int)bits4(a1 >> 4), (int)bits4(a2), (int)bits4(a2 >> 4)};
+                const uint32_t u = *reinterpret_cast<const uint16_t*>(af + 4u * s);
+                const i32x4 A = {(int)bits4(u), (int)bits4(u >> 4), (int)bits4(u >> 8), (int)bits4(u >> 12)};
 #pragma unroll
                 for (uint32_t t = 0; t < kMfmaTiles; ++t) {
                     const i32x4 B = *reinterpret_cast<const i32x4*>(bits + ((t * S + s) * 32 + r) * 32 + h * 16);
@@ -2747,7 +2822,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
                 }
             }
             // D[row][col]: row = (reg & 3) + 8 (reg >> 2) + 4 h, col = r; row
-            // 8 g + 4 h + q is bit 4 h + q of X row 4 mt + g
+            // 8 g + 4 h + q is bit 4 h + q of output row 4 wave + g (local)
 #pragma unroll
             for (uint32_t t = 0; t < kMfmaTiles; ++t)
 #pragma unroll
@@ -2757,23 +2832,21 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
                     const uint32_t v = nib << (4 * h);
                     const uint32_t byte = v | (uint32_t)__shfl_xor((int)v, 32);
                     if (h == 0)
-                        outT[(4 * mt + g) * kMfmaChunk + t * 32 + r] = (uint8_t)byte;
+                        outT[(4 * wave + g) * kMfmaChunk + t * 32 + r] = (uint8_t)byte;
                 }
         }
-#endif
         __syncthreads();
         // x masked past the recovered length, stored below the row's final
         // bytes (the stores of the exact back-substitution)
-        for (uint32_t it = tid; it < m * (kMfmaChunk / 16); it += kMfmaThreads) {
-            const uint32_t i = it / (kMfmaChunk / 16), u = it % (kMfmaChunk / 16);
-            const uint32_t p = c0 + 16 * u;
+        for (uint32_t it = tid; it < rowsHere * (kMfmaChunk / 16); it += kMfmaThreads) {
+            const uint32_t il = it / (kMfmaChunk / 16), u = it % (kMfmaChunk / 16);
+            const uint32_t i = row0 + il, p = c0 + 16 * u;
             if (p < finB[i]) {
-                uint4 v = *reinterpret_cast<const uint4*>(outT + i * kMfmaChunk + 16 * u);
+                uint4 v = *reinterpret_cast<const uint4*>(outT + il * kMfmaChunk + 16 * u);
                 v = mask16(v, (int)bbB[i] - (int)p);
                 st16(R[i].buf + p, v);
             }
         }
-        __syncthreads();
     }
 }
 
@@ -3282,6 +3355,11 @@ bool be_init(int device, const char** err)
         *err = "the device refused the matrix-core solve's LDS";
         return false;
     }
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_pre), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)solve_pre_lds_bytes(kSolveLdsMaxRows)) != hipSuccess) {
+        *err = "the device refused the solve pre-pass's LDS";
+        return false;
+    }
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_prefix),
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)solve_prefix_lds_bytes(kSolveLdsMaxRows)) != hipSuccess) {
@@ -3522,21 +3600,26 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
     // in parallel); few (single-stream flushes): fused into the tiles, one
     // launch fewer on the flush's critical path.
     const bool separate = solveCount >= kSolvePrefixSplit;
-    if (separate)
-        hipLaunchKernelGGL(k_solve_prefix, dim3(solveCount), dim3(64), (size_t)solve_prefix_lds_bytes(rowsCap),
-                           g_stream, solves + solveBegin, rows, coef, results,
-                           reinterpret_cast<unsigned long long*>(acct));
-    // the solves whose lengths all came out valid on the matrix cores
-    // (SGPU_MFMA_SOLVE=0: every solve by the sweeps, A/B aid)
+    // the solves whose lengths all come out valid on the matrix cores
+    // (SGPU_MFMA_SOLVE=0: every solve by the sweeps, A/B aid): the prefix
+    // pass and the solves' inverses in one launch, then the products
     static const bool kMfmaSolve = [] {
         const char* v = std::getenv("SGPU_MFMA_SOLVE");
         return !v || std::atoi(v) != 0;
     }();
     const bool mfma = separate && kMfmaSolve;
-    if (mfma)
-        hipLaunchKernelGGL(k_solve_mfma, dim3(solveCount * kMfmaSplit), dim3(kMfmaThreads),
+    if (mfma) {
+        hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
+                           g_stream, solves + solveBegin, rows, coef, results,
+                           reinterpret_cast<unsigned long long*>(acct), solveCount);
+        hipLaunchKernelGGL(k_solve_mfma, dim3(solveCount * kMfmaGroups), dim3(kMfmaThreads),
                            (size_t)solve_mfma_lds_bytes(rowsCap < kMfmaMaxRows ? rowsCap : kMfmaMaxRows), g_stream,
-                           solves + solveBegin, rows, coef, results);
+                           solves + solveBegin, rows, results);
+    } else if (separate) {
+        hipLaunchKernelGGL(k_solve_prefix, dim3(solveCount), dim3(64), (size_t)solve_prefix_lds_bytes(rowsCap),
+                           g_stream, solves + solveBegin, rows, coef, results,
+                           reinterpret_cast<unsigned long long*>(acct));
+    }
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
                        (size_t)solve_launch_lds_bytes(rowsCap, !separate), g_stream, solves, rows, coef, results,
                        items, reinterpret_cast<unsigned long long*>(acct), (separate ? 1u : 0u) | (mfma ? 2u : 0u));

@@ -1435,7 +1435,7 @@ bool async_assembly()
 {
     static const bool v = [] {
         const char* e = std::getenv("SIAMESE_AMD_ASYNC_ASSEMBLY");
-        return e && std::atoi(e) != 0;
+        return !e || std::atoi(e) != 0;
     }();
     return v;
 }
@@ -1452,12 +1452,11 @@ uint64_t Engine::enqueue()
         return nextTicket_;   // nothing queued: the latest submission covers everything
     const uint64_t ticket = b->ticket;
     const uint64_t tq1 = now_ns();
-    // The batch is laid out here, on the caller's thread and the shared
-    // pool.  SIAMESE_AMD_ASYNC_ASSEMBLY=1 hands it to the launcher thread and
-    // its own pool instead, so the caller goes back to driving instances at
-    // once; on the MI355X box's 16-core host share that only moved the same
-    // CPU work beside the stepping threads (same-box A/B), so
-    // it is off by default.
+    // The batch is laid out by the launcher thread and its own pool, so the
+    // caller goes back to driving instances at once (same-box A/B of the
+    // headline, 5 interleaved runs each: median 6.34 vs 6.63 ms/step,
+    // profiles/r4i_async_ab.txt).  SIAMESE_AMD_ASYNC_ASSEMBLY=0 lays it out
+    // here, on the caller's thread and the shared pool.
     if (!async_assembly()) {
         claim_set(*b);
         const uint64_t tq2 = now_ns();
@@ -1706,7 +1705,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     size_t nSolveRows = 0, nCoef = 0;
     std::vector<SolveItem> sitems;
     size_t nOps = 0, nTerms = 0, nWords = 0, nItems = 0, nWide = 0;
-    uint64_t wideBytes = 0;
+    uint64_t wideBytes = 0, tBytes = 0;
     for (int g = 0; g < 2; ++g) {
         size_t maxSegs = 0;
         for (ProgramBody* p : bt.bodies[g])
@@ -1791,6 +1790,17 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
 #endif
             sv.itemCount = sitems.size() - sv.itemBegin;
             sv.solveCount = sdescs.size() - sv.solveBegin;
+            if (sv.solveCount >= kSolvePrefixSplit)
+                for (size_t i = sv.solveBegin; i < sdescs.size(); ++i) {
+                    // the inverse's scratch (matrix-core path), in the k_ldpc ring
+                    // after this submission's k_ldpc scratch (1 + its offset
+                    // there until placed below)
+                    const uint32_t tb = solve_t_bytes(sdescs[i].m);
+                    if (tb) {
+                        sdescs[i].tinv = 1 + tBytes;
+                        tBytes += tb;
+                    }
+                }
             if (sv.solveCount)
                 phases.push_back(sv);
         }
@@ -1914,16 +1924,23 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         return v ? (size_t)std::atol(v) : (size_t)32768;
     }();
     bt.upBase = (xs.upHostDev && bt.upBytes <= kZeroCopyUp) ? xs.upHostDev : xs.upDev;
-    if (wideBytes) {
+    if (wideBytes + tBytes) {
         // k_ldpc scratch comes from the set's ring, which is zeroed as a whole
-        // when it wraps (not per submission: most flushes then need no memset)
-        if (xs.wideUsed + wideBytes > xs.wideCap) {
-            ensure_wide(xs, std::max<size_t>(wideBytes, 16u << 20));
+        // when it wraps (not per submission: most flushes then need no memset);
+        // the solves' inverses follow it (written before they are read, in
+        // this submission, so the zeroing is no concern of theirs)
+        const uint64_t need = wideBytes + tBytes;
+        if (xs.wideUsed + need > xs.wideCap) {
+            ensure_wide(xs, std::max<size_t>(need, 16u << 20));
             xs.wideUsed = 0;
             bt.wideZero = true;
         }
         bt.wideBase = xs.wideUsed;
-        xs.wideUsed += wideBytes;
+        xs.wideUsed += need;
+        const uint64_t tBase = (uint64_t)(uintptr_t)xs.wideDev + bt.wideBase + wideBytes;
+        for (SolveDesc& d : sdescs)
+            if (d.tinv)
+                d.tinv = tBase + (d.tinv - 1);
     }
 
     const uint64_t tLayout = now_ns();

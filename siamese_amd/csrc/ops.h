@@ -268,7 +268,21 @@ struct SolveDesc
                          // starts (copied by the segment before it), so every
                          // tile can solve the length prefixes while tile 0
                          // overwrites the rows
+    uint64_t tinv;       // device scratch of solve_t_bytes(m) for the solve's
+                         // inverse T (matrix-core path; 0: none)
+    uint64_t pad;
 };
+
+/// Solves of up to this many rows may run on the matrix cores (their
+/// inverse T = U^-1 L^-1 in scratch, rows of kTStride bytes), in launches of
+/// at least kSolvePrefixSplit solves (the prefix pass is then its own launch).
+constexpr unsigned kMfmaMaxRows = 120;
+constexpr unsigned kSolvePrefixSplit = 16;
+constexpr uint32_t kTStride = 128;
+constexpr uint32_t solve_t_bytes(uint32_t m)
+{
+    return m <= kMfmaMaxRows ? ((m + 3u) & ~3u) * kTStride : 0u;
+}
 
 struct SolveRow
 {
