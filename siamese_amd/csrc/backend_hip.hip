@@ -2491,8 +2491,18 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     // flags bit 0: k_solve_prefix already solved the length prefixes; bit 1:
     // k_solve_mfma ran before this launch and took every solve it could
     const bool prefixDone = (flags & 1u) != 0;
-    if ((flags & 2u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m)
+    if ((flags & 2u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m) {
+        // solved on the matrix cores: this tile of the result rows from the
+        // scratch into the rows (bytes below each row's final length)
+        static_assert(kMfmaMaxRows <= kSolveWideMaxRows, "matrix-core solves take 1 KiB tiles");
+        const uint32_t xs = solve_x_stride(sd.maxBytes), tb = kTileBytes;
+        for (uint32_t x = threadIdx.x; x < m * (tb / 16u); x += 64u * kSolveWaves) {
+            const uint32_t i = x / (tb / 16u), p = it.tileBase + 16u * (x - i * (tb / 16u));
+            if (p < R[i].finalBytes)
+                st16(R[i].buf + p, ld16(sd.xout + (uint64_t)i * xs + p));
+        }
         return;
+    }
     const uint32_t* resIn = prefixDone ? results + sd.result : nullptr;
     uint32_t* out = (!prefixDone && it.tileBase == 0) ? results + sd.result : nullptr;
     if (m <= kSolveWideMaxRows)
@@ -2784,6 +2794,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
     const uint8_t* af = AF + ((4u * wave + (r >> 3)) * 8u + (7u - (r & 7u))) * mp + 2u * h;
     const bool active = row0 + 4u * wave < mp;
     const uint32_t rowsHere = (m - row0 < kMfmaGroupRows ? m - row0 : kMfmaGroupRows);
+    const uint32_t xs = solve_x_stride(sd.maxBytes);
     for (uint32_t c0 = 0; c0 < maxB; c0 += kMfmaChunk) {
         // the B operand: byte (j, col) as eight 0/1 bytes at
         // bits[((t * S + j / 4) * 32 + col % 32) * 32 + (j % 4) * 8], t = col / 32
@@ -2837,14 +2848,16 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
         }
         __syncthreads();
         // x masked past the recovered length, stored below the row's final
-        // bytes (the stores of the exact back-substitution)
+        // bytes (the stores of the exact back-substitution) into the result
+        // scratch: another group may still read these rows' bytes; the tile
+        // pass (k_solve_main) copies them into the rows
         for (uint32_t it = tid; it < rowsHere * (kMfmaChunk / 16); it += kMfmaThreads) {
             const uint32_t il = it / (kMfmaChunk / 16), u = it % (kMfmaChunk / 16);
             const uint32_t i = row0 + il, p = c0 + 16 * u;
             if (p < finB[i]) {
                 uint4 v = *reinterpret_cast<const uint4*>(outT + il * kMfmaChunk + 16 * u);
                 v = mask16(v, (int)bbB[i] - (int)p);
-                st16(R[i].buf + p, v);
+                st16(sd.xout + (uint64_t)i * xs + p, v);
             }
         }
     }

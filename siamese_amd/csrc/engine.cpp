@@ -1799,6 +1799,8 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                     if (tb) {
                         sdescs[i].tinv = 1 + tBytes;
                         tBytes += tb;
+                        sdescs[i].xout = 1 + tBytes;
+                        tBytes += (solve_x_bytes(sdescs[i].m, sdescs[i].maxBytes) + 255u) & ~(uint64_t)255u;
                     }
                 }
             if (sv.solveCount)
@@ -1939,8 +1941,10 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         xs.wideUsed += need;
         const uint64_t tBase = (uint64_t)(uintptr_t)xs.wideDev + bt.wideBase + wideBytes;
         for (SolveDesc& d : sdescs)
-            if (d.tinv)
+            if (d.tinv) {
                 d.tinv = tBase + (d.tinv - 1);
+                d.xout = tBase + (d.xout - 1);
+            }
     }
 
     const uint64_t tLayout = now_ns();

@@ -270,7 +270,10 @@ struct SolveDesc
                          // overwrites the rows
     uint64_t tinv;       // device scratch of solve_t_bytes(m) for the solve's
                          // inverse T (matrix-core path; 0: none)
-    uint64_t pad;
+    uint64_t xout;       // device scratch of solve_x_bytes(m, maxBytes): the
+                         // matrix-core path's result rows, copied into the
+                         // rows by the tile pass (several workgroups write
+                         // one solve's rows, so not in place)
 };
 
 /// Solves of up to this many rows may run on the matrix cores (their
@@ -282,6 +285,12 @@ constexpr uint32_t kTStride = 128;
 constexpr uint32_t solve_t_bytes(uint32_t m)
 {
     return m <= kMfmaMaxRows ? ((m + 3u) & ~3u) * kTStride : 0u;
+}
+/// Row stride of the matrix-core path's result scratch (64-column chunks).
+constexpr uint32_t solve_x_stride(uint32_t maxBytes) { return (maxBytes + 63u) & ~63u; }
+constexpr uint64_t solve_x_bytes(uint32_t m, uint32_t maxBytes)
+{
+    return m <= kMfmaMaxRows ? (uint64_t)m * solve_x_stride(maxBytes) : 0u;
 }
 
 struct SolveRow
