@@ -2642,7 +2642,7 @@ __host__ __device__ constexpr uint32_t solve_pre_lds_bytes(uint32_t m)
 __host__ __device__ constexpr uint32_t solve_mfma_lds_bytes(uint32_t m)
 {
     return kMfmaGroupRows * 8u * mfma_rows(m) + mfma_rows(m) * 8u * kMfmaChunk + kMfmaGroupRows * kMfmaChunk +
-           ((3u * m * 4u + 15u) & ~15u);
+           ((3u * m * 4u + 15u) & ~15u) + m * 8u + 16u;
 }
 
 // the four low bits of v as four 0/1 bytes (byte q = bit q)
@@ -2766,6 +2766,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
     uint32_t* initB = reinterpret_cast<uint32_t*>(outT + kMfmaGroupRows * kMfmaChunk);
     uint32_t* finB = initB + m;
     uint32_t* bbB = finB + m;                                    // recovered header + length
+    uint64_t* rowBuf = reinterpret_cast<uint64_t*>(bbB + ((m + 1u) & ~1u));
 
     const GMEM uint8_t* T = reinterpret_cast<const GMEM uint8_t*>(sd.tinv);
     for (uint32_t x = tid; x < kMfmaGroupRows * mp; x += kMfmaThreads) {
@@ -2780,6 +2781,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
     for (uint32_t j = tid; j < m; j += kMfmaThreads) {
         initB[j] = R[j].initBytes;
         finB[j] = R[j].finalBytes;
+        rowBuf[j] = R[j].buf;
         const uint32_t w = results[sd.result + 1 + j];
         bbB[j] = (w >> 29) + (w & kSolveLengthMask);
     }
@@ -2797,24 +2799,23 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
     const uint32_t xs = solve_x_stride(sd.maxBytes);
     for (uint32_t c0 = 0; c0 < maxB; c0 += kMfmaChunk) {
         // the B operand: byte (j, col) as eight 0/1 bytes at
-        // bits[((t * S + j / 4) * 32 + col % 32) * 32 + (j % 4) * 8], t = col / 32
-        for (uint32_t it = tid; it < mp * (kMfmaChunk / 4); it += kMfmaThreads) {
-            const uint32_t j = it / (kMfmaChunk / 4), q = it % (kMfmaChunk / 4);
-            uint32_t x = 0;
+        // bits[((t * S + j / 4) * 64 + (j % 4) / 2 * 32 + col % 32) * 16 + (j % 2) * 8],
+        // t = col / 32 (lane h * 32 + r's 16-byte fragment of K step s is
+        // contiguous, lanes in order: conflict-free ds_read_b128); item `it`
+        // is the 8-byte slot it * 8, so a wave's stores are one contiguous
+        // 512-byte run (the per-dword stores they replace were 16-way bank
+        // conflicts: SQ_LDS_BANK_CONFLICT 47.7 M cycles per launch)
+        for (uint32_t it = tid; it < mp * kMfmaChunk; it += kMfmaThreads) {
+            const uint32_t blk = it >> 7, w = it & 127u;
+            const uint32_t t = blk / S, g = blk - t * S;
+            const uint32_t j = 4u * g + 2u * (w >> 6) + (w & 1u), col = 32u * t + ((w >> 1) & 31u);
+            uint32_t v = 0;
             if (j < m) {
-                const uint32_t p = c0 + 4 * q, ib = initB[j];
-                if (p < ib) {
-                    x = ld4(R[j].buf + p);
-                    if (p + 4 > ib)
-                        x &= byte_mask((int)(ib - p));
-                }
+                const uint32_t p = c0 + col;
+                if (p < initB[j])
+                    v = *reinterpret_cast<const GMEM uint8_t*>(rowBuf[j] + p);
             }
-#pragma unroll
-            for (uint32_t cc = 0; cc < 4; ++cc) {
-                const uint32_t col = 4 * q + cc, v = (x >> (8 * cc)) & 0xffu;
-                *reinterpret_cast<uint2*>(bits + (((col / 32) * S + j / 4) * 32 + col % 32) * 32 + (j % 4) * 8) =
-                    make_uint2(bits4(v), bits4(v >> 4));
-            }
+            *reinterpret_cast<uint2*>(bits + 8u * it) = make_uint2(bits4(v), bits4(v >> 4));
         }
         __syncthreads();
         if (active) {
@@ -2828,7 +2829,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
                 const i32x4 A = {(int)bits4(u), (int)bits4(u >> 4), (int)bits4(u >> 8), (int)bits4(u >> 12)};
 #pragma unroll
                 for (uint32_t t = 0; t < kMfmaTiles; ++t) {
-                    const i32x4 B = *reinterpret_cast<const i32x4*>(bits + ((t * S + s) * 32 + r) * 32 + h * 16);
+                    const i32x4 B = *reinterpret_cast<const i32x4*>(bits + ((t * S + s) * 64 + h * 32 + r) * 16);
                     acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc[t], 0, 0, 0);
                 }
             }
@@ -3613,12 +3614,14 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
     // in parallel); few (single-stream flushes): fused into the tiles, one
     // launch fewer on the flush's critical path.
     const bool separate = solveCount >= kSolvePrefixSplit;
-    // the solves whose lengths all come out valid on the matrix cores
-    // (SGPU_MFMA_SOLVE=0: every solve by the sweeps, A/B aid): the prefix
-    // pass and the solves' inverses in one launch, then the products
+    // SGPU_MFMA_SOLVE=1: the solves whose lengths all come out valid on the
+    // matrix cores (the prefix pass and the solves' inverses in one launch,
+    // then the products).  Off by default: on the headline it measured
+    // slower than the sweeps (k_solve_pre 80 + k_solve_mfma 322 us per launch
+    // against k_solve_prefix 58 + k_solve_main 277; profiles/r4l_*)
     static const bool kMfmaSolve = [] {
         const char* v = std::getenv("SGPU_MFMA_SOLVE");
-        return !v || std::atoi(v) != 0;
+        return v && std::atoi(v) != 0;
     }();
     const bool mfma = separate && kMfmaSolve;
     if (mfma) {
