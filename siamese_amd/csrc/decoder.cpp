@@ -2090,9 +2090,25 @@ SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
 SiameseResult DecoderCore::get_range(unsigned firstNum, unsigned count, SiameseOriginalPacket* out, unsigned* got)
 {
     *got = 0;
-    for (unsigned k = 0; k < count; ++k) {
-        out[k].PacketNum = (firstNum + k) & SIAMESE_PACKET_NUM_MAX;
-        const SiameseResult r = get(out[k]);
+    // get() per packet, with the state checks made once and the window
+    // walked slot by slot; a packet whose length is still on the device (or
+    // anything else get() handles) goes through get() itself
+    settle();
+    const bool ok = !dead();
+    unsigned e = column_to_element(firstNum);
+    for (unsigned k = 0; k < count; ++k, e = (e + 1) % kColumnPeriod) {
+        SiameseOriginalPacket& p = out[k];
+        p.PacketNum = (firstNum + k) & SIAMESE_PACKET_NUM_MAX;
+        if (ok && e < count_) {
+            DecSlot& s = slot(e);
+            if (s.bytes != 0 && !s.pending) {
+                p.Data = (mirror_ ? s.host().data() : s.buf.ptr) + s.header;
+                p.DataBytes = s.bytes - s.header;
+                ++*got;
+                continue;
+            }
+        }
+        const SiameseResult r = get(p);
         if (r != Siamese_Success)
             return r;
         ++*got;

@@ -1640,10 +1640,12 @@ void Engine::claim_set(Batch& b)
 WorkerPool& Engine::asm_pool()
 {
     // the launcher's own pool: the application may be running a fork-join
-    // on pool() while a batch is laid out (SIAMESE_AMD_ASM_THREADS, default 8)
+    // on pool() while a batch is laid out (SIAMESE_AMD_ASM_THREADS, default 4)
     if (!asmPool_) {
+        // (4 measured best on the box's 16-core share: 6.07/5.93/6.34 ms
+        // per step vs 7.88/6.34/6.98 with 8, profiles/r4p_threads_ab.txt)
         const char* v = std::getenv("SIAMESE_AMD_ASM_THREADS");
-        const int n = v ? std::atoi(v) : 8;
+        const int n = v ? std::atoi(v) : 4;
         asmPool_.reset(new WorkerPool((unsigned)std::max(1, std::min(64, n))));
     }
     return *asmPool_;
