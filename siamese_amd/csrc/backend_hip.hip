@@ -2489,8 +2489,11 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     if (m > kSolveLdsMaxRows)
         return;   // (the host never queues m > 255: kMaximumLossRecoveryCount)
     // flags bit 0: k_solve_prefix already solved the length prefixes; bit 1:
-    // k_solve_mfma ran before this launch and took every solve it could
+    // k_solve_mfma ran before this launch and took every solve it could; bit
+    // 2: k_solve_tr did
     const bool prefixDone = (flags & 1u) != 0;
+    if ((flags & 4u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m)
+        return;   // solved in place by k_solve_tr (bit 2)
     if ((flags & 2u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m) {
         // solved on the matrix cores: this tile of the result rows from the
         // scratch into the rows (bytes below each row's final length)
@@ -2862,6 +2865,172 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// The same product on the vector ALUs (k_solve_tr; the default for launches
+// of many solves)
+//
+// X = T R for the solves k_solve_pre found all valid (results[0] == m), one
+// workgroup per (solve, 1 KiB tile): the tile of every row is staged in LDS
+// once, then wave w accumulates output rows w, w + 8, ... in registers, each
+// source row's bytes split once into the multiply's bit groups and multiplied
+// by every output row's coefficient T[r][k] (its v_perm tables fetched by
+// scalar loads: the coefficient is uniform across the wave).  No pivot chain
+// and no barrier after the staging, one LDS read per source row and wave,
+// and no LDS writes: the sweeps read and wrote a row tile per row update and
+// waited on a barrier per pivot step.  The workgroup owns its tile of every
+// row of the solve, so it stores the results in place after reading them.
+//
+// Lane l holds the dwords at bytes 256 q + 4 l of the tile (q < 4): a tile
+// that ends early (a 1402-byte row's second KiB has 378 bytes) skips the
+// whole quarters past the solve's largest row, a quarter of the multiplies
+// each instead of the idle lanes of 16-byte-per-lane tiles.
+constexpr unsigned kTrWaves = 8;
+constexpr unsigned kTrThreads = 64 * kTrWaves;
+
+__host__ __device__ constexpr uint32_t solve_tr_lds_bytes(uint32_t m) { return m * 1024u; }
+
+template <unsigned NQ, unsigned RW>
+__device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRow* __restrict__ R,
+                                              const uint32_t* __restrict__ res, uint32_t tileBase,
+                                              uint4* __restrict__ X)
+{
+    const uint32_t m = sd.m, tid = threadIdx.x, lane = tid & 63, wave = uni(tid >> 6);
+    // the tile of every row, bytes past a row's initial length as zero
+    for (uint32_t j = wave; j < m; j += kTrWaves) {
+        const uint64_t buf = R[j].buf;
+        const uint32_t ib = R[j].initBytes;
+        uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (unsigned q = 0; q < NQ; ++q) {
+            const uint32_t p = tileBase + 256u * q + 4u * lane;
+            if (p < ib)
+                v[q] = ld4(buf + p) & byte_mask((int)ib - (int)p);
+        }
+        X[j * 64u + lane] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    // this wave's rows of T (lane l < 32: bytes 4 l .. 4 l + 3 of each)
+    const uint32_t rw = wave < m ? (m - wave + kTrWaves - 1) / kTrWaves : 0;
+    uint32_t trow[RW];
+#pragma unroll
+    for (unsigned t = 0; t < RW; ++t)
+        trow[t] = (t < rw && lane < kTStride / 4)
+                      ? ld4(sd.tinv + (uint64_t)(wave + kTrWaves * t) * kTStride + 4u * lane)
+                      : 0u;
+    __syncthreads();
+
+    uint32_t acc[RW][NQ];
+#pragma unroll
+    for (unsigned t = 0; t < RW; ++t)
+#pragma unroll
+        for (unsigned q = 0; q < NQ; ++q)
+            acc[t][q] = 0;
+    for (uint32_t k0 = 0; k0 < m; k0 += 4) {
+        uint32_t tw[RW];
+#pragma unroll
+        for (unsigned t = 0; t < RW; ++t)
+            tw[t] = rl(trow[t], k0 >> 2);   // T[r_t][k0 .. k0 + 3]
+        const uint32_t kn = m - k0 < 4 ? m - k0 : 4;
+        for (uint32_t kk = 0; kk < kn; ++kk) {
+            const uint4 s4 = X[(k0 + kk) * 64u + lane];
+            const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            uint32_t sa[NQ], sb[NQ], sc[NQ];
+#pragma unroll
+            for (unsigned q = 0; q < NQ; ++q) {
+                sa[q] = sv[q] & 0x07070707u;
+                sb[q] = (sv[q] >> 3) & 0x07070707u;
+                sc[q] = (sv[q] >> 6) & 0x03030303u;
+            }
+            // the tables of up to eight rows fetched together, then their
+            // products, with no branch (RW = ceil(m / 8) or a little more: a
+            // wave's rows past m have T zero, the table of 0, and are not
+            // stored)
+#pragma unroll
+            for (unsigned t0 = 0; t0 < RW; t0 += 8) {
+                constexpr unsigned kG = 8;
+                GfTab tb[kG];
+#pragma unroll
+                for (unsigned u = 0; u < kG && t0 + u < RW; ++u)
+                    tb[u] = gf_tab(uni((tw[t0 + u] >> (8u * kk)) & 255u));
+#pragma unroll
+                for (unsigned u = 0; u < kG && t0 + u < RW; ++u) {
+#pragma unroll
+                    for (unsigned q = 0; q < NQ; ++q)
+                        acc[t0 + u][q] ^= __builtin_amdgcn_perm(tb[u].a1, tb[u].a0, sa[q]) ^
+                                          __builtin_amdgcn_perm(tb[u].b1, tb[u].b0, sb[q]) ^
+                                          __builtin_amdgcn_perm(0u, tb[u].c, sc[q]);
+                }
+            }
+        }
+    }
+    // masked past the recovered length, stored below the row's final bytes
+    // (the exact back-substitution's stores)
+#pragma unroll
+    for (unsigned t = 0; t < RW; ++t) {
+        if (t < rw) {
+            const uint32_t i = wave + kTrWaves * t;
+            const uint32_t w = res[1 + i];
+            const uint32_t bb = (w >> 29) + (w & kSolveLengthMask), fb = R[i].finalBytes;
+            const uint64_t buf = R[i].buf;
+#pragma unroll
+            for (unsigned q = 0; q < NQ; ++q) {
+                const uint32_t p = tileBase + 256u * q + 4u * lane;
+                if (p < fb)
+                    st4(buf + p, acc[t][q] & byte_mask((int)bb - (int)p));
+            }
+        }
+    }
+}
+
+template <unsigned NQ>
+__device__ __forceinline__ void solve_tr_rows(const SolveDesc& sd, const SolveRow* R, const uint32_t* res,
+                                              uint32_t tileBase, uint4* X)
+{
+    // output rows per wave: ceil(m / 8) <= 15 (m <= kMfmaMaxRows), rounded
+    // up to one of these
+    static_assert(kMfmaMaxRows <= 15 * kTrWaves, "k_solve_tr keeps at most 15 rows per wave");
+    const uint32_t rw = (sd.m + kTrWaves - 1) / kTrWaves;
+    switch (rw) {
+    case 1:
+    case 2: solve_tr_tile<NQ, 2>(sd, R, res, tileBase, X); break;
+    case 3:
+    case 4: solve_tr_tile<NQ, 4>(sd, R, res, tileBase, X); break;
+    case 5: solve_tr_tile<NQ, 5>(sd, R, res, tileBase, X); break;
+    case 6: solve_tr_tile<NQ, 6>(sd, R, res, tileBase, X); break;
+    case 7: solve_tr_tile<NQ, 7>(sd, R, res, tileBase, X); break;
+    case 8: solve_tr_tile<NQ, 8>(sd, R, res, tileBase, X); break;
+    case 9: solve_tr_tile<NQ, 9>(sd, R, res, tileBase, X); break;
+    case 10: solve_tr_tile<NQ, 10>(sd, R, res, tileBase, X); break;
+    case 11:
+    case 12: solve_tr_tile<NQ, 12>(sd, R, res, tileBase, X); break;
+    default: solve_tr_tile<NQ, 15>(sd, R, res, tileBase, X); break;
+    }
+}
+
+__global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __restrict__ solves,
+                                                         const SolveRow* __restrict__ rows,
+                                                         const uint32_t* __restrict__ results,
+                                                         const SolveItem* __restrict__ items)
+{
+    extern __shared__ uint4 X[];
+    const SolveItem it = items[blockIdx.x];
+    const SolveDesc sd = solves[it.solve];
+    if (sd.m == 0 || sd.m > kMfmaMaxRows || sd.tinv == 0 || results[sd.result] != sd.m ||
+        it.tileBase >= sd.maxBytes)
+        return;   // (uniform: k_solve_main solves it)
+    const uint32_t left = sd.maxBytes - it.tileBase;
+    const uint32_t nq = left >= 768u ? 4u : (left + 255u) / 256u;
+    const SolveRow* R = rows + sd.rowBegin;
+    const uint32_t* res = results + sd.result;
+    if (nq == 4)
+        solve_tr_rows<4>(sd, R, res, it.tileBase, X);
+    else if (nq == 3)
+        solve_tr_rows<3>(sd, R, res, it.tileBase, X);
+    else if (nq == 2)
+        solve_tr_rows<2>(sd, R, res, it.tileBase, X);
+    else
+        solve_tr_rows<1>(sd, R, res, it.tileBase, X);
 }
 
 // ---------------------------------------------------------------------------
@@ -3369,6 +3538,11 @@ bool be_init(int device, const char** err)
         *err = "the device refused the matrix-core solve's LDS";
         return false;
     }
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_tr), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)solve_tr_lds_bytes(kMfmaMaxRows)) != hipSuccess) {
+        *err = "the device refused the vector product solve's LDS";
+        return false;
+    }
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_pre), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)solve_pre_lds_bytes(kSolveLdsMaxRows)) != hipSuccess) {
         *err = "the device refused the solve pre-pass's LDS";
@@ -3623,8 +3797,24 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
         const char* v = std::getenv("SGPU_MFMA_SOLVE");
         return v && std::atoi(v) != 0;
     }();
+    // Default: the same solves as X = T R on the vector ALUs, in place
+    // (k_solve_pre 80 + k_solve_tr 114 + k_solve_main 4 us per headline
+    // launch against k_solve_prefix 58 + k_solve_main 277 for the sweeps;
+    // profiles/r4s_*).  SGPU_TR_SOLVE=0: the sweeps alone.
+    static const bool kTrSolve = [] {
+        const char* v = std::getenv("SGPU_TR_SOLVE");
+        return !v || std::atoi(v) != 0;
+    }();
     const bool mfma = separate && kMfmaSolve;
-    if (mfma) {
+    const bool tr = separate && !mfma && kTrSolve;
+    if (tr) {
+        hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
+                           g_stream, solves + solveBegin, rows, coef, results,
+                           reinterpret_cast<unsigned long long*>(acct), solveCount);
+        hipLaunchKernelGGL(k_solve_tr, dim3(count), dim3(kTrThreads),
+                           (size_t)solve_tr_lds_bytes(rowsCap < kMfmaMaxRows ? rowsCap : kMfmaMaxRows), g_stream,
+                           solves, rows, results, items);
+    } else if (mfma) {
         hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
                            g_stream, solves + solveBegin, rows, coef, results,
                            reinterpret_cast<unsigned long long*>(acct), solveCount);
@@ -3638,7 +3828,8 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
     }
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
                        (size_t)solve_launch_lds_bytes(rowsCap, !separate), g_stream, solves, rows, coef, results,
-                       items, reinterpret_cast<unsigned long long*>(acct), (separate ? 1u : 0u) | (mfma ? 2u : 0u));
+                       items, reinterpret_cast<unsigned long long*>(acct),
+                       (separate ? 1u : 0u) | (mfma ? 2u : 0u) | (tr ? 4u : 0u));
 }
 
 void* be_stage_h2d(void* dst, const void* src, size_t bytes)
