@@ -2489,14 +2489,17 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     if (m > kSolveLdsMaxRows)
         return;   // (the host never queues m > 255: kMaximumLossRecoveryCount)
     // flags bit 0: k_solve_prefix already solved the length prefixes; bit 1:
-    // k_solve_mfma ran before this launch and took every solve it could; bit
-    // 2: k_solve_tr did
+    // k_solve_mfma ran before this launch, bit 2: k_solve_tr did (each took
+    // every solve it could, into the scratch)
     const bool prefixDone = (flags & 1u) != 0;
-    if ((flags & 4u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m)
-        return;   // solved in place by k_solve_tr (bit 2)
-    if ((flags & 2u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m) {
-        // solved on the matrix cores: this tile of the result rows from the
-        // scratch into the rows (bytes below each row's final length)
+    if ((flags & 6u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m &&
+        results[sd.result + m + 1] == 0) {
+        // solved as X = T R (k_solve_tr or k_solve_mfma), every row zero past
+        // its recovered length, so the sweeps' clipping would change nothing:
+        // this tile of the result rows from the scratch into the rows (bytes
+        // below each row's final length).  A solve whose products have
+        // non-zero bytes there (inconsistent recovery data) falls through to
+        // the sweeps, on its rows as they were: the products went to scratch.
         static_assert(kMfmaMaxRows <= kSolveWideMaxRows, "matrix-core solves take 1 KiB tiles");
         const uint32_t xs = solve_x_stride(sd.maxBytes), tb = kTileBytes;
         for (uint32_t x = threadIdx.x; x < m * (tb / 16u); x += 64u * kSolveWaves) {
@@ -2737,6 +2740,8 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __r
         permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
         permC[tid] = t[4];
     }
+    if (tid == 0)
+        results[sd.result + m + 1] = 0;   // the product solves' tail flag
     // (every wave stages; then wave 0 alone runs the serial pass)
     stage_transposed<kMfmaThreads, 2>(Ct, C, m, tid);
     for (uint32_t j = tid; j < m; j += kMfmaThreads) {
@@ -2751,7 +2756,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __r
 
 __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __restrict__ solves,
                                                            const SolveRow* __restrict__ rows,
-                                                           const uint32_t* __restrict__ results)
+                                                           uint32_t* results)
 {
     extern __shared__ uint4 Ls[];
     const uint32_t grp = blockIdx.x % kMfmaGroups;
@@ -2855,15 +2860,20 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
         // bytes (the stores of the exact back-substitution) into the result
         // scratch: another group may still read these rows' bytes; the tile
         // pass (k_solve_main) copies them into the rows
+        // (a non-zero byte past a row's recovered length flags the solve for
+        // the exact sweeps, as in k_solve_tr)
+        uint32_t tail = 0;
         for (uint32_t it = tid; it < rowsHere * (kMfmaChunk / 16); it += kMfmaThreads) {
             const uint32_t il = it / (kMfmaChunk / 16), u = it % (kMfmaChunk / 16);
             const uint32_t i = row0 + il, p = c0 + 16 * u;
-            if (p < finB[i]) {
-                uint4 v = *reinterpret_cast<const uint4*>(outT + il * kMfmaChunk + 16 * u);
-                v = mask16(v, (int)bbB[i] - (int)p);
-                st16(sd.xout + (uint64_t)i * xs + p, v);
-            }
+            const uint4 v = *reinterpret_cast<const uint4*>(outT + il * kMfmaChunk + 16 * u);
+            const uint4 k = mask16(v, (int)bbB[i] - (int)p);
+            tail |= (v.x ^ k.x) | (v.y ^ k.y) | (v.z ^ k.z) | (v.w ^ k.w);
+            if (p < finB[i])
+                st16(sd.xout + (uint64_t)i * xs + p, k);
         }
+        if (__any(tail != 0) && lane == 0)
+            atomicOr(results + sd.result + 1 + m, 1u);
     }
 }
 
@@ -2886,28 +2896,50 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
 // that ends early (a 1402-byte row's second KiB has 378 bytes) skips the
 // whole quarters past the solve's largest row, a quarter of the multiplies
 // each instead of the idle lanes of 16-byte-per-lane tiles.
-constexpr unsigned kTrWaves = 8;
+#ifndef SGPU_TR_WAVES
+#define SGPU_TR_WAVES 8
+#endif
+#ifndef SGPU_TR_PHASE
+#define SGPU_TR_PHASE 0   // timing aids (wrong outputs): 1 no products, 2 no row loads
+#endif
+#ifndef SGPU_TR_LDS_TABLES
+#define SGPU_TR_LDS_TABLES 0
+#endif
+constexpr unsigned kTrWaves = SGPU_TR_WAVES;
 constexpr unsigned kTrThreads = 64 * kTrWaves;
+constexpr uint32_t kTrTableBytes = SGPU_TR_LDS_TABLES ? 256u * 20u : 0u;
 
-__host__ __device__ constexpr uint32_t solve_tr_lds_bytes(uint32_t m) { return m * 1024u; }
+__host__ __device__ constexpr uint32_t solve_tr_lds_bytes(uint32_t m) { return kTrTableBytes + m * 1024u; }
 
 template <unsigned NQ, unsigned RW>
 __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRow* __restrict__ R,
-                                              const uint32_t* __restrict__ res, uint32_t tileBase,
+                                              uint32_t* res, uint32_t tileBase,
                                               uint4* __restrict__ X)
 {
     const uint32_t m = sd.m, tid = threadIdx.x, lane = tid & 63, wave = uni(tid >> 6);
+#if SGPU_TR_LDS_TABLES
+    const uint4* permL = X;
+    const uint32_t* permC = reinterpret_cast<const uint32_t*>(X + 256);
+    if (tid < 256) {
+        const uint32_t* t = c_perm[tid];
+        X[tid] = make_uint4(t[0], t[1], t[2], t[3]);
+        reinterpret_cast<uint32_t*>(X + 256)[tid] = t[4];
+    }
+    X += 256 + 64;
+#endif
     // the tile of every row, bytes past a row's initial length as zero
     for (uint32_t j = wave; j < m; j += kTrWaves) {
         const uint64_t buf = R[j].buf;
         const uint32_t ib = R[j].initBytes;
         uint32_t v[4] = {0, 0, 0, 0};
+#if SGPU_TR_PHASE != 2
 #pragma unroll
         for (unsigned q = 0; q < NQ; ++q) {
             const uint32_t p = tileBase + 256u * q + 4u * lane;
             if (p < ib)
                 v[q] = ld4(buf + p) & byte_mask((int)ib - (int)p);
         }
+#endif
         X[j * 64u + lane] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     // this wave's rows of T (lane l < 32: bytes 4 l .. 4 l + 3 of each)
@@ -2926,7 +2958,7 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
 #pragma unroll
         for (unsigned q = 0; q < NQ; ++q)
             acc[t][q] = 0;
-    for (uint32_t k0 = 0; k0 < m; k0 += 4) {
+    for (uint32_t k0 = 0; k0 < (SGPU_TR_PHASE == 1 ? 0u : m); k0 += 4) {
         uint32_t tw[RW];
 #pragma unroll
         for (unsigned t = 0; t < RW; ++t)
@@ -2952,7 +2984,11 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
                 GfTab tb[kG];
 #pragma unroll
                 for (unsigned u = 0; u < kG && t0 + u < RW; ++u)
+#if SGPU_TR_LDS_TABLES
+                    tb[u] = gf_tab_l(permL, permC, uni((tw[t0 + u] >> (8u * kk)) & 255u));
+#else
                     tb[u] = gf_tab(uni((tw[t0 + u] >> (8u * kk)) & 255u));
+#endif
 #pragma unroll
                 for (unsigned u = 0; u < kG && t0 + u < RW; ++u) {
 #pragma unroll
@@ -2964,32 +3000,41 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
             }
         }
     }
-    // masked past the recovered length, stored below the row's final bytes
-    // (the exact back-substitution's stores)
+    // Into the scratch, masked past the recovered length, every 16-byte
+    // chunk that starts below the row's final bytes (the chunks the exact
+    // back-substitution stores).  A non-zero byte past a row's recovered
+    // length flags the solve (res[m + 1]): the sweeps clip there, so the
+    // tile pass redoes it the reference's way.
+    const uint32_t xs = solve_x_stride(sd.maxBytes);
+    uint32_t tail = 0;
 #pragma unroll
     for (unsigned t = 0; t < RW; ++t) {
         if (t < rw) {
             const uint32_t i = wave + kTrWaves * t;
             const uint32_t w = res[1 + i];
             const uint32_t bb = (w >> 29) + (w & kSolveLengthMask), fb = R[i].finalBytes;
-            const uint64_t buf = R[i].buf;
+            const uint64_t out = sd.xout + (uint64_t)i * xs;
 #pragma unroll
             for (unsigned q = 0; q < NQ; ++q) {
                 const uint32_t p = tileBase + 256u * q + 4u * lane;
-                if (p < fb)
-                    st4(buf + p, acc[t][q] & byte_mask((int)bb - (int)p));
+                const uint32_t keep = byte_mask((int)bb - (int)p);
+                tail |= acc[t][q] & ~keep;
+                if ((p & ~15u) < fb)
+                    st4(out + p, acc[t][q] & keep);
             }
         }
     }
+    if (__any(tail != 0) && lane == 0)
+        atomicOr(res + 1 + m, 1u);
 }
 
 template <unsigned NQ>
-__device__ __forceinline__ void solve_tr_rows(const SolveDesc& sd, const SolveRow* R, const uint32_t* res,
+__device__ __forceinline__ void solve_tr_rows(const SolveDesc& sd, const SolveRow* R, uint32_t* res,
                                               uint32_t tileBase, uint4* X)
 {
     // output rows per wave: ceil(m / 8) <= 15 (m <= kMfmaMaxRows), rounded
     // up to one of these
-    static_assert(kMfmaMaxRows <= 15 * kTrWaves, "k_solve_tr keeps at most 15 rows per wave");
+    static_assert(kMfmaMaxRows <= 15 * kTrWaves && kTrThreads <= 1024, "k_solve_tr keeps at most 15 rows per wave");
     const uint32_t rw = (sd.m + kTrWaves - 1) / kTrWaves;
     switch (rw) {
     case 1:
@@ -3010,7 +3055,7 @@ __device__ __forceinline__ void solve_tr_rows(const SolveDesc& sd, const SolveRo
 
 __global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __restrict__ solves,
                                                          const SolveRow* __restrict__ rows,
-                                                         const uint32_t* __restrict__ results,
+                                                         uint32_t* results,
                                                          const SolveItem* __restrict__ items)
 {
     extern __shared__ uint4 X[];
@@ -3022,7 +3067,7 @@ __global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __rest
     const uint32_t left = sd.maxBytes - it.tileBase;
     const uint32_t nq = left >= 768u ? 4u : (left + 255u) / 256u;
     const SolveRow* R = rows + sd.rowBegin;
-    const uint32_t* res = results + sd.result;
+    uint32_t* res = results + sd.result;
     if (nq == 4)
         solve_tr_rows<4>(sd, R, res, it.tileBase, X);
     else if (nq == 3)

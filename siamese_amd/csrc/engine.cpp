@@ -587,7 +587,7 @@ uint32_t Program::solve(const std::vector<SolveRow>& rows, const uint8_t* coef, 
     ps.desc.m = (uint32_t)rows.size();
     ps.desc.maxBytes = maxBytes;
     ps.desc.result = b_->resultWords;
-    b_->resultWords += ps.desc.m + 1;
+    b_->resultWords += ps.desc.m + 2;
     ps.rows.assign(rows.begin(), rows.end());
     ps.coef.assign(coef, coef + rows.size() * rows.size());
     const uint32_t r = ps.desc.result;

@@ -262,7 +262,10 @@ struct SolveDesc
     uint32_t m;
     uint32_t rowBegin;   // index into SolveRow array
     uint64_t coefOffset; // byte offset into coefficient array
-    uint32_t result;     // index into the uint32 result array (m+1 words)
+    uint32_t result;     // index into the uint32 result array (m+2 words:
+                         // [0] rows recovered, [1..m] lengths, [m+1] set
+                         // when a product solve's rows have non-zero bytes
+                         // past their recovered lengths)
     uint32_t maxBytes;   // max finalBytes over rows (tile count)
     uint64_t head;       // m x 16 bytes: each row's first 16 bytes as the solve
                          // starts (copied by the segment before it), so every

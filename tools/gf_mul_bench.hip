@@ -5,12 +5,12 @@
 //   logexp  log/exp tables in LDS (reference gf256.cpp:379-403): per byte one
 //           log lookup of the source and one exp lookup of the sum
 //   mulrow  the 256-byte product row of y in LDS: one lookup per byte
-// Each kernel computes dst ^= sum_k (y + k) * src, k < 16, over `bytes`
+// Each kernel computes dst ^= sum_k (y + k) * src, k < Y, over `bytes`
 // bytes with a per-block base y, 16 bytes per lane (the solve's tile width):
-// sixteen multiplies per loaded byte, as a sweep step multiplies one source
-// row into many target rows, so the multiply -- not HBM -- sets the time.  The
-// host checks every byte.  Prints products per second per primitive (median
-// of 5 timed launches).
+// Y = 16 or 64 multiplies per loaded byte, as a solve multiplies one source
+// row into many output rows; at 64 the multiply -- not HBM -- sets the time.
+// The host checks every byte.  Prints products per second per primitive
+// (median of 5 timed launches).
 //   hipcc --offload-arch=gfx950 -O3 -o tools/gf_mul_bench tools/gf_mul_bench.hip
 #include <hip/hip_runtime.h>
 
@@ -41,7 +41,6 @@ void tables()
             g_mul[a][b] = (a && b) ? g_exp[g_log[a] + g_log[b]] : 0;
 }
 
-constexpr uint32_t kY = 16;   // multiplies per loaded byte
 __constant__ uint32_t c_perm[256][8];
 __constant__ uint8_t c_exp[512];
 __constant__ uint8_t c_log[256];
@@ -54,6 +53,7 @@ __device__ __forceinline__ uint32_t perm_mul(uint32_t x, uint32_t a0, uint32_t a
            __builtin_amdgcn_perm(0u, c, (x >> 6) & 0x03030303u);
 }
 
+template <uint32_t kY>
 __global__ __launch_bounds__(256) void k_perm(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16)
 {
     const uint32_t y0 = (blockIdx.x * 97u + 13u) & 255u;
@@ -85,6 +85,7 @@ __device__ __forceinline__ uint32_t logexp_mul(uint32_t x, uint32_t ly, const ui
     return r;
 }
 
+template <uint32_t kY>
 __global__ __launch_bounds__(256) void k_logexp(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16)
 {
     __shared__ uint8_t L[256], E[512];
@@ -119,12 +120,13 @@ __device__ __forceinline__ uint32_t row_mul(uint32_t x, const uint8_t* M)
            (uint32_t)M[x >> 24] << 24;
 }
 
+template <uint32_t kY>
 __global__ __launch_bounds__(256) void k_mulrow(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16)
 {
     __shared__ uint8_t M[kY][256];
     const uint32_t y0 = (blockIdx.x * 97u + 13u) & 255u;
     for (uint32_t k = 0; k < kY; ++k)
-        M[k][threadIdx.x] = c_mul[(y0 + k) & 255u][threadIdx.x];
+        M[k][threadIdx.x] = c_mul[(y0 + k) & 255u][threadIdx.x];   // (kY x 256 B of LDS)
     __syncthreads();
     for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256u) {
         const uint4 s = src[i];
@@ -186,16 +188,32 @@ int main()
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const char* names[3] = {"perm", "logexp", "mulrow"};
+    for (uint32_t Y : {16u, 64u})
     for (int kind = 0; kind < 3; ++kind) {
         // correctness: one launch from a known dst
         CK(hipMemcpy(dst, hd.data(), bytes, hipMemcpyHostToDevice));
         auto launch = [&]() {
             if (kind == 0)
-                hipLaunchKernelGGL(k_perm, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+                {
+                if (Y == 16)
+                    hipLaunchKernelGGL(k_perm<16>, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+                else
+                    hipLaunchKernelGGL(k_perm<64>, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+            }
             else if (kind == 1)
-                hipLaunchKernelGGL(k_logexp, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+                {
+                if (Y == 16)
+                    hipLaunchKernelGGL(k_logexp<16>, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+                else
+                    hipLaunchKernelGGL(k_logexp<64>, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+            }
             else
-                hipLaunchKernelGGL(k_mulrow, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+                {
+                if (Y == 16)
+                    hipLaunchKernelGGL(k_mulrow<16>, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+                else
+                    hipLaunchKernelGGL(k_mulrow<64>, dim3(blocks), dim3(256), 0, 0, src, dst, n16);
+            }
         };
         launch();
         CK(hipDeviceSynchronize());
@@ -206,7 +224,7 @@ int main()
             const unsigned blk = (unsigned)((lanei / 256) % blocks);
             const unsigned y0 = (blk * 97u + 13u) & 255u;
             uint8_t want = hd[i];
-            for (unsigned k = 0; k < 16; ++k)
+            for (unsigned k = 0; k < Y; ++k)
                 want ^= g_mul[(y0 + k) & 255u][hs[i]];
             if (out[i] != want)
                 ++bad;
@@ -224,9 +242,9 @@ int main()
         }
         std::sort(ms.begin(), ms.end());
         const double t = ms[ms.size() / 2];
-        std::printf("%-7s %8.3f ms per pass over %zu MiB x 16 multipliers: %7.1f G byte-products/s "
+        std::printf("%-7s Y=%-3u %8.3f ms per pass over %zu MiB: %7.1f G byte-products/s "
                     "(HBM %6.1f GB/s), %zu wrong bytes\n",
-                    names[kind], t, bytes >> 20, 16.0 * bytes / t / 1e6, 3.0 * bytes / t / 1e6, bad);
+                    names[kind], Y, t, bytes >> 20, (double)Y * bytes / t / 1e6, 3.0 * bytes / t / 1e6, bad);
     }
     return 0;
 }
