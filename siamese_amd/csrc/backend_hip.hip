@@ -3821,6 +3821,49 @@ void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32
     hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), 0, g_stream, descs, in, results);
 }
 
+namespace {
+
+// How a launch of many solves runs (launches of fewer than kSolvePrefixSplit
+// solves always take the fused sweeps)
+enum SolvePath
+{
+    kPathSweeps = 0,   // k_solve_prefix + k_solve_main
+    kPathMfma = 1,     // k_solve_pre + k_solve_mfma + k_solve_main
+    kPathVector = 2,   // k_solve_pre + k_solve_tr + k_solve_main
+};
+
+void launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
+                  const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct, uint32_t solveBegin,
+                  uint32_t solveCount, SolvePath path)
+{
+    const uint32_t rowsCap = maxRows < kSolveLdsMaxRows ? maxRows : kSolveLdsMaxRows;
+    // Many solves: their prefixes in one wave each first (once per solve, all
+    // in parallel); few (single-stream flushes): fused into the tiles, one
+    // launch fewer on the flush's critical path.
+    const bool separate = solveCount >= kSolvePrefixSplit;
+    const bool mfma = separate && path == kPathMfma;
+    const bool tr = separate && path == kPathVector;
+    unsigned long long* acctL = reinterpret_cast<unsigned long long*>(acct);
+    const uint32_t prodCap = rowsCap < kMfmaMaxRows ? rowsCap : kMfmaMaxRows;
+    if (tr || mfma)
+        hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
+                           g_stream, solves + solveBegin, rows, coef, results, acctL, solveCount);
+    if (tr)
+        hipLaunchKernelGGL(k_solve_tr, dim3(count), dim3(kTrThreads), (size_t)solve_tr_lds_bytes(prodCap), g_stream,
+                           solves, rows, results, items);
+    else if (mfma)
+        hipLaunchKernelGGL(k_solve_mfma, dim3(solveCount * kMfmaGroups), dim3(kMfmaThreads),
+                           (size_t)solve_mfma_lds_bytes(prodCap), g_stream, solves + solveBegin, rows, results);
+    else if (separate)
+        hipLaunchKernelGGL(k_solve_prefix, dim3(solveCount), dim3(64), (size_t)solve_prefix_lds_bytes(rowsCap),
+                           g_stream, solves + solveBegin, rows, coef, results, acctL);
+    hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
+                       (size_t)solve_launch_lds_bytes(rowsCap, !separate), g_stream, solves, rows, coef, results,
+                       items, acctL, (separate ? 1u : 0u) | (mfma ? 2u : 0u) | (tr ? 4u : 0u));
+}
+
+} // namespace
+
 void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
                      const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
                      uint32_t solveBegin, uint32_t solveCount)
@@ -3828,53 +3871,216 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
     if (count == 0)
         return;
     Timed t(kBeSolve);
-    const uint32_t rowsCap = maxRows < kSolveLdsMaxRows ? maxRows : kSolveLdsMaxRows;
-    // Many solves: their prefixes in one wave each first (once per solve, all
-    // in parallel); few (single-stream flushes): fused into the tiles, one
-    // launch fewer on the flush's critical path.
-    const bool separate = solveCount >= kSolvePrefixSplit;
-    // SGPU_MFMA_SOLVE=1: the solves whose lengths all come out valid on the
-    // matrix cores (the prefix pass and the solves' inverses in one launch,
-    // then the products).  Off by default: on the headline it measured
-    // slower than the sweeps (k_solve_pre 80 + k_solve_mfma 322 us per launch
-    // against k_solve_prefix 58 + k_solve_main 277; profiles/r4l_*)
-    static const bool kMfmaSolve = [] {
-        const char* v = std::getenv("SGPU_MFMA_SOLVE");
-        return v && std::atoi(v) != 0;
-    }();
-    // Default: the same solves as X = T R on the vector ALUs, in place
-    // (k_solve_pre 80 + k_solve_tr 114 + k_solve_main 4 us per headline
-    // launch against k_solve_prefix 58 + k_solve_main 277 for the sweeps;
-    // profiles/r4s_*).  SGPU_TR_SOLVE=0: the sweeps alone.
-    static const bool kTrSolve = [] {
+    // Default: the solves whose lengths all come out valid as X = T R on the
+    // vector ALUs (k_solve_pre 80 + k_solve_tr 114 + k_solve_main 9 us per
+    // headline launch against k_solve_prefix 58 + k_solve_main 277 for the
+    // sweeps; profiles/r4s_*, r4w_*).  SGPU_TR_SOLVE=0: the sweeps alone.
+    // SGPU_MFMA_SOLVE=1: the product on the int8 matrix cores (slower: 80 +
+    // 322 us; profiles/r4l_*).
+    static const SolvePath kPath = [] {
+        const char* m = std::getenv("SGPU_MFMA_SOLVE");
+        if (m && std::atoi(m) != 0)
+            return kPathMfma;
         const char* v = std::getenv("SGPU_TR_SOLVE");
-        return !v || std::atoi(v) != 0;
+        return (!v || std::atoi(v) != 0) ? kPathVector : kPathSweeps;
     }();
-    const bool mfma = separate && kMfmaSolve;
-    const bool tr = separate && !mfma && kTrSolve;
-    if (tr) {
-        hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
-                           g_stream, solves + solveBegin, rows, coef, results,
-                           reinterpret_cast<unsigned long long*>(acct), solveCount);
-        hipLaunchKernelGGL(k_solve_tr, dim3(count), dim3(kTrThreads),
-                           (size_t)solve_tr_lds_bytes(rowsCap < kMfmaMaxRows ? rowsCap : kMfmaMaxRows), g_stream,
-                           solves, rows, results, items);
-    } else if (mfma) {
-        hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
-                           g_stream, solves + solveBegin, rows, coef, results,
-                           reinterpret_cast<unsigned long long*>(acct), solveCount);
-        hipLaunchKernelGGL(k_solve_mfma, dim3(solveCount * kMfmaGroups), dim3(kMfmaThreads),
-                           (size_t)solve_mfma_lds_bytes(rowsCap < kMfmaMaxRows ? rowsCap : kMfmaMaxRows), g_stream,
-                           solves + solveBegin, rows, results);
-    } else if (separate) {
-        hipLaunchKernelGGL(k_solve_prefix, dim3(solveCount), dim3(64), (size_t)solve_prefix_lds_bytes(rowsCap),
-                           g_stream, solves + solveBegin, rows, coef, results,
-                           reinterpret_cast<unsigned long long*>(acct));
+    launch_solve(solves, rows, coef, results, items, count, maxRows, acct, solveBegin, solveCount, kPath);
+}
+
+// Test hook: the solve paths against one another on random systems.  Builds
+// `nsolves` (>= kSolvePrefixSplit) solves of 16..80 rows whose true rows carry
+// valid length prefixes and zero bytes past their lengths, as the decoder's
+// recovered originals do (with `corrupt`, every third solve gets non-zero
+// bytes past one row's length: inconsistent recovery data), forms the rows
+// R = L U X the sweeps invert, and runs the sweeps, the vector product and the
+// matrix-core product on copies of them.  stats[0..1]: bytes of the rows (and
+// result words [0..m]) where the vector / matrix-core product's outcome differs
+// from the sweeps'; stats[2..3]: solves those two flagged for the sweeps.
+// Returns 0 when both match the sweeps, 1 when not, -1 on a device error.
+extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(uint32_t seed, uint32_t nsolves,
+                                                                                uint32_t corrupt,
+                                                                                uint32_t* stats)
+{
+    if (nsolves < kSolvePrefixSplit || !gf_init())
+        return -1;
+    bind_device();
+    uint64_t st = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&]() -> uint32_t {
+        st ^= st << 13;
+        st ^= st >> 7;
+        st ^= st << 17;
+        return (uint32_t)(st >> 16);
+    };
+    struct Sys
+    {
+        uint32_t m, maxB, rowBase, coefOff, result;
+        std::vector<uint8_t> C, R;   // C[j*m + i]; rows of maxB bytes
+    };
+    std::vector<Sys> sys(nsolves);
+    uint32_t rows = 0, coefBytes = 0, resWords = 0, maxRows = 0;
+    for (uint32_t s = 0; s < nsolves; ++s) {
+        Sys& y = sys[s];
+        y.m = 16 + rnd() % 65;
+        static const uint32_t kLens[4] = {1402, 600, 1100, 2000};
+        y.maxB = kLens[rnd() % 4];
+        y.rowBase = rows;
+        y.coefOff = coefBytes;
+        y.result = resWords;
+        rows += y.m;
+        coefBytes += (y.m * y.m + 15u) & ~15u;
+        resWords += y.m + 2;
+        maxRows = std::max(maxRows, y.m);
+        const uint32_t m = y.m, B = y.maxB;
+        y.C.resize(m * m);
+        for (uint32_t k = 0; k < m * m; ++k)
+            y.C[k] = (rnd() % 8) ? (uint8_t)rnd() : 0;
+        for (uint32_t i = 0; i < m; ++i)
+            if (!y.C[i * m + i])
+                y.C[i * m + i] = 1 + rnd() % 255;
+        // the true rows: a length prefix, bytes up to the length, zeros after
+        std::vector<uint8_t> X((size_t)m * B, 0);
+        for (uint32_t i = 0; i < m; ++i) {
+            uint8_t* x = &X[(size_t)i * B];
+            uint32_t b;
+            if (rnd() % 4 == 0) {
+                const uint32_t len = 1 + rnd() % 100;   // one-byte prefix
+                x[0] = (uint8_t)len;
+                b = 1 + len;
+            } else {
+                const uint32_t len = 128 + rnd() % (B - 130);   // two-byte prefix
+                x[0] = (uint8_t)(0x80 | (len >> 8));
+                x[1] = (uint8_t)len;
+                b = 2 + len;
+            }
+            for (uint32_t p = (x[0] & 0x80) ? 2 : 1; p < b; ++p)
+                x[p] = (uint8_t)rnd();
+            if (corrupt && s % 3 == 0 && i == m / 2 && b < B)
+                for (unsigned k = 0; k < 3; ++k)
+                    x[b + rnd() % (B - b)] = 1 + rnd() % 255;
+        }
+        // y = U x (upper part with the diagonal), then R = L y (unit lower)
+        std::vector<uint8_t> Y((size_t)m * B, 0);
+        for (uint32_t j = 0; j < m; ++j)
+            for (uint32_t i = j; i < m; ++i)
+                if (const uint8_t c = y.C[j * m + i])
+                    for (uint32_t p = 0; p < B; ++p)
+                        Y[(size_t)j * B + p] ^= gf_mul(X[(size_t)i * B + p], c);
+        y.R = Y;
+        for (uint32_t j = 0; j < m; ++j)
+            for (uint32_t i = 0; i < j; ++i)
+                if (const uint8_t c = y.C[j * m + i])
+                    for (uint32_t p = 0; p < B; ++p)
+                        y.R[(size_t)j * B + p] ^= gf_mul(Y[(size_t)i * B + p], c);
     }
-    hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
-                       (size_t)solve_launch_lds_bytes(rowsCap, !separate), g_stream, solves, rows, coef, results,
-                       items, reinterpret_cast<unsigned long long*>(acct),
-                       (separate ? 1u : 0u) | (mfma ? 2u : 0u) | (tr ? 4u : 0u));
+    // device layout: row buffers of 2 KiB + 1 KiB slack, coefficients,
+    // results, heads, scratch, descriptors, items
+    constexpr uint32_t kRowCap = 3072;
+    std::vector<SolveItem> items;
+    std::vector<SolveDesc> descs(nsolves);
+    std::vector<SolveRow> rdesc(rows);
+    uint64_t scratch = 0;
+    for (uint32_t s = 0; s < nsolves; ++s) {
+        const Sys& y = sys[s];
+        for (uint32_t t = 0; t < y.maxB; t += solve_tile_bytes(y.m))
+            items.push_back(SolveItem{s, t});
+        scratch += solve_t_bytes(y.m) + ((solve_x_bytes(y.m, y.maxB) + 255u) & ~(uint64_t)255u);
+    }
+    uint8_t *dRows = nullptr, *dCoef = nullptr, *dHead = nullptr, *dScratch = nullptr;
+    uint32_t* dRes = nullptr;
+    SolveDesc* dDesc = nullptr;
+    SolveRow* dRowD = nullptr;
+    SolveItem* dItems = nullptr;
+    uint64_t* dAcct = nullptr;
+    bool ok = hipMalloc(&dRows, (size_t)rows * kRowCap) == hipSuccess &&
+              hipMalloc(&dCoef, coefBytes) == hipSuccess && hipMalloc(&dHead, (size_t)rows * 16) == hipSuccess &&
+              hipMalloc(&dScratch, scratch + 256) == hipSuccess &&
+              hipMalloc(&dRes, (size_t)resWords * 4) == hipSuccess &&
+              hipMalloc(&dDesc, nsolves * sizeof(SolveDesc)) == hipSuccess &&
+              hipMalloc(&dRowD, rows * sizeof(SolveRow)) == hipSuccess &&
+              hipMalloc(&dItems, items.size() * sizeof(SolveItem)) == hipSuccess &&
+              hipMalloc(&dAcct, 4 * sizeof(uint64_t)) == hipSuccess;
+    std::vector<uint8_t> hostRows((size_t)rows * kRowCap, 0), hostHead((size_t)rows * 16, 0);
+    std::vector<uint8_t> hostCoef(coefBytes, 0);
+    if (ok) {
+        uint64_t sc = (uint64_t)(uintptr_t)dScratch;
+        for (uint32_t s = 0; s < nsolves; ++s) {
+            const Sys& y = sys[s];
+            SolveDesc& d = descs[s];
+            std::memset(&d, 0, sizeof(d));
+            d.m = y.m;
+            d.rowBegin = y.rowBase;
+            d.coefOffset = y.coefOff;
+            d.result = y.result;
+            d.maxBytes = y.maxB;
+            d.head = (uint64_t)(uintptr_t)(dHead + (size_t)y.rowBase * 16);
+            d.tinv = sc;
+            sc += solve_t_bytes(y.m);
+            d.xout = sc;
+            sc += (solve_x_bytes(y.m, y.maxB) + 255u) & ~(uint64_t)255u;
+            std::memcpy(&hostCoef[y.coefOff], y.C.data(), y.m * y.m);
+            for (uint32_t j = 0; j < y.m; ++j) {
+                const uint32_t r = y.rowBase + j;
+                std::memcpy(&hostRows[(size_t)r * kRowCap], &y.R[(size_t)j * y.maxB], y.maxB);
+                std::memcpy(&hostHead[(size_t)r * 16], &y.R[(size_t)j * y.maxB], 16);
+                SolveRow& w = rdesc[r];
+                std::memset(&w, 0, sizeof(w));
+                w.buf = (uint64_t)(uintptr_t)(dRows + (size_t)r * kRowCap);
+                w.initBytes = w.lowerLen = w.finalBytes = y.maxB;
+            }
+        }
+        ok = hipMemcpy(dCoef, hostCoef.data(), coefBytes, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(dHead, hostHead.data(), hostHead.size(), hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(dDesc, descs.data(), nsolves * sizeof(SolveDesc), hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(dRowD, rdesc.data(), rows * sizeof(SolveRow), hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(dItems, items.data(), items.size() * sizeof(SolveItem), hipMemcpyHostToDevice) == hipSuccess;
+    }
+    std::vector<uint8_t> outRows[3];
+    std::vector<uint32_t> outRes[3];
+    const SolvePath paths[3] = {kPathSweeps, kPathVector, kPathMfma};
+    for (int k = 0; k < 3 && ok; ++k) {
+        ok = hipMemcpy(dRows, hostRows.data(), hostRows.size(), hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemset(dRes, 0xff, (size_t)resWords * 4) == hipSuccess &&
+             hipMemset(dScratch, 0xa5, scratch + 256) == hipSuccess &&
+             hipMemset(dAcct, 0, 4 * sizeof(uint64_t)) == hipSuccess;
+        if (!ok)
+            break;
+        launch_solve(dDesc, dRowD, dCoef, dRes, dItems, (uint32_t)items.size(), maxRows, dAcct, 0, nsolves,
+                     paths[k]);
+        outRows[k].resize(hostRows.size());
+        outRes[k].resize(resWords);
+        ok = hipStreamSynchronize(g_stream) == hipSuccess &&
+             hipMemcpy(outRows[k].data(), dRows, hostRows.size(), hipMemcpyDeviceToHost) == hipSuccess &&
+             hipMemcpy(outRes[k].data(), dRes, (size_t)resWords * 4, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    (void)hipFree(dRows);
+    (void)hipFree(dCoef);
+    (void)hipFree(dHead);
+    (void)hipFree(dScratch);
+    (void)hipFree(dRes);
+    (void)hipFree(dDesc);
+    (void)hipFree(dRowD);
+    (void)hipFree(dItems);
+    (void)hipFree(dAcct);
+    if (!ok)
+        return -1;
+    uint32_t diff[2] = {0, 0}, flagged[2] = {0, 0};
+    for (int k = 1; k < 3; ++k) {
+        for (size_t b = 0; b < hostRows.size(); ++b)
+            diff[k - 1] += outRows[k][b] != outRows[0][b];
+        for (uint32_t s = 0; s < nsolves; ++s) {
+            const Sys& y = sys[s];
+            for (uint32_t w = 0; w <= y.m; ++w)
+                diff[k - 1] += outRes[k][y.result + w] != outRes[0][y.result + w];
+            flagged[k - 1] += outRes[k][y.result + y.m + 1] != 0;
+        }
+    }
+    if (stats) {
+        stats[0] = diff[0];
+        stats[1] = diff[1];
+        stats[2] = flagged[0];
+        stats[3] = flagged[1];
+    }
+    return (diff[0] || diff[1]) ? 1 : 0;
 }
 
 void* be_stage_h2d(void* dst, const void* src, size_t bytes)
