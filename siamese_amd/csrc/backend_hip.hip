@@ -2618,6 +2618,12 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 // clips of the sequential sweeps change nothing).  A solve with a corrupt
 // prefix, or m > kMfmaMaxRows, is left to k_solve_main, which reproduces the
 // reference's partial back-substitution exactly.
+#ifndef SGPU_TBUILD_REGS
+#define SGPU_TBUILD_REGS 0   // 1: rows of T in registers (112 vs 80 us per headline k_solve_pre, profiles/r4z_*)
+#endif
+#ifndef SGPU_PRE_PHASE
+#define SGPU_PRE_PHASE 0   // timing aids (wrong outputs): 1 no inverses, 2 no prefix pass
+#endif
 constexpr unsigned kMfmaWaves = 8;
 constexpr unsigned kMfmaThreads = 64 * kMfmaWaves;
 constexpr unsigned kMfmaYStride = kTStride;            // bytes per row of T in LDS
@@ -2668,6 +2674,96 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
         permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
         permC[tid] = t[4];
     }
+#if SGPU_TBUILD_REGS
+    // Rows of T in registers: half-wave hw (of 16) owns rows hw, hw + 16, ...
+    // (a row is m <= 120 bytes: four per lane of the half-wave).  A pivot
+    // step reads only its source row from LDS, written there by its owner
+    // once final; the coefficients and multiply tables of the next step are
+    // fetched during this one (they do not depend on the rows), so a step
+    // costs one LDS read, the products and a barrier.
+    uint32_t* Yw = reinterpret_cast<uint32_t*>(Y);
+    constexpr uint32_t kHalves = kMfmaThreads / 32;
+    constexpr uint32_t kRows = (kMfmaMaxRows + kHalves - 1) / kHalves;   // rows per half-wave
+    const uint32_t hw = tid >> 5, l32 = tid & 31;
+    uint32_t reg[kRows];
+#pragma unroll
+    for (uint32_t t = 0; t < kRows; ++t) {
+        const uint32_t j = hw + kHalves * t;
+        reg[t] = (j < m && (j >> 2) == l32) ? 1u << (8 * (j & 3)) : 0u;
+    }
+    __syncthreads();   // (Ct and the tables staged)
+    if (hw == 0)
+        Yw[l32] = reg[0];   // row 0 is final for the lower sweep
+    const uint8_t* zero = reinterpret_cast<const uint8_t*>(permL);   // a zero byte: the table of 0
+    // MultiplyLowerTriangle on the identity: row j ^= C[j][i] row i, j > i
+    auto lowerTab = [&](uint32_t i, uint32_t t) -> GfTab {
+        const uint32_t j = hw + kHalves * t;
+        return gf_tab_l(permL, permC, *((i < m && j > i && j < m) ? Ct + i * m + j : zero));
+    };
+    GfTab tn[kRows];
+#pragma unroll
+    for (uint32_t t = 0; t < kRows; ++t)
+        tn[t] = lowerTab(0, t);
+    for (uint32_t i = 0; i + 1 < m; ++i) {
+        GfTab tc[kRows];
+#pragma unroll
+        for (uint32_t t = 0; t < kRows; ++t) {
+            tc[t] = tn[t];
+            tn[t] = lowerTab(i + 1, t);
+        }
+        __syncthreads();
+        const uint32_t src = Yw[i * 32 + l32];
+#pragma unroll
+        for (uint32_t t = 0; t < kRows; ++t)
+            reg[t] ^= gf_mul_tab(src, tc[t]);
+        const uint32_t n = i + 1;   // final now: its owner publishes it
+        if (hw == n % kHalves) {
+#pragma unroll
+            for (uint32_t t = 0; t < kRows; ++t)
+                if (t == n / kHalves)
+                    Yw[n * 32 + l32] = reg[t];
+        }
+    }
+    // BackSubstitution on the result: row j ^= C[j][i] (row i / C[i][i]), j < i
+    auto upperTab = [&](int i, uint32_t t) -> GfTab {
+        const uint32_t j = hw + kHalves * t;
+        return gf_tab_l(permL, permC, *((i > 0 && j < (uint32_t)i) ? Ct + (uint32_t)i * m + j : zero));
+    };
+#pragma unroll
+    for (uint32_t t = 0; t < kRows; ++t)
+        tn[t] = upperTab((int)m - 1, t);
+    for (int i = (int)m - 1; i > 0; --i) {
+        GfTab tc[kRows];
+#pragma unroll
+        for (uint32_t t = 0; t < kRows; ++t) {
+            tc[t] = tn[t];
+            tn[t] = upperTab(i - 1, t);
+        }
+        const GfTab d = gf_tab_l(permL, permC, c_inv[Ct[(uint32_t)i * m + (uint32_t)i]]);
+        __syncthreads();
+        const uint32_t xi = gf_mul_tab(Yw[(uint32_t)i * 32 + l32], d);
+#pragma unroll
+        for (uint32_t t = 0; t < kRows; ++t)
+            reg[t] ^= gf_mul_tab(xi, tc[t]);
+        const uint32_t n = (uint32_t)i - 1;   // final now
+        if (hw == n % kHalves) {
+#pragma unroll
+            for (uint32_t t = 0; t < kRows; ++t)
+                if (t == n / kHalves)
+                    Yw[n * 32 + l32] = reg[t];
+        }
+    }
+    // T = the rows / their diagonal coefficients; rows past m zero
+    GMEM uint32_t* out = reinterpret_cast<GMEM uint32_t*>(sd.tinv);
+#pragma unroll
+    for (uint32_t t = 0; t < kRows; ++t) {
+        const uint32_t j = hw + kHalves * t;
+        if (j < mp)
+            out[j * 32 + l32] =
+                j < m ? gf_mul_tab(reg[t], gf_tab_l(permL, permC, c_inv[Ct[j * m + j]])) : 0u;
+    }
+}
+#else
     // T starts as the identity (rows past m stay zero)
     uint32_t* Yw = reinterpret_cast<uint32_t*>(Y);
     for (uint32_t k = tid; k < mp * (kMfmaYStride / 4); k += kMfmaThreads) {
@@ -2703,6 +2799,7 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
         out[k] = i < m ? gf_mul_tab(Yw[k], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]])) : 0u;
     }
 }
+#endif
 
 __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __restrict__ solves,
                                                           const SolveRow* __restrict__ rows,
@@ -2715,7 +2812,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __r
     const uint32_t tid = threadIdx.x;
     if (blockIdx.x >= count) {
         const SolveDesc sd = solves[blockIdx.x - count];
-        if (sd.m == 0 || sd.m > kMfmaMaxRows || sd.tinv == 0)
+        if (sd.m == 0 || sd.m > kMfmaMaxRows || sd.tinv == 0 || SGPU_PRE_PHASE == 1)
             return;   // (uniform)
         solve_tbuild(sd, coef + sd.coefOffset, reinterpret_cast<uint8_t*>(X), tid);
         return;
@@ -2742,6 +2839,8 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __r
     }
     if (tid == 0)
         results[sd.result + m + 1] = 0;   // the product solves' tail flag
+    if (SGPU_PRE_PHASE == 2)
+        return;
     // (every wave stages; then wave 0 alone runs the serial pass)
     stage_transposed<kMfmaThreads, 2>(Ct, C, m, tid);
     for (uint32_t j = tid; j < m; j += kMfmaThreads) {
@@ -2905,7 +3004,12 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
 #ifndef SGPU_TR_LDS_TABLES
 #define SGPU_TR_LDS_TABLES 0
 #endif
+#ifndef SGPU_TR_SPLIT
+#define SGPU_TR_SPLIT 1
+#endif
 constexpr unsigned kTrWaves = SGPU_TR_WAVES;
+constexpr unsigned kTrSplit = SGPU_TR_SPLIT;            // workgroups per (solve, tile)
+constexpr unsigned kTrStep = kTrWaves * kTrSplit;       // output row stride of a wave
 constexpr unsigned kTrThreads = 64 * kTrWaves;
 constexpr uint32_t kTrTableBytes = SGPU_TR_LDS_TABLES ? 256u * 20u : 0u;
 
@@ -2943,12 +3047,15 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
         X[j * 64u + lane] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     // this wave's rows of T (lane l < 32: bytes 4 l .. 4 l + 3 of each)
-    const uint32_t rw = wave < m ? (m - wave + kTrWaves - 1) / kTrWaves : 0;
+    // output rows r0 + kTrStep t of this wave (kTrSplit workgroups share a
+    // tile, each its own rows)
+    const uint32_t r0 = wave + kTrWaves * (kTrSplit > 1 ? blockIdx.x % kTrSplit : 0u);
+    const uint32_t rw = r0 < m ? (m - r0 + kTrStep - 1) / kTrStep : 0;
     uint32_t trow[RW];
 #pragma unroll
     for (unsigned t = 0; t < RW; ++t)
         trow[t] = (t < rw && lane < kTStride / 4)
-                      ? ld4(sd.tinv + (uint64_t)(wave + kTrWaves * t) * kTStride + 4u * lane)
+                      ? ld4(sd.tinv + (uint64_t)(r0 + kTrStep * t) * kTStride + 4u * lane)
                       : 0u;
     __syncthreads();
 
@@ -2992,10 +3099,14 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
 #pragma unroll
                 for (unsigned u = 0; u < kG && t0 + u < RW; ++u) {
 #pragma unroll
-                    for (unsigned q = 0; q < NQ; ++q)
-                        acc[t0 + u][q] ^= __builtin_amdgcn_perm(tb[u].a1, tb[u].a0, sa[q]) ^
-                                          __builtin_amdgcn_perm(tb[u].b1, tb[u].b0, sb[q]) ^
-                                          __builtin_amdgcn_perm(0u, tb[u].c, sc[q]);
+                    for (unsigned q = 0; q < NQ; ++q) {
+                        // (v_bitop3_b32 0x96 = three-way XOR: two XORs per
+                        // product instead of three)
+                        const uint32_t pa = __builtin_amdgcn_perm(tb[u].a1, tb[u].a0, sa[q]);
+                        const uint32_t pb = __builtin_amdgcn_perm(tb[u].b1, tb[u].b0, sb[q]);
+                        const uint32_t pc = __builtin_amdgcn_perm(0u, tb[u].c, sc[q]);
+                        acc[t0 + u][q] = __builtin_amdgcn_bitop3_b32(acc[t0 + u][q], pa, pb, 0x96) ^ pc;
+                    }
                 }
             }
         }
@@ -3010,7 +3121,7 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
 #pragma unroll
     for (unsigned t = 0; t < RW; ++t) {
         if (t < rw) {
-            const uint32_t i = wave + kTrWaves * t;
+            const uint32_t i = r0 + kTrStep * t;
             const uint32_t w = res[1 + i];
             const uint32_t bb = (w >> 29) + (w & kSolveLengthMask), fb = R[i].finalBytes;
             const uint64_t out = sd.xout + (uint64_t)i * xs;
@@ -3034,8 +3145,8 @@ __device__ __forceinline__ void solve_tr_rows(const SolveDesc& sd, const SolveRo
 {
     // output rows per wave: ceil(m / 8) <= 15 (m <= kMfmaMaxRows), rounded
     // up to one of these
-    static_assert(kMfmaMaxRows <= 15 * kTrWaves && kTrThreads <= 1024, "k_solve_tr keeps at most 15 rows per wave");
-    const uint32_t rw = (sd.m + kTrWaves - 1) / kTrWaves;
+    static_assert(kMfmaMaxRows <= 15 * kTrStep && kTrThreads <= 1024, "k_solve_tr keeps at most 15 rows per wave");
+    const uint32_t rw = (sd.m + kTrStep - 1) / kTrStep;
     switch (rw) {
     case 1:
     case 2: solve_tr_tile<NQ, 2>(sd, R, res, tileBase, X); break;
@@ -3059,7 +3170,7 @@ __global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __rest
                                                          const SolveItem* __restrict__ items)
 {
     extern __shared__ uint4 X[];
-    const SolveItem it = items[blockIdx.x];
+    const SolveItem it = items[blockIdx.x / kTrSplit];
     const SolveDesc sd = solves[it.solve];
     if (sd.m == 0 || sd.m > kMfmaMaxRows || sd.tinv == 0 || results[sd.result] != sd.m ||
         it.tileBase >= sd.maxBytes)
@@ -3849,7 +3960,7 @@ void launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* 
         hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
                            g_stream, solves + solveBegin, rows, coef, results, acctL, solveCount);
     if (tr)
-        hipLaunchKernelGGL(k_solve_tr, dim3(count), dim3(kTrThreads), (size_t)solve_tr_lds_bytes(prodCap), g_stream,
+        hipLaunchKernelGGL(k_solve_tr, dim3(count * kTrSplit), dim3(kTrThreads), (size_t)solve_tr_lds_bytes(prodCap), g_stream,
                            solves, rows, results, items);
     else if (mfma)
         hipLaunchKernelGGL(k_solve_mfma, dim3(solveCount * kMfmaGroups), dim3(kMfmaThreads),
