@@ -50,7 +50,7 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 STREAMS_PER_GPU = 1024
 METRIC = "device-resident GB/s encode+decode, 1400B pkts @20% loss; % HBM peak"
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r4r_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r4ac_traffic.json")
 
 
 def pmc_traffic(kernel):

@@ -58,8 +58,9 @@ __device__ __forceinline__ uint32_t gf_mul_dword(uint32_t x, uint32_t y)
     const uint32_t a = x & 0x07070707u;
     const uint32_t b = (x >> 3) & 0x07070707u;
     const uint32_t c = (x >> 6) & 0x03030303u;
-    return __builtin_amdgcn_perm(t[1], t[0], a) ^ __builtin_amdgcn_perm(t[3], t[2], b) ^
-           __builtin_amdgcn_perm(0u, t[4], c);
+    // (v_bitop3_b32 0x96: the three lookups' XOR in one full-rate instruction)
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t[1], t[0], a), __builtin_amdgcn_perm(t[3], t[2], b),
+                                       __builtin_amdgcn_perm(0u, t[4], c), 0x96);
 }
 
 // the same multiply with y's three lookup words already in registers (per
@@ -87,8 +88,8 @@ __device__ __forceinline__ uint32_t gf_mul_tab(uint32_t x, const GfTab& t)
     const uint32_t a = x & 0x07070707u;
     const uint32_t b = (x >> 3) & 0x07070707u;
     const uint32_t c = (x >> 6) & 0x03030303u;
-    return __builtin_amdgcn_perm(t.a1, t.a0, a) ^ __builtin_amdgcn_perm(t.b1, t.b0, b) ^
-           __builtin_amdgcn_perm(0u, t.c, c);
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t.a1, t.a0, a), __builtin_amdgcn_perm(t.b1, t.b0, b),
+                                       __builtin_amdgcn_perm(0u, t.c, c), 0x96);
 }
 
 __device__ __forceinline__ uint4 gf_mul16(uint4 v, uint32_t y)
@@ -2162,8 +2163,9 @@ __device__ __forceinline__ uint4 gf_mul16_split(const Split16& s, const GfTab& t
     uint32_t r[4];
 #pragma unroll
     for (unsigned k = 0; k < 4; ++k)
-        r[k] = __builtin_amdgcn_perm(t.a1, t.a0, s.a[k]) ^ __builtin_amdgcn_perm(t.b1, t.b0, s.b[k]) ^
-               __builtin_amdgcn_perm(0u, t.c, s.c[k]);
+        r[k] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t.a1, t.a0, s.a[k]),
+                                           __builtin_amdgcn_perm(t.b1, t.b0, s.b[k]),
+                                           __builtin_amdgcn_perm(0u, t.c, s.c[k]), 0x96);
     return make_uint4(r[0], r[1], r[2], r[3]);
 }
 
