@@ -9,16 +9,23 @@
 //                  of up to thousands of source symbols into one destination,
 //                  OP_ROWS Siamese row batches staged in LDS
 //   k_ldpc         the LDPC picks of wide rows (windows of >= 512 elements)
-//   k_solve_prefix solve bytes 0..3 of every row of each triangular system
-//                  (one wave per solve) to learn the recovered lengths
-//   k_solve_main   lower-triangle multiply + back-substitution per tile
+//   k_solve_pre    per solve: bytes 0..3 of every row (the recovered lengths,
+//                  one wave) beside the inverse T = U^-1 L^-1 of its matrix
+//   k_solve_tr     X = T R on the vector ALUs, per (solve, 1 KiB tile)
+//   k_solve_main   the copy of a product-solved tile, or lower-triangle
+//                  multiply + back-substitution per tile (the reference's
+//                  sweeps: small launches, flagged solves)
+//   k_solve_prefix the length pass alone (sweeps-only launches)
+//   k_solve_mfma   X = T R on the int8 matrix cores (opt-in)
+//   k_ge           a decode's recovery matrix and its elimination (opt-in)
 //
 // GF(256) multiply by a wave-uniform constant uses three v_perm_b32 byte
-// lookups per dword (bits 0-2, 3-5, 6-7 of each byte); the 32-byte table per
-// constant lives in constant memory.  The algorithmic roofline is HBM
-// bandwidth, but the measured bounds are on-chip: k_exec waits on LDS
-// staging and its per-op barriers (SQ_WAIT_ANY ~60 %, real HBM traffic about
-// a tenth of peak), and k_solve_main is VALU-issue-bound.
+// lookups per dword (bits 0-2, 3-5, 6-7 of each byte) and one v_bitop3_b32
+// to XOR them; the 32-byte table per constant lives in constant memory.  The
+// algorithmic roofline is HBM bandwidth, but the measured bounds are
+// on-chip: k_exec waits on LDS staging and its per-op barriers (SQ_WAIT_ANY
+// ~60 %, real HBM traffic about a tenth of peak), k_solve_tr on v_perm_b32
+// issue (half rate) and its per-pivot waits.
 #include <hip/hip_runtime.h>
 
 #include "backend.h"

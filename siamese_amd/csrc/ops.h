@@ -272,11 +272,11 @@ struct SolveDesc
                          // tile can solve the length prefixes while tile 0
                          // overwrites the rows
     uint64_t tinv;       // device scratch of solve_t_bytes(m) for the solve's
-                         // inverse T (matrix-core path; 0: none)
+                         // inverse T (product solves; 0: none)
     uint64_t xout;       // device scratch of solve_x_bytes(m, maxBytes): the
-                         // matrix-core path's result rows, copied into the
-                         // rows by the tile pass (several workgroups write
-                         // one solve's rows, so not in place)
+                         // product solves' result rows, copied into the rows
+                         // by the tile pass unless the solve is flagged (the
+                         // rows keep their inputs for the exact sweeps)
 };
 
 /// Solves of up to this many rows may run on the matrix cores (their
