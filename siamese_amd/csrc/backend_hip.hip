@@ -4203,9 +4203,31 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
     return (diff[0] || diff[1]) ? 1 : 0;
 }
 
+// H2D staging as a kernel reading mapped pinned memory over the bus (on the
+// staging stream), so the copy engines are left to the gathers' D2H copies:
+// SGPU_H2D_KERNEL=1 (measured in the end-to-end leg)
+__global__ __launch_bounds__(256) void k_h2d(uint4* __restrict__ dst, const uint4* __restrict__ src, uint64_t words)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    for (; i + 3 * stride < words; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < words; i += stride)
+        dst[i] = src[i];
+}
+
 void* be_stage_h2d(void* dst, const void* src, size_t bytes)
 {
     bind_device();
+    static const bool kKernelH2D = [] {
+        const char* v = std::getenv("SGPU_H2D_KERNEL");
+        return v && std::atoi(v) != 0;
+    }();
     hipEvent_t e = nullptr;
     {
         std::lock_guard<std::mutex> g(g_evMu);
@@ -4216,8 +4238,21 @@ void* be_stage_h2d(void* dst, const void* src, size_t bytes)
     }
     if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
         return nullptr;
-    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g_stageStream) != hipSuccess ||
-        hipEventRecord(e, g_stageStream) != hipSuccess)
+    void* mapped = nullptr;
+    const size_t head = bytes & ~(size_t)15;
+    if (kKernelH2D && head && (((uintptr_t)dst | (uintptr_t)src) & 15u) == 0 &&
+        hipHostGetDevicePointer(&mapped, const_cast<void*>(src), 0) == hipSuccess && mapped) {
+        const uint64_t words = head / 16;
+        const unsigned blocks = (unsigned)std::min<uint64_t>(2048, (words + 1023) / 1024);
+        hipLaunchKernelGGL(k_h2d, dim3(std::max(1u, blocks)), dim3(256), 0, g_stageStream, static_cast<uint4*>(dst),
+                           static_cast<const uint4*>(mapped), words);
+        if (bytes > head && hipMemcpyAsync(static_cast<uint8_t*>(dst) + head, static_cast<const uint8_t*>(src) + head,
+                                           bytes - head, hipMemcpyHostToDevice, g_stageStream) != hipSuccess)
+            return nullptr;
+    } else if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g_stageStream) != hipSuccess) {
+        return nullptr;
+    }
+    if (hipEventRecord(e, g_stageStream) != hipSuccess)
         return nullptr;
     return e;
 }
