@@ -2627,9 +2627,6 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 // clips of the sequential sweeps change nothing).  A solve with a corrupt
 // prefix, or m > kMfmaMaxRows, is left to k_solve_main, which reproduces the
 // reference's partial back-substitution exactly.
-#ifndef SGPU_TBUILD_REGS
-#define SGPU_TBUILD_REGS 0   // 1: rows of T in registers (112 vs 80 us per headline k_solve_pre, profiles/r4z_*)
-#endif
 #ifndef SGPU_PRE_PHASE
 #define SGPU_PRE_PHASE 0   // timing aids (wrong outputs): 1 no inverses, 2 no prefix pass
 #endif
@@ -2683,96 +2680,6 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
         permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
         permC[tid] = t[4];
     }
-#if SGPU_TBUILD_REGS
-    // Rows of T in registers: half-wave hw (of 16) owns rows hw, hw + 16, ...
-    // (a row is m <= 120 bytes: four per lane of the half-wave).  A pivot
-    // step reads only its source row from LDS, written there by its owner
-    // once final; the coefficients and multiply tables of the next step are
-    // fetched during this one (they do not depend on the rows), so a step
-    // costs one LDS read, the products and a barrier.
-    uint32_t* Yw = reinterpret_cast<uint32_t*>(Y);
-    constexpr uint32_t kHalves = kMfmaThreads / 32;
-    constexpr uint32_t kRows = (kMfmaMaxRows + kHalves - 1) / kHalves;   // rows per half-wave
-    const uint32_t hw = tid >> 5, l32 = tid & 31;
-    uint32_t reg[kRows];
-#pragma unroll
-    for (uint32_t t = 0; t < kRows; ++t) {
-        const uint32_t j = hw + kHalves * t;
-        reg[t] = (j < m && (j >> 2) == l32) ? 1u << (8 * (j & 3)) : 0u;
-    }
-    __syncthreads();   // (Ct and the tables staged)
-    if (hw == 0)
-        Yw[l32] = reg[0];   // row 0 is final for the lower sweep
-    const uint8_t* zero = reinterpret_cast<const uint8_t*>(permL);   // a zero byte: the table of 0
-    // MultiplyLowerTriangle on the identity: row j ^= C[j][i] row i, j > i
-    auto lowerTab = [&](uint32_t i, uint32_t t) -> GfTab {
-        const uint32_t j = hw + kHalves * t;
-        return gf_tab_l(permL, permC, *((i < m && j > i && j < m) ? Ct + i * m + j : zero));
-    };
-    GfTab tn[kRows];
-#pragma unroll
-    for (uint32_t t = 0; t < kRows; ++t)
-        tn[t] = lowerTab(0, t);
-    for (uint32_t i = 0; i + 1 < m; ++i) {
-        GfTab tc[kRows];
-#pragma unroll
-        for (uint32_t t = 0; t < kRows; ++t) {
-            tc[t] = tn[t];
-            tn[t] = lowerTab(i + 1, t);
-        }
-        __syncthreads();
-        const uint32_t src = Yw[i * 32 + l32];
-#pragma unroll
-        for (uint32_t t = 0; t < kRows; ++t)
-            reg[t] ^= gf_mul_tab(src, tc[t]);
-        const uint32_t n = i + 1;   // final now: its owner publishes it
-        if (hw == n % kHalves) {
-#pragma unroll
-            for (uint32_t t = 0; t < kRows; ++t)
-                if (t == n / kHalves)
-                    Yw[n * 32 + l32] = reg[t];
-        }
-    }
-    // BackSubstitution on the result: row j ^= C[j][i] (row i / C[i][i]), j < i
-    auto upperTab = [&](int i, uint32_t t) -> GfTab {
-        const uint32_t j = hw + kHalves * t;
-        return gf_tab_l(permL, permC, *((i > 0 && j < (uint32_t)i) ? Ct + (uint32_t)i * m + j : zero));
-    };
-#pragma unroll
-    for (uint32_t t = 0; t < kRows; ++t)
-        tn[t] = upperTab((int)m - 1, t);
-    for (int i = (int)m - 1; i > 0; --i) {
-        GfTab tc[kRows];
-#pragma unroll
-        for (uint32_t t = 0; t < kRows; ++t) {
-            tc[t] = tn[t];
-            tn[t] = upperTab(i - 1, t);
-        }
-        const GfTab d = gf_tab_l(permL, permC, c_inv[Ct[(uint32_t)i * m + (uint32_t)i]]);
-        __syncthreads();
-        const uint32_t xi = gf_mul_tab(Yw[(uint32_t)i * 32 + l32], d);
-#pragma unroll
-        for (uint32_t t = 0; t < kRows; ++t)
-            reg[t] ^= gf_mul_tab(xi, tc[t]);
-        const uint32_t n = (uint32_t)i - 1;   // final now
-        if (hw == n % kHalves) {
-#pragma unroll
-            for (uint32_t t = 0; t < kRows; ++t)
-                if (t == n / kHalves)
-                    Yw[n * 32 + l32] = reg[t];
-        }
-    }
-    // T = the rows / their diagonal coefficients; rows past m zero
-    GMEM uint32_t* out = reinterpret_cast<GMEM uint32_t*>(sd.tinv);
-#pragma unroll
-    for (uint32_t t = 0; t < kRows; ++t) {
-        const uint32_t j = hw + kHalves * t;
-        if (j < mp)
-            out[j * 32 + l32] =
-                j < m ? gf_mul_tab(reg[t], gf_tab_l(permL, permC, c_inv[Ct[j * m + j]])) : 0u;
-    }
-}
-#else
     // T starts as the identity (rows past m stay zero)
     uint32_t* Yw = reinterpret_cast<uint32_t*>(Y);
     for (uint32_t k = tid; k < mp * (kMfmaYStride / 4); k += kMfmaThreads) {
@@ -2808,7 +2715,6 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
         out[k] = i < m ? gf_mul_tab(Yw[k], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]])) : 0u;
     }
 }
-#endif
 
 __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __restrict__ solves,
                                                           const SolveRow* __restrict__ rows,
