@@ -2721,12 +2721,14 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __r
                                                           const uint8_t* __restrict__ coef,
                                                           uint32_t* __restrict__ results,
                                                           unsigned long long* __restrict__ acct,
-                                                          uint32_t count)
+                                                          uint32_t count, uint32_t mode)
 {
+    // mode 0: workgroups [0, count) prefix passes, [count, 2 count) inverses;
+    // 1: inverses only (workgroup b: solve b); 2: prefix passes only
     extern __shared__ uint4 X[];
     const uint32_t tid = threadIdx.x;
-    if (blockIdx.x >= count) {
-        const SolveDesc sd = solves[blockIdx.x - count];
+    if (mode == 1 || (mode == 0 && blockIdx.x >= count)) {
+        const SolveDesc sd = solves[mode == 1 ? blockIdx.x : blockIdx.x - count];
         if (sd.m == 0 || sd.m > kMfmaMaxRows || sd.tinv == 0 || SGPU_PRE_PHASE == 1)
             return;   // (uniform)
         solve_tbuild(sd, coef + sd.coefOffset, reinterpret_cast<uint8_t*>(X), tid);
@@ -3367,6 +3369,10 @@ namespace {
 hipStream_t g_stream = nullptr;
 hipStream_t g_stageStream = nullptr;    // application H2D staging (be_stage_h2d)
 hipStream_t g_gatherStream = nullptr;   // gathers of completed results (be_gather)
+hipStream_t g_invStream = nullptr;      // the product solves' inverses beside k_exec (be_prepare_solve)
+std::mutex g_invMu;
+std::deque<hipEvent_t> g_invPending;    // one per prepared solve phase, in launch order
+std::vector<hipEvent_t> g_invFree;
 bool g_ready = false;
 int g_device = 0;
 
@@ -3530,7 +3536,8 @@ bool be_init(int device, const char** err)
         return false;
     }
     if (hipStreamCreateWithFlags(&g_stageStream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&g_gatherStream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&g_gatherStream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&g_invStream, hipStreamNonBlocking) != hipSuccess) {
         *err = "hipStreamCreate (transfer streams) failed";
         return false;
     }
@@ -3871,9 +3878,24 @@ void launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* 
     const bool tr = separate && path == kPathVector;
     unsigned long long* acctL = reinterpret_cast<unsigned long long*>(acct);
     const uint32_t prodCap = rowsCap < kMfmaMaxRows ? rowsCap : kMfmaMaxRows;
+    // the inverses, when be_prepare_solve started them on the side stream
+    hipEvent_t inv = nullptr;
+    if (tr) {
+        std::lock_guard<std::mutex> g(g_invMu);
+        if (!g_invPending.empty()) {
+            inv = g_invPending.front();
+            g_invPending.pop_front();
+        }
+    }
     if (tr || mfma)
-        hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
-                           g_stream, solves + solveBegin, rows, coef, results, acctL, solveCount);
+        hipLaunchKernelGGL(k_solve_pre, dim3(inv ? solveCount : 2 * solveCount), dim3(kMfmaThreads),
+                           (size_t)solve_pre_lds_bytes(rowsCap), g_stream, solves + solveBegin, rows, coef, results,
+                           acctL, solveCount, inv ? 2u : 0u);
+    if (inv) {
+        check(hipStreamWaitEvent(g_stream, inv, 0), "hipStreamWaitEvent(inverses)");
+        std::lock_guard<std::mutex> g(g_invMu);
+        g_invFree.push_back(inv);
+    }
     if (tr)
         hipLaunchKernelGGL(k_solve_tr, dim3(count * kTrSplit), dim3(kTrThreads), (size_t)solve_tr_lds_bytes(prodCap), g_stream,
                            solves, rows, results, items);
@@ -3890,19 +3912,16 @@ void launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* 
 
 } // namespace
 
-void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
-                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
-                     uint32_t solveBegin, uint32_t solveCount)
+namespace {
+
+// Default: the solves whose lengths all come out valid as X = T R on the
+// vector ALUs (k_solve_pre 80 + k_solve_tr 103 + k_solve_main 9 us per
+// headline launch against k_solve_prefix 58 + k_solve_main 277 for the
+// sweeps; profiles/r4ac_*).  SGPU_TR_SOLVE=0: the sweeps alone.
+// SGPU_MFMA_SOLVE=1: the product on the int8 matrix cores (slower: 80 +
+// 322 us; profiles/r4l_*).
+SolvePath solve_path()
 {
-    if (count == 0)
-        return;
-    Timed t(kBeSolve);
-    // Default: the solves whose lengths all come out valid as X = T R on the
-    // vector ALUs (k_solve_pre 80 + k_solve_tr 114 + k_solve_main 9 us per
-    // headline launch against k_solve_prefix 58 + k_solve_main 277 for the
-    // sweeps; profiles/r4s_*, r4w_*).  SGPU_TR_SOLVE=0: the sweeps alone.
-    // SGPU_MFMA_SOLVE=1: the product on the int8 matrix cores (slower: 80 +
-    // 322 us; profiles/r4l_*).
     static const SolvePath kPath = [] {
         const char* m = std::getenv("SGPU_MFMA_SOLVE");
         if (m && std::atoi(m) != 0)
@@ -3910,7 +3929,69 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
         const char* v = std::getenv("SGPU_TR_SOLVE");
         return (!v || std::atoi(v) != 0) ? kPathVector : kPathSweeps;
     }();
-    launch_solve(solves, rows, coef, results, items, count, maxRows, acct, solveBegin, solveCount, kPath);
+    return kPath;
+}
+
+// SGPU_INV_SIDE=1: the inverses on a side stream during the exec launches
+// instead of in k_solve_pre beside the prefix passes.  Off: the solve phase
+// gets 25 us shorter but k_exec, sharing the CUs, 18 us longer per launch,
+// and device time per step rises (2.40-2.42 vs 2.34-2.36 ms,
+// profiles/r4ai_side_ab.txt)
+bool inverses_aside()
+{
+    static const bool on = [] {
+        const char* v = std::getenv("SGPU_INV_SIDE");
+        return v && std::atoi(v) != 0;
+    }();
+    return on;
+}
+
+hipEvent_t take_event()
+{
+    {
+        std::lock_guard<std::mutex> g(g_invMu);
+        if (!g_invFree.empty()) {
+            hipEvent_t e = g_invFree.back();
+            g_invFree.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(inverses)");
+    return e;
+}
+
+} // namespace
+
+void be_prepare_solve(const SolveDesc* solves, const uint8_t* coef, uint32_t maxRows, uint32_t solveBegin,
+                      uint32_t solveCount)
+{
+    if (solveCount < kSolvePrefixSplit || solve_path() != kPathVector || !inverses_aside())
+        return;
+    bind_device();
+    const uint32_t rowsCap = maxRows < kSolveLdsMaxRows ? maxRows : kSolveLdsMaxRows;
+    // T reads only the coefficients: it runs on the side stream once the
+    // codec stream has the upload (and the scratch ring zeroed), beside the
+    // submission's exec launches; the solve phase waits for it
+    hipEvent_t start = take_event(), done = take_event();
+    check(hipEventRecord(start, g_stream), "hipEventRecord(inverses)");
+    check(hipStreamWaitEvent(g_invStream, start, 0), "hipStreamWaitEvent(inverses)");
+    hipLaunchKernelGGL(k_solve_pre, dim3(solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
+                       g_invStream, solves + solveBegin, nullptr, coef, nullptr, nullptr, solveCount, 1u);
+    check(hipEventRecord(done, g_invStream), "hipEventRecord(inverses)");
+    std::lock_guard<std::mutex> g(g_invMu);
+    g_invFree.push_back(start);
+    g_invPending.push_back(done);
+}
+
+void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
+                     const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
+                     uint32_t solveBegin, uint32_t solveCount)
+{
+    if (count == 0)
+        return;
+    Timed t(kBeSolve);
+    launch_solve(solves, rows, coef, results, items, count, maxRows, acct, solveBegin, solveCount, solve_path());
 }
 
 // Test hook: the solve paths against one another on random systems.  Builds

@@ -2119,6 +2119,11 @@ void Engine::launch_batch(Batch& bt)
     }
     if (bt.wideZero)
         be_memset(xs.wideDev, 0, xs.wideCap);
+    // (work of the solve phases that needs only the upload may start now)
+    for (const Phase& ph : bt.phases)
+        if (ph.kind != Phase::EXEC)
+            be_prepare_solve((const SolveDesc*)(bt.upBase + bt.oSD), bt.upBase + bt.oCoef, ph.maxRows,
+                             (uint32_t)ph.solveBegin, (uint32_t)ph.solveCount);
     if (bt.nGe)
         be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev);
     // k_ldpc items of every exec phase before the first solve go in one
