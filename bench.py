@@ -263,6 +263,7 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
         "workload": "%d stream%s x %d originals x %d B, %d%% loss" % (
             cfg.streams, "s" if cfg.streams > 1 else "", cfg.originals, cfg.payload_bytes,
             cfg.loss_pct),
+        "add_calls": "range (up to each encode point)" if cfg.add_ranges else "per packet",
         "runs": runs,
         "stream_groups": groups,
         "defer": defer,
@@ -378,7 +379,11 @@ def dropin_threads_leg(library, use_cpu, threads=16, runs=3):
 def legs(library, device, threads, use_cpu):
     cpu_threads = min(16, host_info()["usable_cpus"] or 1)
     specs = [
-        # C2: 1024 streams, Cauchy/parity path; reference on all host cores
+        # C2: 1024 streams, Cauchy/parity path; reference on all host cores.
+        # Per-packet calls: range calls up to each encode point (fixture
+        # C2hr) measured the same wall time (13.2-14.4 vs 13.7-15.8 ms per
+        # run, profiles/r4ak_c2_ranges_ab.txt): a run is bound by its ten
+        # rounds' flush-to-completion latency, not by host CPU
         ("C2", S.replace(S.CONFIGS["C2"], hash_data=0), 3,
          S.replace(S.CONFIGS["C2"], hash_data=0), cpu_threads,
          "the full C2 (1024 streams x 256 x 1400 B)", 4),

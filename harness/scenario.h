@@ -14,6 +14,7 @@
 // issuing exactly the same per-stream call sequence as the sequential driver.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -118,7 +119,8 @@ struct ScenarioConfig
     uint32_t tail_limit;        ///< extra encodes after the last original / block limit
     uint32_t seed;              ///< loss channel seed (1013 = reference kSeed)
     uint32_t hash_data;         ///< 1: digests cover packet bytes; 0: lengths only
-    uint32_t add_ranges;        ///< block mode: originals added by range calls (see Stream::add_ranges)
+    uint32_t add_ranges;        ///< originals added by range calls (see Stream::add_ranges): block mode all
+                                ///< at once; interleaved mode those up to each encode point
 };
 
 /// Per-stream outcome (ctypes-visible).
@@ -170,8 +172,8 @@ inline uint64_t ev(uint64_t type, uint64_t result, uint64_t a = 0, uint64_t b = 
       uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok);
       bool wants_yield_after_decode();        // batch: lengths known after a flush
 
-    Range calls (cfg->add_ranges, block mode; every codec supports them, a
-    per-call API as loops of its single calls):
+    Range calls (cfg->add_ranges; every codec supports them, a per-call API
+    as loops of its single calls):
 
       int  enc_add_range(unsigned firstId, unsigned count, unsigned* firstNum, unsigned* added);
       int  dec_add_range(unsigned firstId, unsigned firstNum, unsigned count, int* results, unsigned* calls);
@@ -296,9 +298,8 @@ struct Stream
     // event log records every call's observed results: the same events as
     // the per-call sequence, without its NeedMoreData probes of packets not
     // yet added (a run's deliveries are fetched once the run is in).
-    void add_ranges()
+    void add_ranges(unsigned n)
     {
-        const unsigned n = cfg->originals - i;
         unsigned first = 0, added = 0;
         const int r = codec->enc_add_range(packet_id(i), n, &first, &added);
         const unsigned i0 = i;
@@ -404,7 +405,20 @@ struct Stream
                 return false;
             }
             if (cfg->add_ranges && cfg->block_mode) {
-                add_ranges();
+                add_ranges(cfg->originals - i);
+                return false;
+            }
+            if (cfg->add_ranges) {
+                // interleaved: the originals up to the next encode point in
+                // one range call, then that encode, then one acknowledgement
+                // (the per-call sequence acknowledges after every add)
+                const unsigned iv = cfg->recovery_interval, ph = cfg->recovery_phase % iv;
+                const unsigned toEncode = (ph + iv - i % iv) % iv;   // originals after i before the encode point
+                const unsigned n = std::min(cfg->originals - i, toEncode + 1);
+                add_ranges(n);
+                if (res->status)
+                    return false;
+                phase = ((i - 1) % iv == ph) ? ENCODE : ACK;
                 return false;
             }
             const unsigned id = packet_id(i);

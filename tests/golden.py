@@ -55,6 +55,13 @@ FIXTURES = {
     "C4r": ("C4", dict(hash_data=0, add_ranges=1)),
     "edge_var_block_r": ("C4", dict(streams=32, originals=300, payload_bytes=0, loss_pct=30,
                                     recovery_loss_pct=10, add_ranges=1)),
+    # interleaved configs with range calls: the originals up to each encode
+    # point in one call, one acknowledgement per encode interval (the C2 leg
+    # as bench.py runs it, every byte hashed; lag-based acks; variable sizes)
+    "C2hr": ("C2", dict(hash_data=1, add_ranges=1)),
+    "C2x64r": ("C2", dict(streams=64, add_ranges=1)),
+    "C1r": ("C1", dict(add_ranges=1, streams=8)),
+    "C1var_r": ("C1var", dict(add_ranges=1)),
 }
 
 

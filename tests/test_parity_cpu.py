@@ -16,7 +16,7 @@ import golden
 import scenario_lib as S
 
 SMALL = ["smoke_C4x8", "C1", "C1var", "C2x64", "edge_tiny", "edge_var_block", "edge_heavy",
-         "edge_maxloss", "edge_lag", "smoke_C4x8r", "edge_var_block_r"]
+         "edge_maxloss", "edge_lag", "smoke_C4x8r", "edge_var_block_r", "C2x64r", "C1r", "C1var_r"]
 
 
 def _check(name, results):
@@ -27,7 +27,7 @@ def _check(name, results):
     assert [int(r.status) for r in results] == want["status"]
 
 
-@pytest.mark.parametrize("name", SMALL + ["C3", "C4x256", "C2", "C2h", "C4x1024h", "C4x1024hr"])
+@pytest.mark.parametrize("name", SMALL + ["C3", "C4x256", "C2", "C2h", "C2hr", "C4x1024h", "C4x1024hr"])
 def test_reference_matches_golden(name, ref_available):
     if not ref_available:
         pytest.skip("oracle/_ref not built")
