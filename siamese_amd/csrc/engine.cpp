@@ -1524,7 +1524,11 @@ bool Engine::flush_and_sync(std::shared_mutex* detach)
         return !v || std::atoi(v) != 0;
     }();
     bool inl = false;
-    if (kInline && !async_assembly()) {
+    // (whether or not submissions are laid out by the launcher thread: with
+    // nothing queued or running the caller lays out and launches its own,
+    // and the launcher takes nothing while inlineBusy_ is set; the hand-off
+    // costs the drop-in path ~15 us per flush, profiles/r4ao_dropin_ab.txt)
+    if (kInline) {
         std::lock_guard<std::mutex> g(qMu_);
         // Inline only when the ticket's transfer set is free right now, and
         // claimed in this same critical section: a later ticket of the same
