@@ -12,7 +12,19 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 lib = sys.argv[1]
-bench.main(["--library", lib, "--steps", "3", "--warmup", "1", "--no-cpu", "--no-e2e", "--no-legs"] + sys.argv[2:])
+if len(sys.argv) > 2 and sys.argv[2] in ("C2", "C3", "C5"):
+    # a leg instead of the headline: python tools/phase_clocks.py LIB C3
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import scenario_lib as S  # noqa: E402
+    cfg = S.replace(S.CONFIGS[sys.argv[2]], hash_data=0)
+    sess = S.BatchSession(lib, cfg, device=0)
+    try:
+        sess.run(steps=1, warmup=0, verify=False, threads=0, groups=2 if sys.argv[2] == "C2" else 1,
+                 digest=False, defer=4 if sys.argv[2] == "C2" else 8)
+    finally:
+        sess.close()
+else:
+    bench.main(["--library", lib, "--steps", "3", "--warmup", "1", "--no-cpu", "--no-e2e", "--no-legs"] + sys.argv[2:])
 L = ctypes.CDLL(os.path.abspath(lib))
 out = (ctypes.c_ulonglong * 64)()
 L.sgpu_debug_phase_clocks(out)
