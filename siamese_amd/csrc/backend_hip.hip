@@ -3995,7 +3995,7 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 }
 
 // Test hook: the solve paths against one another on random systems.  Builds
-// `nsolves` (>= kSolvePrefixSplit) solves of 16..80 rows whose true rows carry
+// `nsolves` (>= kSolvePrefixSplit) solves of 16..120 rows whose true rows carry
 // valid length prefixes and zero bytes past their lengths, as the decoder's
 // recovered originals do (with `corrupt`, every third solve gets non-zero
 // bytes past one row's length: inconsistent recovery data), forms the rows
@@ -4027,7 +4027,9 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
     uint32_t rows = 0, coefBytes = 0, resWords = 0, maxRows = 0;
     for (uint32_t s = 0; s < nsolves; ++s) {
         Sys& y = sys[s];
-        y.m = 16 + rnd() % 65;
+        // (every row count the product solves take: 16..120, so every
+        // rows-per-wave variant of k_solve_tr runs)
+        y.m = 16 + rnd() % (kMfmaMaxRows - 15);
         static const uint32_t kLens[4] = {1402, 600, 1100, 2000};
         y.maxB = kLens[rnd() % 4];
         y.rowBase = rows;
