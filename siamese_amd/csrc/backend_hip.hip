@@ -4030,8 +4030,8 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
         // (every row count the product solves take: 16..120, so every
         // rows-per-wave variant of k_solve_tr runs)
         y.m = 16 + rnd() % (kMfmaMaxRows - 15);
-        static const uint32_t kLens[4] = {1402, 600, 1100, 2000};
-        y.maxB = kLens[rnd() % 4];
+        static const uint32_t kLens[6] = {1402, 600, 1100, 2000, 4100, 6000};
+        y.maxB = kLens[rnd() % 6];
         y.rowBase = rows;
         y.coefOff = coefBytes;
         y.result = resWords;
@@ -4081,9 +4081,9 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
                     for (uint32_t p = 0; p < B; ++p)
                         y.R[(size_t)j * B + p] ^= gf_mul(Y[(size_t)i * B + p], c);
     }
-    // device layout: row buffers of 2 KiB + 1 KiB slack, coefficients,
+    // device layout: row buffers of 6 KiB + 2 KiB slack, coefficients,
     // results, heads, scratch, descriptors, items
-    constexpr uint32_t kRowCap = 3072;
+    constexpr uint32_t kRowCap = 8192;
     std::vector<SolveItem> items;
     std::vector<SolveDesc> descs(nsolves);
     std::vector<SolveRow> rdesc(rows);
