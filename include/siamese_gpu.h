@@ -278,7 +278,9 @@ SIAMESE_EXPORT long long sgpu_frames_send(unsigned count, const SgpuRecoveryPack
 SIAMESE_EXPORT void sgpu_timing(int enable, int reset, double* execMs, double* totalMs);
 /// Device milliseconds per kernel class since the last sgpu_timing reset,
 /// while timing is enabled: [0] k_ingest, [1] k_exec, [2] k_ldpc, [3] the
-/// solve kernels (k_solve_prefix + k_solve_main); count entries at most.
+/// solve kernels (k_solve_pre + k_solve_tr + k_solve_main on launches of
+/// >= 16 solves, k_solve_main alone below that), [4] k_ge (sgpu_decode_device);
+/// count entries at most.
 SIAMESE_EXPORT void sgpu_timing_kernels(double* msOut, unsigned count);
 /// Engine counters (15 values): flushes, launches, ops, terms, solves,
 /// ingests, upload bytes, algorithmic op bytes, algorithmic output bytes,

@@ -1,9 +1,10 @@
 // api.cpp -- the drop-in siamese.h entry points (reference siamese.cpp:35-302).
 //
 // Argument validation and result codes follow the reference entry points
-// one-for-one.  Instances are independent: as in the reference, each is used
-// by one thread at a time (siamese.h:57-58), and calls on different instances
-// run concurrently, holding the engine's instance lock shared.  Calls that
+// one-for-one.  The reference API is not thread-safe (siamese.h:59: "a lock
+// should be held while calling").  This library keeps that contract for one
+// instance and extends it: calls on different instances may run concurrently,
+// holding the engine's instance lock shared.  Calls that
 // must hand host memory back to the caller (siamese_encode, siamese_decode,
 // and siamese_decoder_get on a freshly recovered packet) queue their device
 // work, drop the lock and flush: concurrent flushes commit as a group (the
@@ -230,14 +231,19 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder, Siamese
     DecoderCore& core = D(decoder)->core;
     {
         Shared lock;
-        if (!core.pending(packet->PacketNum))
-            return core.get(*packet);
+        const SiameseResult r = core.get(*packet);
+        if (r != kNeedsFlush)
+            return r;
     }
-    // a freshly recovered packet whose exact length is still on the device
+    // a freshly recovered packet whose exact length is still on the device:
+    // flushed outside the instance lock (DecoderCore::get never flushes in
+    // drop-in mode, so no thread waits for the lock's exclusive side while
+    // holding its shared side)
     if (!eng->flush_and_sync(&eng->instance_lock()))
         return Siamese_Disabled;
     Shared lock;
-    return core.get(*packet);
+    const SiameseResult r = core.get(*packet);
+    return r == kNeedsFlush ? Siamese_Disabled : r;
 }
 
 SIAMESE_EXPORT SiameseResult siamese_decoder_is_ready(SiameseDecoder decoder)

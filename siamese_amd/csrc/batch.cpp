@@ -440,6 +440,12 @@ SIAMESE_EXPORT SiameseResult sgpu_frames_recv(const SgpuDecoder* decoders, unsig
             const size_t off = at + f.offset;
             SiameseResult r = Siamese_InvalidInput;
             SgpuDecoder d = f.flow < decoderCount ? decoders[f.flow] : nullptr;
+            // (a decoder with a device matrix job in flight takes no packets:
+            // the job was built from its current window, like every other
+            // sgpu_decoder_* call it answers InvalidInput until decode_device
+            // has finished the job)
+            if (d && BD(d)->core.ge_pending())
+                d = nullptr;
             if (d && f.type == kFrameOriginal) {
                 if (f.bytes <= SIAMESE_MAX_PACKET_BYTES && f.packetNum <= SIAMESE_PACKET_NUM_MAX) {
                     SiameseOriginalPacket p;

@@ -1335,8 +1335,19 @@ SiameseResult DecoderCore::finish_device_ge(SiameseOriginalPacket** packetsOut, 
 {
     {
         std::lock_guard<std::mutex> g(res_->mu);
-        if (!res_->geDone)
-            return kDecodePending;   // (its flush has not completed yet)
+        if (!res_->geDone) {
+            // A failed submission delivers no completions (Engine::wait), so
+            // the job's result never arrives: give the decoder back as the
+            // reference's EmergencyDisabled would, instead of pending forever.
+            if (!dead())
+                return kDecodePending;   // (its flush has not completed yet)
+            geState_ = 0;
+            if (packetsOut) {
+                *packetsOut = nullptr;
+                *countOut = 0;
+            }
+            return Siamese_Disabled;
+        }
         geOut_.swap(res_->geOut);
         res_->geDone = false;
     }
@@ -2075,6 +2086,11 @@ SiameseResult DecoderCore::get(SiameseOriginalPacket& packet)
     }
     if (slot(element).pending) {
         // Exact length still on the device: finish the outstanding work.
+        // The drop-in API calls this under its shared instance lock, which a
+        // detaching flush takes exclusively: it must flush outside the lock
+        // (siamese_decoder_get does), so it gets kNeedsFlush back here.
+        if (mirror_)
+            return kNeedsFlush;
         if (!eng_->flush_and_sync())
             return Siamese_Disabled;
         settle();

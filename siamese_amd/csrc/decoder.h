@@ -31,6 +31,9 @@ namespace sgpu {
 /// decode_device: a matrix job was queued; call again after the flush
 /// (siamese_gpu.h SGPU_DECODE_PENDING)
 constexpr SiameseResult kDecodePending = static_cast<SiameseResult>(6);
+/// DecoderCore::get in drop-in (mirror) mode: the packet's exact length is
+/// still on the device; flush outside the instance lock and call again
+constexpr SiameseResult kNeedsFlush = static_cast<SiameseResult>(7);
 
 struct DecSlot
 {

@@ -437,7 +437,8 @@ public:
     /// Serialises the exclusive siamese_gpu.h calls.
     std::mutex& mutex() { return mu_; }
     /// Shared by the drop-in siamese.h instance calls (each instance used by
-    /// one thread at a time, siamese.h:57-58), exclusive only while a flush
+    /// one thread at a time; concurrent calls on different instances are this
+    /// library's extension of siamese.h:59), exclusive only while a flush
     /// detaches the queued work (flush_and_sync(&instance_lock())).
     std::shared_mutex& instance_lock() { return instMu_; }
 
