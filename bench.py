@@ -16,9 +16,11 @@ value  = algorithmic bytes / step time, summed over ranks (GB/s): the source
          bytes of every GF(256) add/mul/muladd the reference codec performs
          for the same call sequence, plus the recovery packets and recovered
          originals written (counted by the library).
-roofline = the executor kernel k_exec: its share of the algorithmic bytes over
-         its summed launch time (HIP events on the codec's stream), against
-         the 8 TB/s HBM3E peak.
+roofline = the executor kernel k_exec: the bytes it must move per launch (the
+         physical HBM traffic of a committed rocprofv3 PMC capture of this
+         build, else the compulsory bytes the library counts) over its
+         average launch time (HIP events on the codec's stream), against the
+         8 TB/s HBM3E peak.
 cpu_baseline = the upstream reference (oracle/_ref, built from
          /root/reference's own sources) on the host cores, same workload on a
          bounded sample of streams.
@@ -50,18 +52,31 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 STREAMS_PER_GPU = 1024
 METRIC = "device-resident GB/s encode+decode, 1400B pkts @20% loss; % HBM peak"
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r4ac_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r5_traffic.json")
 
 
-def pmc_traffic(kernel):
-    """Per-launch HBM traffic of `kernel` from the committed PMC profile
-    (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py)."""
+def lib_sha256(path):
+    import hashlib
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
+def pmc_traffic(kernel, library):
+    """Per-launch HBM traffic of `kernel` from the committed PMC capture
+    (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per dispatch, tools/pmc_traffic.py)
+    and whether that capture measured the very library this run loads
+    (sha256 of the .so recorded at capture time)."""
     try:
         with open(TRAFFIC_JSON) as f:
             d = json.load(f)
-        return d[kernel]["traffic_bytes"], d.get("_source", TRAFFIC_JSON)
+        want = d.get("_lib_sha256")
+        same = want is not None and want == lib_sha256(library)
+        return d[kernel]["traffic_bytes"], d.get("_source", TRAFFIC_JSON), same
     except (OSError, KeyError, ValueError):
-        return None, None
+        return None, None, False
 
 
 def workload(rank, streams, ranges=True):
@@ -392,7 +407,7 @@ def legs(library, device, threads, use_cpu):
          S.replace(S.CONFIGS["C3"], hash_data=0), 1, "the full C3 (1 stream x 8192 x 1400 B)", 8),
         # C5: one stream of 64 KiB symbols; reference on one core over the
         # first 2000 originals (the whole stream takes it ~15 s)
-        ("C5", S.replace(S.CONFIGS["C5"], hash_data=0), 1,
+        ("C5", S.replace(S.CONFIGS["C5"], hash_data=0), 3,
          S.replace(S.CONFIGS["C5"], hash_data=0, originals=2000), 1,
          "C5's first 2000 originals (1 stream x 2000 x 64 KiB)", 8),
     ]
@@ -431,6 +446,18 @@ def run_rank(rank, world, local, args, library, use_cuda):
     # sample of C4 streams, one run before the timed steps, one after them
     # and one after the end-to-end leg (interleaved with the GPU's runs)
     cb = None
+    side = []   # GPU values of the short side runs taken beside each CPU run
+
+    def side_run():
+        # a few untimed steps of the same workload right beside a CPU run, so
+        # each reference run has a GPU run under the same box conditions
+        # (cpu_baseline.ratio); never part of `value`
+        n = max(3, args.steps // 4)
+        t = time.perf_counter()
+        _, r = sess.run(steps=n, warmup=0, verify=False, threads=args.threads, groups=args.groups,
+                        digest=False, defer=args.defer, device_ge=dge, timing=False)
+        side.append(engine_bytes(r)[1] / (time.perf_counter() - t) / 1e9)
+
     if not args.no_cpu and world == 1:
         threads = min(16, host_info()["usable_cpus"] or 1)
         sample_cfg = S.replace(S.CONFIGS["C4"], streams=args.cpu_streams, first_stream=0,
@@ -438,6 +465,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
         cb = CpuBaseline(sample_cfg, threads, "%d C4 streams (256 x 1400 B, 20%% loss, block mode)"
                          % args.cpu_streams)
         cb.measure()
+        side_run()
 
     coll.barrier()
     t0 = time.perf_counter()
@@ -445,8 +473,14 @@ def run_rank(rank, world, local, args, library, use_cuda):
                         groups=args.groups, digest=False, defer=args.defer, device_ge=dge)
     coll.barrier()
     elapsed = time.perf_counter() - t0
+    # one untimed step that counts the executor's compulsory bytes (every
+    # distinct symbol read once, every output written once: the roofline's
+    # byte figure; counting it costs assembly time, so never in the timed run)
+    _, urep = sess.run(steps=1, warmup=0, verify=False, threads=args.threads, groups=args.groups,
+                       digest=False, defer=args.defer, device_ge=dge, unique=True)
     if cb is not None:
         cb.measure()
+        side_run()
 
     # End-to-end (PCIe-inclusive) leg, timed separately: the originals start
     # in pinned host memory and every recovery packet and recovered original
@@ -469,9 +503,10 @@ def run_rank(rank, world, local, args, library, use_cuda):
                  groups=args.groups, e2e=True, digest=False, defer=args.defer, frames=args.frames, device_ge=dge)
         coll.barrier()
         e2e_elapsed = time.perf_counter() - t1
-    sess.close()
     if cb is not None:
         cb.measure()
+        side_run()
+    sess.close()
 
     eng, alg_bytes = engine_bytes(rep)
     payload = rep.payload_bytes   # (all timed steps)
@@ -493,11 +528,20 @@ def run_rank(rank, world, local, args, library, use_cuda):
     value = alg_total / t_max / 1e9
     exec_s = rep.exec_ms / 1e3
     exec_bytes = alg_bytes - eng["solve_bytes"]
-    achieved = (exec_bytes / exec_s / 1e9) if exec_s > 0 else 0.0
+    achieved_alg = (exec_bytes / exec_s / 1e9) if exec_s > 0 else 0.0
     steps = args.steps
     launches = max(1, eng["exec_launches"])
-    traffic, traffic_src = pmc_traffic("sgpu::k_exec")
+    traffic, traffic_src, traffic_same = pmc_traffic("sgpu::k_exec", library)
     exec_ms_per_launch = rep.exec_ms / launches
+    ueng = S.engine_dict(urep)
+    unique_per_launch = ueng["exec_unique_bytes"] / max(1, ueng["exec_launches"])
+    t_launch = exec_ms_per_launch / 1e3
+    unique_gbps = unique_per_launch / t_launch / 1e9 if t_launch > 0 else 0.0
+    traffic_gbps = traffic / t_launch / 1e9 if traffic and t_launch > 0 else None
+    # the roofline's bytes: the physical HBM traffic of this very build when
+    # a PMC capture of it is committed, the compulsory bytes otherwise
+    phys = traffic_gbps is not None and traffic_same
+    achieved = traffic_gbps if phys else unique_gbps
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -555,20 +599,28 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "frac_basis": ("physical HBM bytes per launch (rocprofv3 PMC capture of this same library build)"
+                           if phys else "compulsory bytes per launch (no PMC capture of this build committed)"),
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "traffic_GBps": (round(traffic / (exec_ms_per_launch / 1e3) / 1e9, 2)
-                             if traffic and exec_ms_per_launch > 0 else None),
-            "traffic_frac": (round(traffic / (exec_ms_per_launch / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)
-                             if traffic and exec_ms_per_launch > 0 else None),
-            "exec_bytes_per_step": exec_bytes // steps,
-            "exec_launches_per_step": eng["exec_launches"] / steps,
-            "exec_bytes_per_launch": exec_bytes // launches,
+            "traffic_build_matches": traffic_same,
+            "traffic_GBps": round(traffic_gbps, 2) if traffic_gbps else None,
+            "traffic_frac": round(traffic_gbps / HBM_PEAK_GBPS, 4) if traffic_gbps else None,
+            "unique_bytes_per_launch": int(unique_per_launch),
+            "unique_GBps": round(unique_gbps, 2),
+            "unique_frac": round(unique_gbps / HBM_PEAK_GBPS, 4),
             "exec_ms_per_launch": round(exec_ms_per_launch, 4),
-            "note": "achieved/frac = k_exec's ALGORITHMIC bytes per launch / its average launch "
-                    "time (HIP events on the codec stream, this run); traffic = measured HBM "
-                    "bytes per launch (rocprofv3 PMC, traffic_source) and traffic_GBps/"
-                    "traffic_frac = that over this run's launch time",
+            "exec_launches_per_step": eng["exec_launches"] / steps,
+            "achieved_alg": round(achieved_alg, 2),
+            "alg_bytes_per_launch": exec_bytes // launches,
+            "alg_bytes_per_step": exec_bytes // steps,
+            "note": "launch time = k_exec's average HIP-event duration on the codec stream in this run; "
+                    "traffic = rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per dispatch of a committed capture "
+                    "(traffic_build_matches: the capture's library sha256 equals this run's); unique = "
+                    "every distinct symbol read once + every output written once + the op stream, counted "
+                    "by the library in one extra untimed step; achieved_alg = SURVEY 8d's ALGORITHMIC "
+                    "bytes (every re-read the reference performs) over the same time: NOT a roofline, "
+                    "the kernel serves those re-reads from LDS",
         },
         "cpu_baseline": None,
         "end_to_end": None,
@@ -589,7 +641,11 @@ def run_rank(rank, world, local, args, library, use_cuda):
                         "(framed by sgpu_frames_send) " if args.frames else ""),
         }
     if cb is not None:
-        line["cpu_baseline"] = cb.result([value] * len(cb.runs))
+        line["cpu_baseline"] = cb.result(side)
+        if line["cpu_baseline"] is not None:
+            line["cpu_baseline"]["ratio_note"] = (
+                "GPU/reference per pair: each reference run beside a short untimed GPU run of the same "
+                "workload (%d steps), both under the same box conditions" % max(3, args.steps // 4))
     return line
 
 

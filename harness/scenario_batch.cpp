@@ -55,6 +55,8 @@ struct BatchOptions
     uint32_t no_timing; ///< timed steps without the per-launch device timing events
     uint32_t device_ge; ///< defer 0: decodes by sgpu_decode_device (recovery matrix generated and
                         ///< eliminated on the device; a decode then takes two submissions)
+    uint32_t unique;    ///< count the executor launches' compulsory bytes (sgpu_measure_unique)
+                        ///< during the run (a measurement run: it costs assembly time)
                         ///< (device_ms / exec_ms read 0): the events order every launch
                         ///< behind a timestamp, tens of microseconds a flush on the
                         ///< latency-bound single-stream legs
@@ -67,7 +69,7 @@ struct BatchReport
     double exec_ms;        ///< device time of the executor launches only
     double setup_seconds;  ///< payload generation + staging (untimed)
     uint64_t rounds;       ///< rounds (flushes) in the timed steps
-    uint64_t engine[17];   ///< engine counters over the timed steps (see sgpu_engine_stats_ex),
+    uint64_t engine[18];   ///< engine counters over the timed steps (see sgpu_engine_stats_ex),
                            ///< then the arena growth (sgpu_arena_bytes)
     uint64_t checked;      ///< packets whose bytes were verified
     uint64_t mismatches;   ///< verification failures
@@ -83,7 +85,7 @@ struct BatchReport
 
 namespace {
 
-constexpr int kEngineStats = 16;
+constexpr int kEngineStats = 17;
 using Clock = std::chrono::steady_clock;
 
 struct Api
@@ -134,6 +136,7 @@ struct Api
     void (*timing)(int, int, double*, double*);
     void (*engine_stats)(uint64_t*);
     void (*engine_stats_ex)(uint64_t*, unsigned);
+    void (*measure_unique)(int);
     void (*timing_kernels)(double*, unsigned);
     uint64_t (*arena_bytes)(void);
     int (*arena_reserve)(size_t);
@@ -192,6 +195,7 @@ bool load_api(const char* path, Api& a)
            bind_optional(h, a.decoder_add_original_range, "sgpu_decoder_add_original_range") &&
            bind_optional(h, a.decoder_get_range, "sgpu_decoder_get_range") &&
            bind_optional(h, a.engine_stats_ex, "sgpu_engine_stats_ex") &&
+           bind_optional(h, a.measure_unique, "sgpu_measure_unique") &&
            bind_optional(h, a.timing_kernels, "sgpu_timing_kernels") &&
            bind_optional(h, a.decode_device, "sgpu_decode_device");
 }
@@ -1265,7 +1269,7 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
             return -2;
         uint64_t e0[kEngineStats + 1], e1[kEngineStats + 1];
         auto stats = [&](uint64_t* e) {
-            e[kEngineStats - 1] = 0;
+            e[kEngineStats - 2] = e[kEngineStats - 1] = 0;
             if (api.engine_stats_ex)
                 api.engine_stats_ex(e, kEngineStats);
             else
@@ -1274,9 +1278,13 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
         };
         stats(e0);
         api.timing(timed && !opt->no_timing ? 1 : 0, 1, nullptr, nullptr);
+        if (api.measure_unique)
+            api.measure_unique(opt->unique ? 1 : 0);
         const auto t1 = Clock::now();
         rc = run_pipeline(sh, results, timed ? opt->steps : 1, &rounds, phase, &payload);
         const double dt = std::chrono::duration<double>(Clock::now() - t1).count();
+        if (api.measure_unique)
+            api.measure_unique(0);
         double execMs = 0, totalMs = 0, kernelMs[5] = {0, 0, 0, 0, 0};
         if (api.timing_kernels)
             api.timing_kernels(kernelMs, 5);

@@ -290,8 +290,16 @@ SIAMESE_EXPORT void sgpu_timing_kernels(double* msOut, unsigned count);
 /// executor launches.
 SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15);
 /// sgpu_engine_stats' 15 values, then the algorithmic bytes of k_ldpc (the
-/// wide rows' picks, part of the algorithmic op bytes); count entries at most.
+/// wide rows' picks, part of the algorithmic op bytes), then the executor
+/// launches' compulsory bytes (see sgpu_measure_unique); count entries at most.
 SIAMESE_EXPORT void sgpu_engine_stats_ex(uint64_t* out, unsigned count);
+/// Measurement aid: while on, flush assembly counts the executor launches'
+/// compulsory bytes -- each distinct source symbol read once, each
+/// destination written once, the op stream once -- into sgpu_engine_stats_ex
+/// [16].  The algorithmic bytes count every re-read of a symbol the reference
+/// performs; this is the traffic a kernel that re-reads nothing from HBM
+/// would move.  Off by default (it sorts every segment's operands).
+SIAMESE_EXPORT void sgpu_measure_unique(int on);
 
 /// Device bytes the engine's symbol arena has taken from hipMalloc so far
 /// (grows while warming up, then stays flat: buffers are recycled).

@@ -530,12 +530,17 @@ SIAMESE_EXPORT void sgpu_timing_kernels(double* msOut, unsigned count)
 SIAMESE_EXPORT void sgpu_engine_stats_ex(uint64_t* out, unsigned count)
 {
     const EngineStats s = Engine::global()->stats();
-    const uint64_t v[16] = {s.flushes,    s.launches,    s.ops,        s.terms,    s.solves,
+    const uint64_t v[17] = {s.flushes,    s.launches,    s.ops,        s.terms,    s.solves,
                             s.ingests,    s.uploadBytes, s.refOpBytes, s.outBytes, s.solveBytes,
                             s.assembleNs, s.waitNs,      s.completeNs, s.reclaimNs,
-                            s.execLaunches, s.ldpcBytes};
-    for (unsigned k = 0; k < count && k < 16; ++k)
+                            s.execLaunches, s.ldpcBytes, s.execUniqueBytes};
+    for (unsigned k = 0; k < count && k < 17; ++k)
         out[k] = v[k];
+}
+
+SIAMESE_EXPORT void sgpu_measure_unique(int on)
+{
+    Engine::set_measure_unique(on != 0);
 }
 
 SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15)

@@ -37,6 +37,7 @@ void EngineStats::add(const EngineStats& o)
     completeNs += o.completeNs;
     reclaimNs += o.reclaimNs;
     execLaunches += o.execLaunches;
+    execUniqueBytes += o.execUniqueBytes;
 }
 
 namespace {
@@ -1350,7 +1351,107 @@ constexpr size_t kParallelWords = 1u << 16;
 #define SGPU_SOLVE_CHUNK 64
 #endif
 
+// ---- compulsory bytes of an executor segment (Engine::set_measure_unique) --
+std::atomic<bool> g_measureUnique{false};
+
+struct Range
+{
+    uint64_t addr;
+    uint32_t len;
+};
+
+// every distinct symbol counted once at the largest extent any op of the
+// segment touches it with
+uint64_t distinct_bytes(std::vector<Range>& v)
+{
+    std::sort(v.begin(), v.end(), [](const Range& a, const Range& b) { return a.addr < b.addr; });
+    uint64_t total = 0;
+    for (size_t i = 0; i < v.size();) {
+        uint32_t len = v[i].len;
+        size_t j = i + 1;
+        for (; j < v.size() && v[j].addr == v[i].addr; ++j)
+            len = std::max(len, v[j].len);
+        total += len;
+        i = j;
+    }
+    return total;
+}
+
+// The bytes one executor segment must move at the least: each source symbol
+// read once (a window element or sum re-read by several rows of a batch is
+// one read: the kernel stages them in LDS), each destination written once
+// (and its kept prefix read once), the op stream itself read once.  The
+// algorithmic bytes count every re-read; this does not.
+uint64_t segment_unique_bytes(const ProgramBody::Segment& s, std::vector<Range>& rd, std::vector<Range>& wr)
+{
+    rd.clear();
+    wr.clear();
+    uint64_t words = 0;
+    auto R = [&](uint64_t a, uint32_t n) {
+        if (a && n)
+            rd.push_back(Range{a, n});
+    };
+    auto W = [&](uint64_t a, uint32_t n, uint32_t valid) {
+        if (a && n)
+            wr.push_back(Range{a, n});
+        R(a, std::min(valid, n));
+    };
+    for (const GfOp& op : s.ops) {
+        words += op_words(op);
+        const uint8_t* blk = s.rowsData.data() + (size_t)op.termBegin * 16;
+        switch (op.kind) {
+        case OP_LINCOMB:
+            W(op.dst, op.n, op.valid);
+            for (uint32_t t = 0; t < op.termCount; ++t)
+                R(s.terms[op.termBegin + t].src, s.terms[op.termBegin + t].len);
+            break;
+        case OP_LITERAL:
+            W(op.dst + op.n, op.valid, 0);
+            break;
+        case OP_ROWS: {
+            const WinEntry* sums = reinterpret_cast<const WinEntry*>(blk);
+            const WinEntry* win = sums + kRowSums;
+            const SumUpdate* up = reinterpret_cast<const SumUpdate*>(win + op.valid);
+            const RowItem* rows = reinterpret_cast<const RowItem*>(up + op.mix);
+            for (unsigned k = 0; k < kRowSums; ++k)
+                R(sums[k].src, sums[k].len);
+            for (uint32_t e = (uint32_t)op.dst; e < op.valid; ++e)   // (from stageLo)
+                R(win[e].src, win[e].len);
+            for (uint32_t u = 0; u < op.mix; ++u)
+                W((uint64_t)up[u].dstHi << 32 | up[u].dstLo, up[u].n, up[u].valid);
+            for (uint32_t r = 0; r < op.n; ++r)
+                W(rows[r].dst, rows[r].n + row_lit_len(rows[r].mask0), rows[r].valid);
+            break;
+        }
+        case OP_COPIES: {
+            const CopyItem* c = reinterpret_cast<const CopyItem*>(blk);
+            for (uint32_t i = 0; i < op.n; ++i) {
+                W(c[i].dst, c[i].len, 0);
+                R(c[i].src, c[i].len);
+            }
+            break;
+        }
+        case OP_LINCOMBS: {
+            const LcItem* it = reinterpret_cast<const LcItem*>(blk);
+            for (uint32_t i = 0; i < op.n; ++i) {
+                W(it[i].dst, std::max(it[i].n, it[i].litOffset + ((it[i].mixLit >> 8) & 0xff)), it[i].valid);
+                const GfTerm* t = reinterpret_cast<const GfTerm*>(blk + (size_t)it[i].termStart * 16);
+                for (uint32_t k = 0; k < it[i].termCount; ++k)
+                    R(t[k].src, t[k].len);
+            }
+            break;
+        }
+        default:
+            break;
+        }
+    }
+    return words * 16 + distinct_bytes(rd) + distinct_bytes(wr);
+}
+
 } // namespace
+
+void Engine::set_measure_unique(bool on) { g_measureUnique.store(on, std::memory_order_relaxed); }
+bool Engine::measure_unique() { return g_measureUnique.load(std::memory_order_relaxed); }
 
 void Engine::start_threads()
 {
@@ -1974,9 +2075,18 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     for (size_t qi = 0; qi < bt.queues.size(); ++qi)
         for (size_t c = 0; c < std::max<size_t>(1, bt.queues[qi].ingest.size()); c += kIngestChunk)
             tasks.push_back(Task{1, qi, c});
+    const bool measureUnique = measure_unique();
+    std::atomic<uint64_t> uniqueBytes{0};
     run(tasks.size(), [&](size_t ti) {
         const Task& t = tasks[ti];
         if (t.kind == 0) {
+            if (measureUnique) {
+                std::vector<Range> rd, wr;
+                uint64_t u = 0;
+                for (size_t si = t.a; si < t.b; ++si)
+                    u += segment_unique_bytes(*segs[si].seg, rd, wr);
+                uniqueBytes.fetch_add(u, std::memory_order_relaxed);
+            }
             for (size_t si = t.a; si < t.b; ++si) {
                 const SegRef& r = segs[si];
                 const ProgramBody::Segment& s = *r.seg;
@@ -2089,6 +2199,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     st.solves = sdescs.size();
     st.ingests = nIngest;
     st.uploadBytes = bt.upBytes;
+    st.execUniqueBytes = uniqueBytes.load(std::memory_order_relaxed);
     st.assembleNs = now_ns() - t0;
     // SGPU_ASM_STATS=1: one stderr line per flush, assembly time by stage (profiling aid)
     static const bool asmStats = std::getenv("SGPU_ASM_STATS") != nullptr;

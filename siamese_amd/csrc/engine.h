@@ -336,6 +336,10 @@ struct EngineStats
     // buffers to the arena (nanoseconds)
     uint64_t assembleNs = 0, waitNs = 0, completeNs = 0, reclaimNs = 0;
     uint64_t execLaunches = 0;   // executor launches (part of `launches`)
+    // Compulsory bytes of the executor launches, counted only while
+    // set_measure_unique(true) (bench.py's roofline): every distinct source
+    // symbol read once, every destination written once, plus the op stream.
+    uint64_t execUniqueBytes = 0;
 
     void add(const EngineStats& o);
 };
@@ -441,6 +445,11 @@ public:
     /// library's extension of siamese.h:59), exclusive only while a flush
     /// detaches the queued work (flush_and_sync(&instance_lock())).
     std::shared_mutex& instance_lock() { return instMu_; }
+
+    /// Count EngineStats::execUniqueBytes at flush assembly (a measurement
+    /// aid: off by default, it sorts every segment's operands).
+    static void set_measure_unique(bool on);
+    static bool measure_unique();
 
     /// Counts toward the calling thread's statistics.
     void account(uint64_t opBytes, uint64_t outBytes = 0, bool inSolve = false);

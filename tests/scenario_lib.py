@@ -80,13 +80,13 @@ class BatchOptions(ctypes.Structure):
                 ("threads", ctypes.c_uint32), ("groups", ctypes.c_uint32),
                 ("e2e", ctypes.c_uint32), ("digest", ctypes.c_uint32), ("defer", ctypes.c_uint32),
                 ("frames", ctypes.c_uint32), ("no_timing", ctypes.c_uint32),
-                ("device_ge", ctypes.c_uint32)]
+                ("device_ge", ctypes.c_uint32), ("unique", ctypes.c_uint32)]
 
 
 class BatchReport(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("device_ms", ctypes.c_double),
                 ("exec_ms", ctypes.c_double), ("setup_seconds", ctypes.c_double),
-                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 17),
+                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 18),
                 ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64),
                 ("phase_seconds", ctypes.c_double * 5), ("payload_bytes", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double * 5)]
@@ -134,7 +134,7 @@ def run_capi(library, cfg, threads=1, event_log=None):
 
 
 def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0, groups=1,
-              e2e=False, defer=0, frames=False, device_ge=False):
+              e2e=False, defer=0, frames=False, device_ge=False, unique=False):
     """Run `cfg` through the device-resident batch API (lock-step rounds),
     streams driven by `threads` host threads (0 = library default), split
     into `groups` groups whose host work and device work alternate.  With
@@ -149,7 +149,7 @@ def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0
     Returns (results of the last run, BatchReport)."""
     res = (StreamResult * cfg.streams)()
     opt = BatchOptions(steps, warmup, 1 if verify else 0, device, threads, groups, 1 if e2e else 0, 1, defer,
-                       1 if frames else 0, 0, 1 if device_ge else 0)
+                       1 if frames else 0, 0, 1 if device_ge else 0, 1 if unique else 0)
     rep = BatchReport()
     rc = lib().scenario_run_batch(library.encode(), ctypes.byref(cfg), res, ctypes.byref(opt),
                                   ctypes.byref(rep))
@@ -160,7 +160,7 @@ def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0
 
 ENGINE_KEYS = ("flushes launches ops terms solves ingests upload_bytes ref_op_bytes "
                "out_bytes solve_bytes assemble_ns wait_ns complete_ns reclaim_ns "
-               "exec_launches ldpc_bytes arena_growth").split()
+               "exec_launches ldpc_bytes exec_unique_bytes arena_growth").split()
 
 
 def engine_dict(report):
@@ -185,14 +185,15 @@ class BatchSession:
             raise RuntimeError("scenario_batch_open(%s) failed" % library)
 
     def run(self, steps=1, warmup=0, verify=False, threads=0, groups=1, e2e=False, digest=True, defer=0,
-            frames=False, timing=True, device_ge=False):
+            frames=False, timing=True, device_ge=False, unique=False):
         """digest=False: timed runs skip the per-stream event logs (results
         then carry no digest; take it from a verified run).  device_ge (with
-        defer=0): decodes by sgpu_decode_device."""
+        defer=0): decodes by sgpu_decode_device.  unique: count the executor
+        launches' compulsory bytes (sgpu_measure_unique; a measurement run)."""
         res = (StreamResult * self.cfg.streams)()
         opt = BatchOptions(steps, warmup, 1 if verify else 0, -1, threads, groups,
                            1 if e2e else 0, 1 if digest else 0, defer, 1 if frames else 0,
-                           0 if timing else 1, 1 if device_ge else 0)
+                           0 if timing else 1, 1 if device_ge else 0, 1 if unique else 0)
         rep = BatchReport()
         rc = lib().scenario_batch_run(self.handle, res, ctypes.byref(opt), ctypes.byref(rep))
         if rc != 0:
