@@ -178,6 +178,8 @@ inline uint64_t ev(uint64_t type, uint64_t result, uint64_t a = 0, uint64_t b = 
       int  enc_add_range(unsigned firstId, unsigned count, unsigned* firstNum, unsigned* added);
       int  dec_add_range(unsigned firstId, unsigned firstNum, unsigned count, int* results, unsigned* calls);
       int  dec_get_range(unsigned firstNum, unsigned count, Pkt* out, unsigned* got);
+      void encode_hint(unsigned n);           // the next n encode() calls are sure to come
+                                              // (a codec may make them in one range call)
 */
 
 inline uint64_t data_token(bool hashData, const uint8_t* p, unsigned bytes)
@@ -213,8 +215,10 @@ struct Stream
     Phase phase = ADD;
     unsigned i = 0;               // next original index
     unsigned tail = 0;            // encodes issued after the originals
+    unsigned encodedAhead = 0;    // block mode, ranges: tail count the last encode_hint covers
     unsigned nextExpected = 0;
     unsigned lastNum = 0;         // PacketNum of the most recent add
+    unsigned recReceived = 0;     // recovery packets the decoder took
     bool tailMode = false;        // all originals added; only encodes remain
     std::vector<uint8_t> buf;
     std::vector<Pkt> decoded;     // output of the last successful decode
@@ -372,6 +376,7 @@ struct Stream
             fail(2);
             return;
         }
+        ++recReceived;
         phase = DECODE_LOOP;
     }
 
@@ -521,6 +526,21 @@ struct Stream
             if (tail >= cfg->tail_limit) {
                 fail(1);
                 return false;
+            }
+            if (cfg->add_ranges && cfg->block_mode && tail == encodedAhead) {
+                // Block mode: the decoder cannot be ready before it holds as
+                // many recovery packets as originals were lost (every row
+                // covers the whole block, SiameseDecoder.cpp:541-600), so at
+                // least that many more encodes follow, one per TAIL step,
+                // whatever the channel drops; the codec may make them in one
+                // range call.  The calls and their results are the per-call
+                // sequence's (the encoder's state depends on its own calls
+                // only), so the event log is unchanged.
+                const unsigned lost = res->originals_lost;
+                unsigned n = lost > recReceived ? lost - recReceived : 1;
+                n = std::min(n, cfg->tail_limit - tail);
+                encodedAhead = tail + n;
+                codec->encode_hint(n);
             }
             ++tail;
             encode_once();

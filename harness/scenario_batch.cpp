@@ -28,6 +28,7 @@
 #include <deque>
 #include <malloc.h>
 #include <memory>
+#include <mutex>
 
 extern "C" {
 
@@ -96,6 +97,7 @@ struct Api
     SiameseResult (*encoder_add)(SgpuEncoder, const void*, unsigned, unsigned*);
     SiameseResult (*encoder_remove_before)(SgpuEncoder, unsigned);
     SiameseResult (*encode)(SgpuEncoder, SgpuRecoveryPacket*);
+    SiameseResult (*encode_range)(SgpuEncoder, SgpuRecoveryPacket*, unsigned, unsigned*);
     SgpuDecoder (*decoder_create)(void);
     void (*decoder_free)(SgpuDecoder);
     SiameseResult (*decoder_add_original)(SgpuDecoder, unsigned, const void*, unsigned);
@@ -196,37 +198,54 @@ bool load_api(const char* path, Api& a)
            bind_optional(h, a.decoder_get_range, "sgpu_decoder_get_range") &&
            bind_optional(h, a.engine_stats_ex, "sgpu_engine_stats_ex") &&
            bind_optional(h, a.measure_unique, "sgpu_measure_unique") &&
+           bind_optional(h, a.encode_range, "sgpu_encode_range") &&
            bind_optional(h, a.timing_kernels, "sgpu_timing_kernels") &&
            bind_optional(h, a.decode_device, "sgpu_decode_device");
 }
 
-// SCENARIO_BATCH_CALLS=1: time every codec call by kind and print the
-// totals after each run (diagnostic: the clock reads add ~40 ns per call)
+// SCENARIO_BATCH_CALLS=1: time every codec call by kind (TSC ticks, summed
+// per thread without shared atomics so the counting does not perturb a
+// multithreaded run) and print the totals after each run (diagnostic)
 enum CallKind { kEncAdd, kEncode, kDecAddOrig, kDecAddRec, kIsReady, kDecode, kDecGet, kRemove, kCreate, kFree,
                 kCallKinds };
 const char* const kCallNames[kCallKinds] = {"enc_add", "encode", "dec_add_orig", "dec_add_rec", "is_ready",
                                             "decode", "dec_get", "remove", "create", "free"};
-std::atomic<uint64_t> g_calls[kCallKinds][3];   // calls, ns, items
 const bool kCallTiming = std::getenv("SCENARIO_BATCH_CALLS") != nullptr;
+struct CallCounts
+{
+    uint64_t v[kCallKinds][3] = {};   // calls, ticks, items
+};
+std::mutex g_callsMu;
+std::vector<CallCounts*> g_callCounts;   // one per thread that timed a call (never freed)
+CallCounts& call_counts()
+{
+    thread_local CallCounts* c = nullptr;
+    if (!c) {
+        c = new CallCounts;
+        std::lock_guard<std::mutex> g(g_callsMu);
+        g_callCounts.push_back(c);
+    }
+    return *c;
+}
 
 struct CallTimer
 {
     CallKind k;
     uint64_t items;
-    Clock::time_point t0;
+    uint64_t t0 = 0;
     explicit CallTimer(CallKind kind, uint64_t n = 1) : k(kind), items(n)
     {
         if (kCallTiming)
-            t0 = Clock::now();
+            t0 = __builtin_ia32_rdtsc();
     }
     ~CallTimer()
     {
         if (!kCallTiming)
             return;
-        g_calls[k][0].fetch_add(1, std::memory_order_relaxed);
-        g_calls[k][1].fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count(),
-                                std::memory_order_relaxed);
-        g_calls[k][2].fetch_add(items, std::memory_order_relaxed);
+        CallCounts& c = call_counts();
+        c.v[k][0] += 1;
+        c.v[k][1] += __builtin_ia32_rdtsc() - t0;
+        c.v[k][2] += items;
     }
 };
 
@@ -234,8 +253,23 @@ void print_calls()
 {
     if (!kCallTiming)
         return;
+    // TSC rate from a short wall-clock window
+    const auto w0 = Clock::now();
+    const uint64_t c0 = __builtin_ia32_rdtsc();
+    while (Clock::now() - w0 < std::chrono::milliseconds(20)) {
+    }
+    const double ticksPerNs =
+        (double)(__builtin_ia32_rdtsc() - c0) / (double)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - w0).count();
+    std::lock_guard<std::mutex> g(g_callsMu);
     for (unsigned k = 0; k < kCallKinds; ++k) {
-        const uint64_t c = g_calls[k][0].exchange(0), ns = g_calls[k][1].exchange(0), it = g_calls[k][2].exchange(0);
+        uint64_t c = 0, t = 0, it = 0;
+        for (CallCounts* cc : g_callCounts) {
+            c += cc->v[k][0];
+            t += cc->v[k][1];
+            it += cc->v[k][2];
+            cc->v[k][0] = cc->v[k][1] = cc->v[k][2] = 0;
+        }
+        const double ns = (double)t / ticksPerNs;
         if (c)
             std::fprintf(stderr, "batch %-13s %9llu calls %9llu items %10.1f us  %8.3f us/item\n", kCallNames[k],
                          (unsigned long long)c, (unsigned long long)it, ns / 1e3, ns / 1e3 / (double)it);
@@ -362,8 +396,37 @@ struct BatchCodec
         CallTimer ct(kEncAdd);
         return sh->api->encoder_add(enc, dev_payload(id), bytes, num);
     }
+    // encode_hint: packets made ahead by one sgpu_encode_range, handed out
+    // by the encode() calls that follow (the same packets, in order)
+    std::vector<SgpuRecoveryPacket> ahead;
+    unsigned aheadNext = 0;
+    int aheadFail = 0;   // the range's result when it stopped early (returned after the packets)
+    void encode_hint(unsigned n)
+    {
+        if (n < 2 || !sh->api->encode_range || aheadNext < ahead.size() || aheadFail)
+            return;
+        ahead.resize(n);
+        unsigned made = 0;
+        CallTimer ct(kEncode, n);
+        const int r = sh->api->encode_range(enc, ahead.data(), n, &made);
+        ahead.resize(made);
+        aheadNext = 0;
+        aheadFail = r;
+    }
     int encode(Rec* r)
     {
+        if (aheadNext < ahead.size()) {
+            r->pkt = ahead[aheadNext++];
+            r->bytes = r->pkt.DataBytes;
+            return 0;
+        }
+        if (aheadFail) {
+            const int res = aheadFail;
+            aheadFail = 0;
+            r->pkt.DataBytes = 0;
+            r->bytes = 0;
+            return res;
+        }
         CallTimer ct(kEncode);
         const int res = sh->api->encode(enc, &r->pkt);
         r->bytes = r->pkt.DataBytes;
@@ -896,6 +959,7 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                     break;
             BatchCodec& c = J.codecs[i];
             if (st.done() && c.inFlight == 0) {
+                CallTimer ct(kFree);
                 api.encoder_free(c.enc);
                 api.decoder_free(c.dec);
                 c.enc = nullptr;
@@ -1010,6 +1074,7 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 land_gathers(sh);   // (their requests point into the job's streams)
             for_streams(sh, J.end - J.begin, [&](size_t i) {
                 J.streams[i].finish();
+                CallTimer ct(kFree);
                 api.encoder_free(J.codecs[i].enc);   // (null if freed already)
                 api.decoder_free(J.codecs[i].dec);
                 J.codecs[i].enc = nullptr;
@@ -1074,8 +1139,11 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 BatchCodec& c = J.codecs[i];
                 c.sh = &sh;
                 c.payload = sh.frames ? (second ? sh.frameDev2 : sh.frameDev) : (second ? sh.payload2 : sh.payload);
-                c.enc = api.encoder_create();
-                c.dec = api.decoder_create();
+                {
+                    CallTimer ct(kCreate);
+                    c.enc = api.encoder_create();
+                    c.dec = api.decoder_create();
+                }
                 c.flow = J.begin + (unsigned)i;
                 if (sh.frames) {
                     J.decTable[c.flow] = c.dec;

@@ -260,6 +260,7 @@ struct CapiCodec
             *ok = false;
         return p.data ? scen::data_token(cfg->hash_data, p.data, p.bytes) : 0;
     }
+    void encode_hint(unsigned) {}   // (siamese.h encodes one packet per call)
     bool wants_yield_after_decode() const { return false; }
     bool wants_yield_after_encode() const { return false; }
 };

@@ -97,6 +97,16 @@ SIAMESE_EXPORT SiameseResult sgpu_encoder_add_range(SgpuEncoder encoder, const v
                                                     unsigned* firstPacketNumOut, unsigned* addedOut);
 SIAMESE_EXPORT SiameseResult sgpu_encoder_remove_before(SgpuEncoder encoder, unsigned firstKept);
 SIAMESE_EXPORT SiameseResult sgpu_encode(SgpuEncoder encoder, SgpuRecoveryPacket* out);
+/// `count` sgpu_encode calls in one: out[k] = what the k-th call returns,
+/// until a call does not succeed, whose result is returned (Success if none
+/// failed; that call's out[k].DataBytes = 0); *producedOut = packets made.
+/// Every packet of the call stays valid until the next sgpu_encode /
+/// sgpu_encode_range on the same encoder.  Bit-exact with the single calls
+/// (the reference's siamese_encode, siamese.cpp:159-168, per packet,
+/// SiameseEncoder.cpp:1146-1254): a block-mode sender that knows how many
+/// recovery packets it needs asks for them in one call.
+SIAMESE_EXPORT SiameseResult sgpu_encode_range(SgpuEncoder encoder, SgpuRecoveryPacket* out, unsigned count,
+                                               unsigned* producedOut);
 
 SIAMESE_EXPORT SgpuDecoder sgpu_decoder_create(void);
 SIAMESE_EXPORT void sgpu_decoder_free(SgpuDecoder decoder);

@@ -132,6 +132,48 @@ SIAMESE_EXPORT SiameseResult sgpu_encode(SgpuEncoder encoder, SgpuRecoveryPacket
     return Siamese_Success;
 }
 
+SIAMESE_EXPORT SiameseResult sgpu_encode_range(SgpuEncoder encoder, SgpuRecoveryPacket* out, unsigned count,
+                                               unsigned* producedOut)
+{
+    if (producedOut)
+        *producedOut = 0;
+    if (!encoder || (!out && count) || !producedOut)
+        return Siamese_InvalidInput;
+    EncoderCore& core = BE(encoder)->core;
+    // (EncodeOut is larger than the caller's records: encode in chunks)
+    constexpr unsigned kChunk = 64;
+    EncodeOut o[kChunk];
+    SiameseResult r = Siamese_Success;
+    unsigned done = 0;
+    while (done < count && r == Siamese_Success) {
+        const unsigned n = std::min(kChunk, count - done);
+        unsigned made = 0;
+        // (chunks after the first must keep the packets of the earlier ones:
+        // one encode_range call per sgpu_encode_range, so chunking is by
+        // hand below when count > kChunk)
+        if (done == 0)
+            r = core.encode_range(o, n, &made);
+        else
+            r = core.encode_range_more(o, n, &made);
+        for (unsigned k = 0; k < made; ++k) {
+            SgpuRecoveryPacket& p = out[done + k];
+            p.DeviceData = o[k].buf.ptr;
+            p.DataBytes = o[k].bytes;
+            p.FooterBytes = o[k].footerBytes;
+            std::memcpy(p.Footer, o[k].footer, sizeof(p.Footer));
+            std::memcpy(p.Head, o[k].head, sizeof(p.Head));
+            p.Producer = &core.program();
+        }
+        done += made;
+        if (made < n && r == Siamese_Success)
+            break;
+    }
+    if (r != Siamese_Success && done < count)
+        out[done].DataBytes = 0;
+    *producedOut = done;
+    return r;
+}
+
 SIAMESE_EXPORT SgpuDecoder sgpu_decoder_create(void)
 {
     if (!g_batchReady)

@@ -1735,6 +1735,7 @@ bool DecoderCore::eliminate_original_data()
     uint32_t clip[kRowSums];   // min(sum bytes, row bytes): reference source bytes
     uint32_t present = 0;      // sums holding bytes
     bool tableStale = true;
+    uint64_t tableVersion = 0;   // Program::rows_row's tag of `sums` as last rebuilt
     for (unsigned ri = 0; ri < rows; ++ri) {
         if (!rows_[ri].used)
             continue;
@@ -1804,6 +1805,7 @@ bool DecoderCore::eliminate_original_data()
         fresh |= want;
         if (tableStale) {
             tableStale = false;
+            tableVersion = Program::next_table_version();
             present = 0;
             for (unsigned k = 0; k < kRowSums; ++k) {
                 const DevSum& d = sum(k / kSums, k % kSums).d;
@@ -1827,7 +1829,7 @@ bool DecoderCore::eliminate_original_data()
         // rows of one decode share the sums: one row of the program's batch
         cover(windowLo_, ee);
         prog_.rows_row(sums, rec->buf.addr(), rb, rb, row_value(m.row), mask[0], mask[1], m.row,
-                       m.ldpcCount, es, ee);
+                       m.ldpcCount, es, ee, nullptr, 0, tableVersion);
         eng_->account(opBytes);
     }
     // the window snapshot must not see this decode's recoveries

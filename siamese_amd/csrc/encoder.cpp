@@ -32,6 +32,8 @@ EncoderCore::~EncoderCore()
         for (DevSum& s : l.sum)
             eng_->release(s.buf);
     eng_->release(recovery_);
+    for (DevBuf& b : recoveryHeld_)
+        eng_->release(b);
     subwindows_.clear();   // (subwindows go back to their own pool)
     SubwindowTable* t = CapStash<SubwindowTable>::shell();
     subwindows_.swap(t->v);
@@ -391,6 +393,9 @@ SiameseResult EncoderCore::get(SiameseOriginalPacket& packet)
 
 bool EncoderCore::ensure_recovery(unsigned bytes)
 {
+    for (DevBuf& b : recoveryHeld_)
+        eng_->release(b);
+    recoveryHeld_.clear();
     // Every recovery packet gets a fresh buffer.  The previous one is
     // recycled only after the flush that produced it completes, so a decoder
     // that copies the packet later in the same flush (its own program, group
@@ -449,6 +454,35 @@ SiameseResult EncoderCore::encode(EncodeOut& out)
     if (++nextRow_ >= kRowValuePeriod)
         nextRow_ = 0;
     return siamese_row(out, row);
+}
+
+SiameseResult EncoderCore::encode_range(EncodeOut* out, unsigned count, unsigned* produced)
+{
+    for (DevBuf& b : recoveryHeld_)   // (the previous call's packets)
+        eng_->release(b);
+    recoveryHeld_.clear();
+    return encode_range_more(out, count, produced);
+}
+
+SiameseResult EncoderCore::encode_range_more(EncodeOut* out, unsigned count, unsigned* produced)
+{
+    *produced = 0;
+    std::vector<DevBuf> held;   // this call's packets before the last (and the chunks' before it)
+    held.swap(recoveryHeld_);   // (capacity reused; ensure_recovery below finds none to release)
+    SiameseResult r = Siamese_Success;
+    for (unsigned k = 0; k < count; ++k) {
+        if (k > 0 || !held.empty() || *produced) {
+            // keep the previous packet: ensure_recovery would release it
+            held.push_back(recovery_);
+            recovery_ = DevBuf();
+        }
+        r = encode(out[k]);
+        if (r != Siamese_Success)
+            break;
+        ++*produced;
+    }
+    recoveryHeld_.swap(held);
+    return r;
 }
 
 SiameseResult EncoderCore::single_row(EncodeOut& out)
@@ -545,6 +579,7 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     if (sumTableStale_) {
         // the 24 sums as the rows read them (rebuilt only after a change)
         sumTableStale_ = false;
+        sumTableVersion_ = Program::next_table_version();
         sumPresent_ = 0;
         for (unsigned k = 0; k < kRowSums; ++k) {
             const DevSum& d = lanes_[k / kSums].sum[k % kSums];
@@ -580,7 +615,7 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     // of the program's Siamese row batch (consecutive rows share the sums)
     cover(std::min(start, sumStart_), sumEnd_);
     prog_.rows_row(sumTable_, recovery_.addr(), recoveryBytes, 0, row_value(row), mask[0], mask[1], row,
-                   n, start, count_, footer, footerBytes);
+                   n, start, count_, footer, footerBytes, sumTableVersion_);
     eng_->account(opBytes);
 
     finish_row(out, m, recoveryBytes, true);

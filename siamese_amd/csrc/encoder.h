@@ -106,6 +106,14 @@ public:
     SiameseResult get(SiameseOriginalPacket& packet);
     /// Generate the next recovery packet (device ops queued, not flushed).
     SiameseResult encode(EncodeOut& out);
+    /// `count` encode() calls in one (sgpu_encode_range): out[k] as the k-th
+    /// call fills it, stopping at the first call that does not succeed (its
+    /// result returned, Success otherwise); *produced = packets made.  Every
+    /// packet's buffer stays valid until the next encode call.
+    SiameseResult encode_range(EncodeOut* out, unsigned count, unsigned* produced);
+    /// encode_range continued: the packets of the call before are kept too
+    /// (one sgpu_encode_range made in several chunks).
+    SiameseResult encode_range_more(EncodeOut* out, unsigned count, unsigned* produced);
     SiameseResult stats(uint64_t* out, unsigned count);
     /// ARQ: siamese_encoder_ack / siamese_encoder_retransmit (arq.cpp)
     SiameseResult acknowledge(const uint8_t* data, unsigned bytes, unsigned& nextExpectedOut);
@@ -196,8 +204,10 @@ private:
     WinEntry sumTable_[kRowSums];
     uint32_t sumPresent_ = 0;   // sums holding bytes
     bool sumTableStale_ = true;
+    uint64_t sumTableVersion_ = 0;   // Program::rows_row's tag of sumTable_ as last rebuilt
 
     DevBuf recovery_;          // reused recovery packet buffer
+    std::vector<DevBuf> recoveryHeld_;   // encode_range's earlier packets (released by the next encode)
     unsigned nextRow_ = 0;
     unsigned nextParityColumn_ = 0;
     unsigned nextCauchyRow_ = 0;

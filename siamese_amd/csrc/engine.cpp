@@ -116,6 +116,7 @@ void ProgramBody::rows_open(uint32_t base, bool keepWindow)
         new_segment();
     rb.open = true;
     rb.haveSums = false;
+    rb.sumsVersion = 0;
     rb.readMask = 0;
     rb.cutMax = 0;
     rb.versioned = false;
@@ -696,11 +697,20 @@ void Program::rows_update(unsigned k, uint64_t dst, uint32_t n, uint32_t valid, 
         b.maxExtent = n;
 }
 
+uint64_t Program::next_table_version()
+{
+    static std::atomic<uint64_t> next{1};
+    return next.fetch_add(1, std::memory_order_relaxed);
+}
+
 void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix,
                        uint32_t mask0, uint32_t mask1, unsigned row, uint32_t ldpcN,
-                       uint32_t ldpcFirst, uint32_t cutoff, const uint8_t* lit, uint32_t litLen)
+                       uint32_t ldpcFirst, uint32_t cutoff, const uint8_t* lit, uint32_t litLen,
+                       uint64_t sumsVersion)
 {
     ProgramBody::RowsBuild& b = b_->rb;
+    // (the batch already holds this very table: nothing to compare or copy)
+    const bool unchanged = sumsVersion != 0 && b.haveSums && b.sumsVersion == sumsVersion;
     // (a row whose cutoff is below an earlier row's reads sums folded past
     // its own cutoff: it starts a batch after every update so far; a
     // versioned batch takes at most kVersionRows rows)
@@ -710,7 +720,7 @@ void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t 
     // before do not read it), so consecutive rows over one window share a
     // batch while the sums fill in.
     bool same = true;
-    if (b.haveSums)
+    if (b.haveSums && !unchanged)
         for (uint32_t r = b.readMask; r; r &= r - 1) {
             const unsigned k = (unsigned)__builtin_ctz(r);
             if (std::memcmp(&b.sums[k], &sums[k], sizeof(WinEntry)) != 0) {
@@ -721,8 +731,10 @@ void Program::rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t 
     if (!same || cutoff < b.cutMax || (b.versioned && b.rows.size() >= kVersionRows))
         rows_open(b.base, true);
     b.cutMax = std::max(b.cutMax, cutoff);
-    std::memcpy(b.sums, sums, sizeof(b.sums));
+    if (!(unchanged && b.haveSums))   // (a batch opened just above copies)
+        std::memcpy(b.sums, sums, sizeof(b.sums));
     b.haveSums = true;
+    b.sumsVersion = sumsVersion;
     RowItem r;
     std::memset(&r, 0, sizeof(r));
     r.dst = dst;

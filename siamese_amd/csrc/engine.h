@@ -114,6 +114,7 @@ struct ProgramBody
     {
         bool open = false;
         bool haveSums = false;
+        uint64_t sumsVersion = 0;       // the caller's table `sums` was copied from (0: none)
         WinEntry sums[kRowSums];
         uint32_t readMask = 0;          // sums read by the batch's rows
         uint32_t cutMax = 0;            // largest row cutoff so far (absolute element)
@@ -287,9 +288,15 @@ public:
                      uint32_t fromElement, uint32_t toElement);
     /// `cutoff`: the row reads each sum as folded over window elements below
     /// it (every sum the row reads was brought up to it; RowItem.cutoff).
+    /// `sumsVersion` (optional, from next_table_version()): the caller's
+    /// table has not changed since a row passed it with this version, so
+    /// the batch's copy is not compared or copied again.
     void rows_row(const WinEntry* sums, uint64_t dst, uint32_t n, uint32_t valid, uint8_t mix,
                   uint32_t mask0, uint32_t mask1, unsigned row, uint32_t ldpcN,
-                  uint32_t ldpcFirst, uint32_t cutoff, const uint8_t* lit = nullptr, uint32_t litLen = 0);
+                  uint32_t ldpcFirst, uint32_t cutoff, const uint8_t* lit = nullptr, uint32_t litLen = 0,
+                  uint64_t sumsVersion = 0);
+    /// A fresh version tag for a caller's sums table (rows_row), unique in the process.
+    static uint64_t next_table_version();
     /// Close the open batch (its window may change after this).
     void rows_seal()
     {
