@@ -214,7 +214,9 @@ const bool kCallTiming = std::getenv("SCENARIO_BATCH_CALLS") != nullptr;
 struct CallCounts
 {
     uint64_t v[kCallKinds][3] = {};   // calls, ticks, items
+    uint64_t busy = 0;                // ticks inside for_streams tasks
 };
+std::atomic<uint64_t> g_fjWall{0}, g_fjCount{0};   // for_streams: wall ticks, fork-joins
 std::mutex g_callsMu;
 std::vector<CallCounts*> g_callCounts;   // one per thread that timed a call (never freed)
 CallCounts& call_counts()
@@ -261,6 +263,20 @@ void print_calls()
     const double ticksPerNs =
         (double)(__builtin_ia32_rdtsc() - c0) / (double)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - w0).count();
     std::lock_guard<std::mutex> g(g_callsMu);
+    {
+        uint64_t busy = 0;
+        unsigned threads = 0;
+        for (CallCounts* cc : g_callCounts) {
+            busy += cc->busy;
+            threads += cc->busy ? 1 : 0;
+            cc->busy = 0;
+        }
+        const uint64_t wall = g_fjWall.exchange(0), n = g_fjCount.exchange(0);
+        if (wall)
+            std::fprintf(stderr, "batch fork-joins %llu: wall %.1f us, busy %.1f us on %u threads, "
+                         "busy/(wall*threads) %.3f\n", (unsigned long long)n, wall / ticksPerNs / 1e3,
+                         busy / ticksPerNs / 1e3, threads, threads ? (double)busy / ((double)wall * threads) : 0.0);
+    }
     for (unsigned k = 0; k < kCallKinds; ++k) {
         uint64_t c = 0, t = 0, it = 0;
         for (CallCounts* cc : g_callCounts) {
@@ -865,10 +881,24 @@ void for_streams(Shared& sh, size_t count, const F& fn)
     }();
     const size_t blocks = (count + kBlock - 1) / kBlock;
     auto body = [&](size_t b) {
+        const uint64_t t0 = kCallTiming ? __builtin_ia32_rdtsc() : 0;
         const size_t end = std::min(count, (b + 1) * kBlock);
         for (size_t i = b * kBlock; i < end; ++i)
             fn(i);
+        if (kCallTiming)
+            call_counts().busy += __builtin_ia32_rdtsc() - t0;
     };
+    struct Wall
+    {
+        uint64_t t0 = kCallTiming ? __builtin_ia32_rdtsc() : 0;
+        ~Wall()
+        {
+            if (kCallTiming) {
+                g_fjWall += __builtin_ia32_rdtsc() - t0;
+                ++g_fjCount;
+            }
+        }
+    } wall;
     if (sh.pool) {
         sh.pool->run(blocks, body);
         return;

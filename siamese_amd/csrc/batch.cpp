@@ -9,6 +9,7 @@
 #include "frames.h"
 #include "encoder.h"
 #include "engine.h"
+#include "objpool.h"
 #include "pool.h"
 
 #include <algorithm>
@@ -61,14 +62,17 @@ SIAMESE_EXPORT SgpuEncoder sgpu_encoder_create(void)
 {
     if (!g_batchReady)
         return nullptr;
-    return reinterpret_cast<SgpuEncoder>(new (std::nothrow) BatchEncoder);
+    // (storage recycled per thread: objpool.h RawPool)
+    void* m = RawPool<BatchEncoder>::get();
+    return m ? reinterpret_cast<SgpuEncoder>(new (m) BatchEncoder) : nullptr;
 }
 
 SIAMESE_EXPORT void sgpu_encoder_free(SgpuEncoder encoder)
 {
     if (!encoder)
         return;
-    delete BE(encoder);
+    BE(encoder)->~BatchEncoder();
+    RawPool<BatchEncoder>::put(BE(encoder));
 }
 
 SIAMESE_EXPORT SiameseResult sgpu_encoder_add(SgpuEncoder encoder, const void* deviceData, unsigned bytes,
@@ -178,14 +182,16 @@ SIAMESE_EXPORT SgpuDecoder sgpu_decoder_create(void)
 {
     if (!g_batchReady)
         return nullptr;
-    return reinterpret_cast<SgpuDecoder>(new (std::nothrow) BatchDecoder);
+    void* m = RawPool<BatchDecoder>::get();
+    return m ? reinterpret_cast<SgpuDecoder>(new (m) BatchDecoder) : nullptr;
 }
 
 SIAMESE_EXPORT void sgpu_decoder_free(SgpuDecoder decoder)
 {
     if (!decoder)
         return;
-    delete BD(decoder);
+    BD(decoder)->~BatchDecoder();
+    RawPool<BatchDecoder>::put(BD(decoder));
 }
 
 SIAMESE_EXPORT SiameseResult sgpu_decoder_add_original(SgpuDecoder decoder, unsigned packetNum,

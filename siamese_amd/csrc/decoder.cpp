@@ -166,10 +166,27 @@ DecoderCore::~DecoderCore()
         free_packet(r);
         r = n;
     }
+    // one pass over each subwindow: release the buffers slots own and leave
+    // every slot fresh, so the pool's recycle (DecSubwindowRecycle) need not
+    // walk them again (a decoder's teardown is memory-bound on these slots)
     for (auto& sw : subwindows_) {
-        for (DecSlot& s : sw->slot)
-            release_slot(s);
+        for (DecSlot& s : sw->slot) {
+            if (!s.inSlab)
+                eng_->release(s.buf);
+            s.buf = DevBuf();
+            s.inSlab = false;
+            s.bytes = 0;
+            s.column = 0;
+            s.header = 0;
+            s.pending = false;
+            if (s.hostp)
+                s.hostp->clear();
+        }
+        sw->got = 0;
+        sw->gotCount = 0;
         eng_->slab_release(sw->slab);
+        sw->slab = Slab();
+        sw->clean = true;
     }
     for (auto& lane : lanes_)
         for (Sum& s : lane)
@@ -250,8 +267,10 @@ void DecoderCore::iterate_next_expected(unsigned start)
 bool DecoderCore::grow_window(unsigned end)
 {
     const unsigned needed = (end + kLanes + kSubwindow - 1) / kSubwindow;
-    while (subwindows_.size() < needed)
+    while (subwindows_.size() < needed) {
         subwindows_.emplace_back(ObjPool<DecSubwindow>::get());
+        subwindows_.back()->clean = false;
+    }
     if (end > count_)
         count_ = end;
     return true;
@@ -712,14 +731,21 @@ void DecoderCore::remove_elements()
 
 void DecSubwindowRecycle::operator()(DecSubwindow* w) const
 {
-    w->reset();
-    w->slab = Slab();
-    for (DecSlot& s : w->slot) {
-        s.buf = DevBuf();
-        s.inSlab = false;
-        s.header = 0;
-        if (s.hostp)
-            s.hostp->clear();
+    if (!w->clean) {
+        w->got = 0;
+        w->gotCount = 0;
+        w->slab = Slab();
+        for (DecSlot& s : w->slot) {
+            s.buf = DevBuf();
+            s.inSlab = false;
+            s.bytes = 0;
+            s.column = 0;
+            s.header = 0;
+            s.pending = false;
+            if (s.hostp)
+                s.hostp->clear();
+        }
+        w->clean = true;
     }
     ObjPool<DecSubwindow>::put(w);
 }

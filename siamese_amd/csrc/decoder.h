@@ -62,6 +62,7 @@ struct DecSubwindow
     uint64_t got = 0;           // CustomBitSet<64> (PacketAllocator.h:189-437)
     unsigned gotCount = 0;
     Slab slab;                  // the received originals' shared buffer (engine.h)
+    bool clean = false;         // every slot already in its fresh state (the owner's teardown)
     void reset()
     {
         got = 0;

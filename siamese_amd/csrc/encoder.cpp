@@ -23,10 +23,22 @@ EncoderCore::EncoderCore(Engine* eng, bool hostMirror) : eng_(eng), prog_(eng, 0
 
 EncoderCore::~EncoderCore()
 {
+    // one pass per subwindow: release owned buffers and leave the slots
+    // fresh for the pool (EncSubwindowRecycle skips a clean subwindow)
     for (auto& sw : subwindows_) {
-        for (EncSlot& s : sw->slot)
-            release_slot(s);
+        for (EncSlot& s : sw->slot) {
+            if (!s.inSlab)
+                eng_->release(s.buf);
+            s.buf = DevBuf();
+            s.inSlab = false;
+            s.bytes = s.column = s.header = 0;
+            s.lastSend = 0;
+            if (s.hostp)
+                s.hostp->clear();
+        }
         eng_->slab_release(sw->slab);
+        sw->slab = Slab();
+        sw->clean = true;
     }
     for (Lane& l : lanes_)
         for (DevSum& s : l.sum)
@@ -50,8 +62,10 @@ unsigned EncoderCore::take_element()
     unsigned element = count_;
 
     // Keep one lane-width of spare slots ahead of the last subwindow (:108-118)
-    if (element + kLanes >= subwindows_.size() * kSubwindow)
+    if (element + kLanes >= subwindows_.size() * kSubwindow) {
         subwindows_.emplace_back(ObjPool<EncSubwindow>::get());
+        subwindows_.back()->clean = false;
+    }
 
     if (count_ > 0)
         ++count_;

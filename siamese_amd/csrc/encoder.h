@@ -41,6 +41,7 @@ struct EncSubwindow
 {
     EncSlot slot[kSubwindow];
     Slab slab;                  // the slots' shared buffer (engine.h)
+    bool clean = false;         // every slot already in its fresh state (the owner's teardown)
 };
 
 /// unique_ptr deleter: subwindows go back to the thread's pool, emptied
@@ -49,14 +50,17 @@ struct EncSubwindowRecycle
 {
     void operator()(EncSubwindow* w) const
     {
-        w->slab = Slab();
-        for (EncSlot& s : w->slot) {
-            s.buf = DevBuf();
-            s.inSlab = false;
-            s.bytes = s.column = s.header = 0;
-            s.lastSend = 0;
-            if (s.hostp)
-                s.hostp->clear();
+        if (!w->clean) {
+            w->slab = Slab();
+            for (EncSlot& s : w->slot) {
+                s.buf = DevBuf();
+                s.inSlab = false;
+                s.bytes = s.column = s.header = 0;
+                s.lastSend = 0;
+                if (s.hostp)
+                    s.hostp->clear();
+            }
+            w->clean = true;
         }
         ObjPool<EncSubwindow>::put(w);
     }

@@ -6,6 +6,7 @@
 #pragma once
 
 #include <cstddef>
+#include <new>
 #include <vector>
 
 namespace sgpu {
@@ -43,6 +44,57 @@ private:
         {
             for (T* p : items)
                 delete p;
+        }
+    };
+    static Stash& stash()
+    {
+        thread_local Stash s;
+        return s;
+    }
+};
+
+/// Per-thread recycling of raw storage for objects of type T (the codec
+/// instances themselves: 1.5-2.5 KB each, past the C heap's per-thread
+/// caches, so every create and free would take an arena lock -- contended,
+/// since instances are created and freed on different threads).  get()
+/// returns uninitialised storage (construct with placement new); put() takes
+/// storage whose object was destroyed.
+template <class T>
+class RawPool
+{
+public:
+    static void* get()
+    {
+        Stash& s = stash();
+        if (!s.items.empty()) {
+            void* p = s.items.back();
+            s.items.pop_back();
+            return p;
+        }
+        return ::operator new(sizeof(T), std::align_val_t(alignof(T) > 64 ? alignof(T) : 64), std::nothrow);
+    }
+    static void put(void* p)
+    {
+        Stash& s = stash();
+        if (s.items.size() < kMax)
+            s.items.push_back(p);
+        else
+            release(p);
+    }
+
+private:
+    static constexpr size_t kMax = 1u << 13;
+    static void release(void* p)
+    {
+        ::operator delete(p, std::align_val_t(alignof(T) > 64 ? alignof(T) : 64));
+    }
+    struct Stash
+    {
+        std::vector<void*> items;
+        ~Stash()
+        {
+            for (void* p : items)
+                release(p);
         }
     };
     static Stash& stash()
