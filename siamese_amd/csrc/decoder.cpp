@@ -1872,14 +1872,16 @@ SiameseResult DecoderCore::solve_and_substitute()
     // (scratch vectors are members: a decode allocates nothing once warm)
     std::vector<RecPacket*>& pr = scratchRec_;
     std::vector<unsigned>& len = scratchLen_;
-    std::vector<SolveRow>& desc = scratchRows_;
     pr.resize(m);
     len.resize(m);
     for (unsigned i = 0; i < m; ++i) {
         pr[i] = rows_[pivots_[i]].rec;
         len[i] = pr[i]->bytes;
     }
-    desc.resize(m);
+    // the queued solve's own descriptors and coefficients, filled in place
+    SolveRow* desc = nullptr;
+    uint8_t* coefOut = nullptr;
+    prog_.solve_reserve(m, &desc, &coefOut);
     for (unsigned i = 0; i < m; ++i) {
         std::memset(&desc[i], 0, sizeof(SolveRow));
         desc[i].initBytes = len[i];
@@ -1934,12 +1936,10 @@ SiameseResult DecoderCore::solve_and_substitute()
         desc[i].finalBytes = len[i];
         maxBytes = std::max(maxBytes, len[i]);
     }
-    std::vector<uint8_t>& coef = scratchCoef_;
-    coef.resize((size_t)m * m);
     for (unsigned j = 0; j < m; ++j)
-        std::memcpy(coef.data() + (size_t)j * m, mrow(pivots_[j]), m);
+        std::memcpy(coefOut + (size_t)j * m, mrow(pivots_[j]), m);
 
-    const uint32_t base = prog_.solve(desc, coef.data(), maxBytes);
+    const uint32_t base = prog_.solve_commit(maxBytes);
 
     // Host side of BackSubstitution: swap buffers into the window, record
     // the outputs (exact lengths arrive with the completion, complete_solve).
@@ -1990,7 +1990,8 @@ SiameseResult DecoderCore::solve_and_substitute()
             advanced |= mark_got(col.column);
             fixes.push_back(Fix{o, o->buf.ptr, (uint32_t)ci, (unsigned)ci, len[ci]});
         }
-        lastDecoded_ = fixes;
+        if (mirror_)   // (download_recovered's list: the drop-in API only)
+            lastDecoded_ = fixes;
         publish_outputs();
     }
     lastPendSlot_ = slot;

@@ -569,29 +569,70 @@ void Program::ingest_run(uint64_t dst, uint32_t dstStride, uint64_t src, uint32_
 
 uint32_t Program::solve(const std::vector<SolveRow>& rows, const uint8_t* coef, uint32_t maxBytes)
 {
+    SolveRow* r = nullptr;
+    uint8_t* c = nullptr;
+    solve_reserve((unsigned)rows.size(), &r, &c);
+    std::memcpy(r, rows.data(), rows.size() * sizeof(SolveRow));
+    std::memcpy(c, coef, rows.size() * rows.size());
+    return solve_commit(maxBytes);
+}
+
+void Program::solve_reserve(unsigned m, SolveRow** rows, uint8_t** coef)
+{
     touch();
     if (b_->nsegs == 0)
         b_->new_segment(); // the segment preceding this solve
     if (b_->nsolves == b_->solves.size())
         b_->solves.emplace_back();
+    ProgramBody::PendingSolve& ps = b_->solves[b_->nsolves];
+    ps.rows.resize(m);
+    ps.coef.resize((size_t)m * m);
+    *rows = ps.rows.data();
+    *coef = ps.coef.data();
+}
+
+uint32_t Program::solve_commit(uint32_t maxBytes)
+{
+    ProgramBody::PendingSolve& ps = b_->solves[b_->nsolves++];
+    const size_t m = ps.rows.size();
     // each row's first 16 bytes as the solve will find them, for the length
-    // prefix pass every tile of the solve runs (SolveDesc.head)
-    DevBuf head = eng_->alloc((uint32_t)rows.size() * 16u);
+    // prefix pass every tile of the solve runs (SolveDesc.head): one copy
+    // batch, built in place
+    DevBuf head = eng_->alloc((uint32_t)m * 16u);
     if (head) {
-        for (size_t i = 0; i < rows.size(); ++i)
-            copy(head.addr() + i * 16, rows[i].buf, std::min<uint32_t>(16u, rows[i].initBytes));
+        if (b_->copies.empty()) {
+            b_->rows_close();
+            if (b_->nsegs == 0)
+                b_->new_segment();
+        }
+        std::vector<CopyItem>& cp = b_->copies;
+        size_t at = cp.size();
+        cp.resize(at + m);
+        uint32_t ext = 0;
+        for (size_t i = 0; i < m; ++i) {
+            const uint32_t len = std::min<uint32_t>(16u, ps.rows[i].initBytes);
+            if (len == 0)
+                continue;   // (as copy(): nothing to move)
+            CopyItem& c = cp[at++];
+            std::memset(&c, 0, sizeof(c));
+            c.dst = head.addr() + i * 16;
+            c.src = ps.rows[i].buf;
+            c.len = len;
+            ext = std::max(ext, len);
+        }
+        cp.resize(at);
+        ProgramBody::Segment& g = b_->segs[b_->nsegs - 1];
+        if (ext > g.maxExtent)
+            g.maxExtent = ext;
         b_->rows_close();   // (seal the copy batch into this segment)
     }
-    ProgramBody::PendingSolve& ps = b_->solves[b_->nsolves++];
     std::memset(&ps.desc, 0, sizeof(ps.desc));
     ps.desc.head = head.addr();
     eng_->release(head);   // (reused only after this submission completes)
-    ps.desc.m = (uint32_t)rows.size();
+    ps.desc.m = (uint32_t)m;
     ps.desc.maxBytes = maxBytes;
     ps.desc.result = b_->resultWords;
     b_->resultWords += ps.desc.m + 2;
-    ps.rows.assign(rows.begin(), rows.end());
-    ps.coef.assign(coef, coef + rows.size() * rows.size());
     const uint32_t r = ps.desc.result;
     b_->new_segment(); // ops after the solve go to the next segment
     return r;

@@ -257,6 +257,12 @@ public:
     /// Queue a triangular solve; returns the result-word index it will fill
     /// (valid in this program's completion callbacks of the flush that runs it).
     uint32_t solve(const std::vector<SolveRow>& rows, const uint8_t* coef, uint32_t maxBytes);
+    /// solve() in two halves, without the copies: solve_reserve hands out the
+    /// queued solve's own row descriptors (m) and coefficients (m x m) to
+    /// fill; solve_commit queues it (same result word as solve()).  No other
+    /// solve may be queued in between.
+    void solve_reserve(unsigned m, SolveRow** rows, uint8_t** coef);
+    uint32_t solve_commit(uint32_t maxBytes);
 
     /// Queue a device matrix generation + elimination (ops.h GeDesc) of
     /// rows x cols with a pick table of pickLen bytes: returns the job's
