@@ -227,6 +227,15 @@ struct Stream
 
     void init(const ScenarioConfig* c, Codec* k, StreamResult* r, unsigned globalIndex)
     {
+        // (a recycled stream starts over: every field back to its initial
+        // value, the vectors keeping their capacity)
+        phase = ADD;
+        i = tail = nextExpected = lastNum = recReceived = encodedAhead = 0;
+        tailMode = false;
+        dataOk = true;
+        log.clear();
+        decoded.clear();
+        getBuf.clear();
         cfg = c;
         codec = k;
         res = r;

@@ -664,6 +664,20 @@ struct BatchCodec
         return true;
     }
     bool wants_yield_after_encode() const { return sh->hashData; }
+    /// Back to the freshly constructed state (a recycled job's codec slot).
+    void reset()
+    {
+        enc = nullptr;
+        dec = nullptr;
+        cur.clear();
+        inFlight = 0;
+        decodes = 0;
+        slabs.clear();
+        slabUsed = kSlab;
+        ahead.clear();
+        aheadNext = 0;
+        aheadFail = 0;
+    }
 };
 
 using BatchStream = scen::Stream<BatchCodec, Rec, Pkt>;
@@ -929,6 +943,8 @@ struct Job
 {
     unsigned step = 0, begin = 0, end = 0;
     unsigned index = 0;             // step * groups + group
+    bool fresh = false;             // codecs not created yet: the first advance does it
+    bool second = false;            // e2e: the job's originals are in the second device copy
     std::vector<BatchCodec> codecs;
     std::unique_ptr<BatchStream[]> streams;
     // the job's own per-stream results: jobs of different steps run the
@@ -980,9 +996,38 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
     // their codecs right away (their state is still hot) unless tokens of
     // theirs still wait for device results; digests wait for the job's last
     // device bytes (retirement)
+    // a stream's codecs and state, made on the thread that then steps it
+    // (its first round: one fork-join instead of two, and the codec's memory
+    // first touched by the core that works on it)
+    auto start_stream = [&](Job& J, size_t i) {
+        BatchCodec& c = J.codecs[i];
+        c.reset();
+        c.sh = &sh;
+        c.payload = sh.frames ? (J.second ? sh.frameDev2 : sh.frameDev) : (J.second ? sh.payload2 : sh.payload);
+        {
+            CallTimer ct(kCreate);
+            c.enc = api.encoder_create();
+            c.dec = api.decoder_create();
+        }
+        c.flow = J.begin + (unsigned)i;
+        if (sh.frames) {
+            J.decTable[c.flow] = c.dec;   // (frames_recv reads only the entry of its frame's flow)
+            c.decTable = J.decTable.data();
+        }
+        c.log = &J.streams[i].log;
+        // the event log only feeds digests: timed bench steps run without it
+        J.streams[i].logOn = sh.verify || sh.hashData || sh.digest;
+        J.streams[i].init(cfg, &c, &J.res[i], cfg->first_stream + J.begin + (unsigned)i);
+        if (!c.enc || !c.dec)
+            J.streams[i].fail(2);
+    };
     auto advance = [&](Job& J) {
+        const bool fresh = J.fresh;
+        J.fresh = false;
         for_streams(sh, J.live.size(), [&](size_t k) {
             const unsigned i = J.live[k];
+            if (fresh)
+                start_stream(J, i);
             BatchStream& st = J.streams[i];
             while (!st.done())
                 if (st.step())
@@ -1001,6 +1046,7 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                      J.live.end());
     };
     std::vector<std::unique_ptr<Job>> active;
+    std::vector<std::unique_ptr<Job>> spareJobs;   // retired jobs, reused (their streams' vectors kept)
     // Resolve the tokens of J's completed rounds (oldest first).  -1 on a
     // device failure, else the number resolved.
     auto collect = [&](Job& J) {
@@ -1102,19 +1148,27 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             resolve_requests(sh, reqs);
             if (sh.verify || sh.hashData)
                 land_gathers(sh);   // (their requests point into the job's streams)
-            for_streams(sh, J.end - J.begin, [&](size_t i) {
+            auto finish_one = [&](size_t i) {
                 J.streams[i].finish();
                 CallTimer ct(kFree);
                 api.encoder_free(J.codecs[i].enc);   // (null if freed already)
                 api.decoder_free(J.codecs[i].dec);
                 J.codecs[i].enc = nullptr;
                 J.codecs[i].dec = nullptr;
-            });
+            };
+            // (without event logs there is no digest to hash and the codecs
+            // were freed as their streams finished: no fork-join for this)
+            if (sh.verify || sh.hashData || sh.digest)
+                for_streams(sh, J.end - J.begin, finish_one);
+            else
+                for (size_t i = 0; i < J.end - J.begin; ++i)
+                    finish_one(i);
             for (const StreamResult& r : J.res)
                 *payloadBytes += r.payload_bytes;
             if (J.step + 1 == nsteps)
                 std::copy(J.res.begin(), J.res.end(), results + J.begin);
             dump(J);
+            spareJobs.push_back(std::move(active[k]));   // (its vectors are reused by a later job)
             active.erase(active.begin() + (long)k);
             lap(4);
         }
@@ -1131,8 +1185,16 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
         };
         if (rc == 0 && next < jobs && active.size() < depth && !copy_busy(next)) {
             did = true;
-            std::unique_ptr<Job> jp(new Job);
+            std::unique_ptr<Job> jp;
+            if (!spareJobs.empty()) {
+                jp = std::move(spareJobs.back());
+                spareJobs.pop_back();
+            } else {
+                jp.reset(new Job);
+            }
             Job& J = *jp;
+            J.rounds.clear();
+            J.live.clear();
             J.step = next / G;
             const unsigned g = next % G;
             J.begin = (unsigned)((uint64_t)n * g / G);
@@ -1160,32 +1222,16 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 }
             }
             const unsigned cnt = J.end - J.begin;
-            J.codecs.resize(cnt);
-            J.streams.reset(new BatchStream[cnt]);
-            J.res.resize(cnt);
+            if (J.codecs.size() != cnt || !J.streams) {
+                J.codecs.clear();
+                J.codecs.resize(cnt);
+                J.streams.reset(new BatchStream[cnt]);
+            }
+            J.res.assign(cnt, StreamResult{});
             if (sh.frames)
                 J.decTable.assign(n, nullptr);
-            for_streams(sh, cnt, [&](size_t i) {
-                BatchCodec& c = J.codecs[i];
-                c.sh = &sh;
-                c.payload = sh.frames ? (second ? sh.frameDev2 : sh.frameDev) : (second ? sh.payload2 : sh.payload);
-                {
-                    CallTimer ct(kCreate);
-                    c.enc = api.encoder_create();
-                    c.dec = api.decoder_create();
-                }
-                c.flow = J.begin + (unsigned)i;
-                if (sh.frames) {
-                    J.decTable[c.flow] = c.dec;
-                    c.decTable = J.decTable.data();
-                }
-                c.log = &J.streams[i].log;
-                // the event log only feeds digests: timed bench steps run without it
-                J.streams[i].logOn = sh.verify || sh.hashData || sh.digest;
-                J.streams[i].init(cfg, &c, &J.res[i], cfg->first_stream + J.begin + (unsigned)i);
-                if (!c.enc || !c.dec)
-                    J.streams[i].fail(2);
-            });
+            J.second = second;
+            J.fresh = true;   // (the codecs are made by the first advance, start_stream)
             for (unsigned i = 0; i < cnt; ++i)
                 J.live.push_back(i);
             lap(0);
