@@ -441,6 +441,7 @@ void EncoderCore::finish_row(EncodeOut& out, const RowMeta& meta, unsigned paylo
 SiameseResult EncoderCore::encode(EncodeOut& out)
 {
     // :1146-1254
+    lastRowSiamese_ = false;
     if (dead())
         return Siamese_Disabled;
     if (count_ == 0) {
@@ -484,17 +485,46 @@ SiameseResult EncoderCore::encode_range_more(EncodeOut* out, unsigned count, uns
     std::vector<DevBuf> held;   // this call's packets before the last (and the chunks' before it)
     held.swap(recoveryHeld_);   // (capacity reused; ensure_recovery below finds none to release)
     SiameseResult r = Siamese_Success;
+    // After a Siamese row, encode() would choose a Siamese row again: its
+    // path depends on the window only, which no call of a range changes.
+    // Those rows skip the per-call dispatch and share one accounting.
+    bool siamese = false;
+    uint64_t opAcc = 0, outAcc = 0;
     for (unsigned k = 0; k < count; ++k) {
         if (k > 0 || !held.empty() || *produced) {
             // keep the previous packet: ensure_recovery would release it
             held.push_back(recovery_);
             recovery_ = DevBuf();
         }
-        r = encode(out[k]);
-        if (r != Siamese_Success)
-            break;
+        if (siamese) {
+            if (dead()) {
+                r = Siamese_Disabled;
+                break;
+            }
+            const unsigned row = nextRow_;
+            if (++nextRow_ >= kRowValuePeriod)
+                nextRow_ = 0;
+            recovery_ = eng_->alloc(longest_ + kMaxFooterBytes);
+            if (!recovery_) {
+                disabled_ = true;
+                r = Siamese_Disabled;
+                break;
+            }
+            uint64_t ob = 0;
+            r = siamese_row_body(out[k], row, &ob);
+            if (r != Siamese_Success)
+                break;
+            opAcc += ob;
+            outAcc += out[k].bytes;
+        } else {
+            r = encode(out[k]);
+            if (r != Siamese_Success)
+                break;
+            siamese = lastRowSiamese_;
+        }
         ++*produced;
     }
+    eng_->account(opAcc, outAcc);
     recoveryHeld_.swap(held);
     return r;
 }
@@ -568,9 +598,18 @@ SiameseResult EncoderCore::cauchy_row(EncodeOut& out)
 
 SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
 {
-    const unsigned recoveryBytes = longest_;
-    if (!ensure_recovery(recoveryBytes + kMaxFooterBytes))
+    if (!ensure_recovery(longest_ + kMaxFooterBytes))
         return Siamese_Disabled;
+    uint64_t opBytes = 0;
+    const SiameseResult r = siamese_row_body(out, row, &opBytes);
+    if (r == Siamese_Success)
+        eng_->account(opBytes, out.bytes);
+    return r;
+}
+
+SiameseResult EncoderCore::siamese_row_body(EncodeOut& out, unsigned row, uint64_t* opBytesOut)
+{
+    const unsigned recoveryBytes = longest_;
 
     // Dense part (:1046-1098): opcode bits 0-2 feed the row, 3-5 the product.
     // The lane sums are brought up to date first (their own ops precede the
@@ -590,11 +629,13 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
             return Siamese_Disabled;
     }
     staleSums_ &= ~want;
-    if (sumTableStale_) {
-        // the 24 sums as the rows read them (rebuilt only after a change)
+    if (sumTableStale_ || sumClipBytes_ != recoveryBytes) {
+        // the 24 sums as the rows read them (rebuilt only after a change),
+        // and the reference source bytes of each (clipped to the row)
         sumTableStale_ = false;
         sumTableVersion_ = Program::next_table_version();
         sumPresent_ = 0;
+        sumClipBytes_ = recoveryBytes;
         for (unsigned k = 0; k < kRowSums; ++k) {
             const DevSum& d = lanes_[k / kSums].sum[k % kSums];
             WinEntry& t = sumTable_[k];
@@ -603,13 +644,14 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
             t.column = 0;
             if (d.bytes > 0)
                 sumPresent_ |= 1u << k;
+            sumClip_[k] = std::min(d.bytes, recoveryBytes);
         }
     }
     const uint32_t mask[2] = {sel.mask[0] & sumPresent_, sel.mask[1] & sumPresent_};
     uint64_t opBytes = recoveryBytes; // final RX * product muladd
     for (unsigned h = 0; h < 2; ++h)
         for (uint32_t b = mask[h]; b; b &= b - 1)
-            opBytes += std::min(sumTable_[__builtin_ctz(b)].len, recoveryBytes);
+            opBytes += sumClip_[__builtin_ctz(b)];
     sumEnd_ = count_;
 
     RowMeta m;
@@ -617,8 +659,7 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     m.ldpcCount = unacked();
     m.columnStart = sumColumnStart_;
     m.row = row;
-    uint8_t footer[kMaxFooterBytes];
-    const unsigned footerBytes = write_footer(m, footer);
+    const unsigned footerBytes = write_footer(m, out.footer);
 
     // Sparse part (:1100-1144): ceil(n/16) PCG-chosen pairs, drawn on the
     // device, which also counts their reference source bytes
@@ -629,10 +670,16 @@ SiameseResult EncoderCore::siamese_row(EncodeOut& out, unsigned row)
     // of the program's Siamese row batch (consecutive rows share the sums)
     cover(std::min(start, sumStart_), sumEnd_);
     prog_.rows_row(sumTable_, recovery_.addr(), recoveryBytes, 0, row_value(row), mask[0], mask[1], row,
-                   n, start, count_, footer, footerBytes, sumTableVersion_);
-    eng_->account(opBytes);
+                   n, start, count_, out.footer, footerBytes, sumTableVersion_);
 
-    finish_row(out, m, recoveryBytes, true);
+    out.meta = m;
+    out.footerBytes = footerBytes;
+    out.buf = recovery_;
+    out.bytes = recoveryBytes + footerBytes;
+    stats_[SiameseEncoderStats_RecoveryCount]++;
+    stats_[SiameseEncoderStats_RecoveryBytes] += out.bytes;
+    lastRowSiamese_ = true;
+    *opBytesOut = opBytes;
     return Siamese_Success;
 }
 

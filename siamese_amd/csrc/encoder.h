@@ -169,6 +169,9 @@ private:
     SiameseResult single_row(EncodeOut& out);
     SiameseResult cauchy_row(EncodeOut& out);
     SiameseResult siamese_row(EncodeOut& out, unsigned row);
+    /// siamese_row without the buffer (recovery_ holds it) and the
+    /// accounting (*opBytes: the row's reference source bytes)
+    SiameseResult siamese_row_body(EncodeOut& out, unsigned row, uint64_t* opBytes);
     bool ensure_recovery(unsigned bytes);
     void finish_row(EncodeOut& out, const RowMeta& meta, unsigned payloadBytes,
                     bool footerWritten = false);
@@ -209,6 +212,9 @@ private:
     uint32_t sumPresent_ = 0;   // sums holding bytes
     bool sumTableStale_ = true;
     uint64_t sumTableVersion_ = 0;   // Program::rows_row's tag of sumTable_ as last rebuilt
+    uint32_t sumClip_[kRowSums] = {};   // min(sum bytes, sumClipBytes_): reference source bytes
+    unsigned sumClipBytes_ = ~0u;       // the row length sumClip_ was made for
+    bool lastRowSiamese_ = false;       // the last encode() made a Siamese row
 
     DevBuf recovery_;          // reused recovery packet buffer
     std::vector<DevBuf> recoveryHeld_;   // encode_range's earlier packets (released by the next encode)
