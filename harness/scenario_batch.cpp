@@ -1156,9 +1156,13 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 J.codecs[i].enc = nullptr;
                 J.codecs[i].dec = nullptr;
             };
-            // (without event logs there is no digest to hash and the codecs
-            // were freed as their streams finished: no fork-join for this)
-            if (sh.verify || sh.hashData || sh.digest)
+            // (without event logs there is no digest to hash, and codecs are
+            // freed as their streams finish unless tokens of theirs were
+            // still in flight then: no fork-join when nothing is left to do)
+            bool work = sh.verify || sh.hashData || sh.digest;
+            for (size_t i = 0; i < J.end - J.begin && !work; ++i)
+                work = J.codecs[i].enc || J.codecs[i].dec;
+            if (work)
                 for_streams(sh, J.end - J.begin, finish_one);
             else
                 for (size_t i = 0; i < J.end - J.begin; ++i)
