@@ -69,12 +69,6 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct);
 void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
                      const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
                      uint32_t solveBegin, uint32_t solveCount);
-/// Called once per later be_launch_solve phase of the submission, in the same
-/// order, after the upload and before the submission's first exec launch:
-/// the backend may start work that reads only the coefficients (the product
-/// solves' inverses) beside the exec launches.  Optional for the caller.
-void be_prepare_solve(const SolveDesc* solves, const uint8_t* coef, uint32_t maxRows, uint32_t solveBegin,
-                      uint32_t solveCount);
 
 /// Device recovery-matrix generation + elimination (ops.h GeDesc): one job
 /// per desc, its input at in + desc.in, its output in results + desc.result.

@@ -16,7 +16,6 @@
 //                  multiply + back-substitution per tile (the reference's
 //                  sweeps: small launches, flagged solves)
 //   k_solve_prefix the length pass alone (sweeps-only launches)
-//   k_solve_mfma   X = T R on the int8 matrix cores (opt-in)
 //   k_ge           a decode's recovery matrix and its elimination (opt-in)
 //
 // GF(256) multiply by a wave-uniform constant uses three v_perm_b32 byte
@@ -908,11 +907,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint32_t updMaxLast1;   // 1 + the last element any update of the batch folds in (0: none)
     // the version corrections of the batch's first kVersionRows rows (this
     // tile, dword layout), computed per lane sum in phase A
-#ifdef SGPU_NO_CORR
-    __shared__ uint32_t corrL[1][2][64];
-#else
     __shared__ uint32_t corrL[kVersionRows][2][64];
-#endif
     __shared__ uint4 permL[256];                   // c_perm[y] words 0..3
     __shared__ uint32_t permC[256];                // c_perm[y] word 4
     // stage slot k < 24: lane sum k after the batch's updates; slot 24 + e:
@@ -1081,11 +1076,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 updAcc[i] = 0;
             // rows [0, Rv) of a versioned batch (GfOp.dst high word, ops.h)
             // take their corrections from corrL
-#ifdef SGPU_NO_CORR
-            const uint32_t Rv = 0;
-#else
             const uint32_t Rv = min(min(uni(h0.y), R), (uint32_t)kVersionRows);
-#endif
             for (uint32_t i = tid; i < Rv * 128; i += kExecThreads)
                 (&corrL[0][0][0])[i] = 0;
             if (tid == 0)
@@ -2497,19 +2488,19 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const uint8_t* C = coef + sd.coefOffset;
     if (m > kSolveLdsMaxRows)
         return;   // (the host never queues m > 255: kMaximumLossRecoveryCount)
-    // flags bit 0: k_solve_prefix already solved the length prefixes; bit 1:
-    // k_solve_mfma ran before this launch, bit 2: k_solve_tr did (each took
-    // every solve it could, into the scratch)
+    // flags bit 0: the length prefixes are already solved (k_solve_prefix or
+    // k_solve_pre); bit 2: k_solve_tr ran before this launch (it took every
+    // solve it could, into the scratch)
     const bool prefixDone = (flags & 1u) != 0;
-    if ((flags & 6u) && m <= kMfmaMaxRows && sd.tinv && results[sd.result] == m &&
+    if ((flags & 6u) && m <= kProductMaxRows && sd.tinv && results[sd.result] == m &&
         results[sd.result + m + 1] == 0) {
-        // solved as X = T R (k_solve_tr or k_solve_mfma), every row zero past
+        // solved as X = T R (k_solve_tr), every row zero past
         // its recovered length, so the sweeps' clipping would change nothing:
         // this tile of the result rows from the scratch into the rows (bytes
         // below each row's final length).  A solve whose products have
         // non-zero bytes there (inconsistent recovery data) falls through to
         // the sweeps, on its rows as they were: the products went to scratch.
-        static_assert(kMfmaMaxRows <= kSolveWideMaxRows, "matrix-core solves take 1 KiB tiles");
+        static_assert(kProductMaxRows <= kSolveWideMaxRows, "product solves take 1 KiB tiles");
         const uint32_t xs = solve_x_stride(sd.maxBytes), tb = kTileBytes;
         for (uint32_t x = threadIdx.x; x < m * (tb / 16u); x += 64u * kSolveWaves) {
             const uint32_t i = x / (tb / 16u), p = it.tileBase + 16u * (x - i * (tb / 16u));
@@ -2593,17 +2584,12 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// Bulk solve on the matrix cores (k_solve_pre + k_solve_mfma)
+// The product solve's inverse and length prefixes (k_solve_pre)
 //
 // The solve's result rows are X = T R, with T = U^-1 L^-1 the m x m inverse
 // of the eliminated coefficient matrix (MultiplyLowerTriangle applies L^-1,
-// BackSubstitution U^-1; reference SiameseDecoder.cpp:1065-1238).  Over
-// GF(2) a GF(256) product c*x is the 8x8 bit matrix of c applied to x's bits,
-// so X's bits are one binary matrix product,
-//     bit b of X[i][n] = parity( sum_{j,k} bit b of (T[i][j] * 2^k) * bit k of R[j][n] ),
-// an integer dot product of 0/1 bytes whose low bit is the GF(2) sum: the
-// int8 MFMA v_mfma_i32_32x32x32_i8 computes 32 output bits x 32 columns over
-// 32 input bits (four input rows) per instruction, exactly.
+// BackSubstitution U^-1; reference SiameseDecoder.cpp:1065-1238); k_solve_tr
+// forms the product.
 //
 // k_solve_pre (one launch, two kinds of workgroup):
 //   workgroups [0, n): the length-prefix pass of solve b (all waves stage the
@@ -2612,69 +2598,38 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
 //   to the identity in LDS (rows of m <= 120 bytes, one half-wave a row),
 //   written to the solve's scratch (SolveDesc.tinv, rows of kTStride bytes).
 // The two kinds run side by side, so T costs no time on the prefix pass's
-// serial critical path.
-//
-// k_solve_mfma: one workgroup per (solve, 32 output rows); wave w computes
-// output rows 4w..4w+3 of its group, its A operands read from the group's
-// bit-matrix table AF (8 bytes per T coefficient: c_aff, the multiply-by-y
-// bit matrix) one 16-bit LDS read per K step.  Per 64-column chunk: the rows'
-// bytes are expanded to 0/1 bytes in LDS (the B operand, laid out so a
-// lane's 16-byte fragment is one ds_read_b128), each wave runs its K loop,
-// the parities are packed back to bytes and stored.
-// It runs only when the prefix pass found every recovered length valid
-// (results[0] == m): the exact sweeps and the prefixes then agree byte for
-// byte, since bytes past a row's length are zero in the true originals (the
-// clips of the sequential sweeps change nothing).  A solve with a corrupt
-// prefix, or m > kMfmaMaxRows, is left to k_solve_main, which reproduces the
-// reference's partial back-substitution exactly.
-#ifndef SGPU_PRE_PHASE
-#define SGPU_PRE_PHASE 0   // timing aids (wrong outputs): 1 no inverses, 2 no prefix pass
-#endif
-constexpr unsigned kMfmaWaves = 8;
-constexpr unsigned kMfmaThreads = 64 * kMfmaWaves;
-constexpr unsigned kMfmaYStride = kTStride;            // bytes per row of T in LDS
-constexpr unsigned kMfmaTiles = 2;                     // 32-column MFMA tiles per chunk
-constexpr unsigned kMfmaChunk = 32 * kMfmaTiles;       // columns per chunk
-constexpr unsigned kMfmaGroupRows = 4 * kMfmaWaves;    // output rows per workgroup
-constexpr unsigned kMfmaGroups = (kMfmaMaxRows + kMfmaGroupRows - 1) / kMfmaGroupRows;
+// serial critical path.  The product runs only when the prefix pass found
+// every recovered length valid (results[0] == m): the exact sweeps and the
+// prefixes then agree byte for byte, since bytes past a row's length are zero
+// in the true originals.  A solve with a corrupt prefix, or m >
+// kProductMaxRows, is left to k_solve_main, which reproduces the reference's
+// partial back-substitution exactly.  (The same product on the int8 matrix
+// cores was built and measured slower: tools/variants/solve_mfma.hip.)
+constexpr unsigned kPreWaves = 8;
+constexpr unsigned kPreThreads = 64 * kPreWaves;
 
-__constant__ __attribute__((aligned(16))) uint8_t c_aff[256][8];   // [y][7 - b]: bit k = bit b of y * 2^k (GF2P8AFFINEQB rows)
-
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x16 __attribute__((ext_vector_type(16)));
-
-__host__ __device__ constexpr uint32_t mfma_rows(uint32_t m) { return (m + 3u) & ~3u; }
+__host__ __device__ constexpr uint32_t t_rows(uint32_t m) { return (m + 3u) & ~3u; }
 // k_solve_pre: the larger of the prefix pass's staging and the T build's
 __host__ __device__ constexpr uint32_t solve_tbuild_lds_bytes(uint32_t m)
 {
-    return ((m * m + 15u) & ~15u) + mfma_rows(m) * kMfmaYStride + 256u * 20u;
+    return ((m * m + 15u) & ~15u) + t_rows(m) * kTStride + 256u * 20u;
 }
 __host__ __device__ constexpr uint32_t solve_pre_lds_bytes(uint32_t m)
 {
-    return solve_prefix_lds_bytes(m) > solve_tbuild_lds_bytes(m < kMfmaMaxRows ? m : kMfmaMaxRows)
+    return solve_prefix_lds_bytes(m) > solve_tbuild_lds_bytes(m < kProductMaxRows ? m : kProductMaxRows)
                ? solve_prefix_lds_bytes(m)
-               : solve_tbuild_lds_bytes(m < kMfmaMaxRows ? m : kMfmaMaxRows);
+               : solve_tbuild_lds_bytes(m < kProductMaxRows ? m : kProductMaxRows);
 }
-// k_solve_mfma: the group's bit-matrix table, the B operand, the packed
-// outputs, the rows' lengths
-__host__ __device__ constexpr uint32_t solve_mfma_lds_bytes(uint32_t m)
-{
-    return kMfmaGroupRows * 8u * mfma_rows(m) + mfma_rows(m) * 8u * kMfmaChunk + kMfmaGroupRows * kMfmaChunk +
-           ((3u * m * 4u + 15u) & ~15u) + m * 8u + 16u;
-}
-
-// the four low bits of v as four 0/1 bytes (byte q = bit q)
-__device__ __forceinline__ uint32_t bits4(uint32_t v) { return ((v & 15u) * 0x00204081u) & 0x01010101u; }
 
 // T = U^-1 L^-1 of solve sd into sd.tinv (all waves of the workgroup)
 __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C, uint8_t* base, uint32_t tid)
 {
-    const uint32_t m = sd.m, mp = mfma_rows(m);
+    const uint32_t m = sd.m, mp = t_rows(m);
     uint8_t* Ct = base;                                          // Ct[i*m + j] = C[j][i]
-    uint8_t* Y = Ct + ((m * m + 15u) & ~15u);                    // T, rows of kMfmaYStride bytes
-    uint4* permL = reinterpret_cast<uint4*>(Y + mp * kMfmaYStride);
+    uint8_t* Y = Ct + ((m * m + 15u) & ~15u);                    // T, rows of kTStride bytes
+    uint4* permL = reinterpret_cast<uint4*>(Y + mp * kTStride);
     uint32_t* permC = reinterpret_cast<uint32_t*>(permL + 256);
-    stage_transposed<kMfmaThreads, 2>(Ct, C, m, tid);
+    stage_transposed<kPreThreads, 2>(Ct, C, m, tid);
     if (tid < 256) {
         const uint32_t* t = c_perm[tid];
         permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
@@ -2682,14 +2637,14 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
     }
     // T starts as the identity (rows past m stay zero)
     uint32_t* Yw = reinterpret_cast<uint32_t*>(Y);
-    for (uint32_t k = tid; k < mp * (kMfmaYStride / 4); k += kMfmaThreads) {
-        const uint32_t i = k / (kMfmaYStride / 4), c4 = (k % (kMfmaYStride / 4)) * 4;
+    for (uint32_t k = tid; k < mp * (kTStride / 4); k += kPreThreads) {
+        const uint32_t i = k / (kTStride / 4), c4 = (k % (kTStride / 4)) * 4;
         Yw[k] = (i < m && i >= c4 && i < c4 + 4) ? 1u << (8 * (i - c4)) : 0u;
     }
     __syncthreads();
     // MultiplyLowerTriangle, then BackSubstitution, on the identity's rows (a
     // row of T is m <= 120 bytes: one half-wave, four bytes a lane)
-    constexpr uint32_t kHalves = kMfmaThreads / 32;
+    constexpr uint32_t kHalves = kPreThreads / 32;
     const uint32_t hw = tid >> 5, l32 = tid & 31;
     for (uint32_t i = 0; i + 1 < m; ++i) {
         const uint32_t src = Yw[i * 32 + l32];
@@ -2710,13 +2665,13 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
         __syncthreads();
     }
     GMEM uint32_t* out = reinterpret_cast<GMEM uint32_t*>(sd.tinv);
-    for (uint32_t k = tid; k < mp * 32u; k += kMfmaThreads) {
+    for (uint32_t k = tid; k < mp * 32u; k += kPreThreads) {
         const uint32_t i = k >> 5;
         out[k] = i < m ? gf_mul_tab(Yw[k], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]])) : 0u;
     }
 }
 
-__global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __restrict__ solves,
+__global__ __launch_bounds__(kPreThreads) void k_solve_pre(const SolveDesc* __restrict__ solves,
                                                           const SolveRow* __restrict__ rows,
                                                           const uint8_t* __restrict__ coef,
                                                           uint32_t* __restrict__ results,
@@ -2729,7 +2684,7 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __r
     const uint32_t tid = threadIdx.x;
     if (mode == 1 || (mode == 0 && blockIdx.x >= count)) {
         const SolveDesc sd = solves[mode == 1 ? blockIdx.x : blockIdx.x - count];
-        if (sd.m == 0 || sd.m > kMfmaMaxRows || sd.tinv == 0 || SGPU_PRE_PHASE == 1)
+        if (sd.m == 0 || sd.m > kProductMaxRows || sd.tinv == 0)
             return;   // (uniform)
         solve_tbuild(sd, coef + sd.coefOffset, reinterpret_cast<uint8_t*>(X), tid);
         return;
@@ -2756,11 +2711,9 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __r
     }
     if (tid == 0)
         results[sd.result + m + 1] = 0;   // the product solves' tail flag
-    if (SGPU_PRE_PHASE == 2)
-        return;
     // (every wave stages; then wave 0 alone runs the serial pass)
-    stage_transposed<kMfmaThreads, 2>(Ct, C, m, tid);
-    for (uint32_t j = tid; j < m; j += kMfmaThreads) {
+    stage_transposed<kPreThreads, 2>(Ct, C, m, tid);
+    for (uint32_t j = tid; j < m; j += kPreThreads) {
         lowL[j] = R[j].lowerLen;
         finB[j] = R[j].finalBytes;
     }
@@ -2768,129 +2721,6 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_pre(const SolveDesc* __r
     if (tid >= 64)
         return;
     solve_prefix_wave(m, tid, p4, Ct, lowL, finB, permL, permC, rw, results + sd.result, acct);
-}
-
-__global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __restrict__ solves,
-                                                           const SolveRow* __restrict__ rows,
-                                                           uint32_t* results)
-{
-    extern __shared__ uint4 Ls[];
-    const uint32_t grp = blockIdx.x % kMfmaGroups;
-    const SolveDesc sd = solves[blockIdx.x / kMfmaGroups];
-    const uint32_t m = sd.m, mp = mfma_rows(m);
-    if (m == 0 || m > kMfmaMaxRows || sd.tinv == 0 || grp * kMfmaGroupRows >= mp || results[sd.result] != m)
-        return;   // (uniform: k_solve_main solves it, or another group has these rows)
-    const SolveRow* R = rows + sd.rowBegin;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t row0 = grp * kMfmaGroupRows;
-
-    uint8_t* AF = reinterpret_cast<uint8_t*>(Ls);                // [il][q][j]: c_aff[T[row0+il][j]][q]
-    uint8_t* bits = AF + kMfmaGroupRows * 8u * mp;
-    uint8_t* outT = bits + mp * 8u * kMfmaChunk;
-    uint32_t* initB = reinterpret_cast<uint32_t*>(outT + kMfmaGroupRows * kMfmaChunk);
-    uint32_t* finB = initB + m;
-    uint32_t* bbB = finB + m;                                    // recovered header + length
-    uint64_t* rowBuf = reinterpret_cast<uint64_t*>(bbB + ((m + 1u) & ~1u));
-
-    const GMEM uint8_t* T = reinterpret_cast<const GMEM uint8_t*>(sd.tinv);
-    for (uint32_t x = tid; x < kMfmaGroupRows * mp; x += kMfmaThreads) {
-        const uint32_t il = x / mp, j = x - il * mp;
-        const uint32_t i = row0 + il;
-        const uint32_t y = (i < m && j < m) ? T[i * kMfmaYStride + j] : 0u;
-        const uint2 a = *reinterpret_cast<const uint2*>(c_aff[y]);
-#pragma unroll
-        for (uint32_t q = 0; q < 8; ++q)
-            AF[(il * 8u + q) * mp + j] = (uint8_t)((q < 4 ? a.x : a.y) >> (8 * (q & 3)));
-    }
-    for (uint32_t j = tid; j < m; j += kMfmaThreads) {
-        initB[j] = R[j].initBytes;
-        finB[j] = R[j].finalBytes;
-        rowBuf[j] = R[j].buf;
-        const uint32_t w = results[sd.result + 1 + j];
-        bbB[j] = (w >> 29) + (w & kSolveLengthMask);
-    }
-    __syncthreads();
-
-    const uint32_t S = mp / 4;   // K steps (four input rows = 32 input bits each)
-    uint32_t maxB = 0;
-    for (uint32_t j = 0; j < m; ++j)
-        maxB = finB[j] > maxB ? finB[j] : maxB;
-    const uint32_t r = lane & 31, h = lane >> 5;
-    // lane's A row: output bit 7 - (r & 7) of row row0 + 4 wave + r / 8
-    const uint8_t* af = AF + ((4u * wave + (r >> 3)) * 8u + (7u - (r & 7u))) * mp + 2u * h;
-    const bool active = row0 + 4u * wave < mp;
-    const uint32_t rowsHere = (m - row0 < kMfmaGroupRows ? m - row0 : kMfmaGroupRows);
-    const uint32_t xs = solve_x_stride(sd.maxBytes);
-    for (uint32_t c0 = 0; c0 < maxB; c0 += kMfmaChunk) {
-        // the B operand: byte (j, col) as eight 0/1 bytes at
-        // bits[((t * S + j / 4) * 64 + (j % 4) / 2 * 32 + col % 32) * 16 + (j % 2) * 8],
-        // t = col / 32 (lane h * 32 + r's 16-byte fragment of K step s is
-        // contiguous, lanes in order: conflict-free ds_read_b128); item `it`
-        // is the 8-byte slot it * 8, so a wave's stores are one contiguous
-        // 512-byte run (the per-dword stores they replace were 16-way bank
-        // conflicts: SQ_LDS_BANK_CONFLICT 47.7 M cycles per launch)
-        for (uint32_t it = tid; it < mp * kMfmaChunk; it += kMfmaThreads) {
-            const uint32_t blk = it >> 7, w = it & 127u;
-            const uint32_t t = blk / S, g = blk - t * S;
-            const uint32_t j = 4u * g + 2u * (w >> 6) + (w & 1u), col = 32u * t + ((w >> 1) & 31u);
-            uint32_t v = 0;
-            if (j < m) {
-                const uint32_t p = c0 + col;
-                if (p < initB[j])
-                    v = *reinterpret_cast<const GMEM uint8_t*>(rowBuf[j] + p);
-            }
-            *reinterpret_cast<uint2*>(bits + 8u * it) = make_uint2(bits4(v), bits4(v >> 4));
-        }
-        __syncthreads();
-        if (active) {
-            i32x16 acc[kMfmaTiles];
-#pragma unroll
-            for (uint32_t t = 0; t < kMfmaTiles; ++t)
-                acc[t] = i32x16{};
-            for (uint32_t s = 0; s < S; ++s) {
-                // A[r][16 h + jj]: bit b of T[i][4 s + 2 h + jj / 8] * 2^(jj % 8)
-                const uint32_t u = *reinterpret_cast<const uint16_t*>(af + 4u * s);
-                const i32x4 A = {(int)bits4(u), (int)bits4(u >> 4), (int)bits4(u >> 8), (int)bits4(u >> 12)};
-#pragma unroll
-                for (uint32_t t = 0; t < kMfmaTiles; ++t) {
-                    const i32x4 B = *reinterpret_cast<const i32x4*>(bits + ((t * S + s) * 64 + h * 32 + r) * 16);
-                    acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc[t], 0, 0, 0);
-                }
-            }
-            // D[row][col]: row = (reg & 3) + 8 (reg >> 2) + 4 h, col = r; row
-            // 8 g + 4 h + q is bit 4 h + q of output row 4 wave + g (local)
-#pragma unroll
-            for (uint32_t t = 0; t < kMfmaTiles; ++t)
-#pragma unroll
-                for (uint32_t g = 0; g < 4; ++g) {
-                    const uint32_t nib = (acc[t][4 * g] & 1) | (acc[t][4 * g + 1] & 1) << 1 |
-                                         (acc[t][4 * g + 2] & 1) << 2 | (acc[t][4 * g + 3] & 1) << 3;
-                    const uint32_t v = nib << (4 * h);
-                    const uint32_t byte = v | (uint32_t)__shfl_xor((int)v, 32);
-                    if (h == 0)
-                        outT[(4 * wave + g) * kMfmaChunk + t * 32 + r] = (uint8_t)byte;
-                }
-        }
-        __syncthreads();
-        // x masked past the recovered length, stored below the row's final
-        // bytes (the stores of the exact back-substitution) into the result
-        // scratch: another group may still read these rows' bytes; the tile
-        // pass (k_solve_main) copies them into the rows
-        // (a non-zero byte past a row's recovered length flags the solve for
-        // the exact sweeps, as in k_solve_tr)
-        uint32_t tail = 0;
-        for (uint32_t it = tid; it < rowsHere * (kMfmaChunk / 16); it += kMfmaThreads) {
-            const uint32_t il = it / (kMfmaChunk / 16), u = it % (kMfmaChunk / 16);
-            const uint32_t i = row0 + il, p = c0 + 16 * u;
-            const uint4 v = *reinterpret_cast<const uint4*>(outT + il * kMfmaChunk + 16 * u);
-            const uint4 k = mask16(v, (int)bbB[i] - (int)p);
-            tail |= (v.x ^ k.x) | (v.y ^ k.y) | (v.z ^ k.z) | (v.w ^ k.w);
-            if (p < finB[i])
-                st16(sd.xout + (uint64_t)i * xs + p, k);
-        }
-        if (__any(tail != 0) && lane == 0)
-            atomicOr(results + sd.result + 1 + m, 1u);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2914,9 +2744,6 @@ __global__ __launch_bounds__(kMfmaThreads) void k_solve_mfma(const SolveDesc* __
 // each instead of the idle lanes of 16-byte-per-lane tiles.
 #ifndef SGPU_TR_WAVES
 #define SGPU_TR_WAVES 8
-#endif
-#ifndef SGPU_TR_PHASE
-#define SGPU_TR_PHASE 0   // timing aids (wrong outputs): 1 no products, 2 no row loads
 #endif
 #ifndef SGPU_TR_LDS_TABLES
 #define SGPU_TR_LDS_TABLES 0
@@ -2953,14 +2780,12 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
         const uint64_t buf = R[j].buf;
         const uint32_t ib = R[j].initBytes;
         uint32_t v[4] = {0, 0, 0, 0};
-#if SGPU_TR_PHASE != 2
 #pragma unroll
         for (unsigned q = 0; q < NQ; ++q) {
             const uint32_t p = tileBase + 256u * q + 4u * lane;
             if (p < ib)
                 v[q] = ld4(buf + p) & byte_mask((int)ib - (int)p);
         }
-#endif
         X[j * 64u + lane] = make_uint4(v[0], v[1], v[2], v[3]);
     }
     // this wave's rows of T (lane l < 32: bytes 4 l .. 4 l + 3 of each)
@@ -2982,7 +2807,7 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
 #pragma unroll
         for (unsigned q = 0; q < NQ; ++q)
             acc[t][q] = 0;
-    for (uint32_t k0 = 0; k0 < (SGPU_TR_PHASE == 1 ? 0u : m); k0 += 4) {
+    for (uint32_t k0 = 0; k0 < m; k0 += 4) {
         uint32_t tw[RW];
 #pragma unroll
         for (unsigned t = 0; t < RW; ++t)
@@ -3060,9 +2885,9 @@ template <unsigned NQ>
 __device__ __forceinline__ void solve_tr_rows(const SolveDesc& sd, const SolveRow* R, uint32_t* res,
                                               uint32_t tileBase, uint4* X)
 {
-    // output rows per wave: ceil(m / 8) <= 15 (m <= kMfmaMaxRows), rounded
+    // output rows per wave: ceil(m / 8) <= 15 (m <= kProductMaxRows), rounded
     // up to one of these
-    static_assert(kMfmaMaxRows <= 15 * kTrStep && kTrThreads <= 1024, "k_solve_tr keeps at most 15 rows per wave");
+    static_assert(kProductMaxRows <= 15 * kTrStep && kTrThreads <= 1024, "k_solve_tr keeps at most 15 rows per wave");
     const uint32_t rw = (sd.m + kTrStep - 1) / kTrStep;
     switch (rw) {
     case 1:
@@ -3089,7 +2914,7 @@ __global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __rest
     extern __shared__ uint4 X[];
     const SolveItem it = items[blockIdx.x / kTrSplit];
     const SolveDesc sd = solves[it.solve];
-    if (sd.m == 0 || sd.m > kMfmaMaxRows || sd.tinv == 0 || results[sd.result] != sd.m ||
+    if (sd.m == 0 || sd.m > kProductMaxRows || sd.tinv == 0 || results[sd.result] != sd.m ||
         it.tileBase >= sd.maxBytes)
         return;   // (uniform: k_solve_main solves it)
     const uint32_t left = sd.maxBytes - it.tileBase;
@@ -3340,27 +3165,6 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
     }
 }
 
-// Layout check of the int8 MFMA (tests): D = A B for 32 x 32 x 32 with
-// asymmetric integer data, fragments as k_solve_mfma reads them.
-__global__ void k_mfma_i8_check(int* __restrict__ out)
-{
-    const uint32_t l = threadIdx.x, r = l & 31, h = l >> 5;
-    i32x4 A, B;
-    int8_t* a = reinterpret_cast<int8_t*>(&A);
-    int8_t* b = reinterpret_cast<int8_t*>(&B);
-    for (uint32_t jj = 0; jj < 16; ++jj) {
-        const uint32_t k = 16 * h + jj;
-        a[jj] = (int8_t)((int)((r * 7 + k * 3) % 5) - 2);
-        b[jj] = (int8_t)((int)((k * 11 + r * 5) % 7) - 3);
-    }
-    i32x16 acc = {};
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, acc, 0, 0, 0);
-    for (uint32_t reg = 0; reg < 16; ++reg) {
-        const uint32_t row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        out[row * 32 + r] = acc[reg];
-    }
-}
-
 // ---------------------------------------------------------------------------
 // Host side
 
@@ -3369,10 +3173,6 @@ namespace {
 hipStream_t g_stream = nullptr;
 hipStream_t g_stageStream = nullptr;    // application H2D staging (be_stage_h2d)
 hipStream_t g_gatherStream = nullptr;   // gathers of completed results (be_gather)
-hipStream_t g_invStream = nullptr;      // the product solves' inverses beside k_exec (be_prepare_solve)
-std::mutex g_invMu;
-std::deque<hipEvent_t> g_invPending;    // one per prepared solve phase, in launch order
-std::vector<hipEvent_t> g_invFree;
 bool g_ready = false;
 int g_device = 0;
 
@@ -3536,8 +3336,7 @@ bool be_init(int device, const char** err)
         return false;
     }
     if (hipStreamCreateWithFlags(&g_stageStream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&g_gatherStream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&g_invStream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&g_gatherStream, hipStreamNonBlocking) != hipSuccess) {
         *err = "hipStreamCreate (transfer streams) failed";
         return false;
     }
@@ -3562,12 +3361,6 @@ bool be_init(int device, const char** err)
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_perm), perm, sizeof(perm)), "hipMemcpyToSymbol(perm)");
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_inv), g_gf.inv, 256), "hipMemcpyToSymbol(inv)");
     check(hipMemcpyToSymbol(HIP_SYMBOL(c_sqr), g_gf.sqr, 256), "hipMemcpyToSymbol(sqr)");
-    // the multiply-by-y bit matrices, row b of y at [y][7 - b] (gf.h affine)
-    static uint8_t aff[256][8];
-    for (unsigned y = 0; y < 256; ++y)
-        for (unsigned k = 0; k < 8; ++k)
-            aff[y][k] = (uint8_t)(g_gf.affine[y] >> (8 * k));
-    check(hipMemcpyToSymbol(HIP_SYMBOL(c_aff), aff, sizeof(aff)), "hipMemcpyToSymbol(aff)");
     // PCG jump-ahead: state after j draws = A^j s + inc * (A^0 + ... + A^(j-1))
     uint64_t pa[65], pg[65];
     pa[0] = 1;
@@ -3597,8 +3390,6 @@ bool be_init(int device, const char** err)
         const size_t dyn = ldsPerCu > staticLds ? ldsPerCu - staticLds : 0;
         // (the sums, the window and one zero slot)
         g_stageCap = dyn / kExecTileBytes > kRowSums + 1 ? (uint32_t)(dyn / kExecTileBytes) - kRowSums - 1 : 0;
-        if (const char* sc = std::getenv("SGPU_STAGE"))
-            g_stageCap = std::min<uint32_t>(g_stageCap, (uint32_t)std::atoi(sc));
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_exec),
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)((kRowSums + g_stageCap + 1) * kExecTileBytes)) != hipSuccess)
@@ -3611,13 +3402,8 @@ bool be_init(int device, const char** err)
         *err = "the device refused the triangular solve's LDS (gfx950 grants 160 KiB per workgroup)";
         return false;
     }
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_mfma), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)solve_mfma_lds_bytes(kMfmaMaxRows)) != hipSuccess) {
-        *err = "the device refused the matrix-core solve's LDS";
-        return false;
-    }
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_tr), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)solve_tr_lds_bytes(kMfmaMaxRows)) != hipSuccess) {
+                            (int)solve_tr_lds_bytes(kProductMaxRows)) != hipSuccess) {
         *err = "the device refused the vector product solve's LDS";
         return false;
     }
@@ -3642,32 +3428,6 @@ bool be_init(int device, const char** err)
 
 const char* be_name() { return "hip-gfx950"; }
 
-// Test hook: the int8 MFMA fragment layout k_solve_mfma relies on, against
-// the host's product of the same 32 x 32 x 32 integer matrices.  Returns the
-// number of differing outputs (0: the layout holds), -1 on a device error.
-extern "C" __attribute__((visibility("default"))) int sgpu_selftest_mfma_i8(void)
-{
-    bind_device();
-    int* d = nullptr;
-    if (hipMalloc(&d, 32 * 32 * sizeof(int)) != hipSuccess)
-        return -1;
-    hipLaunchKernelGGL(k_mfma_i8_check, dim3(1), dim3(64), 0, g_stream, d);
-    int h[32 * 32];
-    const bool ok = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, g_stream) == hipSuccess &&
-                    hipStreamSynchronize(g_stream) == hipSuccess;
-    (void)hipFree(d);
-    if (!ok)
-        return -1;
-    int bad = 0;
-    for (int i = 0; i < 32; ++i)
-        for (int j = 0; j < 32; ++j) {
-            int want = 0;
-            for (int k = 0; k < 32; ++k)
-                want += ((i * 7 + k * 3) % 5 - 2) * ((k * 11 + j * 5) % 7 - 3);
-            bad += h[i * 32 + j] != want;
-        }
-    return bad;
-}
 
 #ifdef SGPU_PHASE_CLOCKS
 extern "C" __attribute__((visibility("default"))) void sgpu_debug_phase_clocks(unsigned long long* out32)
@@ -3861,7 +3621,6 @@ namespace {
 enum SolvePath
 {
     kPathSweeps = 0,   // k_solve_prefix + k_solve_main
-    kPathMfma = 1,     // k_solve_pre + k_solve_mfma + k_solve_main
     kPathVector = 2,   // k_solve_pre + k_solve_tr + k_solve_main
 };
 
@@ -3874,40 +3633,21 @@ void launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* 
     // in parallel); few (single-stream flushes): fused into the tiles, one
     // launch fewer on the flush's critical path.
     const bool separate = solveCount >= kSolvePrefixSplit;
-    const bool mfma = separate && path == kPathMfma;
     const bool tr = separate && path == kPathVector;
     unsigned long long* acctL = reinterpret_cast<unsigned long long*>(acct);
-    const uint32_t prodCap = rowsCap < kMfmaMaxRows ? rowsCap : kMfmaMaxRows;
-    // the inverses, when be_prepare_solve started them on the side stream
-    hipEvent_t inv = nullptr;
+    const uint32_t prodCap = rowsCap < kProductMaxRows ? rowsCap : kProductMaxRows;
     if (tr) {
-        std::lock_guard<std::mutex> g(g_invMu);
-        if (!g_invPending.empty()) {
-            inv = g_invPending.front();
-            g_invPending.pop_front();
-        }
-    }
-    if (tr || mfma)
-        hipLaunchKernelGGL(k_solve_pre, dim3(inv ? solveCount : 2 * solveCount), dim3(kMfmaThreads),
-                           (size_t)solve_pre_lds_bytes(rowsCap), g_stream, solves + solveBegin, rows, coef, results,
-                           acctL, solveCount, inv ? 2u : 0u);
-    if (inv) {
-        check(hipStreamWaitEvent(g_stream, inv, 0), "hipStreamWaitEvent(inverses)");
-        std::lock_guard<std::mutex> g(g_invMu);
-        g_invFree.push_back(inv);
-    }
-    if (tr)
-        hipLaunchKernelGGL(k_solve_tr, dim3(count * kTrSplit), dim3(kTrThreads), (size_t)solve_tr_lds_bytes(prodCap), g_stream,
-                           solves, rows, results, items);
-    else if (mfma)
-        hipLaunchKernelGGL(k_solve_mfma, dim3(solveCount * kMfmaGroups), dim3(kMfmaThreads),
-                           (size_t)solve_mfma_lds_bytes(prodCap), g_stream, solves + solveBegin, rows, results);
-    else if (separate)
+        hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kPreThreads), (size_t)solve_pre_lds_bytes(rowsCap),
+                           g_stream, solves + solveBegin, rows, coef, results, acctL, solveCount, 0u);
+        hipLaunchKernelGGL(k_solve_tr, dim3(count * kTrSplit), dim3(kTrThreads), (size_t)solve_tr_lds_bytes(prodCap),
+                           g_stream, solves, rows, results, items);
+    } else if (separate) {
         hipLaunchKernelGGL(k_solve_prefix, dim3(solveCount), dim3(64), (size_t)solve_prefix_lds_bytes(rowsCap),
                            g_stream, solves + solveBegin, rows, coef, results, acctL);
+    }
     hipLaunchKernelGGL(k_solve_main, dim3(count), dim3(64 * kSolveWaves),
                        (size_t)solve_launch_lds_bytes(rowsCap, !separate), g_stream, solves, rows, coef, results,
-                       items, acctL, (separate ? 1u : 0u) | (mfma ? 2u : 0u) | (tr ? 4u : 0u));
+                       items, acctL, (separate ? 1u : 0u) | (tr ? 4u : 0u));
 }
 
 } // namespace
@@ -3917,72 +3657,18 @@ namespace {
 // Default: the solves whose lengths all come out valid as X = T R on the
 // vector ALUs (k_solve_pre 80 + k_solve_tr 103 + k_solve_main 9 us per
 // headline launch against k_solve_prefix 58 + k_solve_main 277 for the
-// sweeps; profiles/r4ac_*).  SGPU_TR_SOLVE=0: the sweeps alone.
-// SGPU_MFMA_SOLVE=1: the product on the int8 matrix cores (slower: 80 +
-// 322 us; profiles/r4l_*).
+// sweeps; profiles/r4ac_*).  SGPU_TR_SOLVE=0: the sweeps alone (a test knob:
+// test_product_solve_paths runs the hashed fixtures through them).
 SolvePath solve_path()
 {
     static const SolvePath kPath = [] {
-        const char* m = std::getenv("SGPU_MFMA_SOLVE");
-        if (m && std::atoi(m) != 0)
-            return kPathMfma;
         const char* v = std::getenv("SGPU_TR_SOLVE");
         return (!v || std::atoi(v) != 0) ? kPathVector : kPathSweeps;
     }();
     return kPath;
 }
 
-// SGPU_INV_SIDE=1: the inverses on a side stream during the exec launches
-// instead of in k_solve_pre beside the prefix passes.  Off: the solve phase
-// gets 25 us shorter but k_exec, sharing the CUs, 18 us longer per launch,
-// and device time per step rises (2.40-2.42 vs 2.34-2.36 ms,
-// profiles/r4ai_side_ab.txt)
-bool inverses_aside()
-{
-    static const bool on = [] {
-        const char* v = std::getenv("SGPU_INV_SIDE");
-        return v && std::atoi(v) != 0;
-    }();
-    return on;
-}
-
-hipEvent_t take_event()
-{
-    {
-        std::lock_guard<std::mutex> g(g_invMu);
-        if (!g_invFree.empty()) {
-            hipEvent_t e = g_invFree.back();
-            g_invFree.pop_back();
-            return e;
-        }
-    }
-    hipEvent_t e = nullptr;
-    check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate(inverses)");
-    return e;
-}
-
 } // namespace
-
-void be_prepare_solve(const SolveDesc* solves, const uint8_t* coef, uint32_t maxRows, uint32_t solveBegin,
-                      uint32_t solveCount)
-{
-    if (solveCount < kSolvePrefixSplit || solve_path() != kPathVector || !inverses_aside())
-        return;
-    bind_device();
-    const uint32_t rowsCap = maxRows < kSolveLdsMaxRows ? maxRows : kSolveLdsMaxRows;
-    // T reads only the coefficients: it runs on the side stream once the
-    // codec stream has the upload (and the scratch ring zeroed), beside the
-    // submission's exec launches; the solve phase waits for it
-    hipEvent_t start = take_event(), done = take_event();
-    check(hipEventRecord(start, g_stream), "hipEventRecord(inverses)");
-    check(hipStreamWaitEvent(g_invStream, start, 0), "hipStreamWaitEvent(inverses)");
-    hipLaunchKernelGGL(k_solve_pre, dim3(solveCount), dim3(kMfmaThreads), (size_t)solve_pre_lds_bytes(rowsCap),
-                       g_invStream, solves + solveBegin, nullptr, coef, nullptr, nullptr, solveCount, 1u);
-    check(hipEventRecord(done, g_invStream), "hipEventRecord(inverses)");
-    std::lock_guard<std::mutex> g(g_invMu);
-    g_invFree.push_back(start);
-    g_invPending.push_back(done);
-}
 
 void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
                      const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
@@ -4029,7 +3715,7 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
         Sys& y = sys[s];
         // (every row count the product solves take: 16..120, so every
         // rows-per-wave variant of k_solve_tr runs)
-        y.m = 16 + rnd() % (kMfmaMaxRows - 15);
+        y.m = 16 + rnd() % (kProductMaxRows - 15);
         static const uint32_t kLens[6] = {1402, 600, 1100, 2000, 4100, 6000};
         y.maxB = kLens[rnd() % 6];
         y.rowBase = rows;
@@ -4143,10 +3829,10 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
              hipMemcpy(dRowD, rdesc.data(), rows * sizeof(SolveRow), hipMemcpyHostToDevice) == hipSuccess &&
              hipMemcpy(dItems, items.data(), items.size() * sizeof(SolveItem), hipMemcpyHostToDevice) == hipSuccess;
     }
-    std::vector<uint8_t> outRows[3];
-    std::vector<uint32_t> outRes[3];
-    const SolvePath paths[3] = {kPathSweeps, kPathVector, kPathMfma};
-    for (int k = 0; k < 3 && ok; ++k) {
+    std::vector<uint8_t> outRows[2];
+    std::vector<uint32_t> outRes[2];
+    const SolvePath paths[2] = {kPathSweeps, kPathVector};
+    for (int k = 0; k < 2 && ok; ++k) {
         ok = hipMemcpy(dRows, hostRows.data(), hostRows.size(), hipMemcpyHostToDevice) == hipSuccess &&
              hipMemset(dRes, 0xff, (size_t)resWords * 4) == hipSuccess &&
              hipMemset(dScratch, 0xa5, scratch + 256) == hipSuccess &&
@@ -4172,8 +3858,8 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
     (void)hipFree(dAcct);
     if (!ok)
         return -1;
-    uint32_t diff[2] = {0, 0}, flagged[2] = {0, 0};
-    for (int k = 1; k < 3; ++k) {
+    uint32_t diff[2] = {0, 0}, flagged[2] = {0, 0};   // [1]: a second product path (none since round 5)
+    for (int k = 1; k < 2; ++k) {
         for (size_t b = 0; b < hostRows.size(); ++b)
             diff[k - 1] += outRows[k][b] != outRows[0][b];
         for (uint32_t s = 0; s < nsolves; ++s) {
@@ -4192,31 +3878,10 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
     return (diff[0] || diff[1]) ? 1 : 0;
 }
 
-// H2D staging as a kernel reading mapped pinned memory over the bus (on the
-// staging stream), so the copy engines are left to the gathers' D2H copies:
-// SGPU_H2D_KERNEL=1 (measured in the end-to-end leg)
-__global__ __launch_bounds__(256) void k_h2d(uint4* __restrict__ dst, const uint4* __restrict__ src, uint64_t words)
-{
-    const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    for (; i + 3 * stride < words; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
-    }
-    for (; i < words; i += stride)
-        dst[i] = src[i];
-}
 
 void* be_stage_h2d(void* dst, const void* src, size_t bytes)
 {
     bind_device();
-    static const bool kKernelH2D = [] {
-        const char* v = std::getenv("SGPU_H2D_KERNEL");
-        return v && std::atoi(v) != 0;
-    }();
     hipEvent_t e = nullptr;
     {
         std::lock_guard<std::mutex> g(g_evMu);
@@ -4227,20 +3892,10 @@ void* be_stage_h2d(void* dst, const void* src, size_t bytes)
     }
     if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
         return nullptr;
-    void* mapped = nullptr;
-    const size_t head = bytes & ~(size_t)15;
-    if (kKernelH2D && head && (((uintptr_t)dst | (uintptr_t)src) & 15u) == 0 &&
-        hipHostGetDevicePointer(&mapped, const_cast<void*>(src), 0) == hipSuccess && mapped) {
-        const uint64_t words = head / 16;
-        const unsigned blocks = (unsigned)std::min<uint64_t>(2048, (words + 1023) / 1024);
-        hipLaunchKernelGGL(k_h2d, dim3(std::max(1u, blocks)), dim3(256), 0, g_stageStream, static_cast<uint4*>(dst),
-                           static_cast<const uint4*>(mapped), words);
-        if (bytes > head && hipMemcpyAsync(static_cast<uint8_t*>(dst) + head, static_cast<const uint8_t*>(src) + head,
-                                           bytes - head, hipMemcpyHostToDevice, g_stageStream) != hipSuccess)
-            return nullptr;
-    } else if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g_stageStream) != hipSuccess) {
+    // (a copy-engine copy: staging it by a kernel reading mapped pinned
+    // memory slowed the codec kernels beside it)
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, g_stageStream) != hipSuccess)
         return nullptr;
-    }
     if (hipEventRecord(e, g_stageStream) != hipSuccess)
         return nullptr;
     return e;
@@ -4389,12 +4044,7 @@ bool be_fence_wait(void* fence, unsigned spinUs)
 
 void be_timing_enable(bool on)
 {
-    // SGPU_TIMING=0: no per-launch events at all (A/B of their cost)
-    static const bool allowed = [] {
-        const char* v = std::getenv("SGPU_TIMING");
-        return !v || std::atoi(v) != 0;
-    }();
-    g_timing = on && allowed;
+    g_timing = on;
 }
 double be_timing_kernel_ms(BeKernel kind)
 {

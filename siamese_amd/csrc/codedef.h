@@ -133,15 +133,6 @@ struct FastMod
 /// The pointer stays valid until the calling thread's next ldpc_offsets().
 const uint32_t* ldpc_offsets(unsigned row, unsigned n, unsigned* count);
 
-/// The same picks as column hits, for rows of at most 64 columns: pick k
-/// lands on col[k] = pc[offset k]; the ones with col - lo < span toggle bit
-/// col of *hit1 (even k) or *hitRx (odd k), so a row byte j takes
-/// (hit1 bit j) ^ RX * (hitRx bit j) (XOR-ing a value twice cancels).
-/// Drawn eight at a time (PCG jump-ahead, AVX-512) when
-/// SIAMESE_AMD_VECTOR_PICKS=1 and the host has it; returns false otherwise
-/// (the caller walks ldpc_offsets instead).
-bool ldpc_pick_hits(unsigned row, unsigned n, const uint32_t* pc, uint32_t lo, uint32_t span, uint64_t* hit1,
-                    uint64_t* hitRx);
 
 // ---- Metadata carried in every recovery footer (SiameseCommon.h:364-389) --
 struct RowMeta

@@ -1588,8 +1588,7 @@ bool DecoderCore::generate_matrix()
         uint64_t hit1 = 0, hitRx = 0;
         unsigned picks = 0;
         const uint32_t* off = nullptr;
-        if (columns <= 64 && (ldpc_pick_hits(m.row, m.ldpcCount, pc, startCol, span, &hit1, &hitRx) ||
-                              (off = ldpc_offsets(m.row, m.ldpcCount, &picks)) != nullptr)) {
+        if (columns <= 64 && (off = ldpc_offsets(m.row, m.ldpcCount, &picks)) != nullptr) {
             // XOR-ing 1 (even picks) or RX (odd picks) into a byte any number
             // of times is the parity of its hits: a bit per column each, in
             // registers (no byte read-modify-write chains through memory)

@@ -687,17 +687,13 @@ void Program::rows_update(unsigned k, uint64_t dst, uint32_t n, uint32_t valid, 
     // byte they saw), so each row can take back what was folded in after it
     // (RowItem.cutoff).  A restarted or moved sum starts a new batch, whose
     // rows run after this batch's rows.
-    static const bool versioned = [] {
-        const char* v = std::getenv("SIAMESE_AMD_ROW_VERSIONS");   // 0: a batch per sum re-read (A/B aid)
-        return !v || std::atoi(v) != 0;
-    }();
     // Rows that read the sum before the update take its elements back out
     // (ops.h RowItem), so only short extensions join (a streaming encoder's
     // few new originals per row; not a decoder row whose range ends far past
     // the previous row's), into a batch of fewer than kVersionRows rows.
     if (b.readMask >> k & 1) {
         const WinEntry& seen = b.sums[k];
-        if (!versioned || seen.src != dst || valid < seen.len || toElement - fromElement > kVersionMaxSpan ||
+        if (seen.src != dst || valid < seen.len || toElement - fromElement > kVersionMaxSpan ||
             b.rows.size() >= kVersionRows)
             rows_open(b.base, true);
         else
@@ -1054,20 +1050,10 @@ DevBuf Engine::alloc(uint32_t bytes)
     return b;
 }
 
-bool slabs_enabled()
-{
-    static const bool v = [] {
-        const char* e = std::getenv("SIAMESE_AMD_SLABS");
-        return !e || std::atoi(e) != 0;
-    }();
-    return v;
-}
 
 DevBuf Engine::slab_slot(Slab& sl, unsigned bit, uint32_t need, bool* failed)
 {
     *failed = false;
-    if (!slabs_enabled())
-        return DevBuf();
     if (!sl.buf) {
         // slots of one MTU-sized class at least: a subwindow of small and
         // mixed-size datagrams still shares one slab
@@ -1584,43 +1570,20 @@ Batch* Engine::take_batch()
     return b;
 }
 
-namespace {
-bool async_assembly()
-{
-    static const bool v = [] {
-        const char* e = std::getenv("SIAMESE_AMD_ASYNC_ASSEMBLY");
-        return !e || std::atoi(e) != 0;
-    }();
-    return v;
-}
-} // namespace
 
 uint64_t Engine::enqueue()
 {
     if (failed())
         return 0;
     std::lock_guard<std::mutex> sub(submitMu_);
-    const uint64_t tq0 = now_ns();
     Batch* b = take_batch();
     if (!b)
         return nextTicket_;   // nothing queued: the latest submission covers everything
     const uint64_t ticket = b->ticket;
-    const uint64_t tq1 = now_ns();
     // The batch is laid out by the launcher thread and its own pool, so the
     // caller goes back to driving instances at once (same-box A/B of the
-    // headline, 5 interleaved runs each: median 6.34 vs 6.63 ms/step,
-    // profiles/r4i_async_ab.txt).  SIAMESE_AMD_ASYNC_ASSEMBLY=0 lays it out
-    // here, on the caller's thread and the shared pool.
-    if (!async_assembly()) {
-        claim_set(*b);
-        const uint64_t tq2 = now_ns();
-        assemble_batch(*b, pool());
-        tl("assembled", ticket);
-        static const bool asmStats = std::getenv("SGPU_ASM_STATS") != nullptr;
-        if (asmStats)
-            std::fprintf(stderr, "enq %zu: take %.3f claim %.3f assemble %.3f ms\n", (size_t)ticket,
-                         (tq1 - tq0) / 1e6, (tq2 - tq1) / 1e6, (now_ns() - tq2) / 1e6);
-    }
+    // headline, 5 interleaved runs each: median 6.34 vs 6.63 ms/step against
+    // laying it out here, profiles/r4i_async_ab.txt).
     {
         std::lock_guard<std::mutex> g(qMu_);
         toLaunch_.push_back(b);   // (b belongs to the pipeline from here on)
@@ -1630,23 +1593,9 @@ uint64_t Engine::enqueue()
     return ticket;
 }
 
-namespace {
-// SIAMESE_AMD_HANDOFF_SPIN_US: how long the launcher spins for the next batch,
-// and a waiting caller for its ticket, before blocking.  Off by default: a
-// same-box A/B of 100 us showed no gain on C3 or the headline.
-const uint64_t kHandoffSpinNs = [] {
-    const char* v = std::getenv("SIAMESE_AMD_HANDOFF_SPIN_US");
-    return (uint64_t)(v ? std::atol(v) : 0) * 1000u;
-}();
-} // namespace
 
 bool Engine::wait(uint64_t ticket)
 {
-    if (kHandoffSpinNs && doneSeen_.load(std::memory_order_acquire) < ticket) {
-        const uint64_t until = now_ns() + kHandoffSpinNs;
-        while (doneSeen_.load(std::memory_order_acquire) < ticket && !failed() && now_ns() < until)
-            __builtin_ia32_pause();
-    }
     std::unique_lock<std::mutex> lk(qMu_);
     doneCv_.wait(lk, [&] { return stop_ || doneTicket_ >= ticket; });
     return !failed();
@@ -1672,17 +1621,12 @@ bool Engine::flush_and_sync(std::shared_mutex* detach)
         return wait(last) && last != 0;
     }
     const uint64_t ticket = b->ticket;
-    // SIAMESE_AMD_INLINE_SYNC=0 always hands the submission to the threads
-    static const bool kInline = [] {
-        const char* v = std::getenv("SIAMESE_AMD_INLINE_SYNC");
-        return !v || std::atoi(v) != 0;
-    }();
     bool inl = false;
     // (whether or not submissions are laid out by the launcher thread: with
     // nothing queued or running the caller lays out and launches its own,
     // and the launcher takes nothing while inlineBusy_ is set; the hand-off
     // costs the drop-in path ~15 us per flush, profiles/r4ao_dropin_ab.txt)
-    if (kInline) {
+    {
         std::lock_guard<std::mutex> g(qMu_);
         // Inline only when the ticket's transfer set is free right now, and
         // claimed in this same critical section: a later ticket of the same
@@ -1696,10 +1640,6 @@ bool Engine::flush_and_sync(std::shared_mutex* detach)
         }
     }
     if (!inl) {
-        if (!async_assembly()) {
-            claim_set(*b);
-            assemble_batch(*b, pool());
-        }
         {
             std::lock_guard<std::mutex> g(qMu_);
             toLaunch_.push_back(b);
@@ -1748,11 +1688,6 @@ void Engine::launcher_loop()
     uint64_t taken = 0;   // batches taken from toLaunch_
     for (;;) {
         Batch* b = nullptr;
-        if (kHandoffSpinNs && queuedSeen_.load(std::memory_order_acquire) == taken) {
-            const uint64_t until = now_ns() + kHandoffSpinNs;
-            while (queuedSeen_.load(std::memory_order_acquire) == taken && now_ns() < until)
-                __builtin_ia32_pause();
-        }
         {
             std::unique_lock<std::mutex> lk(qMu_);
             launchCv_.wait(lk, [&] { return stop_ || (!toLaunch_.empty() && !inlineBusy_); });
@@ -1843,7 +1778,6 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         }
     });
 
-    const uint64_t tSeal = now_ns();
     // ---- 2. layout -----------------------------------------------------------
     uint32_t resultWords = 0;
     for (int g = 0; g < 2; ++g)
@@ -2044,47 +1978,13 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     bt.oGeIn = off;
     off = align16(off + geInBytes);
     bt.upBytes = off;
-    // SGPU_UPLOAD_STATS=1: one stderr line per flush, upload bytes by part (profiling aid)
-    static const bool upStats = std::getenv("SGPU_UPLOAD_STATS") != nullptr;
-    if (upStats) {
-        std::fprintf(stderr, "upload %zu: stage %zu ingest %zu stream %zu items %zu solves %zu wide %zu\n",
-                     bt.upBytes, bt.oIngD - oStage, bt.oStream - bt.oIngD, bt.oItems - bt.oStream,
-                     bt.oSD - bt.oItems, bt.oWide - bt.oSD, bt.upBytes - bt.oWide);
-        // per phase: kind, work items, ops by kind (exec) or solve sizes
-        for (const Phase& ph : phases) {
-            if (ph.kind == Phase::EXEC) {
-                size_t k[6] = {0, 0, 0, 0, 0, 0}, rows = 0, upd = 0, win = 0;
-                for (const SegRef& r : segs) {
-                    if (r.itemBase < ph.itemBegin || r.itemBase >= ph.itemBegin + ph.itemCount)
-                        continue;
-                    for (const GfOp& op : r.seg->ops) {
-                        k[op.kind < 6 ? op.kind : 0]++;
-                        if (op.kind == OP_ROWS) {
-                            rows += op.n;
-                            upd += op.mix;
-                            win += op.valid;
-                        }
-                    }
-                }
-                std::fprintf(stderr, "  exec items %zu wide %zu: lincomb %zu literal %zu rows %zu(r%zu u%zu w%zu) "
-                             "copies %zu lcs %zu\n", ph.itemCount, ph.wideCount, k[OP_LINCOMB], k[OP_LITERAL],
-                             k[OP_ROWS], rows, upd, win, k[OP_COPIES], k[OP_LINCOMBS]);
-            } else {
-                std::fprintf(stderr, "  solve items %zu solves %zu maxm %u\n", ph.itemCount, ph.solveCount,
-                             ph.maxRows);
-            }
-        }
-    }
     if (bt.upBytes)
         ensure_up(xs, bt.upBytes);
     // A small upload is not copied: the kernels read it from the pinned
     // buffer over the bus (zero-copy), which skips a copy and its hand-off
     // on the latency-bound paths (SIAMESE_AMD_ZEROCOPY_UP bytes at most,
     // default 32 KiB; 0 disables).
-    static const size_t kZeroCopyUp = [] {
-        const char* v = std::getenv("SIAMESE_AMD_ZEROCOPY_UP");
-        return v ? (size_t)std::atol(v) : (size_t)32768;
-    }();
+    constexpr size_t kZeroCopyUp = 32768;
     bt.upBase = (xs.upHostDev && bt.upBytes <= kZeroCopyUp) ? xs.upHostDev : xs.upDev;
     if (wideBytes + tBytes) {
         // k_ldpc scratch comes from the set's ring, which is zeroed as a whole
@@ -2107,7 +2007,6 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
             }
     }
 
-    const uint64_t tLayout = now_ns();
     // ---- 3. copy into the pinned upload buffer -------------------------------
     uint8_t* up = xs.upHost;
     const uint64_t stageDev = (uint64_t)(uintptr_t)(bt.upBase + oStage);
@@ -2254,12 +2153,6 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     st.uploadBytes = bt.upBytes;
     st.execUniqueBytes = uniqueBytes.load(std::memory_order_relaxed);
     st.assembleNs = now_ns() - t0;
-    // SGPU_ASM_STATS=1: one stderr line per flush, assembly time by stage (profiling aid)
-    static const bool asmStats = std::getenv("SGPU_ASM_STATS") != nullptr;
-    if (asmStats)
-        std::fprintf(stderr, "asm %zu bodies %zu up %zu: seal %.3f layout %.3f copy %.3f ms (%s)\n", (size_t)bt.ticket,
-                     totalBodies, bt.upBytes, (tSeal - t0) / 1e6, (tLayout - tSeal) / 1e6,
-                     (now_ns() - tLayout) / 1e6, parallel ? "parallel" : "serial");
 }
 
 void Engine::launch_batch(Batch& bt)
@@ -2287,11 +2180,6 @@ void Engine::launch_batch(Batch& bt)
     }
     if (bt.wideZero)
         be_memset(xs.wideDev, 0, xs.wideCap);
-    // (work of the solve phases that needs only the upload may start now)
-    for (const Phase& ph : bt.phases)
-        if (ph.kind != Phase::EXEC)
-            be_prepare_solve((const SolveDesc*)(bt.upBase + bt.oSD), bt.upBase + bt.oCoef, ph.maxRows,
-                             (uint32_t)ph.solveBegin, (uint32_t)ph.solveCount);
     if (bt.nGe)
         be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev);
     // k_ldpc items of every exec phase before the first solve go in one

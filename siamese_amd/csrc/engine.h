@@ -63,8 +63,6 @@ struct Slab
     uint32_t stride = 0;
     uint64_t used = 0;   // slots written since the slab was taken
 };
-/// SIAMESE_AMD_SLABS=0 gives every symbol its own buffer (A/B aid).
-bool slabs_enabled();
 
 class Engine;
 struct Shard;

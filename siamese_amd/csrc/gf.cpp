@@ -68,7 +68,7 @@ bool gf_init()
     if (__builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vl"))
         gf_count_nonzero = count_nonzero_avx512;
     if (__builtin_cpu_supports("gfni") && __builtin_cpu_supports("avx512bw") &&
-        __builtin_cpu_supports("avx512vl") && !std::getenv("SIAMESE_AMD_NO_GFNI")) {
+        __builtin_cpu_supports("avx512vl")) {
         gf_muladd_fast = gf_muladd_gfni;
         // the instruction against the tables, every y on every x
         alignas(64) uint8_t x[256], d[256];

@@ -279,21 +279,21 @@ struct SolveDesc
                          // rows keep their inputs for the exact sweeps)
 };
 
-/// Solves of up to this many rows may run on the matrix cores (their
+/// Solves of up to this many rows may run as the product X = T R (their
 /// inverse T = U^-1 L^-1 in scratch, rows of kTStride bytes), in launches of
 /// at least kSolvePrefixSplit solves (the prefix pass is then its own launch).
-constexpr unsigned kMfmaMaxRows = 120;
+constexpr unsigned kProductMaxRows = 120;
 constexpr unsigned kSolvePrefixSplit = 16;
 constexpr uint32_t kTStride = 128;
 constexpr uint32_t solve_t_bytes(uint32_t m)
 {
-    return m <= kMfmaMaxRows ? ((m + 3u) & ~3u) * kTStride : 0u;
+    return m <= kProductMaxRows ? ((m + 3u) & ~3u) * kTStride : 0u;
 }
-/// Row stride of the matrix-core path's result scratch (64-column chunks).
+/// Row stride of the product solves' result scratch (64-byte chunks).
 constexpr uint32_t solve_x_stride(uint32_t maxBytes) { return (maxBytes + 63u) & ~63u; }
 constexpr uint64_t solve_x_bytes(uint32_t m, uint32_t maxBytes)
 {
-    return m <= kMfmaMaxRows ? (uint64_t)m * solve_x_stride(maxBytes) : 0u;
+    return m <= kProductMaxRows ? (uint64_t)m * solve_x_stride(maxBytes) : 0u;
 }
 
 struct SolveRow

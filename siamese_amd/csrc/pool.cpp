@@ -9,30 +9,12 @@
 
 namespace sgpu {
 
-namespace {
-// pause iterations a worker (or a joining caller) spins before blocking
-// (SIAMESE_AMD_POOL_SPIN).  Off by default: on the MI355X box's host share,
-// spinning workers slowed the codec stepping they share the cores with
-// (A/B); it helps on hosts with idle cores.
-const unsigned kSpin = [] {
-    const char* v = std::getenv("SIAMESE_AMD_POOL_SPIN");
-    return v ? (unsigned)std::atoi(v) : 0u;
-}();
-inline void cpu_relax()
-{
-#if defined(__x86_64__)
-    __builtin_ia32_pause();
-#endif
-}
-} // namespace
 
 int WorkerPool::shared_nice()
 {
-    static const int n = [] {
-        const char* v = std::getenv("SIAMESE_AMD_WORKER_NICE");
-        return v ? std::atoi(v) : 10;
-    }();
-    return n;
+    // the shared pool's workers yield to the launcher and completer threads
+    // (0 measured no different on the box, profiles/r5a ab runs)
+    return 10;
 }
 
 unsigned WorkerPool::default_threads()
@@ -81,13 +63,6 @@ void WorkerPool::loop()
 {
     uint64_t seen = 0;
     for (;;) {
-        // Fork-joins come in quick succession (one per job round and per
-        // assembly pass): optionally spin a short while for the next one
-        // before sleeping, so a worker joins it without a futex wake-up.
-        for (unsigned k = 0; k < kSpin && gen_.load(std::memory_order_acquire) == seen &&
-                             !stop_.load(std::memory_order_relaxed);
-             ++k)
-            cpu_relax();
         {
             std::unique_lock<std::mutex> lk(mu_);
             if (gen_.load(std::memory_order_relaxed) == seen && !stop_.load(std::memory_order_relaxed)) {
@@ -133,8 +108,8 @@ void WorkerPool::run(size_t count, const std::function<void(size_t)>& fn)
         cv_.notify_all();
     drain();
     // every index has been claimed; wait for the workers still finishing one
-    for (unsigned k = 0; k < kSpin && busy_.load(std::memory_order_acquire) != 0; ++k)
-        cpu_relax();
+    // (a spinning wait measured slower on the box's 16-core share: the
+    // spinners take cycles from the stepping threads)
     std::unique_lock<std::mutex> lk(mu_);
     doneCv_.wait(lk, [&] { return busy_.load(std::memory_order_acquire) == 0; });
     fn_ = nullptr;

@@ -129,7 +129,6 @@ double be_timing_kernel_ms(BeKernel) { return 0; }
 double be_timing_exec_ms() { return 0; }
 double be_timing_total_ms() { return 0; }
 
-void be_prepare_solve(const SolveDesc*, const uint8_t*, uint32_t, uint32_t, uint32_t) {}
 
 void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* coef, uint32_t* results,
                      const SolveItem* items, uint32_t count, uint32_t maxRows, uint64_t* acct,
