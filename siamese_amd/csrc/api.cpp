@@ -50,7 +50,7 @@ using Lock = std::lock_guard<std::mutex>;
 // an instance call (shared: other instances' calls run beside it)
 struct Shared
 {
-    std::shared_lock<std::shared_mutex> l;
+    std::shared_lock<InstanceLock> l;
     Shared() : l(Engine::global()->instance_lock()) {}
 };
 

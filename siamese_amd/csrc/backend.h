@@ -42,6 +42,11 @@ struct BeCopy
 };
 constexpr unsigned kBeCopyMax = 8;   // ranges per be_copy_pinned call
 void be_copy_pinned(const BeCopy* ranges, unsigned count, bool toDevice);
+/// The same ranges with a device-readable copy of the list (devList: each
+/// range's host side as the device addresses it, be_host_device_ptr), so
+/// that any number of small ranges takes one kernel launch; null devList, or
+/// ranges too large for a kernel, fall back to be_copy_pinned.
+void be_copy_list(const BeCopy* ranges, const void* devList, unsigned count, bool toDevice);
 
 /// One wave per (descriptor, kIngestChunkBytes chunk): maxBytes is the
 /// largest hdrLen + bytes among the descriptors (sizes the grid).

@@ -3511,9 +3511,8 @@ struct HostCopyArgs
 // Pinned host <-> device copies as a kernel (be_copy_pinned): blockIdx.y is
 // the range, each thread moves 16-byte words (bytes at the unaligned ends);
 // host memory is page-locked and mapped, written with ordinary stores.
-__global__ __launch_bounds__(kHostCopyThreads) void k_hostcopy(HostCopyArgs a)
+__device__ __forceinline__ void copy_range(const BeCopy& c)
 {
-    const BeCopy& c = a.r[blockIdx.y];
     uint8_t* dst = reinterpret_cast<uint8_t*>(c.dst);
     const uint8_t* src = reinterpret_cast<const uint8_t*>(c.src);
     const uint64_t n = c.bytes;
@@ -3525,6 +3524,14 @@ __global__ __launch_bounds__(kHostCopyThreads) void k_hostcopy(HostCopyArgs a)
     for (uint64_t i = words * 16 + (uint64_t)blockIdx.x * kHostCopyThreads + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * kHostCopyThreads)
         dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(kHostCopyThreads) void k_hostcopy(HostCopyArgs a) { copy_range(a.r[blockIdx.y]); }
+
+// The same from a device-readable range list (be_copy_list).
+__global__ __launch_bounds__(kHostCopyThreads) void k_copylist(const BeCopy* __restrict__ list)
+{
+    copy_range(list[blockIdx.y]);
 }
 
 void be_copy_pinned(const BeCopy* ranges, unsigned count, bool toDevice)
@@ -3560,6 +3567,24 @@ void be_copy_pinned(const BeCopy* ranges, unsigned count, bool toDevice)
     const uint64_t perBlock = (uint64_t)kHostCopyThreads * 16u * 4u;   // four words per thread
     const unsigned blocks = (unsigned)std::min<uint64_t>(64, (most + perBlock - 1) / perBlock);
     hipLaunchKernelGGL(k_hostcopy, dim3(std::max(1u, blocks), count), dim3(kHostCopyThreads), 0, g_stream, a);
+}
+
+void be_copy_list(const BeCopy* ranges, const void* devList, unsigned count, bool toDevice)
+{
+    uint64_t total = 0, most = 0;
+    for (unsigned i = 0; i < count; ++i) {
+        total += ranges[i].bytes;
+        most = std::max<uint64_t>(most, ranges[i].bytes);
+    }
+    if (count <= kBeCopyMax || !devList || total > kKernelCopyMax || count > 65535u) {
+        be_copy_pinned(ranges, count, toDevice);
+        return;
+    }
+    bind_device();
+    const uint64_t perBlock = (uint64_t)kHostCopyThreads * 16u * 4u;   // four words per thread
+    const unsigned blocks = (unsigned)std::min<uint64_t>(64, (most + perBlock - 1) / perBlock);
+    hipLaunchKernelGGL(k_copylist, dim3(std::max(1u, blocks), count), dim3(kHostCopyThreads), 0, g_stream,
+                       static_cast<const BeCopy*>(devList));
 }
 
 void be_memset(void* dst, int value, size_t bytes)

@@ -1283,6 +1283,7 @@ void Engine::ensure_down(XferSet& x, size_t bytes)
         be_dev_free(x.downDev);
     x.downHost = (uint8_t*)be_host_alloc_mapped(cap);
     x.downDev = (uint8_t*)be_dev_alloc(cap);
+    x.downHostDev = x.downHost ? (uint8_t*)be_host_device_ptr(x.downHost) : nullptr;
     x.downCap = cap;
     x.acctZero = true;
     x.acctPrev[0] = x.acctPrev[1] = x.acctPrev[2] = x.acctPrev[3] = 0;
@@ -1335,6 +1336,7 @@ struct Batch
     uint32_t maxIngest = 0;
     size_t oIngD = 0, oIngB = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
     size_t oGeD = 0, oGeIn = 0, nGe = 0;   // device matrix jobs: descs, inputs
+    size_t oCopy = 0;                      // the download copy list (BeCopy records)
     uint64_t wideBase = 0;                 // this submission's k_ldpc scratch: bytes into the ring
     bool wideZero = false;                 // the ring wrapped: zero it before the first exec launch
     uint32_t resultWords = 0;
@@ -1590,6 +1592,7 @@ uint64_t Engine::enqueue()
         queuedSeen_.fetch_add(1, std::memory_order_release);
     }
     launchCv_.notify_one();
+    setCv_.notify_all();   // (a launcher waiting for a set to take requests re-checks toLaunch_)
     return ticket;
 }
 
@@ -1601,20 +1604,17 @@ bool Engine::wait(uint64_t ticket)
     return !failed();
 }
 
-bool Engine::flush_and_sync(std::shared_mutex* detach)
+bool Engine::flush_and_sync(InstanceLock* detach)
 {
     if (failed())
         return false;
     std::unique_lock<std::mutex> sub(submitMu_);
+    if (detach)
+        return flush_requested(sub, *detach);
     Batch* b;
     uint64_t last;
-    {
-        std::unique_lock<std::shared_mutex> w;
-        if (detach)
-            w = std::unique_lock<std::shared_mutex>(*detach);
-        b = take_batch();
-        last = nextTicket_;
-    }
+    b = take_batch();
+    last = nextTicket_;
     if (!b) {
         // (an earlier submission took this caller's work: wait for it)
         sub.unlock();
@@ -1622,10 +1622,10 @@ bool Engine::flush_and_sync(std::shared_mutex* detach)
     }
     const uint64_t ticket = b->ticket;
     bool inl = false;
-    // (whether or not submissions are laid out by the launcher thread: with
-    // nothing queued or running the caller lays out and launches its own,
-    // and the launcher takes nothing while inlineBusy_ is set; the hand-off
-    // costs the drop-in path ~15 us per flush, profiles/r4ao_dropin_ab.txt)
+    // (with nothing queued or running the caller lays out and launches its
+    // own submission, and the launcher takes nothing while inlineBusy_ is
+    // set; the hand-off costs a per-call flush ~15 us,
+    // profiles/r4ao_dropin_ab.txt)
     {
         std::lock_guard<std::mutex> g(qMu_);
         // Inline only when the ticket's transfer set is free right now, and
@@ -1633,7 +1633,7 @@ bool Engine::flush_and_sync(std::shared_mutex* detach)
         // set (T + kSets) could otherwise claim it first and then wait in
         // toLaunch_ behind inlineBusy_ while this caller waits for the set.
         if (toLaunch_.empty() && toComplete_.empty() && !launching_ && !completing_ && !inlineBusy_ &&
-            doneTicket_ + 1 == ticket && sets_[b->set].busyTicket == 0) {
+            flushReq_ == takenReq_ && doneTicket_ + 1 == ticket && sets_[b->set].busyTicket == 0) {
             sets_[b->set].busyTicket = ticket;
             inlineBusy_ = true;   // (the launcher waits: its stream order stays ticket order)
             inl = true;
@@ -1647,13 +1647,83 @@ bool Engine::flush_and_sync(std::shared_mutex* detach)
         }
         sub.unlock();
         launchCv_.notify_one();
+        setCv_.notify_all();   // (a launcher waiting for a set to take requests re-checks toLaunch_)
         return wait(ticket) && !failed();
     }
-    tl("inline", ticket);
-    assemble_batch(*b, pool());   // (the set was claimed above)
+    return run_inline(b, sub);
+}
+
+bool Engine::flush_requested(std::unique_lock<std::mutex>& sub, InstanceLock& detach)
+{
+    // The drop-in API's flush.  An idle pipeline: the caller detaches, lays
+    // out and launches the submission itself (one stream's per-call
+    // latency).  Otherwise the caller files a request and the launcher
+    // detaches the queued work once the next ticket's transfer set is free,
+    // so every call the other application threads queued meanwhile rides in
+    // the same submission: concurrent callers share few large submissions
+    // instead of paying one submission each behind the transfer sets.
+    bool idle;
+    {
+        std::lock_guard<std::mutex> g(qMu_);
+        const uint64_t next = nextTicket_.load(std::memory_order_relaxed) + 1;
+        idle = toLaunch_.empty() && toComplete_.empty() && !launching_ && !completing_ && !inlineBusy_ &&
+               flushReq_ == takenReq_ && doneTicket_ + 1 == next && sets_[next % kSets].busyTicket == 0;
+        if (idle)
+            inlineBusy_ = true;   // (the launcher takes nothing until this caller has launched)
+    }
+    if (!idle) {
+        sub.unlock();
+        uint64_t my;
+        {
+            std::lock_guard<std::mutex> g(qMu_);
+            my = ++flushReq_;
+        }
+        launchCv_.notify_one();
+        std::unique_lock<std::mutex> lk(qMu_);
+        doneCv_.wait(lk, [&] { return stop_ || takenReq_ >= my; });
+        const uint64_t t = reqTicket_;   // (covers this caller's work: every ticket up to it)
+        doneCv_.wait(lk, [&] { return stop_ || doneTicket_ >= t; });
+        return t != 0 && doneTicket_ >= t && !failed();
+    }
+    Batch* b;
+    {
+        std::unique_lock<InstanceLock> w(detach);
+        b = take_batch();
+    }
+    if (!b) {
+        // (an earlier submission took this caller's work: wait for it)
+        const uint64_t last = nextTicket_;
+        {
+            std::lock_guard<std::mutex> g(qMu_);
+            inlineBusy_ = false;
+        }
+        sub.unlock();
+        launchCv_.notify_one();
+        return wait(last) && last != 0;
+    }
+    {
+        std::lock_guard<std::mutex> g(qMu_);
+        sets_[b->set].busyTicket = b->ticket;   // (free: checked above, and nobody took a ticket since)
+    }
+    return run_inline(b, sub);
+}
+
+bool Engine::run_inline(Batch* b, std::unique_lock<std::mutex>& sub)
+{
+    tl("inline", b->ticket);
+    assemble_batch(*b, pool());   // (the set was claimed by the caller)
     if (!failed())
         launch_batch(*b);
+    {
+        // Launched: later tickets follow it on the stream, so the launcher
+        // may lay out and launch other threads' submissions while this caller
+        // waits for its fence; the completer publishes them only after this
+        // ticket.
+        std::lock_guard<std::mutex> g(qMu_);
+        inlineBusy_ = false;
+    }
     sub.unlock();   // (the next submission may be laid out while this one runs)
+    launchCv_.notify_one();
     if (complete_batch(*b))
         reclaim_batch(*b);
     {
@@ -1662,13 +1732,47 @@ bool Engine::flush_and_sync(std::shared_mutex* detach)
             sets_[b->set].busyTicket = 0;
         doneTicket_ = b->ticket;
         doneSeen_.store(b->ticket, std::memory_order_release);
-        inlineBusy_ = false;
     }
     setCv_.notify_all();
     doneCv_.notify_all();
-    launchCv_.notify_one();
     delete b;
     return !failed();
+}
+
+Batch* Engine::take_requested()
+{
+    // Wait for the next ticket's transfer set before detaching: calls that
+    // arrive meanwhile join this submission.
+    for (;;) {
+        uint64_t next;
+        {
+            std::unique_lock<std::mutex> lk(qMu_);
+            next = nextTicket_.load(std::memory_order_acquire) + 1;
+            setCv_.wait(lk, [&] { return stop_ || !toLaunch_.empty() || sets_[next % kSets].busyTicket == 0; });
+            if (stop_ || !toLaunch_.empty())
+                return nullptr;   // (queued submissions go first)
+        }
+        std::lock_guard<std::mutex> sub(submitMu_);
+        if (nextTicket_.load(std::memory_order_relaxed) + 1 != next)
+            continue;   // (a ticket was handed out meanwhile)
+        uint64_t reqs;
+        {
+            std::lock_guard<std::mutex> g(qMu_);
+            reqs = flushReq_;
+        }
+        Batch* b;
+        {
+            std::unique_lock<InstanceLock> w(instMu_);
+            b = take_batch();
+        }
+        {
+            std::lock_guard<std::mutex> g(qMu_);
+            takenReq_ = reqs;
+            reqTicket_ = nextTicket_.load(std::memory_order_relaxed);
+        }
+        doneCv_.notify_all();
+        return b;
+    }
 }
 
 bool Engine::flush()
@@ -1690,13 +1794,26 @@ void Engine::launcher_loop()
         Batch* b = nullptr;
         {
             std::unique_lock<std::mutex> lk(qMu_);
-            launchCv_.wait(lk, [&] { return stop_ || (!toLaunch_.empty() && !inlineBusy_); });
+            launchCv_.wait(lk, [&] {
+                return stop_ || (!inlineBusy_ && (!toLaunch_.empty() || flushReq_ > takenReq_));
+            });
             if (stop_)
                 return;
-            b = toLaunch_.front();
-            toLaunch_.pop_front();
-            ++taken;
+            if (!toLaunch_.empty()) {
+                b = toLaunch_.front();
+                toLaunch_.pop_front();
+                ++taken;
+            }
             launching_ = true;
+        }
+        if (!b) {
+            // drop-in flush requests: detach everything queued so far
+            b = take_requested();
+            if (!b) {
+                std::lock_guard<std::mutex> g(qMu_);
+                launching_ = false;
+                continue;
+            }
         }
         if (!b->assembled && !failed()) {
             claim_set(*b);
@@ -1977,6 +2094,12 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     off = align16(off + gdescs.size() * sizeof(GeDesc));
     bt.oGeIn = off;
     off = align16(off + geInBytes);
+    // the download copy list (the counters and results, then every range)
+    size_t nDownloads = 0;
+    for (const Shard::Queues& q : bt.queues)
+        nDownloads += q.downloads.size();
+    bt.oCopy = off;
+    off = align16(off + (nDownloads + 1) * sizeof(BeCopy));
     bt.upBytes = off;
     if (bt.upBytes)
         ensure_up(xs, bt.upBytes);
@@ -2143,6 +2266,23 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
             dOff = align16(dOff + d.bytes);
         }
     ensure_down(xs, dOff);
+    {
+        // the same list for the device (one copy kernel however many ranges,
+        // launch_batch): host sides as the device addresses them
+        std::vector<BeCopy>& cp = bt.copies;
+        cp.clear();
+        cp.push_back(BeCopy{(uint64_t)(uintptr_t)xs.downHost, (uint64_t)(uintptr_t)xs.downDev,
+                            kAcctBytes + (uint64_t)resultWords * 4});
+        for (size_t i = 0; i < bt.dls.size(); ++i)
+            cp.push_back(BeCopy{(uint64_t)(uintptr_t)(xs.downHost + bt.downloads[i].off), bt.dls[i]->dev,
+                                bt.dls[i]->bytes});
+        if (xs.downHostDev) {
+            BeCopy* dl = (BeCopy*)(up + bt.oCopy);
+            const uint64_t shift = (uint64_t)(uintptr_t)xs.downHostDev - (uint64_t)(uintptr_t)xs.downHost;
+            for (size_t i = 0; i < cp.size(); ++i)
+                dl[i] = BeCopy{cp[i].dst + shift, cp[i].src, cp[i].bytes};
+        }
+    }
 
     st.flushes = 1;
     st.launches = phases.size() + (nIngest ? 1 : 0) + (gdescs.empty() ? 0 : 1);
@@ -2159,6 +2299,7 @@ void Engine::launch_batch(Batch& bt)
 {
     XferSet& xs = sets_[bt.set];
     EngineStats& st = bt.st;
+
     // originals the application staged on the transfer stream (stage_in)
     for (void* m : bt.marks) {
         be_wait_mark(m);
@@ -2206,18 +2347,11 @@ void Engine::launch_batch(Batch& bt)
                             (uint32_t)ph.solveCount);
         }
     }
-    {
-        // the counters and solve results, then the downloads, in one call
-        // (one kernel when small: be_copy_pinned)
-        std::vector<BeCopy>& cp = bt.copies;
-        cp.clear();
-        cp.push_back(BeCopy{(uint64_t)(uintptr_t)xs.downHost, (uint64_t)(uintptr_t)xs.downDev,
-                            kAcctBytes + (uint64_t)bt.resultWords * 4});
-        for (size_t i = 0; i < bt.dls.size(); ++i)
-            cp.push_back(BeCopy{(uint64_t)(uintptr_t)(xs.downHost + bt.downloads[i].off), bt.dls[i]->dev,
-                                bt.dls[i]->bytes});
-        be_copy_pinned(cp.data(), (unsigned)cp.size(), false);
-    }
+    // the counters and solve results, then the downloads, in one call (one
+    // kernel when small; its range list was laid out with the upload: a
+    // drop-in submission carries a range per application call)
+    be_copy_list(bt.copies.data(), xs.downHostDev ? bt.upBase + bt.oCopy : nullptr, (unsigned)bt.copies.size(),
+                 false);
     bt.fence = be_fence();
     bt.launched = true;
     std::lock_guard<std::mutex> g(statsMu_);
@@ -2255,7 +2389,10 @@ void Engine::completer_loop()
         if (kPublishDelayUs > 0)
             std::this_thread::sleep_for(std::chrono::microseconds(kPublishDelayUs));
         {
-            std::lock_guard<std::mutex> g(qMu_);
+            // tickets publish in order: an earlier one may still be completing
+            // on the thread that flushed it inline
+            std::unique_lock<std::mutex> g(qMu_);
+            doneCv_.wait(g, [&] { return stop_ || doneTicket_ + 1 >= b->ticket; });
             if (sets_[b->set].busyTicket == b->ticket)   // (a failed batch may never have claimed it)
                 sets_[b->set].busyTicket = 0;
             doneTicket_ = b->ticket;

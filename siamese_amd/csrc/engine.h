@@ -27,11 +27,44 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <pthread.h>
 #include <shared_mutex>
 #include <thread>
 #include <vector>
 
 namespace sgpu {
+
+/// The drop-in API's instance lock: a reader-writer lock that prefers the
+/// writer.  Instance calls hold it shared for microseconds; a flush holds it
+/// exclusively only to detach the queued work.  std::shared_mutex (glibc's
+/// default rwlock) prefers readers, so with many application threads calling
+/// in, a flush's exclusive request waited behind an unbroken stream of
+/// instance calls.  Never taken shared twice by one thread (a waiting writer
+/// would block the second acquisition).
+class InstanceLock
+{
+public:
+    InstanceLock()
+    {
+        pthread_rwlockattr_t a;
+        pthread_rwlockattr_init(&a);
+        pthread_rwlockattr_setkind_np(&a, PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
+        pthread_rwlock_init(&l_, &a);
+        pthread_rwlockattr_destroy(&a);
+    }
+    ~InstanceLock() { pthread_rwlock_destroy(&l_); }
+    InstanceLock(const InstanceLock&) = delete;
+    InstanceLock& operator=(const InstanceLock&) = delete;
+    void lock() { pthread_rwlock_wrlock(&l_); }
+    bool try_lock() { return pthread_rwlock_trywrlock(&l_) == 0; }
+    void unlock() { pthread_rwlock_unlock(&l_); }
+    void lock_shared() { pthread_rwlock_rdlock(&l_); }
+    bool try_lock_shared() { return pthread_rwlock_tryrdlock(&l_) == 0; }
+    void unlock_shared() { pthread_rwlock_unlock(&l_); }
+
+private:
+    pthread_rwlock_t l_;
+};
 
 class WorkerPool;
 
@@ -418,7 +451,7 @@ public:
     /// exclusively while the queued work is detached; concurrent callers
     /// commit as a group (the first one's submission carries everything
     /// queued before it, the others find their work taken and only wait).
-    bool flush_and_sync(std::shared_mutex* detach = nullptr);
+    bool flush_and_sync(InstanceLock* detach = nullptr);
     /// A device operation failed; the engine accepts no further work.
     bool failed() const { return failed_.load(std::memory_order_relaxed); }
     bool pending() const;
@@ -455,7 +488,7 @@ public:
     /// one thread at a time; concurrent calls on different instances are this
     /// library's extension of siamese.h:59), exclusive only while a flush
     /// detaches the queued work (flush_and_sync(&instance_lock())).
-    std::shared_mutex& instance_lock() { return instMu_; }
+    InstanceLock& instance_lock() { return instMu_; }
 
     /// Count EngineStats::execUniqueBytes at flush assembly (a measurement
     /// aid: off by default, it sorts every segment's operands).
@@ -488,6 +521,9 @@ private:
     void assemble_batch(Batch& b, WorkerPool& wp);
     Batch* take_batch();   // queued programs and queues as a batch with its ticket (nullptr: none)
     void claim_set(Batch& b);
+    bool flush_requested(std::unique_lock<std::mutex>& sub, InstanceLock& detach);
+    bool run_inline(Batch* b, std::unique_lock<std::mutex>& sub);
+    Batch* take_requested();   // launcher thread: detach for filed flush requests
     WorkerPool& asm_pool();   // launcher thread only
     void launch_batch(Batch& b);
     bool complete_batch(Batch& b);   // false: the submission failed
@@ -498,7 +534,7 @@ private:
     bool ready_ = false;
     std::atomic<bool> failed_{false};
     std::mutex mu_;
-    std::shared_mutex instMu_;
+    InstanceLock instMu_;
     // one submission detached and assembled at a time (take_batch hands out
     // tickets, and toLaunch_ keeps ticket order); held by enqueue() and
     // flush_and_sync() until the batch is queued or launched
@@ -548,6 +584,11 @@ private:
     std::atomic<uint64_t> queuedSeen_{0};           // batches pushed to toLaunch_
     bool stop_ = false;
     bool launching_ = false;                        // the launcher holds a batch (qMu_)
+    // drop-in flush requests (qMu_): filed, and covered by the launcher's
+    // latest detach, whose last ticket is reqTicket_
+    uint64_t flushReq_ = 0;
+    uint64_t takenReq_ = 0;
+    uint64_t reqTicket_ = 0;
     bool completing_ = false;                       // the completer holds a batch (qMu_)
     bool inlineBusy_ = false;                       // a caller runs a submission itself (qMu_)
     std::thread launcher_, completer_;
@@ -564,6 +605,7 @@ private:
         size_t upCap = 0;
         uint8_t* downHost = nullptr;
         uint8_t* downDev = nullptr;   // device-side gather area for downloads + results
+        uint8_t* downHostDev = nullptr;   // downHost as the device addresses it, or null
         size_t downCap = 0;
         uint64_t busyTicket = 0;      // submission using it (0: free)
         uint8_t* wideDev = nullptr;   // k_ldpc scratch ring (see ensure_wide)

@@ -347,6 +347,7 @@ void be_copy_pinned(const BeCopy* r, unsigned n, bool)
     for (unsigned i = 0; i < n; ++i)
         std::memcpy((void*)(uintptr_t)r[i].dst, (const void*)(uintptr_t)r[i].src, r[i].bytes);
 }
+void be_copy_list(const BeCopy* r, const void*, unsigned n, bool toDevice) { be_copy_pinned(r, n, toDevice); }
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
 static bool noexec();
