@@ -16,6 +16,12 @@
 #ifndef SGPU_EXEC_LPT
 #define SGPU_EXEC_LPT 1
 #endif
+// k_exec workgroups a launch aims for: a phase with more tiles than this
+// gives each workgroup a run of its segment's tiles (one LDS-filling
+// workgroup per CU: 256 CUs)
+#ifndef SGPU_EXEC_GROUPS
+#define SGPU_EXEC_GROUPS 256
+#endif
 
 namespace sgpu {
 
@@ -1317,6 +1323,7 @@ struct SegRef
 {
     const ProgramBody::Segment* seg;
     uint32_t wordBase, words, itemBase;
+    uint32_t tilesPerItem = 1;      // tiles one k_exec workgroup runs
     uint32_t wideBase = 0;          // first k_ldpc item of its wide rows
     uint64_t wideOff = 0;           // their scratch (bytes into the set's wideDev)
 };
@@ -1924,6 +1931,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         for (size_t k = 0; k < maxSegs; ++k) {
             Phase ex{Phase::EXEC, nItems, 0, 0, 0, kNoRows};
             const size_t segBegin = segs.size();
+            size_t phaseTiles = 0;
             for (ProgramBody* p : bt.bodies[g]) {
                 if (k >= p->nsegs)
                     continue;
@@ -1934,26 +1942,36 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                     if (op.kind == OP_ROWS)
                         ex.maxRows = ex.maxRows == kNoRows ? op.valid : std::max(ex.maxRows, op.valid);
                 const size_t words = kOpWords * s.ops.size() + s.terms.size() + s.rowsWords;
-                segs.push_back(SegRef{&s, (uint32_t)nWords, (uint32_t)words, (uint32_t)nItems, 0, 0});
+                segs.push_back(SegRef{&s, (uint32_t)nWords, (uint32_t)words, 0});
                 nOps += s.ops.size();
                 nTerms += s.terms.size();
                 nWords += words;
-                nItems += (s.maxExtent + kExecTileBytes - 1) / kExecTileBytes;
+                phaseTiles += (s.maxExtent + kExecTileBytes - 1) / kExecTileBytes;
             }
 #if SGPU_EXEC_LPT
             // Longest op lists first: workgroups are dispatched in blockIdx
             // order and a launch runs in a few rounds of workgroups per CU,
             // so the short segments fill the last round's tail.
+            std::stable_sort(segs.begin() + (long)segBegin, segs.end(),
+                             [](const SegRef& a, const SegRef& b) { return a.words > b.words; });
+#endif
             {
-                std::stable_sort(segs.begin() + (long)segBegin, segs.end(),
-                                 [](const SegRef& a, const SegRef& b) { return a.words > b.words; });
+                // Runs of a segment's tiles per workgroup once the launch has
+                // more tiles than the chip runs at once: a workgroup then
+                // loads each OP_ROWS table and draws its row plans once for
+                // all of its tiles (a single stream's few tiles stay spread
+                // over as many workgroups)
+                const size_t tpi = std::min<size_t>(
+                    0xffff, std::max<size_t>(1, (phaseTiles + SGPU_EXEC_GROUPS - 1) / SGPU_EXEC_GROUPS));
                 uint32_t ib = (uint32_t)ex.itemBegin;
                 for (size_t i = segBegin; i < segs.size(); ++i) {
+                    const size_t tiles = (segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes;
                     segs[i].itemBase = ib;
-                    ib += (segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes;
+                    segs[i].tilesPerItem = (uint32_t)tpi;
+                    ib += (uint32_t)((tiles + tpi - 1) / tpi);
                 }
+                nItems = ib;
             }
-#endif
             ex.itemCount = nItems - ex.itemBegin;
             ex.wideBegin = nWide;
             for (size_t i = segBegin; i < segs.size(); ++i) {
@@ -2215,9 +2233,11 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 }
                 ExecItem* items = (ExecItem*)(up + bt.oItems) + r.itemBase;
                 const uint32_t nOpsSeg = (uint32_t)s.ops.size();
+                const uint32_t tiles = (s.maxExtent + kExecTileBytes - 1) / kExecTileBytes;
                 uint32_t n = 0;
-                for (uint32_t tb = 0; tb < s.maxExtent; tb += kExecTileBytes)
-                    items[n++] = ExecItem{r.wordBase, r.words, nOpsSeg, tb};
+                for (uint32_t t = 0; t < tiles; t += r.tilesPerItem)
+                    items[n++] = ExecItem{r.wordBase, r.words, nOpsSeg,
+                                          t | std::min(r.tilesPerItem, tiles - t) << 16};
             }
         } else if (t.kind == 3) {
             for (size_t i = t.a; i < t.b; ++i)

@@ -251,7 +251,8 @@ struct ExecItem
     uint32_t streamBegin;  // first 16-byte word of the segment's stream
     uint32_t streamWords;  // words in the segment's stream
     uint32_t opCount;
-    uint32_t tileBase;     // first byte of this tile
+    uint32_t tiles;        // first 256-byte tile | tile count << 16: the workgroup runs the
+                           // op list over each tile (op by op, every tile in turn)
 };
 
 /// Triangular solve of one decode (reference SiameseDecoder.cpp:1065-1238).

@@ -149,11 +149,10 @@ void literal_tile(uint64_t dst, uint32_t at, const uint8_t* lit, uint32_t len, u
     }
 }
 
-void exec_tile(const uint8_t* stream, const ExecItem& it, uint64_t* acct)
+void exec_tile(const uint8_t* stream, const ExecItem& it, uint32_t t0, uint64_t* acct)
 {
     const uint8_t* w = stream + (size_t)it.streamBegin * 16;
     const uint8_t* end = w + (size_t)it.streamWords * 16;
-    const uint32_t t0 = it.tileBase;
     std::vector<TileTerm> terms;
     for (uint32_t oi = 0; oi < it.opCount; ++oi) {
         GfOp op;
@@ -407,8 +406,12 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
 {
     if (noexec())
         return;
+    // (tile by tile: every op is local to its byte columns, so this order
+    // gives the device's op-by-op, tile-by-tile results)
     for (uint32_t i = 0; i < count; ++i)
-        exec_tile(static_cast<const uint8_t*>(stream), items[i], acct);
+        for (uint32_t t = 0; t < (items[i].tiles >> 16); ++t)
+            exec_tile(static_cast<const uint8_t*>(stream), items[i],
+                      ((items[i].tiles & 0xffffu) + t) * kExecTileBytes, acct);
 }
 
 void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
