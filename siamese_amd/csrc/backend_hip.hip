@@ -39,6 +39,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <string>
+#include <type_traits>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -292,6 +293,10 @@ constexpr unsigned kExecThreads = 64 * kExecWaves;
 constexpr unsigned kExecDepth = 16;          // term loads in flight per wave
 constexpr unsigned kExecSolo = 4;            // ops with <= this many terms run on wave 0 alone
 constexpr unsigned kRingWords = 256;         // prefetched words per op (threads < 256 fetch one)
+#ifndef SGPU_STAGE_PRE
+#define SGPU_STAGE_PRE 2
+#endif
+constexpr unsigned kStagePre = SGPU_STAGE_PRE;   // stage entries per thread fetched a tile ahead (<= 4: VGPRs)
 constexpr unsigned kRowsTableLds = 1024;     // sum + window descriptors of an OP_ROWS batch in LDS
 constexpr unsigned kPlanCap = 8192;          // planned row terms (LDS slot indices) per batch
 constexpr unsigned kPlanRows = 256;          // rows of a batch that get a plan
@@ -552,28 +557,44 @@ __device__ __forceinline__ uint64_t pcg_jump(uint64_t s, uint64_t inc, uint32_t 
 // entries below the batch's stageLo, which only k_ldpc reads, stay in memory.
 // table_entry: a word past the window (updates, rows); win_entry: window
 // element e; table_word: any word)
+// Fit: the whole block from `skip` lies in the LDS table (OP_ROWS checks it
+// once per batch), so no read has a memory fallback: a fallback's load would
+// make every later use wait for all of the wave's outstanding memory loads
+// (the waits merge at the join), the update units' and rows' among them.
+// (The executor reads no window element below skip: Program::rows_close.)
+template <bool Fit>
 __device__ __forceinline__ uint4 table_entry(const uint4* tableL, const uint4* __restrict__ seg,
                                              uint32_t blockWord, uint32_t i, uint32_t skip)
 {
     const uint32_t j = i - skip;
-    return j < kRowsTableLds ? tableL[j] : ld16((uint64_t)(seg + blockWord + i));
+    if constexpr (Fit)
+        return tableL[j];
+    else
+        return j < kRowsTableLds ? tableL[j] : ld16((uint64_t)(seg + blockWord + i));
 }
+template <bool Fit>
 __device__ __forceinline__ uint4 win_entry(const uint4* tableL, const uint4* __restrict__ seg, uint32_t blockWord,
                                            uint32_t e, uint32_t skip)
 {
     const uint32_t j = e - skip;   // (wraps for e < skip)
-    return j < kRowsTableLds - kRowSums ? tableL[kRowSums + j] : ld16((uint64_t)(seg + blockWord + kRowSums + e));
+    if constexpr (Fit)
+        return tableL[kRowSums + j];
+    else
+        return j < kRowsTableLds - kRowSums ? tableL[kRowSums + j]
+                                            : ld16((uint64_t)(seg + blockWord + kRowSums + e));
 }
+template <bool Fit>
 __device__ __forceinline__ uint4 table_word(const uint4* tableL, const uint4* __restrict__ seg, uint32_t blockWord,
                                             uint32_t i, uint32_t skip)
 {
-    return i < kRowSums ? tableL[i] : win_entry(tableL, seg, blockWord, i - kRowSums, skip);
+    return i < kRowSums ? tableL[i] : win_entry<Fit>(tableL, seg, blockWord, i - kRowSums, skip);
 }
 
 // One Siamese row's LDPC picks [d0, d1) of PCG.Seed(row, N) (pair index
 // d / 2; even draws feed acc0, odd acc1), from the staged window where it
 // holds the element and from memory otherwise.  Returns the reference source
 // bytes of the picks (SiameseEncoder.cpp:1100-1144 adds min(len, rowBytes)).
+template <bool Fit>
 __device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t off, uint32_t d0,
                                               uint32_t d1, uint32_t rn, uint32_t tileBase, uint32_t p,
                                               uint32_t lane, uint64_t pcgA, uint64_t pcgG,
@@ -590,7 +611,7 @@ __device__ __forceinline__ uint32_t row_picks(uint32_t row, uint32_t N, uint32_t
         // lane j: draw c + j -> window element e and its descriptor
         const uint64_t st = pcgA * sc + inc * pcgG;
         const uint32_t e = off + pcg_output(st) % N;
-        const uint4 ev = win_entry(tableL, seg, blk, e, stageLo);
+        const uint4 ev = win_entry<Fit>(tableL, seg, blk, e, stageLo);
         sc = c_pcgA[64] * sc + inc * c_pcgG[64];
         const uint32_t cnt = d1 - c < 64 ? d1 - c : 64;
         for (uint32_t j0 = 0; j0 < cnt; j0 += kExecDepth) {
@@ -723,13 +744,14 @@ __global__ __launch_bounds__(64 * kLdpcWaves) void k_ldpc(const LdpcItem* __rest
 // rows): the lane holds bytes [p16, p16 + 16) of its quad's row; m0 / m1 /
 // cut are the quad's row's masks and cutoff (per lane), `live` whether the
 // row reaches this tile.
+template <bool Fit>
 __device__ __forceinline__ uint4 version_elem16(uint32_t e, uint32_t p16, uint32_t b4, const uint32_t* stage,
                                                 uint32_t stageLo, uint32_t staged, const uint4* tableL,
                                                 const uint4* __restrict__ seg, uint32_t blk)
 {
     if (e - stageLo < staged)
         return lds16(stage, (kRowSums + e - stageLo) * 64 + b4);
-    const uint4 d = win_entry(tableL, seg, blk, e, stageLo);
+    const uint4 d = win_entry<Fit>(tableL, seg, blk, e, stageLo);
     const uint64_t src = ((uint64_t)d.y << 32) | d.x;
     return p16 < d.z ? ld16(src + p16) : make_uint4(0, 0, 0, 0);
 }
@@ -741,6 +763,7 @@ __device__ __forceinline__ uint4 version_elem16(uint32_t e, uint32_t p16, uint32
 // masks pick them): one load and at most two multiplies per element.  A sum
 // whose length ends inside this 16-byte lane is taken per sum, with its
 // exact clip.
+template <bool Fit>
 __device__ __forceinline__ void version_lane16(uint32_t l, uint32_t m0, uint32_t m1, uint32_t cut, bool live,
                                                uint32_t p16, uint32_t b4, const uint32_t* updOfL,
                                                const uint32_t* updFromL, const uint32_t* updToL,
@@ -784,7 +807,7 @@ __device__ __forceinline__ void version_lane16(uint32_t l, uint32_t m0, uint32_t
             for (uint32_t s = 0; s < kSums; ++s)
                 need |= (full >> s & 1u) && s != 0 && e >= f[s] && e < t[s];
             if (need) {
-                const uint32_t col = win_entry(tableL, seg, blk, e, stageLo).w;
+                const uint32_t col = win_entry<Fit>(tableL, seg, blk, e, stageLo).w;
                 cx = cxL[col % kColumnValuePeriod];
             }
 #pragma unroll
@@ -800,7 +823,7 @@ __device__ __forceinline__ void version_lane16(uint32_t l, uint32_t m0, uint32_t
             }
             if (!(y0 | y1))
                 continue;
-            const uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
+            const uint4 v = version_elem16<Fit>(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
             if (y0)
                 a0 = xor16(a0, y0 == 1 ? v : gf_mul16_tab(v, gf_tab_l(permL, permC, y0)));
             if (y1)
@@ -815,9 +838,9 @@ __device__ __forceinline__ void version_lane16(uint32_t l, uint32_t m0, uint32_t
             for (uint32_t e = cut <= f[s] ? f[s] : f[s] + ((cut - f[s] + kLanes - 1) / kLanes) * kLanes; e < t[s];
                  e += kLanes) {
                 PHASE_ADD(25, 1);
-                uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
+                uint4 v = version_elem16<Fit>(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
                 if (s != 0) {
-                    const uint32_t col = win_entry(tableL, seg, blk, e, stageLo).w;
+                    const uint32_t col = win_entry<Fit>(tableL, seg, blk, e, stageLo).w;
                     const uint32_t cx = cxL[col % kColumnValuePeriod];
                     v = gf_mul16_tab(v, gf_tab_l(permL, permC, s == 1 ? (cx & 0xffu) : (cx >> 8)));
                 }
@@ -831,6 +854,7 @@ __device__ __forceinline__ void version_lane16(uint32_t l, uint32_t m0, uint32_t
     }
 }
 
+template <bool Fit>
 __device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_t cut, bool live, uint32_t p16,
                                                uint32_t b4, const uint32_t* updOfL, const uint32_t* updFromL,
                                                const uint32_t* updToL, const uint32_t* cxL, const uint4* permL,
@@ -839,12 +863,13 @@ __device__ __forceinline__ void row_versions16(uint32_t m0, uint32_t m1, uint32_
                                                uint32_t blk, uint4& a0, uint4& a1)
 {
     for (uint32_t l = 0; l < kLanes; ++l)
-        version_lane16(l, m0, m1, cut, live, p16, b4, updOfL, updFromL, updToL, cxL, permL, permC, stage, stageLo,
+        version_lane16<Fit>(l, m0, m1, cut, live, p16, b4, updOfL, updFromL, updToL, cxL, permL, permC, stage, stageLo,
                        staged, tableL, seg, blk, a0, a1);
 }
 
 // The same for a row in the dword layout (general path: one wave, the lane
 // holds bytes [p, p + 4)); m0 / m1 / cut are wave-uniform.
+template <bool Fit>
 __device__ __forceinline__ void row_versions4(uint32_t m0, uint32_t m1, uint32_t cut, uint32_t tileBase, uint32_t p,
                                               uint32_t lane, const uint32_t* updOfL, const uint32_t* updFromL,
                                               const uint32_t* updToL, const uint32_t* cxL, const uint32_t* stage,
@@ -865,7 +890,7 @@ __device__ __forceinline__ void row_versions4(uint32_t m0, uint32_t m1, uint32_t
         for (uint32_t e = cut <= from ? from : from + ((cut - from + kLanes - 1) / kLanes) * kLanes; e < to;
              e += kLanes) {
             uint32_t v;
-            const uint4 d = win_entry(tableL, seg, blk, e, stageLo);
+            const uint4 d = win_entry<Fit>(tableL, seg, blk, e, stageLo);
             if (e - stageLo < staged) {
                 v = stage[(kRowSums + e - stageLo) * 64 + lane];
             } else {
@@ -983,6 +1008,10 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
             }
         } else if (kind == OP_LINCOMB) {
             for (uint32_t ti = 0; ti < nTiles; ++ti) {
+                // (lane-derived values re-derived per tile: hoisted out of the
+                // tile loop they would hold VGPRs through every phase)
+                const uint32_t tid = opaque(threadIdx.x);
+                const uint32_t lane = tid & 63;
                 const uint32_t tileBase = tile0 + ti * kExecTileBytes, p = tileBase + lane * 4;
                 if (tileBase >= align16u(n))
                     break;   // uniform: the op ends before this tile
@@ -1025,708 +1054,753 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 }
             }
         } else if (kind == OP_ROWS) {
+            // (specialised on whether the batch's whole block lies in the
+            // LDS table: table_entry)
+            auto rows_op = [&](auto fitTag) {
+                constexpr bool Fit = decltype(fitTag)::value;
 #ifdef SGPU_PHASE_CLOCKS
-            unsigned long long tclk = clock64();
+                unsigned long long tclk = clock64();
 #endif
-            const uint32_t R = n, E = valid, U = uni(h1.y);
-            const uint32_t blk = pos + kOpWords;        // stream word of sum entry 0
-            const uint32_t T = kRowSums + E;
-            // the whole block (descriptors, updates, rows) to LDS: every
-            // later header read is an LDS read, not a memory round trip
-            const uint32_t blockWords = uni(h1.w);
-            // (the host points the stage at the elements the batch reads:
-            // GfOp.dst low word = stageLo, ops.h; the LDS table skips the
-            // window entries below it: table_entry)
-            const uint32_t stageLo = uni(h0.x) < E ? uni(h0.x) : E;
-            for (uint32_t i = tid; i < kRowsTableLds; i += kExecThreads) {
-                const uint32_t word = i < kRowSums ? i : i + stageLo;
-                if (word < blockWords)
-                    tableL[i] = op_word(rb, seg, pos, kOpWords + word);
-            }
-            if (tid == 0)
-                generalRows = 0;
-            // the next op's prefetched block goes to the ring now (the ring's
-            // other half is free: the previous op ended with a barrier), so
-            // it holds no registers through the batch
-            if (tid < kRingWords)
-                ring[cur ^ 1][tid] = pf;
-            __syncthreads();
-            PHASE_MARK(0, tclk);
-
-            for (uint32_t ti = 0; ti < nTiles; ++ti) {
-                const uint32_t tileBase = tile0 + ti * kExecTileBytes, p = tileBase + lane * 4;
-                // phase S: stage this tile of the 24 lane sums (slots 0..23, as
-                // they stand before the batch's updates) and of window elements
-                // [0, staged) (slots 24..): table entry x is stage slot x.  Thread
-                // t loads 16 bytes of entry t/16 per pass, four passes in flight;
-                // bytes past an entry's length (absent elements: all of them)
-                // read zero.
-                if (ti == 0 && tid < kRowSums) {
-                    // (at most one update per sum in a batch: Program::rows_update)
-                    uint32_t found = 0xffu, from = 0, to = 0;
-                    for (uint32_t u = 0; u < U; ++u) {
-                        const uint4 w1 = table_entry(tableL, seg, blk, kRowSums + E + u * kUpdateWords + 1, stageLo);
-                        if (w1.z == tid && w1.y > w1.x) {
-                            found = u;
-                            from = w1.x;
-                            to = w1.y;
-                        }
-                    }
-                    updOfL[tid] = found;
-                    updFromL[tid] = from;
-                    updToL[tid] = to;
+                const uint32_t R = n, E = valid, U = uni(h1.y);
+                const uint32_t blk = pos + kOpWords;        // stream word of sum entry 0
+                const uint32_t T = kRowSums + E;
+                // the whole block (descriptors, updates, rows) to LDS: every
+                // later header read is an LDS read, not a memory round trip
+                const uint32_t blockWords = uni(h1.w);
+                // (the host points the stage at the elements the batch reads:
+                // GfOp.dst low word = stageLo, ops.h; the LDS table skips the
+                // window entries below it: table_entry)
+                const uint32_t stageLo = uni(h0.x) < E ? uni(h0.x) : E;
+                for (uint32_t i = tid; i < kRowsTableLds; i += kExecThreads) {
+                    const uint32_t word = i < kRowSums ? i : i + stageLo;
+                    if (word < blockWords)
+                        tableL[i] = op_word(rb, seg, pos, kOpWords + word);
                 }
-                const uint32_t staged = E - stageLo < stageCap ? E - stageLo : stageCap;
-                const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
-                const bool sumsStaged = stageSlots >= kRowSums;
-                const uint32_t updWord = kOpWords + T;
-                const uint32_t rowWord = updWord + U * kUpdateWords;
-                const uint32_t planned = R < kPlanRows ? R : kPlanRows;
-                constexpr unsigned kPass = kExecThreads / 16;   // entries per pass
-                uint32_t* updAcc = &part[0][0][0];              // U <= 24 update accumulators of 64 dwords
-                static_assert(kExecWaves * 2 >= kRowSums, "update accumulators fit part[]");
-                for (uint32_t i = tid; i < U * 64; i += kExecThreads)
-                    updAcc[i] = 0;
-                // rows [0, Rv) of a versioned batch (GfOp.dst high word, ops.h)
-                // take their corrections from corrL
-                const uint32_t Rv = min(min(uni(h0.y), R), (uint32_t)kVersionRows);
-                for (uint32_t i = tid; i < Rv * 128; i += kExecThreads)
-                    (&corrL[0][0][0])[i] = 0;
                 if (tid == 0)
-                    sumsDirty = 0;
-                {
-                    const uint32_t entries = sumsStaged ? kRowSums + staged : 0u;
-                    for (uint32_t x0 = tid / 16; x0 < entries; x0 += 4 * kPass) {
-                        uint4 v[4];
-#pragma unroll
-                        for (unsigned u = 0; u < 4; ++u) {
-                            const uint32_t x = x0 + u * kPass;
-                            v[u] = make_uint4(0, 0, 0, 0);
-                            if (x < entries) {
-                                const uint4 d = table_word(tableL, seg, blk, x < kRowSums ? x : x + stageLo, stageLo);
-                                const uint64_t src = ((uint64_t)d.y << 32) | d.x;
-                                if (tileBase + q16 < d.z)
-                                    v[u] = ld16(src + tileBase + q16);
-                            }
-                        }
-#pragma unroll
-                        for (unsigned u = 0; u < 4; ++u) {
-                            const uint32_t x = x0 + u * kPass;
-                            if (x < entries)
-                                *reinterpret_cast<uint4*>(&stage[x * 64 + q16 / 4]) = v[u];
-                        }
-                    }
-                }
+                    generalRows = 0;
+                // the next op's prefetched block goes to the ring now (the ring's
+                // other half is free: the previous op ended with a barrier), so
+                // it holds no registers through the batch
+                if (tid < kRingWords)
+                    ring[cur ^ 1][tid] = pf;
                 __syncthreads();
-                PHASE_MARK(1, tclk);
+                PHASE_MARK(0, tclk);
 
-                // phase A + B0: the lane-sum updates and the rows' term plans,
-                // dealt to the waves as units: unit < U*Q is part unit%Q of update
-                // unit/Q, the rest are row pairs of the plan.
-                //
-                // Updates (SiameseEncoder.cpp:359-418, SiameseDecoder.cpp:
-                // 1680-1739): element e = from, from+8, ... < to, coefficient 1, CX
-                // or CX^2 of its column.  Staged elements go four per wave
-                // instruction (quad g of the wave takes element 4j+g, lane l bytes
-                // 16*(l%16).., each lane with its element's multiply table from
-                // LDS); an update reaching past the stage falls back to the dword
-                // layout (lane j holds element j's descriptor and table, moved to
-                // scalars with readlane) with memory reads.  Partial sums meet in
-                // LDS accumulators (XOR atomics).
-                //
-                // Plan: row sizes are its selected sums plus one slot per LDPC
-                // draw, offsets a prefix sum over rows (every wave scans them all
-                // and keeps the rows whose pair it owns); the draws are made lane
-                // parallel, two rows per wave (lanes 32h.. take row 2i+h), and
-                // their reference source bytes counted; a row with a draw outside
-                // the staged window keeps reading memory (phase B1b).
-                //
-                // Version corrections (rows [0, Rv)): quad g of version task t
-                // takes lane sum 4t + g for every row; the sums of a row meet in
-                // corrL.
-                // Units x < vTasks are version tasks, then the update parts, then
-                // the row pairs.  Fewer than 16 version tasks own a wave each (the
-                // longest units, started first); the other waves share the rest.
-                const uint32_t vTasks = Rv ? kRowSums / 4 : 0u;
-                const uint32_t vWaves = vTasks < kExecWaves ? vTasks : 0u;
-                const uint32_t W2 = kExecWaves - vWaves;
-                const uint32_t Q = U == 0 ? 1u : (U >= W2 ? 1u : W2 / U);
-                const uint32_t uUnits = U * Q;
-                const uint32_t nPairs = sumsStaged ? (planned + 1) / 2 : 0u;
-                // (the row plans are the same for every tile: drawn for the first)
-                const uint32_t nUnits = vTasks + uUnits + (ti == 0 ? nPairs : 0u);
-                auto unit_wave = [&](uint32_t x) { return vWaves ? (x < vWaves ? x : vWaves + (x - vWaves) % W2) : x % kExecWaves; };
-                // the update this wave stores: its dst as kept, fetched now
-                uint64_t sdst = 0;
-                uint32_t sn = 0, svalid = 0, scur = 0;
-                if (wave < U) {
-                    const uint4 w0 = table_entry(tableL, seg, blk, updWord + wave * kUpdateWords - kOpWords, stageLo);
-                    sdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                    sn = uni(w0.z);
-                    svalid = uni(w0.w) & 0x3fffffffu;
-                    if (tileBase < align16u(sn))
-                        scur = load_cur(p, sdst, sn, svalid);
-                }
-                if (ti == 0 && nPairs) {
-                    uint32_t carry = 0;
-                    for (uint32_t r0 = 0; r0 < planned; r0 += 64) {
-                        const uint32_t r = r0 + lane;
-                        uint32_t size = 0, n01 = 0;
-                        if (r < planned) {
-                            const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
-                            // (a wide row reads its two k_ldpc sums as one pair)
-                            const uint32_t pairs = (w1.x & kRowWide) ? 1u : (w1.w + kPairRate - 1) / kPairRate;
-                            const uint32_t n0 = __builtin_popcount(w1.x & 0xffffffu) + pairs;
-                            const uint32_t n1 = __builtin_popcount(w1.y & 0xffffffu) + pairs;
-                            size = n0 + n1;
-                            n01 = n0 | (n1 << 16);
-                        }
-                        uint32_t incl = size;
-#pragma unroll
-                        for (unsigned d = 1; d < 64; d <<= 1) {
-                            const uint32_t t = __shfl_up(incl, d, 64);
-                            if (lane >= d)
-                                incl += t;
-                        }
-                        const uint32_t offs = carry + incl - size;
-                        if (r < planned && unit_wave(vTasks + uUnits + (r >> 1)) == wave) {
-                            const bool fits = offs + size <= kPlanCap;
-                            rowInfo[r] = make_uint2(fits ? offs : kNoPlan, n01);
-                            if (!fits)
-                                generalRows = 1;
-                        }
-                        carry += __shfl(incl, 63, 64);
-                    }
-                }
-                const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
-                if (wave == kExecWaves - 1) {
-                    // rows whose cutoff is past every update's last element read
-                    // the final sums as they are (no version corrections)
-                    uint32_t m = 0;
-                    if (lane < kRowSums && updOfL[lane] != 0xffu) {
-                        const uint32_t f = updFromL[lane], t = updToL[lane];
-                        m = f + ((t - f - 1) / kLanes) * kLanes + 1;
-                    }
-#pragma unroll
-                    for (unsigned d = 16; d >= 1; d >>= 1)
-                        m = max(m, (uint32_t)__shfl_xor(m, d, 64));
-                    if (lane == 0)
-                        updMaxLast1 = m;
-                }
-                PHASE_MARK(30, tclk);
-                const uint32_t xStep = vWaves ? (wave < vWaves ? nUnits : W2) : kExecWaves;
-                for (uint32_t x = vWaves && wave >= vWaves ? vTasks + wave - vWaves : wave; x < nUnits; x += xStep) {
-                    const uint32_t unit = x - vTasks;   // (update parts, then row pairs)
-                    if (x < vTasks) {
-                        [[maybe_unused]] const unsigned long long vclk0 = PHASE_CLK();
-                        // sum k's update elements as suffix sums: rows from the
-                        // last (largest cutoff) down, each adding the elements
-                        // in [its cutoff, the previous row's) and handing the
-                        // suffix to the row if its masks select sum k (the rows'
-                        // cutoffs never decrease: Program::rows_row)
-                        const uint32_t k = 4 * x + g;
-                        const uint32_t sidx = k % kSums;
-                        const uint32_t p16 = tileBase + (lane & 15u) * 16u;
-                        const uint32_t f = updFromL[k], t = updToL[k], slen = tableL[k].z;
-                        const bool any = updOfL[k] != 0xffu && t > f && p16 < slen;
-                        uint4 S = make_uint4(0, 0, 0, 0);
-                        uint32_t hiE = t;
-                        for (uint32_t r1 = Rv; r1 > 0; --r1) {
-                            const uint32_t r = r1 - 1;
-                            const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
-                            const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
-                            const uint32_t cut = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo).y;
-                            if (any) {
-                                const uint32_t first = cut <= f ? f : f + ((cut - f + kLanes - 1) / kLanes) * kLanes;
-                                for (uint32_t e = first; e < hiE; e += kLanes) {
-                                    uint4 v = version_elem16(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
-                                    if (sidx != 0) {
-                                        const uint32_t cx = cxL[win_entry(tableL, seg, blk, e, stageLo).w %
-                                                                kColumnValuePeriod];
-                                        v = gf_mul16_tab(v, gf_tab_l(permL, permC, sidx == 1 ? (cx & 0xffu) : (cx >> 8)));
-                                    }
-                                    S = xor16(S, v);
-                                }
-                                hiE = min(hiE, first);
-                            }
-                            const bool in0 = (w1.x >> k) & 1u, in1 = (w1.y >> k) & 1u;
-                            if (any && (in0 || in1) && tileBase < align16u(w0.z) && (S.x | S.y | S.z | S.w)) {
-                                const uint4 V = p16 + 16 > slen ? mask16(S, (int)slen - (int)p16) : S;
-                                if (in0) {
-                                    uint32_t* c0 = &corrL[r][0][b4];
-                                    atomicXor(c0 + 0, V.x);
-                                    atomicXor(c0 + 1, V.y);
-                                    atomicXor(c0 + 2, V.z);
-                                    atomicXor(c0 + 3, V.w);
-                                }
-                                if (in1) {
-                                    uint32_t* c1 = &corrL[r][1][b4];
-                                    atomicXor(c1 + 0, V.x);
-                                    atomicXor(c1 + 1, V.y);
-                                    atomicXor(c1 + 2, V.z);
-                                    atomicXor(c1 + 3, V.w);
-                                }
+                uint4 pre[kStagePre];   // the next tile's first stage entries (prefetched)
+                for (uint32_t ti = 0; ti < nTiles; ++ti) {
+                    // (lane-derived values re-derived per tile: hoisted out of the
+                    // tile loop they would hold VGPRs through every phase)
+                    const uint32_t tid = opaque(threadIdx.x);
+                    const uint32_t lane = tid & 63;
+                    const uint32_t tileBase = tile0 + ti * kExecTileBytes, p = tileBase + lane * 4;
+                    // phase S: stage this tile of the 24 lane sums (slots 0..23, as
+                    // they stand before the batch's updates) and of window elements
+                    // [0, staged) (slots 24..): table entry x is stage slot x.  Thread
+                    // t loads 16 bytes of entry t/16 per pass, four passes in flight;
+                    // bytes past an entry's length (absent elements: all of them)
+                    // read zero.
+                    if (ti == 0 && tid < kRowSums) {
+                        // (at most one update per sum in a batch: Program::rows_update)
+                        uint32_t found = 0xffu, from = 0, to = 0;
+                        for (uint32_t u = 0; u < U; ++u) {
+                            const uint4 w1 = table_entry<Fit>(tableL, seg, blk, kRowSums + E + u * kUpdateWords + 1, stageLo);
+                            if (w1.z == tid && w1.y > w1.x) {
+                                found = u;
+                                from = w1.x;
+                                to = w1.y;
                             }
                         }
-                        PHASE_ADD(26, PHASE_CLK() - vclk0);
-                        PHASE_ADD(29, 1);
-                    } else if (unit < uUnits) {
-                        [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
-                        const uint32_t u = unit / Q;
-                        const uint32_t uq = unit % Q;
-                        const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords, stageLo);
-                        const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords, stageLo);
-                        const uint32_t un = uni(w0.z), us = uni(w0.w) >> 30;
-                        const uint32_t from = uni(w1.x), to = uni(w1.y);
-                        const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
-                        const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
-                        if (tileBase < align16u(un) && k0 < k1) {
-                            uint32_t refBytes = 0;   // reference source bytes (one add/muladd per original)
-                            if (from + k0 * kLanes >= stageLo && from + (k1 - 1) * kLanes - stageLo < staged) {
-                                // quad layout, four elements per quad in flight
-                                // (elements past the range read the zero slot)
-                                uint4 a = make_uint4(0, 0, 0, 0);
-                                for (uint32_t kk = k0; kk < k1; kk += 16) {
-                                    uint32_t slot[4], y[4];
+                        updOfL[tid] = found;
+                        updFromL[tid] = from;
+                        updToL[tid] = to;
+                    }
+                    const uint32_t staged = E - stageLo < stageCap ? E - stageLo : stageCap;
+                    const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
+                    const bool sumsStaged = stageSlots >= kRowSums;
+                    const uint32_t updWord = kOpWords + T;
+                    const uint32_t rowWord = updWord + U * kUpdateWords;
+                    const uint32_t planned = R < kPlanRows ? R : kPlanRows;
+                    constexpr unsigned kPass = kExecThreads / 16;   // entries per pass
+                    uint32_t* updAcc = &part[0][0][0];              // U <= 24 update accumulators of 64 dwords
+                    static_assert(kExecWaves * 2 >= kRowSums, "update accumulators fit part[]");
+                    for (uint32_t i = tid; i < U * 64; i += kExecThreads)
+                        updAcc[i] = 0;
+                    // rows [0, Rv) of a versioned batch (GfOp.dst high word, ops.h)
+                    // take their corrections from corrL
+                    const uint32_t Rv = min(min(uni(h0.y), R), (uint32_t)kVersionRows);
+                    for (uint32_t i = tid; i < Rv * 128; i += kExecThreads)
+                        (&corrL[0][0][0])[i] = 0;
+                    if (tid == 0)
+                        sumsDirty = 0;
+                    const uint32_t entries = sumsStaged ? kRowSums + staged : 0u;
+                    {
+                        for (uint32_t x0 = tid / 16; x0 < entries; x0 += 4 * kPass) {
+                            uint4 v[4];
+                            // (a thread's first kStagePre entries of a later tile
+                            // were fetched during the previous tile's rows)
+                            const bool pref = ti > 0 && x0 < 4 * kPass;
 #pragma unroll
-                                    for (unsigned j = 0; j < 4; ++j) {
-                                        const uint32_t k = kk + 4 * j + g;
-                                        const bool act = k < k1;
-                                        const uint32_t e = from + (act ? k : k0) * kLanes;
-                                        const uint4 ev = win_entry(tableL, seg, blk, e, stageLo);
-                                        if (act && (lane & 15u) == 0)
-                                            refBytes += ev.z;
-                                        slot[j] = act ? kRowSums + e - stageLo : zeroSlot;
-                                        const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
-                                        y[j] = us == 1 ? (cx & 0xff) : (cx >> 8);
+                            for (unsigned u = 0; u < kStagePre; ++u)
+                                v[u] = pre[u];
+                            {
+#pragma unroll
+                                for (unsigned u = 0; u < 4; ++u) {
+                                    const uint32_t x = x0 + u * kPass;
+                                    if (pref && u < kStagePre)
+                                        continue;
+                                    v[u] = make_uint4(0, 0, 0, 0);
+                                    if (x < entries) {
+                                        const uint4 d =
+                                            table_word<Fit>(tableL, seg, blk, x < kRowSums ? x : x + stageLo, stageLo);
+                                        const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+                                        if (tileBase + q16 < d.z)
+                                            v[u] = ld16(src + tileBase + q16);
                                     }
-                                    uint4 v[4];
+                                }
+                            }
 #pragma unroll
-                                    for (unsigned j = 0; j < 4; ++j)
-                                        v[j] = lds16(stage, slot[j] * 64 + b4);
-                                    if (us != 0) {
+                            for (unsigned u = 0; u < 4; ++u) {
+                                const uint32_t x = x0 + u * kPass;
+                                if (x < entries)
+                                    *reinterpret_cast<uint4*>(&stage[x * 64 + q16 / 4]) = v[u];
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    PHASE_MARK(1, tclk);
+
+                    // phase A + B0: the lane-sum updates and the rows' term plans,
+                    // dealt to the waves as units: unit < U*Q is part unit%Q of update
+                    // unit/Q, the rest are row pairs of the plan.
+                    //
+                    // Updates (SiameseEncoder.cpp:359-418, SiameseDecoder.cpp:
+                    // 1680-1739): element e = from, from+8, ... < to, coefficient 1, CX
+                    // or CX^2 of its column.  Staged elements go four per wave
+                    // instruction (quad g of the wave takes element 4j+g, lane l bytes
+                    // 16*(l%16).., each lane with its element's multiply table from
+                    // LDS); an update reaching past the stage falls back to the dword
+                    // layout (lane j holds element j's descriptor and table, moved to
+                    // scalars with readlane) with memory reads.  Partial sums meet in
+                    // LDS accumulators (XOR atomics).
+                    //
+                    // Plan: row sizes are its selected sums plus one slot per LDPC
+                    // draw, offsets a prefix sum over rows (every wave scans them all
+                    // and keeps the rows whose pair it owns); the draws are made lane
+                    // parallel, two rows per wave (lanes 32h.. take row 2i+h), and
+                    // their reference source bytes counted; a row with a draw outside
+                    // the staged window keeps reading memory (phase B1b).
+                    //
+                    // Version corrections (rows [0, Rv)): quad g of version task t
+                    // takes lane sum 4t + g for every row; the sums of a row meet in
+                    // corrL.
+                    // Units x < vTasks are version tasks, then the update parts, then
+                    // the row pairs.  Fewer than 16 version tasks own a wave each (the
+                    // longest units, started first); the other waves share the rest.
+                    const uint32_t vTasks = Rv ? kRowSums / 4 : 0u;
+                    const uint32_t vWaves = vTasks < kExecWaves ? vTasks : 0u;
+                    const uint32_t W2 = kExecWaves - vWaves;
+                    const uint32_t Q = U == 0 ? 1u : (U >= W2 ? 1u : W2 / U);
+                    const uint32_t uUnits = U * Q;
+                    const uint32_t nPairs = sumsStaged ? (planned + 1) / 2 : 0u;
+                    // (the row plans are the same for every tile: drawn for the first)
+                    const uint32_t nUnits = vTasks + uUnits + (ti == 0 ? nPairs : 0u);
+                    auto unit_wave = [&](uint32_t x) { return vWaves ? (x < vWaves ? x : vWaves + (x - vWaves) % W2) : x % kExecWaves; };
+                    // the update this wave stores: its dst as kept, fetched now
+                    uint64_t sdst = 0;
+                    uint32_t sn = 0, svalid = 0, scur = 0;
+                    if (wave < U) {
+                        const uint4 w0 = table_entry<Fit>(tableL, seg, blk, updWord + wave * kUpdateWords - kOpWords, stageLo);
+                        sdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                        sn = uni(w0.z);
+                        svalid = uni(w0.w) & 0x3fffffffu;
+                        if (tileBase < align16u(sn))
+                            scur = load_cur(p, sdst, sn, svalid);
+                    }
+                    if (ti == 0 && nPairs) {
+                        uint32_t carry = 0;
+                        for (uint32_t r0 = 0; r0 < planned; r0 += 64) {
+                            const uint32_t r = r0 + lane;
+                            uint32_t size = 0, n01 = 0;
+                            if (r < planned) {
+                                const uint4 w1 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
+                                // (a wide row reads its two k_ldpc sums as one pair)
+                                const uint32_t pairs = (w1.x & kRowWide) ? 1u : (w1.w + kPairRate - 1) / kPairRate;
+                                const uint32_t n0 = __builtin_popcount(w1.x & 0xffffffu) + pairs;
+                                const uint32_t n1 = __builtin_popcount(w1.y & 0xffffffu) + pairs;
+                                size = n0 + n1;
+                                n01 = n0 | (n1 << 16);
+                            }
+                            uint32_t incl = size;
+#pragma unroll
+                            for (unsigned d = 1; d < 64; d <<= 1) {
+                                const uint32_t t = __shfl_up(incl, d, 64);
+                                if (lane >= d)
+                                    incl += t;
+                            }
+                            const uint32_t offs = carry + incl - size;
+                            if (r < planned && unit_wave(vTasks + uUnits + (r >> 1)) == wave) {
+                                const bool fits = offs + size <= kPlanCap;
+                                rowInfo[r] = make_uint2(fits ? offs : kNoPlan, n01);
+                                if (!fits)
+                                    generalRows = 1;
+                            }
+                            carry += __shfl(incl, 63, 64);
+                        }
+                    }
+                    const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
+                    if (wave == kExecWaves - 1) {
+                        // rows whose cutoff is past every update's last element read
+                        // the final sums as they are (no version corrections)
+                        uint32_t m = 0;
+                        if (lane < kRowSums && updOfL[lane] != 0xffu) {
+                            const uint32_t f = updFromL[lane], t = updToL[lane];
+                            m = f + ((t - f - 1) / kLanes) * kLanes + 1;
+                        }
+#pragma unroll
+                        for (unsigned d = 16; d >= 1; d >>= 1)
+                            m = max(m, (uint32_t)__shfl_xor(m, d, 64));
+                        if (lane == 0)
+                            updMaxLast1 = m;
+                    }
+                    PHASE_MARK(30, tclk);
+                    const uint32_t xStep = vWaves ? (wave < vWaves ? nUnits : W2) : kExecWaves;
+                    for (uint32_t x = vWaves && wave >= vWaves ? vTasks + wave - vWaves : wave; x < nUnits; x += xStep) {
+                        const uint32_t unit = x - vTasks;   // (update parts, then row pairs)
+                        if (x < vTasks) {
+                            [[maybe_unused]] const unsigned long long vclk0 = PHASE_CLK();
+                            // sum k's update elements as suffix sums: rows from the
+                            // last (largest cutoff) down, each adding the elements
+                            // in [its cutoff, the previous row's) and handing the
+                            // suffix to the row if its masks select sum k (the rows'
+                            // cutoffs never decrease: Program::rows_row)
+                            const uint32_t k = 4 * x + g;
+                            const uint32_t sidx = k % kSums;
+                            const uint32_t p16 = tileBase + (lane & 15u) * 16u;
+                            const uint32_t f = updFromL[k], t = updToL[k], slen = tableL[k].z;
+                            const bool any = updOfL[k] != 0xffu && t > f && p16 < slen;
+                            uint4 S = make_uint4(0, 0, 0, 0);
+                            uint32_t hiE = t;
+                            for (uint32_t r1 = Rv; r1 > 0; --r1) {
+                                const uint32_t r = r1 - 1;
+                                const uint4 w0 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
+                                const uint4 w1 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
+                                const uint32_t cut = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo).y;
+                                if (any) {
+                                    const uint32_t first = cut <= f ? f : f + ((cut - f + kLanes - 1) / kLanes) * kLanes;
+                                    for (uint32_t e = first; e < hiE; e += kLanes) {
+                                        uint4 v = version_elem16<Fit>(e, p16, b4, stage, stageLo, staged, tableL, seg, blk);
+                                        if (sidx != 0) {
+                                            const uint32_t cx = cxL[win_entry<Fit>(tableL, seg, blk, e, stageLo).w %
+                                                                    kColumnValuePeriod];
+                                            v = gf_mul16_tab(v, gf_tab_l(permL, permC, sidx == 1 ? (cx & 0xffu) : (cx >> 8)));
+                                        }
+                                        S = xor16(S, v);
+                                    }
+                                    hiE = min(hiE, first);
+                                }
+                                const bool in0 = (w1.x >> k) & 1u, in1 = (w1.y >> k) & 1u;
+                                if (any && (in0 || in1) && tileBase < align16u(w0.z) && (S.x | S.y | S.z | S.w)) {
+                                    const uint4 V = p16 + 16 > slen ? mask16(S, (int)slen - (int)p16) : S;
+                                    if (in0) {
+                                        uint32_t* c0 = &corrL[r][0][b4];
+                                        atomicXor(c0 + 0, V.x);
+                                        atomicXor(c0 + 1, V.y);
+                                        atomicXor(c0 + 2, V.z);
+                                        atomicXor(c0 + 3, V.w);
+                                    }
+                                    if (in1) {
+                                        uint32_t* c1 = &corrL[r][1][b4];
+                                        atomicXor(c1 + 0, V.x);
+                                        atomicXor(c1 + 1, V.y);
+                                        atomicXor(c1 + 2, V.z);
+                                        atomicXor(c1 + 3, V.w);
+                                    }
+                                }
+                            }
+                            PHASE_ADD(26, PHASE_CLK() - vclk0);
+                            PHASE_ADD(29, 1);
+                        } else if (unit < uUnits) {
+                            [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
+                            const uint32_t u = unit / Q;
+                            const uint32_t uq = unit % Q;
+                            const uint4 w0 = table_entry<Fit>(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords, stageLo);
+                            const uint4 w1 = table_entry<Fit>(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords, stageLo);
+                            const uint32_t un = uni(w0.z), us = uni(w0.w) >> 30;
+                            const uint32_t from = uni(w1.x), to = uni(w1.y);
+                            const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
+                            const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
+                            if (tileBase < align16u(un) && k0 < k1) {
+                                uint32_t refBytes = 0;   // reference source bytes (one add/muladd per original)
+                                if (from + k0 * kLanes >= stageLo && from + (k1 - 1) * kLanes - stageLo < staged) {
+                                    // quad layout, four elements per quad in flight
+                                    // (elements past the range read the zero slot)
+                                    uint4 a = make_uint4(0, 0, 0, 0);
+                                    for (uint32_t kk = k0; kk < k1; kk += 16) {
+                                        uint32_t slot[4], y[4];
+#pragma unroll
+                                        for (unsigned j = 0; j < 4; ++j) {
+                                            const uint32_t k = kk + 4 * j + g;
+                                            const bool act = k < k1;
+                                            const uint32_t e = from + (act ? k : k0) * kLanes;
+                                            const uint4 ev = win_entry<Fit>(tableL, seg, blk, e, stageLo);
+                                            if (act && (lane & 15u) == 0)
+                                                refBytes += ev.z;
+                                            slot[j] = act ? kRowSums + e - stageLo : zeroSlot;
+                                            const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
+                                            y[j] = us == 1 ? (cx & 0xff) : (cx >> 8);
+                                        }
+                                        uint4 v[4];
 #pragma unroll
                                         for (unsigned j = 0; j < 4; ++j)
-                                            v[j] = gf_mul16_tab(v[j], gf_tab_l(permL, permC, y[j]));
-                                    }
-                                    a = xor16(xor16(a, xor16(v[0], v[1])), xor16(v[2], v[3]));
-                                }
-                                atomicXor(&updAcc[u * 64 + b4 + 0], a.x);
-                                atomicXor(&updAcc[u * 64 + b4 + 1], a.y);
-                                atomicXor(&updAcc[u * 64 + b4 + 2], a.z);
-                                atomicXor(&updAcc[u * 64 + b4 + 3], a.w);
-                            } else {
-                                uint32_t acc = 0;
-                                for (uint32_t c = k0; c < k1; c += 64) {
-                                    const uint32_t e = from + (c + lane) * kLanes;
-                                    const uint4 ev = c + lane < k1 ? win_entry(tableL, seg, blk, e, stageLo)
-                                                                   : make_uint4(0, 0, 0, 0);
-                                    const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
-                                    const GfTab tab = gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8));
-                                    refBytes += ev.z;
-                                    const uint32_t cnt = k1 - c < 64 ? k1 - c : 64;
-                                    for (uint32_t j0 = 0; j0 < cnt; j0 += 16) {
-                                        uint32_t v[16];
+                                            v[j] = lds16(stage, slot[j] * 64 + b4);
+                                        if (us != 0) {
 #pragma unroll
-                                        for (unsigned k = 0; k < 16; ++k) {
-                                            const uint32_t j = j0 + k;
-                                            const uint32_t ej = from + (c + j) * kLanes;
-                                            v[k] = 0;
-                                            if (j < cnt) {
-                                                if (ej - stageLo < staged) {
-                                                    v[k] = stage[(kRowSums + ej - stageLo) * 64 + lane];
-                                                } else {
-                                                    uint64_t src;
-                                                    uint32_t len;
-                                                    lane_term(ev, j, src, len);
-                                                    if (tileBase < len)
-                                                        v[k] = term_load(src, len, p);
+                                            for (unsigned j = 0; j < 4; ++j)
+                                                v[j] = gf_mul16_tab(v[j], gf_tab_l(permL, permC, y[j]));
+                                        }
+                                        a = xor16(xor16(a, xor16(v[0], v[1])), xor16(v[2], v[3]));
+                                    }
+                                    atomicXor(&updAcc[u * 64 + b4 + 0], a.x);
+                                    atomicXor(&updAcc[u * 64 + b4 + 1], a.y);
+                                    atomicXor(&updAcc[u * 64 + b4 + 2], a.z);
+                                    atomicXor(&updAcc[u * 64 + b4 + 3], a.w);
+                                } else {
+                                    uint32_t acc = 0;
+                                    for (uint32_t c = k0; c < k1; c += 64) {
+                                        const uint32_t e = from + (c + lane) * kLanes;
+                                        const uint4 ev = c + lane < k1 ? win_entry<Fit>(tableL, seg, blk, e, stageLo)
+                                                                       : make_uint4(0, 0, 0, 0);
+                                        const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX, CX^2
+                                        const GfTab tab = gf_tab_l(permL, permC, us == 1 ? (cx & 0xff) : (cx >> 8));
+                                        refBytes += ev.z;
+                                        const uint32_t cnt = k1 - c < 64 ? k1 - c : 64;
+                                        for (uint32_t j0 = 0; j0 < cnt; j0 += 16) {
+                                            uint32_t v[16];
+#pragma unroll
+                                            for (unsigned k = 0; k < 16; ++k) {
+                                                const uint32_t j = j0 + k;
+                                                const uint32_t ej = from + (c + j) * kLanes;
+                                                v[k] = 0;
+                                                if (j < cnt) {
+                                                    if (ej - stageLo < staged) {
+                                                        v[k] = stage[(kRowSums + ej - stageLo) * 64 + lane];
+                                                    } else {
+                                                        uint64_t src;
+                                                        uint32_t len;
+                                                        lane_term(ev, j, src, len);
+                                                        if (tileBase < len)
+                                                            v[k] = term_load(src, len, p);
+                                                    }
+                                                }
+                                            }
+#pragma unroll
+                                            for (unsigned k = 0; k < 16; ++k) {
+                                                const uint32_t j = j0 + k;
+                                                if (j < cnt) {
+                                                    if (us == 0) {
+                                                        acc ^= v[k];
+                                                    } else {
+                                                        const GfTab t{rl(tab.a0, j), rl(tab.a1, j), rl(tab.b0, j),
+                                                                      rl(tab.b1, j), rl(tab.c, j)};
+                                                        acc ^= gf_mul_tab(v[k], t);
+                                                    }
                                                 }
                                             }
                                         }
-#pragma unroll
-                                        for (unsigned k = 0; k < 16; ++k) {
-                                            const uint32_t j = j0 + k;
-                                            if (j < cnt) {
-                                                if (us == 0) {
-                                                    acc ^= v[k];
-                                                } else {
-                                                    const GfTab t{rl(tab.a0, j), rl(tab.a1, j), rl(tab.b0, j),
-                                                                  rl(tab.b1, j), rl(tab.c, j)};
-                                                    acc ^= gf_mul_tab(v[k], t);
-                                                }
-                                            }
-                                        }
                                     }
+                                    atomicXor(&updAcc[u * 64 + lane], acc);
                                 }
-                                atomicXor(&updAcc[u * 64 + lane], acc);
+                                if (tileBase == 0)
+                                    acct_wave(&acctL, refBytes);
+                            }
+                            PHASE_ADD(19, PHASE_CLK() - uclk0);
+                            PHASE_ADD(27, 1);
+                        } else {
+                            [[maybe_unused]] const unsigned long long pclk0 = PHASE_CLK();
+                            const uint32_t h = lane >> 5, hl = lane & 31u;
+                            const uint32_t r = 2 * (unit - uUnits) + h;
+                            const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);   // (own write)
+                            const bool act = info.x != kNoPlan;
+                            if (!__any(act ? 1 : 0))
+                                continue;
+                            const uint4 z4 = make_uint4(0, 0, 0, 0);
+                            const uint4 w0 = act ? table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo) : z4;
+                            const uint4 w1 = act ? table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo) : z4;
+                            const uint4 w2 = act ? table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo) : z4;
+                            const uint32_t rn = w0.z;
+                            const uint32_t m0 = w1.x & 0xffffffu, m1 = w1.y & 0xffffffu;
+                            const uint32_t row = w1.z, N = act ? w1.w : 0u, woff = w2.x;
+                            const uint32_t off0 = info.x, off1 = info.x + (info.y & 0xffffu);
+                            const uint32_t pc0 = __builtin_popcount(m0), pc1 = __builtin_popcount(m1);
+                            // sums: lane k < 24 of the half places slot k if its bit is set
+                            if (act && hl < kRowSums) {
+                                const uint32_t below = (1u << hl) - 1u;
+                                if (m0 >> hl & 1u)
+                                    plan[off0 + __builtin_popcount(m0 & below)] = (uint16_t)hl;
+                                if (m1 >> hl & 1u)
+                                    plan[off1 + __builtin_popcount(m1 & below)] = (uint16_t)hl;
+                            }
+                            // draws: even -> row list, odd -> product list; a wide
+                            // row's two "draws" are its k_ldpc sums L0 / L1 at
+                            // window entries woff, woff + 1 (counted by k_ldpc)
+                            const bool wide = act && (w1.x & kRowWide) != 0;
+                            const uint32_t D = N ? 2 * ((N + kPairRate - 1) / kPairRate) : (wide ? 2u : 0u);
+                            uint32_t Dmax = max(D, (uint32_t)__shfl_xor(D, 32, 64));
+                            Dmax = uni(Dmax);
+                            bool general = false;
+                            uint32_t refBytes = 0;
+                            const uint64_t inc = ((uint64_t)row << 1) | 1u;
+                            uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
+                            // x % N through a double reciprocal: the quotient estimate
+                            // is within one for 32-bit x, then corrected exactly
+                            const double invN = N ? 1.0 / (double)N : 0.0;
+                            // (an opaque lane index keeps these loads in the loop: hoisted
+                            // out of the op loop they would hold 4 VGPRs through every phase)
+                            const uint32_t jl = opaque(hl);
+                            const uint64_t ja = c_pcgA[jl], jg = c_pcgG[jl];
+                            for (uint32_t c = 0; c < Dmax; c += 32) {
+                                const uint32_t d = c + hl;
+                                const uint64_t st = ja * sc + inc * jg;
+                                sc = c_pcgA[32] * sc + inc * c_pcgG[32];
+                                if (d < D) {
+                                    uint32_t e = woff + d;
+                                    if (!wide) {
+                                        const uint32_t x = pcg_output(st);
+                                        const uint32_t qn = (uint32_t)((double)x * invN);
+                                        int64_t rr = (int64_t)x - (int64_t)qn * N;
+                                        rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
+                                        e = woff + (uint32_t)rr;
+                                    }
+                                    const uint32_t len = win_entry<Fit>(tableL, seg, blk, e, stageLo).z;
+                                    if (!wide)
+                                        refBytes += len < rn ? len : rn;
+                                    general |= e - stageLo >= staged;
+                                    const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
+                                    plan[at] = (uint16_t)(e - stageLo < staged ? kRowSums + e - stageLo : 0);
+                                }
                             }
                             if (tileBase == 0)
                                 acct_wave(&acctL, refBytes);
-                        }
-                        PHASE_ADD(19, PHASE_CLK() - uclk0);
-                        PHASE_ADD(27, 1);
-                    } else {
-                        [[maybe_unused]] const unsigned long long pclk0 = PHASE_CLK();
-                        const uint32_t h = lane >> 5, hl = lane & 31u;
-                        const uint32_t r = 2 * (unit - uUnits) + h;
-                        const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);   // (own write)
-                        const bool act = info.x != kNoPlan;
-                        if (!__any(act ? 1 : 0))
-                            continue;
-                        const uint4 z4 = make_uint4(0, 0, 0, 0);
-                        const uint4 w0 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo) : z4;
-                        const uint4 w1 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo) : z4;
-                        const uint4 w2 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo) : z4;
-                        const uint32_t rn = w0.z;
-                        const uint32_t m0 = w1.x & 0xffffffu, m1 = w1.y & 0xffffffu;
-                        const uint32_t row = w1.z, N = act ? w1.w : 0u, woff = w2.x;
-                        const uint32_t off0 = info.x, off1 = info.x + (info.y & 0xffffu);
-                        const uint32_t pc0 = __builtin_popcount(m0), pc1 = __builtin_popcount(m1);
-                        // sums: lane k < 24 of the half places slot k if its bit is set
-                        if (act && hl < kRowSums) {
-                            const uint32_t below = (1u << hl) - 1u;
-                            if (m0 >> hl & 1u)
-                                plan[off0 + __builtin_popcount(m0 & below)] = (uint16_t)hl;
-                            if (m1 >> hl & 1u)
-                                plan[off1 + __builtin_popcount(m1 & below)] = (uint16_t)hl;
-                        }
-                        // draws: even -> row list, odd -> product list; a wide
-                        // row's two "draws" are its k_ldpc sums L0 / L1 at
-                        // window entries woff, woff + 1 (counted by k_ldpc)
-                        const bool wide = act && (w1.x & kRowWide) != 0;
-                        const uint32_t D = N ? 2 * ((N + kPairRate - 1) / kPairRate) : (wide ? 2u : 0u);
-                        uint32_t Dmax = max(D, (uint32_t)__shfl_xor(D, 32, 64));
-                        Dmax = uni(Dmax);
-                        bool general = false;
-                        uint32_t refBytes = 0;
-                        const uint64_t inc = ((uint64_t)row << 1) | 1u;
-                        uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed()
-                        // x % N through a double reciprocal: the quotient estimate
-                        // is within one for 32-bit x, then corrected exactly
-                        const double invN = N ? 1.0 / (double)N : 0.0;
-                        // (an opaque lane index keeps these loads in the loop: hoisted
-                        // out of the op loop they would hold 4 VGPRs through every phase)
-                        const uint32_t jl = opaque(hl);
-                        const uint64_t ja = c_pcgA[jl], jg = c_pcgG[jl];
-                        for (uint32_t c = 0; c < Dmax; c += 32) {
-                            const uint32_t d = c + hl;
-                            const uint64_t st = ja * sc + inc * jg;
-                            sc = c_pcgA[32] * sc + inc * c_pcgG[32];
-                            if (d < D) {
-                                uint32_t e = woff + d;
-                                if (!wide) {
-                                    const uint32_t x = pcg_output(st);
-                                    const uint32_t qn = (uint32_t)((double)x * invN);
-                                    int64_t rr = (int64_t)x - (int64_t)qn * N;
-                                    rr = rr < 0 ? rr + N : (rr >= (int64_t)N ? rr - N : rr);
-                                    e = woff + (uint32_t)rr;
-                                }
-                                const uint32_t len = win_entry(tableL, seg, blk, e, stageLo).z;
-                                if (!wide)
-                                    refBytes += len < rn ? len : rn;
-                                general |= e - stageLo >= staged;
-                                const uint32_t at = (d & 1u) ? off1 + pc1 + d / 2 : off0 + pc0 + d / 2;
-                                plan[at] = (uint16_t)(e - stageLo < staged ? kRowSums + e - stageLo : 0);
+                            const uint64_t gb = __ballot(general ? 1 : 0);
+                            if (hl == 0 && act && (uint32_t)(gb >> (32 * h)) != 0) {
+                                rowInfo[r].x = kPlanGeneral;
+                                generalRows = 1;
                             }
-                        }
-                        if (tileBase == 0)
-                            acct_wave(&acctL, refBytes);
-                        const uint64_t gb = __ballot(general ? 1 : 0);
-                        if (hl == 0 && act && (uint32_t)(gb >> (32 * h)) != 0) {
-                            rowInfo[r].x = kPlanGeneral;
-                            generalRows = 1;
-                        }
-                        PHASE_ADD(20, PHASE_CLK() - pclk0);
-                        PHASE_ADD(28, 1);
-                    }
-                }
-                PHASE_MARK(31, tclk);
-                __syncthreads();
-                PHASE_MARK(2, tclk);
-
-                // update stores.  Update u's sum (SumUpdate.sum = k)
-                // also refreshes stage slot k straight from registers when it is
-                // the buffer the rows read and the stored bytes cover the staged
-                // ones; anything else marks the stage stale and the sums are
-                // re-read from memory after a barrier.
-                for (uint32_t u = wave; u < U; u += kExecWaves) {
-                    const uint4 w0 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords, stageLo);
-                    const uint4 w1 = table_entry(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords, stageLo);
-                    const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                    const uint32_t un = uni(w0.z), uvalid = uni(w0.w) & 0x3fffffffu;
-                    if (tileBase >= align16u(un))
-                        continue;   // (this tile of the sum is unchanged, as staged)
-                    const uint32_t cu = u == wave ? scur : load_cur(p, udst, un, uvalid);
-                    const uint32_t out = item_value(updAcc[u * 64 + lane], p, un, uvalid, cu);
-                    if (p < align16u(un))
-                        st4(udst + p, out);
-                    // (slot k holds the buffer the rows read as sum k; an update of
-                    // another buffer -- the rows of this batch do not read the sum,
-                    // it grew after they took their table -- leaves it as staged)
-                    const uint32_t k = uni(w1.z);
-                    bool stale = k >= kRowSums;
-                    if (k < kRowSums && sumsStaged) {
-                        const uint4 d = tableL[k];
-                        const uint64_t src = ((uint64_t)uni(d.y) << 32) | uni(d.x);
-                        const uint32_t len = uni(d.z);
-                        if (src == udst) {
-                            // (exactly the sum's first `len` bytes, as the rows read
-                            // it: with versioned reads the update may have grown it)
-                            if (align16u(len) <= align16u(un))
-                                stage[k * 64 + lane] = p < len ? out & byte_mask((int)len - (int)p) : 0u;
-                            else
-                                stale = true;
+                            PHASE_ADD(20, PHASE_CLK() - pclk0);
+                            PHASE_ADD(28, 1);
                         }
                     }
-                    if (stale && nPairs && lane == 0)   // (no plan: no row reads the stage)
-                        sumsDirty = 1;
-                }
-                __syncthreads();
-                PHASE_MARK(3, tclk);
-                if (tid == 0)
-                    PHASE_ADD(21, sumsDirty ? 1 : 0);
-                if (sumsStaged && uni(sumsDirty)) {
-                    // (this workgroup's own stores, visible after the barrier)
-                    if (tid < kRowSums * 16) {
-                        const uint32_t k = tid / 16;
-                        const uint4 d = tableL[k];
-                        const uint64_t src = ((uint64_t)d.y << 32) | d.x;
-                        uint4 v = make_uint4(0, 0, 0, 0);
-                        if (tileBase + q16 < d.z)
-                            v = mask16(ld16(src + tileBase + q16), (int)d.z - (int)(tileBase + q16));
-                        *reinterpret_cast<uint4*>(&stage[k * 64 + q16 / 4]) = v;
-                    }
+                    PHASE_MARK(31, tclk);
                     __syncthreads();
-                }
-                PHASE_MARK(4, tclk);
+                    PHASE_MARK(2, tclk);
 
-                // phase B1a: planned rows, four per wave at a time: quad g of the
-                // wave (lanes 16g..16g+15) takes row 4t+g, and lane l holds bytes
-                // 16*(l%16).. of the tile, so one 16-byte LDS read per lane moves
-                // one term of each of four rows and every per-row step (the
-                // descriptors, the RX product, the stores) is paid once per four
-                // rows.
-                {
-                    const uint32_t nq = (planned + 3) / 4;
-                    const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
-                    const uint32_t p16 = tileBase + (lane & 15u) * 16u;
-                    for (uint32_t task = wave; task < nq; task += kExecWaves) {
-#ifdef SGPU_PHASE_CLOCKS
-                        unsigned long long qclk = clock64();
-#endif
-                        const uint32_t r = task * 4 + g;
-                        const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
-                        const bool act = info.x < kPlanGeneral;
-                        if (!__any(act ? 1 : 0))
-                            continue;
-                        const uint4 z4 = make_uint4(0, 0, 0, 0);
-                        const uint4 w0 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo) : z4;
-                        const uint4 w1 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo) : z4;
-                        const uint4 w2 = act ? table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo) : z4;
-                        const uint64_t rdst = ((uint64_t)w0.y << 32) | w0.x;
-                        const uint32_t rn = w0.z, rvalid = w0.w;
-                        const uint32_t mix = w1.y >> 24;
-                        const bool live = act && tileBase < align16u(rn);
-                        // dst as kept (decoder rows), fetched before the terms stream in
-                        const uint4 cur = live ? load_cur16(p16, rdst, rn, rvalid) : z4;
-                        const GfTab tab = gf_tab_l(permL, permC, mix > 1 ? mix : 1u);
-                        const uint32_t off0 = info.x, n0 = live ? (info.y & 0xffffu) : 0u;
-                        const uint32_t off1 = info.x + (info.y & 0xffffu), n1 = live ? (info.y >> 16) : 0u;
-                        uint32_t most = n0 > n1 ? n0 : n1;
-                        most = max(most, (uint32_t)__shfl_xor(most, 16, 64));
-                        most = uni(max(most, (uint32_t)__shfl_xor(most, 32, 64)));
-                        PHASE_MARK(13, qclk);
-                        uint4 a0 = z4, a1 = z4;
-                        // 16 terms at a time: lane i of a quad reads plan entry
-                        // t+i of its row's lists, a row broadcast (DPP) hands
-                        // entry j to the whole quad, 4 terms of each list in flight
-                        // (no masking after the reads, so they go out together)
-                        for (uint32_t t = 0; t < most; t += 16) {
-                            const uint32_t i = t + (lane & 15u);
-                            // (entries past a list's end name the zero slot)
-                            const uint32_t s0 = i < n0 ? (uint32_t)plan[off0 + i] : zeroSlot;
-                            const uint32_t s1 = i < n1 ? (uint32_t)plan[off1 + i] : zeroSlot;
-                            const uint32_t left = most - t;   // (uniform)
-#define SGPU_QUAD_GROUP(J)                                                                                  \
-        {                                                                                                       \
-            const uint4 x0 = lds16(stage, row_bcast<(J)>(s0) * 64 + b4);                                        \
-            const uint4 x1 = lds16(stage, row_bcast<(J) + 1>(s0) * 64 + b4);                                    \
-            const uint4 x2 = lds16(stage, row_bcast<(J) + 2>(s0) * 64 + b4);                                    \
-            const uint4 x3 = lds16(stage, row_bcast<(J) + 3>(s0) * 64 + b4);                                    \
-            const uint4 y0 = lds16(stage, row_bcast<(J)>(s1) * 64 + b4);                                        \
-            const uint4 y1 = lds16(stage, row_bcast<(J) + 1>(s1) * 64 + b4);                                    \
-            const uint4 y2 = lds16(stage, row_bcast<(J) + 2>(s1) * 64 + b4);                                    \
-            const uint4 y3 = lds16(stage, row_bcast<(J) + 3>(s1) * 64 + b4);                                    \
-            a0 = xor16(xor16(a0, xor16(x0, x1)), xor16(x2, x3));                                                \
-            a1 = xor16(xor16(a1, xor16(y0, y1)), xor16(y2, y3));                                                \
-        }
-                            SGPU_QUAD_GROUP(0)
-                            if (left > 4)
-                                SGPU_QUAD_GROUP(4)
-                            if (left > 8)
-                                SGPU_QUAD_GROUP(8)
-                            if (left > 12)
-                                SGPU_QUAD_GROUP(12)
-#undef SGPU_QUAD_GROUP
-                        }
-                        PHASE_MARK(14, qclk);
-                        // (rows read the sums as of their cutoff, ops.h RowItem)
-                        if (r < Rv) {
-                            a0 = xor16(a0, lds16(&corrL[r][0][0], b4));
-                            a1 = xor16(a1, lds16(&corrL[r][1][0], b4));
-                        }
-                        if (__any(act && r >= Rv && w2.y < updMaxLast1 ? 1 : 0)) {
-                            row_versions16(w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, live && r >= Rv, p16, b4, updOfL, updFromL,
-                                           updToL, cxL, permL, permC, stage, stageLo, staged, tableL, seg, blk, a0, a1);
-                            PHASE_MARK(16, qclk);
-                            if (lane == 0)
-                                PHASE_ADD(17, 1);
-                        }
-                        if (live)
-                            store_item16(xor16(a0, gf_mul16_tab(a1, tab)), p16, rdst, rn, rvalid, cur);
-                        if (act) {
-                            store_literal(p16, rdst, rn, row_lit_len(w1.x), w2.z, w2.w, 16);
-                        }
-                        PHASE_MARK(15, qclk);
-                    }
-                }
-
-                // phase B1b: rows without a plan (a draw outside the staged
-                // window, or past the plan's capacity).  R >= W: wave w takes rows
-                // w, w+W, ...; R < W: row r's terms are split into P = W / R parts,
-                // unit w = (w / P, w % P), and the parts meet in LDS.  They read
-                // sums and undrawn-from-LDS picks from memory; lane j < 24 holds
-                // sum entry j.
-                const uint4 sumv = lane < kRowSums ? tableL[lane] : make_uint4(0, 0, 0, 0);
-                const uint32_t P = R >= kExecWaves ? 1u : kExecWaves / R;
-                const uint32_t units = (R > planned || uni(generalRows)) ? (P == 1 ? R : R * P) : 0u;
-                for (uint32_t unit = wave; unit < units; unit += kExecWaves) {
-                    const uint32_t r = P == 1 ? unit : unit / P;
-                    const uint32_t q = P == 1 ? 0 : unit % P;
-                    const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
-                    const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
-                    const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo);
-                    const uint64_t rdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                    const uint32_t rn = uni(w0.z), rvalid = uni(w0.w);
-                    const uint32_t m0 = uni(w1.x), m1 = uni(w1.y), row = uni(w1.z), N = uni(w1.w);
-                    const uint32_t off = uni(w2.x);
-                    const uint32_t mix = m1 >> 24;
-                    const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
-                    const uint32_t pinfo = uni(info.x);
-                    if (pinfo < kPlanGeneral)
-                        continue;   // (phase B1a)
-#ifdef SGPU_PHASE_CLOCKS
-                    unsigned long long rclk = clock64();
-#endif
-                    // dst as kept (decoder rows) and the product's multiply table,
-                    // fetched before the terms stream in
-                    const uint32_t c0 = (P == 1 && tileBase < align16u(rn)) ? load_cur(p, rdst, rn, rvalid) : 0u;
-                    const GfTab mixTab = gf_tab_l(permL, permC, mix);
-                    uint32_t acc0 = 0, acc1 = 0;
-                    if (tileBase < align16u(rn)) {
-                        // dense part (part 0): the sums the opcodes select (bit
-                        // lane*3+s; mask1 feeds the product)
-                        if (q == 0) {
-                            uint64_t bits = (uint64_t)(m0 & 0xffffffu) | ((uint64_t)(m1 & 0xffffffu) << 24);
-                            gather<true>(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
-                                   [&](uint32_t, uint64_t& src, uint32_t& len, uint32_t& ca) {
-                                       const uint32_t b = (uint32_t)__builtin_ctzll(bits);
-                                       bits &= bits - 1;
-                                       const uint32_t k = b < kRowSums ? b : b - kRowSums;
-                                       lane_term(sumv, k, src, len);
-                                       ca = 1u | ((b >= kRowSums ? 1u : 0u) << 8);
-                                       return len != 0;
-                                   });
-                            // (the sums as of the row's cutoff, ops.h RowItem)
-                            if (r < Rv) {
-                                acc0 ^= corrL[r][0][lane];
-                                acc1 ^= corrL[r][1][lane];
-                            } else if (uni(w2.y) < updMaxLast1)
-                                row_versions4(m0 & 0xffffffu, m1 & 0xffffffu, uni(w2.y), tileBase, p, lane, updOfL, updFromL,
-                                          updToL, cxL, stage, stageLo, staged, tableL, seg, blk, acc0, acc1);
-                        }
-                        // sparse part: this unit's share of the 2*ceil(N/16) draws
-                        // (pairs stay whole: even draw -> row, odd -> product)
-                        if ((m0 & kRowWide) && q == 0) {
-                            // a wide row's k_ldpc sums L0 -> acc0, L1 -> acc1
-#pragma unroll
-                            for (uint32_t k = 0; k < 2; ++k) {
-                                const uint32_t e = off + k;
-                                uint32_t v = 0;
-                                if (e - stageLo < staged) {
-                                    v = stage[(kRowSums + e - stageLo) * 64 + lane];
-                                } else {
-                                    const uint4 ev = win_entry(tableL, seg, blk, e, stageLo);
-                                    const uint64_t src = ((uint64_t)uni(ev.y) << 32) | uni(ev.x);
-                                    const uint32_t len = uni(ev.z);
-                                    if (tileBase < len)
-                                        v = term_load(src, len, p);
-                                }
-                                if (k == 0)
-                                    acc0 ^= v;
+                    // update stores.  Update u's sum (SumUpdate.sum = k)
+                    // also refreshes stage slot k straight from registers when it is
+                    // the buffer the rows read and the stored bytes cover the staged
+                    // ones; anything else marks the stage stale and the sums are
+                    // re-read from memory after a barrier.
+                    for (uint32_t u = wave; u < U; u += kExecWaves) {
+                        const uint4 w0 = table_entry<Fit>(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords, stageLo);
+                        const uint4 w1 = table_entry<Fit>(tableL, seg, blk, updWord + u * kUpdateWords + 1 - kOpWords, stageLo);
+                        const uint64_t udst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                        const uint32_t un = uni(w0.z), uvalid = uni(w0.w) & 0x3fffffffu;
+                        if (tileBase >= align16u(un))
+                            continue;   // (this tile of the sum is unchanged, as staged)
+                        const uint32_t cu = u == wave ? scur : load_cur(p, udst, un, uvalid);
+                        const uint32_t out = item_value(updAcc[u * 64 + lane], p, un, uvalid, cu);
+                        if (p < align16u(un))
+                            st4(udst + p, out);
+                        // (slot k holds the buffer the rows read as sum k; an update of
+                        // another buffer -- the rows of this batch do not read the sum,
+                        // it grew after they took their table -- leaves it as staged)
+                        const uint32_t k = uni(w1.z);
+                        bool stale = k >= kRowSums;
+                        if (k < kRowSums && sumsStaged) {
+                            const uint4 d = tableL[k];
+                            const uint64_t src = ((uint64_t)uni(d.y) << 32) | uni(d.x);
+                            const uint32_t len = uni(d.z);
+                            if (src == udst) {
+                                // (exactly the sum's first `len` bytes, as the rows read
+                                // it: with versioned reads the update may have grown it)
+                                if (align16u(len) <= align16u(un))
+                                    stage[k * 64 + lane] = p < len ? out & byte_mask((int)len - (int)p) : 0u;
                                 else
-                                    acc1 ^= v;
+                                    stale = true;
                             }
                         }
-                        if (N != 0) {
-                            const uint32_t pairs = (N + kPairRate - 1) / kPairRate;
-                            const uint32_t d0 = 2 * (pairs * q / P), d1 = 2 * (pairs * (q + 1) / P);
-                            const uint32_t refBytes = row_picks(row, N, off, d0, d1, rn, tileBase, p, lane,
-                                                                c_pcgA[opaque(lane)], c_pcgG[opaque(lane)], stage, stageLo, staged, tableL, seg, blk, acc0, acc1);
-                            // (a planned row's draws were counted by its plan)
-                            if (pinfo == kNoPlan && tileBase == 0 && lane == 0 && refBytes)
-                                atomicAdd(&acctL, (unsigned long long)refBytes);
+                        if (stale && nPairs && lane == 0)   // (no plan: no row reads the stage)
+                            sumsDirty = 1;
+                    }
+                    __syncthreads();
+                    PHASE_MARK(3, tclk);
+                    if (tid == 0)
+                        PHASE_ADD(21, sumsDirty ? 1 : 0);
+                    if (sumsStaged && uni(sumsDirty)) {
+                        // (this workgroup's own stores, visible after the barrier)
+                        if (tid < kRowSums * 16) {
+                            const uint32_t k = tid / 16;
+                            const uint4 d = tableL[k];
+                            const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+                            uint4 v = make_uint4(0, 0, 0, 0);
+                            if (tileBase + q16 < d.z)
+                                v = mask16(ld16(src + tileBase + q16), (int)d.z - (int)(tileBase + q16));
+                            *reinterpret_cast<uint4*>(&stage[k * 64 + q16 / 4]) = v;
+                        }
+                        __syncthreads();
+                    }
+                    PHASE_MARK(4, tclk);
+                    if (ti + 1 < nTiles) {
+                        // the next tile's first kStagePre stage entries per thread, in
+                        // flight through this tile's rows (its bytes are untouched
+                        // until its own phases: every op is byte-column local)
+                        const uint32_t nb = tileBase + kExecTileBytes;
+#pragma unroll
+                        for (unsigned u = 0; u < kStagePre; ++u) {
+                            const uint32_t x = tid / 16 + u * kPass;
+                            pre[u] = make_uint4(0, 0, 0, 0);
+                            if (x < entries) {
+                                const uint4 d = table_word<Fit>(tableL, seg, blk, x < kRowSums ? x : x + stageLo, stageLo);
+                                const uint64_t src = ((uint64_t)d.y << 32) | d.x;
+                                if (nb + q16 < d.z)
+                                    pre[u] = ld16(src + nb + q16);
+                            }
                         }
                     }
-                    if (P > 1) {
-                        part[wave][0][lane] = acc0;
-                        part[wave][1][lane] = acc1;
-                    } else {
-                        if (tileBase < align16u(rn))
-                            store_item(acc0 ^ (mix > 1 ? gf_mul_tab(acc1, mixTab) : acc1), p, rdst, rn, rvalid, c0);
-                        PHASE_MARK(18, rclk);
-                        PHASE_ADD(23, 1);
-                        store_literal(p, rdst, rn, row_lit_len(m0), uni(w2.z), uni(w2.w));
-                        PHASE_MARK(22, rclk);
+
+                    // phase B1a: planned rows, four per wave at a time: quad g of the
+                    // wave (lanes 16g..16g+15) takes row 4t+g, and lane l holds bytes
+                    // 16*(l%16).. of the tile, so one 16-byte LDS read per lane moves
+                    // one term of each of four rows and every per-row step (the
+                    // descriptors, the RX product, the stores) is paid once per four
+                    // rows.
+                    {
+                        const uint32_t nq = (planned + 3) / 4;
+                        const uint32_t g = lane >> 4, b4 = (lane & 15u) * 4u;
+                        const uint32_t p16 = tileBase + (lane & 15u) * 16u;
+                        for (uint32_t task = wave; task < nq; task += kExecWaves) {
+#ifdef SGPU_PHASE_CLOCKS
+                            unsigned long long qclk = clock64();
+#endif
+                            const uint32_t r = task * 4 + g;
+                            const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
+                            const bool act = info.x < kPlanGeneral;
+                            if (!__any(act ? 1 : 0))
+                                continue;
+                            const uint4 z4 = make_uint4(0, 0, 0, 0);
+                            const uint4 w0 = act ? table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo) : z4;
+                            const uint4 w1 = act ? table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo) : z4;
+                            const uint4 w2 = act ? table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo) : z4;
+                            const uint64_t rdst = ((uint64_t)w0.y << 32) | w0.x;
+                            const uint32_t rn = w0.z, rvalid = w0.w;
+                            const uint32_t mix = w1.y >> 24;
+                            const bool live = act && tileBase < align16u(rn);
+                            // dst as kept (decoder rows), fetched before the terms stream in
+                            const uint4 cur = live ? load_cur16(p16, rdst, rn, rvalid) : z4;
+                            const GfTab tab = gf_tab_l(permL, permC, mix > 1 ? mix : 1u);
+                            const uint32_t off0 = info.x, n0 = live ? (info.y & 0xffffu) : 0u;
+                            const uint32_t off1 = info.x + (info.y & 0xffffu), n1 = live ? (info.y >> 16) : 0u;
+                            uint32_t most = n0 > n1 ? n0 : n1;
+                            most = max(most, (uint32_t)__shfl_xor(most, 16, 64));
+                            most = uni(max(most, (uint32_t)__shfl_xor(most, 32, 64)));
+                            PHASE_MARK(13, qclk);
+                            uint4 a0 = z4, a1 = z4;
+                            // 16 terms at a time: lane i of a quad reads plan entry
+                            // t+i of its row's lists, a row broadcast (DPP) hands
+                            // entry j to the whole quad, 4 terms of each list in flight
+                            // (no masking after the reads, so they go out together)
+                            for (uint32_t t = 0; t < most; t += 16) {
+                                const uint32_t i = t + (lane & 15u);
+                                // (entries past a list's end name the zero slot)
+                                const uint32_t s0 = i < n0 ? (uint32_t)plan[off0 + i] : zeroSlot;
+                                const uint32_t s1 = i < n1 ? (uint32_t)plan[off1 + i] : zeroSlot;
+                                const uint32_t left = most - t;   // (uniform)
+#define SGPU_QUAD_GROUP(J)                                                                                  \
+            {                                                                                                       \
+                const uint4 x0 = lds16(stage, row_bcast<(J)>(s0) * 64 + b4);                                        \
+                const uint4 x1 = lds16(stage, row_bcast<(J) + 1>(s0) * 64 + b4);                                    \
+                const uint4 x2 = lds16(stage, row_bcast<(J) + 2>(s0) * 64 + b4);                                    \
+                const uint4 x3 = lds16(stage, row_bcast<(J) + 3>(s0) * 64 + b4);                                    \
+                const uint4 y0 = lds16(stage, row_bcast<(J)>(s1) * 64 + b4);                                        \
+                const uint4 y1 = lds16(stage, row_bcast<(J) + 1>(s1) * 64 + b4);                                    \
+                const uint4 y2 = lds16(stage, row_bcast<(J) + 2>(s1) * 64 + b4);                                    \
+                const uint4 y3 = lds16(stage, row_bcast<(J) + 3>(s1) * 64 + b4);                                    \
+                a0 = xor16(xor16(a0, xor16(x0, x1)), xor16(x2, x3));                                                \
+                a1 = xor16(xor16(a1, xor16(y0, y1)), xor16(y2, y3));                                                \
+            }
+                                SGPU_QUAD_GROUP(0)
+                                if (left > 4)
+                                    SGPU_QUAD_GROUP(4)
+                                if (left > 8)
+                                    SGPU_QUAD_GROUP(8)
+                                if (left > 12)
+                                    SGPU_QUAD_GROUP(12)
+#undef SGPU_QUAD_GROUP
+                            }
+                            PHASE_MARK(14, qclk);
+                            // (rows read the sums as of their cutoff, ops.h RowItem)
+                            if (r < Rv) {
+                                a0 = xor16(a0, lds16(&corrL[r][0][0], b4));
+                                a1 = xor16(a1, lds16(&corrL[r][1][0], b4));
+                            }
+                            if (__any(act && r >= Rv && w2.y < updMaxLast1 ? 1 : 0)) {
+                                row_versions16<Fit>(w1.x & 0xffffffu, w1.y & 0xffffffu, w2.y, live && r >= Rv, p16, b4, updOfL, updFromL,
+                                               updToL, cxL, permL, permC, stage, stageLo, staged, tableL, seg, blk, a0, a1);
+                                PHASE_MARK(16, qclk);
+                                if (lane == 0)
+                                    PHASE_ADD(17, 1);
+                            }
+                            if (live)
+                                store_item16(xor16(a0, gf_mul16_tab(a1, tab)), p16, rdst, rn, rvalid, cur);
+                            if (act) {
+                                store_literal(p16, rdst, rn, row_lit_len(w1.x), w2.z, w2.w, 16);
+                            }
+                            PHASE_MARK(15, qclk);
+                        }
                     }
-                }
-                if (P > 1 && units) {
-                    __syncthreads();
-                    if (wave < units && wave % P == 0 &&
-                        !(wave / P < planned && uni(rowInfo[wave / P].x) < kPlanGeneral)) {
-                        const uint32_t r = wave / P;
-                        const uint4 w0 = table_entry(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
-                        const uint4 w1 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
-                        const uint4 w2 = table_entry(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo);
+
+                    // phase B1b: rows without a plan (a draw outside the staged
+                    // window, or past the plan's capacity).  R >= W: wave w takes rows
+                    // w, w+W, ...; R < W: row r's terms are split into P = W / R parts,
+                    // unit w = (w / P, w % P), and the parts meet in LDS.  They read
+                    // sums and undrawn-from-LDS picks from memory; lane j < 24 holds
+                    // sum entry j.
+                    const uint4 sumv = lane < kRowSums ? tableL[lane] : make_uint4(0, 0, 0, 0);
+                    const uint32_t P = R >= kExecWaves ? 1u : kExecWaves / R;
+                    const uint32_t units = (R > planned || uni(generalRows)) ? (P == 1 ? R : R * P) : 0u;
+                    for (uint32_t unit = wave; unit < units; unit += kExecWaves) {
+                        const uint32_t r = P == 1 ? unit : unit / P;
+                        const uint32_t q = P == 1 ? 0 : unit % P;
+                        const uint4 w0 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
+                        const uint4 w1 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
+                        const uint4 w2 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo);
                         const uint64_t rdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
                         const uint32_t rn = uni(w0.z), rvalid = uni(w0.w);
-                        const uint32_t m0 = uni(w1.x), mix = uni(w1.y) >> 24;
-                        uint32_t acc0 = 0, acc1 = 0;
-                        for (uint32_t k = 0; k < P; ++k) {
-                            acc0 ^= part[wave + k][0][lane];
-                            acc1 ^= part[wave + k][1][lane];
-                        }
-                        if (tileBase < align16u(rn)) {
-                            const uint32_t c0 = load_cur(p, rdst, rn, rvalid);
-                            store_item(acc0 ^ (mix > 1 ? gf_mul_dword(acc1, mix) : acc1), p, rdst, rn, rvalid, c0);
-                        }
-                        store_literal(p, rdst, rn, row_lit_len(m0), uni(w2.z), uni(w2.w));
-                    }
-                }
-                if (ti + 1 < nTiles)
-                    __syncthreads();   // (the stage, plans' readers and part[] turn over)
-            }
-            PHASE_MARK(5, tclk);
-            if (tid == 0) {
+                        const uint32_t m0 = uni(w1.x), m1 = uni(w1.y), row = uni(w1.z), N = uni(w1.w);
+                        const uint32_t off = uni(w2.x);
+                        const uint32_t mix = m1 >> 24;
+                        const uint2 info = r < planned ? rowInfo[r] : make_uint2(kNoPlan, 0u);
+                        const uint32_t pinfo = uni(info.x);
+                        if (pinfo < kPlanGeneral)
+                            continue;   // (phase B1a)
 #ifdef SGPU_PHASE_CLOCKS
-                t5 = clock64();
-                atomicAdd(&g_phaseClk[8], 1ull);
-                atomicAdd(&g_phaseClk[9], (unsigned long long)R);
-                atomicAdd(&g_phaseClk[10], (unsigned long long)U);
-                atomicAdd(&g_phaseClk[11], (unsigned long long)E);
-                atomicAdd(&g_phaseClk[12], (unsigned long long)staged);
+                        unsigned long long rclk = clock64();
 #endif
+                        // dst as kept (decoder rows) and the product's multiply table,
+                        // fetched before the terms stream in
+                        const uint32_t c0 = (P == 1 && tileBase < align16u(rn)) ? load_cur(p, rdst, rn, rvalid) : 0u;
+                        const GfTab mixTab = gf_tab_l(permL, permC, mix);
+                        uint32_t acc0 = 0, acc1 = 0;
+                        if (tileBase < align16u(rn)) {
+                            // dense part (part 0): the sums the opcodes select (bit
+                            // lane*3+s; mask1 feeds the product)
+                            if (q == 0) {
+                                uint64_t bits = (uint64_t)(m0 & 0xffffffu) | ((uint64_t)(m1 & 0xffffffu) << 24);
+                                gather<true>(0, (uint32_t)__builtin_popcountll(bits), tileBase, p, acc0, acc1,
+                                       [&](uint32_t, uint64_t& src, uint32_t& len, uint32_t& ca) {
+                                           const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+                                           bits &= bits - 1;
+                                           const uint32_t k = b < kRowSums ? b : b - kRowSums;
+                                           lane_term(sumv, k, src, len);
+                                           ca = 1u | ((b >= kRowSums ? 1u : 0u) << 8);
+                                           return len != 0;
+                                       });
+                                // (the sums as of the row's cutoff, ops.h RowItem)
+                                if (r < Rv) {
+                                    acc0 ^= corrL[r][0][lane];
+                                    acc1 ^= corrL[r][1][lane];
+                                } else if (uni(w2.y) < updMaxLast1)
+                                    row_versions4<Fit>(m0 & 0xffffffu, m1 & 0xffffffu, uni(w2.y), tileBase, p, lane, updOfL, updFromL,
+                                              updToL, cxL, stage, stageLo, staged, tableL, seg, blk, acc0, acc1);
+                            }
+                            // sparse part: this unit's share of the 2*ceil(N/16) draws
+                            // (pairs stay whole: even draw -> row, odd -> product)
+                            if ((m0 & kRowWide) && q == 0) {
+                                // a wide row's k_ldpc sums L0 -> acc0, L1 -> acc1
+#pragma unroll
+                                for (uint32_t k = 0; k < 2; ++k) {
+                                    const uint32_t e = off + k;
+                                    uint32_t v = 0;
+                                    if (e - stageLo < staged) {
+                                        v = stage[(kRowSums + e - stageLo) * 64 + lane];
+                                    } else {
+                                        const uint4 ev = win_entry<Fit>(tableL, seg, blk, e, stageLo);
+                                        const uint64_t src = ((uint64_t)uni(ev.y) << 32) | uni(ev.x);
+                                        const uint32_t len = uni(ev.z);
+                                        if (tileBase < len)
+                                            v = term_load(src, len, p);
+                                    }
+                                    if (k == 0)
+                                        acc0 ^= v;
+                                    else
+                                        acc1 ^= v;
+                                }
+                            }
+                            if (N != 0) {
+                                const uint32_t pairs = (N + kPairRate - 1) / kPairRate;
+                                const uint32_t d0 = 2 * (pairs * q / P), d1 = 2 * (pairs * (q + 1) / P);
+                                const uint32_t refBytes = row_picks<Fit>(row, N, off, d0, d1, rn, tileBase, p, lane,
+                                                                    c_pcgA[opaque(lane)], c_pcgG[opaque(lane)], stage, stageLo, staged, tableL, seg, blk, acc0, acc1);
+                                // (a planned row's draws were counted by its plan)
+                                if (pinfo == kNoPlan && tileBase == 0 && lane == 0 && refBytes)
+                                    atomicAdd(&acctL, (unsigned long long)refBytes);
+                            }
+                        }
+                        if (P > 1) {
+                            part[wave][0][lane] = acc0;
+                            part[wave][1][lane] = acc1;
+                        } else {
+                            if (tileBase < align16u(rn))
+                                store_item(acc0 ^ (mix > 1 ? gf_mul_tab(acc1, mixTab) : acc1), p, rdst, rn, rvalid, c0);
+                            PHASE_MARK(18, rclk);
+                            PHASE_ADD(23, 1);
+                            store_literal(p, rdst, rn, row_lit_len(m0), uni(w2.z), uni(w2.w));
+                            PHASE_MARK(22, rclk);
+                        }
+                    }
+                    if (P > 1 && units) {
+                        __syncthreads();
+                        if (wave < units && wave % P == 0 &&
+                            !(wave / P < planned && uni(rowInfo[wave / P].x) < kPlanGeneral)) {
+                            const uint32_t r = wave / P;
+                            const uint4 w0 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords - kOpWords, stageLo);
+                            const uint4 w1 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 1 - kOpWords, stageLo);
+                            const uint4 w2 = table_entry<Fit>(tableL, seg, blk, rowWord + r * kRowWords + 2 - kOpWords, stageLo);
+                            const uint64_t rdst = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                            const uint32_t rn = uni(w0.z), rvalid = uni(w0.w);
+                            const uint32_t m0 = uni(w1.x), mix = uni(w1.y) >> 24;
+                            uint32_t acc0 = 0, acc1 = 0;
+                            for (uint32_t k = 0; k < P; ++k) {
+                                acc0 ^= part[wave + k][0][lane];
+                                acc1 ^= part[wave + k][1][lane];
+                            }
+                            if (tileBase < align16u(rn)) {
+                                const uint32_t c0 = load_cur(p, rdst, rn, rvalid);
+                                store_item(acc0 ^ (mix > 1 ? gf_mul_dword(acc1, mix) : acc1), p, rdst, rn, rvalid, c0);
+                            }
+                            store_literal(p, rdst, rn, row_lit_len(m0), uni(w2.z), uni(w2.w));
+                        }
+                    }
+                    if (ti + 1 < nTiles)
+                        __syncthreads();   // (the stage, plans' readers and part[] turn over)
+                }
+                PHASE_MARK(5, tclk);
+                if (tid == 0) {
+#ifdef SGPU_PHASE_CLOCKS
+                    t5 = clock64();
+                    atomicAdd(&g_phaseClk[8], 1ull);
+                    atomicAdd(&g_phaseClk[9], (unsigned long long)R);
+                    atomicAdd(&g_phaseClk[10], (unsigned long long)U);
+                    atomicAdd(&g_phaseClk[11], (unsigned long long)E);
+                    atomicAdd(&g_phaseClk[12], (unsigned long long)(E - stageLo < stageCap ? E - stageLo : stageCap));
+#endif
+                }
+            };
+            {
+                const uint32_t lo = uni(h0.x) < valid ? uni(h0.x) : valid;   // (stageLo)
+                if (uni(h1.w) <= kRowsTableLds + lo)
+                    rows_op(std::true_type{});
+                else
+                    rows_op(std::false_type{});
             }
         } else if (kind == OP_LINCOMBS) {
             // independent combinations, whole items per wave: each wave

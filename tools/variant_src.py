@@ -19,12 +19,22 @@ src = os.path.join(ROOT, "siamese_amd", "csrc")
 dst = os.path.join(ROOT, "vbuild", name)   # (two levels down: the sources include ../../include)
 shutil.rmtree(dst, ignore_errors=True)
 shutil.copytree(src, dst)
-for f, old, new in runpy.run_path(spec)["PATCHES"]:
+specd = runpy.run_path(spec)
+for f, old, new in specd.get("PATCHES", []):
     p = os.path.join(dst, f)
     s = open(p).read()
     if old not in s:
         sys.exit("patch not found in %s: %r" % (f, old[:80]))
     open(p, "w").write(s.replace(old, new, 1))
+if "transform" in specd:
+    # transform(name, text) -> text, for every copied source file
+    for f in sorted(os.listdir(dst)):
+        p = os.path.join(dst, f)
+        if os.path.isfile(p):
+            s = open(p).read()
+            t = specd["transform"](f, s)
+            if t != s:
+                open(p, "w").write(t)
 obj = os.path.join(dst, "obj")
 os.makedirs(obj)
 procs = []
