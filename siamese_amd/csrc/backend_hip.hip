@@ -930,6 +930,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint32_t updOfL[kRowSums];
     __shared__ uint32_t updFromL[kRowSums], updToL[kRowSums];
     __shared__ uint32_t updMaxLast1;   // 1 + the last element any update of the batch folds in (0: none)
+    __shared__ uint32_t updSpanL;      // elements of the batch's longest update
     // the version corrections of the batch's first kVersionRows rows (this
     // tile, dword layout), computed per lane sum in phase A
     __shared__ uint32_t corrL[kVersionRows][2][64];
@@ -1099,6 +1100,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     // t loads 16 bytes of entry t/16 per pass, four passes in flight;
                     // bytes past an entry's length (absent elements: all of them)
                     // read zero.
+                    uint32_t span = 0;   // this sum's update: elements (lanes < 24 of wave 0)
                     if (ti == 0 && tid < kRowSums) {
                         // (at most one update per sum in a batch: Program::rows_update)
                         uint32_t found = 0xffu, from = 0, to = 0;
@@ -1113,6 +1115,15 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                         updOfL[tid] = found;
                         updFromL[tid] = from;
                         updToL[tid] = to;
+                        span = to > from ? (to - from + kLanes - 1) / kLanes : 0u;
+                    }
+                    if (ti == 0 && wave == 0) {
+                        // (the longest update's element count)
+#pragma unroll
+                        for (unsigned d = 32; d >= 1; d >>= 1)
+                            span = max(span, (uint32_t)__shfl_xor(span, d, 64));
+                        if (lane == 0)
+                            updSpanL = span;
                     }
                     const uint32_t staged = E - stageLo < stageCap ? E - stageLo : stageCap;
                     const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
@@ -1199,7 +1210,21 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     const uint32_t vTasks = Rv ? kRowSums / 4 : 0u;
                     const uint32_t vWaves = vTasks < kExecWaves ? vTasks : 0u;
                     const uint32_t W2 = kExecWaves - vWaves;
-                    const uint32_t Q = U == 0 ? 1u : (U >= W2 ? 1u : W2 / U);
+                    // updates split into Q parts each, Q chosen for the fewest
+                    // 16-element passes on the busiest wave (its parts of the
+                    // longest update)
+                    uint32_t Q = 1;
+                    if (U) {
+                        const uint32_t span = uni(updSpanL);   // (elements of the longest update)
+                        uint32_t best = 0xffffffffu;
+                        for (uint32_t q = 1; q <= 4; ++q) {
+                            const uint32_t cost = ((U * q + W2 - 1) / W2) * ((span + 16 * q - 1) / (16 * q));
+                            if (cost < best) {
+                                best = cost;
+                                Q = q;
+                            }
+                        }
+                    }
                     const uint32_t uUnits = U * Q;
                     const uint32_t nPairs = sumsStaged ? (planned + 1) / 2 : 0u;
                     // (the row plans are the same for every tile: drawn for the first)
@@ -1354,9 +1379,16 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                         for (unsigned j = 0; j < 4; ++j)
                                             v[j] = lds16(stage, slot[j] * 64 + b4);
                                         if (us != 0) {
+                                            // (the four tables read before any multiply: one
+                                            // LDS round trip, not four)
+                                            GfTab tb[4];
 #pragma unroll
                                             for (unsigned j = 0; j < 4; ++j)
-                                                v[j] = gf_mul16_tab(v[j], gf_tab_l(permL, permC, y[j]));
+                                                tb[j] = gf_tab_l(permL, permC, y[j]);
+                                            __builtin_amdgcn_sched_barrier(0);   // (keep the reads together)
+#pragma unroll
+                                            for (unsigned j = 0; j < 4; ++j)
+                                                v[j] = gf_mul16_tab(v[j], tb[j]);
                                         }
                                         a = xor16(xor16(a, xor16(v[0], v[1])), xor16(v[2], v[3]));
                                     }
@@ -1842,33 +1874,46 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 }
             }
         } else if (kind == OP_COPIES) {
-            // kCopyBatch copies per wave at a time, all their loads in flight
-            // before the first store; sources carry their zero tails
-            constexpr unsigned kCopyBatch = 4;
+            // kCopyBatch copies per wave at a time over kCopyTiles tiles, all
+            // their loads in flight before the first store; sources carry
+            // their zero tails
+            constexpr unsigned kCopyBatch = 4, kCopyTiles = 4;
             for (uint32_t k0 = wave * kCopyBatch; k0 < n; k0 += kExecWaves * kCopyBatch) {
-                for (uint32_t ti = 0; ti < nTiles; ++ti) {
-                    const uint32_t p = tile0 + ti * kExecTileBytes + lane * 4;
-                    uint64_t d[kCopyBatch];
-                    uint32_t l[kCopyBatch], v[kCopyBatch];
+                uint64_t d[kCopyBatch], sr[kCopyBatch];
+                uint32_t l[kCopyBatch];
 #pragma unroll
-                    for (unsigned u = 0; u < kCopyBatch; ++u) {
-                        l[u] = 0;
-                        v[u] = 0;
-                        if (k0 + u < n) {
-                            const uint4 w0 = op_word(rb, seg, pos, kOpWords + (k0 + u) * kCopyWords);
-                            const uint4 w1 = op_word(rb, seg, pos, kOpWords + (k0 + u) * kCopyWords + 1);
-                            d[u] = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
-                            const uint64_t s = ((uint64_t)uni(w0.w) << 32) | uni(w0.z);
-                            l[u] = uni(w1.x);
-                            v[u] = term_load(s, l[u], p);
-                        }
+                for (unsigned u = 0; u < kCopyBatch; ++u) {
+                    d[u] = sr[u] = 0;
+                    l[u] = 0;
+                    if (k0 + u < n) {
+                        const uint4 w0 = op_word(rb, seg, pos, kOpWords + (k0 + u) * kCopyWords);
+                        const uint4 w1 = op_word(rb, seg, pos, kOpWords + (k0 + u) * kCopyWords + 1);
+                        d[u] = ((uint64_t)uni(w0.y) << 32) | uni(w0.x);
+                        sr[u] = ((uint64_t)uni(w0.w) << 32) | uni(w0.z);
+                        l[u] = uni(w1.x);
+                    }
+                }
+                for (uint32_t t0 = 0; t0 < nTiles; t0 += kCopyTiles) {
+                    uint32_t v[kCopyTiles][kCopyBatch];
+#pragma unroll
+                    for (unsigned t = 0; t < kCopyTiles; ++t) {
+                        const uint32_t p = tile0 + (t0 + t) * kExecTileBytes + lane * 4;
+#pragma unroll
+                        for (unsigned u = 0; u < kCopyBatch; ++u)
+                            v[t][u] = t0 + t < nTiles ? term_load(sr[u], l[u], p) : 0u;
                     }
 #pragma unroll
-                    for (unsigned u = 0; u < kCopyBatch; ++u) {
-                        if (p < l[u])
-                            st4(d[u] + p, v[u] & byte_mask((int)l[u] - (int)p));
-                        else if (p < align16u(l[u]))
-                            st4(d[u] + p, 0u);
+                    for (unsigned t = 0; t < kCopyTiles; ++t) {
+                        const uint32_t p = tile0 + (t0 + t) * kExecTileBytes + lane * 4;
+                        if (t0 + t >= nTiles)
+                            break;
+#pragma unroll
+                        for (unsigned u = 0; u < kCopyBatch; ++u) {
+                            if (p < l[u])
+                                st4(d[u] + p, v[t][u] & byte_mask((int)l[u] - (int)p));
+                            else if (p < align16u(l[u]))
+                                st4(d[u] + p, 0u);
+                        }
                     }
                 }
             }
