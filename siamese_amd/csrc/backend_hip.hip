@@ -134,6 +134,18 @@ __device__ __forceinline__ uint4 xor16(uint4 a, uint4 b)
     return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
 }
 
+// a ^ b ^ c ^ d ^ e: two full-rate v_bitop3_b32 (0x96, three-way XOR) per
+// dword instead of four XORs
+__device__ __forceinline__ uint32_t xor5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e)
+{
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(a, b, c, 0x96), d, e, 0x96);
+}
+__device__ __forceinline__ uint4 xor5_16(uint4 a, uint4 b, uint4 c, uint4 d, uint4 e)
+{
+    return make_uint4(xor5(a.x, b.x, c.x, d.x, e.x), xor5(a.y, b.y, c.y, d.y, e.y), xor5(a.z, b.z, c.z, d.z, e.z),
+                      xor5(a.w, b.w, c.w, d.w, e.w));
+}
+
 __device__ __forceinline__ uint4 ld16(uint64_t addr)
 {
     const u32x4 r = *reinterpret_cast<const GMEM u32x4*>(addr);
@@ -497,7 +509,8 @@ template <unsigned K>
 __device__ __forceinline__ uint32_t row_bcast(uint32_t v)
 {
     static_assert(K < 16, "row lane");
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + K, 0xf, 0xf, false);
+    // (row_newbcast fills every lane: no old value to materialise)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + K, 0xf, 0xf, true);
 }
 
 // the four quads (16-lane groups) of a wave hold partial sums of one tile:
@@ -1390,7 +1403,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                             for (unsigned j = 0; j < 4; ++j)
                                                 v[j] = gf_mul16_tab(v[j], tb[j]);
                                         }
-                                        a = xor16(xor16(a, xor16(v[0], v[1])), xor16(v[2], v[3]));
+                                        a = xor5_16(a, v[0], v[1], v[2], v[3]);
                                     }
                                     atomicXor(&updAcc[u * 64 + b4 + 0], a.x);
                                     atomicXor(&updAcc[u * 64 + b4 + 1], a.y);
@@ -1656,8 +1669,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 const uint4 y1 = lds16(stage, row_bcast<(J) + 1>(s1) * 64 + b4);                                    \
                 const uint4 y2 = lds16(stage, row_bcast<(J) + 2>(s1) * 64 + b4);                                    \
                 const uint4 y3 = lds16(stage, row_bcast<(J) + 3>(s1) * 64 + b4);                                    \
-                a0 = xor16(xor16(a0, xor16(x0, x1)), xor16(x2, x3));                                                \
-                a1 = xor16(xor16(a1, xor16(y0, y1)), xor16(y2, y3));                                                \
+                a0 = xor5_16(a0, x0, x1, x2, x3);                                                                   \
+                a1 = xor5_16(a1, y0, y1, y2, y3);                                                                   \
             }
                                 SGPU_QUAD_GROUP(0)
                                 if (left > 4)
