@@ -114,6 +114,38 @@ __device__ __forceinline__ uint4 gf_mul16_tab(uint4 v, const GfTab& t)
     return make_uint4(gf_mul_tab(v.x, t), gf_mul_tab(v.y, t), gf_mul_tab(v.z, t), gf_mul_tab(v.w, t));
 }
 
+// A source row's 16 bytes split into the three bit groups gf_mul_tab looks
+// up, once per pivot step instead of once per row update
+// (k_solve_main 295 -> 270 us per C4 launch; profiles/r3k_solve_ab.txt)
+struct Split16
+{
+    uint32_t a[4], b[4], c[4];
+};
+
+__device__ __forceinline__ Split16 gf_split16(uint4 v)
+{
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    Split16 s;
+#pragma unroll
+    for (unsigned k = 0; k < 4; ++k) {
+        s.a[k] = w[k] & 0x07070707u;
+        s.b[k] = (w[k] >> 3) & 0x07070707u;
+        s.c[k] = (w[k] >> 6) & 0x03030303u;
+    }
+    return s;
+}
+
+__device__ __forceinline__ uint4 gf_mul16_split(const Split16& s, const GfTab& t)
+{
+    uint32_t r[4];
+#pragma unroll
+    for (unsigned k = 0; k < 4; ++k)
+        r[k] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t.a1, t.a0, s.a[k]),
+                                           __builtin_amdgcn_perm(t.b1, t.b0, s.b[k]),
+                                           __builtin_amdgcn_perm(0u, t.c, s.c[k]), 0x96);
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
 __device__ __forceinline__ uint32_t byte_mask(int n)
 {
     // mask of the low n bytes of a dword, n clamped to [0,4]
@@ -944,6 +976,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     __shared__ uint32_t updFromL[kRowSums], updToL[kRowSums];
     __shared__ uint32_t updMaxLast1;   // 1 + the last element any update of the batch folds in (0: none)
     __shared__ uint32_t updSpanL;      // elements of the batch's longest update
+    __shared__ uint32_t laneModeL;     // updates folded per window lane (see phase A)
     // the version corrections of the batch's first kVersionRows rows (this
     // tile, dword layout), computed per lane sum in phase A
     __shared__ uint32_t corrL[kVersionRows][2][64];
@@ -1114,9 +1147,11 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     // bytes past an entry's length (absent elements: all of them)
                     // read zero.
                     uint32_t span = 0;   // this sum's update: elements (lanes < 24 of wave 0)
+                    const uint32_t staged = E - stageLo < stageCap ? E - stageLo : stageCap;
+                    uint32_t from = 0, to = 0, usv = 0xffu;   // sum tid's update (lanes < 24 of wave 0)
                     if (ti == 0 && tid < kRowSums) {
                         // (at most one update per sum in a batch: Program::rows_update)
-                        uint32_t found = 0xffu, from = 0, to = 0;
+                        uint32_t found = 0xffu;
                         for (uint32_t u = 0; u < U; ++u) {
                             const uint4 w1 = table_entry<Fit>(tableL, seg, blk, kRowSums + E + u * kUpdateWords + 1, stageLo);
                             if (w1.z == tid && w1.y > w1.x) {
@@ -1125,6 +1160,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                 to = w1.y;
                             }
                         }
+                        if (found != 0xffu)
+                            usv = table_entry<Fit>(tableL, seg, blk, kRowSums + E + found * kUpdateWords, stageLo).w >> 30;
                         updOfL[tid] = found;
                         updFromL[tid] = from;
                         updToL[tid] = to;
@@ -1132,13 +1169,28 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     }
                     if (ti == 0 && wave == 0) {
                         // (the longest update's element count)
+                        uint32_t m = span;
 #pragma unroll
                         for (unsigned d = 32; d >= 1; d >>= 1)
-                            span = max(span, (uint32_t)__shfl_xor(span, d, 64));
-                        if (lane == 0)
-                            updSpanL = span;
+                            m = max(m, (uint32_t)__shfl_xor(m, d, 64));
+                        // Lane mode: the three sums of every window lane l (k =
+                        // 3l + s, coefficient 1 / CX / CX^2) are updated over one
+                        // element range, all staged, or none of them is; each
+                        // element is then read and split for the multiplies once
+                        // for its three sums (a block-mode encoder's or decoder's
+                        // batch)
+                        const uint32_t k0 = lane < kRowSums ? lane - lane % kSums : 0u;
+                        const uint32_t f0 = __shfl(from, k0, 64), t0 = __shfl(to, k0, 64);
+                        const bool has = span != 0, has0 = __shfl(span, k0, 64) != 0;
+                        bool ok = lane >= kRowSums ||
+                                  (has == has0 && (!has || (from == f0 && to == t0 && usv == lane % kSums && from >= stageLo &&
+                                                            from + (to - from - 1) / kLanes * kLanes - stageLo < staged)));
+                        ok = __all(ok ? 1 : 0) != 0;
+                        if (lane == 0) {
+                            updSpanL = m;
+                            laneModeL = (ok && m) ? 1u : 0u;
+                        }
                     }
-                    const uint32_t staged = E - stageLo < stageCap ? E - stageLo : stageCap;
                     const uint32_t q16 = (tid & 15u) * 16u;         // byte within the tile
                     const bool sumsStaged = stageSlots >= kRowSums;
                     const uint32_t updWord = kOpWords + T;
@@ -1226,19 +1278,21 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                     // updates split into Q parts each, Q chosen for the fewest
                     // 16-element passes on the busiest wave (its parts of the
                     // longest update)
+                    const bool laneMode = uni(laneModeL) != 0;
+                    const uint32_t UL = laneMode ? (uint32_t)kLanes : U;   // update units before the split
                     uint32_t Q = 1;
-                    if (U) {
+                    if (UL) {
                         const uint32_t span = uni(updSpanL);   // (elements of the longest update)
                         uint32_t best = 0xffffffffu;
                         for (uint32_t q = 1; q <= 4; ++q) {
-                            const uint32_t cost = ((U * q + W2 - 1) / W2) * ((span + 16 * q - 1) / (16 * q));
+                            const uint32_t cost = ((UL * q + W2 - 1) / W2) * ((span + 16 * q - 1) / (16 * q));
                             if (cost < best) {
                                 best = cost;
                                 Q = q;
                             }
                         }
                     }
-                    const uint32_t uUnits = U * Q;
+                    const uint32_t uUnits = UL * Q;
                     const uint32_t nPairs = sumsStaged ? (planned + 1) / 2 : 0u;
                     // (the row plans are the same for every tile: drawn for the first)
                     const uint32_t nUnits = vTasks + uUnits + (ti == 0 ? nPairs : 0u);
@@ -1357,6 +1411,70 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             }
                             PHASE_ADD(26, PHASE_CLK() - vclk0);
                             PHASE_ADD(29, 1);
+                        } else if (unit < uUnits && laneMode) {
+                            [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
+                            // part unit%Q of window lane l's three sums: each element is
+                            // read and split once, then XORed into sum 3l and
+                            // multiplied by its column's CX / CX^2 into 3l+1 / 3l+2
+                            // (SiameseEncoder.cpp:359-418; all staged: lane mode)
+                            const uint32_t l = unit / Q, uq = unit % Q;
+                            const uint32_t ua = uni(updOfL[kSums * l]), ub = uni(updOfL[kSums * l + 1]),
+                                           uc = uni(updOfL[kSums * l + 2]);
+                            const uint32_t from = uni(updFromL[kSums * l]), to = uni(updToL[kSums * l]);
+                            const uint32_t total = to > from ? (to - from + kLanes - 1) / kLanes : 0;
+                            const uint32_t k0 = total * uq / Q, k1 = total * (uq + 1) / Q;
+                            if (ua != 0xffu && k0 < k1) {
+                                auto live = [&](uint32_t u) {
+                                    return tileBase <
+                                           align16u(uni(table_entry<Fit>(tableL, seg, blk, updWord + u * kUpdateWords - kOpWords,
+                                                                         stageLo).z));
+                                };
+                                const bool la = live(ua), lb = live(ub), lc = live(uc);
+                                if (la || lb || lc) {
+                                    uint32_t refBytes = 0;
+                                    uint4 A0 = make_uint4(0, 0, 0, 0), A1 = A0, A2 = A0;
+                                    for (uint32_t kk = k0; kk < k1; kk += 4) {
+                                        const uint32_t k = kk + g;
+                                        const bool act = k < k1;
+                                        const uint32_t e = from + (act ? k : k0) * kLanes;
+                                        const uint4 ev = win_entry<Fit>(tableL, seg, blk, e, stageLo);
+                                        if (act && (lane & 15u) == 0)
+                                            refBytes += ev.z;
+                                        const uint32_t cx = cxL[ev.w % kColumnValuePeriod];   // CX | CX^2 << 8
+                                        const uint4 v = lds16(stage, (act ? kRowSums + e - stageLo : zeroSlot) * 64 + b4);
+                                        const GfTab t1 = gf_tab_l(permL, permC, cx & 0xffu);
+                                        const GfTab t2 = gf_tab_l(permL, permC, cx >> 8);
+                                        const Split16 sp = gf_split16(v);
+                                        A0 = xor16(A0, v);
+                                        A1 = xor16(A1, gf_mul16_split(sp, t1));
+                                        A2 = xor16(A2, gf_mul16_split(sp, t2));
+                                    }
+                                    // (the quads hold different elements: each adds its share)
+                                    if (la) {
+                                        atomicXor(&updAcc[ua * 64 + b4 + 0], A0.x);
+                                        atomicXor(&updAcc[ua * 64 + b4 + 1], A0.y);
+                                        atomicXor(&updAcc[ua * 64 + b4 + 2], A0.z);
+                                        atomicXor(&updAcc[ua * 64 + b4 + 3], A0.w);
+                                    }
+                                    if (lb) {
+                                        atomicXor(&updAcc[ub * 64 + b4 + 0], A1.x);
+                                        atomicXor(&updAcc[ub * 64 + b4 + 1], A1.y);
+                                        atomicXor(&updAcc[ub * 64 + b4 + 2], A1.z);
+                                        atomicXor(&updAcc[ub * 64 + b4 + 3], A1.w);
+                                    }
+                                    if (lc) {
+                                        atomicXor(&updAcc[uc * 64 + b4 + 0], A2.x);
+                                        atomicXor(&updAcc[uc * 64 + b4 + 1], A2.y);
+                                        atomicXor(&updAcc[uc * 64 + b4 + 2], A2.z);
+                                        atomicXor(&updAcc[uc * 64 + b4 + 3], A2.w);
+                                    }
+                                    // (reference bytes: one add / muladd per original and sum)
+                                    if (tileBase == 0)
+                                        acct_wave(&acctL, refBytes * ((la ? 1u : 0u) + (lb ? 1u : 0u) + (lc ? 1u : 0u)));
+                                }
+                            }
+                            PHASE_ADD(19, PHASE_CLK() - uclk0);
+                            PHASE_ADD(27, 1);
                         } else if (unit < uUnits) {
                             [[maybe_unused]] const unsigned long long uclk0 = PHASE_CLK();
                             const uint32_t u = unit / Q;
@@ -2288,38 +2406,6 @@ __host__ __device__ constexpr uint32_t solve_lds_bytes(uint32_t m, bool prefix =
 {
     return m * 1024u + ((m * m + 15u) & ~15u) + ((m * 12u + (m + 1u) * 4u + 15u) & ~15u) +
            (prefix ? 256u * 20u : 0u);
-}
-
-// A source row's 16 bytes split into the three bit groups gf_mul_tab looks
-// up, once per pivot step instead of once per row update
-// (k_solve_main 295 -> 270 us per C4 launch; profiles/r3k_solve_ab.txt)
-struct Split16
-{
-    uint32_t a[4], b[4], c[4];
-};
-
-__device__ __forceinline__ Split16 gf_split16(uint4 v)
-{
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    Split16 s;
-#pragma unroll
-    for (unsigned k = 0; k < 4; ++k) {
-        s.a[k] = w[k] & 0x07070707u;
-        s.b[k] = (w[k] >> 3) & 0x07070707u;
-        s.c[k] = (w[k] >> 6) & 0x03030303u;
-    }
-    return s;
-}
-
-__device__ __forceinline__ uint4 gf_mul16_split(const Split16& s, const GfTab& t)
-{
-    uint32_t r[4];
-#pragma unroll
-    for (unsigned k = 0; k < 4; ++k)
-        r[k] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t.a1, t.a0, s.a[k]),
-                                           __builtin_amdgcn_perm(t.b1, t.b0, s.b[k]),
-                                           __builtin_amdgcn_perm(0u, t.c, s.c[k]), 0x96);
-    return make_uint4(r[0], r[1], r[2], r[3]);
 }
 
 __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow* __restrict__ R,
