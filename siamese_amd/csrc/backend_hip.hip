@@ -2998,13 +2998,29 @@ constexpr unsigned kTrStep = kTrWaves * kTrSplit;       // output row stride of 
 constexpr unsigned kTrThreads = 64 * kTrWaves;
 constexpr uint32_t kTrTableBytes = SGPU_TR_LDS_TABLES ? 256u * 20u : 0u;
 
-__host__ __device__ constexpr uint32_t solve_tr_lds_bytes(uint32_t m) { return kTrTableBytes + m * 1024u; }
+// A workgroup takes half of a (solve, 1 KiB tile): m x 512 bytes of LDS, so
+// the launch's largest solve (m <= 120) still leaves room for two or more
+// workgroups per CU (a whole tile per workgroup, m KiB, ran one per CU:
+// 512 workgroups in two rounds at 2 waves per SIMD)
+constexpr unsigned kTrHalves = 2;
+__host__ __device__ constexpr uint32_t solve_tr_lds_bytes(uint32_t m) { return kTrTableBytes + m * (1024u / kTrHalves); }
+
+// a row's bytes in this workgroup's half tile: two dwords per lane
+using TrRow = uint2;
+__device__ __forceinline__ TrRow tr_row(const uint32_t (&v)[4]) { return make_uint2(v[0], v[1]); }
+__device__ __forceinline__ void tr_unrow(TrRow r, uint32_t (&v)[4])
+{
+    v[0] = r.x;
+    v[1] = r.y;
+    v[2] = v[3] = 0;
+}
 
 template <unsigned NQ, unsigned RW>
 __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRow* __restrict__ R,
                                               uint32_t* res, uint32_t tileBase,
                                               uint4* __restrict__ X)
 {
+    static_assert(NQ <= 4 / kTrHalves, "a workgroup's quarters of the tile");
     const uint32_t m = sd.m, tid = threadIdx.x, lane = tid & 63, wave = uni(tid >> 6);
 #if SGPU_TR_LDS_TABLES
     const uint4* permL = X;
@@ -3016,6 +3032,7 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
     }
     X += 256 + 64;
 #endif
+    TrRow* XR = reinterpret_cast<TrRow*>(X);
     // the tile of every row, bytes past a row's initial length as zero
     for (uint32_t j = wave; j < m; j += kTrWaves) {
         const uint64_t buf = R[j].buf;
@@ -3027,12 +3044,12 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
             if (p < ib)
                 v[q] = ld4(buf + p) & byte_mask((int)ib - (int)p);
         }
-        X[j * 64u + lane] = make_uint4(v[0], v[1], v[2], v[3]);
+        XR[j * 64u + lane] = tr_row(v);
     }
     // this wave's rows of T (lane l < 32: bytes 4 l .. 4 l + 3 of each)
     // output rows r0 + kTrStep t of this wave (kTrSplit workgroups share a
     // tile, each its own rows)
-    const uint32_t r0 = wave + kTrWaves * (kTrSplit > 1 ? blockIdx.x % kTrSplit : 0u);
+    const uint32_t r0 = wave + kTrWaves * (kTrSplit > 1 ? (blockIdx.x / kTrHalves) % kTrSplit : 0u);
     const uint32_t rw = r0 < m ? (m - r0 + kTrStep - 1) / kTrStep : 0;
     uint32_t trow[RW];
 #pragma unroll
@@ -3055,8 +3072,8 @@ __device__ __forceinline__ void solve_tr_tile(const SolveDesc& sd, const SolveRo
             tw[t] = rl(trow[t], k0 >> 2);   // T[r_t][k0 .. k0 + 3]
         const uint32_t kn = m - k0 < 4 ? m - k0 : 4;
         for (uint32_t kk = 0; kk < kn; ++kk) {
-            const uint4 s4 = X[(k0 + kk) * 64u + lane];
-            const uint32_t sv[4] = {s4.x, s4.y, s4.z, s4.w};
+            uint32_t sv[4];
+            tr_unrow(XR[(k0 + kk) * 64u + lane], sv);
             uint32_t sa[NQ], sb[NQ], sc[NQ];
 #pragma unroll
             for (unsigned q = 0; q < NQ; ++q) {
@@ -3153,23 +3170,20 @@ __global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __rest
                                                          const SolveItem* __restrict__ items)
 {
     extern __shared__ uint4 X[];
-    const SolveItem it = items[blockIdx.x / kTrSplit];
+    const SolveItem it = items[blockIdx.x / (kTrSplit * kTrHalves)];
     const SolveDesc sd = solves[it.solve];
+    const uint32_t tileBase = it.tileBase + (blockIdx.x % kTrHalves) * (1024u / kTrHalves);
     if (sd.m == 0 || sd.m > kProductMaxRows || sd.tinv == 0 || results[sd.result] != sd.m ||
-        it.tileBase >= sd.maxBytes)
+        tileBase >= sd.maxBytes)
         return;   // (uniform: k_solve_main solves it)
-    const uint32_t left = sd.maxBytes - it.tileBase;
-    const uint32_t nq = left >= 768u ? 4u : (left + 255u) / 256u;
+    const uint32_t left = sd.maxBytes - tileBase;
+    const uint32_t nq = left >= 256u ? 2u : 1u;   // (quarters of this half)
     const SolveRow* R = rows + sd.rowBegin;
     uint32_t* res = results + sd.result;
-    if (nq == 4)
-        solve_tr_rows<4>(sd, R, res, it.tileBase, X);
-    else if (nq == 3)
-        solve_tr_rows<3>(sd, R, res, it.tileBase, X);
-    else if (nq == 2)
-        solve_tr_rows<2>(sd, R, res, it.tileBase, X);
+    if (nq == 2)
+        solve_tr_rows<2>(sd, R, res, tileBase, X);
     else
-        solve_tr_rows<1>(sd, R, res, it.tileBase, X);
+        solve_tr_rows<1>(sd, R, res, tileBase, X);
 }
 
 // ---------------------------------------------------------------------------
@@ -3905,7 +3919,7 @@ void launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* 
     if (tr) {
         hipLaunchKernelGGL(k_solve_pre, dim3(2 * solveCount), dim3(kPreThreads), (size_t)solve_pre_lds_bytes(rowsCap),
                            g_stream, solves + solveBegin, rows, coef, results, acctL, solveCount, 0u);
-        hipLaunchKernelGGL(k_solve_tr, dim3(count * kTrSplit), dim3(kTrThreads), (size_t)solve_tr_lds_bytes(prodCap),
+        hipLaunchKernelGGL(k_solve_tr, dim3(count * kTrSplit * kTrHalves), dim3(kTrThreads), (size_t)solve_tr_lds_bytes(prodCap),
                            g_stream, solves, rows, results, items);
     } else if (separate) {
         hipLaunchKernelGGL(k_solve_prefix, dim3(solveCount), dim3(64), (size_t)solve_prefix_lds_bytes(rowsCap),

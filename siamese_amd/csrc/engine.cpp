@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstddef>
 #include <cstdlib>
@@ -1931,7 +1932,6 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         for (size_t k = 0; k < maxSegs; ++k) {
             Phase ex{Phase::EXEC, nItems, 0, 0, 0, kNoRows};
             const size_t segBegin = segs.size();
-            size_t phaseTiles = 0;
             for (ProgramBody* p : bt.bodies[g]) {
                 if (k >= p->nsegs)
                     continue;
@@ -1946,7 +1946,6 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 nOps += s.ops.size();
                 nTerms += s.terms.size();
                 nWords += words;
-                phaseTiles += (s.maxExtent + kExecTileBytes - 1) / kExecTileBytes;
             }
 #if SGPU_EXEC_LPT
             // Longest op lists first: workgroups are dispatched in blockIdx
@@ -1957,18 +1956,31 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
 #endif
             {
                 // Runs of a segment's tiles per workgroup once the launch has
-                // more tiles than the chip runs at once: a workgroup then
+                // more work than the chip runs at once: a workgroup then
                 // loads each OP_ROWS table and draws its row plans once for
                 // all of its tiles (a single stream's few tiles stay spread
-                // over as many workgroups)
-                const size_t tpi = std::min<size_t>(
-                    0xffff, std::max<size_t>(1, (phaseTiles + SGPU_EXEC_GROUPS - 1) / SGPU_EXEC_GROUPS));
+                // over as many workgroups).
+                // Runs only for segments with row batches (their tables and
+                // plans are what a run shares), and no longer than keeps the
+                // segment's workgroup within the launch's average load per
+                // workgroup slot (op-stream words as the per-tile work): a
+                // heavy segment among light ones (a C2 decode beside one-row
+                // encodes) keeps its tiles on separate workgroups, or it
+                // becomes the launch's tail (C2 k_exec 4.26 vs 10.7 ms per
+                // run with uniform runs, tools/leg_ab.sh)
+                double load = 0;   // tile-words per workgroup slot
+                for (size_t i = segBegin; i < segs.size(); ++i)
+                    load += (double)((segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes) * segs[i].words;
+                load /= SGPU_EXEC_GROUPS;
                 uint32_t ib = (uint32_t)ex.itemBegin;
                 for (size_t i = segBegin; i < segs.size(); ++i) {
                     const size_t tiles = (segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes;
+                    size_t run = 1;
+                    if (segs[i].seg->rowsWords && segs[i].words)
+                        run = std::min<size_t>(0xffff, std::max<size_t>(1, (size_t)std::ceil(load / segs[i].words)));
                     segs[i].itemBase = ib;
-                    segs[i].tilesPerItem = (uint32_t)tpi;
-                    ib += (uint32_t)((tiles + tpi - 1) / tpi);
+                    segs[i].tilesPerItem = (uint32_t)run;
+                    ib += (uint32_t)((tiles + run - 1) / run);
                 }
                 nItems = ib;
             }
