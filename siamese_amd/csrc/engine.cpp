@@ -1961,23 +1961,30 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 // all of its tiles (a single stream's few tiles stay spread
                 // over as many workgroups).
                 // Runs only for segments with row batches (their tables and
-                // plans are what a run shares), and no longer than keeps the
-                // segment's workgroup within the launch's average load per
-                // workgroup slot (op-stream words as the per-tile work): a
-                // heavy segment among light ones (a C2 decode beside one-row
-                // encodes) keeps its tiles on separate workgroups, or it
-                // becomes the launch's tail (C2 k_exec 4.26 vs 10.7 ms per
-                // run with uniform runs, tools/leg_ab.sh)
-                double load = 0;   // tile-words per workgroup slot
-                for (size_t i = segBegin; i < segs.size(); ++i)
-                    load += (double)((segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes) * segs[i].words;
-                load /= SGPU_EXEC_GROUPS;
+                // plans are what a run shares), of tpi tiles when the launch
+                // has more tiles than workgroup slots; a segment much heavier
+                // than the launch's average (op-stream words as the per-tile
+                // work: a C2 decode beside one-row encodes) gets a shorter
+                // run, or it becomes the launch's tail (C2 k_exec 4.25 vs
+                // 10.7 ms per run with uniform runs, tools/leg_ab.sh)
+                size_t phaseTiles = 0;
+                double words = 0;
+                for (size_t i = segBegin; i < segs.size(); ++i) {
+                    const size_t t = (segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes;
+                    phaseTiles += t;
+                    words += (double)t * segs[i].words;
+                }
+                const double avg = phaseTiles ? words / (double)phaseTiles : 0.0;   // words per tile
+                const size_t tpi = std::min<size_t>(
+                    0xffff, std::max<size_t>(1, (phaseTiles + SGPU_EXEC_GROUPS - 1) / SGPU_EXEC_GROUPS));
                 uint32_t ib = (uint32_t)ex.itemBegin;
                 for (size_t i = segBegin; i < segs.size(); ++i) {
                     const size_t tiles = (segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes;
                     size_t run = 1;
-                    if (segs[i].seg->rowsWords && segs[i].words)
-                        run = std::min<size_t>(0xffff, std::max<size_t>(1, (size_t)std::ceil(load / segs[i].words)));
+                    if (segs[i].seg->rowsWords && tpi > 1) {
+                        const double heavy = segs[i].words / (2.0 * avg);
+                        run = heavy > 1.0 ? std::max<size_t>(1, (size_t)((double)tpi / heavy)) : tpi;
+                    }
                     segs[i].itemBase = ib;
                     segs[i].tilesPerItem = (uint32_t)run;
                     ib += (uint32_t)((tiles + run - 1) / run);
