@@ -2862,6 +2862,47 @@ __host__ __device__ constexpr uint32_t solve_pre_lds_bytes(uint32_t m)
                : solve_tbuild_lds_bytes(m < kProductMaxRows ? m : kProductMaxRows);
 }
 
+// One T-build step's row updates: rows j in [j0, j1) (this half-wave's,
+// stride kPreThreads / 32) take Y_j ^= Ct[c0 + j] a ^ Ct[c1 + j] b.  Four
+// rows at a time with every LDS read of the four issued before any product,
+// and the two sources' multiply fields split once: the rows' chains overlap
+// instead of running one LDS round trip after another.
+__device__ __forceinline__ void tbuild_rows(uint32_t* Yw, const uint8_t* Ct, const uint4* permL, const uint32_t* permC,
+                                            uint32_t m, uint32_t j0, uint32_t j1, uint32_t hw, uint32_t l32,
+                                            uint32_t c0, uint32_t c1, uint32_t a, uint32_t b)
+{
+    constexpr uint32_t kHalves = kPreThreads / 32;
+    const uint32_t aa = a & 0x07070707u, ab = (a >> 3) & 0x07070707u, ac = (a >> 6) & 0x03030303u;
+    const uint32_t ba = b & 0x07070707u, bb = (b >> 3) & 0x07070707u, bc = (b >> 6) & 0x03030303u;
+    for (uint32_t j = j0 + hw; j < j1; j += 4 * kHalves) {
+        uint32_t cur[4];
+        GfTab t0[4], t1[4];
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+            const uint32_t r = j + u * kHalves;
+            const bool in = r < j1;
+            const uint32_t y0 = in ? Ct[c0 + r] : 0u, y1 = in ? Ct[c1 + r] : 0u;
+            t0[u] = gf_tab_l(permL, permC, y0);   // (the table of 0 gives 0)
+            t1[u] = gf_tab_l(permL, permC, y1);
+            cur[u] = in ? Yw[r * 32 + l32] : 0u;
+        }
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+            const uint32_t r = j + u * kHalves;
+            if (r < j1)
+                Yw[r * 32 + l32] = __builtin_amdgcn_bitop3_b32(
+                    cur[u],
+                    __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t0[u].a1, t0[u].a0, aa),
+                                                __builtin_amdgcn_perm(t0[u].b1, t0[u].b0, ab),
+                                                __builtin_amdgcn_perm(0u, t0[u].c, ac), 0x96),
+                    __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(t1[u].a1, t1[u].a0, ba),
+                                                __builtin_amdgcn_perm(t1[u].b1, t1[u].b0, bb),
+                                                __builtin_amdgcn_perm(0u, t1[u].c, bc), 0x96),
+                    0x96);
+        }
+    }
+}
+
 // T = U^-1 L^-1 of solve sd into sd.tinv (all waves of the workgroup)
 __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C, uint8_t* base, uint32_t tid)
 {
@@ -2884,24 +2925,66 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
     }
     __syncthreads();
     // MultiplyLowerTriangle, then BackSubstitution, on the identity's rows (a
-    // row of T is m <= 120 bytes: one half-wave, four bytes a lane)
+    // row of T is m <= 120 bytes: one half-wave, four bytes a lane), two
+    // pivots per barrier: every half-wave forms the second pivot's row from
+    // the first itself, so a step applies both to the rows past them (two
+    // multiplies a row) and the serial chain is m barriers instead of 2m.
+    // The second pivot's new row is written after the step's barrier (no
+    // later step of the sweep reads it; the other half-waves read the old one
+    // during the step).
     constexpr uint32_t kHalves = kPreThreads / 32;
     const uint32_t hw = tid >> 5, l32 = tid & 31;
-    for (uint32_t i = 0; i + 1 < m; ++i) {
-        const uint32_t src = Yw[i * 32 + l32];
-        for (uint32_t j = i + 1 + hw; j < m; j += kHalves) {
-            const uint32_t y = Ct[i * m + j];   // C[j][i]
-            if (y)
-                Yw[j * 32 + l32] ^= gf_mul_tab(src, gf_tab_l(permL, permC, y));
+    auto mul = [&](uint32_t v, uint32_t y) { return y ? gf_mul_tab(v, gf_tab_l(permL, permC, y)) : 0u; };
+    uint32_t pend = 0, pendRow = 0xffffffffu;   // a pivot row to store (half-wave 0)
+    auto flush_pend = [&]() {
+        if (pendRow != 0xffffffffu && hw == 0)
+            Yw[pendRow * 32 + l32] = pend;
+        pendRow = 0xffffffffu;
+    };
+    {
+        uint32_t i = 0;
+        for (; i + 2 < m; i += 2) {
+            flush_pend();
+            const uint32_t a = Yw[i * 32 + l32];
+            const uint32_t b = Yw[(i + 1) * 32 + l32] ^ mul(a, Ct[i * m + i + 1]);   // row i+1 after pivot i
+            tbuild_rows(Yw, Ct, permL, permC, m, i + 2, m, hw, l32, i * m, (i + 1) * m, a, b);
+            pend = b;
+            pendRow = i + 1;
+            __syncthreads();
+        }
+        flush_pend();
+        if (i + 1 < m) {
+            // (one pivot left before the last row)
+            const uint32_t src = Yw[i * 32 + l32];
+            for (uint32_t j = i + 1 + hw; j < m; j += kHalves) {
+                const uint32_t y = Ct[i * m + j];
+                if (y)
+                    Yw[j * 32 + l32] ^= mul(src, y);
+            }
         }
         __syncthreads();
     }
-    for (int i = (int)m - 1; i > 0; --i) {
-        const uint32_t xi = gf_mul_tab(Yw[i * 32 + l32], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]]));
-        for (uint32_t j = hw; j < (uint32_t)i; j += kHalves) {
-            const uint32_t y = Ct[(uint32_t)i * m + j];   // C[j][i]
-            if (y)
-                Yw[j * 32 + l32] ^= gf_mul_tab(xi, gf_tab_l(permL, permC, y));
+    {
+        int i = (int)m - 1;
+        for (; i >= 2; i -= 2) {
+            flush_pend();
+            const uint32_t xi = mul(Yw[i * 32 + l32], c_inv[Ct[i * m + i]]);
+            const uint32_t ym = Yw[(i - 1) * 32 + l32] ^ mul(xi, Ct[(uint32_t)i * m + i - 1]);   // row i-1 after pivot i
+            const uint32_t xm = mul(ym, c_inv[Ct[(i - 1) * m + i - 1]]);
+            tbuild_rows(Yw, Ct, permL, permC, m, 0, (uint32_t)i - 1, hw, l32, (uint32_t)i * m, (uint32_t)(i - 1) * m, xi,
+                        xm);
+            pend = ym;
+            pendRow = (uint32_t)i - 1;
+            __syncthreads();
+        }
+        flush_pend();
+        if (i == 1) {
+            const uint32_t xi = mul(Yw[32 + l32], c_inv[Ct[m + 1]]);
+            if (hw == 0) {
+                const uint32_t y = Ct[m];   // C[0][1]
+                if (y)
+                    Yw[l32] ^= mul(xi, y);
+            }
         }
         __syncthreads();
     }
