@@ -78,6 +78,7 @@ void be_copy_pinned(const BeCopy* r, unsigned n, bool toDevice)
             be_d2h((void*)(uintptr_t)r[i].dst, (const void*)(uintptr_t)r[i].src, r[i].bytes);
     }
 }
+void be_copy_list(const BeCopy* r, const void*, unsigned n, bool toDevice) { be_copy_pinned(r, n, toDevice); }
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
 void be_launch_ingest(const IngestDesc*, uint32_t, uint32_t, const uint32_t*, uint32_t) {}
