@@ -1771,22 +1771,27 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                             // t+i of its row's lists, a row broadcast (DPP) hands
                             // entry j to the whole quad, 4 terms of each list in flight
                             // (no masking after the reads, so they go out together)
+                            const char* lb = reinterpret_cast<const char*>(stage) + b4 * 4u;   // (this lane's 16 bytes)
                             for (uint32_t t = 0; t < most; t += 16) {
                                 const uint32_t i = t + (lane & 15u);
                                 // (entries past a list's end name the zero slot)
                                 const uint32_t s0 = i < n0 ? (uint32_t)plan[off0 + i] : zeroSlot;
                                 const uint32_t s1 = i < n1 ? (uint32_t)plan[off1 + i] : zeroSlot;
+                                // (byte offsets of the slots, so a term's address is one
+                                // v_add with the row broadcast folded in as its DPP source)
+                                const uint32_t s0b = s0 * (64u * 4u), s1b = s1 * (64u * 4u);
                                 const uint32_t left = most - t;   // (uniform)
+#define SGPU_TERM(S, K) (*reinterpret_cast<const uint4*>(lb + row_bcast<(K)>(S)))
 #define SGPU_QUAD_GROUP(J)                                                                                  \
             {                                                                                                       \
-                const uint4 x0 = lds16(stage, row_bcast<(J)>(s0) * 64 + b4);                                        \
-                const uint4 x1 = lds16(stage, row_bcast<(J) + 1>(s0) * 64 + b4);                                    \
-                const uint4 x2 = lds16(stage, row_bcast<(J) + 2>(s0) * 64 + b4);                                    \
-                const uint4 x3 = lds16(stage, row_bcast<(J) + 3>(s0) * 64 + b4);                                    \
-                const uint4 y0 = lds16(stage, row_bcast<(J)>(s1) * 64 + b4);                                        \
-                const uint4 y1 = lds16(stage, row_bcast<(J) + 1>(s1) * 64 + b4);                                    \
-                const uint4 y2 = lds16(stage, row_bcast<(J) + 2>(s1) * 64 + b4);                                    \
-                const uint4 y3 = lds16(stage, row_bcast<(J) + 3>(s1) * 64 + b4);                                    \
+                const uint4 x0 = SGPU_TERM(s0b, (J));                                                               \
+                const uint4 x1 = SGPU_TERM(s0b, (J) + 1);                                                           \
+                const uint4 x2 = SGPU_TERM(s0b, (J) + 2);                                                           \
+                const uint4 x3 = SGPU_TERM(s0b, (J) + 3);                                                           \
+                const uint4 y0 = SGPU_TERM(s1b, (J));                                                               \
+                const uint4 y1 = SGPU_TERM(s1b, (J) + 1);                                                           \
+                const uint4 y2 = SGPU_TERM(s1b, (J) + 2);                                                           \
+                const uint4 y3 = SGPU_TERM(s1b, (J) + 3);                                                           \
                 a0 = xor5_16(a0, x0, x1, x2, x3);                                                                   \
                 a1 = xor5_16(a1, y0, y1, y2, y3);                                                                   \
             }
@@ -1797,6 +1802,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                                     SGPU_QUAD_GROUP(8)
                                 if (left > 12)
                                     SGPU_QUAD_GROUP(12)
+#undef SGPU_TERM
 #undef SGPU_QUAD_GROUP
                             }
                             PHASE_MARK(14, qclk);
