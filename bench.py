@@ -65,18 +65,19 @@ def lib_sha256(path):
 
 
 def pmc_traffic(kernel, library):
-    """Per-launch HBM traffic of `kernel` from the committed PMC capture
-    (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per dispatch, tools/pmc_traffic.py)
-    and whether that capture measured the very library this run loads
-    (sha256 of the .so recorded at capture time)."""
+    """Per-launch memory traffic of `kernel` from the committed PMC capture
+    (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per dispatch, tools/pmc_traffic.py),
+    whether that capture measured the very library this run loads (sha256 of
+    the .so recorded at capture time), and the capture's traffic of all the
+    library's kernels per workload step (None if it has none)."""
     try:
         with open(TRAFFIC_JSON) as f:
             d = json.load(f)
         want = d.get("_lib_sha256")
         same = want is not None and want == lib_sha256(library)
-        return d[kernel]["traffic_bytes"], d.get("_source", TRAFFIC_JSON), same
+        return d[kernel]["traffic_bytes"], d.get("_source", TRAFFIC_JSON), same, d.get("_step_traffic_bytes")
     except (OSError, KeyError, ValueError):
-        return None, None, False
+        return None, None, False, None
 
 
 def workload(rank, streams, ranges=True):
@@ -531,7 +532,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
     achieved_alg = (exec_bytes / exec_s / 1e9) if exec_s > 0 else 0.0
     steps = args.steps
     launches = max(1, eng["exec_launches"])
-    traffic, traffic_src, traffic_same = pmc_traffic("sgpu::k_exec", library)
+    traffic, traffic_src, traffic_same, step_traffic = pmc_traffic("sgpu::k_exec", library)
     exec_ms_per_launch = rep.exec_ms / launches
     ueng = S.engine_dict(urep)
     unique_per_launch = ueng["exec_unique_bytes"] / max(1, ueng["exec_launches"])
@@ -572,6 +573,19 @@ def run_rank(rank, world, local, args, library, use_cuda):
         },
         "payload_GBps": round(payload_total / t_max / 1e9, 3),
         "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
+        "pct_hbm_peak_basis": "ALGORITHMIC bytes (SURVEY 8d: every source byte of the reference's GF ops, "
+                              "re-reads included) over wall time; the memory traffic the step moves is "
+                              "physical_step below",
+        "physical_step": ({
+            "traffic_bytes_per_step": step_traffic,
+            "GBps": round(step_traffic * world / t_max * steps / 1e9, 3),
+            "pct_hbm_peak": round(100.0 * step_traffic * world / t_max * steps / 1e9
+                                  / (HBM_PEAK_GBPS * world), 2),
+            "build_matches": traffic_same,
+            "note": "all kernels' rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per workload step from the "
+                    "committed capture (traffic_source; L2 <-> fabric bytes, MALL hits included) over "
+                    "this run's wall time per step",
+        } if step_traffic else None),
         "device": {
             "exec_ms_per_step": round(rep.exec_ms / steps, 3),
             "kernel_ms_per_step": {k: round(v / steps, 3) for k, v in zip(S.KERNELS, rep.kernel_ms)},
@@ -599,7 +613,9 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "frac_basis": ("physical HBM bytes per launch (rocprofv3 PMC capture of this same library build)"
+            "frac_basis": ("L2 <-> fabric bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of a "
+                           "separate --steps 1 capture of this same library build; MALL hits included, so "
+                           "an upper bound on HBM bytes: unique_frac beside it is the compulsory floor)"
                            if phys else "compulsory bytes per launch (no PMC capture of this build committed)"),
             "traffic": traffic,
             "traffic_source": traffic_src,

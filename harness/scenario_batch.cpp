@@ -70,7 +70,7 @@ struct BatchReport
     double exec_ms;        ///< device time of the executor launches only
     double setup_seconds;  ///< payload generation + staging (untimed)
     uint64_t rounds;       ///< rounds (flushes) in the timed steps
-    uint64_t engine[18];   ///< engine counters over the timed steps (see sgpu_engine_stats_ex),
+    uint64_t engine[21];   ///< engine counters over the timed steps (see sgpu_engine_stats_ex),
                            ///< then the arena growth (sgpu_arena_bytes)
     uint64_t checked;      ///< packets whose bytes were verified
     uint64_t mismatches;   ///< verification failures
@@ -86,7 +86,7 @@ struct BatchReport
 
 namespace {
 
-constexpr int kEngineStats = 17;
+constexpr int kEngineStats = 20;
 using Clock = std::chrono::steady_clock;
 
 struct Api
@@ -1417,7 +1417,8 @@ int scenario_batch_run(void* session, StreamResult* results, const BatchOptions*
             return -2;
         uint64_t e0[kEngineStats + 1], e1[kEngineStats + 1];
         auto stats = [&](uint64_t* e) {
-            e[kEngineStats - 2] = e[kEngineStats - 1] = 0;
+            for (int k = 15; k < kEngineStats; ++k)
+                e[k] = 0;
             if (api.engine_stats_ex)
                 api.engine_stats_ex(e, kEngineStats);
             else

@@ -301,7 +301,10 @@ SIAMESE_EXPORT void sgpu_timing_kernels(double* msOut, unsigned count);
 SIAMESE_EXPORT void sgpu_engine_stats(uint64_t* out15);
 /// sgpu_engine_stats' 15 values, then the algorithmic bytes of k_ldpc (the
 /// wide rows' picks, part of the algorithmic op bytes), then the executor
-/// launches' compulsory bytes (see sgpu_measure_unique); count entries at most.
+/// launches' compulsory bytes (see sgpu_measure_unique), then the device
+/// recovery-matrix jobs (sgpu_decode_device), those of them chained into
+/// their decode's submission, and the chained ones whose matrix was singular
+/// (the host repeated the elimination); count entries at most.
 SIAMESE_EXPORT void sgpu_engine_stats_ex(uint64_t* out, unsigned count);
 /// Measurement aid: while on, flush assembly counts the executor launches'
 /// compulsory bytes -- each distinct source symbol read once, each

@@ -59,8 +59,11 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes
 /// the terms it expands itself (sum updates, LDPC picks) to (ops.h).
 /// `maxWindow`: the largest OP_ROWS window (entries) among the launched
 /// segments, kNoRows when none has a row batch (sizes the LDS stage).
+/// `results`: the submission's result words, which gate the rows of an
+/// OP_ROWS batch whose GfOp.termBegin is non-zero (1 + the word; a zero word
+/// skips the rows: a chained device elimination that failed, ops.h GeDesc).
 void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct,
-                    uint32_t maxWindow);
+                    const uint32_t* results, uint32_t maxWindow);
 /// Wide rows' LDPC picks (ops.h LdpcItem), one workgroup per item; adds the
 /// reference's source bytes of the picks (min(len, n) each) to acct[0].
 void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct);
@@ -76,9 +79,13 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
                      uint32_t solveBegin, uint32_t solveCount);
 
 /// Device recovery-matrix generation + elimination (ops.h GeDesc): one job
-/// per desc, its input at in + desc.in, its output in results + desc.result.
-/// Reads nothing any other launch of the flush writes.
-void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results);
+/// per desc, its input at in + desc.in, its output in results + desc.result;
+/// a kGeChained job that succeeds also writes its solve's coefficients
+/// (coef + solveCoef) and permutes its SolveRows (rows + solveRow).  Reads
+/// nothing any other launch of the flush writes; runs before them.
+/// maxRows / maxCols: the largest job of the launch (sizes its LDS).
+void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
+                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols);
 
 /// Block until all queued work has finished.  Returns false on a device fault.
 bool be_sync();

@@ -959,6 +959,7 @@ __device__ __forceinline__ void row_versions4(uint32_t m0, uint32_t m1, uint32_t
 __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__ stream,
                                                        const ExecItem* __restrict__ items,
                                                        unsigned long long* __restrict__ acct,
+                                                       const uint32_t* __restrict__ results,
                                                        uint32_t stageSlots)
 {
     __shared__ uint4 ring[2][kRingWords];
@@ -995,8 +996,8 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
     // this workgroup's tiles [tile0, tile0 + nTiles * 256): every op runs
     // over each of them in turn, so an OP_ROWS batch loads its table and
     // draws its row plans once for all of them
-    const uint32_t tile0 = (it.tiles & 0xffffu) * kExecTileBytes;
-    const uint32_t nTiles = it.tiles >> 16;
+    const uint32_t tile0 = exec_first_tile(it.tiles) * kExecTileBytes;
+    const uint32_t nTiles = exec_tile_count(it.tiles);
 #ifdef SGPU_PHASE_CLOCKS
     unsigned long long kclk = clock64();
 #endif
@@ -1048,7 +1049,12 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
         if (tid < kRingWords && oi + 1 < it.opCount && next + tid < words)
             pf = ld16((uint64_t)(seg + next + tid));
 
-        if (kind == OP_LITERAL) {
+        // an op gated on a chained device elimination that failed (GfOp
+        // termBegin: 1 + its outcome word, ops.h) does nothing
+        const uint32_t gate = kind != OP_LITERAL ? uni(h1.z) : 0u;
+        const bool skip = gate != 0 && results[gate - 1u] == 0u;
+        if (skip) {
+        } else if (kind == OP_LITERAL) {
             if (wave == 0) {
                 for (uint32_t ti = 0; ti < nTiles; ++ti)
                     store_literal(tile0 + ti * kExecTileBytes + lane * 4, dst, n, valid, uni(h1.z), uni(h1.w));
@@ -2055,7 +2061,7 @@ __global__ __launch_bounds__(kExecThreads) void k_exec(const uint4* __restrict__
                 }
             }
         }
-        if (kind != OP_ROWS && tid < kRingWords)
+        if ((kind != OP_ROWS || skip) && tid < kRingWords)
             ring[cur ^ 1][tid] = pf;
         __syncthreads();
 #ifdef SGPU_PHASE_CLOCKS
@@ -2368,6 +2374,13 @@ __device__ void solve_prefix_wave(uint32_t m, uint32_t lane, uint32_t (&p4)[4], 
     }
 }
 
+// A solve gated on a chained device elimination that failed (SolveDesc.gate):
+// its coefficients and row order were never written, so it does not run.
+__device__ __forceinline__ bool solve_gated_off(const SolveDesc& sd, const uint32_t* results)
+{
+    return sd.gate != 0 && results[sd.gate - 1u] == 0u;
+}
+
 // rows' first words for the prefix pass (wave 0), loaded before the staging
 // so their latency overlaps it
 __device__ __forceinline__ void prefix_load(uint32_t (&p4)[4], uint32_t m, uint32_t lane, uint64_t head,
@@ -2376,7 +2389,7 @@ __device__ __forceinline__ void prefix_load(uint32_t (&p4)[4], uint32_t m, uint3
 #pragma unroll
     for (unsigned k = 0; k < 4; ++k) {
         const uint32_t j = lane + 64u * k;
-        p4[k] = j < m ? ld4_masked(head + (uint64_t)j * 16u, R[j].initBytes) : 0u;
+        p4[k] = j < m ? ld4_masked(head + (uint64_t)solve_head_slot(R[j].headIndex, j) * 16u, R[j].initBytes) : 0u;
     }
 }
 
@@ -2733,7 +2746,7 @@ __global__ __launch_bounds__(64 * kSolveWaves) void k_solve_main(
     const uint32_t m = sd.m;
     const SolveRow* R = rows + sd.rowBegin;
     const uint8_t* C = coef + sd.coefOffset;
-    if (m > kSolveLdsMaxRows)
+    if (m > kSolveLdsMaxRows || solve_gated_off(sd, results))
         return;   // (the host never queues m > 255: kMaximumLossRecoveryCount)
     // flags bit 0: the length prefixes are already solved (k_solve_prefix or
     // k_solve_pre); bit 2: k_solve_tr ran before this launch (it took every
@@ -2781,7 +2794,7 @@ __global__ __launch_bounds__(64) void k_solve_prefix(const SolveDesc* __restrict
     extern __shared__ uint4 X[];
     const SolveDesc sd = solves[blockIdx.x];
     const uint32_t m = sd.m;
-    if (m > kSolveLdsMaxRows)
+    if (m > kSolveLdsMaxRows || solve_gated_off(sd, results))
         return;
     const SolveRow* R = rows + sd.rowBegin;
     const uint8_t* C = coef + sd.coefOffset;
@@ -3014,14 +3027,14 @@ __global__ __launch_bounds__(kPreThreads) void k_solve_pre(const SolveDesc* __re
     const uint32_t tid = threadIdx.x;
     if (mode == 1 || (mode == 0 && blockIdx.x >= count)) {
         const SolveDesc sd = solves[mode == 1 ? blockIdx.x : blockIdx.x - count];
-        if (sd.m == 0 || sd.m > kProductMaxRows || sd.tinv == 0)
+        if (sd.m == 0 || sd.m > kProductMaxRows || sd.tinv == 0 || solve_gated_off(sd, results))
             return;   // (uniform)
         solve_tbuild(sd, coef + sd.coefOffset, reinterpret_cast<uint8_t*>(X), tid);
         return;
     }
     const SolveDesc sd = solves[blockIdx.x];
     const uint32_t m = sd.m;
-    if (m > kSolveLdsMaxRows)
+    if (m > kSolveLdsMaxRows || solve_gated_off(sd, results))
         return;
     const SolveRow* R = rows + sd.rowBegin;
     const uint8_t* C = coef + sd.coefOffset;
@@ -3262,9 +3275,9 @@ __global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __rest
     const SolveItem it = items[blockIdx.x / (kTrSplit * kTrHalves)];
     const SolveDesc sd = solves[it.solve];
     const uint32_t tileBase = it.tileBase + (blockIdx.x % kTrHalves) * (1024u / kTrHalves);
-    if (sd.m == 0 || sd.m > kProductMaxRows || sd.tinv == 0 || results[sd.result] != sd.m ||
-        tileBase >= sd.maxBytes)
-        return;   // (uniform: k_solve_main solves it)
+    if (sd.m == 0 || sd.m > kProductMaxRows || sd.tinv == 0 || solve_gated_off(sd, results) ||
+        results[sd.result] != sd.m || tileBase >= sd.maxBytes)
+        return;   // (uniform: k_solve_main solves it, or the solve is gated off)
     const uint32_t left = sd.maxBytes - tileBase;
     const uint32_t nq = left >= 256u ? 2u : 1u;   // (quarters of this half)
     const SolveRow* R = rows + sd.rowBegin;
@@ -3278,18 +3291,21 @@ __global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __rest
 // ---------------------------------------------------------------------------
 // The recovery matrix of a decode on the device (k_ge, ops.h GeDesc)
 //
-// One workgroup per decode, the matrix resident in LDS (kGeStride bytes a
-// row).  Generation (the host's generate_matrix; reference
-// SiameseDecoder.cpp:2157-2383) writes four columns per thread: the dense
-// part from the row's opcodes (Siamese), 1/(X ^ Y) (Cauchy) or 1 (parity);
-// then the LDPC picks, one row per wave and 64 PCG draws per pass (jump-ahead
-// c_pcgA/c_pcgG), land by LDS XOR atomics.  The elimination is the
-// reference's (:2423-2531): no pivoting while each pivot byte is non-zero,
-// then row pivoting from the first zero one; each pivot is one multiplier
-// pass over the rows below (y = row[p] / pivot, kept at [p]) and one
-// row-update pass over their bytes (p, end), a dword per thread.
-constexpr unsigned kGeThreads = 256;
-constexpr unsigned kGeStride = kGeMaxCols + 4;   // 33 dwords: consecutive rows start in different banks
+// One wave per decode, the matrix resident in LDS (ge_stride_words dwords a
+// row: odd, so the rows the lanes own start in different banks).  Generation
+// (the host's generate_matrix; reference SiameseDecoder.cpp:2157-2383) writes
+// four columns per lane: the dense part from the row's opcodes (Siamese),
+// 1/(X ^ Y) (Cauchy) or 1 (parity); then the LDPC picks, 64 PCG draws of one
+// row per pass (jump-ahead c_pcgA/c_pcgG), land by LDS XOR atomics.  The
+// elimination is the reference's (:2423-2531): no pivoting while each pivot
+// byte is non-zero, then row pivoting from the first zero one.  Lane k owns
+// the rows k, k + 64, ...: at each pivot it takes its multiplier y = row[p] /
+// pivot (kept at [p]) and XORs y times the pivot row's bytes (p, end) into its
+// own row, a dword at a time with the pivot row's dword broadcast from LDS
+// and y's multiply table read once per pivot.  No barrier inside a step: the
+// wave is the workgroup (round 5's four waves with two barriers per pivot ran
+// 130 us per headline launch).
+constexpr unsigned kGeThreads = 64;
 
 __device__ __forceinline__ uint32_t ge_opcode(uint32_t lane, uint32_t row)
 {
@@ -3310,72 +3326,77 @@ __device__ __forceinline__ uint32_t ge_comb(uint32_t k, uint32_t cx, uint32_t cx
     return (k & 1u) ^ ((k & 2u) ? cx : 0u) ^ ((k & 4u) ? cx2 : 0u);
 }
 
-__global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ descs, const uint8_t* __restrict__ in,
-                                                  uint32_t* __restrict__ results)
+__host__ __device__ constexpr uint32_t ge_lds_bytes(uint32_t rows, uint32_t cols)
 {
-    constexpr uint32_t S4 = kGeStride / 4;
-    __shared__ uint32_t M[kGeMaxRows * S4];
+    return rows * ge_stride_words(cols) * 4u;
+}
+
+__global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ descs, const uint8_t* __restrict__ in,
+                                                  uint32_t* __restrict__ results, SolveRow* __restrict__ srows,
+                                                  uint8_t* __restrict__ scoef)
+{
+    extern __shared__ uint32_t M[];   // rows x S4 dwords
     __shared__ uint4 permL[256];
     __shared__ uint32_t permC[256];
-    __shared__ uint8_t piv[kGeMaxRows], used[kGeMaxRows], yv[kGeMaxRows];
+    __shared__ uint8_t piv[kGeMaxRows], used[kGeMaxRows];
     __shared__ uint16_t cnt[kGeMaxRows];
-    __shared__ uint32_t found;
-    __shared__ unsigned long long bytesL;
     uint8_t* Mb = reinterpret_cast<uint8_t*>(M);
     const GeDesc d = descs[blockIdx.x];
     const uint32_t rows = d.rows, cols = d.cols;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t S4 = ge_stride_words(cols), SB = 4u * S4;
+    const uint32_t lane = threadIdx.x;
     const GeRow* R = reinterpret_cast<const GeRow*>(in + d.in);
     const GeCol* C = reinterpret_cast<const GeCol*>(R + rows);
     const uint8_t* pick = reinterpret_cast<const uint8_t*>(C + cols);
-    {
-        const uint32_t* t = c_perm[tid];   // (kGeThreads == 256)
-        permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
-        permC[tid] = t[4];
+    for (uint32_t y = lane; y < 256; y += kGeThreads) {
+        const uint32_t* t = c_perm[y];
+        permL[y] = make_uint4(t[0], t[1], t[2], t[3]);
+        permC[y] = t[4];
     }
-    for (uint32_t i = tid; i < rows; i += kGeThreads) {
+    for (uint32_t i = lane; i < rows; i += kGeThreads) {
         piv[i] = (uint8_t)i;
         used[i] = 0;
         cnt[i] = R[i].colCount;
     }
-    if (tid == 0)
-        bytesL = 0;
     __syncthreads();
 
-    // 1. dense parts, a dword (four columns) per thread
+    // 1. dense parts, a dword (four columns) per lane
     const uint32_t wpr = (cols + 3u) / 4u;
-    for (uint32_t x = tid; x < rows * wpr; x += kGeThreads) {
-        const uint32_t r = x / wpr, w = x - r * wpr;
-        const GeRow g = R[r];
-        uint32_t lo = 0, hi = 0;
+    for (uint32_t x = lane; x < rows * S4; x += kGeThreads) {
+        const uint32_t r = x / S4, w = x - r * S4;
+        uint32_t lo = 0;
+        if (w < wpr) {
+            const GeRow g = R[r];
+            uint32_t hi = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t j = 4u * w + q;
-            if (j < cols && j < g.jEnd) {
-                const GeCol c = C[j];
-                uint32_t v = 1u, h = 0u;
-                if (g.kind == GE_CAUCHY) {
-                    v = c_inv[(uint8_t)(g.rbase ^ c.ccol)];
-                } else if (g.kind == GE_SIAMESE) {
-                    const uint32_t op = ge_opcode(c.lane, g.row);
-                    v = ge_comb(op & 7u, c.cx, c.cx2);
-                    h = ge_comb(op >> 3, c.cx, c.cx2);
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t j = 4u * w + q;
+                if (j < cols && j < g.jEnd) {
+                    const GeCol c = C[j];
+                    uint32_t v = 1u, h = 0u;
+                    if (g.kind == GE_CAUCHY) {
+                        v = c_inv[(uint8_t)(g.rbase ^ c.ccol)];
+                    } else if (g.kind == GE_SIAMESE) {
+                        const uint32_t op = ge_opcode(c.lane, g.row);
+                        v = ge_comb(op & 7u, c.cx, c.cx2);
+                        h = ge_comb(op >> 3, c.cx, c.cx2);
+                    }
+                    lo |= v << (8u * q);
+                    hi |= h << (8u * q);
                 }
-                lo |= v << (8u * q);
-                hi |= h << (8u * q);
             }
+            if (hi)   // v ^ RX * h
+                lo ^= gf_mul_tab(hi, gf_tab_l(permL, permC, 1u + (g.row + 1u) % kRowValuePeriod));
         }
-        if (hi)   // v ^ RX * h
-            lo ^= gf_mul_tab(hi, gf_tab_l(permL, permC, 1u + (g.row + 1u) % kRowValuePeriod));
-        M[r * S4 + w] = lo;
+        M[x] = lo;
     }
     __syncthreads();
 
-    // 2. LDPC picks: one Siamese row per wave, draws c0 + lane per pass
-    for (uint32_t r = wave; r < rows; r += kGeThreads / 64u) {
+    // 2. LDPC picks: one Siamese row at a time, draws c0 + lane per pass
+    for (uint32_t r = 0; r < rows; ++r) {
         const GeRow g = R[r];
         if (g.kind != GE_SIAMESE || g.ldpcN == 0)
-            continue;   // (uniform in the wave)
+            continue;   // (uniform)
         const uint32_t N = g.ldpcN, P = 2u * ((N + kPairRate - 1u) / kPairRate);
         const uint64_t inc = ((uint64_t)g.row << 1) | 1u;
         uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed(row, N)
@@ -3394,48 +3415,42 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
     }
     __syncthreads();
 
-    // 3. elimination.  One pivot step: the rows below `pivot` (through piv[]
-    // when pivoting) take y = row[pivot] / val at [pivot], then y * the
+    // 3. elimination.  One pivot step: every row below `pivot` (through piv[]
+    // once pivoting) takes y = row[pivot] / val at [pivot], then y * the
     // source row's bytes (pivot, end) (SiameseDecoder.h:504-541)
     unsigned long long myBytes = 0;
     auto eliminate = [&](uint32_t src, uint32_t pivot, uint32_t end, uint32_t val, bool pivoted) {
         const GfTab iv = gf_tab_l(permL, permC, c_inv[val]);
-        for (uint32_t k = pivot + 1u + tid; k < rows; k += kGeThreads) {
+        const uint32_t w0 = (pivot + 1u) / 4u, w1 = (end + 3u) / 4u;
+        const uint32_t* S = M + src * S4;
+        for (uint32_t k = pivot + 1u + lane; k < rows; k += kGeThreads) {
             const uint32_t rk = pivoted ? piv[k] : k;
-            const uint32_t v = Mb[rk * kGeStride + pivot];
-            uint32_t y = 0;
-            if (v) {
-                y = gf_mul_tab(v, iv) & 0xffu;
-                Mb[rk * kGeStride + pivot] = (uint8_t)y;
-                if (end > pivot + 1u)
-                    myBytes += end - pivot - 1u;
-                if (pivoted && cnt[rk] < end)
-                    cnt[rk] = (uint16_t)end;
-            }
-            yv[rk] = (uint8_t)y;
-        }
-        __syncthreads();
-        if (end > pivot + 1u) {
-            const uint32_t w0 = (pivot + 1u) / 4u, nw = (end + 3u) / 4u - w0;
-            const uint32_t nr = rows - pivot - 1u;
-            for (uint32_t x = tid; x < nr * nw; x += kGeThreads) {
-                const uint32_t kk = x / nw, w = w0 + (x - kk * nw);
-                const uint32_t rk = pivoted ? piv[pivot + 1u + kk] : pivot + 1u + kk;
-                const uint32_t y = yv[rk];
-                if (!y)
-                    continue;
-                const uint32_t mask = byte_mask((int)end - (int)(4u * w)) & ~byte_mask((int)(pivot + 1u) - (int)(4u * w));
-                M[rk * S4 + w] ^= gf_mul_tab(M[src * S4 + w], gf_tab_l(permL, permC, y)) & mask;
+            const uint32_t v = Mb[rk * SB + pivot];
+            if (!v)
+                continue;
+            const uint32_t y = gf_mul_tab(v, iv) & 0xffu;
+            Mb[rk * SB + pivot] = (uint8_t)y;
+            if (pivoted && cnt[rk] < end)
+                cnt[rk] = (uint16_t)end;
+            if (end <= pivot + 1u)
+                continue;
+            myBytes += end - pivot - 1u;
+            const GfTab ty = gf_tab_l(permL, permC, y);
+            uint32_t* D = M + rk * S4;
+            for (uint32_t w = w0; w < w1; ++w) {
+                const uint32_t mask =
+                    byte_mask((int)end - (int)(4u * w)) & ~byte_mask((int)(pivot + 1u) - (int)(4u * w));
+                D[w] ^= gf_mul_tab(S[w], ty) & mask;
             }
         }
-        __syncthreads();
+        __syncthreads();   // (the next step reads the rows this one wrote)
     };
     uint32_t p = 0;
     for (; p < cols; ++p) {
-        const uint32_t val = Mb[p * kGeStride + p];
+        const uint32_t val = Mb[p * SB + p];
         if (val == 0)
             break;
-        if (tid == 0)
+        if (lane == 0)
             used[p] = 1;
         eliminate(p, p, cnt[p], val, false);
     }
@@ -3443,21 +3458,24 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
     if (p < cols) {
         uint32_t jFrom = p + 1u;   // (the caller found column p zero in row p)
         for (uint32_t pivot = p; pivot < cols; ++pivot) {
-            if (tid == 0)
-                found = 0xffffffffu;
-            __syncthreads();
-            for (uint32_t j = jFrom + tid; j < rows; j += kGeThreads)
-                if (Mb[piv[j] * kGeStride + pivot])
-                    atomicMin(&found, j);
-            __syncthreads();
-            const uint32_t j = found;
+            // the first row at or after jFrom (in pivot order) with a
+            // non-zero byte at the pivot column
+            uint32_t j = 0xffffffffu;
+            for (uint32_t j0 = jFrom; j0 < rows; j0 += kGeThreads) {
+                const uint32_t jj = j0 + lane;
+                const uint64_t b = __ballot(jj < rows && Mb[piv[jj] * SB + pivot] != 0);
+                if (b) {
+                    j = j0 + (uint32_t)__builtin_ctzll(b);
+                    break;
+                }
+            }
             if (j == 0xffffffffu) {
                 stop = pivot;
                 break;
             }
             const uint32_t rj = piv[j];
-            __syncthreads();   // (every thread has read piv[j])
-            if (tid == 0) {
+            __syncthreads();   // (every lane has read piv[j])
+            if (lane == 0) {
                 piv[j] = piv[pivot];
                 piv[pivot] = (uint8_t)rj;
                 used[rj] = 1;
@@ -3465,23 +3483,41 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
             __syncthreads();
             if (pivot >= cols - 1u)
                 break;
-            eliminate(rj, pivot, cnt[rj], Mb[rj * kGeStride + pivot], true);
+            eliminate(rj, pivot, cnt[rj], Mb[rj * SB + pivot], true);
             jFrom = pivot + 1u;
         }
     }
 
-    // 4. outcome, pivots, used rows, column counts, the matrix
-    if (myBytes)
-        atomicAdd(&bytesL, myBytes);
-    __syncthreads();
+    // 4. outcome: the header words, the pivots, and for a chained job the
+    // solve's coefficients and rows in pivot order; else the used rows, the
+    // column counts and the matrix for the host to install
+#pragma unroll
+    for (unsigned o = 32; o >= 1; o >>= 1)
+        myBytes += __shfl_xor(myBytes, o, 64);
+    const bool ok = stop == cols;
+    const bool chained = (d.flags & kGeChained) != 0;
+    // MultiplyLowerTriangle's multipliers: the eliminated matrix's non-zero
+    // bytes below the diagonal, in pivot order (SiameseDecoder.cpp:1065-1104)
+    uint32_t nz = 0;
+    if (ok)
+        for (uint32_t j = lane; j < cols; j += kGeThreads) {
+            const uint8_t* row = Mb + piv[j] * SB;
+            for (uint32_t i = 0; i < j; ++i)
+                nz += row[i] != 0;
+        }
+#pragma unroll
+    for (unsigned o = 32; o >= 1; o >>= 1)
+        nz += __shfl_xor(nz, o, 64);
     uint32_t* out = results + d.result;
-    if (tid == 0) {
-        out[0] = stop;
-        out[1] = (uint32_t)bytesL;
-        out[2] = (uint32_t)(bytesL >> 32);
-        out[3] = 0;
+    if (lane < kGeOutHeader) {
+        const uint32_t hdr[kGeOutHeader] = {stop, (uint32_t)myBytes, (uint32_t)(myBytes >> 32), ok ? 1u : 0u, nz, 0, 0, 0};
+        uint32_t v = 0;
+#pragma unroll
+        for (unsigned k = 0; k < kGeOutHeader; ++k)
+            v = lane == k ? hdr[k] : v;
+        out[lane] = v;
     }
-    for (uint32_t w = tid; w < (rows + 3u) / 4u; w += kGeThreads) {
+    for (uint32_t w = lane; w < (rows + 3u) / 4u; w += kGeThreads) {
         uint32_t a = 0, b = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 4; ++q)
@@ -3490,19 +3526,51 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
                 b |= (uint32_t)used[4u * w + q] << (8u * q);
             }
         out[ge_out_pivots(rows) + w] = a;
-        out[ge_out_used(rows) + w] = b;
+        if (!chained)
+            out[ge_out_used(rows) + w] = b;
     }
-    for (uint32_t w = tid; w < (rows + 1u) / 2u; w += kGeThreads)
+    if (chained) {
+        if (!ok)
+            return;   // (the gated items of the submission do not run)
+        // coefficients: coef[j * cols + i] = the pivot-order row j's column i
+        uint8_t* co = scoef + d.solveCoef;
+        for (uint32_t x = lane; x < cols * cols; x += kGeThreads) {
+            const uint32_t j = x / cols, i = x - j * cols;
+            co[x] = Mb[piv[j] * SB + i];
+        }
+        // the solve's rows in pivot order, each keeping its head slot: every
+        // lane reads its rows before any lane writes
+        SolveRow* sr = srows + d.solveRow;
+        SolveRow t[4];
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+            const uint32_t j = lane + kGeThreads * u;
+            if (j < cols) {
+                const uint32_t src = piv[j];
+                t[u] = sr[src];
+                t[u].headIndex = 1u + solve_head_slot(t[u].headIndex, src);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+            const uint32_t j = lane + kGeThreads * u;
+            if (j < cols)
+                sr[j] = t[u];
+        }
+        return;
+    }
+    for (uint32_t w = lane; w < (rows + 1u) / 2u; w += kGeThreads)
         out[ge_out_counts(rows) + w] = (uint32_t)cnt[2u * w] | (2u * w + 1u < rows ? (uint32_t)cnt[2u * w + 1u] << 16 : 0u);
     const uint32_t total = rows * cols;
-    for (uint32_t w = tid; w < (total + 3u) / 4u; w += kGeThreads) {
+    for (uint32_t w = lane; w < (total + 3u) / 4u; w += kGeThreads) {
         uint32_t a = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 4; ++q) {
             const uint32_t b = 4u * w + q;
             if (b < total) {
                 const uint32_t r = b / cols;
-                a |= (uint32_t)Mb[r * kGeStride + (b - r * cols)] << (8u * q);
+                a |= (uint32_t)Mb[r * SB + (b - r * cols)] << (8u * q);
             }
         }
         out[ge_out_matrix(rows) + w] = a;
@@ -3762,6 +3830,11 @@ bool be_init(int device, const char** err)
         *err = "the device refused the solve prefix pass's LDS";
         return false;
     }
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ge), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)ge_lds_bytes(kGeMaxRows, kGeMaxCols)) != hipSuccess) {
+        *err = "the device refused the recovery matrix's LDS";
+        return false;
+    }
     if (hipDeviceSynchronize() != hipSuccess) {
         *err = "device synchronisation failed during init";
         return false;
@@ -3951,7 +4024,7 @@ void be_launch_ingest(const IngestDesc* descs, uint32_t count, uint32_t maxBytes
 }
 
 void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct,
-                    uint32_t maxWindow)
+                    const uint32_t* results, uint32_t maxWindow)
 {
     if (count == 0)
         return;
@@ -3963,7 +4036,7 @@ void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, u
         slots = kRowSums + (maxWindow < g_stageCap ? maxWindow : g_stageCap);
     hipLaunchKernelGGL(k_exec, dim3(count), dim3(kExecThreads), (size_t)(slots ? slots + 1 : 0) * kExecTileBytes,
                        g_stream, static_cast<const uint4*>(stream), items,
-                       reinterpret_cast<unsigned long long*>(acct), slots);
+                       reinterpret_cast<unsigned long long*>(acct), results, slots);
 }
 
 void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
@@ -3975,12 +4048,14 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
                        reinterpret_cast<unsigned long long*>(acct));
 }
 
-void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results)
+void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
+                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols)
 {
     if (count == 0)
         return;
     Timed t(kBeGe);
-    hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), 0, g_stream, descs, in, results);
+    hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), (size_t)ge_lds_bytes(maxRows, maxCols), g_stream, descs,
+                       in, results, rows, coef);
 }
 
 namespace {

@@ -578,11 +578,12 @@ SIAMESE_EXPORT void sgpu_timing_kernels(double* msOut, unsigned count)
 SIAMESE_EXPORT void sgpu_engine_stats_ex(uint64_t* out, unsigned count)
 {
     const EngineStats s = Engine::global()->stats();
-    const uint64_t v[17] = {s.flushes,    s.launches,    s.ops,        s.terms,    s.solves,
+    const uint64_t v[20] = {s.flushes,    s.launches,    s.ops,        s.terms,    s.solves,
                             s.ingests,    s.uploadBytes, s.refOpBytes, s.outBytes, s.solveBytes,
                             s.assembleNs, s.waitNs,      s.completeNs, s.reclaimNs,
-                            s.execLaunches, s.ldpcBytes, s.execUniqueBytes};
-    for (unsigned k = 0; k < count && k < 17; ++k)
+                            s.execLaunches, s.ldpcBytes, s.execUniqueBytes,
+                            s.geJobs,     s.geChained,   s.geRetried};
+    for (unsigned k = 0; k < count && k < 20; ++k)
         out[k] = v[k];
 }
 

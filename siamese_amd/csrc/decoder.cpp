@@ -115,6 +115,7 @@ void DecoderCore::donate_spare()
             pd.serial = 0;
             pd.live = false;
             pd.done = false;
+            pd.held = false;
         }
         res_->doneCount.store(0, std::memory_order_relaxed);
         res_->orphan = false;
@@ -191,6 +192,8 @@ DecoderCore::~DecoderCore()
     for (auto& lane : lanes_)
         for (Sum& s : lane)
             eng_->release(s.d.buf);
+    if (geState_ == 2)
+        chain_sums_commit();   // (a chained decode never finished: its replaced sum buffers)
     donate_spare();
 }
 
@@ -444,7 +447,7 @@ bool DecoderCore::grow_sum(DevSum& s, unsigned bytes)
             prog_.lc_term(s.buf.addr(), s.devValid, 1);
             prog_.lc_end();
         }
-        eng_->release(s.buf);
+        release_sum_buf(s.buf);
         s.buf = nb;
     }
     s.bytes = bytes; // [devValid, bytes) is zero, materialised lazily
@@ -549,7 +552,7 @@ bool DecoderCore::plug_sum_holes(unsigned elementStart)
             prog_.lc_begin(S.d.buf.addr(), S.d.bytes, S.d.devValid);
             prog_.lc_term(o.buf.addr(), o.bytes, sum_coeff(s, column));
             prog_.lc_end();
-            eng_->account(o.bytes);
+            account_elim(o.bytes);
             S.d.devValid = S.d.bytes;
         }
     }
@@ -1273,12 +1276,13 @@ SiameseResult DecoderCore::decode_device(SiameseOriginalPacket** packetsOut, uns
         return Siamese_NeedMoreData;
     // (the search's first attempt, on a fresh matrix: decode_loop's first
     // decode_region)
-    if (region_.recoveryCount >= region_.lostCount && rows_.empty() && geResume_ == 0 && submit_device_ge())
+    if (region_.recoveryCount >= region_.lostCount && rows_.empty() && geResume_ == 0 &&
+        (submit_chained() || submit_device_ge()))
         return kDecodePending;
     return decode_loop(packetsOut, countOut);
 }
 
-bool DecoderCore::submit_device_ge()
+bool DecoderCore::submit_device_ge(bool chained)
 {
     const unsigned columns = region_.lostCount;
     const unsigned rows = region_.recoveryCount;
@@ -1305,7 +1309,7 @@ bool DecoderCore::submit_device_ge()
         return false;
     }
     uint32_t base = 0;
-    uint8_t* in = prog_.ge_job(rows, columns, pickLen, &base);
+    uint8_t* in = prog_.ge_job(rows, columns, pickLen, &base, chained);
     GeRow* R = reinterpret_cast<GeRow*>(in);
     GeCol* C = reinterpret_cast<GeCol*>(R + rows);
     uint8_t* pick = reinterpret_cast<uint8_t*>(C + columns);
@@ -1345,16 +1349,146 @@ bool DecoderCore::submit_device_ge()
             g.pickOff = rec->elementStart - pickLo;
         }
     }
-    const uint32_t words = ge_result_words(rows, columns);
+    const uint32_t words = ge_result_words(rows, columns, chained);
     prog_.on_complete([r = res_, base, words](const uint32_t* results) {
         std::lock_guard<std::mutex> g(r->mu);
         r->geOut.assign(results + base, results + base + words);
         r->geDone = true;
     });
-    geState_ = 1;
+    geState_ = chained ? 2 : 1;
+    EngineStats& st = eng_->shard().stats;
+    st.geJobs++;
+    st.geChained += chained ? 1 : 0;
     geRows_ = rows;
     geCols_ = columns;
+    geBase_ = base;
     return true;
+}
+
+// A block decode on the device in one submission.  The first attempt on a
+// square matrix (as many recovery rows as lost columns) of Siamese rows of one
+// length: whatever pivot order the elimination takes, it uses every row, and
+// rows of one length never grow in MultiplyLowerTriangle, so the elimination
+// of received data (EliminateOriginalData, SiameseDecoder.cpp:812-1063) and
+// the solve's layout do not depend on the coefficients.  Both are queued now,
+// gated on the job's outcome word (every op the elimination of received data
+// emits -- row batches with their sum updates, Cauchy rows, sum growth -- and
+// the solve run only if the device elimination succeeds; otherwise the
+// host's sums go back to their state before it, chain_sums_restore), and the
+// job writes the solve's coefficients and row order itself.  The host side of
+// BackSubstitution waits for finish_chained.  Siamese rows of wide LDPC sums
+// are not chained (their k_ldpc items are not gated).
+bool DecoderCore::submit_chained()
+{
+    const unsigned columns = region_.lostCount;
+    const unsigned rows = region_.recoveryCount;
+    if (mirror_ || rows != columns || columns == 0 || columns > kGeMaxCols)
+        return false;
+    const RecPacket* r = region_.first;
+    const unsigned bytes = r->bytes;
+    for (unsigned i = 0; i < rows; ++i, r = r->next)
+        if ((r->meta.sumCount > kCauchyThreshold && r->meta.ldpcCount >= kLdpcSplitMin) || r->bytes != bytes)
+            return false;
+    if (!submit_device_ge(true))
+        return false;
+    pivots_.resize(rows);
+    for (unsigned i = 0; i < rows; ++i) {
+        rows_[i].used = true;
+        pivots_[i] = i;
+    }
+    const uint32_t okWord = geBase_ + 3;   // (ops.h GeDesc: 1 once eliminated)
+    for (unsigned l = 0; l < kLanes; ++l)
+        for (unsigned k = 0; k < kSums; ++k)
+            chainSums_.lanes[l][k] = lanes_[l][k];
+    chainSums_.columnStart = sumColumnStart_;
+    chainSums_.columnCount = sumColumnCount_;
+    chainSums_.recoveredColumns = recoveredColumns_;
+    chainReleases_.clear();
+    prog_.gate_begin(okWord);
+    deferAccount_ = true;
+    deferRelease_ = true;
+    deferredBytes_ = 0;
+    chainElimFailed_ = !eliminate_original_data();
+    deferAccount_ = false;
+    deferRelease_ = false;
+    prog_.gate_end();
+    chainSlot_ = ~0u;
+    chainBytes_ = bytes;
+    if (!chainElimFailed_) {
+        unsigned slot = 0;
+        if (solve_plan(okWord + 1, &slot))
+            chainSlot_ = slot;
+        else
+            chainElimFailed_ = true;   // (an arena failure: disabled_ is set)
+    }
+    return true;
+}
+
+SiameseResult DecoderCore::finish_chained(SiameseOriginalPacket** packetsOut, unsigned* countOut)
+{
+    const unsigned columns = geCols_;
+    const uint32_t* o = geOut_.data();
+    const bool ok = o[3] != 0;
+    auto drop_solve = [&] {
+        // the planned solve did not run (or is not wanted): its slot goes
+        // back without touching the decoder's state
+        if (chainSlot_ == ~0u)
+            return;
+        std::lock_guard<std::mutex> g(res_->mu);
+        PendingDecode& pd = res_->pend[chainSlot_];
+        if (pd.done)
+            ++appliedCount_;   // (its completion counted in doneCount)
+        pd.live = pd.done = pd.held = false;
+        pendingSolves_--;
+        chainSlot_ = ~0u;
+    };
+    if (dead()) {
+        drop_solve();
+        chain_sums_commit();
+        return Siamese_Disabled;
+    }
+    if (!ok) {
+        // a singular matrix: nothing gated ran (the elimination of received
+        // data, its sum updates, the solve).  The sums go back to their state
+        // before it, the host repeats the elimination (the resumable state
+        // the reference keeps for the next attempt) and the search goes on
+        // as decode() does.
+        drop_solve();
+        chain_sums_restore();
+        eng_->shard().stats.geRetried++;
+        matrix_reset();
+        return decode_loop(packetsOut, countOut);
+    }
+    chain_sums_commit();
+    // the device's muladds: the elimination's, the rows' (deferred), the
+    // lower triangle's (MultiplyLowerTriangle: rows of one length, non-zero
+    // multipliers x that length)
+    eng_->account(((uint64_t)o[2] << 32) | o[1]);
+    eng_->account(deferredBytes_);
+    eng_->account((uint64_t)o[4] * chainBytes_, 0, true);
+    if (chainElimFailed_) {
+        drop_solve();
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    const uint8_t* piv = reinterpret_cast<const uint8_t*>(o + ge_out_pivots(geRows_));
+    scratchRec_.resize(columns);
+    scratchLen_.resize(columns);
+    for (unsigned i = 0; i < columns; ++i) {
+        pivots_[i] = piv[i];
+        scratchRec_[i] = rows_[piv[i]].rec;
+        scratchLen_[i] = chainBytes_;
+    }
+    const unsigned slot = chainSlot_;
+    chainSlot_ = ~0u;
+    const SiameseResult res = solve_publish(slot);
+    settle();   // (its completion has arrived: the exact lengths)
+    region_reset();
+    if (res == Siamese_Success && packetsOut) {
+        *packetsOut = recovered_.data();
+        *countOut = (unsigned)recovered_.size();
+    }
+    return res;
 }
 
 SiameseResult DecoderCore::finish_device_ge(SiameseOriginalPacket** packetsOut, unsigned* countOut)
@@ -1367,6 +1501,12 @@ SiameseResult DecoderCore::finish_device_ge(SiameseOriginalPacket** packetsOut, 
             // reference's EmergencyDisabled would, instead of pending forever.
             if (!dead())
                 return kDecodePending;   // (its flush has not completed yet)
+            if (geState_ == 2 && chainSlot_ != ~0u) {
+                PendingDecode& pd = res_->pend[chainSlot_];
+                pd.live = pd.done = pd.held = false;
+                pendingSolves_--;
+                chainSlot_ = ~0u;
+            }
             geState_ = 0;
             if (packetsOut) {
                 *packetsOut = nullptr;
@@ -1377,12 +1517,15 @@ SiameseResult DecoderCore::finish_device_ge(SiameseOriginalPacket** packetsOut, 
         geOut_.swap(res_->geOut);
         res_->geDone = false;
     }
+    const bool chained = geState_ == 2;
     geState_ = 0;
     settle();
     if (packetsOut) {
         *packetsOut = nullptr;
         *countOut = 0;
     }
+    if (chained)
+        return finish_chained(packetsOut, countOut);
     if (dead())
         return Siamese_Disabled;
     const unsigned rows = geRows_, columns = geCols_;
@@ -1413,6 +1556,41 @@ SiameseResult DecoderCore::finish_device_ge(SiameseOriginalPacket** packetsOut, 
         *countOut = (unsigned)recovered_.size();
     }
     return res;
+}
+
+void DecoderCore::chain_sums_commit()
+{
+    for (DevBuf& b : chainReleases_)
+        eng_->release(b);
+    chainReleases_.clear();
+}
+
+void DecoderCore::chain_sums_restore()
+{
+    // buffers the elimination allocated (grown sums) go back; the ones it
+    // replaced are the snapshot's again
+    auto in_snapshot = [&](const uint8_t* p) {
+        for (unsigned l = 0; l < kLanes; ++l)
+            for (unsigned k = 0; k < kSums; ++k)
+                if (chainSums_.lanes[l][k].d.buf.ptr == p)
+                    return true;
+        return false;
+    };
+    for (DevBuf& b : chainReleases_)
+        if (b && !in_snapshot(b.ptr))
+            eng_->release(b);
+    chainReleases_.clear();
+    for (unsigned l = 0; l < kLanes; ++l)
+        for (unsigned k = 0; k < kSums; ++k) {
+            Sum& S = lanes_[l][k];
+            if (S.d.buf && !in_snapshot(S.d.buf.ptr))
+                eng_->release(S.d.buf);
+            S = chainSums_.lanes[l][k];
+        }
+    sumColumnStart_ = chainSums_.columnStart;
+    sumColumnCount_ = chainSums_.columnCount;
+    recoveredColumns_ = chainSums_.recoveredColumns;
+    ++scanEpoch_;   // (get_sum's lane walks were of the discarded state)
 }
 
 // ---------------------------------------------------------------------------
@@ -1778,7 +1956,7 @@ bool DecoderCore::eliminate_original_data()
                     continue;
                 const uint8_t y = m.row == 0 ? 1 : cauchy_element(m.row - 1, o.column % kCauchyMaxColumns);
                 prog_.lc_term(o.buf.addr(), std::min(o.bytes, rb), y);
-                eng_->account(std::min(o.bytes, rb));
+                account_elim(std::min(o.bytes, rb));
             }
             prog_.lc_end();
             continue;
@@ -1855,7 +2033,7 @@ bool DecoderCore::eliminate_original_data()
         cover(windowLo_, ee);
         prog_.rows_row(sums, rec->buf.addr(), rb, rb, row_value(m.row), mask[0], mask[1], m.row,
                        m.ldpcCount, es, ee, nullptr, 0, tableVersion);
-        eng_->account(opBytes);
+        account_elim(opBytes);
     }
     // the window snapshot must not see this decode's recoveries
     prog_.rows_seal();
@@ -1866,6 +2044,16 @@ bool DecoderCore::eliminate_original_data()
 // Lower-triangle multiply + back-substitution (:1065-1238) as one device solve
 
 SiameseResult DecoderCore::solve_and_substitute()
+{
+    unsigned slot = 0;
+    if (!solve_plan(0, &slot)) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    return solve_publish(slot);
+}
+
+bool DecoderCore::solve_plan(uint32_t gateWord, unsigned* slotOut)
 {
     const unsigned m = region_.lostCount;
     // (scratch vectors are members: a decode allocates nothing once warm)
@@ -1893,11 +2081,14 @@ SiameseResult DecoderCore::solve_and_substitute()
     if (equal) {
         // rows of one length (a block of equal packets) never grow: the
         // lower step's source bytes are that length per non-zero multiplier
-        // below the diagonal, counted a row at a time
-        uint64_t nz = 0;
-        for (unsigned j = 1; j < m; ++j)
-            nz += gf_count_nonzero(mrow(pivots_[j]), j);
-        lowerOpBytes = nz * (m ? len[0] : 0);
+        // below the diagonal, counted a row at a time (a chained solve's by
+        // its device elimination, finish_chained)
+        if (!gateWord) {
+            uint64_t nz = 0;
+            for (unsigned j = 1; j < m; ++j)
+                nz += gf_count_nonzero(mrow(pivots_[j]), j);
+            lowerOpBytes = nz * (m ? len[0] : 0);
+        }
         for (unsigned i = 0; i + 1 < m; ++i)
             desc[i].lowerLen = len[i];
     } else {
@@ -1912,7 +2103,8 @@ SiameseResult DecoderCore::solve_and_substitute()
             }
         }
     }
-    eng_->account(lowerOpBytes, 0, true);
+    if (lowerOpBytes)
+        eng_->account(lowerOpBytes, 0, true);
     if (m > 0)
         desc[m - 1].lowerLen = len[m - 1];
 
@@ -1921,10 +2113,8 @@ SiameseResult DecoderCore::solve_and_substitute()
         RecPacket* r = pr[i];
         if (len[i] > r->buf.cap) {
             DevBuf nb = eng_->alloc(len[i]);
-            if (!nb) {
-                disabled_ = true;
-                return Siamese_Disabled;
-            }
+            if (!nb)
+                return false;
             prog_.lc_begin(nb.addr(), desc[i].initBytes, 0);
             prog_.lc_term(r->buf.addr(), desc[i].initBytes, 1);
             prog_.lc_end();
@@ -1935,20 +2125,18 @@ SiameseResult DecoderCore::solve_and_substitute()
         desc[i].finalBytes = len[i];
         maxBytes = std::max(maxBytes, len[i]);
     }
-    for (unsigned j = 0; j < m; ++j)
-        std::memcpy(coefOut + (size_t)j * m, mrow(pivots_[j]), m);
+    // (a chained solve's coefficients come from its device elimination)
+    if (!gateWord)
+        for (unsigned j = 0; j < m; ++j)
+            std::memcpy(coefOut + (size_t)j * m, mrow(pivots_[j]), m);
 
-    const uint32_t base = prog_.solve_commit(maxBytes);
+    const uint32_t base = prog_.solve_commit(maxBytes, gateWord);
 
-    // Host side of BackSubstitution: swap buffers into the window, record
-    // the outputs (exact lengths arrive with the completion, complete_solve).
-    bool advanced = false;
+    // a slot for this solve's completion state; a chained solve's is held
+    // (apply_resolved leaves it alone) until solve_publish
     unsigned slot = 0;
     {
         std::lock_guard<std::mutex> g(res_->mu);
-        recovered_.resize(m);
-        ++decodeSerial_;
-        // a free slot for this solve's completion state
         std::vector<PendingDecode>& pend = res_->pend;
         while (slot < pend.size() && pend[slot].live)
             ++slot;
@@ -1957,11 +2145,36 @@ SiameseResult DecoderCore::solve_and_substitute()
         PendingDecode& pd = pend[slot];
         pd.live = true;
         pd.done = false;
+        pd.held = gateWord != 0;
         pd.base = base;
         pd.m = m;
-        pd.serial = decodeSerial_;
+        pd.serial = ~0ull;   // (no output array of its own until published)
         pd.words.clear();
         pd.targets.clear();
+        pd.fixes.clear();
+    }
+    pendingSolves_++;
+    // (the back-substitution's reference source bytes need the recovered
+    // lengths: the solve kernel counts them, SiameseDecoder.cpp:1131-1212)
+    prog_.on_complete([r = res_, slot](const uint32_t* results) { complete_solve(*r, slot, results); });
+    *slotOut = slot;
+    return true;
+}
+
+SiameseResult DecoderCore::solve_publish(unsigned slot)
+{
+    const unsigned m = region_.lostCount;
+    const std::vector<RecPacket*>& pr = scratchRec_;
+    const std::vector<unsigned>& len = scratchLen_;
+    // Host side of BackSubstitution: swap buffers into the window, record
+    // the outputs (exact lengths arrive with the completion, complete_solve).
+    bool advanced = false;
+    {
+        std::lock_guard<std::mutex> g(res_->mu);
+        recovered_.resize(m);
+        ++decodeSerial_;
+        PendingDecode& pd = res_->pend[slot];
+        pd.serial = decodeSerial_;
         std::vector<Fix>& fixes = pd.fixes;
         fixes.clear();
         for (int ci = (int)m - 1; ci >= 0; --ci) {
@@ -1992,12 +2205,15 @@ SiameseResult DecoderCore::solve_and_substitute()
         if (mirror_)   // (download_recovered's list: the drop-in API only)
             lastDecoded_ = fixes;
         publish_outputs();
+        if (pd.held) {
+            // a chained solve: its completion already arrived
+            pd.held = false;
+            if (pd.done && !mirror_)
+                for (unsigned ci = 0; ci < m; ++ci)
+                    fill_entry(pd, ci, recovered_[ci]);
+        }
     }
     lastPendSlot_ = slot;
-    pendingSolves_++;
-    // (the back-substitution's reference source bytes need the recovered
-    // lengths: the solve kernel counts them, SiameseDecoder.cpp:1131-1212)
-    prog_.on_complete([r = res_, slot](const uint32_t* results) { complete_solve(*r, slot, results); });
 
     if (!advanced) {
         disabled_ = true;
@@ -2055,7 +2271,7 @@ void DecoderCore::apply_resolved()
     std::vector<PendingDecode>& pend = res_->pend;
     for (unsigned k = 0; k < pend.size(); ++k) {
         PendingDecode& pd = pend[k];
-        if (!pd.live || !pd.done)
+        if (!pd.live || !pd.done || pd.held)
             continue;
         const unsigned m = pd.m;
         const unsigned okCount = pd.words[0];

@@ -141,7 +141,11 @@ public:
     /// device (sgpu_decode_device): returns kDecodePending after queueing the
     /// matrix job; the next call after the flush that ran it finishes the
     /// decode as decode() would have (an elimination that stopped short is
-    /// repeated on the host, which keeps the resumable state).
+    /// repeated on the host, which keeps the resumable state).  A square
+    /// matrix of Siamese rows of one length (a block decode) is chained: the
+    /// elimination of received data and the solve go into the same
+    /// submission, gated on the device elimination's outcome, so the call
+    /// after the flush returns the recovered packets with their lengths.
     SiameseResult decode_device(SiameseOriginalPacket** packetsOut, unsigned* countOut);
     /// A device matrix job is queued and not yet finished by decode_device.
     bool ge_pending() const { return geState_ != 0; }
@@ -262,11 +266,55 @@ private:
     /// elimination of received data and the solve
     SiameseResult finish_region(bool solved);
     /// decode_device's two halves
-    bool submit_device_ge();
+    bool submit_device_ge(bool chained = false);
     SiameseResult finish_device_ge(SiameseOriginalPacket** packetsOut, unsigned* countOut);
-    unsigned geState_ = 0;               // 1: a device matrix job is queued
+    /// The chained form (decode_device): the job, the gated elimination of
+    /// received data and the gated solve in one submission; its finish
+    bool submit_chained();
+    SiameseResult finish_chained(SiameseOriginalPacket** packetsOut, unsigned* countOut);
+    unsigned geState_ = 0;               // 1: a device matrix job is queued; 2: a chained one
     unsigned geRows_ = 0, geCols_ = 0;   // ... of this size
+    uint32_t geBase_ = 0;                // ... and its first result word
     std::vector<uint32_t> geOut_;        // its output (ops.h GeDesc)
+    // the chained decode's deferred accounting (its rows' reference bytes,
+    // counted only once the device elimination succeeded) and its solve
+    bool deferAccount_ = false;
+    uint64_t deferredBytes_ = 0;
+    bool chainElimFailed_ = false;       // eliminate_original_data refused (Disabled if the job succeeds)
+    unsigned chainSlot_ = 0;             // its solve's Resolver::pend slot
+    unsigned chainBytes_ = 0;            // its rows' common length
+    void account_elim(uint64_t bytes)
+    {
+        if (deferAccount_)
+            deferredBytes_ += bytes;
+        else
+            eng_->account(bytes);
+    }
+    // The decoder's sums as they stood before a chained elimination of
+    // received data: restored if the device elimination fails (the gated sum
+    // updates did not run), so the host is in the reference's state for the
+    // retry.  Sum buffers the elimination replaced are released only once
+    // the outcome is known.
+    struct SumState
+    {
+        Sum lanes[kLanes][kSums];
+        unsigned columnStart = 0, columnCount = 0;
+        std::vector<unsigned> recoveredColumns;
+    };
+    SumState chainSums_;
+    bool deferRelease_ = false;
+    std::vector<DevBuf> chainReleases_;
+    void release_sum_buf(DevBuf& b)
+    {
+        if (deferRelease_) {
+            chainReleases_.push_back(b);
+            b = DevBuf();
+        } else {
+            eng_->release(b);
+        }
+    }
+    void chain_sums_commit();    // the elimination ran: release what it replaced
+    void chain_sums_restore();   // it did not: back to chainSums_
     bool generate_matrix();
     void populate_columns(unsigned oldColumns, unsigned newColumns);
     void populate_rows(unsigned oldRows, unsigned newRows);
@@ -280,6 +328,13 @@ private:
 
     bool eliminate_original_data();
     SiameseResult solve_and_substitute();
+    /// solve_and_substitute's halves: the device solve (rows in pivots_
+    /// order; gateWord: 1 + the chained job's outcome word, whose solve then
+    /// takes the job's coefficients, ops.h GeDesc) and its Resolver slot;
+    /// then the host side of BackSubstitution (the window takes the
+    /// recovered buffers).  solve_plan returns false on an arena failure.
+    bool solve_plan(uint32_t gateWord, unsigned* slotOut);
+    SiameseResult solve_publish(unsigned slot);
 
     bool add_single(const RowMeta& m, const uint8_t* headBytes, unsigned payloadBytes,
                     const void* hostData, uint64_t devData, Program* producer);
@@ -376,6 +431,7 @@ private:
         uint64_t serial = 0;
         bool live = false;            // queued, not yet applied to the decoder's slots
         bool done = false;            // the completion arrived: `words` holds the results
+        bool held = false;            // a chained solve not yet published (apply_resolved skips it)
         std::vector<uint32_t> words;  // [0] rows recovered, [1 + ci] header << 29 | length
         /// caller-owned outputs to fill at completion (deferred API): (ci, entry)
         std::vector<std::pair<unsigned, SiameseOriginalPacket*>> targets;

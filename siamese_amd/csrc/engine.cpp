@@ -45,6 +45,9 @@ void EngineStats::add(const EngineStats& o)
     reclaimNs += o.reclaimNs;
     execLaunches += o.execLaunches;
     execUniqueBytes += o.execUniqueBytes;
+    geJobs += o.geJobs;
+    geChained += o.geChained;
+    geRetried += o.geRetried;
 }
 
 namespace {
@@ -106,6 +109,7 @@ void ProgramBody::clear()
     rb.rows.clear();
     copies.clear();
     lcb.clear();
+    gateOpen = false;
 }
 
 void ProgramBody::new_segment()
@@ -598,7 +602,7 @@ void Program::solve_reserve(unsigned m, SolveRow** rows, uint8_t** coef)
     *coef = ps.coef.data();
 }
 
-uint32_t Program::solve_commit(uint32_t maxBytes)
+uint32_t Program::solve_commit(uint32_t maxBytes, uint32_t gateWord)
 {
     ProgramBody::PendingSolve& ps = b_->solves[b_->nsolves++];
     const size_t m = ps.rows.size();
@@ -638,6 +642,11 @@ uint32_t Program::solve_commit(uint32_t maxBytes)
     eng_->release(head);   // (reused only after this submission completes)
     ps.desc.m = (uint32_t)m;
     ps.desc.maxBytes = maxBytes;
+    ps.desc.gate = gateWord;
+    if (gateWord && b_->nges) {
+        ProgramBody::PendingGe& g = b_->ges[b_->nges - 1];
+        g.solve = (uint32_t)(b_->nsolves - 1);
+    }
     ps.desc.result = b_->resultWords;
     b_->resultWords += ps.desc.m + 2;
     const uint32_t r = ps.desc.result;
@@ -645,7 +654,30 @@ uint32_t Program::solve_commit(uint32_t maxBytes)
     return r;
 }
 
-uint8_t* Program::ge_job(unsigned rows, unsigned cols, unsigned pickLen, uint32_t* resultWord)
+void Program::gate_begin(uint32_t word)
+{
+    touch();
+    b_->rows_close();   // (ops queued before stay ungated)
+    if (b_->nsegs == 0)
+        b_->new_segment();
+    b_->gateOpen = true;
+    b_->gateSeg = b_->nsegs - 1;
+    b_->gateOp = (uint32_t)b_->segs[b_->nsegs - 1].ops.size();
+    b_->gateWord = word;
+}
+
+void Program::gate_end()
+{
+    if (!b_ || !b_->gateOpen)
+        return;
+    b_->rows_close();
+    b_->gateOpen = false;
+    ProgramBody::Segment& s = b_->segs[b_->gateSeg];
+    if (b_->gateSeg + 1 == b_->nsegs && s.ops.size() > b_->gateOp)
+        s.gates.push_back(ProgramBody::Segment::Gate{b_->gateOp, (uint32_t)s.ops.size(), b_->gateWord});
+}
+
+uint8_t* Program::ge_job(unsigned rows, unsigned cols, unsigned pickLen, uint32_t* resultWord, bool chained)
 {
     touch();
     if (b_->nges == b_->ges.size())
@@ -655,7 +687,9 @@ uint8_t* Program::ge_job(unsigned rows, unsigned cols, unsigned pickLen, uint32_
     g.cols = (uint16_t)cols;
     g.pickLen = pickLen;
     g.result = b_->resultWords;
-    b_->resultWords += ge_result_words(rows, cols);
+    g.chained = chained;
+    g.solve = 0;
+    b_->resultWords += ge_result_words(rows, cols, chained);
     g.in.resize(ge_input_bytes(rows, cols, pickLen));
     *resultWord = g.result;
     return g.in.data();
@@ -1327,6 +1361,7 @@ struct SegRef
     uint32_t tilesPerItem = 1;      // tiles one k_exec workgroup runs
     uint32_t wideBase = 0;          // first k_ldpc item of its wide rows
     uint64_t wideOff = 0;           // their scratch (bytes into the set's wideDev)
+    uint32_t resultBase = 0;        // its body's first result word (gated batches)
 };
 
 } // namespace
@@ -1344,6 +1379,8 @@ struct Batch
     uint32_t maxIngest = 0;
     size_t oIngD = 0, oIngB = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
     size_t oGeD = 0, oGeIn = 0, nGe = 0;   // device matrix jobs: descs, inputs
+    uint32_t geMaxRows = 0, geMaxCols = 0;  // ... their largest matrix (k_ge's LDS)
+    bool geChained = false;                 // a job writes into the upload (kGeChained)
     size_t oCopy = 0;                      // the download copy list (BeCopy records)
     uint64_t wideBase = 0;                 // this submission's k_ldpc scratch: bytes into the ring
     bool wideZero = false;                 // the ring wrapped: zero it before the first exec launch
@@ -1932,7 +1969,8 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         for (size_t k = 0; k < maxSegs; ++k) {
             Phase ex{Phase::EXEC, nItems, 0, 0, 0, kNoRows};
             const size_t segBegin = segs.size();
-            for (ProgramBody* p : bt.bodies[g]) {
+            for (size_t pi = 0; pi < bt.bodies[g].size(); ++pi) {
+                const ProgramBody* p = bt.bodies[g][pi];
                 if (k >= p->nsegs)
                     continue;
                 const ProgramBody::Segment& s = p->segs[k];
@@ -1943,6 +1981,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                         ex.maxRows = ex.maxRows == kNoRows ? op.valid : std::max(ex.maxRows, op.valid);
                 const size_t words = kOpWords * s.ops.size() + s.terms.size() + s.rowsWords;
                 segs.push_back(SegRef{&s, (uint32_t)nWords, (uint32_t)words, 0});
+                segs.back().resultBase = bt.resultBase[g][pi];
                 nOps += s.ops.size();
                 nTerms += s.terms.size();
                 nWords += words;
@@ -1976,7 +2015,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 }
                 const double avg = phaseTiles ? words / (double)phaseTiles : 0.0;   // words per tile
                 const size_t tpi = std::min<size_t>(
-                    0xffff, std::max<size_t>(1, (phaseTiles + SGPU_EXEC_GROUPS - 1) / SGPU_EXEC_GROUPS));
+                    kExecRunMax, std::max<size_t>(1, (phaseTiles + SGPU_EXEC_GROUPS - 1) / SGPU_EXEC_GROUPS));
                 uint32_t ib = (uint32_t)ex.itemBegin;
                 for (size_t i = segBegin; i < segs.size(); ++i) {
                     const size_t tiles = (segs[i].seg->maxExtent + kExecTileBytes - 1) / kExecTileBytes;
@@ -2014,8 +2053,12 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 const ProgramBody::PendingSolve& ps = p->solves[k];
                 SolveDesc d = ps.desc;
                 d.result += bt.resultBase[g][pi];
+                if (d.gate)
+                    d.gate += bt.resultBase[g][pi];
                 d.rowBegin = (uint32_t)nSolveRows;
                 d.coefOffset = nCoef;
+                ps.asmRow = (uint32_t)nSolveRows;
+                ps.asmCoef = (uint32_t)nCoef;
                 srefs.push_back(SolveRef{&ps, nSolveRows, nCoef});
                 nSolveRows += ps.rows.size();
                 nCoef += ps.coef.size();
@@ -2071,11 +2114,20 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
             for (size_t k = 0; k < p->nges; ++k) {
                 const ProgramBody::PendingGe& ge = p->ges[k];
                 GeDesc d;
+                std::memset(&d, 0, sizeof(d));
                 d.in = (uint32_t)geInBytes;
                 d.result = ge.result + bt.resultBase[g][pi];
                 d.rows = ge.rows;
                 d.cols = ge.cols;
                 d.pickLen = ge.pickLen;
+                if (ge.chained && ge.solve < p->nsolves) {
+                    d.flags = kGeChained;
+                    d.solveRow = p->solves[ge.solve].asmRow;
+                    d.solveCoef = p->solves[ge.solve].asmCoef;
+                    bt.geChained = true;
+                }
+                bt.geMaxRows = std::max<uint32_t>(bt.geMaxRows, ge.rows);
+                bt.geMaxCols = std::max<uint32_t>(bt.geMaxCols, ge.cols);
                 gdescs.push_back(d);
                 grefs.push_back(GeRef{&ge, geInBytes});
                 geInBytes = align16(geInBytes + ge.in.size());
@@ -2145,7 +2197,9 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     // on the latency-bound paths (SIAMESE_AMD_ZEROCOPY_UP bytes at most,
     // default 32 KiB; 0 disables).
     constexpr size_t kZeroCopyUp = 32768;
-    bt.upBase = (xs.upHostDev && bt.upBytes <= kZeroCopyUp) ? xs.upHostDev : xs.upDev;
+    // (a chained matrix job writes its solve's rows and coefficients into
+    // the upload: the device copy then)
+    bt.upBase = (xs.upHostDev && bt.upBytes <= kZeroCopyUp && !bt.geChained) ? xs.upHostDev : xs.upDev;
     if (wideBytes + tBytes) {
         // k_ldpc scratch comes from the set's ring, which is zeroed as a whole
         // when it wraps (not per submission: most flushes then need no memset);
@@ -2206,9 +2260,18 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 size_t wi = 0;                                      // next wide row
                 LdpcItem* wItem = (LdpcItem*)(up + bt.oWide) + r.wideBase;
                 uint64_t wOff = bt.wideBase + r.wideOff;
+                size_t gi = 0;   // next gated range
                 for (uint32_t oi = 0; oi < (uint32_t)s.ops.size(); ++oi) {
                     const GfOp& op = s.ops[oi];
                     std::memcpy(w, &op, sizeof(GfOp));
+                    if (op.kind != OP_LITERAL) {
+                        // termBegin on the device: the op's gate, 1 + a result
+                        // word (ops.h GeDesc), or 0
+                        while (gi < s.gates.size() && s.gates[gi].opEnd <= oi)
+                            ++gi;
+                        const bool gated = gi < s.gates.size() && s.gates[gi].opBegin <= oi;
+                        reinterpret_cast<GfOp*>(w)->termBegin = gated ? 1u + s.gates[gi].word + r.resultBase : 0u;
+                    }
                     w += sizeof(GfOp);
                     if (op.kind == OP_ROWS || op.kind == OP_COPIES || op.kind == OP_LINCOMBS) {
                         const size_t bytes = (size_t)op.termCount * 16;   // block (rows_close)
@@ -2256,7 +2319,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 uint32_t n = 0;
                 for (uint32_t t = 0; t < tiles; t += r.tilesPerItem)
                     items[n++] = ExecItem{r.wordBase, r.words, nOpsSeg,
-                                          t | std::min(r.tilesPerItem, tiles - t) << 16};
+                                          exec_tiles(t, std::min(r.tilesPerItem, tiles - t))};
             }
         } else if (t.kind == 3) {
             for (size_t i = t.a; i < t.b; ++i)
@@ -2361,7 +2424,8 @@ void Engine::launch_batch(Batch& bt)
     if (bt.wideZero)
         be_memset(xs.wideDev, 0, xs.wideCap);
     if (bt.nGe)
-        be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev);
+        be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev,
+                     (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols);
     // k_ldpc items of every exec phase before the first solve go in one
     // launch (they read only window elements that exist before the flush's
     // first solve); a phase after a solve launches its own
@@ -2376,7 +2440,7 @@ void Engine::launch_batch(Batch& bt)
                 be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide) + ph.wideBegin, (uint32_t)ph.wideCount,
                                acctDev + 3);
             be_launch_exec(bt.upBase + bt.oStream, (const ExecItem*)(bt.upBase + bt.oItems) + ph.itemBegin,
-                           (uint32_t)ph.itemCount, acctDev, ph.maxRows);
+                           (uint32_t)ph.itemCount, acctDev, resultsDev, ph.maxRows);
             st.execLaunches++;
         } else {
             // solve items index solves globally; pass the global desc base

@@ -23,6 +23,8 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <deque>
 #include <functional>
 #include <memory>
@@ -46,7 +48,12 @@ namespace sgpu {
 /// profiles/r5k_dropin_calls_16threads.txt).  A writer raises its flag and
 /// waits for every slot to drain; readers that see the flag step back and
 /// wait for it to drop.  Never taken shared twice by one thread (a waiting
-/// writer would block the second acquisition).
+/// writer would block the second acquisition): builds with SGPU_DEBUG_LOCKS
+/// abort on a nested shared acquisition (tests/instance_lock_test.cpp is
+/// built so).  Unlike glibc's rwlock it is not re-entrant and prefers the
+/// writer, so no instance call may wait on a flush while it holds the lock
+/// shared (the flush's detach takes it exclusively): the decoder and encoder
+/// mirror paths return kNeedsFlush instead and flush outside it.
 class InstanceLock
 {
 public:
@@ -84,6 +91,7 @@ public:
     }
     void lock_shared()
     {
+        debug_enter();
         std::atomic<int>& n = slot();
         for (;;) {
             n.fetch_add(1, std::memory_order_seq_cst);
@@ -95,16 +103,40 @@ public:
     }
     bool try_lock_shared()
     {
+        debug_enter();
         std::atomic<int>& n = slot();
         n.fetch_add(1, std::memory_order_seq_cst);
         if (writer_.load(std::memory_order_seq_cst) == 0)
             return true;
         n.fetch_sub(1, std::memory_order_seq_cst);
+        debug_leave();
         return false;
     }
-    void unlock_shared() { slot().fetch_sub(1, std::memory_order_release); }
+    void unlock_shared()
+    {
+        slot().fetch_sub(1, std::memory_order_release);
+        debug_leave();
+    }
 
 private:
+#ifdef SGPU_DEBUG_LOCKS
+    static int& depth()
+    {
+        thread_local int d = 0;
+        return d;
+    }
+    static void debug_enter()
+    {
+        if (depth()++ != 0) {
+            std::fprintf(stderr, "InstanceLock: nested shared acquisition\n");
+            std::abort();
+        }
+    }
+    static void debug_leave() { --depth(); }
+#else
+    static void debug_enter() {}
+    static void debug_leave() {}
+#endif
     static constexpr unsigned kSlots = 64;
     struct alignas(64) Slot
     {
@@ -207,6 +239,15 @@ struct ProgramBody
         std::vector<Wide> wide;
         uint32_t wideItems = 0;          // k_ldpc items of those rows
         uint64_t wideBytes = 0;          // scratch bytes of those rows
+        /// Ops gated on a chained matrix job's outcome (ops.h GeDesc
+        /// kGeChained): ops [opBegin, opEnd) run only if the body's result
+        /// word `word` is non-zero (the header's termBegin on the device,
+        /// made absolute at assembly)
+        struct Gate
+        {
+            uint32_t opBegin, opEnd, word;
+        };
+        std::vector<Gate> gates;
         void clear()
         {
             ops.clear();
@@ -217,6 +258,7 @@ struct ProgramBody
             wide.clear();
             wideItems = 0;
             wideBytes = 0;
+            gates.clear();
         }
     };
     /// The OP_ROWS batch under construction (always the segment's last op).
@@ -241,6 +283,9 @@ struct ProgramBody
         SolveDesc desc;
         std::vector<SolveRow> rows;
         std::vector<uint8_t> coef;
+        // where assembly placed its rows and coefficients (a chained matrix
+        // job of the same body writes them there, GeDesc.solveRow/solveCoef)
+        mutable uint32_t asmRow = 0, asmCoef = 0;
     };
     /// A device matrix generation + elimination (ops.h GeDesc): its input
     /// as k_ge reads it and its first result word.
@@ -249,6 +294,8 @@ struct ProgramBody
         uint16_t rows = 0, cols = 0;
         uint32_t pickLen = 0;
         uint32_t result = 0;
+        bool chained = false;   // kGeChained: feeds solves[solve] of the same body
+        uint32_t solve = 0;
         std::vector<uint8_t> in;
     };
 
@@ -262,6 +309,9 @@ struct ProgramBody
     size_t nges = 0;
     std::vector<Completion> callbacks;
     RowsBuild rb;
+    bool gateOpen = false;        // ops from (segment gateSeg, op gateOp) on are gated on gateWord
+    size_t gateSeg = 0;
+    uint32_t gateOp = 0, gateWord = 0;
     std::vector<CopyItem> copies;       // the open OP_COPIES batch (segment's last op)
     /// The open OP_LINCOMBS batch (ops.h): independent combinations waiting
     /// to be sealed as one op after the segment's last op.
@@ -372,16 +422,33 @@ public:
     /// fill; solve_commit queues it (same result word as solve()).  No other
     /// solve may be queued in between.
     void solve_reserve(unsigned m, SolveRow** rows, uint8_t** coef);
-    uint32_t solve_commit(uint32_t maxBytes);
+    /// gateWord (optional, 1 + a result word): the solve runs only if that
+    /// word is non-zero, on the coefficients and row order the program's
+    /// last chained matrix job writes (ge_job chained).
+    uint32_t solve_commit(uint32_t maxBytes, uint32_t gateWord = 0);
 
     /// Queue a device matrix generation + elimination (ops.h GeDesc) of
     /// rows x cols with a pick table of pickLen bytes: returns the job's
     /// input buffer (ge_input_bytes, for the caller to fill before the next
     /// flush) and *resultWord, its first result word (valid in this
-    /// program's completion callbacks).
-    uint8_t* ge_job(unsigned rows, unsigned cols, unsigned pickLen, uint32_t* resultWord);
+    /// program's completion callbacks).  chained (rows == cols): the next
+    /// solve this program queues is the decode's, and the job writes its
+    /// coefficients and row order (solve_commit with the job's gate).
+    uint8_t* ge_job(unsigned rows, unsigned cols, unsigned pickLen, uint32_t* resultWord, bool chained = false);
+    /// Gate every op queued from now until gate_end() on result word `word`:
+    /// they run only if it is non-zero (a chained matrix job's outcome, ops.h
+    /// GeDesc word 3).  No solve and no literal may be queued in between.
+    void gate_begin(uint32_t word);
+    void gate_end();
 
     /// Run `fn(results)` once the flush holding this program's work completes.
+    /// Callbacks of one flush run in registration order on one thread, but
+    /// callbacks of different flushes may run concurrently and out of ticket
+    /// order (an inline flush's caller completes its own submission while the
+    /// completer thread completes the next one; only the tickets' publication
+    /// is ordered).  A callback may therefore touch only state keyed by its
+    /// own submission -- the decoder's Resolver slots under Resolver::mu
+    /// (complete_solve) -- never state a later flush's callback also writes.
     void on_complete(Completion fn);
     /// Forget the completions of work not yet submitted (owner going away).
     void drop_callbacks()
@@ -463,6 +530,9 @@ struct EngineStats
     // set_measure_unique(true) (bench.py's roofline): every distinct source
     // symbol read once, every destination written once, plus the op stream.
     uint64_t execUniqueBytes = 0;
+    // device recovery-matrix jobs (sgpu_decode_device): all, chained into
+    // their decode's submission, chained ones that found a singular matrix
+    uint64_t geJobs = 0, geChained = 0, geRetried = 0;
 
     void add(const EngineStats& o);
 };

@@ -6,6 +6,7 @@
 #pragma once
 
 #include <cstddef>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -58,7 +59,11 @@ private:
 /// caches, so every create and free would take an arena lock -- contended,
 /// since instances are created and freed on different threads).  get()
 /// returns uninitialised storage (construct with placement new); put() takes
-/// storage whose object was destroyed.
+/// storage whose object was destroyed.  A thread keeps at most kLocal blocks;
+/// past that, half of them move to a shared depot (one lock per kBatch
+/// blocks), which a thread whose own stash is empty drains first.  Instances
+/// created on one thread and freed on another therefore circulate instead of
+/// piling up in the freeing thread's stash.
 template <class T>
 class RawPool
 {
@@ -66,6 +71,8 @@ public:
     static void* get()
     {
         Stash& s = stash();
+        if (s.items.empty())
+            refill(s);
         if (!s.items.empty()) {
             void* p = s.items.back();
             s.items.pop_back();
@@ -76,27 +83,66 @@ public:
     static void put(void* p)
     {
         Stash& s = stash();
-        if (s.items.size() < kMax)
-            s.items.push_back(p);
-        else
-            release(p);
+        if (s.items.size() >= kLocal)
+            spill(s);
+        s.items.push_back(p);
     }
 
 private:
-    static constexpr size_t kMax = 1u << 13;
+    static constexpr size_t kLocal = 256;
+    static constexpr size_t kBatch = kLocal / 2;
+    static constexpr size_t kDepotMax = 1u << 14;   // blocks the depot keeps at most
     static void release(void* p)
     {
         ::operator delete(p, std::align_val_t(alignof(T) > 64 ? alignof(T) : 64));
+    }
+    struct Depot
+    {
+        std::mutex mu;
+        std::vector<void*> items;
+    };
+    static Depot& depot()
+    {
+        static Depot* d = new Depot;   // (never destroyed: threads may exit after static teardown)
+        return *d;
     }
     struct Stash
     {
         std::vector<void*> items;
         ~Stash()
         {
-            for (void* p : items)
-                release(p);
+            // back to the depot for the threads still running
+            Depot& d = depot();
+            std::lock_guard<std::mutex> g(d.mu);
+            for (void* p : items) {
+                if (d.items.size() < kDepotMax)
+                    d.items.push_back(p);
+                else
+                    release(p);
+            }
         }
     };
+    static void spill(Stash& s)
+    {
+        Depot& d = depot();
+        std::lock_guard<std::mutex> g(d.mu);
+        for (size_t k = 0; k < kBatch; ++k) {
+            void* p = s.items.back();
+            s.items.pop_back();
+            if (d.items.size() < kDepotMax)
+                d.items.push_back(p);
+            else
+                release(p);
+        }
+    }
+    static void refill(Stash& s)
+    {
+        Depot& d = depot();
+        std::lock_guard<std::mutex> g(d.mu);
+        const size_t n = d.items.size() < kBatch ? d.items.size() : kBatch;
+        s.items.insert(s.items.end(), d.items.end() - (long)n, d.items.end());
+        d.items.resize(d.items.size() - n);
+    }
     static Stash& stash()
     {
         thread_local Stash s;

@@ -65,7 +65,9 @@ static_assert(sizeof(GfTerm) == 16, "GfTerm layout");
 
 /// On the device a segment is one instruction stream of 16-byte words: each
 /// op is its GfOp (2 words) followed, for OP_LINCOMB, by its termCount
-/// GfTerm words (termBegin is unused there).  A workgroup streams through it
+/// GfTerm words.  On the device termBegin is the op's gate (every kind but
+/// OP_LITERAL): 0, or 1 + a result word; the op is skipped when that word is
+/// zero (a chained device elimination that failed, GeDesc kGeChained).  A workgroup streams through it
 /// front to back, so one coalesced prefetch brings an op and its term list.
 constexpr unsigned kOpWords = sizeof(GfOp) / 16;
 
@@ -251,9 +253,17 @@ struct ExecItem
     uint32_t streamBegin;  // first 16-byte word of the segment's stream
     uint32_t streamWords;  // words in the segment's stream
     uint32_t opCount;
-    uint32_t tiles;        // first 256-byte tile | tile count << 16: the workgroup runs the
-                           // op list over each tile (op by op, every tile in turn)
+    uint32_t tiles;        // exec_tiles(first 256-byte tile, tile count): the workgroup runs
+                           // the op list over each tile (op by op, every tile in turn)
 };
+/// ExecItem.tiles: the first tile in the low 24 bits (16M tiles of 256 B:
+/// 4 GiB, past SIAMESE_MAX_PACKET_BYTES), the run's tile count (1..255) in
+/// the high 8.
+constexpr uint32_t kExecRunMax = 255;
+constexpr uint32_t kExecFirstTileMask = 0xffffffu;
+constexpr uint32_t exec_tiles(uint32_t firstTile, uint32_t count) { return firstTile | count << 24; }
+constexpr uint32_t exec_first_tile(uint32_t tiles) { return tiles & kExecFirstTileMask; }
+constexpr uint32_t exec_tile_count(uint32_t tiles) { return tiles >> 24; }
 
 /// Triangular solve of one decode (reference SiameseDecoder.cpp:1065-1238).
 /// Rows are listed in pivot order; coef is an m x m byte matrix with
@@ -278,6 +288,11 @@ struct SolveDesc
                          // product solves' result rows, copied into the rows
                          // by the tile pass unless the solve is flagged (the
                          // rows keep their inputs for the exact sweeps)
+    uint32_t gate;       // 0, or 1 + a result word: the solve runs only if that
+                         // word is non-zero (a chained device elimination's
+                         // outcome, GeDesc kGeChained: its rows and
+                         // coefficients are what k_ge wrote)
+    uint32_t pad;
 };
 
 /// Solves of up to this many rows may run as the product X = T R (their
@@ -303,8 +318,11 @@ struct SolveRow
     uint32_t initBytes;  // Bytes before MultiplyLowerTriangle
     uint32_t lowerLen;   // Bytes when this row is the source of the lower step
     uint32_t finalBytes; // Bytes after MultiplyLowerTriangle
-    uint32_t pad;
+    uint32_t headIndex;  // 1 + the row's slot in SolveDesc.head (0: its own
+                         // index; a chained elimination permutes the rows into
+                         // pivot order after their heads were laid out)
 };
+constexpr uint32_t solve_head_slot(uint32_t headIndex, uint32_t j) { return headIndex ? headIndex - 1u : j; }
 
 /// Result word layout for each recovered row: (headerBytes << 29) | length,
 /// or 0 if the prefix failed validation.  Word 0 holds the number of rows
@@ -373,10 +391,19 @@ inline unsigned solve_tile_bytes(uint32_t m)
 ///   output (GeDesc.result words of the result array, ge_result_words):
 ///     [0] the first pivot whose column has no non-zero left (== cols: the
 ///         matrix was eliminated), [1..2] the elimination's multiplied bytes
-///         (the reference's muladds, u64), [3] 0;
-///     then per row, bytes padded to words: pivots (u8 row index per pivot
-///     position), used (u8 0/1), column counts (u16); then the matrix, rows
-///     x cols bytes in row order.
+///         (the reference's muladds, u64), [3] 1 when [0] == cols, else 0,
+///     [4] the non-zero coefficients below the diagonal of the eliminated
+///         matrix in pivot order (MultiplyLowerTriangle's muladds per row
+///         byte), [5..7] 0;
+///     then the pivots (u8 row index per pivot position, padded to words);
+///     without kGeChained also the used rows (u8 0/1), the column counts
+///     (u16) and the matrix, rows x cols bytes in row order.
+/// kGeChained (rows == cols): the decode's elimination of received data and
+/// its solve were queued in the same submission, gated on word [3] (OP_ROWS
+/// GfOp.termBegin, SolveDesc.gate).  On success the job writes the solve's
+/// coefficients in pivot order (coef + solveCoef, cols x cols) and permutes
+/// the solve's rows (rows + solveRow) into pivot order, each keeping its head
+/// slot (SolveRow.headIndex).
 /// Row kinds: Siamese (dense over [0, jEnd) from the row's opcodes, then
 /// 2*ceil(ldpcN/16) PCG picks over [pickOff, pickOff + ldpcN)), Cauchy
 /// (1/((rbase) ^ ccol) over [0, jEnd)) and parity (1 over [0, jEnd)).
@@ -386,7 +413,13 @@ struct GeDesc
     uint32_t result;    // first result word
     uint16_t rows, cols;
     uint32_t pickLen;
+    uint32_t flags;     // kGeChained
+    uint32_t solveRow;  // kGeChained: the solve's first SolveRow
+    uint32_t solveCoef; // kGeChained: its coefficients' byte offset
+    uint32_t pad;
 };
+static_assert(sizeof(GeDesc) == 32, "GeDesc layout");
+constexpr uint32_t kGeChained = 1;
 
 enum : uint8_t
 {
@@ -413,24 +446,30 @@ struct GeCol
     uint8_t ccol;        // column % kCauchyMaxColumns
 };
 
-/// Device elimination limits (LDS-resident matrix of one workgroup).
-constexpr unsigned kGeMaxCols = 128;
-constexpr unsigned kGeMaxRows = 192;
+/// Device elimination limits (LDS-resident matrix of one wave): the
+/// reference's 255 lost columns (SiameseCommon.h:80, kMaximumLossRecoveryCount)
+/// and up to 256 recovery rows.
+constexpr unsigned kGeMaxCols = 255;
+constexpr unsigned kGeMaxRows = 256;
 constexpr unsigned kGeMaxPick = 65535;
 constexpr uint8_t kGeNoColumn = 0xff;
+/// k_ge's LDS row stride in dwords: odd, so the rows a wave's lanes own
+/// start in different banks.
+constexpr uint32_t ge_stride_words(uint32_t cols) { return ((cols + 3u) / 4u) | 1u; }
 
 constexpr uint32_t ge_input_bytes(uint32_t rows, uint32_t cols, uint32_t pickLen)
 {
     return (rows * 16u + cols * 4u + pickLen + 15u) & ~15u;
 }
 /// Word offsets of the output parts (ge_result_words: the total).
-constexpr uint32_t ge_out_pivots(uint32_t) { return 4; }
-constexpr uint32_t ge_out_used(uint32_t rows) { return 4 + (rows + 3) / 4; }
-constexpr uint32_t ge_out_counts(uint32_t rows) { return 4 + 2 * ((rows + 3) / 4); }
+constexpr uint32_t kGeOutHeader = 8;
+constexpr uint32_t ge_out_pivots(uint32_t) { return kGeOutHeader; }
+constexpr uint32_t ge_out_used(uint32_t rows) { return kGeOutHeader + (rows + 3) / 4; }
+constexpr uint32_t ge_out_counts(uint32_t rows) { return kGeOutHeader + 2 * ((rows + 3) / 4); }
 constexpr uint32_t ge_out_matrix(uint32_t rows) { return ge_out_counts(rows) + (rows + 1) / 2; }
-constexpr uint32_t ge_result_words(uint32_t rows, uint32_t cols)
+constexpr uint32_t ge_result_words(uint32_t rows, uint32_t cols, bool chained = false)
 {
-    return ge_out_matrix(rows) + (rows * cols + 3) / 4;
+    return chained ? ge_out_used(rows) : ge_out_matrix(rows) + (rows * cols + 3) / 4;
 }
 
 constexpr uint32_t kNoRows = 0xffffffffu;   // be_launch_exec: no OP_ROWS in the launch

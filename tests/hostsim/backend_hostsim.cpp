@@ -149,7 +149,7 @@ void literal_tile(uint64_t dst, uint32_t at, const uint8_t* lit, uint32_t len, u
     }
 }
 
-void exec_tile(const uint8_t* stream, const ExecItem& it, uint32_t t0, uint64_t* acct)
+void exec_tile(const uint8_t* stream, const ExecItem& it, uint32_t t0, uint64_t* acct, const uint32_t* results)
 {
     const uint8_t* w = stream + (size_t)it.streamBegin * 16;
     const uint8_t* end = w + (size_t)it.streamWords * 16;
@@ -161,6 +161,9 @@ void exec_tile(const uint8_t* stream, const ExecItem& it, uint32_t t0, uint64_t*
         w += (size_t)op_words(op) * 16;
         if (w > end)
             std::abort(); // malformed stream
+        // (a gated op of a chained elimination that failed: termBegin, ops.h)
+        if (op.kind != OP_LITERAL && op.termBegin != 0 && results[op.termBegin - 1] == 0)
+            continue;
         if (op.kind == OP_LITERAL) {
             literal_tile(op.dst, op.n, op.lit, op.valid, t0);
             continue;
@@ -402,16 +405,17 @@ static bool noexec()
     return v == 1;
 }
 
-void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct, uint32_t)
+void be_launch_exec(const void* stream, const ExecItem* items, uint32_t count, uint64_t* acct,
+                    const uint32_t* results, uint32_t)
 {
     if (noexec())
         return;
     // (tile by tile: every op is local to its byte columns, so this order
     // gives the device's op-by-op, tile-by-tile results)
     for (uint32_t i = 0; i < count; ++i)
-        for (uint32_t t = 0; t < (items[i].tiles >> 16); ++t)
+        for (uint32_t t = 0; t < exec_tile_count(items[i].tiles); ++t)
             exec_tile(static_cast<const uint8_t*>(stream), items[i],
-                      ((items[i].tiles & 0xffffu) + t) * kExecTileBytes, acct);
+                      (exec_first_tile(items[i].tiles) + t) * kExecTileBytes, acct, results);
 }
 
 void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
@@ -442,6 +446,8 @@ static void solve_prefix(const SolveDesc* solves, const SolveRow* rows, const ui
 {
     for (uint32_t s = 0; s < count; ++s) {
         const SolveDesc& sd = solves[s];
+        if (sd.gate && results[sd.gate - 1] == 0)
+            continue;   // (a chained elimination that failed, ops.h GeDesc)
         const uint32_t m = sd.m;
         const SolveRow* R = rows + sd.rowBegin;
         const uint8_t* C = coef + sd.coefOffset;
@@ -503,6 +509,8 @@ static void solve_main(const SolveDesc* solves, const SolveRow* rows, const uint
         return;
     for (uint32_t it = 0; it < count; ++it) {
         const SolveDesc& sd = solves[items[it].solve];
+        if (sd.gate && results[sd.gate - 1] == 0)
+            continue;
         const uint32_t m = sd.m;
         const SolveRow* R = rows + sd.rowBegin;
         const uint8_t* C = coef + sd.coefOffset;
@@ -611,7 +619,8 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 // generate_matrix, reference SiameseDecoder.cpp:2157-2383), then the
 // elimination without pivoting while the pivots allow it and with row
 // pivoting from the first zero pivot (:2423-2531), as the kernel runs it.
-void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results)
+void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* srows,
+                  uint8_t* scoef, uint32_t, uint32_t)
 {
     for (uint32_t jb = 0; jb < count; ++jb) {
         const GeDesc d = descs[jb];
@@ -704,12 +713,37 @@ void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32
                 }
             }
         }
+        const bool ok = stop == cols;
+        uint32_t nz = 0;   // non-zero multipliers below the diagonal, pivot order
+        if (ok)
+            for (unsigned j = 0; j < cols; ++j)
+                for (unsigned i = 0; i < j; ++i)
+                    nz += M[(size_t)piv[j] * cols + i] != 0;
         uint32_t* out = results + d.result;
+        std::memset(out, 0, kGeOutHeader * 4);
         out[0] = stop;
         out[1] = (uint32_t)bytes;
         out[2] = (uint32_t)(bytes >> 32);
-        out[3] = 0;
+        out[3] = ok ? 1 : 0;
+        out[4] = nz;
         uint8_t* po = reinterpret_cast<uint8_t*>(out + ge_out_pivots(rows));
+        if (d.flags & kGeChained) {
+            std::memset(po, 0, 4 * ((rows + 3) / 4));
+            for (unsigned i = 0; i < rows; ++i)
+                po[i] = piv[i];
+            if (!ok)
+                continue;
+            uint8_t* co = scoef + d.solveCoef;
+            for (unsigned j = 0; j < cols; ++j)
+                std::memcpy(co + (size_t)j * cols, &M[(size_t)piv[j] * cols], cols);
+            SolveRow* sr = srows + d.solveRow;
+            std::vector<SolveRow> t(sr, sr + cols);
+            for (unsigned j = 0; j < cols; ++j) {
+                sr[j] = t[piv[j]];
+                sr[j].headIndex = 1 + solve_head_slot(t[piv[j]].headIndex, piv[j]);
+            }
+            continue;
+        }
         uint8_t* uo = reinterpret_cast<uint8_t*>(out + ge_out_used(rows));
         uint16_t* co = reinterpret_cast<uint16_t*>(out + ge_out_counts(rows));
         std::memset(po, 0, 4 * ((rows + 3) / 4));

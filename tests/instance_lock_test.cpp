@@ -8,11 +8,20 @@
 #include <cstdio>
 #include <mutex>
 #include <shared_mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
-int main()
+int main(int argc, char** argv)
 {
+    if (argc > 1 && std::string(argv[1]) == "nested") {
+        // a second shared acquisition on one thread: SGPU_DEBUG_LOCKS aborts
+        static sgpu::InstanceLock lk;
+        lk.lock_shared();
+        lk.lock_shared();
+        std::printf("nested acquisition not caught\n");
+        return 0;
+    }
     sgpu::InstanceLock lk;
     std::atomic<int> readersIn{0}, writersIn{0};
     std::atomic<long> reads{0}, writes{0}, bad{0};

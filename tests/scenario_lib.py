@@ -86,7 +86,7 @@ class BatchOptions(ctypes.Structure):
 class BatchReport(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("device_ms", ctypes.c_double),
                 ("exec_ms", ctypes.c_double), ("setup_seconds", ctypes.c_double),
-                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 18),
+                ("rounds", ctypes.c_uint64), ("engine", ctypes.c_uint64 * 21),
                 ("checked", ctypes.c_uint64), ("mismatches", ctypes.c_uint64),
                 ("phase_seconds", ctypes.c_double * 5), ("payload_bytes", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double * 5)]
@@ -160,7 +160,8 @@ def run_batch(library, cfg, steps=1, warmup=0, verify=True, device=-1, threads=0
 
 ENGINE_KEYS = ("flushes launches ops terms solves ingests upload_bytes ref_op_bytes "
                "out_bytes solve_bytes assemble_ns wait_ns complete_ns reclaim_ns "
-               "exec_launches ldpc_bytes exec_unique_bytes arena_growth").split()
+               "exec_launches ldpc_bytes exec_unique_bytes ge_jobs ge_chained ge_retried "
+               "arena_growth").split()
 
 
 def engine_dict(report):

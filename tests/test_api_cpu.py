@@ -170,3 +170,32 @@ def test_range_adds_use_few_ingest_descriptors():
     assert rep.mismatches == 0 and all(r.status == 0 for r in res)
     ingests = S.engine_dict(rep)["ingests"]
     assert ingests <= 16 * 6, ingests   # (4 slabs of originals per stream, a few recovery staging runs)
+
+
+def test_symbols_past_16_mib_match_reference(ref, sim):
+    """Symbols past 16 MiB span more than 65536 executor tiles of 256 bytes:
+    ExecItem.tiles (ops.h exec_tiles) must still name each tile once
+    (reference siamese.h SIAMESE_MAX_PACKET_BYTES)."""
+    import hashlib
+    import random
+    rng = random.Random(5)
+    sizes = [(17 << 20) + 13, (20 << 20) + 1001, (16 << 20) + 77]
+    data = [rng.randbytes(n) for n in sizes]
+    outs = []
+    for lib in (ref, sim):
+        enc, dec = lib.Encoder(), lib.Decoder()
+        o = []
+        for i, d in enumerate(data):
+            n = enc.add(d)
+            if i == 0:
+                o.append(dec.add_original(n, d))
+        for _ in range(2):
+            r = enc.encode()
+            o.append(hashlib.sha256(r).hexdigest())
+            o.append(dec.add_recovery(r))
+        got = dec.decode()
+        o.append(sorted((num, hashlib.sha256(b).hexdigest()) for num, b in got))
+        outs.append(o)
+    assert outs[0] == outs[1]
+    want = sorted((k, hashlib.sha256(data[k]).hexdigest()) for k in (1, 2))
+    assert outs[1][-1] == want

@@ -82,7 +82,7 @@ void be_copy_list(const BeCopy* r, const void*, unsigned n, bool toDevice) { be_
 void be_memset(void* dst, int value, size_t bytes) { std::memset(dst, value, bytes); }
 
 void be_launch_ingest(const IngestDesc*, uint32_t, uint32_t, const uint32_t*, uint32_t) {}
-void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*, uint32_t) {}
+void be_launch_exec(const void*, const ExecItem*, uint32_t, uint64_t*, const uint32_t*, uint32_t) {}
 void be_launch_ldpc(const LdpcItem*, uint32_t, uint64_t*) {}
 
 static void solve_prefix(const SolveDesc* solves, const SolveRow*, const uint8_t*,
@@ -146,15 +146,23 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 
 // matrix jobs: every one reports an eliminated matrix with identity pivots,
 // its first `cols` rows used and zero coefficients (no elimination on the host)
-void be_launch_ge(const GeDesc* descs, const uint8_t*, uint32_t count, uint32_t* results)
+void be_launch_ge(const GeDesc* descs, const uint8_t*, uint32_t count, uint32_t* results, SolveRow*, uint8_t*,
+                  uint32_t, uint32_t)
 {
     const GeDesc* dd = host_view(descs);
     for (uint32_t j = 0; j < count; ++j) {
         const GeDesc d = dd[j];
         uint32_t* out = results + d.result;
-        std::memset(out, 0, (size_t)ge_result_words(d.rows, d.cols) * 4);
+        const bool chained = (d.flags & kGeChained) != 0;
+        std::memset(out, 0, (size_t)ge_result_words(d.rows, d.cols, chained) * 4);
         out[0] = d.cols;
+        out[3] = 1;
         uint8_t* po = reinterpret_cast<uint8_t*>(out + ge_out_pivots(d.rows));
+        if (chained) {
+            for (unsigned i = 0; i < d.rows; ++i)
+                po[i] = (uint8_t)i;
+            continue;
+        }
         uint8_t* uo = reinterpret_cast<uint8_t*>(out + ge_out_used(d.rows));
         uint16_t* co = reinterpret_cast<uint16_t*>(out + ge_out_counts(d.rows));
         for (unsigned i = 0; i < d.rows; ++i) {

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel HBM traffic from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-Usage: pmc_traffic.py FETCH.csv WRITE.csv OUT.json [SOURCE-LABEL [LIBRARY.so]]
+Usage: pmc_traffic.py FETCH.csv WRITE.csv OUT.json [SOURCE-LABEL [LIBRARY.so [STEPS]]]
 
 Both counters are reported in KiB per dispatch.  Following
 MI355X_MICROARCH.md (HBM section), FETCH_SIZE on gfx950 counts half the
@@ -10,7 +10,10 @@ Writes {kernel: {dispatches, fetch_bytes, write_bytes, traffic_bytes}}: the
 byte figures are PER-DISPATCH AVERAGES (traffic_bytes_all is the sum over every
 dispatch of the capture, traffic_bytes_max the largest dispatch).  With a
 library path, "_lib_sha256" records the build the capture measured (bench.py
-reports whether the library it loads is the same build).
+reports whether the library it loads is the same build).  STEPS: the workload
+steps the captured process ran (bench.py runs --steps + --warmup + 2: the
+verified warm-up and the unique-bytes step); "_step_traffic_bytes" is then
+the traffic of all sgpu kernels per step (bench.py's physical step figure).
 """
 import hashlib
 import collections
@@ -47,6 +50,12 @@ def main():
         out["_source"] = sys.argv[4]
     if len(sys.argv) > 5:
         out["_lib_sha256"] = hashlib.sha256(open(sys.argv[5], "rb").read()).hexdigest()
+    if len(sys.argv) > 6:
+        steps = int(sys.argv[6])
+        out["_workload_steps"] = steps
+        out["_step_traffic_bytes"] = round(sum(v["traffic_bytes_all"] for k, v in out.items()
+                                               if k.startswith("sgpu::")) / steps)
+        out["_step_dispatches"] = {k: v["dispatches"] / steps for k, v in out.items() if k.startswith("sgpu::")}
     json.dump(out, open(sys.argv[3], "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
 

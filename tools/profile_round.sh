@@ -12,7 +12,8 @@ timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o 
 B1="bench.py --steps 1 --warmup 1 --no-cpu --no-e2e --no-legs"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $D -o pmc_fetch -- python3 $B1 > /dev/null 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $D -o pmc_write -- python3 $B1 > /dev/null 2>&1
-python3 tools/pmc_traffic.py $(ls $D/pmc_fetch*counter_collection.csv | head -n1) $(ls $D/pmc_write*counter_collection.csv | head -n1) $D/traffic.json "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per dispatch (averages), bench.py --steps 1 --no-legs, tag $TAG" siamese_amd/libsiamese_amd.so > /dev/null
+# (B1 runs 1 + 1 + 2 workload steps: timed, warm-up, the verified warm-up and the unique-bytes step)
+python3 tools/pmc_traffic.py $(ls $D/pmc_fetch*counter_collection.csv | head -n1) $(ls $D/pmc_write*counter_collection.csv | head -n1) $D/traffic.json "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per dispatch (averages), bench.py --steps 1 --warmup 1 --no-legs, tag $TAG" siamese_amd/libsiamese_amd.so 4 > /dev/null
 ls -R $D | head -n 40
 # single-stream legs: kernel traces of C3 and C5 (tools/leg_run.py)
 # (groups and deferred-output depth as bench.py runs them)
