@@ -171,6 +171,7 @@ inline uint64_t ev(uint64_t type, uint64_t result, uint64_t a = 0, uint64_t b = 
       uint64_t rec_token(const Rec& rec);
       uint64_t pkt_token(const Pkt& p, unsigned id, bool* ok);
       bool wants_yield_after_decode();        // batch: lengths known after a flush
+      bool outputs_final(const std::vector<Pkt>&);   // every decoded packet's length known
 
     Range calls (cfg->add_ranges; every codec supports them, a per-call API
     as loops of its single calls):
@@ -498,7 +499,10 @@ struct Stream
             const int r = codec->decode(&decoded);
             if (r == kDecodePending)
                 return true;
-            return decoded_result(r);
+            // (a decode finished after its flush -- a chained device decode --
+            // returns its packets with their lengths: no flush to wait for)
+            const bool yield = decoded_result(r);
+            return yield && !codec->outputs_final(decoded);
         }
         case DECODED: {
             for (const Pkt& p : decoded) {

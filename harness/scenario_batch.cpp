@@ -664,6 +664,13 @@ struct BatchCodec
         return true;
     }
     bool wants_yield_after_encode() const { return sh->hashData; }
+    bool outputs_final(const std::vector<Pkt>& v) const
+    {
+        for (const Pkt& p : v)
+            if (!p.entry || !p.entry->Data)
+                return false;
+        return true;
+    }
     /// Back to the freshly constructed state (a recycled job's codec slot).
     void reset()
     {

@@ -262,6 +262,7 @@ struct CapiCodec
     }
     void encode_hint(unsigned) {}   // (siamese.h encodes one packet per call)
     bool wants_yield_after_decode() const { return false; }
+    bool outputs_final(const std::vector<Pkt>&) const { return true; }
     bool wants_yield_after_encode() const { return false; }
 };
 

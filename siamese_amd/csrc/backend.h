@@ -82,10 +82,13 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 /// per desc, its input at in + desc.in, its output in results + desc.result;
 /// a kGeChained job that succeeds also writes its solve's coefficients
 /// (coef + solveCoef) and permutes its SolveRows (rows + solveRow).  Reads
-/// nothing any other launch of the flush writes; runs before them.
-/// maxRows / maxCols: the largest job of the launch (sizes its LDS).
+/// nothing any other launch of the flush writes.  It may run beside the
+/// launches queued after it until be_join_ge(), after which every launch
+/// (and the results' download) sees its outputs.  maxRows / maxCols: the
+/// largest job of the launch (sizes its LDS).
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
                   uint8_t* coef, uint32_t maxRows, uint32_t maxCols);
+void be_join_ge();
 
 /// Block until all queued work has finished.  Returns false on a device fault.
 bool be_sync();

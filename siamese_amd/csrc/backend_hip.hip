@@ -2872,7 +2872,7 @@ __host__ __device__ constexpr uint32_t t_rows(uint32_t m) { return (m + 3u) & ~3
 // k_solve_pre: the larger of the prefix pass's staging and the T build's
 __host__ __device__ constexpr uint32_t solve_tbuild_lds_bytes(uint32_t m)
 {
-    return ((m * m + 15u) & ~15u) + t_rows(m) * kTStride + 256u * 20u;
+    return ((m * m + 15u) & ~15u) + t_rows(m) * kTStride + 256u * 20u + 256u;
 }
 __host__ __device__ constexpr uint32_t solve_pre_lds_bytes(uint32_t m)
 {
@@ -2930,7 +2930,12 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
     uint8_t* Y = Ct + ((m * m + 15u) & ~15u);                    // T, rows of kTStride bytes
     uint4* permL = reinterpret_cast<uint4*>(Y + mp * kTStride);
     uint32_t* permC = reinterpret_cast<uint32_t*>(permL + 256);
+    // the diagonal's inverses from LDS: c_inv indexed by a value read from
+    // LDS is a memory round trip on the back-substitution's serial chain
+    uint8_t* invB = reinterpret_cast<uint8_t*>(permC + 256);
     stage_transposed<kPreThreads, 2>(Ct, C, m, tid);
+    if (tid < 64)
+        reinterpret_cast<uint32_t*>(invB)[tid] = reinterpret_cast<const uint32_t*>(c_inv)[tid];
     if (tid < 256) {
         const uint32_t* t = c_perm[tid];
         permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
@@ -2987,9 +2992,9 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
         int i = (int)m - 1;
         for (; i >= 2; i -= 2) {
             flush_pend();
-            const uint32_t xi = mul(Yw[i * 32 + l32], c_inv[Ct[i * m + i]]);
+            const uint32_t xi = mul(Yw[i * 32 + l32], invB[Ct[i * m + i]]);
             const uint32_t ym = Yw[(i - 1) * 32 + l32] ^ mul(xi, Ct[(uint32_t)i * m + i - 1]);   // row i-1 after pivot i
-            const uint32_t xm = mul(ym, c_inv[Ct[(i - 1) * m + i - 1]]);
+            const uint32_t xm = mul(ym, invB[Ct[(i - 1) * m + i - 1]]);
             tbuild_rows(Yw, Ct, permL, permC, m, 0, (uint32_t)i - 1, hw, l32, (uint32_t)i * m, (uint32_t)(i - 1) * m, xi,
                         xm);
             pend = ym;
@@ -2998,7 +3003,7 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
         }
         flush_pend();
         if (i == 1) {
-            const uint32_t xi = mul(Yw[32 + l32], c_inv[Ct[m + 1]]);
+            const uint32_t xi = mul(Yw[32 + l32], invB[Ct[m + 1]]);
             if (hw == 0) {
                 const uint32_t y = Ct[m];   // C[0][1]
                 if (y)
@@ -3010,7 +3015,7 @@ __device__ void solve_tbuild(const SolveDesc& sd, const uint8_t* __restrict__ C,
     GMEM uint32_t* out = reinterpret_cast<GMEM uint32_t*>(sd.tinv);
     for (uint32_t k = tid; k < mp * 32u; k += kPreThreads) {
         const uint32_t i = k >> 5;
-        out[k] = i < m ? gf_mul_tab(Yw[k], gf_tab_l(permL, permC, c_inv[Ct[i * m + i]])) : 0u;
+        out[k] = i < m ? gf_mul_tab(Yw[k], gf_tab_l(permL, permC, invB[Ct[i * m + i]])) : 0u;
     }
 }
 
@@ -3291,21 +3296,24 @@ __global__ __launch_bounds__(kTrThreads) void k_solve_tr(const SolveDesc* __rest
 // ---------------------------------------------------------------------------
 // The recovery matrix of a decode on the device (k_ge, ops.h GeDesc)
 //
-// One wave per decode, the matrix resident in LDS (ge_stride_words dwords a
-// row: odd, so the rows the lanes own start in different banks).  Generation
-// (the host's generate_matrix; reference SiameseDecoder.cpp:2157-2383) writes
-// four columns per lane: the dense part from the row's opcodes (Siamese),
-// 1/(X ^ Y) (Cauchy) or 1 (parity); then the LDPC picks, 64 PCG draws of one
-// row per pass (jump-ahead c_pcgA/c_pcgG), land by LDS XOR atomics.  The
-// elimination is the reference's (:2423-2531): no pivoting while each pivot
-// byte is non-zero, then row pivoting from the first zero one.  Lane k owns
-// the rows k, k + 64, ...: at each pivot it takes its multiplier y = row[p] /
-// pivot (kept at [p]) and XORs y times the pivot row's bytes (p, end) into its
-// own row, a dword at a time with the pivot row's dword broadcast from LDS
-// and y's multiply table read once per pivot.  No barrier inside a step: the
-// wave is the workgroup (round 5's four waves with two barriers per pivot ran
-// 130 us per headline launch).
-constexpr unsigned kGeThreads = 64;
+// One workgroup of eight waves per decode (a launch holds one job per CU: the
+// job's own work must fill the CU's four SIMDs; a launch lasts as long as
+// its largest matrix, so rows up to 128 take one pass), the matrix resident in LDS
+// (ge_stride_words dwords a row: odd, so rows start in different banks) with
+// the job's input staged beside it.  Generation (the host's generate_matrix;
+// reference SiameseDecoder.cpp:2157-2383) writes four columns per thread: the
+// dense part from the row's opcodes (Siamese), 1/(X ^ Y) (Cauchy) or 1
+// (parity); then the LDPC picks, one row per wave and 64 PCG draws per pass
+// (jump-ahead c_pcgA/c_pcgG), land by LDS XOR atomics.  The elimination is
+// the reference's (:2423-2531): no pivoting while each pivot byte is
+// non-zero, then row pivoting from the first zero one.  A pivot step is one
+// pass and one barrier: four threads per row each take the row's multiplier
+// y = row[p] / pivot and XOR y times a quarter of the pivot row's bytes
+// (p, end) into it, their LDS reads all in flight.
+// The GF(256) tables (multiply, inverse) are LDS copies: an inverse read from
+// global memory on every pivot cost a memory round trip per pivot.
+constexpr unsigned kGeThreads = 512;   // four threads for each of up to 128 rows a pass
+constexpr unsigned kGePickLds = 4096;   // pick tables up to this many bytes are staged in LDS
 
 __device__ __forceinline__ uint32_t ge_opcode(uint32_t lane, uint32_t row)
 {
@@ -3330,6 +3338,16 @@ __host__ __device__ constexpr uint32_t ge_lds_bytes(uint32_t rows, uint32_t cols
 {
     return rows * ge_stride_words(cols) * 4u;
 }
+#ifndef SGPU_GE_LDS_MIN
+#define SGPU_GE_LDS_MIN 0
+#endif
+// the launch's dynamic LDS: its largest matrix (SGPU_GE_LDS_MIN: a floor, a
+// timing knob that keeps one job per CU)
+inline size_t ge_launch_lds(uint32_t rows, uint32_t cols)
+{
+    const size_t b = ge_lds_bytes(rows, cols);
+    return b > (size_t)SGPU_GE_LDS_MIN ? b : (size_t)SGPU_GE_LDS_MIN;
+}
 
 __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ descs, const uint8_t* __restrict__ in,
                                                   uint32_t* __restrict__ results, SolveRow* __restrict__ srows,
@@ -3338,31 +3356,70 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
     extern __shared__ uint32_t M[];   // rows x S4 dwords
     __shared__ uint4 permL[256];
     __shared__ uint32_t permC[256];
+    __shared__ uint32_t invL[64];     // GF(256) inverses, bytes
     __shared__ uint8_t piv[kGeMaxRows], used[kGeMaxRows];
+    __shared__ uint8_t pivB[2][kGeMaxRows];   // the pivot order of pivoted steps (double-buffered)
     __shared__ uint16_t cnt[kGeMaxRows];
+    __shared__ GeRow R[kGeMaxRows];
+    __shared__ GeCol C[kGeMaxCols + 1];
+    __shared__ uint8_t pickL[kGePickLds];
+    __shared__ uint32_t foundL[3], nzL;
+    __shared__ unsigned long long bytesL;
+    const uint8_t* invB = reinterpret_cast<const uint8_t*>(invL);
     uint8_t* Mb = reinterpret_cast<uint8_t*>(M);
+#ifdef SGPU_GE_CLOCKS
+    const unsigned long long gclk0 = wall_clock64();
+#endif
     const GeDesc d = descs[blockIdx.x];
     const uint32_t rows = d.rows, cols = d.cols;
     const uint32_t S4 = ge_stride_words(cols), SB = 4u * S4;
-    const uint32_t lane = threadIdx.x;
-    const GeRow* R = reinterpret_cast<const GeRow*>(in + d.in);
-    const GeCol* C = reinterpret_cast<const GeCol*>(R + rows);
-    const uint8_t* pick = reinterpret_cast<const uint8_t*>(C + cols);
-    for (uint32_t y = lane; y < 256; y += kGeThreads) {
-        const uint32_t* t = c_perm[y];
-        permL[y] = make_uint4(t[0], t[1], t[2], t[3]);
-        permC[y] = t[4];
-    }
-    for (uint32_t i = lane; i < rows; i += kGeThreads) {
-        piv[i] = (uint8_t)i;
-        used[i] = 0;
-        cnt[i] = R[i].colCount;
-    }
-    __syncthreads();
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const GeRow* Rg = reinterpret_cast<const GeRow*>(in + d.in);
+    const GeCol* Cg = reinterpret_cast<const GeCol*>(Rg + rows);
+    const uint8_t* pickG = reinterpret_cast<const uint8_t*>(Cg + cols);
+    const bool pickStaged = d.pickLen <= kGePickLds;
+    const uint8_t* pick = pickStaged ? pickL : pickG;
 
-    // 1. dense parts, a dword (four columns) per lane
+    // 0. staging: every load of the job's input and tables in flight at once
+    if (tid < 256) {
+        const uint32_t* t = c_perm[tid];
+        permL[tid] = make_uint4(t[0], t[1], t[2], t[3]);
+        permC[tid] = t[4];
+    }
+    if (tid < 64)
+        invL[tid] = reinterpret_cast<const uint32_t*>(c_inv)[tid];
+    if (tid < rows) {
+        const GeRow g = Rg[tid];
+        R[tid] = g;
+        piv[tid] = (uint8_t)tid;
+        used[tid] = 0;
+        cnt[tid] = g.colCount;
+    }
+    if (tid < cols)
+        C[tid] = Cg[tid];
+    if (pickStaged)
+        for (uint32_t x = 4u * tid; x < d.pickLen; x += 4u * kGeThreads) {
+            // (the pick table starts 4-byte aligned: GeRow 16 B, GeCol 4 B)
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(pickG + x);
+            *reinterpret_cast<uint32_t*>(pickL + x) = v;
+        }
+    if (tid == 0) {
+        bytesL = 0;
+        nzL = 0;
+        foundL[0] = foundL[1] = foundL[2] = 0xffffffffu;
+    }
+    // (the PCG jump-ahead constants of the picks, in registers before any
+    // LDS atomic: loads past those are not hoisted out of the row loop)
+    const uint64_t pcgJa = c_pcgA[lane], pcgJg = c_pcgG[lane];
+    const uint64_t pcgA64 = c_pcgA[64], pcgG64 = c_pcgG[64];
+    __syncthreads();
+#ifdef SGPU_GE_CLOCKS
+    const unsigned long long gclkS = wall_clock64();
+#endif
+
+    // 1. dense parts, a dword (four columns) per thread
     const uint32_t wpr = (cols + 3u) / 4u;
-    for (uint32_t x = lane; x < rows * S4; x += kGeThreads) {
+    for (uint32_t x = tid; x < rows * S4; x += kGeThreads) {
         const uint32_t r = x / S4, w = x - r * S4;
         uint32_t lo = 0;
         if (w < wpr) {
@@ -3375,7 +3432,7 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
                     const GeCol c = C[j];
                     uint32_t v = 1u, h = 0u;
                     if (g.kind == GE_CAUCHY) {
-                        v = c_inv[(uint8_t)(g.rbase ^ c.ccol)];
+                        v = invB[(uint8_t)(g.rbase ^ c.ccol)];
                     } else if (g.kind == GE_SIAMESE) {
                         const uint32_t op = ge_opcode(c.lane, g.row);
                         v = ge_comb(op & 7u, c.cx, c.cx2);
@@ -3392,20 +3449,19 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
     }
     __syncthreads();
 
-    // 2. LDPC picks: one Siamese row at a time, draws c0 + lane per pass
-    for (uint32_t r = 0; r < rows; ++r) {
+    // 2. LDPC picks: one Siamese row per wave, draws c0 + lane per pass
+    for (uint32_t r = wave; r < rows; r += kGeThreads / 64u) {
         const GeRow g = R[r];
         if (g.kind != GE_SIAMESE || g.ldpcN == 0)
-            continue;   // (uniform)
+            continue;   // (uniform in the wave)
         const uint32_t N = g.ldpcN, P = 2u * ((N + kPairRate - 1u) / kPairRate);
         const uint64_t inc = ((uint64_t)g.row << 1) | 1u;
         uint64_t sc = (inc + N) * kPcgMul + inc;   // state after Seed(row, N)
-        const uint64_t ja = c_pcgA[lane], jg = c_pcgG[lane];
         const uint32_t rx = 1u + (g.row + 1u) % kRowValuePeriod;
         for (uint32_t c0 = 0; c0 < P; c0 += 64u) {
             const uint32_t k = c0 + lane;
-            const uint64_t st = ja * sc + inc * jg;
-            sc = c_pcgA[64] * sc + inc * c_pcgG[64];
+            const uint64_t st = pcgJa * sc + inc * pcgJg;
+            sc = pcgA64 * sc + inc * pcgG64;
             if (k < P) {
                 const uint32_t col = pick[g.pickOff + pcg_output(st) % N];
                 if (col < cols)
@@ -3414,34 +3470,75 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
         }
     }
     __syncthreads();
+#ifdef SGPU_GE_CLOCKS
+    const unsigned long long gclk1 = wall_clock64();
+#endif
 
-    // 3. elimination.  One pivot step: every row below `pivot` (through piv[]
-    // once pivoting) takes y = row[pivot] / val at [pivot], then y * the
-    // source row's bytes (pivot, end) (SiameseDecoder.h:504-541)
+    // 3. elimination.  One pivot step: every row below `pivot` (through the
+    // pivot order once pivoting) takes y = row[pivot] / val at [pivot], then
+    // y * the source row's bytes (pivot, end) (SiameseDecoder.h:504-541).
+    // Pivoted steps keep the pivot order in two buffers (step s reads
+    // pivB[s & 1] and writes the order with its swap into the other) and find
+    // the next pivot row while they update the rows: the first position at or
+    // after pivot + 1 whose row holds a non-zero byte at column pivot + 1 goes
+    // into foundL[(s + 1) % 3] (atomicMin); a step resets slot (s + 2) % 3,
+    // read by step s - 1 before step s began.  One barrier a step, pivoted or
+    // not.
     unsigned long long myBytes = 0;
-    auto eliminate = [&](uint32_t src, uint32_t pivot, uint32_t end, uint32_t val, bool pivoted) {
-        const GfTab iv = gf_tab_l(permL, permC, c_inv[val]);
+    // (pivoted: position swapJ's row is swapRow, every other's order[k])
+    auto eliminate = [&](uint32_t src, uint32_t pivot, uint32_t end, uint32_t val, const uint8_t* order,
+                         uint32_t swapJ, uint32_t swapRow, uint32_t* detect) {
+        // four threads per row (one wave holds whole rows): each takes the
+        // row's multiplier y = row[pivot] / val itself (the quarter-0 thread
+        // keeps it at [pivot]: the wave's reads of that byte come before its
+        // store), then XORs y times its quarter of the pivot row's dwords
+        // (pivot, end)
         const uint32_t w0 = (pivot + 1u) / 4u, w1 = (end + 3u) / 4u;
-        const uint32_t* S = M + src * S4;
-        for (uint32_t k = pivot + 1u + lane; k < rows; k += kGeThreads) {
-            const uint32_t rk = pivoted ? piv[k] : k;
+        const uint32_t per = end > pivot + 1u ? (w1 - w0 + 3u) / 4u : 0u;   // dwords a thread
+        const uint32_t quarter = tid & 3u;
+        const GfTab iv = gf_tab_l(permL, permC, invB[val]);
+        // (the source row through a VGPR address: a uniform address is read
+        // into scalars, one LDS round trip per dword)
+        const uint32_t* S = M + opaque(src * S4);
+        for (uint32_t k = pivot + 1u + (tid >> 2); k < rows; k += kGeThreads / 4u) {
+            const uint32_t rk = order ? (k == swapJ ? swapRow : order[k]) : k;
             const uint32_t v = Mb[rk * SB + pivot];
-            if (!v)
-                continue;
-            const uint32_t y = gf_mul_tab(v, iv) & 0xffu;
-            Mb[rk * SB + pivot] = (uint8_t)y;
-            if (pivoted && cnt[rk] < end)
-                cnt[rk] = (uint16_t)end;
-            if (end <= pivot + 1u)
-                continue;
-            myBytes += end - pivot - 1u;
-            const GfTab ty = gf_tab_l(permL, permC, y);
-            uint32_t* D = M + rk * S4;
-            for (uint32_t w = w0; w < w1; ++w) {
-                const uint32_t mask =
-                    byte_mask((int)end - (int)(4u * w)) & ~byte_mask((int)(pivot + 1u) - (int)(4u * w));
-                D[w] ^= gf_mul_tab(S[w], ty) & mask;
+            if (v) {
+                const uint32_t y = gf_mul_tab(v, iv) & 0xffu;
+                if (quarter == 0) {
+                    Mb[rk * SB + pivot] = (uint8_t)y;
+                    if (end > pivot + 1u)
+                        myBytes += end - pivot - 1u;
+                    if (order && cnt[rk] < end)
+                        cnt[rk] = (uint16_t)end;
+                }
+                const uint32_t a = w0 + quarter * per;
+                const uint32_t e = min(a + per, w1);
+                const GfTab ty = gf_tab_l(permL, permC, y);
+                uint32_t* D = M + rk * S4;
+                for (uint32_t w = a; w < e; w += 4u) {
+                    uint32_t sv[4], dv[4];
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q) {
+                        const uint32_t ww = w + q < e ? w + q : w;   // (in bounds, unused past e)
+                        sv[q] = S[ww];
+                        dv[q] = D[ww];
+                    }
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q) {
+                        const uint32_t ww = w + q;
+                        if (ww < e) {
+                            const uint32_t mask = byte_mask((int)end - (int)(4u * ww)) &
+                                                  ~byte_mask((int)(pivot + 1u) - (int)(4u * ww));
+                            D[ww] = dv[q] ^ (gf_mul_tab(sv[q], ty) & mask);
+                        }
+                    }
+                }
             }
+            // (the row as this step leaves it: its quarters' stores came
+            // before this read in the wave's instruction stream)
+            if (detect && quarter == 0 && Mb[rk * SB + pivot + 1u])
+                atomicMin(detect, k);
         }
         __syncthreads();   // (the next step reads the rows this one wrote)
     };
@@ -3450,74 +3547,94 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
         const uint32_t val = Mb[p * SB + p];
         if (val == 0)
             break;
-        if (lane == 0)
+        if (tid == 0)
             used[p] = 1;
-        eliminate(p, p, cnt[p], val, false);
+        eliminate(p, p, cnt[p], val, nullptr, 0u, 0u, nullptr);
     }
     uint32_t stop = cols;
     if (p < cols) {
-        uint32_t jFrom = p + 1u;   // (the caller found column p zero in row p)
+        // row p has a zero at column p: the first row after it with a non-zero
+        for (uint32_t j = p + 1u + tid; j < rows; j += kGeThreads)
+            if (Mb[j * SB + p])
+                atomicMin(&foundL[p % 3u], j);
+        for (uint32_t k = tid; k < rows; k += kGeThreads)
+            pivB[p & 1u][k] = piv[k];
+        __syncthreads();
         for (uint32_t pivot = p; pivot < cols; ++pivot) {
-            // the first row at or after jFrom (in pivot order) with a
-            // non-zero byte at the pivot column
-            uint32_t j = 0xffffffffu;
-            for (uint32_t j0 = jFrom; j0 < rows; j0 += kGeThreads) {
-                const uint32_t jj = j0 + lane;
-                const uint64_t b = __ballot(jj < rows && Mb[piv[jj] * SB + pivot] != 0);
-                if (b) {
-                    j = j0 + (uint32_t)__builtin_ctzll(b);
-                    break;
-                }
-            }
+            const uint32_t j = foundL[pivot % 3u];
+            const uint8_t* cur = pivB[pivot & 1u];
+            uint8_t* nxt = pivB[(pivot & 1u) ^ 1u];
             if (j == 0xffffffffu) {
                 stop = pivot;
+                for (uint32_t k = tid; k < rows; k += kGeThreads)
+                    piv[k] = cur[k];
                 break;
             }
-            const uint32_t rj = piv[j];
-            __syncthreads();   // (every lane has read piv[j])
-            if (lane == 0) {
-                piv[j] = piv[pivot];
-                piv[pivot] = (uint8_t)rj;
+            const uint32_t rj = cur[j], rp = cur[pivot];
+            // this step's order: the swap of positions pivot and j
+            for (uint32_t k = tid; k < rows; k += kGeThreads)
+                nxt[k] = k == j ? (uint8_t)rp : (k == pivot ? (uint8_t)rj : cur[k]);
+            if (tid == 0) {
                 used[rj] = 1;
+                foundL[(pivot + 2u) % 3u] = 0xffffffffu;
             }
-            __syncthreads();
-            if (pivot >= cols - 1u)
+            if (pivot >= cols - 1u) {
+                for (uint32_t k = tid; k < rows; k += kGeThreads)
+                    piv[k] = k == j ? (uint8_t)rp : (k == pivot ? (uint8_t)rj : cur[k]);
                 break;
-            eliminate(rj, pivot, cnt[rj], Mb[rj * SB + pivot], true);
-            jFrom = pivot + 1u;
+            }
+            // (the step reads the order as cur with the swap applied: nxt is
+            // written during the step, for the next one)
+            eliminate(rj, pivot, cnt[rj], Mb[rj * SB + pivot], cur, j, rp, &foundL[(pivot + 1u) % 3u]);
         }
     }
+    __syncthreads();   // (the pivot order and the matrix as the elimination left them)
+#ifdef SGPU_GE_CLOCKS
+    const unsigned long long gclk2 = wall_clock64();
+#endif
 
     // 4. outcome: the header words, the pivots, and for a chained job the
     // solve's coefficients and rows in pivot order; else the used rows, the
     // column counts and the matrix for the host to install
-#pragma unroll
-    for (unsigned o = 32; o >= 1; o >>= 1)
-        myBytes += __shfl_xor(myBytes, o, 64);
     const bool ok = stop == cols;
     const bool chained = (d.flags & kGeChained) != 0;
     // MultiplyLowerTriangle's multipliers: the eliminated matrix's non-zero
     // bytes below the diagonal, in pivot order (SiameseDecoder.cpp:1065-1104)
     uint32_t nz = 0;
-    if (ok)
-        for (uint32_t j = lane; j < cols; j += kGeThreads) {
-            const uint8_t* row = Mb + piv[j] * SB;
-            for (uint32_t i = 0; i < j; ++i)
-                nz += row[i] != 0;
-        }
+    if (ok && tid < cols) {
+        const uint8_t* row = Mb + piv[tid] * SB;
+        for (uint32_t i = 0; i < tid; ++i)
+            nz += row[i] != 0;
+    }
 #pragma unroll
-    for (unsigned o = 32; o >= 1; o >>= 1)
+    for (unsigned o = 32; o >= 1; o >>= 1) {
+        myBytes += __shfl_xor(myBytes, o, 64);
         nz += __shfl_xor(nz, o, 64);
+    }
+    if (lane == 0) {
+        if (myBytes)
+            atomicAdd(&bytesL, myBytes);
+        if (nz)
+            atomicAdd(&nzL, nz);
+    }
+    __syncthreads();
     uint32_t* out = results + d.result;
-    if (lane < kGeOutHeader) {
-        const uint32_t hdr[kGeOutHeader] = {stop, (uint32_t)myBytes, (uint32_t)(myBytes >> 32), ok ? 1u : 0u, nz, 0, 0, 0};
+    if (tid < kGeOutHeader) {
+        const unsigned long long tb = bytesL;
+#ifdef SGPU_GE_CLOCKS
+        const uint32_t hdr[kGeOutHeader] = {stop, (uint32_t)tb, (uint32_t)(tb >> 32), ok ? 1u : 0u, nzL,
+                                            (uint32_t)(gclkS - gclk0), (uint32_t)(gclk1 - gclkS),
+                                            (uint32_t)(gclk2 - gclk1)};
+#else
+        const uint32_t hdr[kGeOutHeader] = {stop, (uint32_t)tb, (uint32_t)(tb >> 32), ok ? 1u : 0u, nzL, 0, 0, 0};
+#endif
         uint32_t v = 0;
 #pragma unroll
         for (unsigned k = 0; k < kGeOutHeader; ++k)
-            v = lane == k ? hdr[k] : v;
-        out[lane] = v;
+            v = tid == k ? hdr[k] : v;
+        out[tid] = v;
     }
-    for (uint32_t w = lane; w < (rows + 3u) / 4u; w += kGeThreads) {
+    for (uint32_t w = tid; w < (rows + 3u) / 4u; w += kGeThreads) {
         uint32_t a = 0, b = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 4; ++q)
@@ -3534,36 +3651,34 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
             return;   // (the gated items of the submission do not run)
         // coefficients: coef[j * cols + i] = the pivot-order row j's column i
         uint8_t* co = scoef + d.solveCoef;
-        for (uint32_t x = lane; x < cols * cols; x += kGeThreads) {
+        for (uint32_t x = tid; x < cols * cols; x += kGeThreads) {
             const uint32_t j = x / cols, i = x - j * cols;
             co[x] = Mb[piv[j] * SB + i];
         }
-        // the solve's rows in pivot order, each keeping its head slot: every
-        // lane reads its rows before any lane writes
-        SolveRow* sr = srows + d.solveRow;
-        SolveRow t[4];
+        // the solve's rows in pivot order, each keeping its head slot
+        // (SolveRow: 6 dwords, the last the head slot): every thread reads
+        // its row before any thread writes
+        static_assert(sizeof(SolveRow) == 24, "SolveRow layout");
+        uint32_t* sr = reinterpret_cast<uint32_t*>(srows + d.solveRow);
+        uint32_t t[6];
+        if (tid < cols) {
+            const uint32_t src = piv[tid];
 #pragma unroll
-        for (unsigned u = 0; u < 4; ++u) {
-            const uint32_t j = lane + kGeThreads * u;
-            if (j < cols) {
-                const uint32_t src = piv[j];
-                t[u] = sr[src];
-                t[u].headIndex = 1u + solve_head_slot(t[u].headIndex, src);
-            }
+            for (unsigned k = 0; k < 6; ++k)
+                t[k] = sr[6u * src + k];
+            t[5] = 1u + solve_head_slot(t[5], src);
         }
         __syncthreads();
+        if (tid < cols)
 #pragma unroll
-        for (unsigned u = 0; u < 4; ++u) {
-            const uint32_t j = lane + kGeThreads * u;
-            if (j < cols)
-                sr[j] = t[u];
-        }
+            for (unsigned k = 0; k < 6; ++k)
+                sr[6u * tid + k] = t[k];
         return;
     }
-    for (uint32_t w = lane; w < (rows + 1u) / 2u; w += kGeThreads)
+    for (uint32_t w = tid; w < (rows + 1u) / 2u; w += kGeThreads)
         out[ge_out_counts(rows) + w] = (uint32_t)cnt[2u * w] | (2u * w + 1u < rows ? (uint32_t)cnt[2u * w + 1u] << 16 : 0u);
     const uint32_t total = rows * cols;
-    for (uint32_t w = lane; w < (total + 3u) / 4u; w += kGeThreads) {
+    for (uint32_t w = tid; w < (total + 3u) / 4u; w += kGeThreads) {
         uint32_t a = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 4; ++q) {
@@ -3585,6 +3700,11 @@ namespace {
 hipStream_t g_stream = nullptr;
 hipStream_t g_stageStream = nullptr;    // application H2D staging (be_stage_h2d)
 hipStream_t g_gatherStream = nullptr;   // gathers of completed results (be_gather)
+// device recovery-matrix jobs (k_ge) beside the submission's first launches
+// (be_launch_ge / be_join_ge)
+hipStream_t g_geStream = nullptr;
+hipEvent_t g_geFork = nullptr, g_geJoin = nullptr;
+bool g_gePending = false;   // (launcher thread only)
 bool g_ready = false;
 int g_device = 0;
 
@@ -3642,18 +3762,19 @@ struct Timed
 {
     EvPair ev;
     bool on;
-    explicit Timed(BeKernel kind) : on(g_timing)
+    hipStream_t stream;
+    explicit Timed(BeKernel kind, hipStream_t s = nullptr) : on(g_timing), stream(s ? s : g_stream)
     {
         bind_device();
         if (on) {
             ev = take_events(kind);
-            (void)hipEventRecord(ev.a, g_stream);
+            (void)hipEventRecord(ev.a, stream);
         }
     }
     ~Timed()
     {
         if (on) {
-            (void)hipEventRecord(ev.b, g_stream);
+            (void)hipEventRecord(ev.b, stream);
             std::lock_guard<std::mutex> g(g_evMu);
             g_evUsed.push_back(ev);
         }
@@ -3748,7 +3869,10 @@ bool be_init(int device, const char** err)
         return false;
     }
     if (hipStreamCreateWithFlags(&g_stageStream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&g_gatherStream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&g_gatherStream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&g_geStream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&g_geFork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g_geJoin, hipEventDisableTiming) != hipSuccess) {
         *err = "hipStreamCreate (transfer streams) failed";
         return false;
     }
@@ -4048,14 +4172,41 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
                        reinterpret_cast<unsigned long long*>(acct));
 }
 
+#ifndef SGPU_GE_SIDE
+#define SGPU_GE_SIDE 0
+#endif
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
                   uint8_t* coef, uint32_t maxRows, uint32_t maxCols)
 {
     if (count == 0)
         return;
-    Timed t(kBeGe);
-    hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), (size_t)ge_lds_bytes(maxRows, maxCols), g_stream, descs,
-                       in, results, rows, coef);
+    if (!SGPU_GE_SIDE) {
+        Timed t(kBeGe);
+        hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), ge_launch_lds(maxRows, maxCols), g_stream, descs, in,
+                           results, rows, coef);
+        return;
+    }
+    // SGPU_GE_SIDE (timing variant): on the side stream, after everything the
+    // codec stream has queued (the upload), beside k_ingest and the encoders'
+    // k_exec, which read nothing they write; be_join_ge puts the codec stream
+    // behind them
+    check(hipEventRecord(g_geFork, g_stream), "hipEventRecord(ge fork)");
+    check(hipStreamWaitEvent(g_geStream, g_geFork, 0), "hipStreamWaitEvent(ge)");
+    {
+        Timed t(kBeGe, g_geStream);
+        hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), ge_launch_lds(maxRows, maxCols), g_geStream,
+                           descs, in, results, rows, coef);
+    }
+    check(hipEventRecord(g_geJoin, g_geStream), "hipEventRecord(ge join)");
+    g_gePending = true;
+}
+
+void be_join_ge()
+{
+    if (!g_gePending)
+        return;
+    check(hipStreamWaitEvent(g_stream, g_geJoin, 0), "hipStreamWaitEvent(ge join)");
+    g_gePending = false;
 }
 
 namespace {

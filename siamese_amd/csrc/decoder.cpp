@@ -1189,6 +1189,34 @@ struct DecodeClocks
                      (double)t[2] / n, (double)t[3] / n);
     }
 } g_decodeClocks;
+// the chained device decode's host phases (same switch): the job's input,
+// the elimination of received data, the solve's layout, the finish
+struct ChainClocks
+{
+    std::mutex mu;
+    std::vector<uint32_t> samples[4];
+    void sample(const uint64_t* d)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (int k = 0; k < 4; ++k)
+            if (samples[k].size() < (1u << 16))
+                samples[k].push_back((uint32_t)d[k]);
+    }
+    ~ChainClocks()
+    {
+        if (!kDecodeClocks || samples[0].empty())
+            return;
+        double med[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 4; ++k)
+            if (!samples[k].empty()) {
+                std::nth_element(samples[k].begin(), samples[k].begin() + samples[k].size() / 2, samples[k].end());
+                med[k] = samples[k][samples[k].size() / 2];
+            }
+        std::fprintf(stderr, "chained decode medians (ticks): job %.0f eliminate %.0f solve %.0f finish %.0f\n",
+                     med[0], med[1], med[2], med[3]);
+    }
+} g_chainClocks;
+thread_local uint64_t t_chain[3];
 } // namespace
 
 SiameseResult DecoderCore::decode_region()
@@ -1384,6 +1412,7 @@ bool DecoderCore::submit_chained()
     const unsigned rows = region_.recoveryCount;
     if (mirror_ || rows != columns || columns == 0 || columns > kGeMaxCols)
         return false;
+    const uint64_t c0 = kDecodeClocks ? __rdtsc() : 0;
     const RecPacket* r = region_.first;
     const unsigned bytes = r->bytes;
     for (unsigned i = 0; i < rows; ++i, r = r->next)
@@ -1391,6 +1420,7 @@ bool DecoderCore::submit_chained()
             return false;
     if (!submit_device_ge(true))
         return false;
+    const uint64_t c1 = kDecodeClocks ? __rdtsc() : 0;
     pivots_.resize(rows);
     for (unsigned i = 0; i < rows; ++i) {
         rows_[i].used = true;
@@ -1412,6 +1442,7 @@ bool DecoderCore::submit_chained()
     deferAccount_ = false;
     deferRelease_ = false;
     prog_.gate_end();
+    const uint64_t c2 = kDecodeClocks ? __rdtsc() : 0;
     chainSlot_ = ~0u;
     chainBytes_ = bytes;
     if (!chainElimFailed_) {
@@ -1421,6 +1452,11 @@ bool DecoderCore::submit_chained()
         else
             chainElimFailed_ = true;   // (an arena failure: disabled_ is set)
     }
+    if (kDecodeClocks) {
+        t_chain[0] = c1 - c0;
+        t_chain[1] = c2 - c1;
+        t_chain[2] = __rdtsc() - c2;
+    }
     return true;
 }
 
@@ -1429,6 +1465,35 @@ SiameseResult DecoderCore::finish_chained(SiameseOriginalPacket** packetsOut, un
     const unsigned columns = geCols_;
     const uint32_t* o = geOut_.data();
     const bool ok = o[3] != 0;
+#ifdef SGPU_GE_CLOCKS
+    // (timing build: k_ge's phases in 100 MHz ticks, averaged at exit)
+    static struct GeClocks
+    {
+        std::atomic<uint64_t> n{0}, t[3];
+        std::mutex mu;
+        std::vector<std::pair<uint32_t, uint32_t>> jobs;   // (ticks, columns)
+        ~GeClocks()
+        {
+            if (!n)
+                return;
+            std::fprintf(stderr, "k_ge phases (us): staging %.2f generate %.2f eliminate %.2f over %llu jobs\n",
+                         t[0] / 100.0 / n, t[1] / 100.0 / n, t[2] / 100.0 / n, (unsigned long long)n.load());
+            std::sort(jobs.begin(), jobs.end());
+            for (double q : {0.5, 0.9, 0.99, 1.0}) {
+                const auto& j = jobs[std::min(jobs.size() - 1, (size_t)(q * jobs.size()))];
+                std::fprintf(stderr, "k_ge job q%.2f: %.2f us, %u columns\n", q, j.first / 100.0, j.second);
+            }
+        }
+    } clocks;
+    clocks.n++;
+    for (int k = 0; k < 3; ++k)
+        clocks.t[k] += o[5 + k];
+    {
+        std::lock_guard<std::mutex> g(clocks.mu);
+        clocks.jobs.emplace_back(o[5] + o[6] + o[7], columns);
+    }
+#endif
+    const uint64_t f0 = kDecodeClocks ? __rdtsc() : 0;
     auto drop_solve = [&] {
         // the planned solve did not run (or is not wanted): its slot goes
         // back without touching the decoder's state
@@ -1481,9 +1546,12 @@ SiameseResult DecoderCore::finish_chained(SiameseOriginalPacket** packetsOut, un
     }
     const unsigned slot = chainSlot_;
     chainSlot_ = ~0u;
-    const SiameseResult res = solve_publish(slot);
-    settle();   // (its completion has arrived: the exact lengths)
+    const SiameseResult res = publish_final(slot);
     region_reset();
+    if (kDecodeClocks) {
+        const uint64_t d[4] = {t_chain[0], t_chain[1], t_chain[2], __rdtsc() - f0};
+        g_chainClocks.sample(d);
+    }
     if (res == Siamese_Success && packetsOut) {
         *packetsOut = recovered_.data();
         *countOut = (unsigned)recovered_.size();
@@ -2215,6 +2283,74 @@ SiameseResult DecoderCore::solve_publish(unsigned slot)
     }
     lastPendSlot_ = slot;
 
+    if (!advanced) {
+        disabled_ = true;
+        return Siamese_Disabled;
+    }
+    iterate_next_expected(region_.nextCheckStart);
+    list_delete_before(nextExpected_);
+    if (region_.nextCheckStart >= kRemoveThreshold)
+        remove_elements();
+    stats_[SiameseDecoderStats_SolveSuccessCount]++;
+    return Siamese_Success;
+}
+
+// finish_chained's host side of BackSubstitution: as solve_publish and the
+// apply_resolved that would follow it, the solve's lengths being known (its
+// submission has completed): the window takes the recovered buffers with
+// their exact lengths, the outputs are final.  A solve that flagged a corrupt
+// length prefix goes the general way.
+SiameseResult DecoderCore::publish_final(unsigned slot)
+{
+    const unsigned m = region_.lostCount;
+    bool ready = false;
+    {
+        std::lock_guard<std::mutex> g(res_->mu);
+        const PendingDecode& pd = res_->pend[slot];
+        ready = pd.done && pd.words.size() > m && pd.words[0] == m;
+    }
+    if (!ready) {
+        const SiameseResult res = solve_publish(slot);
+        settle();
+        return res;
+    }
+    const std::vector<RecPacket*>& pr = scratchRec_;
+    bool advanced = false;
+    {
+        std::lock_guard<std::mutex> g(res_->mu);
+        PendingDecode& pd = res_->pend[slot];
+        recovered_.resize(m);
+        ++decodeSerial_;
+        for (int ci = (int)m - 1; ci >= 0; --ci) {
+            RecPacket* r = pr[ci];
+            ColInfo& col = cols_[ci];
+            DecSlot* o = col.original;
+            const uint32_t w = pd.words[1 + ci];
+            const unsigned hdr = w >> 29, len = w & kSolveLengthMask;
+            DevBuf old = o->inSlab ? DevBuf() : o->buf;
+            o->inSlab = false;
+            o->buf = r->buf;
+            o->bytes = hdr + len;
+            o->column = col.column;
+            o->header = hdr;
+            o->pending = false;
+            r->buf = old;
+            r->bytes = 0;
+            SiameseOriginalPacket& out = recovered_[ci];
+            out.PacketNum = col.column;
+            out.DataBytes = len;
+            out.Data = o->buf.ptr + hdr;
+            recoveredColumns_.push_back(col.column);
+            advanced |= mark_got(col.column);
+        }
+        publish_outputs();
+        // (applied here, as apply_resolved would: its completion counted)
+        pd.live = pd.done = pd.held = false;
+        pd.fixes.clear();
+    }
+    pendingSolves_--;
+    ++appliedCount_;
+    lastPendSlot_ = slot;
     if (!advanced) {
         disabled_ = true;
         return Siamese_Disabled;

@@ -335,6 +335,7 @@ private:
     /// recovered buffers).  solve_plan returns false on an arena failure.
     bool solve_plan(uint32_t gateWord, unsigned* slotOut);
     SiameseResult solve_publish(unsigned slot);
+    SiameseResult publish_final(unsigned slot);   // a chained solve's, its lengths known
 
     bool add_single(const RowMeta& m, const uint8_t* headBytes, unsigned payloadBytes,
                     const void* hostData, uint64_t devData, Program* producer);

@@ -1352,6 +1352,7 @@ struct Phase
     size_t solveBegin, solveCount;  // solve descs (SOLVE)
     uint32_t maxRows;               // largest m among them (SOLVE); largest OP_ROWS window (EXEC)
     size_t wideBegin = 0, wideCount = 0;   // k_ldpc items run before the exec launch (EXEC)
+    int group = 0;                  // the programs' group (1: decoders, which the matrix jobs feed)
 };
 
 struct SegRef
@@ -2042,6 +2043,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                 wideBytes += s.wideBytes;
             }
             ex.wideCount = nWide - ex.wideBegin;
+            ex.group = g;
             if (ex.itemCount)
                 phases.push_back(ex);
 
@@ -2094,6 +2096,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
                         tBytes += (solve_x_bytes(sdescs[i].m, sdescs[i].maxBytes) + 255u) & ~(uint64_t)255u;
                     }
                 }
+            sv.group = g;
             if (sv.solveCount)
                 phases.push_back(sv);
         }
@@ -2412,20 +2415,22 @@ void Engine::launch_batch(Batch& bt)
         const BeCopy up{(uint64_t)(uintptr_t)xs.upDev, (uint64_t)(uintptr_t)xs.upHost, bt.upBytes};
         be_copy_pinned(&up, 1, true);
     }
+    uint64_t* acctDev = (uint64_t*)xs.downDev;
+    uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
+    // the matrix jobs first, on their own stream: they need only the upload
+    // and run beside what follows until the decoders' first phase joins them
+    if (bt.nGe)
+        be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev,
+                     (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols);
     if (bt.nIngest)
         be_launch_ingest((const IngestDesc*)(bt.upBase + bt.oIngD), (uint32_t)bt.nIngest, bt.maxIngest,
                          (const uint32_t*)(bt.upBase + bt.oIngB), (uint32_t)bt.nIngBlocks);
-    uint64_t* acctDev = (uint64_t*)xs.downDev;
-    uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
     if (xs.acctZero) {
         be_memset(acctDev, 0, 4 * sizeof(uint64_t));
         xs.acctZero = false;
     }
     if (bt.wideZero)
         be_memset(xs.wideDev, 0, xs.wideCap);
-    if (bt.nGe)
-        be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev,
-                     (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols);
     // k_ldpc items of every exec phase before the first solve go in one
     // launch (they read only window elements that exist before the flush's
     // first solve); a phase after a solve launches its own
@@ -2435,6 +2440,8 @@ void Engine::launch_batch(Batch& bt)
     if (wideDone)
         be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide), (uint32_t)wideDone, acctDev + 3);
     for (const Phase& ph : bt.phases) {
+        if (ph.group == 1)
+            be_join_ge();   // (the decoders' gated ops and solves read the matrix jobs' outputs)
         if (ph.kind == Phase::EXEC) {
             if (ph.wideCount && ph.wideBegin >= wideDone)
                 be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide) + ph.wideBegin, (uint32_t)ph.wideCount,
@@ -2453,6 +2460,7 @@ void Engine::launch_batch(Batch& bt)
     // the counters and solve results, then the downloads, in one call (one
     // kernel when small; its range list was laid out with the upload: a
     // drop-in submission carries a range per application call)
+    be_join_ge();
     be_copy_list(bt.copies.data(), xs.downHostDev ? bt.upBase + bt.oCopy : nullptr, (unsigned)bt.copies.size(),
                  false);
     bt.fence = be_fence();

@@ -760,4 +760,7 @@ void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32
     }
 }
 
+// (synchronous here)
+void be_join_ge() {}
+
 } // namespace sgpu
