@@ -173,4 +173,7 @@ void be_launch_ge(const GeDesc* descs, const uint8_t*, uint32_t count, uint32_t*
     }
 }
 
+// (synchronous here)
+void be_join_ge() {}
+
 } // namespace sgpu
