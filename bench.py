@@ -52,7 +52,7 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 STREAMS_PER_GPU = 1024
 METRIC = "device-resident GB/s encode+decode, 1400B pkts @20% loss; % HBM peak"
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r5_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r6_traffic.json")
 
 
 def lib_sha256(path):
@@ -479,6 +479,19 @@ def run_rank(rank, world, local, args, library, use_cuda):
     # byte figure; counting it costs assembly time, so never in the timed run)
     _, urep = sess.run(steps=1, warmup=0, verify=False, threads=args.threads, groups=args.groups,
                        digest=False, defer=args.defer, device_ge=dge, unique=True)
+    # the same steps with the other placement of the coefficient elimination
+    # (host / device), timed the same way right after: reported beside
+    # `value`, never as it
+    alt_elapsed = None
+    if args.decode_ab and args.defer == 0:
+        sess.run(steps=max(1, args.warmup), warmup=0, verify=False, threads=args.threads, groups=args.groups,
+                 digest=False, defer=args.defer, device_ge=not dge)
+        coll.barrier()
+        ta = time.perf_counter()
+        sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads, groups=args.groups,
+                 digest=False, defer=args.defer, device_ge=not dge, timing=False)
+        coll.barrier()
+        alt_elapsed = time.perf_counter() - ta
     if cb is not None:
         cb.measure()
         side_run()
@@ -518,6 +531,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
     alg_total, payload_total, streams_total = coll.reduce(
         [float(alg_bytes), float(payload), float(cfg.streams)], "sum")
     e2e_max = coll.reduce([e2e_elapsed], "max")[0] if e2e_elapsed is not None else None
+    alt_max = coll.reduce([alt_elapsed], "max")[0] if alt_elapsed is not None else None
     extra = None
     if rank == 0 and world == 1 and args.legs:
         extra = legs(library, device, args.threads, not args.no_cpu)
@@ -566,11 +580,19 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "loss_pct": 20,
             "add_calls": "range (sgpu_encoder_add_range / sgpu_decoder_add_original_range)"
                          if args.ranges else "per packet",
-            "decode": "sgpu_decode_device (recovery matrix generated and eliminated on the GPU, k_ge)"
+            "decode": "sgpu_decode_device (recovery matrix generated and eliminated on the GPU by k_ge, "
+                      "chained with the elimination of received data and the solve into one submission)"
                       if dge else "sgpu_decode (recovery matrix on the host)",
             "parallelism": "independent streams sharded by index (weak scaling), "
                            "one process per GPU, gloo host barrier",
         },
+        "decode_ab": ({
+            "sgpu_decode_device_ms_per_step": round((t_max if dge else alt_max) / steps * 1e3, 3),
+            "sgpu_decode_ms_per_step": round((alt_max if dge else t_max) / steps * 1e3, 3),
+            "note": "the same workload and steps with the coefficient elimination on the device "
+                    "(GenerateMatrix + GaussianElimination in k_ge, chained into the decode's submission) "
+                    "and on the host, timed back to back in this run; `value` is the first",
+        } if alt_max is not None else None),
         "payload_GBps": round(payload_total / t_max / 1e9, 3),
         "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
         "pct_hbm_peak_basis": "ALGORITHMIC bytes (SURVEY 8d: every source byte of the reference's GF ops, "
@@ -719,9 +741,12 @@ def main(argv=None):
                     help="skip the PCIe-inclusive end-to-end leg")
     ap.add_argument("--no-frames", dest="frames", action="store_false",
                     help="end-to-end leg with raw payloads instead of framed datagrams")
-    ap.add_argument("--device-ge", dest="device_ge", action="store_true",
-                    help="decodes by sgpu_decode_device (recovery matrix on the GPU)")
-    ap.add_argument("--no-device-ge", dest="device_ge", action="store_false")
+    ap.add_argument("--device-ge", dest="device_ge", action="store_true", default=True,
+                    help="decodes by sgpu_decode_device (recovery matrix on the GPU; the default)")
+    ap.add_argument("--no-device-ge", dest="device_ge", action="store_false",
+                    help="decodes by sgpu_decode (recovery matrix on the host)")
+    ap.add_argument("--no-decode-ab", dest="decode_ab", action="store_false",
+                    help="skip the timed run of the other decode placement")
     ap.add_argument("--no-ranges", dest="ranges", action="store_false",
                     help="headline originals through per-packet add/get calls instead of range calls")
     ap.add_argument("--no-legs", dest="legs", action="store_false",

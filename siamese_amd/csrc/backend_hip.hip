@@ -59,6 +59,16 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __constant__ uint32_t c_perm[256][8];   // per constant y: {Ta0,Ta1,Tb0,Tb1,Tc,0,0,0}
 __constant__ uint8_t c_inv[256];
 
+// The inverse of a wave-uniform y through the scalar data cache: c_inv[y]
+// compiles to a vector memory load (a full memory round trip on a solve's
+// serial pivot chain); the dword holding it, uniformly indexed, is a scalar
+// load.
+__device__ __forceinline__ uint32_t inv_u(uint32_t y)
+{
+    const uint32_t w = reinterpret_cast<const uint32_t*>(c_inv)[__builtin_amdgcn_readfirstlane(y) >> 2];
+    return (w >> (8u * (y & 3u))) & 0xffu;
+}
+
 __device__ __forceinline__ uint32_t gf_mul_dword(uint32_t x, uint32_t y)
 {
     const uint32_t* t = c_perm[y];
@@ -2325,7 +2335,7 @@ __device__ void solve_prefix_wave(uint32_t m, uint32_t lane, uint32_t (&p4)[4], 
         const uint8_t* col = Ct + (uint32_t)i * m;
         const uint32_t fb = uni(finB[i]);
         const uint32_t lc = fb < 32 ? fb : 32;
-        const uint32_t x = gf_mul_dword(p4_get(p4, (uint32_t)i), c_inv[uni(col[i])]) & byte_mask((int)lc);
+        const uint32_t x = gf_mul_dword(p4_get(p4, (uint32_t)i), inv_u(uni(col[i]))) & byte_mask((int)lc);
         uint32_t len = 0;
         const int h = parse_prefix(x, lc, &len);
         if (h < 1 || len == 0 || (uint32_t)h + len > fb)
@@ -2537,7 +2547,7 @@ __device__ void solve_tile_lds(uint4* __restrict__ X, uint32_t m, const SolveRow
         const uint32_t w = uni(rw[1 + i]);
         const uint32_t bb = (w >> 29) + (w & kSolveLengthMask);
         const uint8_t* col = Ct + (uint32_t)i * m;
-        uint4 x = gf_mul16(X[i * 64 + lane], c_inv[uni(col[i])]);
+        uint4 x = gf_mul16(X[i * 64 + lane], inv_u(uni(col[i])));
         x = mask16(x, (int)bb - (int)p); // zero beyond the recovered length
         if ((uint32_t)i % kSolveWaves == wave && p < finB[i])
             st16(R[i].buf + p, x);
@@ -2691,7 +2701,7 @@ __device__ void solve_tile_narrow(uint4* __restrict__ X, uint32_t m, const Solve
         const uint32_t w = uni(rw[1 + i]);
         const uint32_t bb = (w >> 29) + (w & kSolveLengthMask);
         const uint8_t* col = Ct + (uint32_t)i * m;
-        uint4 x = gf_mul16(X[i * kChunks + c], c_inv[uni(col[i])]);
+        uint4 x = gf_mul16(X[i * kChunks + c], inv_u(uni(col[i])));
         x = mask16(x, (int)bb - (int)p); // zero beyond the recovered length
         if (slot == (uint32_t)i % kSlots && p < finB[i])
             st16(R[i].buf + p, x);
@@ -3338,16 +3348,7 @@ __host__ __device__ constexpr uint32_t ge_lds_bytes(uint32_t rows, uint32_t cols
 {
     return rows * ge_stride_words(cols) * 4u;
 }
-#ifndef SGPU_GE_LDS_MIN
-#define SGPU_GE_LDS_MIN 0
-#endif
-// the launch's dynamic LDS: its largest matrix (SGPU_GE_LDS_MIN: a floor, a
-// timing knob that keeps one job per CU)
-inline size_t ge_launch_lds(uint32_t rows, uint32_t cols)
-{
-    const size_t b = ge_lds_bytes(rows, cols);
-    return b > (size_t)SGPU_GE_LDS_MIN ? b : (size_t)SGPU_GE_LDS_MIN;
-}
+
 
 __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ descs, const uint8_t* __restrict__ in,
                                                   uint32_t* __restrict__ results, SolveRow* __restrict__ srows,
@@ -4172,29 +4173,21 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
                        reinterpret_cast<unsigned long long*>(acct));
 }
 
-#ifndef SGPU_GE_SIDE
-#define SGPU_GE_SIDE 0
-#endif
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
                   uint8_t* coef, uint32_t maxRows, uint32_t maxCols)
 {
     if (count == 0)
         return;
-    if (!SGPU_GE_SIDE) {
-        Timed t(kBeGe);
-        hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), ge_launch_lds(maxRows, maxCols), g_stream, descs, in,
-                           results, rows, coef);
-        return;
-    }
-    // SGPU_GE_SIDE (timing variant): on the side stream, after everything the
-    // codec stream has queued (the upload), beside k_ingest and the encoders'
-    // k_exec, which read nothing they write; be_join_ge puts the codec stream
-    // behind them
+    // On the side stream, after everything the codec stream has queued (the
+    // upload): the jobs run beside k_ingest and the encoders' k_exec, which
+    // read nothing they write, and be_join_ge puts the codec stream behind
+    // them.  Same box, interleaved: headline 4.97 ms/step against 5.34 with
+    // the jobs in line on the codec stream (profiles/r6q_modes_ab.txt).
     check(hipEventRecord(g_geFork, g_stream), "hipEventRecord(ge fork)");
     check(hipStreamWaitEvent(g_geStream, g_geFork, 0), "hipStreamWaitEvent(ge)");
     {
         Timed t(kBeGe, g_geStream);
-        hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), ge_launch_lds(maxRows, maxCols), g_geStream,
+        hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), (size_t)ge_lds_bytes(maxRows, maxCols), g_geStream,
                            descs, in, results, rows, coef);
     }
     check(hipEventRecord(g_geJoin, g_geStream), "hipEventRecord(ge join)");

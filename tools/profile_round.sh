@@ -7,9 +7,9 @@ TAG=${1:-cur}
 D=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-B="bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-legs"
+B="bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-legs --no-decode-ab"
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o trace -- python3 $B > $D/bench_trace.log 2>&1
-B1="bench.py --steps 1 --warmup 1 --no-cpu --no-e2e --no-legs"
+B1="bench.py --steps 1 --warmup 1 --no-cpu --no-e2e --no-legs --no-decode-ab"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $D -o pmc_fetch -- python3 $B1 > /dev/null 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $D -o pmc_write -- python3 $B1 > /dev/null 2>&1
 # (B1 runs 1 + 1 + 2 workload steps: timed, warm-up, the verified warm-up and the unique-bytes step)
