@@ -130,15 +130,19 @@ SIAMESE_EXPORT SiameseResult sgpu_decode(SgpuDecoder decoder, SiameseOriginalPac
                                          unsigned* countOut);
 /// sgpu_decode with the recovery matrix on the device: when the decode would
 /// start a fresh elimination (GenerateMatrix + GaussianElimination,
-/// reference SiameseDecoder.cpp:2157-2531) of at most 128 lost columns and
-/// 192 recovery rows, the matrix job is queued and SGPU_DECODE_PENDING is
+/// reference SiameseDecoder.cpp:2157-2531) of at most 255 lost columns and
+/// 256 recovery rows, the matrix job is queued and SGPU_DECODE_PENDING is
 /// returned.  Flush (sgpu_flush, or wait for a later sgpu_enqueue ticket),
 /// then call sgpu_decode_device again with the same arguments: it returns
 /// what sgpu_decode would have returned, with the same outputs (an
 /// elimination that stopped short of a pivot is repeated on the host, which
-/// keeps the state the next attempt resumes from).  While a job is pending,
-/// every other call on this decoder returns Siamese_InvalidInput.  Any other
-/// decode runs as sgpu_decode does.
+/// keeps the state the next attempt resumes from).  A square matrix of rows
+/// of one length (a block decode) is chained: the elimination of received
+/// data and the solve ride in the same submission, gated on the device
+/// elimination's outcome, so the packets this second call returns already
+/// carry their exact lengths.  While a job is pending, every other call on
+/// this decoder returns Siamese_InvalidInput.  Any other decode runs as
+/// sgpu_decode does.
 #define SGPU_DECODE_PENDING ((SiameseResult)6)
 SIAMESE_EXPORT SiameseResult sgpu_decode_device(SgpuDecoder decoder, SiameseOriginalPacket** packetsOut,
                                                 unsigned* countOut);

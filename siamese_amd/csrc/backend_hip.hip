@@ -4179,10 +4179,11 @@ void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32
     if (count == 0)
         return;
     // On the side stream, after everything the codec stream has queued (the
-    // upload): the jobs run beside k_ingest and the encoders' k_exec, which
-    // read nothing they write, and be_join_ge puts the codec stream behind
-    // them.  Same box, interleaved: headline 4.97 ms/step against 5.34 with
-    // the jobs in line on the codec stream (profiles/r6q_modes_ab.txt).
+    // upload): the jobs run beside k_ingest, which reads nothing they write,
+    // and be_join_ge puts the codec stream behind them (Engine::launch_batch
+    // joins before the first k_exec).  Same box, interleaved: headline 4.97
+    // ms/step on the side stream against 5.34 with the jobs in line on the
+    // codec stream (profiles/r6q_modes_ab.txt).
     check(hipEventRecord(g_geFork, g_stream), "hipEventRecord(ge fork)");
     check(hipStreamWaitEvent(g_geStream, g_geFork, 0), "hipStreamWaitEvent(ge)");
     {

@@ -2439,9 +2439,13 @@ void Engine::launch_batch(Batch& bt)
         wideDone = bt.phases[k].wideBegin + bt.phases[k].wideCount;
     if (wideDone)
         be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide), (uint32_t)wideDone, acctDev + 3);
+    // The codec stream joins the matrix jobs before the first executor launch
+    // (they run beside k_ingest): joined only before the decoders' phases,
+    // they shared the CUs with the encoders' k_exec, which slowed from 87 to
+    // 107 us per launch for no gain in the step (same box, interleaved,
+    // 4.86 vs 5.04 ms per step: profiles/r6r_ge_join_ab.txt).
     for (const Phase& ph : bt.phases) {
-        if (ph.group == 1)
-            be_join_ge();   // (the decoders' gated ops and solves read the matrix jobs' outputs)
+        be_join_ge();   // (no-op once joined)
         if (ph.kind == Phase::EXEC) {
             if (ph.wideCount && ph.wideBegin >= wideDone)
                 be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide) + ph.wideBegin, (uint32_t)ph.wideCount,
