@@ -57,7 +57,7 @@ namespace sgpu {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __constant__ uint32_t c_perm[256][8];   // per constant y: {Ta0,Ta1,Tb0,Tb1,Tc,0,0,0}
-__constant__ uint8_t c_inv[256];
+__constant__ __attribute__((aligned(16))) uint8_t c_inv[256];   // (read as dwords too)
 
 // The inverse of a wave-uniform y through the scalar data cache: c_inv[y]
 // compiles to a vector memory load (a full memory round trip on a solve's
@@ -4205,8 +4205,8 @@ void be_join_ge()
 
 namespace {
 
-// How a launch of many solves runs (launches of fewer than kSolvePrefixSplit
-// solves always take the fused sweeps)
+// How a split launch runs (solve_split; the others always take the fused
+// sweeps)
 enum SolvePath
 {
     kPathSweeps = 0,   // k_solve_prefix + k_solve_main
@@ -4218,10 +4218,10 @@ void launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_t* 
                   uint32_t solveCount, SolvePath path)
 {
     const uint32_t rowsCap = maxRows < kSolveLdsMaxRows ? maxRows : kSolveLdsMaxRows;
-    // Many solves: their prefixes in one wave each first (once per solve, all
-    // in parallel); few (single-stream flushes): fused into the tiles, one
-    // launch fewer on the flush's critical path.
-    const bool separate = solveCount >= kSolvePrefixSplit;
+    // Many solves or large ones: their prefixes in one wave each first (once
+    // per solve, all in parallel); few small ones (single-stream flushes):
+    // fused into the tiles, one launch fewer on the flush's critical path.
+    const bool separate = solve_split(solveCount, maxRows);
     const bool tr = separate && path == kPathVector;
     unsigned long long* acctL = reinterpret_cast<unsigned long long*>(acct);
     const uint32_t prodCap = rowsCap < kProductMaxRows ? rowsCap : kProductMaxRows;
@@ -4270,7 +4270,7 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 }
 
 // Test hook: the solve paths against one another on random systems.  Builds
-// `nsolves` (>= kSolvePrefixSplit) solves of 16..120 rows whose true rows carry
+// `nsolves` solves of 16..120 rows (split launches: solve_split) whose true rows carry
 // valid length prefixes and zero bytes past their lengths, as the decoder's
 // recovered originals do (with `corrupt`, every third solve gets non-zero
 // bytes past one row's length: inconsistent recovery data), forms the rows
@@ -4283,7 +4283,7 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
                                                                                 uint32_t corrupt,
                                                                                 uint32_t* stats)
 {
-    if (nsolves < kSolvePrefixSplit || !gf_init())
+    if (nsolves == 0 || !gf_init())
         return -1;
     bind_device();
     uint64_t st = seed * 0x9E3779B97F4A7C15ull + 1;
@@ -4422,10 +4422,13 @@ extern "C" __attribute__((visibility("default"))) int sgpu_selftest_solve_paths(
     std::vector<uint32_t> outRes[2];
     const SolvePath paths[2] = {kPathSweeps, kPathVector};
     for (int k = 0; k < 2 && ok; ++k) {
-        ok = hipMemcpy(dRows, hostRows.data(), hostRows.size(), hipMemcpyHostToDevice) == hipSuccess &&
-             hipMemset(dRes, 0xff, (size_t)resWords * 4) == hipSuccess &&
-             hipMemset(dScratch, 0xa5, scratch + 256) == hipSuccess &&
-             hipMemset(dAcct, 0, 4 * sizeof(uint64_t)) == hipSuccess;
+        // (on the solve's own stream: a plain hipMemset runs on the null
+        // stream, which does not order against g_stream (non-blocking), and a
+        // late scratch fill overwrote some T inverses mid-solve)
+        ok = hipMemcpyAsync(dRows, hostRows.data(), hostRows.size(), hipMemcpyHostToDevice, g_stream) == hipSuccess &&
+             hipMemsetAsync(dRes, 0xff, (size_t)resWords * 4, g_stream) == hipSuccess &&
+             hipMemsetAsync(dScratch, 0xa5, scratch + 256, g_stream) == hipSuccess &&
+             hipMemsetAsync(dAcct, 0, 4 * sizeof(uint64_t), g_stream) == hipSuccess;
         if (!ok)
             break;
         launch_solve(dDesc, dRowD, dCoef, dRes, dItems, (uint32_t)items.size(), maxRows, dAcct, 0, nsolves,

@@ -1304,7 +1304,7 @@ SiameseResult DecoderCore::decode_device(SiameseOriginalPacket** packetsOut, uns
         return Siamese_NeedMoreData;
     // (the search's first attempt, on a fresh matrix: decode_loop's first
     // decode_region)
-    if (region_.recoveryCount >= region_.lostCount && rows_.empty() && geResume_ == 0 &&
+    if (region_.recoveryCount >= region_.lostCount && rows_.empty() && geResume_ == 0 && !geHost_ &&
         (submit_chained() || submit_device_ge()))
         return kDecodePending;
     return decode_loop(packetsOut, countOut);
@@ -1521,6 +1521,7 @@ SiameseResult DecoderCore::finish_chained(SiameseOriginalPacket** packetsOut, un
         drop_solve();
         chain_sums_restore();
         eng_->shard().stats.geRetried++;
+        geHost_ = true;
         matrix_reset();
         return decode_loop(packetsOut, countOut);
     }
@@ -1602,6 +1603,7 @@ SiameseResult DecoderCore::finish_device_ge(SiameseOriginalPacket** packetsOut, 
         // the elimination stopped short of a pivot: the host repeats it (the
         // resumable state the reference keeps for the next attempt), and the
         // search goes on as decode() does
+        geHost_ = true;
         matrix_reset();
         return decode_loop(packetsOut, countOut);
     }

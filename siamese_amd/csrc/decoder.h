@@ -403,6 +403,10 @@ private:
     std::vector<unsigned> pivots_;
     std::vector<unsigned> geEnd_;   // gaussian_elimination: each pivot row's column count
     unsigned geResume_ = 0;
+    // a device elimination came out singular: this decoder's later attempts
+    // eliminate on the host, in the round that runs their symbol work (a
+    // lone device job is a 48 us latency-bound launch on the step's tail)
+    bool geHost_ = false;
     uint64_t geBytes_ = 0;   // coefficient bytes the elimination multiplied (accounting)
     // the current pivot row's bytes after the pivot, split for gf_muladd_prepared
     GfRowSrc geSrc_;

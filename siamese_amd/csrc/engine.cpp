@@ -1380,6 +1380,7 @@ struct Batch
     uint32_t maxIngest = 0;
     size_t oIngD = 0, oIngB = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
     size_t oGeD = 0, oGeIn = 0, nGe = 0;   // device matrix jobs: descs, inputs
+    size_t geHead = 0;                      // bytes of the upload's head: the jobs and what they write
     uint32_t geMaxRows = 0, geMaxCols = 0;  // ... their largest matrix (k_ge's LDS)
     bool geChained = false;                 // a job writes into the upload (kGeChained)
     size_t oCopy = 0;                      // the download copy list (BeCopy records)
@@ -2083,7 +2084,7 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
 #endif
             sv.itemCount = sitems.size() - sv.itemBegin;
             sv.solveCount = sdescs.size() - sv.solveBegin;
-            if (sv.solveCount >= kSolvePrefixSplit)
+            if (solve_split((uint32_t)sv.solveCount, sv.maxRows))
                 for (size_t i = sv.solveBegin; i < sdescs.size(); ++i) {
                     // the inverse's scratch (matrix-core path), in the k_ldpc ring
                     // after this submission's k_ldpc scratch (1 + its offset
@@ -2161,7 +2162,20 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     bt.nIngest = nIngest;
     bt.nIngBlocks = nIngBlocks;
 
+    // The matrix jobs, then the solves' rows and coefficients (which a chained
+    // job rewrites), at the head of the upload: that head is copied first and
+    // k_ge starts on it while the rest is still crossing the bus
+    // (launch_batch).
     size_t off = 0;
+    bt.oGeD = off;
+    off = align16(off + gdescs.size() * sizeof(GeDesc));
+    bt.oGeIn = off;
+    off = align16(off + geInBytes);
+    bt.oSR = off;
+    off = align16(off + nSolveRows * sizeof(SolveRow));
+    bt.oCoef = off;
+    off = align16(off + nCoef);
+    bt.geHead = off;
     const size_t oStage = off;
     off = align16(off + stageBytes);
     bt.oIngD = off;
@@ -2174,18 +2188,10 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     off = align16(off + nItems * sizeof(ExecItem));
     bt.oSD = off;
     off = align16(off + sdescs.size() * sizeof(SolveDesc));
-    bt.oSR = off;
-    off = align16(off + nSolveRows * sizeof(SolveRow));
-    bt.oCoef = off;
-    off = align16(off + nCoef);
     bt.oSI = off;
     off = align16(off + sitems.size() * sizeof(SolveItem));
     bt.oWide = off;
     off = align16(off + nWide * sizeof(LdpcItem));
-    bt.oGeD = off;
-    off = align16(off + gdescs.size() * sizeof(GeDesc));
-    bt.oGeIn = off;
-    off = align16(off + geInBytes);
     // the download copy list (the counters and results, then every range)
     size_t nDownloads = 0;
     for (const Shard::Queues& q : bt.queues)
@@ -2411,17 +2417,26 @@ void Engine::launch_batch(Batch& bt)
         be_mark_release(m);
     }
     bt.marks.clear();
-    if (bt.upBytes && bt.upBase == xs.upDev) {
-        const BeCopy up{(uint64_t)(uintptr_t)xs.upDev, (uint64_t)(uintptr_t)xs.upHost, bt.upBytes};
+    // The upload; with matrix jobs, its head first (the jobs' inputs and the
+    // solve rows and coefficients they rewrite): the jobs start on their own
+    // stream once it has landed, beside the rest of the copy and k_ingest,
+    // until the decoders' first phase joins them.
+    const bool copyUp = bt.upBytes && bt.upBase == xs.upDev;
+    const size_t head = (copyUp && bt.nGe) ? bt.geHead : 0;
+    if (head) {
+        const BeCopy up{(uint64_t)(uintptr_t)xs.upDev, (uint64_t)(uintptr_t)xs.upHost, head};
         be_copy_pinned(&up, 1, true);
     }
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
-    // the matrix jobs first, on their own stream: they need only the upload
-    // and run beside what follows until the decoders' first phase joins them
     if (bt.nGe)
         be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev,
                      (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols);
+    if (copyUp && bt.upBytes > head) {
+        const BeCopy up{(uint64_t)(uintptr_t)xs.upDev + head, (uint64_t)(uintptr_t)xs.upHost + head,
+                        bt.upBytes - head};
+        be_copy_pinned(&up, 1, true);
+    }
     if (bt.nIngest)
         be_launch_ingest((const IngestDesc*)(bt.upBase + bt.oIngD), (uint32_t)bt.nIngest, bt.maxIngest,
                          (const uint32_t*)(bt.upBase + bt.oIngB), (uint32_t)bt.nIngBlocks);

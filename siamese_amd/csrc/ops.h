@@ -296,10 +296,19 @@ struct SolveDesc
 };
 
 /// Solves of up to this many rows may run as the product X = T R (their
-/// inverse T = U^-1 L^-1 in scratch, rows of kTStride bytes), in launches of
-/// at least kSolvePrefixSplit solves (the prefix pass is then its own launch).
+/// inverse T = U^-1 L^-1 in scratch, rows of kTStride bytes), in split
+/// launches (solve_split: the prefix pass is then its own launch).
 constexpr unsigned kProductMaxRows = 120;
 constexpr unsigned kSolvePrefixSplit = 16;
+constexpr unsigned kSolveSplitMinRows = 16;
+/// Whether a launch's solves take the split form (prefix pass and inverse,
+/// product, copy-in: three launches) rather than k_solve_main's fused sweeps:
+/// many solves, or any solve whose serial sweeps would outlast the three
+/// launches (a lone 51-row solve: 209 us as sweeps, profiles/r6_kernel_stats).
+constexpr bool solve_split(uint32_t solveCount, uint32_t maxRows)
+{
+    return solveCount >= kSolvePrefixSplit || maxRows >= kSolveSplitMinRows;
+}
 constexpr uint32_t kTStride = 128;
 constexpr uint32_t solve_t_bytes(uint32_t m)
 {
