@@ -85,9 +85,12 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 /// nothing any other launch of the flush writes.  It may run beside the
 /// launches queued after it until be_join_ge(), after which every launch
 /// (and the results' download) sees its outputs.  maxRows / maxCols: the
-/// largest job of the launch (sizes its LDS).
+/// largest job of the launch (sizes its LDS).  head (or null): a pinned H2D
+/// copy that brings the jobs' inputs, rows and coefficients into place, run
+/// ahead of them on their own stream (beside the codec stream's copies); it
+/// must not overlap anything the codec stream writes or copies.
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
-                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols);
+                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head);
 void be_join_ge();
 
 /// Block until all queued work has finished.  Returns false on a device fault.

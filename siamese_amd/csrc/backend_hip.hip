@@ -4174,18 +4174,27 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
 }
 
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
-                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols)
+                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head)
 {
     if (count == 0)
         return;
-    // On the side stream, after everything the codec stream has queued (the
-    // upload): the jobs run beside k_ingest, which reads nothing they write,
-    // and be_join_ge puts the codec stream behind them (Engine::launch_batch
-    // joins before the first k_exec).  Same box, interleaved: headline 4.97
-    // ms/step on the side stream against 5.34 with the jobs in line on the
-    // codec stream (profiles/r6q_modes_ab.txt).
-    check(hipEventRecord(g_geFork, g_stream), "hipEventRecord(ge fork)");
-    check(hipStreamWaitEvent(g_geStream, g_geFork, 0), "hipStreamWaitEvent(ge)");
+    // On the side stream: the jobs run beside the codec stream's copy and
+    // k_ingest, which read nothing they write, and be_join_ge puts the codec
+    // stream behind them (Engine::launch_batch joins before the first
+    // k_exec).  Same box, interleaved: headline 4.97 ms/step on the side
+    // stream against 5.34 with the jobs in line on the codec stream
+    // (profiles/r6q_modes_ab.txt).  With `head`, their part of the upload is
+    // copied on the side stream too, beside the codec stream's copy of the
+    // rest (a second copy behind the first on one stream started ~17 us after
+    // it); without, they wait for everything the codec stream queued.
+    if (head) {
+        check(hipMemcpyAsync((void*)(uintptr_t)head->dst, (const void*)(uintptr_t)head->src, head->bytes,
+                             hipMemcpyHostToDevice, g_geStream),
+              "H2D (ge head)");
+    } else {
+        check(hipEventRecord(g_geFork, g_stream), "hipEventRecord(ge fork)");
+        check(hipStreamWaitEvent(g_geStream, g_geFork, 0), "hipStreamWaitEvent(ge)");
+    }
     {
         Timed t(kBeGe, g_geStream);
         hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), (size_t)ge_lds_bytes(maxRows, maxCols), g_geStream,

@@ -2417,21 +2417,20 @@ void Engine::launch_batch(Batch& bt)
         be_mark_release(m);
     }
     bt.marks.clear();
-    // The upload; with matrix jobs, its head first (the jobs' inputs and the
-    // solve rows and coefficients they rewrite): the jobs start on their own
-    // stream once it has landed, beside the rest of the copy and k_ingest,
-    // until the decoders' first phase joins them.
+    // The upload.  With matrix jobs its head (the jobs' inputs and the solve
+    // rows and coefficients they rewrite) is copied on the jobs' own stream,
+    // and the jobs start once it has landed, beside the codec stream's copy
+    // of the rest and k_ingest, until the decoders' first phase joins them.
     const bool copyUp = bt.upBytes && bt.upBase == xs.upDev;
     const size_t head = (copyUp && bt.nGe) ? bt.geHead : 0;
-    if (head) {
-        const BeCopy up{(uint64_t)(uintptr_t)xs.upDev, (uint64_t)(uintptr_t)xs.upHost, head};
-        be_copy_pinned(&up, 1, true);
-    }
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
-    if (bt.nGe)
+    if (bt.nGe) {
+        const BeCopy hc{(uint64_t)(uintptr_t)xs.upDev, (uint64_t)(uintptr_t)xs.upHost, head};
         be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev,
-                     (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols);
+                     (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols,
+                     head ? &hc : nullptr);
+    }
     if (copyUp && bt.upBytes > head) {
         const BeCopy up{(uint64_t)(uintptr_t)xs.upDev + head, (uint64_t)(uintptr_t)xs.upHost + head,
                         bt.upBytes - head};

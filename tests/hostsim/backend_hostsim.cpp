@@ -620,8 +620,10 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 // elimination without pivoting while the pivots allow it and with row
 // pivoting from the first zero pivot (:2423-2531), as the kernel runs it.
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* srows,
-                  uint8_t* scoef, uint32_t, uint32_t)
+                  uint8_t* scoef, uint32_t, uint32_t, const BeCopy* head)
 {
+    if (head)
+        be_copy_pinned(head, 1, true);
     for (uint32_t jb = 0; jb < count; ++jb) {
         const GeDesc d = descs[jb];
         const unsigned rows = d.rows, cols = d.cols;

@@ -147,8 +147,10 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 // matrix jobs: every one reports an eliminated matrix with identity pivots,
 // its first `cols` rows used and zero coefficients (no elimination on the host)
 void be_launch_ge(const GeDesc* descs, const uint8_t*, uint32_t count, uint32_t* results, SolveRow*, uint8_t*,
-                  uint32_t, uint32_t)
+                  uint32_t, uint32_t, const BeCopy* head)
 {
+    if (head)
+        be_copy_pinned(head, 1, true);
     const GeDesc* dd = host_view(descs);
     for (uint32_t j = 0; j < count; ++j) {
         const GeDesc d = dd[j];
