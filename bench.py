@@ -732,7 +732,11 @@ def main(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--threads", type=int, default=0,
                     help="host threads driving streams (0 = library default)")
-    ap.add_argument("--groups", type=int, default=4,
+    # (8 since round 6: with the device elimination a group's round carries
+    # k_ge and a singular decode's extra round, and smaller groups keep the
+    # pipeline fuller: 4.42-4.54 against 4.69-4.77 ms/step with 4, same box,
+    # interleaved, profiles/r6g_groups_ab.txt)
+    ap.add_argument("--groups", type=int, default=8,
                     help="stream groups alternating host and device work (1 = no overlap)")
     ap.add_argument("--defer", type=int, default=0,
                     help="deferred decode outputs: a stream submits after every DEFER-th decode "
