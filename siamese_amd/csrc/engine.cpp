@@ -1311,6 +1311,19 @@ void Engine::ensure_wide(XferSet& x, size_t bytes)
     x.wideCap = cap;
 }
 
+void Engine::ensure_solve(XferSet& x, size_t bytes)
+{
+    if (bytes <= x.solveCap)
+        return;
+    size_t cap = x.solveCap ? x.solveCap : (4u << 20);
+    while (cap < bytes)
+        cap *= 2;
+    if (x.solveDev)
+        be_dev_free(x.solveDev);
+    x.solveDev = (uint8_t*)be_dev_alloc(cap);
+    x.solveCap = cap;
+}
+
 void Engine::ensure_down(XferSet& x, size_t bytes)
 {
     if (bytes <= x.downCap)
@@ -2209,12 +2222,10 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     // (a chained matrix job writes its solve's rows and coefficients into
     // the upload: the device copy then)
     bt.upBase = (xs.upHostDev && bt.upBytes <= kZeroCopyUp && !bt.geChained) ? xs.upHostDev : xs.upDev;
-    if (wideBytes + tBytes) {
+    if (wideBytes) {
         // k_ldpc scratch comes from the set's ring, which is zeroed as a whole
-        // when it wraps (not per submission: most flushes then need no memset);
-        // the solves' inverses follow it (written before they are read, in
-        // this submission, so the zeroing is no concern of theirs)
-        const uint64_t need = wideBytes + tBytes;
+        // when it wraps (not per submission: most flushes then need no memset)
+        const uint64_t need = wideBytes;
         if (xs.wideUsed + need > xs.wideCap) {
             ensure_wide(xs, std::max<size_t>(need, 16u << 20));
             xs.wideUsed = 0;
@@ -2222,7 +2233,13 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
         }
         bt.wideBase = xs.wideUsed;
         xs.wideUsed += need;
-        const uint64_t tBase = (uint64_t)(uintptr_t)xs.wideDev + bt.wideBase + wideBytes;
+    }
+    if (tBytes) {
+        // the solves' inverses and results: their own scratch, from its start
+        // (sharing the ring made the headline zero 16 MiB every submission or
+        // two, 134 MB of the step's traffic, profiles/r6_traffic.json of r6e)
+        ensure_solve(xs, tBytes);
+        const uint64_t tBase = (uint64_t)(uintptr_t)xs.solveDev;
         for (SolveDesc& d : sdescs)
             if (d.tinv) {
                 d.tinv = tBase + (d.tinv - 1);

@@ -760,6 +760,10 @@ private:
         uint8_t* wideDev = nullptr;   // k_ldpc scratch ring (see ensure_wide)
         size_t wideCap = 0;
         size_t wideUsed = 0;          // bytes of the ring dirtied since it was zeroed
+        // the product solves' inverses and results (written before they are
+        // read within a submission: reused from its start, never zeroed)
+        uint8_t* solveDev = nullptr;
+        size_t solveCap = 0;
         // the device byte counters at the head of downDev only grow (no
         // memset per submission): each completion takes the difference
         uint64_t acctPrev[4] = {0, 0, 0, 0};
@@ -767,6 +771,7 @@ private:
     } sets_[kSets];
     void ensure_up(XferSet& x, size_t bytes);
     void ensure_wide(XferSet& x, size_t bytes);
+    void ensure_solve(XferSet& x, size_t bytes);
     void ensure_down(XferSet& x, size_t bytes);
 
     // gather buffers (separate from the flush buffers)
