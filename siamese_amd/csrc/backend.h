@@ -90,7 +90,13 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 /// ahead of them on their own stream (beside the codec stream's copies); it
 /// must not overlap anything the codec stream writes or copies.
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
-                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head);
+                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head, bool side = true);
+/// The other arrangement: with side = false the jobs (and their head copy)
+/// run in order on the codec stream, and this puts the rest of the upload
+/// (`rest`, or null) and k_ingest (be_launch_ingest's arguments) on the side
+/// stream beside them; be_join_ge joins it.
+void be_side_upload_ingest(const BeCopy* rest, const IngestDesc* descs, uint32_t count, uint32_t maxBytes,
+                           const uint32_t* blocks, uint32_t nblocks);
 void be_join_ge();
 
 /// Block until all queued work has finished.  Returns false on a device fault.

@@ -4174,10 +4174,25 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
 }
 
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
-                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head)
+                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head, bool side)
 {
     if (count == 0)
         return;
+    if (!side) {
+        // in order on the codec stream (be_side_upload_ingest puts the rest
+        // of the upload and k_ingest beside them, after the fork recorded
+        // here)
+        check(hipEventRecord(g_geFork, g_stream), "hipEventRecord(ge fork)");
+        check(hipStreamWaitEvent(g_geStream, g_geFork, 0), "hipStreamWaitEvent(side)");
+        if (head)
+            check(hipMemcpyAsync((void*)(uintptr_t)head->dst, (const void*)(uintptr_t)head->src, head->bytes,
+                                 hipMemcpyHostToDevice, g_stream),
+                  "H2D (ge head)");
+        Timed t(kBeGe);
+        hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), (size_t)ge_lds_bytes(maxRows, maxCols), g_stream,
+                           descs, in, results, rows, coef);
+        return;
+    }
     // On the side stream: the jobs run beside the codec stream's copy and
     // k_ingest, which read nothing they write, and be_join_ge puts the codec
     // stream behind them (Engine::launch_batch joins before the first
@@ -4201,6 +4216,28 @@ void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32
                            descs, in, results, rows, coef);
     }
     check(hipEventRecord(g_geJoin, g_geStream), "hipEventRecord(ge join)");
+    g_gePending = true;
+}
+
+void be_side_upload_ingest(const BeCopy* rest, const IngestDesc* descs, uint32_t count, uint32_t maxBytes,
+                           const uint32_t* blocks, uint32_t nblocks)
+{
+    bind_device();
+    // after everything the codec stream queued before this submission's
+    // matrix jobs (an application may pass the output of an earlier
+    // submission as an original: k_ingest must not read it early); the jobs
+    // were queued after this fork point, so the two run side by side
+    if (rest && rest->bytes)
+        check(hipMemcpyAsync((void*)(uintptr_t)rest->dst, (const void*)(uintptr_t)rest->src, rest->bytes,
+                             hipMemcpyHostToDevice, g_geStream),
+              "H2D (upload rest)");
+    const uint32_t chunks = maxBytes ? (maxBytes + kIngestChunkBytes - 1) / kIngestChunkBytes : 1;
+    const uint32_t grid = blocks ? nblocks : (count + kIngestWaves - 1) / kIngestWaves;
+    if (count && grid) {
+        Timed t(kBeIngest, g_geStream);
+        hipLaunchKernelGGL(k_ingest, dim3(grid, chunks), dim3(64 * kIngestWaves), 0, g_geStream, descs, count, blocks);
+    }
+    check(hipEventRecord(g_geJoin, g_geStream), "hipEventRecord(side join)");
     g_gePending = true;
 }
 

@@ -2423,6 +2423,15 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     st.assembleNs = now_ns() - t0;
 }
 
+// The matrix jobs in order on the codec stream, the rest of the upload and
+// k_ingest beside them (launch_batch).  Traces of both arrangements
+// (tools/r6_trace_libs.sh): a round's first k_exec starts 150 us after its
+// first copy against 157 with the jobs on the side stream; a cross-stream
+// wait costs 16-23 us before the next kernel even when satisfied, and a
+// kernel starts 12-20 us after a copy on its queue.  Headline within noise
+// (profiles/r6l_ge_codec_stream_ab.txt).
+constexpr bool kGeOnCodecStream = true;
+
 void Engine::launch_batch(Batch& bt)
 {
     XferSet& xs = sets_[bt.set];
@@ -2435,25 +2444,35 @@ void Engine::launch_batch(Batch& bt)
     }
     bt.marks.clear();
     // The upload.  With matrix jobs its head (the jobs' inputs and the solve
-    // rows and coefficients they rewrite) is copied on the jobs' own stream,
-    // and the jobs start once it has landed, beside the codec stream's copy
-    // of the rest and k_ingest, until the decoders' first phase joins them.
+    // rows and coefficients they rewrite) is copied first and the jobs run on
+    // it in order on the codec stream, while the rest of the upload and
+    // k_ingest run beside them on the side stream, joined before the first
+    // phase.  (The other way round -- the jobs on the side stream -- the
+    // codec stream's join waited on a job that ended about when k_ingest did,
+    // and a cross-stream wait that is not yet satisfied costs ~24 us of
+    // latency on the join; a satisfied one costs next to nothing.)
     const bool copyUp = bt.upBytes && bt.upBase == xs.upDev;
     const size_t head = (copyUp && bt.nGe) ? bt.geHead : 0;
     uint64_t* acctDev = (uint64_t*)xs.downDev;
     uint32_t* resultsDev = (uint32_t*)(xs.downDev + kAcctBytes);
+    const BeCopy rest{(uint64_t)(uintptr_t)xs.upDev + head, (uint64_t)(uintptr_t)xs.upHost + head,
+                      bt.upBytes - head};
+    bool ingested = false;
     if (bt.nGe) {
         const BeCopy hc{(uint64_t)(uintptr_t)xs.upDev, (uint64_t)(uintptr_t)xs.upHost, head};
         be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev,
                      (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols,
-                     head ? &hc : nullptr);
+                     head ? &hc : nullptr, !(head && kGeOnCodecStream));
+        if (head && kGeOnCodecStream) {
+            be_side_upload_ingest(bt.upBytes > head ? &rest : nullptr, (const IngestDesc*)(bt.upBase + bt.oIngD),
+                                  (uint32_t)bt.nIngest, bt.maxIngest, (const uint32_t*)(bt.upBase + bt.oIngB),
+                                  (uint32_t)bt.nIngBlocks);
+            ingested = true;
+        }
     }
-    if (copyUp && bt.upBytes > head) {
-        const BeCopy up{(uint64_t)(uintptr_t)xs.upDev + head, (uint64_t)(uintptr_t)xs.upHost + head,
-                        bt.upBytes - head};
-        be_copy_pinned(&up, 1, true);
-    }
-    if (bt.nIngest)
+    if (!ingested && copyUp && bt.upBytes > head)
+        be_copy_pinned(&rest, 1, true);
+    if (!ingested && bt.nIngest)
         be_launch_ingest((const IngestDesc*)(bt.upBase + bt.oIngD), (uint32_t)bt.nIngest, bt.maxIngest,
                          (const uint32_t*)(bt.upBase + bt.oIngB), (uint32_t)bt.nIngBlocks);
     if (xs.acctZero) {
@@ -2468,8 +2487,11 @@ void Engine::launch_batch(Batch& bt)
     size_t wideDone = 0;
     for (size_t k = 0; k < bt.phases.size() && bt.phases[k].kind == Phase::EXEC; ++k)
         wideDone = bt.phases[k].wideBegin + bt.phases[k].wideCount;
-    if (wideDone)
+    if (wideDone) {
+        if (ingested)
+            be_join_ge();   // (its items and the elements they read came with the side stream)
         be_launch_ldpc((const LdpcItem*)(bt.upBase + bt.oWide), (uint32_t)wideDone, acctDev + 3);
+    }
     // The codec stream joins the matrix jobs before the first executor launch
     // (they run beside k_ingest): joined only before the decoders' phases,
     // they shared the CUs with the encoders' k_exec, which slowed from 87 to

@@ -619,8 +619,16 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 // generate_matrix, reference SiameseDecoder.cpp:2157-2383), then the
 // elimination without pivoting while the pivots allow it and with row
 // pivoting from the first zero pivot (:2423-2531), as the kernel runs it.
+void be_side_upload_ingest(const BeCopy* rest, const IngestDesc* descs, uint32_t count, uint32_t maxBytes,
+                           const uint32_t* blocks, uint32_t nblocks)
+{
+    if (rest)
+        be_copy_pinned(rest, 1, true);
+    be_launch_ingest(descs, count, maxBytes, blocks, nblocks);
+}
+
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* srows,
-                  uint8_t* scoef, uint32_t, uint32_t, const BeCopy* head)
+                  uint8_t* scoef, uint32_t, uint32_t, const BeCopy* head, bool)
 {
     if (head)
         be_copy_pinned(head, 1, true);

@@ -146,8 +146,14 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 
 // matrix jobs: every one reports an eliminated matrix with identity pivots,
 // its first `cols` rows used and zero coefficients (no elimination on the host)
+void be_side_upload_ingest(const BeCopy* rest, const IngestDesc*, uint32_t, uint32_t, const uint32_t*, uint32_t)
+{
+    if (rest)
+        be_copy_pinned(rest, 1, true);
+}
+
 void be_launch_ge(const GeDesc* descs, const uint8_t*, uint32_t count, uint32_t* results, SolveRow*, uint8_t*,
-                  uint32_t, uint32_t, const BeCopy* head)
+                  uint32_t, uint32_t, const BeCopy* head, bool)
 {
     if (head)
         be_copy_pinned(head, 1, true);
