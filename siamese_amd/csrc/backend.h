@@ -89,8 +89,12 @@ void be_launch_solve(const SolveDesc* solves, const SolveRow* rows, const uint8_
 /// copy that brings the jobs' inputs, rows and coefficients into place, run
 /// ahead of them on their own stream (beside the codec stream's copies); it
 /// must not overlap anything the codec stream writes or copies.
+/// rowsIn (or null: rows): where a chained job reads its solve rows before it
+/// writes them to `rows` in pivot order; with descs, in and rowsIn in mapped
+/// pinned memory and no head, the jobs need no copy at all.
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
-                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head, bool side = true);
+                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head, bool side = true,
+                  const SolveRow* rowsIn = nullptr);
 /// The other arrangement: with side = false the jobs (and their head copy)
 /// run in order on the codec stream, and this puts the rest of the upload
 /// (`rest`, or null) and k_ingest (be_launch_ingest's arguments) on the side

@@ -3352,7 +3352,7 @@ __host__ __device__ constexpr uint32_t ge_lds_bytes(uint32_t rows, uint32_t cols
 
 __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ descs, const uint8_t* __restrict__ in,
                                                   uint32_t* __restrict__ results, SolveRow* __restrict__ srows,
-                                                  uint8_t* __restrict__ scoef)
+                                                  uint8_t* __restrict__ scoef, const SolveRow* __restrict__ srowsIn)
 {
     extern __shared__ uint32_t M[];   // rows x S4 dwords
     __shared__ uint4 permL[256];
@@ -3366,6 +3366,7 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
     __shared__ uint8_t pickL[kGePickLds];
     __shared__ uint32_t foundL[3], nzL;
     __shared__ unsigned long long bytesL;
+    __shared__ uint32_t srL[kGeMaxCols][6];   // a chained job's solve rows as they came (SolveRow)
     const uint8_t* invB = reinterpret_cast<const uint8_t*>(invL);
     uint8_t* Mb = reinterpret_cast<uint8_t*>(M);
 #ifdef SGPU_GE_CLOCKS
@@ -3398,6 +3399,15 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
     }
     if (tid < cols)
         C[tid] = Cg[tid];
+    // (a chained job's solve rows, from wherever the upload's head is read:
+    // they are rewritten in pivot order at the end)
+    static_assert(sizeof(SolveRow) == 24, "SolveRow layout");
+    if ((d.flags & kGeChained) && tid < cols) {
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(srowsIn + d.solveRow) + 6u * tid;
+#pragma unroll
+        for (unsigned k = 0; k < 6; ++k)
+            srL[tid][k] = s[k];
+    }
     if (pickStaged)
         for (uint32_t x = 4u * tid; x < d.pickLen; x += 4u * kGeThreads) {
             // (the pick table starts 4-byte aligned: GeRow 16 B, GeCol 4 B)
@@ -3657,23 +3667,15 @@ __global__ __launch_bounds__(kGeThreads) void k_ge(const GeDesc* __restrict__ de
             co[x] = Mb[piv[j] * SB + i];
         }
         // the solve's rows in pivot order, each keeping its head slot
-        // (SolveRow: 6 dwords, the last the head slot): every thread reads
-        // its row before any thread writes
-        static_assert(sizeof(SolveRow) == 24, "SolveRow layout");
+        // (SolveRow: 6 dwords, the last the head slot), from their staged copy
         uint32_t* sr = reinterpret_cast<uint32_t*>(srows + d.solveRow);
-        uint32_t t[6];
         if (tid < cols) {
             const uint32_t src = piv[tid];
 #pragma unroll
-            for (unsigned k = 0; k < 6; ++k)
-                t[k] = sr[6u * src + k];
-            t[5] = 1u + solve_head_slot(t[5], src);
+            for (unsigned k = 0; k < 5; ++k)
+                sr[6u * tid + k] = srL[src][k];
+            sr[6u * tid + 5] = 1u + solve_head_slot(srL[src][5], src);
         }
-        __syncthreads();
-        if (tid < cols)
-#pragma unroll
-            for (unsigned k = 0; k < 6; ++k)
-                sr[6u * tid + k] = t[k];
         return;
     }
     for (uint32_t w = tid; w < (rows + 1u) / 2u; w += kGeThreads)
@@ -4174,7 +4176,8 @@ void be_launch_ldpc(const LdpcItem* items, uint32_t count, uint64_t* acct)
 }
 
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* rows,
-                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head, bool side)
+                  uint8_t* coef, uint32_t maxRows, uint32_t maxCols, const BeCopy* head, bool side,
+                  const SolveRow* rowsIn)
 {
     if (count == 0)
         return;
@@ -4190,7 +4193,7 @@ void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32
                   "H2D (ge head)");
         Timed t(kBeGe);
         hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), (size_t)ge_lds_bytes(maxRows, maxCols), g_stream,
-                           descs, in, results, rows, coef);
+                           descs, in, results, rows, coef, rowsIn ? rowsIn : rows);
         return;
     }
     // On the side stream: the jobs run beside the codec stream's copy and
@@ -4213,7 +4216,7 @@ void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32
     {
         Timed t(kBeGe, g_geStream);
         hipLaunchKernelGGL(k_ge, dim3(count), dim3(kGeThreads), (size_t)ge_lds_bytes(maxRows, maxCols), g_geStream,
-                           descs, in, results, rows, coef);
+                           descs, in, results, rows, coef, rowsIn ? rowsIn : rows);
     }
     check(hipEventRecord(g_geJoin, g_geStream), "hipEventRecord(ge join)");
     g_gePending = true;

@@ -1394,6 +1394,7 @@ struct Batch
     size_t oIngD = 0, oIngB = 0, oStream = 0, oItems = 0, oSD = 0, oSR = 0, oCoef = 0, oSI = 0, oWide = 0;
     size_t oGeD = 0, oGeIn = 0, nGe = 0;   // device matrix jobs: descs, inputs
     size_t geHead = 0;                      // bytes of the upload's head: the jobs and what they write
+    bool allGated = false;                  // every solve of the submission is a chained job's
     uint32_t geMaxRows = 0, geMaxCols = 0;  // ... their largest matrix (k_ge's LDS)
     bool geChained = false;                 // a job writes into the upload (kGeChained)
     size_t oCopy = 0;                      // the download copy list (BeCopy records)
@@ -2189,6 +2190,9 @@ void Engine::assemble_batch(Batch& bt, WorkerPool& wp)
     bt.oCoef = off;
     off = align16(off + nCoef);
     bt.geHead = off;
+    bt.allGated = !sdescs.empty();
+    for (const SolveDesc& d : sdescs)
+        bt.allGated = bt.allGated && d.gate != 0;
     const size_t oStage = off;
     off = align16(off + stageBytes);
     bt.oIngD = off;
@@ -2458,7 +2462,22 @@ void Engine::launch_batch(Batch& bt)
     const BeCopy rest{(uint64_t)(uintptr_t)xs.upDev + head, (uint64_t)(uintptr_t)xs.upHost + head,
                       bt.upBytes - head};
     bool ingested = false;
-    if (bt.nGe) {
+    if (bt.nGe && head && kGeOnCodecStream && bt.allGated && xs.upHostDev) {
+        // Every solve here is a chained job's, so nothing in the head needs
+        // the copy: the jobs read their descriptors, inputs and solve rows
+        // from the pinned upload over the bus and write the solves' rows and
+        // coefficients to the device copy, starting at once (a kernel starts
+        // 12-20 us after a copy on its queue): a round's first k_exec 148 ->
+        // 118 us after its first copy (profiles/r6m_ge_zero_copy_ab.txt).
+        const uint8_t* hd = xs.upHostDev;
+        be_launch_ge((const GeDesc*)(hd + bt.oGeD), hd + bt.oGeIn, (uint32_t)bt.nGe, resultsDev,
+                     (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols, nullptr,
+                     false, (const SolveRow*)(hd + bt.oSR));
+        be_side_upload_ingest(bt.upBytes > head ? &rest : nullptr, (const IngestDesc*)(bt.upBase + bt.oIngD),
+                              (uint32_t)bt.nIngest, bt.maxIngest, (const uint32_t*)(bt.upBase + bt.oIngB),
+                              (uint32_t)bt.nIngBlocks);
+        ingested = true;
+    } else if (bt.nGe) {
         const BeCopy hc{(uint64_t)(uintptr_t)xs.upDev, (uint64_t)(uintptr_t)xs.upHost, head};
         be_launch_ge((const GeDesc*)(bt.upBase + bt.oGeD), bt.upBase + bt.oGeIn, (uint32_t)bt.nGe, resultsDev,
                      (SolveRow*)(bt.upBase + bt.oSR), bt.upBase + bt.oCoef, bt.geMaxRows, bt.geMaxCols,

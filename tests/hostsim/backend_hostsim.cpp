@@ -628,8 +628,10 @@ void be_side_upload_ingest(const BeCopy* rest, const IngestDesc* descs, uint32_t
 }
 
 void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32_t* results, SolveRow* srows,
-                  uint8_t* scoef, uint32_t, uint32_t, const BeCopy* head, bool)
+                  uint8_t* scoef, uint32_t, uint32_t, const BeCopy* head, bool, const SolveRow* srowsIn)
 {
+    if (!srowsIn)
+        srowsIn = srows;
     if (head)
         be_copy_pinned(head, 1, true);
     for (uint32_t jb = 0; jb < count; ++jb) {
@@ -747,7 +749,7 @@ void be_launch_ge(const GeDesc* descs, const uint8_t* in, uint32_t count, uint32
             for (unsigned j = 0; j < cols; ++j)
                 std::memcpy(co + (size_t)j * cols, &M[(size_t)piv[j] * cols], cols);
             SolveRow* sr = srows + d.solveRow;
-            std::vector<SolveRow> t(sr, sr + cols);
+            std::vector<SolveRow> t(srowsIn + d.solveRow, srowsIn + d.solveRow + cols);
             for (unsigned j = 0; j < cols; ++j) {
                 sr[j] = t[piv[j]];
                 sr[j].headIndex = 1 + solve_head_slot(t[piv[j]].headIndex, piv[j]);

@@ -153,7 +153,7 @@ void be_side_upload_ingest(const BeCopy* rest, const IngestDesc*, uint32_t, uint
 }
 
 void be_launch_ge(const GeDesc* descs, const uint8_t*, uint32_t count, uint32_t* results, SolveRow*, uint8_t*,
-                  uint32_t, uint32_t, const BeCopy* head, bool)
+                  uint32_t, uint32_t, const BeCopy* head, bool, const SolveRow*)
 {
     if (head)
         be_copy_pinned(head, 1, true);
