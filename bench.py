@@ -131,6 +131,45 @@ def host_info():
     return {"nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": model}
 
 
+def cgroup_cpu():
+    """(process CPU seconds, cgroup throttled seconds or None): read around
+    the timed region to tell whether the step is held by the box's CPU quota
+    (cgroup v2 cpu.stat of this process's cgroup)."""
+    t = os.times()
+    cpu = t.user + t.system
+    throttled = None
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = [l.split("::", 1)[1].strip() for l in f if l.startswith("0::")]
+        for base in (("/sys/fs/cgroup" + rel[0]) if rel else None, "/sys/fs/cgroup"):
+            if not base:
+                continue
+            p = os.path.join(base, "cpu.stat")
+            if os.path.exists(p):
+                with open(p) as f:
+                    kv = dict(l.split() for l in f if len(l.split()) == 2)
+                throttled = int(kv.get("throttled_usec", 0)) / 1e6
+                break
+    except (OSError, ValueError, IndexError):
+        pass
+    return cpu, throttled
+
+
+def cgroup_quota():
+    """The cgroup's CPU quota in CPUs (cpu.max), or None."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = [l.split("::", 1)[1].strip() for l in f if l.startswith("0::")]
+        for base in (("/sys/fs/cgroup" + rel[0]) if rel else None, "/sys/fs/cgroup"):
+            if base and os.path.exists(os.path.join(base, "cpu.max")):
+                with open(os.path.join(base, "cpu.max")) as f:
+                    q, per = f.read().split()[:2]
+                return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
 class CpuBaseline:
     """The reference codec on `threads` host cores over `cfg` (a bounded
     sample of the workload), measured once per measure() call so the runs can
@@ -469,11 +508,17 @@ def run_rank(rank, world, local, args, library, use_cuda):
         side_run()
 
     coll.barrier()
+    cpu0, thr0 = cgroup_cpu()
     t0 = time.perf_counter()
     res, rep = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
                         groups=args.groups, digest=False, defer=args.defer, device_ge=dge)
     coll.barrier()
     elapsed = time.perf_counter() - t0
+    cpu1, thr1 = cgroup_cpu()
+    cpu_used = {"process_cpus": round((cpu1 - cpu0) / elapsed, 2),
+                "cgroup_quota_cpus": cgroup_quota(),
+                "cgroup_throttled_ms": round((thr1 - thr0) * 1e3, 2) if thr0 is not None and thr1 is not None
+                else None}
     # one untimed step that counts the executor's compulsory bytes (every
     # distinct symbol read once, every output written once: the roofline's
     # byte figure; counting it costs assembly time, so never in the timed run)
@@ -627,6 +672,7 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "engine_ms_per_step": {k[:-3]: round(eng[k] / 1e6 / steps, 3)
                                    for k in ("assemble_ns", "wait_ns", "complete_ns",
                                              "reclaim_ns")},
+            "timed_region_cpu": cpu_used,
         },
         "roofline": {
             "bound": "hbm",
