@@ -1028,12 +1028,20 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
         if (!c.enc || !c.dec)
             J.streams[i].fail(2);
     };
-    auto advance = [&](Job& J) {
-        const bool fresh = J.fresh;
-        J.fresh = false;
-        for_streams(sh, J.live.size(), [&](size_t k) {
-            const unsigned i = J.live[k];
-            if (fresh)
+    // Advance the live streams of several jobs in ONE fork-join (the first
+    // listed first: a new job's long first rounds, then the short later
+    // rounds of jobs whose submissions completed, which fill the fork-join's
+    // tail instead of paying a fork-join of their own).
+    std::vector<std::pair<Job*, unsigned>> items;
+    auto advance_jobs = [&](Job* const* js, size_t count) {
+        items.clear();
+        for (size_t q = 0; q < count; ++q)
+            for (unsigned i : js[q]->live)
+                items.emplace_back(js[q], i);
+        for_streams(sh, items.size(), [&](size_t k) {
+            Job& J = *items[k].first;
+            const unsigned i = items[k].second;
+            if (J.fresh)
                 start_stream(J, i);
             BatchStream& st = J.streams[i];
             while (!st.done())
@@ -1048,9 +1056,17 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
                 c.dec = nullptr;
             }
         });
-        J.live.erase(std::remove_if(J.live.begin(), J.live.end(),
-                                    [&](unsigned i) { return J.streams[i].done(); }),
-                     J.live.end());
+        for (size_t q = 0; q < count; ++q) {
+            Job& J = *js[q];
+            J.fresh = false;
+            J.live.erase(std::remove_if(J.live.begin(), J.live.end(),
+                                        [&](unsigned i) { return J.streams[i].done(); }),
+                         J.live.end());
+        }
+    };
+    auto advance = [&](Job& J) {
+        Job* one = &J;
+        advance_jobs(&one, 1);
     };
     std::vector<std::unique_ptr<Job>> active;
     std::vector<std::unique_ptr<Job>> spareJobs;   // retired jobs, reused (their streams' vectors kept)
@@ -1096,6 +1112,28 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
         J.rounds.push_back(std::move(r));
         return true;
     };
+    // one submission for the jobs advanced together: each job's round holds
+    // its own tokens and the shared ticket
+    auto submit_jobs = [&](Job* const* js, size_t count) {
+        if (!collect_all())
+            return false;
+        for (size_t q = 0; q < count; ++q) {
+            Round r;
+            r.reqs = take_cur(*js[q]);
+            js[q]->rounds.push_back(std::move(r));
+        }
+        const long long ticket = api.enqueue();
+        if (timeline)
+            std::fprintf(stderr, "tl submit j%d t%lld jobs %zu\n", curJob, ticket, count);
+        ++*rounds;
+        for (size_t q = 0; q < count; ++q) {
+            if (ticket < 0)
+                js[q]->rounds.pop_back();
+            else
+                js[q]->rounds.back().ticket = ticket;
+        }
+        return ticket >= 0;
+    };
     auto dump = [&](Job& J) {
         // debugging aid: SCENARIO_DUMP="<stream index>:<path>" writes that
         // stream's event log (same format as scenario_run_capi's)
@@ -1120,8 +1158,30 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
     // are resolved, a job with room in flight is advanced (or retired), a new
     // job starts (round one, the bulk of a step's host work) while the
     // pipeline is shallow; the thread blocks only when none is possible.
+    // Later rounds ride in the next new job's fork-join and submission
+    // (classic mode, device-resident originals): a block-mode job's second
+    // round (decode finish, frees) is ~1/3 of its first, and on its own paid a
+    // whole fork-join's wake-ups and tail plus a submission
+    // (SCENARIO_MERGE_ROUNDS=0: each round on its own, as before).
+    static const bool kMergeRounds = [] {
+        const char* v = std::getenv("SCENARIO_MERGE_ROUNDS");
+        return !v || std::atoi(v) != 0;
+    }();
+    const bool merge = kMergeRounds && !sh.e2e && inFlightPerJob == 1;
+    std::vector<Job*> ready;   // (merge) jobs whose next round waits for the next fork-join
+    auto run_ready = [&]() {
+        if (ready.empty() || rc != 0)
+            return;
+        advance_jobs(ready.data(), ready.size());
+        lap(1);
+        if (!submit_jobs(ready.data(), ready.size()))
+            rc = -3;
+        lap(2);
+        ready.clear();
+    };
     while (rc == 0 && (next < jobs || !active.empty())) {
         bool did = false;
+        ready.clear();
         for (size_t k = 0; k < active.size() && rc == 0;) {
             Job& J = *active[k];
             curJob = (int)(J.step * G + J.begin);
@@ -1137,11 +1197,15 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             if (!J.live.empty()) {
                 if (J.rounds.size() < inFlightPerJob) {
                     did = true;
-                    advance(J);
-                    lap(1);
-                    if (!submit(J))
-                        rc = -3;
-                    lap(2);
+                    if (merge) {
+                        ready.push_back(&J);
+                    } else {
+                        advance(J);
+                        lap(1);
+                        if (!submit(J))
+                            rc = -3;
+                        lap(2);
+                    }
                 }
                 ++k;
                 continue;
@@ -1246,13 +1310,19 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
             for (unsigned i = 0; i < cnt; ++i)
                 J.live.push_back(i);
             lap(0);
-            advance(J);
-            lap(1);
-            if (!submit(J))
-                rc = -3;
-            lap(2);
+            if (merge) {
+                ready.insert(ready.begin(), &J);   // (its first round leads the fork-join)
+                run_ready();
+            } else {
+                advance(J);
+                lap(1);
+                if (!submit(J))
+                    rc = -3;
+                lap(2);
+            }
             active.push_back(std::move(jp));
         }
+        run_ready();   // (later rounds with no new job to ride with)
         if (rc == 0 && !did && !active.empty()) {
             // nothing to do until the oldest round in flight completes
             for (auto& a : active)
