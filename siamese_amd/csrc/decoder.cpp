@@ -62,6 +62,10 @@ struct DecoderCore::Spare
     std::vector<unsigned> scratchLen;
     std::vector<SolveRow> scratchRows;
     std::vector<uint8_t> scratchCoef;
+    std::vector<unsigned> geEnd;
+    std::vector<DevBuf> chainReleases;
+    std::vector<unsigned> chainColumns;   // (chainSums_.recoveredColumns)
+    std::vector<uint32_t> geOut;
 };
 
 void DecoderCore::adopt_spare()
@@ -86,6 +90,10 @@ void DecoderCore::adopt_spare()
     scratchLen_.swap(s->scratchLen);
     scratchRows_.swap(s->scratchRows);
     scratchCoef_.swap(s->scratchCoef);
+    geEnd_.swap(s->geEnd);
+    chainReleases_.swap(s->chainReleases);
+    chainSums_.recoveredColumns.swap(s->chainColumns);
+    geOut_.swap(s->geOut);
     CapStash<Spare>::put_shell(s);   // (now holding this decoder's empty vectors)
 }
 
@@ -138,6 +146,10 @@ void DecoderCore::donate_spare()
     scratchLen_.clear();
     scratchRows_.clear();
     scratchCoef_.clear();
+    geEnd_.clear();
+    chainReleases_.clear();
+    chainSums_.recoveredColumns.clear();
+    geOut_.clear();
     subwindows_.swap(s->subwindows);
     recovered_.swap(s->recovered);
     recoveredColumns_.swap(s->recoveredColumns);
@@ -155,6 +167,10 @@ void DecoderCore::donate_spare()
     scratchLen_.swap(s->scratchLen);
     scratchRows_.swap(s->scratchRows);
     scratchCoef_.swap(s->scratchCoef);
+    geEnd_.swap(s->geEnd);
+    chainReleases_.swap(s->chainReleases);
+    chainSums_.recoveredColumns.swap(s->chainColumns);
+    geOut_.swap(s->geOut);
     CapStash<Spare>::give(s);
 }
 
@@ -1378,7 +1394,7 @@ bool DecoderCore::submit_device_ge(bool chained)
         }
     }
     const uint32_t words = ge_result_words(rows, columns, chained);
-    prog_.on_complete([r = res_, base, words](const uint32_t* results) {
+    prog_.on_complete(res_, [r = res_.get(), base, words](const uint32_t* results) {
         std::lock_guard<std::mutex> g(r->mu);
         r->geOut.assign(results + base, results + base + words);
         r->geDone = true;
@@ -2226,7 +2242,7 @@ bool DecoderCore::solve_plan(uint32_t gateWord, unsigned* slotOut)
     pendingSolves_++;
     // (the back-substitution's reference source bytes need the recovered
     // lengths: the solve kernel counts them, SiameseDecoder.cpp:1131-1212)
-    prog_.on_complete([r = res_, slot](const uint32_t* results) { complete_solve(*r, slot, results); });
+    prog_.on_complete(res_, [r = res_.get(), slot](const uint32_t* results) { complete_solve(*r, slot, results); });
     *slotOut = slot;
     return true;
 }

@@ -17,6 +17,7 @@ EncoderCore::EncoderCore(Engine* eng, bool hostMirror) : eng_(eng), prog_(eng, 0
     // thread (see DecoderCore::Spare)
     if (SubwindowTable* t = CapStash<SubwindowTable>::take()) {
         subwindows_.swap(t->v);
+        recoveryHeld_.swap(t->held);
         CapStash<SubwindowTable>::put_shell(t);
     }
 }
@@ -47,8 +48,10 @@ EncoderCore::~EncoderCore()
     for (DevBuf& b : recoveryHeld_)
         eng_->release(b);
     subwindows_.clear();   // (subwindows go back to their own pool)
+    recoveryHeld_.clear();
     SubwindowTable* t = CapStash<SubwindowTable>::shell();
     subwindows_.swap(t->v);
+    recoveryHeld_.swap(t->held);
     CapStash<SubwindowTable>::give(t);
 }
 

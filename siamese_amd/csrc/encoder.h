@@ -188,6 +188,7 @@ private:
     struct SubwindowTable
     {
         std::vector<EncSubwindowPtr> v;
+        std::vector<DevBuf> held;   // (recoveryHeld_'s capacity)
     };
     unsigned nextColumn_ = 0;
     unsigned count_ = 0;

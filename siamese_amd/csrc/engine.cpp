@@ -103,6 +103,7 @@ void ProgramBody::clear()
     nsolves = 0;   // (their vectors keep their capacity)
     nges = 0;
     callbacks.clear();
+    keep.clear();
     rb.open = false;
     rb.win.clear();
     rb.updates.clear();
@@ -698,6 +699,13 @@ uint8_t* Program::ge_job(unsigned rows, unsigned cols, unsigned pickLen, uint32_
 void Program::on_complete(Completion fn)
 {
     touch();
+    b_->callbacks.push_back(std::move(fn));
+}
+
+void Program::on_complete(std::shared_ptr<void> keep, Completion fn)
+{
+    touch();
+    b_->keep.push_back(std::move(keep));
     b_->callbacks.push_back(std::move(fn));
 }
 

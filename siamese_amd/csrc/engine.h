@@ -308,6 +308,10 @@ struct ProgramBody
     std::vector<PendingGe> ges;         // independent of the segments (nges in use)
     size_t nges = 0;
     std::vector<Completion> callbacks;
+    // objects the callbacks use, kept alive until they have run (so a
+    // callback captures a raw pointer and fits std::function's inline
+    // storage: no heap block per callback)
+    std::vector<std::shared_ptr<void>> keep;
     RowsBuild rb;
     bool gateOpen = false;        // ops from (segment gateSeg, op gateOp) on are gated on gateWord
     size_t gateSeg = 0;
@@ -450,11 +454,15 @@ public:
     /// own submission -- the decoder's Resolver slots under Resolver::mu
     /// (complete_solve) -- never state a later flush's callback also writes.
     void on_complete(Completion fn);
+    /// on_complete, `keep` held until the callback has run.
+    void on_complete(std::shared_ptr<void> keep, Completion fn);
     /// Forget the completions of work not yet submitted (owner going away).
     void drop_callbacks()
     {
-        if (b_)
+        if (b_) {
             b_->callbacks.clear();
+            b_->keep.clear();
+        }
     }
 
     /// Siamese row batches (OP_ROWS, ops.h).  A batch holds a snapshot of
