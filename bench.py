@@ -270,13 +270,14 @@ def run_leg(name, library, cfg, device, threads, runs, cpu_cfg, cpu_threads, cpu
     """One extra BASELINE config on one GPU: a verified warm-up, then `runs`
     timed runs ONE AT A TIME (no run overlaps another run of the same
     streams), the median reported; the reference on the host beside it.
-    C2's 1024 streams run in two pipelined stream groups (one group's host
-    work beside the other's device work: 22.5-24.4 vs 25.0-26.6 ms per run
-    with one group, same box, profiles/r2l_c2_groups_ab.txt); a single
-    stream is one group.  `defer`: the deferred-output API (siamese_gpu.h),
+    C2's 1024 streams run in four pipelined stream groups (one group's host
+    work beside the others' device work: 22.5-24.4 vs 25.0-26.6 ms per run
+    with one group against two, profiles/r2l_c2_groups_ab.txt; four against
+    two 12.7-13.7 vs 13.2-14.3 ms, round 6, profiles/r6v_c2_groups.txt); a
+    single stream is one group.  `defer`: the deferred-output API (siamese_gpu.h),
     a stream submits after every `defer`-th decode and is driven on while
     up to two of its submissions run (profiles/r3c_defer_sweep.txt)."""
-    groups = 2 if cfg.streams >= 64 else 1
+    groups = 4 if cfg.streams >= 64 else 1
     cb = CpuBaseline(cpu_cfg, cpu_threads, cpu_sample) if cpu_cfg is not None else None
     sess = S.BatchSession(library, cfg, device=device)
     per = []

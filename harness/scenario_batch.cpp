@@ -1163,11 +1163,12 @@ int run_pipeline(Shared& sh, StreamResult* results, unsigned nsteps, uint64_t* r
     // round (decode finish, frees) is ~1/3 of its first, and on its own paid a
     // whole fork-join's wake-ups and tail plus a submission
     // (SCENARIO_MERGE_ROUNDS=0: each round on its own, as before).
-    static const bool kMergeRounds = [] {
+    // (=2: in the deferred-output mode too; a measuring aid)
+    static const int kMergeRounds = [] {
         const char* v = std::getenv("SCENARIO_MERGE_ROUNDS");
-        return !v || std::atoi(v) != 0;
+        return v ? std::atoi(v) : 1;
     }();
-    const bool merge = kMergeRounds && !sh.e2e && inFlightPerJob == 1;
+    const bool merge = kMergeRounds > 0 && !sh.e2e && (inFlightPerJob == 1 || kMergeRounds == 2);
     std::vector<Job*> ready;   // (merge) jobs whose next round waits for the next fork-join
     auto run_ready = [&]() {
         if (ready.empty() || rc != 0)
