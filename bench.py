@@ -155,6 +155,30 @@ def cgroup_cpu():
     return cpu, throttled
 
 
+def thread_cpu():
+    """CPU nanoseconds per thread name (/proc/self/task/*/schedstat): the
+    library names its threads (sgpu-step, sgpu-assemble, sgpu-launch,
+    sgpu-complete); the rest are the process's own."""
+    out = {}
+    base = "/proc/self/task"
+    try:
+        tids = os.listdir(base)
+    except OSError:
+        return out
+    for t in tids:
+        try:
+            with open(os.path.join(base, t, "comm")) as f:
+                name = f.read().strip()
+            with open(os.path.join(base, t, "schedstat")) as f:
+                ns = int(f.read().split()[0])
+        except (OSError, ValueError, IndexError):
+            continue
+        if not name.startswith("sgpu-"):
+            name = "other"
+        out[name] = out.get(name, 0) + ns
+    return out
+
+
 def cgroup_quota():
     """The cgroup's CPU quota in CPUs (cpu.max), or None."""
     try:
@@ -510,13 +534,17 @@ def run_rank(rank, world, local, args, library, use_cuda):
 
     coll.barrier()
     cpu0, thr0 = cgroup_cpu()
+    th0 = thread_cpu()
     t0 = time.perf_counter()
     res, rep = sess.run(steps=args.steps, warmup=0, verify=False, threads=args.threads,
                         groups=args.groups, digest=False, defer=args.defer, device_ge=dge)
     coll.barrier()
     elapsed = time.perf_counter() - t0
     cpu1, thr1 = cgroup_cpu()
+    th1 = thread_cpu()
     cpu_used = {"process_cpus": round((cpu1 - cpu0) / elapsed, 2),
+                "cpu_ms_per_step_by_thread": {k: round((th1[k] - th0.get(k, 0)) / 1e6 / args.steps, 3)
+                                              for k in sorted(th1)},
                 "cgroup_quota_cpus": cgroup_quota(),
                 "cgroup_throttled_ms": round((thr1 - thr0) * 1e3, 2) if thr0 is not None and thr1 is not None
                 else None}

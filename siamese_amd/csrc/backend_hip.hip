@@ -41,6 +41,7 @@
 #include <string>
 #include <type_traits>
 #include <cstring>
+#include <ctime>
 #include <deque>
 #include <mutex>
 #include <vector>
@@ -4670,6 +4671,22 @@ bool be_fence_wait(void* fence, unsigned spinUs)
         } while (r == hipErrorNotReady &&
                  std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0)
                          .count() < kFenceSpinUs);
+    }
+    // Large flushes: poll with short sleeps instead of hipEventSynchronize,
+    // whose runtime spins up to ~200 us on the core before it blocks -- CPU
+    // time the process's quota (16 CPUs on the box, every one of them busy
+    // on the headline) takes from the stepping threads.  A poll every
+    // 10-40 us costs a few us of CPU per fence and at most one interval of
+    // latency on a completion that is ~0.4 ms away.
+    if (r == hipErrorNotReady && kFenceSpinUs == 0) {
+        long ns = 10000;
+        do {
+            struct timespec ts = {0, ns};
+            nanosleep(&ts, nullptr);
+            if (ns < 40000)
+                ns += 10000;
+            r = hipEventQuery(e);
+        } while (r == hipErrorNotReady);
     }
     if (r == hipErrorNotReady)
         r = hipEventSynchronize(e);

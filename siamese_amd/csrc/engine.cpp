@@ -1,6 +1,8 @@
 // engine.cpp -- arena, programs and the asynchronous flush pipeline (see
 // engine.h).
 #include "engine.h"
+
+#include <pthread.h>
 #include "backend.h"
 #include "codedef.h"
 #include "pool.h"
@@ -925,7 +927,7 @@ WorkerPool& Engine::pool()
     static std::mutex m;
     std::lock_guard<std::mutex> g(m);
     if (!pool_)
-        pool_.reset(new WorkerPool(WorkerPool::default_threads(), WorkerPool::shared_nice()));
+        pool_.reset(new WorkerPool(WorkerPool::default_threads(), WorkerPool::shared_nice(), "sgpu-step"));
     return *pool_;
 }
 
@@ -1566,8 +1568,14 @@ bool Engine::measure_unique() { return g_measureUnique.load(std::memory_order_re
 void Engine::start_threads()
 {
     stop_ = false;
-    launcher_ = std::thread([this] { launcher_loop(); });
-    completer_ = std::thread([this] { completer_loop(); });
+    launcher_ = std::thread([this] {
+        pthread_setname_np(pthread_self(), "sgpu-launch");
+        launcher_loop();
+    });
+    completer_ = std::thread([this] {
+        pthread_setname_np(pthread_self(), "sgpu-complete");
+        completer_loop();
+    });
 }
 
 void Engine::stop_threads()
@@ -1925,7 +1933,7 @@ WorkerPool& Engine::asm_pool()
         // per step vs 7.88/6.34/6.98 with 8, profiles/r4p_threads_ab.txt)
         const char* v = std::getenv("SIAMESE_AMD_ASM_THREADS");
         const int n = v ? std::atoi(v) : 4;
-        asmPool_.reset(new WorkerPool((unsigned)std::max(1, std::min(64, n))));
+        asmPool_.reset(new WorkerPool((unsigned)std::max(1, std::min(64, n)), 0, "sgpu-assemble"));
     }
     return *asmPool_;
 }

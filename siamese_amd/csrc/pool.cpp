@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <pthread.h>
 #include <sys/resource.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -28,10 +29,11 @@ unsigned WorkerPool::default_threads()
     return std::max(1u, std::min(16u, hw));
 }
 
-WorkerPool::WorkerPool(unsigned threads, int nice)
+WorkerPool::WorkerPool(unsigned threads, int nice, const char* name)
 {
     for (unsigned i = 1; i < threads; ++i)
-        workers_.emplace_back([this, nice] {
+        workers_.emplace_back([this, nice, name] {
+            pthread_setname_np(pthread_self(), name);
             if (nice != 0)
                 (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice);
             loop();

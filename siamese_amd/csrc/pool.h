@@ -16,8 +16,9 @@ namespace sgpu {
 class WorkerPool
 {
 public:
-    /// `nice`: scheduling priority of the worker threads (0 = the caller's).
-    explicit WorkerPool(unsigned threads, int nice = 0);
+    /// `nice`: scheduling priority of the worker threads (0 = the caller's);
+    /// `name`: their thread name (at most 15 characters; diagnostics).
+    explicit WorkerPool(unsigned threads, int nice = 0, const char* name = "sgpu-pool");
     ~WorkerPool();
     WorkerPool(const WorkerPool&) = delete;
     WorkerPool& operator=(const WorkerPool&) = delete;

@@ -14,6 +14,6 @@ for rep in 1 2 3; do
     timeout -k 10 150 python bench.py --library siamese_amd/$L --steps 20 --warmup 3 --no-cpu --no-e2e --no-legs --no-decode-ab > gpurun_out/${T}_${L}_$rep.json 2> gpurun_out/${T}_${L}_$rep.err
     python3 -c "
 import json; d=json.load(open('gpurun_out/${T}_${L}_$rep.json')); h=d['host']; v=d['device']
-print('$L', d['ms_per_step'], 'ms dev', v['device_ms_per_step'], h['phase_ms_per_step']['step'], h['engine_ms_per_step'], h['timed_region_cpu']['process_cpus'])"
+print('$L', d['ms_per_step'], 'ms dev', v['device_ms_per_step'], h['phase_ms_per_step']['step'], h['engine_ms_per_step'], h['timed_region_cpu']['process_cpus'], h['timed_region_cpu'].get('cpu_ms_per_step_by_thread'))"
   done
 done
