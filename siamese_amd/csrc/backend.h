@@ -111,8 +111,10 @@ bool be_sync();
 /// fault, and releases it.  The launcher thread creates fences, the
 /// completer thread waits for them.
 void* be_fence();
-/// spinUs: poll this long before sleeping (latency-bound small flushes).
-bool be_fence_wait(void* fence, unsigned spinUs);
+/// spinUs: poll this long before sleeping (latency-bound small flushes);
+/// sleepPoll: poll with short sleeps instead of the runtime's blocking wait,
+/// which spins on the core first (large flushes on a CPU-quota-bound host).
+bool be_fence_wait(void* fence, unsigned spinUs, bool sleepPoll);
 
 /// Transfer streams beside the codec stream (end-to-end packet flows).
 /// be_stage_h2d copies host -> device on the staging stream right away (the

@@ -4650,7 +4650,7 @@ void* be_fence()
     return e;
 }
 
-bool be_fence_wait(void* fence, unsigned spinUs)
+bool be_fence_wait(void* fence, unsigned spinUs, bool sleepPoll)
 {
     bind_device();
     if (!fence)
@@ -4678,7 +4678,7 @@ bool be_fence_wait(void* fence, unsigned spinUs)
     // on the headline) takes from the stepping threads.  A poll every
     // 10-40 us costs a few us of CPU per fence and at most one interval of
     // latency on a completion that is ~0.4 ms away.
-    if (r == hipErrorNotReady && kFenceSpinUs == 0) {
+    if (r == hipErrorNotReady && sleepPoll) {
         long ns = 10000;
         do {
             struct timespec ts = {0, ns};

@@ -2614,7 +2614,10 @@ bool Engine::complete_batch(Batch& bt)
     EngineStats st;
     // small flushes (a few instances: single-stream latency) poll the fence
     const size_t bodies = bt.bodies[0].size() + bt.bodies[1].size();
-    const bool ok = bt.launched && be_fence_wait(bt.fence, bodies <= 16 ? 2000u : 0u) && !failed();
+    // (small flushes spin: single-stream latency; mid-size ones take the
+    // runtime's blocking wait: the drop-in ABI's group-committed calls;
+    // large ones sleep-poll, be_fence_wait)
+    const bool ok = bt.launched && be_fence_wait(bt.fence, bodies <= 16 ? 2000u : 0u, bodies > 64) && !failed();
     const uint64_t t1 = now_ns();
     tl("fence passed", bt.ticket);
     st.waitNs = t1 - t0;

@@ -595,7 +595,7 @@ bool be_sync()
 }
 // fences are synchronisations too (they count toward HOSTSIM_FAIL_SYNC)
 void* be_fence() { return reinterpret_cast<void*>(1); }
-bool be_fence_wait(void*, unsigned) { return be_sync(); }
+bool be_fence_wait(void*, unsigned, bool) { return be_sync(); }
 void be_timing_enable(bool) {}
 void be_timing_reset() {}
 double be_timing_kernel_ms(BeKernel) { return 0; }

@@ -123,7 +123,7 @@ bool be_gather(const IngestDesc* descsHost, void* descsDev, uint32_t count, cons
 
 bool be_sync() { return true; }
 void* be_fence() { return reinterpret_cast<void*>(1); }
-bool be_fence_wait(void*, unsigned) { return true; }
+bool be_fence_wait(void*, unsigned, bool) { return true; }
 void be_timing_enable(bool) {}
 void be_timing_reset() {}
 double be_timing_kernel_ms(BeKernel) { return 0; }
