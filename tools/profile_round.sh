@@ -17,7 +17,7 @@ python3 tools/pmc_traffic.py $(ls $D/pmc_fetch*counter_collection.csv | head -n1
 ls -R $D | head -n 40
 # single-stream legs: kernel traces of C3 and C5 (tools/leg_run.py)
 # (groups and deferred-output depth as bench.py runs them)
-for L in "C3 1 1 8" "C5 1 1 8" "C2 1 2 4"; do
+for L in "C3 1 1 8" "C5 1 1 8" "C2 1 4 4"; do
   set -- $L
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o leg_$1 -- python3 tools/leg_run.py $L > $D/leg_$1.log 2>&1
 done
