@@ -75,9 +75,13 @@ def pmc_traffic(kernel, library):
             d = json.load(f)
         want = d.get("_lib_sha256")
         same = want is not None and want == lib_sha256(library)
-        return d[kernel]["traffic_bytes"], d.get("_source", TRAFFIC_JSON), same, d.get("_step_traffic_bytes")
+        per_step = None
+        if kernel in d.get("_step_dispatches", {}):
+            per_step = d[kernel]["traffic_bytes"] * d["_step_dispatches"][kernel]
+        return (d[kernel]["traffic_bytes"], d.get("_source", TRAFFIC_JSON), same, d.get("_step_traffic_bytes"),
+                per_step)
     except (OSError, KeyError, ValueError):
-        return None, None, False, None
+        return None, None, False, None, None
 
 
 def workload(rank, streams, ranges=True):
@@ -627,8 +631,16 @@ def run_rank(rank, world, local, args, library, use_cuda):
     achieved_alg = (exec_bytes / exec_s / 1e9) if exec_s > 0 else 0.0
     steps = args.steps
     launches = max(1, eng["exec_launches"])
-    traffic, traffic_src, traffic_same, step_traffic = pmc_traffic("sgpu::k_exec", library)
+    traffic_capture, traffic_src, traffic_same, step_traffic, exec_traffic_step = pmc_traffic("sgpu::k_exec", library)
     exec_ms_per_launch = rep.exec_ms / launches
+    # The capture's per-dispatch average comes from short runs whose pipeline
+    # fills and drains every step (more, emptier launches: 17.5 per step there
+    # against 16 in a long timed loop); the kernel's traffic PER STEP is the
+    # same work either way, so a launch of this run carries the capture's
+    # per-step traffic over this run's launches per step.
+    traffic = traffic_capture
+    if exec_traffic_step and steps:
+        traffic = exec_traffic_step / (eng["exec_launches"] / steps)
     ueng = S.engine_dict(urep)
     unique_per_launch = ueng["exec_unique_bytes"] / max(1, ueng["exec_launches"])
     t_launch = exec_ms_per_launch / 1e3
@@ -721,7 +733,8 @@ def run_rank(rank, world, local, args, library, use_cuda):
                            "separate --steps 1 capture of this same library build; MALL hits included, so "
                            "an upper bound on HBM bytes: unique_frac beside it is the compulsory floor)"
                            if phys else "compulsory bytes per launch (no PMC capture of this build committed)"),
-            "traffic": traffic,
+            "traffic": round(traffic) if traffic else traffic,
+            "traffic_per_capture_dispatch": traffic_capture,
             "traffic_source": traffic_src,
             "traffic_build_matches": traffic_same,
             "traffic_GBps": round(traffic_gbps, 2) if traffic_gbps else None,
@@ -735,8 +748,10 @@ def run_rank(rank, world, local, args, library, use_cuda):
             "alg_bytes_per_launch": exec_bytes // launches,
             "alg_bytes_per_step": exec_bytes // steps,
             "note": "launch time = k_exec's average HIP-event duration on the codec stream in this run; "
-                    "traffic = rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per dispatch of a committed capture "
-                    "(traffic_build_matches: the capture's library sha256 equals this run's); unique = "
+                    "traffic = rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of a committed capture "
+                    "(traffic_build_matches: the capture's library sha256 equals this run's), the kernel's "
+                    "bytes per workload step there over this run's launches per step "
+                    "(traffic_per_capture_dispatch: the capture's own per-dispatch average); unique = "
                     "every distinct symbol read once + every output written once + the op stream, counted "
                     "by the library in one extra untimed step; achieved_alg = SURVEY 8d's ALGORITHMIC "
                     "bytes (every re-read the reference performs) over the same time: NOT a roofline, "
