@@ -113,3 +113,35 @@ def test_released_buffers_wait_for_the_published_ticket():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().startswith("ok")
+
+
+def test_merged_rounds_match_separate_rounds():
+    """A job's later rounds ride in the next new job's fork-join and
+    submission (the default) or each take their own (SCENARIO_MERGE_ROUNDS=0):
+    the golden C4x256 digests of the reference either way, with the chained
+    device decode (its second round is the decode's finish), 8 groups over 2
+    steps (jobs of both steps in flight together), every recovered byte
+    verified; merged, the run takes fewer submissions."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import scenario_lib as S, golden\n"
+        "sess = S.BatchSession(S.SIM_LIB, golden.config('C4x256'))\n"
+        "res, rep = sess.run(steps=0, warmup=1, verify=True, threads=4, groups=8, device_ge=True)\n"
+        "assert rep.mismatches == 0 and not any(r.status for r in res)\n"
+        "assert S.digests(res) == golden.load('C4x256')['digests']\n"
+        "res2, rep2 = sess.run(steps=2, warmup=0, verify=False, threads=4, groups=8, digest=False,\n"
+        "                      device_ge=True)\n"
+        "assert not any(r.status for r in res2)\n"
+        "sess.close()\n"
+        "print(rep2.rounds)\n" % os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for v in ("0", "1"):
+        env = dict(os.environ, SCENARIO_MERGE_ROUNDS=v)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[v] = int(r.stdout.strip().splitlines()[-1])
+    assert out["1"] < out["0"]   # the later rounds did ride along
