@@ -224,6 +224,8 @@ struct Stream
     std::vector<uint8_t> buf;
     std::vector<Pkt> decoded;     // output of the last successful decode
     std::vector<Pkt> getBuf;      // deliver_range's packets
+    std::vector<uint8_t> lostBuf;  // add_ranges' loss draws (capacity reused)
+    std::vector<int> resultsBuf;   // add_ranges' per-call results (capacity reused)
     bool dataOk = true;           // every returned packet matched its payload
 
     void init(const ScenarioConfig* c, Codec* k, StreamResult* r, unsigned globalIndex)
@@ -317,7 +319,8 @@ struct Stream
         unsigned first = 0, added = 0;
         const int r = codec->enc_add_range(packet_id(i), n, &first, &added);
         const unsigned i0 = i;
-        std::vector<uint8_t> lost(added);
+        std::vector<uint8_t>& lost = lostBuf;
+        lost.assign(added, 0);
         for (unsigned k = 0; k < added; ++k) {
             const unsigned num = (first + k) & 0x3fffff;
             note(ev(EV_ENC_ADD, 0, num));
@@ -332,7 +335,7 @@ struct Stream
             fail(2);
             return;
         }
-        std::vector<int> results;
+        std::vector<int>& results = resultsBuf;
         for (unsigned k = 0; k < added;) {
             if (lost[k]) {
                 ++k;
